@@ -1,0 +1,111 @@
+// Internal launcher API between the C-ABI layer (lance_hip_abi.cpp) and the
+// gfx950 kernels (knn_kernels.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace lhip {
+
+enum Metric : int { METRIC_L2 = 0, METRIC_DOT = 1, METRIC_COSINE = 2 };
+
+// Scan tile geometry (see DESIGN.md "Scan kernel").
+constexpr int SCAN_BR = 128;  // base rows per workgroup tile (MFMA M)
+constexpr int SCAN_BQ = 256;  // queries per workgroup tile   (MFMA N)
+constexpr int SCAN_BK = 64;   // k-step
+constexpr int DPAD = 64;      // row stride of the device store is a multiple of this
+constexpr int MAX_CAND = 256; // max refined candidates per query per pass
+
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+// Per-row auxiliary data kept beside the f32 rows (one float4 per slot):
+//   x = alpha (f32 |x|^2 for l2, 0 otherwise; +inf = tombstone / padding)
+//   y = xn    (|x| for l2/dot, 0 for cosine)
+//   z = ux    (upper bound of |bf16(x)| + |x - bf16(x)|; cosine: divided by |x|)
+//   w = sc    (1 for l2/dot, 1/|x| for cosine)
+struct StoreView {
+	const float *X;          // [n_slots][ld] f32 rows, zero padded to ld
+	const float4 *rowaux;    // [n_slots]
+	const int64_t *labels;   // [n_slots] slot -> label
+	int64_t n_slots;
+	int ld;                  // padded row stride (floats), multiple of DPAD
+	int dim;
+	int metric;
+};
+
+// Per-query constants for the lower-bound epilogue:
+//   LB = alpha + xn*B + ux*A + (s*sc)*S + C      (s = bf16 MFMA dot)
+struct QueryView {
+	const float *Qf;         // [nq_pad][ld] f32 queries, zero padded
+	const uint16_t *Qb;      // [nq_pad][ld] bf16 queries
+	const float4 *qaux;      // [nq_pad] (S, A, B, C)
+	int nq;
+	int nq_pad;              // multiple of SCAN_BQ
+};
+
+// ---- ingest ------------------------------------------------------------------
+// Computes rowaux for slots [s0, s0+n) of a store (f64 norms, bf16 error norms),
+// and folds max(alpha), max(ux) into stats[0], stats[1] (as float bits).
+void launch_rowaux(const float *X, int ld, int dim, int metric, int64_t s0, int64_t n, float4 *rowaux,
+                   unsigned *stats, hipStream_t st);
+
+// Marks the listed slots dead (rowaux.x = +inf).
+void launch_tombstone(float4 *rowaux, const int64_t *slots, int n, hipStream_t st);
+
+// ---- search ------------------------------------------------------------------
+void launch_prep_queries(const float *Q, int nq, int dim, int ld, int nq_pad, int metric, float max_alpha,
+                         float max_ux, float *Qf, uint16_t *Qb, float4 *qaux, hipStream_t st);
+
+// Dense lower-bound scan over row tiles t*tile_stride, t < n_tiles:
+// out[q][t*BR + r] = LB(q, slot) (+inf for tombstones / rows past n_slots).
+void launch_scan_dense(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, float *out,
+                       int64_t ld_out, hipStream_t st);
+
+// Threshold scan over all rows: append (orderedkey(LB), slot) for LB <= tau[q]
+// into pool[q][0..cap); pool_cnt[q] counts every pass (may exceed cap).
+void launch_scan_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *pool, int *pool_cnt,
+                        int cap, hipStream_t st);
+
+// Per-query top-M selection by LB.  Source is either a dense LB matrix
+// (dense != null: n_entries per query, entry i -> slot (i/BR)*stride*BR + i%BR)
+// or the append pools.  Writes cand_slot[q][0..M), cand_cnt[q] and the cut
+// cut[q] = a lower bound on the true distance of every live row not selected
+// (+inf when nothing live was left out; -inf when unknown -> certificate fails).
+void launch_select(const float *dense, int64_t ld_dense, int64_t n_entries, int64_t tile_stride,
+                   const uint2 *pool, const int *pool_cnt, int cap, const float *tau, int nq, int M,
+                   uint32_t *cand_slot, int *cand_cnt, float *cut, hipStream_t st);
+
+// Exact distances (f64 accumulation, rounded to f32) of the candidates.
+void launch_refine(const StoreView &s, const QueryView &q, const uint32_t *cand_slot, const int *cand_cnt, int M,
+                   float *cand_dist, hipStream_t st);
+
+// Sort candidates by (distance, label).  mode 0 (TAU): tau[q] = largest exact
+// distance among the candidates when at least need_for_tau of them exist, else
+// +inf.  mode 1 (FINAL): writes top-k, counts and the certificate ok[q].
+void launch_finalize(const StoreView &s, const uint32_t *cand_slot, const int *cand_cnt, const float *cand_dist,
+                     const float *cut, int nq, int M, int k, int mode, int need_for_tau, float *tau,
+                     int64_t *out_labels, float *out_dists, int *out_counts, int *cert_ok, hipStream_t st);
+
+// Exact fallback for one query: exact distance of every slot into keys[n_slots]
+// (dead slots -> NaN with all-ones payload so they sort last), labels into vals.
+void launch_exact_all(const StoreView &s, const QueryView &q, int qi, float *keys, int64_t *vals, hipStream_t st);
+
+// Radix sort (key f32 asc, stable) of n pairs; temp sized by the first call with
+// temp == nullptr.  Returns hipError_t as int.
+int sort_pairs(void *temp, size_t &temp_bytes, const float *keys_in, float *keys_out, const int64_t *vals_in,
+               int64_t *vals_out, int64_t n, hipStream_t st);
+
+// Merge nshard partial top-k lists (device pointers) into the global top-k.
+void launch_merge_topk(int nshard, int nq, int k, const int64_t *part_labels, const float *part_dists,
+                       const int *part_counts, int64_t *out_labels, float *out_dists, int *out_counts,
+                       hipStream_t st);
+
+// Copies the first n_live entries of a sorted fallback result into the outputs.
+void launch_copy_fallback(const float *keys, const int64_t *vals, int64_t n_live, int k, int qi,
+                          int64_t *out_labels, float *out_dists, int *out_counts, hipStream_t st);
+
+// Gathers slots idx[0..n) of a store into a new store (same ld), in order.
+// Used by lance_detached_compact (drops tombstones, keeps label order).
+void launch_gather_rows(const float *X, const float4 *rowaux, const int64_t *labels, const int64_t *idx, int64_t n,
+                        int ld, float *Xo, float4 *rowaux_o, int64_t *labels_o, hipStream_t st);
+
+}  // namespace lhip

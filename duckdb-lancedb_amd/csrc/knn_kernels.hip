@@ -1,0 +1,860 @@
+// gfx950 (MI355X / CDNA4) kernels of the flat k-NN path.
+//
+// Replaces the arithmetic the reference delegates to lance 0.22 / lance-linalg
+// 0.22 (flat KNN behind rust_lib/src/lance_manager.rs:411-419, paths relative
+// to /root/reference).  Pipeline per search (DESIGN.md "Search pipeline"):
+//
+//   prep_queries   f32 queries -> zero-padded f32 + bf16 copies + LB constants
+//   scan           bf16 MFMA (v_mfma_f32_32x32x16_bf16) query x base tiles with
+//                  the base streamed once from HBM as f32, converted in
+//                  registers, staged through XOR-swizzled LDS; the epilogue
+//                  turns each dot product into a rigorous LOWER BOUND of the
+//                  exact distance and either writes it (dense mode, small N /
+//                  sample) or appends (LB, slot) when LB <= tau[q] (append mode)
+//   select         per-query radix select of the M smallest lower bounds
+//   refine         exact distance of the M candidates, f64 accumulation
+//   finalize       sort by (distance, label), top-k, exactness certificate:
+//                  every row left out has LB >= cut > k-th exact distance
+//   exact_all/sort fallback for a query whose certificate failed
+//
+// No hipify, no CUDA shims: wave64, MFMA and LDS idioms written for CDNA4.
+#include "knn_kernels.h"
+
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include <cfloat>
+#include <cmath>
+
+namespace lhip {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+static constexpr float F_INF = __builtin_huge_valf();
+static constexpr uint32_t KEY_INF = 0xFF800000u;  // ordered key of +inf
+static constexpr uint32_t KEY_NAN = 0xFFFFFFFFu;  // every NaN is canonicalised to this
+
+// ---------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t fkey(float f) {
+	uint32_t u = __float_as_uint(f);
+	if ((u & 0x7FFFFFFFu) > 0x7F800000u) return KEY_NAN;
+	return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float fkey_inv(uint32_t k) {
+	uint32_t u = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+	return __uint_as_float(u);
+}
+__device__ __forceinline__ uint16_t bf16_bits(float f) {
+	__bf16 h = (__bf16)f;  // RNE: v_cvt_pk_bf16_f32 on gfx950
+	return __builtin_bit_cast(uint16_t, h);
+}
+__device__ __forceinline__ float bf16_round(float f) {
+	return (float)(__bf16)f;
+}
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+	return (uint32_t)bf16_bits(a) | ((uint32_t)bf16_bits(b) << 16);
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+	return v;
+}
+// (distance, label) total order used everywhere: NaN after +inf, then label.
+__device__ __forceinline__ bool hit_less(float da, int64_t la, float db, int64_t lb) {
+	bool an = __builtin_isnan(da), bn = __builtin_isnan(db);
+	if (an != bn) return bn;
+	if (!an && da != db) return da < db;
+	return la < lb;
+}
+// unit roundoff used by the bounds; 2^-23 (not 2^-24) leaves room for an
+// accumulation that truncates instead of rounding.
+static constexpr double U_BOUND = 1.1920928955078125e-07;
+
+// ---------------------------------------------------------------------------
+// ingest: per-row auxiliary data
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rowaux_kernel(const float *__restrict__ X, int ld, int dim, int metric,
+                                                     int64_t s0, int64_t n, float4 *__restrict__ rowaux,
+                                                     unsigned *__restrict__ stats) {
+	const int lane = threadIdx.x & 63;
+	const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+	if (r >= n) return;
+	const float *x = X + (s0 + r) * (int64_t)ld;
+	double s2 = 0.0, e2 = 0.0;
+	for (int i = lane; i < dim; i += 64) {
+		float v = x[i];
+		float e = v - bf16_round(v);
+		s2 += (double)v * v;
+		e2 += (double)e * e;
+	}
+	s2 = wave_sum_f64(s2);
+	e2 = wave_sum_f64(e2);
+	if (lane == 0) {
+		double xn = sqrt(s2), ex = sqrt(e2);
+		double ux = (xn + ex) * (1.0 + 4.0 * U_BOUND);
+		float4 a;
+		if (metric == METRIC_L2) {
+			a = make_float4((float)s2, (float)xn, (float)ux, 1.0f);
+		} else if (metric == METRIC_DOT) {
+			a = make_float4(0.0f, (float)xn, (float)ux, 1.0f);
+		} else {
+			if (xn > 0.0) {
+				a = make_float4(0.0f, 0.0f, (float)(ux / xn * (1.0 + 4.0 * U_BOUND)), (float)(1.0 / xn));
+			} else {
+				a = make_float4(__builtin_nanf(""), 0.0f, 0.0f, 0.0f);  // cosine undefined: exact fallback
+			}
+		}
+		rowaux[s0 + r] = a;
+		if (a.x == a.x) atomicMax(&stats[0], __float_as_uint(fabsf(a.x)));
+		atomicMax(&stats[1], __float_as_uint(a.z));
+	}
+}
+
+void launch_rowaux(const float *X, int ld, int dim, int metric, int64_t s0, int64_t n, float4 *rowaux,
+                   unsigned *stats, hipStream_t st) {
+	if (n <= 0) return;
+	int64_t blocks = (n + 3) / 4;
+	rowaux_kernel<<<dim3((unsigned)blocks), dim3(256), 0, st>>>(X, ld, dim, metric, s0, n, rowaux, stats);
+}
+
+__global__ void tombstone_kernel(float4 *rowaux, const int64_t *slots, int n) {
+	int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < n) rowaux[slots[i]].x = F_INF;
+}
+
+void launch_tombstone(float4 *rowaux, const int64_t *slots, int n, hipStream_t st) {
+	if (n <= 0) return;
+	tombstone_kernel<<<dim3((n + 255) / 256), dim3(256), 0, st>>>(rowaux, slots, n);
+}
+
+// ---------------------------------------------------------------------------
+// queries
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void prep_queries_kernel(const float *__restrict__ Q, int nq, int dim, int ld,
+                                                           int metric, float max_alpha, float max_ux,
+                                                           float *__restrict__ Qf, uint16_t *__restrict__ Qb,
+                                                           float4 *__restrict__ qaux) {
+	__shared__ double red[2][4];
+	const int q = blockIdx.x;
+	const int t = threadIdx.x;
+	double s2 = 0.0, e2 = 0.0;
+	for (int i = t; i < ld; i += 256) {
+		float v = (q < nq && i < dim) ? Q[(int64_t)q * dim + i] : 0.0f;
+		Qf[(int64_t)q * ld + i] = v;
+		uint16_t b = bf16_bits(v);
+		Qb[(int64_t)q * ld + i] = b;
+		float e = v - __uint_as_float((uint32_t)b << 16);
+		s2 += (double)v * v;
+		e2 += (double)e * e;
+	}
+	s2 = wave_sum_f64(s2);
+	e2 = wave_sum_f64(e2);
+	if ((t & 63) == 0) {
+		red[0][t >> 6] = s2;
+		red[1][t >> 6] = e2;
+	}
+	__syncthreads();
+	if (t != 0) return;
+	s2 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+	e2 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+	if (q >= nq) {
+		qaux[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+		return;
+	}
+	const double u = U_BOUND;
+	const double gamma = 2.0 * ld * u;  // accumulation of ld exact bf16 products in f32
+	const double qn = sqrt(s2), eq = sqrt(e2);
+	const double uq = (qn + eq) * (1.0 + 4.0 * u);
+	float4 a;
+	if (metric == METRIC_L2) {
+		double slack = 16.0 * u * ((double)max_alpha + s2 + 7.0 * (double)max_ux * uq) + 1e-30;
+		a = make_float4(-2.0f, (float)(-2.0 * (1.0 + gamma) * uq), (float)(2.0 * qn), (float)(s2 - slack));
+	} else if (metric == METRIC_DOT) {
+		double slack = 16.0 * u * (1.0 + 7.0 * (double)max_ux * uq) + 1e-30;
+		a = make_float4(-1.0f, (float)(-(1.0 + gamma) * uq), (float)qn, (float)(1.0 - slack));
+	} else {
+		if (qn > 0.0) {
+			double ruq = uq / qn * (1.0 + 4.0 * u);
+			double slack = 16.0 * u * (2.0 + 7.0 * (double)max_ux * ruq) + 1e-30;
+			a = make_float4((float)(-1.0 / qn), (float)(-(1.0 + gamma) * ruq), 0.0f, (float)(2.0 - slack));
+		} else {
+			a = make_float4(0.f, 0.f, 0.f, __builtin_nanf(""));  // undefined: exact fallback
+		}
+	}
+	qaux[q] = a;
+}
+
+void launch_prep_queries(const float *Q, int nq, int dim, int ld, int nq_pad, int metric, float max_alpha,
+                         float max_ux, float *Qf, uint16_t *Qb, float4 *qaux, hipStream_t st) {
+	prep_queries_kernel<<<dim3(nq_pad), dim3(256), 0, st>>>(Q, nq, dim, ld, metric, max_alpha, max_ux, Qf, Qb,
+	                                                           qaux);
+}
+
+// ---------------------------------------------------------------------------
+// scan: bf16 MFMA lower-bound tiles
+//
+// Workgroup = 512 threads = 8 waves laid out 2 (base rows) x 4 (queries); each
+// wave owns a 64-row x 64-query sub-tile = 2x2 v_mfma_f32_32x32x16_bf16 tiles
+// (A = base rows, B = queries, so the accumulator column = lane&31 = query and
+// the 16 registers walk base rows).  Per 64-deep k-step the workgroup streams
+// a 128 x 64 f32 base tile from HBM (two 16 B loads per thread, converted to
+// bf16 in registers) and a 256 x 64 bf16 query tile from L2 into an
+// XOR-swizzled LDS image (16 B chunk c of row r stored at c ^ ((r>>1)&7), which
+// makes the ds_read_b128 fragment loads of 32 consecutive rows conflict-free).
+// Global loads of step k+1 are issued before the MFMAs of step k.
+// ---------------------------------------------------------------------------
+constexpr int BR = SCAN_BR, BQ = SCAN_BQ, BK = SCAN_BK;
+constexpr int XS_BYTES = BR * BK * 2;  // 16 KiB
+constexpr int QS_BYTES = BQ * BK * 2;  // 32 KiB
+constexpr int SCAN_LDS = XS_BYTES + QS_BYTES + BR * 16;
+
+__device__ __forceinline__ int swz(int row, int chunk) {
+	return row * (BK * 2) + ((chunk ^ ((row >> 1) & 7)) << 4);
+}
+
+template <int METRIC>
+__device__ __forceinline__ float lower_bound(float s, float4 ra, float4 qa) {
+	// LB = alpha + xn*B + ux*A + (s*sc)*S + C
+	float v = fmaf(ra.y, qa.z, ra.x);
+	v = fmaf(ra.z, qa.y, v);
+	float ss = (METRIC == METRIC_COSINE) ? s * ra.w : s;
+	v = fmaf(ss, qa.x, v);
+	return v + qa.w;
+}
+
+template <int METRIC, int MODE>
+__global__ __launch_bounds__(512) void scan_kernel(const float *__restrict__ X, const float4 *__restrict__ rowaux,
+                                                   int64_t n_slots, int ld, const uint16_t *__restrict__ Qb,
+                                                   const float4 *__restrict__ qaux, int nq, int64_t tile_stride,
+                                                   float *__restrict__ dense, int64_t ld_out,
+                                                   const float *__restrict__ tau, uint2 *__restrict__ pool,
+                                                   int *__restrict__ pool_cnt, int cap) {
+	__shared__ __attribute__((aligned(16))) uint8_t smem[SCAN_LDS];
+	uint8_t *Xs = smem;
+	uint8_t *Qs = smem + XS_BYTES;
+	float4 *RA = reinterpret_cast<float4 *>(smem + XS_BYTES + QS_BYTES);
+
+	const int tid = threadIdx.x;
+	const int lane = tid & 63;
+	const int w = tid >> 6;
+	const int wr = w & 1, wq = w >> 1;
+	const int li = lane & 31, hi = lane >> 5;
+	const int64_t row0 = (int64_t)blockIdx.x * tile_stride * BR;
+	const int q0 = blockIdx.y * BQ;
+
+	if (tid < BR) {
+		int64_t r = row0 + tid;
+		RA[tid] = (r < n_slots) ? rowaux[r] : make_float4(F_INF, 0.f, 0.f, 0.f);
+	}
+
+	// staging assignment: X chunks c = tid, tid+512 (row = c>>3, 16 B bf16 chunk = c&7)
+	const int xr0 = tid >> 3, xc = tid & 7;
+	const int xr1 = xr0 + 64;
+	const bool xv0 = row0 + xr0 < n_slots, xv1 = row0 + xr1 < n_slots;
+	const float *xp0 = X + (xv0 ? (row0 + xr0) * (int64_t)ld : 0) + xc * 8;
+	const float *xp1 = X + (xv1 ? (row0 + xr1) * (int64_t)ld : 0) + xc * 8;
+	// Q chunks c = tid + 512*i, i < 4: row = c>>3 (= (tid>>3) + 64 i), chunk = tid&7
+	const uint16_t *qp = Qb + (int64_t)(q0 + (tid >> 3)) * ld + xc * 8;
+	const int64_t qstep = (int64_t)64 * ld;
+
+	float4 xa0, xa1, xb0, xb1;
+	uint4 qv[4];
+	auto gload = [&](int kt) {
+		const int ko = kt * BK;
+		if (xv0) {
+			xa0 = *reinterpret_cast<const float4 *>(xp0 + ko);
+			xa1 = *reinterpret_cast<const float4 *>(xp0 + ko + 4);
+		} else {
+			xa0 = xa1 = make_float4(0.f, 0.f, 0.f, 0.f);
+		}
+		if (xv1) {
+			xb0 = *reinterpret_cast<const float4 *>(xp1 + ko);
+			xb1 = *reinterpret_cast<const float4 *>(xp1 + ko + 4);
+		} else {
+			xb0 = xb1 = make_float4(0.f, 0.f, 0.f, 0.f);
+		}
+#pragma unroll
+		for (int i = 0; i < 4; ++i) qv[i] = *reinterpret_cast<const uint4 *>(qp + i * qstep + ko);
+	};
+	auto swrite = [&]() {
+		uint4 p0 = make_uint4(pk_bf16(xa0.x, xa0.y), pk_bf16(xa0.z, xa0.w), pk_bf16(xa1.x, xa1.y),
+		                      pk_bf16(xa1.z, xa1.w));
+		uint4 p1 = make_uint4(pk_bf16(xb0.x, xb0.y), pk_bf16(xb0.z, xb0.w), pk_bf16(xb1.x, xb1.y),
+		                      pk_bf16(xb1.z, xb1.w));
+		*reinterpret_cast<uint4 *>(Xs + swz(xr0, xc)) = p0;
+		*reinterpret_cast<uint4 *>(Xs + swz(xr1, xc)) = p1;
+#pragma unroll
+		for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4 *>(Qs + swz(xr0 + 64 * i, xc)) = qv[i];
+	};
+
+	f32x16 acc[2][2];
+#pragma unroll
+	for (int a = 0; a < 2; ++a)
+#pragma unroll
+		for (int b = 0; b < 2; ++b)
+#pragma unroll
+			for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+	const int KT = ld / BK;
+	gload(0);
+	for (int kt = 0; kt < KT; ++kt) {
+		swrite();
+		__syncthreads();
+		if (kt + 1 < KT) gload(kt + 1);
+#pragma unroll
+		for (int ks = 0; ks < BK / 16; ++ks) {
+			const int kc = ks * 2 + hi;
+			bf16x8 af[2], bfr[2];
+#pragma unroll
+			for (int tr = 0; tr < 2; ++tr)
+				af[tr] = *reinterpret_cast<const bf16x8 *>(Xs + swz(wr * 64 + tr * 32 + li, kc));
+#pragma unroll
+			for (int tq = 0; tq < 2; ++tq)
+				bfr[tq] = *reinterpret_cast<const bf16x8 *>(Qs + swz(wq * 64 + tq * 32 + li, kc));
+#pragma unroll
+			for (int tr = 0; tr < 2; ++tr)
+#pragma unroll
+				for (int tq = 0; tq < 2; ++tq)
+					acc[tr][tq] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tr], bfr[tq], acc[tr][tq], 0, 0, 0);
+		}
+		__syncthreads();
+	}
+
+	// epilogue: lane holds query q = q0 + wq*64 + tq*32 + li and, in register
+	// reg, base row wr*64 + tr*32 + (reg&3) + 8*(reg>>2) + 4*hi.
+#pragma unroll
+	for (int tq = 0; tq < 2; ++tq) {
+		const int q = q0 + wq * 64 + tq * 32 + li;
+		if (q >= nq) continue;
+		const float4 qa = qaux[q];
+		float t = 0.f;
+		if (MODE == 1) t = tau[q];
+#pragma unroll
+		for (int tr = 0; tr < 2; ++tr) {
+#pragma unroll
+			for (int g = 0; g < 4; ++g) {
+				const int rl = wr * 64 + tr * 32 + 8 * g + 4 * hi;
+				float lb[4];
+#pragma unroll
+				for (int j = 0; j < 4; ++j) lb[j] = lower_bound<METRIC>(acc[tr][tq][4 * g + j], RA[rl + j], qa);
+				if (MODE == 0) {
+					float *o = dense + (int64_t)q * ld_out + (int64_t)blockIdx.x * BR + rl;
+					*reinterpret_cast<float4 *>(o) = make_float4(lb[0], lb[1], lb[2], lb[3]);
+				} else {
+#pragma unroll
+					for (int j = 0; j < 4; ++j) {
+						if (lb[j] <= t && lb[j] < F_INF) {
+							int pos = atomicAdd(&pool_cnt[q], 1);
+							if (pos < cap)
+								pool[(int64_t)q * cap + pos] = make_uint2(fkey(lb[j]), (uint32_t)(row0 + rl + j));
+						}
+					}
+				}
+			}
+		}
+	}
+}
+
+template <int MODE>
+static void scan_dispatch(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, float *dense,
+                          int64_t ld_out, const float *tau, uint2 *pool, int *pool_cnt, int cap, hipStream_t st) {
+	dim3 grid((unsigned)n_tiles, (unsigned)(q.nq_pad / BQ));
+	dim3 block(512);
+	switch (s.metric) {
+	case METRIC_L2:
+		scan_kernel<METRIC_L2, MODE><<<grid, block, 0, st>>>(s.X, s.rowaux, s.n_slots, s.ld, q.Qb, q.qaux, q.nq,
+		                                                      tile_stride, dense, ld_out, tau, pool, pool_cnt, cap);
+		break;
+	case METRIC_DOT:
+		scan_kernel<METRIC_DOT, MODE><<<grid, block, 0, st>>>(s.X, s.rowaux, s.n_slots, s.ld, q.Qb, q.qaux, q.nq,
+		                                                       tile_stride, dense, ld_out, tau, pool, pool_cnt, cap);
+		break;
+	default:
+		scan_kernel<METRIC_COSINE, MODE><<<grid, block, 0, st>>>(s.X, s.rowaux, s.n_slots, s.ld, q.Qb, q.qaux,
+		                                                          q.nq, tile_stride, dense, ld_out, tau, pool,
+		                                                          pool_cnt, cap);
+		break;
+	}
+}
+
+void launch_scan_dense(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, float *out,
+                       int64_t ld_out, hipStream_t st) {
+	if (n_tiles <= 0) return;
+	scan_dispatch<0>(s, q, n_tiles, tile_stride, out, ld_out, nullptr, nullptr, nullptr, 0, st);
+}
+
+void launch_scan_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *pool, int *pool_cnt,
+                        int cap, hipStream_t st) {
+	int64_t n_tiles = (s.n_slots + BR - 1) / BR;
+	if (n_tiles <= 0) return;
+	scan_dispatch<1>(s, q, n_tiles, 1, nullptr, 0, tau, pool, pool_cnt, cap, st);
+}
+
+// ---------------------------------------------------------------------------
+// select: per-query radix select of the M smallest lower bounds
+// One 256-thread workgroup per query; 11/11/10-bit digits over ordered keys.
+// ---------------------------------------------------------------------------
+constexpr int SEL_THREADS = 256;
+constexpr int SEL_BINS = 2048;
+
+struct SelSrc {
+	const float *dense;
+	int64_t ld_dense, n_entries, tile_stride;
+	const uint2 *pool;
+	int cap;
+	__device__ __forceinline__ void get(int q, int64_t i, uint32_t &key, uint32_t &slot) const {
+		if (dense) {
+			key = fkey(dense[(int64_t)q * ld_dense + i]);
+			slot = (uint32_t)((i / BR) * tile_stride * BR + (i % BR));
+		} else {
+			uint2 e = pool[(int64_t)q * cap + i];
+			key = e.x;
+			slot = e.y;
+		}
+	}
+};
+
+// exclusive scan of one value per thread across the 256-thread block
+__device__ __forceinline__ unsigned block_excl_scan(unsigned v, unsigned *sh /*[8]*/, unsigned &total) {
+	const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+	unsigned x = v;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		unsigned y = __shfl_up(x, o, 64);
+		if (lane >= o) x += y;
+	}
+	if (lane == 63) sh[w] = x;
+	__syncthreads();
+	unsigned base = 0;
+	for (int i = 0; i < w; ++i) base += sh[i];
+	total = sh[0] + sh[1] + sh[2] + sh[3];
+	__syncthreads();
+	return base + x - v;
+}
+
+__global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const int *__restrict__ pool_cnt,
+                                                             const float *__restrict__ tau, int M,
+                                                             uint32_t *__restrict__ cand_slot,
+                                                             int *__restrict__ cand_cnt, float *__restrict__ cut) {
+	__shared__ unsigned hist[SEL_BINS];
+	__shared__ unsigned sh[8];
+	__shared__ unsigned s_digit, s_rem, s_nlt, s_neq, s_minex;
+	const int q = blockIdx.x;
+	const int t = threadIdx.x;
+	int64_t n;
+	bool overflow = false;
+	if (src.dense) {
+		n = src.n_entries;
+	} else {
+		int c = pool_cnt[q];
+		overflow = c > src.cap;
+		n = c < src.cap ? c : src.cap;
+	}
+	const float ftau = src.dense ? F_INF : tau[q];
+
+	// pass 1: histogram of the top 11 bits (also counts +inf / NaN keys)
+	for (int i = t; i < SEL_BINS; i += SEL_THREADS) hist[i] = 0;
+	if (t == 0) {
+		s_nlt = 0;
+		s_neq = 0;
+		s_minex = 0xFFFFFFFFu;
+	}
+	__syncthreads();
+	for (int64_t i = t; i < n; i += SEL_THREADS) {
+		uint32_t k, sl;
+		src.get(q, i, k, sl);
+		atomicAdd(&hist[k >> 21], 1u);
+	}
+	__syncthreads();
+	const unsigned n_nan = hist[SEL_BINS - 1];
+	const unsigned n_inf = hist[KEY_INF >> 21];  // bin 0x7FC holds +inf only
+	const int64_t n_fin = n - n_nan - n_inf;
+	float c_out;
+	if (n_fin <= M) {
+		// take every finite entry
+		for (int64_t i = t; i < n; i += SEL_THREADS) {
+			uint32_t k, sl;
+			src.get(q, i, k, sl);
+			if (k < KEY_INF) {
+				unsigned p = atomicAdd(&s_nlt, 1u);
+				cand_slot[(int64_t)q * M + p] = sl;
+			}
+		}
+		__syncthreads();
+		c_out = ftau;
+	} else {
+		unsigned prefix = 0, mask = 0, rem = (unsigned)M;
+		const int shifts[3] = {21, 10, 0};
+		const int widths[3] = {11, 11, 10};
+#pragma unroll 1
+		for (int p = 0; p < 3; ++p) {
+			const int sh_ = shifts[p];
+			const unsigned dmask = (1u << widths[p]) - 1u;
+			if (p > 0) {
+				for (int i = t; i < SEL_BINS; i += SEL_THREADS) hist[i] = 0;
+				__syncthreads();
+				for (int64_t i = t; i < n; i += SEL_THREADS) {
+					uint32_t k, sl;
+					src.get(q, i, k, sl);
+					if ((k & mask) == prefix) atomicAdd(&hist[(k >> sh_) & dmask], 1u);
+				}
+				__syncthreads();
+			}
+			// each thread owns 8 consecutive bins
+			unsigned local = 0;
+#pragma unroll
+			for (int j = 0; j < 8; ++j) local += hist[t * 8 + j];
+			unsigned total;
+			unsigned excl = block_excl_scan(local, sh, total);
+			if (excl < rem && rem <= excl + local) {
+				unsigned c = excl;
+				for (int j = 0; j < 8; ++j) {
+					unsigned h = hist[t * 8 + j];
+					if (rem <= c + h) {
+						s_digit = (unsigned)(t * 8 + j);
+						s_rem = rem - c;
+						break;
+					}
+					c += h;
+				}
+			}
+			__syncthreads();
+			prefix |= s_digit << sh_;
+			mask |= dmask << sh_;
+			rem = s_rem;
+			__syncthreads();
+		}
+		const uint32_t T = prefix;          // key of the M-th smallest
+		const unsigned n_lt = (unsigned)M - rem;  // entries strictly below T
+		for (int64_t i = t; i < n; i += SEL_THREADS) {
+			uint32_t k, sl;
+			src.get(q, i, k, sl);
+			if (k < T) {
+				unsigned p = atomicAdd(&s_nlt, 1u);
+				cand_slot[(int64_t)q * M + p] = sl;
+			} else if (k == T) {
+				unsigned p = atomicAdd(&s_neq, 1u);
+				if (p < rem)
+					cand_slot[(int64_t)q * M + n_lt + p] = sl;
+				else
+					atomicMin(&s_minex, k);
+			} else if (k < KEY_INF) {
+				atomicMin(&s_minex, k);
+			}
+		}
+		__syncthreads();
+		c_out = (s_minex == 0xFFFFFFFFu) ? F_INF : fkey_inv(s_minex);
+		if (ftau < c_out) c_out = ftau;
+		if (t == 0) s_nlt = (unsigned)M;
+		__syncthreads();
+	}
+	if (t == 0) {
+		if (overflow || n_nan > 0) c_out = -F_INF;
+		cand_cnt[q] = (int)s_nlt;
+		cut[q] = c_out;
+	}
+}
+
+void launch_select(const float *dense, int64_t ld_dense, int64_t n_entries, int64_t tile_stride, const uint2 *pool,
+                   const int *pool_cnt, int cap, const float *tau, int nq, int M, uint32_t *cand_slot,
+                   int *cand_cnt, float *cut, hipStream_t st) {
+	SelSrc s{dense, ld_dense, n_entries, tile_stride, pool, cap};
+	select_kernel<<<dim3(nq), dim3(SEL_THREADS), 0, st>>>(s, pool_cnt, tau, M, cand_slot, cand_cnt, cut);
+}
+
+// ---------------------------------------------------------------------------
+// refine: one wave per (query, candidate), f64 accumulation
+// ---------------------------------------------------------------------------
+template <int METRIC>
+__device__ __forceinline__ float exact_distance(const float *__restrict__ x, const float *__restrict__ q, int dim,
+                                                int lane) {
+	double a = 0.0, b = 0.0, c = 0.0;
+	for (int i = lane; i < dim; i += 64) {
+		double xv = x[i], qv = q[i];
+		if (METRIC == METRIC_L2) {
+			double d = xv - qv;
+			a += d * d;
+		} else {
+			a += xv * qv;
+			if (METRIC == METRIC_COSINE) {
+				b += xv * xv;
+				c += qv * qv;
+			}
+		}
+	}
+	a = wave_sum_f64(a);
+	if (METRIC == METRIC_COSINE) {
+		b = wave_sum_f64(b);
+		c = wave_sum_f64(c);
+	}
+	double r;
+	if (METRIC == METRIC_L2)
+		r = a;
+	else if (METRIC == METRIC_DOT)
+		r = 1.0 - a;
+	else
+		r = 1.0 - a / (sqrt(b) * sqrt(c));
+	float f = (float)r + 0.0f;  // canonical +0
+	if (__builtin_isnan(f)) f = __builtin_nanf("");
+	return f;
+}
+
+template <int METRIC>
+__global__ __launch_bounds__(256) void refine_kernel(const float *__restrict__ X, int ld, int dim,
+                                                     const float *__restrict__ Qf,
+                                                     const uint32_t *__restrict__ cand_slot,
+                                                     const int *__restrict__ cand_cnt, int nq, int M,
+                                                     float *__restrict__ cand_dist) {
+	const int lane = threadIdx.x & 63;
+	const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+	if (g >= (int64_t)nq * M) return;
+	const int q = (int)(g / M), m = (int)(g % M);
+	if (m >= cand_cnt[q]) return;
+	const uint32_t slot = cand_slot[(int64_t)q * M + m];
+	float d = exact_distance<METRIC>(X + (int64_t)slot * ld, Qf + (int64_t)q * ld, dim, lane);
+	if (lane == 0) cand_dist[(int64_t)q * M + m] = d;
+}
+
+void launch_refine(const StoreView &s, const QueryView &q, const uint32_t *cand_slot, const int *cand_cnt, int M,
+                   float *cand_dist, hipStream_t st) {
+	int64_t waves = (int64_t)q.nq * M;
+	dim3 grid((unsigned)((waves + 3) / 4));
+	switch (s.metric) {
+	case METRIC_L2:
+		refine_kernel<METRIC_L2><<<grid, 256, 0, st>>>(s.X, s.ld, s.dim, q.Qf, cand_slot, cand_cnt, q.nq, M, cand_dist);
+		break;
+	case METRIC_DOT:
+		refine_kernel<METRIC_DOT><<<grid, 256, 0, st>>>(s.X, s.ld, s.dim, q.Qf, cand_slot, cand_cnt, q.nq, M, cand_dist);
+		break;
+	default:
+		refine_kernel<METRIC_COSINE><<<grid, 256, 0, st>>>(s.X, s.ld, s.dim, q.Qf, cand_slot, cand_cnt, q.nq, M,
+		                                                    cand_dist);
+		break;
+	}
+}
+
+// ---------------------------------------------------------------------------
+// finalize: rank candidates by (distance, label); top-k + certificate, or tau
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void finalize_kernel(const int64_t *__restrict__ labels,
+                                                       const uint32_t *__restrict__ cand_slot,
+                                                       const int *__restrict__ cand_cnt,
+                                                       const float *__restrict__ cand_dist,
+                                                       const float *__restrict__ cut, int M, int k, int mode,
+                                                       int need_for_tau, float *__restrict__ tau,
+                                                       int64_t *__restrict__ out_labels,
+                                                       float *__restrict__ out_dists, int *__restrict__ out_counts,
+                                                       int *__restrict__ cert_ok) {
+	__shared__ float sd[MAX_CAND];
+	__shared__ int64_t sl[MAX_CAND];
+	__shared__ float s_dk;
+	const int q = blockIdx.x;
+	const int t = threadIdx.x;
+	const int m = cand_cnt[q];
+	for (int i = t; i < m; i += 256) {
+		sd[i] = cand_dist[(int64_t)q * M + i];
+		sl[i] = labels[cand_slot[(int64_t)q * M + i]];
+	}
+	if (t == 0) s_dk = F_INF;
+	__syncthreads();
+	if (mode == 0) {
+		// tau = largest exact distance among the candidates (they are real rows)
+		if (t == 0) {
+			float mx = -F_INF;
+			bool nan = false;
+			for (int i = 0; i < m; ++i) {
+				if (__builtin_isnan(sd[i])) nan = true;
+				mx = fmaxf(mx, sd[i]);
+			}
+			tau[q] = (m >= need_for_tau && m > 0) ? (nan ? __builtin_nanf("") : mx) : F_INF;
+		}
+		return;
+	}
+	const int nout = m < k ? m : k;
+	for (int i = t; i < m; i += 256) {
+		int rank = 0;
+		const float d = sd[i];
+		const int64_t l = sl[i];
+		for (int j = 0; j < m; ++j) rank += hit_less(sd[j], sl[j], d, l) ? 1 : 0;
+		if (rank < k) {
+			out_labels[(int64_t)q * k + rank] = l;
+			out_dists[(int64_t)q * k + rank] = d;
+		}
+		if (rank == k - 1) s_dk = d;
+	}
+	for (int i = nout + t; i < k; i += 256) {
+		out_labels[(int64_t)q * k + i] = -1;
+		out_dists[(int64_t)q * k + i] = __builtin_nanf("");
+	}
+	__syncthreads();
+	if (t == 0) {
+		out_counts[q] = nout;
+		const float c = cut[q];
+		bool ok;
+		if (c == F_INF) {
+			ok = true;  // nothing live was left out
+		} else {
+			const float dk = s_dk;  // +inf when fewer than k candidates
+			ok = !__builtin_isnan(dk) && dk < F_INF && c > nextafterf(dk, F_INF);
+		}
+		cert_ok[q] = ok ? 1 : 0;
+	}
+}
+
+void launch_finalize(const StoreView &s, const uint32_t *cand_slot, const int *cand_cnt, const float *cand_dist,
+                     const float *cut, int nq, int M, int k, int mode, int need_for_tau, float *tau,
+                     int64_t *out_labels, float *out_dists, int *out_counts, int *cert_ok, hipStream_t st) {
+	finalize_kernel<<<dim3(nq), dim3(256), 0, st>>>(s.labels, cand_slot, cand_cnt, cand_dist, cut, M, k, mode,
+	                                                 need_for_tau, tau, out_labels, out_dists, out_counts, cert_ok);
+}
+
+// ---------------------------------------------------------------------------
+// exact fallback
+// ---------------------------------------------------------------------------
+template <int METRIC>
+__global__ __launch_bounds__(256) void exact_all_kernel(const float *__restrict__ X, const float4 *__restrict__ rowaux,
+                                                        const int64_t *__restrict__ labels, int64_t n, int ld,
+                                                        int dim, const float *__restrict__ q,
+                                                        float *__restrict__ keys, int64_t *__restrict__ vals) {
+	const int lane = threadIdx.x & 63;
+	const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+	if (r >= n) return;
+	float d = exact_distance<METRIC>(X + r * ld, q, dim, lane);
+	if (lane == 0) {
+		const float a = rowaux[r].x;
+		const bool dead = (a == F_INF);
+		keys[r] = dead ? __uint_as_float(0x7FFFFFFFu) : d;
+		vals[r] = labels[r];
+	}
+}
+
+void launch_exact_all(const StoreView &s, const QueryView &q, int qi, float *keys, int64_t *vals, hipStream_t st) {
+	if (s.n_slots <= 0) return;
+	dim3 grid((unsigned)((s.n_slots + 3) / 4));
+	const float *qq = q.Qf + (int64_t)qi * s.ld;
+	switch (s.metric) {
+	case METRIC_L2:
+		exact_all_kernel<METRIC_L2><<<grid, 256, 0, st>>>(s.X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim, qq, keys,
+		                                                   vals);
+		break;
+	case METRIC_DOT:
+		exact_all_kernel<METRIC_DOT><<<grid, 256, 0, st>>>(s.X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim, qq, keys,
+		                                                    vals);
+		break;
+	default:
+		exact_all_kernel<METRIC_COSINE><<<grid, 256, 0, st>>>(s.X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim, qq,
+		                                                       keys, vals);
+		break;
+	}
+}
+
+int sort_pairs(void *temp, size_t &temp_bytes, const float *keys_in, float *keys_out, const int64_t *vals_in,
+               int64_t *vals_out, int64_t n, hipStream_t st) {
+	hipError_t e = rocprim::radix_sort_pairs(temp, temp_bytes, keys_in, keys_out, vals_in, vals_out, (size_t)n, 0,
+	                                         32, st);
+	return (int)e;
+}
+
+__global__ void copy_fallback_kernel(const float *keys, const int64_t *vals, int64_t n_live, int k, int qi,
+                                     int64_t *out_labels, float *out_dists, int *out_counts) {
+	int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= k) return;
+	if (i < n_live) {
+		out_labels[(int64_t)qi * k + i] = vals[i];
+		out_dists[(int64_t)qi * k + i] = keys[i];
+	} else {
+		out_labels[(int64_t)qi * k + i] = -1;
+		out_dists[(int64_t)qi * k + i] = __builtin_nanf("");
+	}
+	if (i == 0) out_counts[qi] = (int)(n_live < k ? n_live : k);
+}
+
+void launch_copy_fallback(const float *keys, const int64_t *vals, int64_t n_live, int k, int qi, int64_t *out_labels,
+                          float *out_dists, int *out_counts, hipStream_t st) {
+	copy_fallback_kernel<<<dim3((k + 255) / 256), dim3(256), 0, st>>>(keys, vals, n_live, k, qi, out_labels,
+	                                                                   out_dists, out_counts);
+}
+
+// ---------------------------------------------------------------------------
+// multi-shard merge of partial top-k lists (one workgroup per query)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void merge_topk_kernel(int nshard, int nq, int k,
+                                                         const int64_t *__restrict__ part_labels,
+                                                         const float *__restrict__ part_dists,
+                                                         const int *__restrict__ part_counts,
+                                                         int64_t *__restrict__ out_labels,
+                                                         float *__restrict__ out_dists, int *__restrict__ out_counts) {
+	const int q = blockIdx.x;
+	const int t = threadIdx.x;
+	const int total = nshard * k;
+	int written = 0;
+	for (int s = 0; s < nshard; ++s) {
+		int c = part_counts[(int64_t)s * nq + q];
+		written += c < k ? c : k;
+	}
+	for (int e = t; e < total; e += 256) {
+		const int s = e / k, i = e % k;
+		int c = part_counts[(int64_t)s * nq + q];
+		if (i >= c) continue;
+		const int64_t base = ((int64_t)s * nq + q) * k;
+		const float d = part_dists[base + i];
+		const int64_t l = part_labels[base + i];
+		int rank = 0;
+		for (int s2 = 0; s2 < nshard; ++s2) {
+			int c2 = part_counts[(int64_t)s2 * nq + q];
+			c2 = c2 < k ? c2 : k;
+			const int64_t b2 = ((int64_t)s2 * nq + q) * k;
+			for (int j = 0; j < c2; ++j) rank += hit_less(part_dists[b2 + j], part_labels[b2 + j], d, l) ? 1 : 0;
+			if (rank >= k) break;
+		}
+		if (rank < k) {
+			out_labels[(int64_t)q * k + rank] = l;
+			out_dists[(int64_t)q * k + rank] = d;
+		}
+	}
+	const int nout = written < k ? written : k;
+	for (int i = nout + t; i < k; i += 256) {
+		out_labels[(int64_t)q * k + i] = -1;
+		out_dists[(int64_t)q * k + i] = __builtin_nanf("");
+	}
+	if (t == 0) out_counts[q] = nout;
+}
+
+void launch_merge_topk(int nshard, int nq, int k, const int64_t *part_labels, const float *part_dists,
+                       const int *part_counts, int64_t *out_labels, float *out_dists, int *out_counts,
+                       hipStream_t st) {
+	merge_topk_kernel<<<dim3(nq), dim3(256), 0, st>>>(nshard, nq, k, part_labels, part_dists, part_counts,
+	                                                   out_labels, out_dists, out_counts);
+}
+
+// ---------------------------------------------------------------------------
+// compaction gather
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gather_rows_kernel(const float *__restrict__ X, const float4 *__restrict__ rowaux,
+                                                          const int64_t *__restrict__ labels,
+                                                          const int64_t *__restrict__ idx, int64_t n, int ld,
+                                                          float *__restrict__ Xo, float4 *__restrict__ rowaux_o,
+                                                          int64_t *__restrict__ labels_o) {
+	const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+	const int lane = threadIdx.x & 63;
+	if (r >= n) return;
+	const int64_t s = idx[r];
+	for (int i = lane * 4; i < ld; i += 256)
+		*reinterpret_cast<float4 *>(Xo + r * ld + i) = *reinterpret_cast<const float4 *>(X + s * ld + i);
+	if (lane == 0) {
+		rowaux_o[r] = rowaux[s];
+		labels_o[r] = labels[s];
+	}
+}
+
+void launch_gather_rows(const float *X, const float4 *rowaux, const int64_t *labels, const int64_t *idx, int64_t n,
+                        int ld, float *Xo, float4 *rowaux_o, int64_t *labels_o, hipStream_t st) {
+	if (n <= 0) return;
+	gather_rows_kernel<<<dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st>>>(X, rowaux, labels, idx, n, ld, Xo,
+	                                                                       rowaux_o, labels_o);
+}
+
+}  // namespace lhip

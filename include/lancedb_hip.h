@@ -1,0 +1,174 @@
+/*
+ * lancedb_hip.h — the drop-in C-ABI of the MI355X-native k-NN path.
+ *
+ * Every symbol below replaces the export of the same name in the reference's
+ * Rust library (rust_lib/src/ffi.rs), consumed unchanged by the reference's C++
+ * shim src/rust_ffi.cpp:7-42 (paths relative to /root/reference).  Conventions
+ * kept from ffi.rs:
+ *   - handle = opaque pointer owning all state (ffi.rs:51), freed only by
+ *     lance_free_detached (null-safe, ffi.rs:137-142);
+ *   - errors: NULL / -1 return plus a NUL-terminated message truncated to
+ *     err_buf_len-1 bytes (ffi.rs:15-24); a NULL handle reports "null handle";
+ *   - every output buffer is caller-allocated; strings are borrowed;
+ *   - calls may arrive from any thread; search may run concurrently with
+ *     add/delete (the handle serialises internally).
+ * Symbols marked NEW have no counterpart in the shipped ffi.rs.
+ */
+#ifndef LANCEDB_HIP_H
+#define LANCEDB_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- create / open / free ------------------------------------------------ */
+
+/* ffi.rs:37-57 (called from rust_ffi.cpp:47).  Creates (replacing any existing
+ * table of that name, lance_manager.rs:42) an empty vector-only table.
+ * metric: "l2" (default) | "dot" | "ip" | "cosine".  db_path "" = in-memory. */
+void *lance_create_detached(const char *db_path, int32_t dimension, const char *metric, const char *table_name,
+                            char *err_buf, int err_buf_len);
+
+/* ffi.rs:62-89 (rust_ffi.cpp:58).  Multi-column Arrow tables: not supported by
+ * this build yet — returns NULL with an error message. */
+void *lance_create_detached_from_arrow(const char *db_path, void *arrow_schema, const char *metric,
+                                       const char *table_name, char *err_buf, int err_buf_len);
+
+/* ffi.rs:92-111 (rust_ffi.cpp:68).  Re-opens a table persisted under db_path;
+ * next label = max(label)+1 (lance_manager.rs:157-158). */
+void *lance_open_detached(const char *db_path, const char *table_name, const char *metric, char *err_buf,
+                          int err_buf_len);
+
+/* ffi.rs:137-142 (rust_ffi.cpp:76).  Null-safe. */
+void lance_free_detached(void *handle);
+
+/* ffi.rs:114-123 / :126-135 (rust_ffi.cpp:80,84).  0 for a null handle. */
+int32_t lance_detached_has_extra_columns(void *handle);
+int32_t lance_detached_dimension(void *handle);
+
+/* ---- ingest --------------------------------------------------------------- */
+
+/* ffi.rs:228-250 (rust_ffi.cpp:88).  Returns the new label or -1. */
+int64_t lance_detached_add(void *handle, const float *vector, int32_t dimension, char *err_buf, int err_buf_len);
+
+/* ffi.rs:252-289 (rust_ffi.cpp:97).  vectors: num x dim row-major f32 (DuckDB
+ * ARRAY child buffer, lance_index.cpp:940-946).  Labels are dense consecutive
+ * [next_label, next_label+num) (lance_manager.rs:232-233).  Returns num or -1. */
+int32_t lance_detached_add_batch(void *handle, const float *vectors, int32_t num, int32_t dim, int64_t *out_labels,
+                                 char *err_buf, int err_buf_len);
+
+/* ffi.rs:147-180 (rust_ffi.cpp:108).  Not supported yet: returns -1. */
+int32_t lance_detached_add_batch_arrow(void *handle, void *arrow_schema, void *arrow_array, int64_t *out_labels,
+                                       char *err_buf, int err_buf_len);
+
+/* ffi.rs:186-222 (rust_ffi.cpp:118).  Copies the listed live rows of source
+ * into target under fresh target labels; writes the (old,new) label pairs. */
+int32_t lance_detached_merge(void *target_handle, void *source_handle, const int64_t *live_source_labels,
+                             int32_t live_count, int64_t *out_old_labels, int64_t *out_new_labels, char *err_buf,
+                             int err_buf_len);
+
+/* ---- search --------------------------------------------------------------- */
+
+/* ffi.rs:295-329 (rust_ffi.cpp:130-139).  Exact top-k of one query over all
+ * live rows, ascending distance (ties: label ascending); writes n <= k
+ * (label, distance) pairs, returns n or -1.  dim != index dim is an error here
+ * (lance_manager.rs:401-407); the C++ caller returns {} before calling
+ * (lance_index.cpp:444-446).  nprobes / refine_factor only matter once an
+ * IVF index exists (lance_index.hpp:91-92 defaults 20 / 1). */
+int32_t lance_detached_search(void *handle, const float *query, int32_t dim, int32_t k, int32_t nprobes,
+                              int32_t refine_factor, int64_t *out_labels, float *out_distances, char *err_buf,
+                              int err_buf_len);
+
+/* NEW — the form the reference's C++ already calls (lance_index.cpp:452-453):
+ * a nullable Lance-SQL predicate inserted after refine_factor.  NULL or "" =
+ * unfiltered.  A non-empty predicate needs metadata columns (Arrow path), which
+ * this build does not store yet: returns -1 with an error. */
+int32_t lance_detached_search_with_predicate(void *handle, const float *query, int32_t dim, int32_t k,
+                                             int32_t nprobes, int32_t refine_factor, const char *predicate,
+                                             int64_t *out_labels, float *out_distances, char *err_buf,
+                                             int err_buf_len);
+
+/* NEW — batched search.  queries: nq x dim row-major f32;
+ * out_labels / out_distances: nq x k (unused slots: label -1, distance NaN);
+ * out_counts: nq.  Returns nq or -1. */
+int32_t lance_detached_search_batch(void *handle, const float *queries, int32_t nq, int32_t dim, int32_t k,
+                                    int32_t nprobes, int32_t refine_factor, const char *predicate,
+                                    int64_t *out_labels, float *out_distances, int32_t *out_counts, char *err_buf,
+                                    int err_buf_len);
+
+/* ---- count / delete ------------------------------------------------------- */
+
+/* ffi.rs:335-353 (rust_ffi.cpp:141).  Live rows, or -1. */
+int64_t lance_detached_count(void *handle, char *err_buf, int err_buf_len);
+
+/* ffi.rs:355-374 / :376-397 (rust_ffi.cpp:150,159).  0 or -1.  Unknown or
+ * already-deleted labels are a no-op (a SQL `label IN (..)` delete). */
+int32_t lance_detached_delete(void *handle, int64_t label, char *err_buf, int err_buf_len);
+int32_t lance_detached_delete_batch(void *handle, const int64_t *labels, int32_t count, char *err_buf,
+                                    int err_buf_len);
+
+/* ---- ANN index / maintenance --------------------------------------------- */
+
+/* ffi.rs:403-423 (rust_ffi.cpp:168).  IVF build: not in this build yet; the
+ * flat path stays exact, so this returns 0 and records the parameters. */
+int32_t lance_detached_create_index(void *handle, int32_t num_partitions, int32_t num_sub_vectors, char *err_buf,
+                                    int err_buf_len);
+
+/* ffi.rs:425-445 (rust_ffi.cpp:176).  HNSW is out of scope:
+ * returns 0 and keeps serving exact flat search (lance_hnsw.test pins only
+ * result counts). */
+int32_t lance_detached_create_hnsw_index(void *handle, int32_t m, int32_t ef_construction, char *err_buf,
+                                          int err_buf_len);
+
+/* ffi.rs:447-465 (rust_ffi.cpp:184).  Drops tombstoned rows from the device
+ * store (labels are preserved).  0 or -1. */
+int32_t lance_detached_compact(void *handle, char *err_buf, int err_buf_len);
+
+/* ffi.rs:471-500 (rust_ffi.cpp:192).  Copies the vector of a live label into
+ * out_vec (capacity floats); returns dim or -1 ("output buffer too small",
+ * "label N not found"). */
+int32_t lance_detached_get_vector(void *handle, int64_t label, float *out_vec, int32_t capacity, char *err_buf,
+                                  int err_buf_len);
+
+/* ffi.rs:510-541 (rust_ffi.cpp:201).  With out_labels/out_vectors NULL only
+ * *out_count is written.  Rows in ascending label order. */
+int32_t lance_detached_get_all_vectors(void *handle, int64_t *out_labels, float *out_vectors, int64_t *out_count,
+                                       char *err_buf, int err_buf_len);
+
+/* ---- NEW: device / sharding / introspection -------------------------------- */
+
+/* Library version string (static storage). */
+const char *lance_hip_version(void);
+
+/* Number of HIP devices visible to the library (0 when none / no driver). */
+int32_t lance_hip_device_count(void);
+
+/* Per-handle options, key/value strings:
+ *   "device"       HIP device ordinal for the store (default: current device)
+ *   "metric_quirk" "1" = rank every search by squared L2 whatever the index
+ *                  metric, exactly as the reference does (lance_manager.rs:
+ *                  411-418 never sets distance_type); default "0"
+ * Returns 0 or -1. */
+int32_t lance_hip_set_option(void *handle, const char *key, const char *value, char *err_buf, int err_buf_len);
+
+/* Statistics of the last search on this handle (for benches/tests):
+ * out[0] = queries whose exactness certificate failed and took the exact
+ * fallback, out[1] = total candidates refined, out[2] = max pool size,
+ * out[3] = 1 if the dense (small-N) path ran.  Returns 0 or -1. */
+int32_t lance_hip_last_search_stats(void *handle, int64_t *out, int32_t n);
+
+/* Merge per-shard partial top-k lists into a global top-k, on the device of
+ * the handle (multi-GPU path: shards all-gathered over RCCL).
+ * part_labels / part_dists: nshard x nq x k (host pointers), part_counts:
+ * nshard x nq.  Order (distance asc, label asc).  Returns nq or -1. */
+int32_t lance_hip_merge_topk(int32_t nshard, int32_t nq, int32_t k, const int64_t *part_labels,
+                             const float *part_dists, const int32_t *part_counts, int64_t *out_labels,
+                             float *out_dists, int32_t *out_counts, char *err_buf, int err_buf_len);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LANCEDB_HIP_H */

@@ -1,0 +1,72 @@
+"""ctypes loader for oracle/build/liboracle_knn.so — TEST INFRASTRUCTURE ONLY.
+
+Used by tests/ (checker at sizes where numpy is slow) and by bench.py's
+``cpu_baseline`` leg (the timed "port" of the reference's flat search,
+``rust_lib/src/lance_manager.rs:393-451``).  Never imported by the product.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle_knn.so")
+_lib = None
+
+METRIC_IDS = {"l2": 0, "dot": 1, "cosine": 2}
+
+
+def build() -> str:
+    import subprocess
+
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        P = ctypes.c_void_p
+        L.oracle_flat_search_batch.argtypes = [P, ctypes.c_int64, ctypes.c_int32, P, P, P, ctypes.c_int32,
+                                               ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                               P, P, P]
+        L.oracle_flat_search_batch.restype = ctypes.c_int
+        L.oracle_distances.argtypes = [P, ctypes.c_int64, ctypes.c_int32, P, ctypes.c_int32, P]
+        L.oracle_distances.restype = None
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def flat_search_batch(base, Q, k, metric="l2", live=None, labels=None, acc64=True, nthreads=0):
+    base = np.ascontiguousarray(base, dtype=np.float32)
+    Q = np.ascontiguousarray(Q, dtype=np.float32)
+    n, d = base.shape
+    nq = Q.shape[0]
+    live_a = None if live is None else np.ascontiguousarray(live, dtype=np.uint8)
+    lab_a = None if labels is None else np.ascontiguousarray(labels, dtype=np.int64)
+    out_l = np.empty((nq, k), np.int64)
+    out_d = np.empty((nq, k), np.float32)
+    cnt = np.empty(nq, np.int32)
+    rc = lib().oracle_flat_search_batch(_ptr(base), n, d, _ptr(live_a), _ptr(lab_a), _ptr(Q), nq, k,
+                                        METRIC_IDS[metric], 1 if acc64 else 0, int(nthreads),
+                                        _ptr(out_l), _ptr(out_d), _ptr(cnt))
+    if rc != 0:
+        raise MemoryError("oracle_flat_search_batch failed")
+    return out_l, out_d, cnt
+
+
+def distances(base, q, metric="l2"):
+    base = np.ascontiguousarray(base, dtype=np.float32)
+    q = np.ascontiguousarray(q, dtype=np.float32)
+    out = np.empty(base.shape[0], np.float32)
+    lib().oracle_distances(_ptr(base), base.shape[0], base.shape[1], _ptr(q), METRIC_IDS[metric], _ptr(out))
+    return out

@@ -1,0 +1,215 @@
+/*
+ * CPU ORACLE / CPU BASELINE — test infrastructure only, never the product path.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load this
+ * library (oracle/build/liboracle_knn.so).  The product search path is the HIP
+ * library behind include/lancedb_hip.h; it never links or calls this file.
+ *
+ * Restates the reference's flat exact k-NN (paths relative to /root/reference):
+ *   rust_lib/src/lance_manager.rs:393-451  LanceIndex::search -> lancedb 0.15
+ *   Table::vector_search(q).limit(k) with no ANN index = lance 0.22 flat KNN:
+ *   distance of every live row (lance-linalg 0.22: l2 = sum (x-q)^2, no sqrt;
+ *   dot = 1 - x.q; cosine = 1 - x.q/(|x||q|)), ascending, at most k hits.
+ * The reference itself cannot be built here (no cargo/rustc, crates offline,
+ * duckdb submodule empty — SURVEY.md §0.3), so this file is the "port" CPU
+ * baseline of BASELINE.md: OpenMP over host cores, per-thread top-k heaps,
+ * merged at the end.
+ *
+ *   acc64 = 1 : float64 accumulation, rounded once to float32 (the checker:
+ *               identical to oracle/flat_knn.py and to the HIP refine stage)
+ *   acc64 = 0 : float32 accumulation in a SIMD-friendly loop (what
+ *               lance-linalg does; used for the timed cpu_baseline)
+ * Ties: (distance asc, label asc).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <omp.h>
+
+typedef struct {
+	float d;
+	int64_t l;
+} hit_t;
+
+static inline int hit_less(hit_t a, hit_t b) {
+	/* NaN sorts after everything */
+	int an = isnan(a.d), bn = isnan(b.d);
+	if (an != bn) return bn;
+	if (a.d != b.d) return a.d < b.d;
+	return a.l < b.l;
+}
+
+/* max-heap on hit_less (root = worst kept hit) */
+static void heap_push(hit_t *h, int *n, int cap, hit_t x) {
+	if (*n < cap) {
+		int i = (*n)++;
+		h[i] = x;
+		while (i > 0) {
+			int p = (i - 1) >> 1;
+			if (hit_less(h[p], h[i])) {
+				hit_t t = h[p];
+				h[p] = h[i];
+				h[i] = t;
+				i = p;
+			} else {
+				break;
+			}
+		}
+		return;
+	}
+	if (!hit_less(x, h[0])) return;
+	h[0] = x;
+	int i = 0;
+	for (;;) {
+		int l = 2 * i + 1, r = l + 1, m = i;
+		if (l < cap && hit_less(h[m], h[l])) m = l;
+		if (r < cap && hit_less(h[m], h[r])) m = r;
+		if (m == i) break;
+		hit_t t = h[m];
+		h[m] = h[i];
+		h[i] = t;
+		i = m;
+	}
+}
+
+static int cmp_hit(const void *a, const void *b) {
+	hit_t x = *(const hit_t *)a, y = *(const hit_t *)b;
+	if (hit_less(x, y)) return -1;
+	if (hit_less(y, x)) return 1;
+	return 0;
+}
+
+static inline float dist64(const float *x, const float *q, int32_t d, int metric, double qn2) {
+	if (metric == 0) {
+		double s = 0.0;
+		for (int32_t i = 0; i < d; i++) {
+			double t = (double)x[i] - (double)q[i];
+			s += t * t;
+		}
+		return (float)s;
+	}
+	double dot = 0.0, xx = 0.0;
+	for (int32_t i = 0; i < d; i++) {
+		dot += (double)x[i] * (double)q[i];
+		xx += (double)x[i] * (double)x[i];
+	}
+	if (metric == 1) return (float)(1.0 - dot);
+	return (float)(1.0 - dot / (sqrt(xx) * sqrt(qn2)));
+}
+
+static inline float dist32(const float *restrict x, const float *restrict q, int32_t d, int metric, float qn2) {
+	/* 8 independent f32 partial sums: vectorises to one AVX2 register */
+	float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	float acc2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	int32_t i = 0;
+	if (metric == 0) {
+		for (; i + 8 <= d; i += 8)
+			for (int j = 0; j < 8; j++) {
+				float t = x[i + j] - q[i + j];
+				acc[j] += t * t;
+			}
+		float s = 0.f;
+		for (int j = 0; j < 8; j++) s += acc[j];
+		for (; i < d; i++) {
+			float t = x[i] - q[i];
+			s += t * t;
+		}
+		return s;
+	}
+	for (; i + 8 <= d; i += 8)
+		for (int j = 0; j < 8; j++) {
+			acc[j] += x[i + j] * q[i + j];
+			acc2[j] += x[i + j] * x[i + j];
+		}
+	float dot = 0.f, xx = 0.f;
+	for (int j = 0; j < 8; j++) {
+		dot += acc[j];
+		xx += acc2[j];
+	}
+	for (; i < d; i++) {
+		dot += x[i] * q[i];
+		xx += x[i] * x[i];
+	}
+	if (metric == 1) return 1.f - dot;
+	return 1.f - dot / (sqrtf(xx) * sqrtf(qn2));
+}
+
+/*
+ * Batched exact top-k.  base [n][d] row-major f32; live (nullable) 1 = live;
+ * labels (nullable) -> label = row index; Q [nq][d].
+ * Rows are split over threads in blocks of ROWBLK so each block of base rows is
+ * reused from cache for every query; per-(thread, query) heaps of size k are
+ * merged at the end.  Returns 0, or -1 on allocation failure.
+ */
+#define ROWBLK 64
+int oracle_flat_search_batch(const float *base, int64_t n, int32_t d, const uint8_t *live, const int64_t *labels,
+                             const float *Q, int32_t nq, int32_t k, int32_t metric, int32_t acc64, int32_t nthreads,
+                             int64_t *out_labels, float *out_dist, int32_t *out_counts) {
+	if (k <= 0 || nq <= 0) return 0;
+	if (nthreads <= 0) nthreads = omp_get_max_threads();
+	double *qn2 = (double *)calloc((size_t)nq, sizeof(double));
+	hit_t *heaps = (hit_t *)malloc((size_t)nthreads * nq * k * sizeof(hit_t));
+	int *hn = (int *)calloc((size_t)nthreads * nq, sizeof(int));
+	if (!qn2 || !heaps || !hn) {
+		free(qn2);
+		free(heaps);
+		free(hn);
+		return -1;
+	}
+	for (int32_t j = 0; j < nq; j++) {
+		double s = 0;
+		for (int32_t i = 0; i < d; i++) s += (double)Q[(size_t)j * d + i] * Q[(size_t)j * d + i];
+		qn2[j] = s;
+	}
+	int64_t nblk = (n + ROWBLK - 1) / ROWBLK;
+#pragma omp parallel num_threads(nthreads)
+	{
+		int t = omp_get_thread_num();
+		hit_t *my = heaps + (size_t)t * nq * k;
+		int *myn = hn + (size_t)t * nq;
+#pragma omp for schedule(dynamic, 16)
+		for (int64_t b = 0; b < nblk; b++) {
+			int64_t r0 = b * ROWBLK, r1 = r0 + ROWBLK < n ? r0 + ROWBLK : n;
+			for (int32_t j = 0; j < nq; j++) {
+				const float *q = Q + (size_t)j * d;
+				for (int64_t r = r0; r < r1; r++) {
+					if (live && !live[r]) continue;
+					const float *x = base + (size_t)r * d;
+					float dd = acc64 ? dist64(x, q, d, metric, qn2[j]) : dist32(x, q, d, metric, (float)qn2[j]);
+					hit_t h = {dd, labels ? labels[r] : r};
+					heap_push(my + (size_t)j * k, &myn[j], k, h);
+				}
+			}
+		}
+	}
+	/* merge per-thread heaps */
+	hit_t *tmp = (hit_t *)malloc((size_t)nthreads * k * sizeof(hit_t));
+	for (int32_t j = 0; j < nq; j++) {
+		int m = 0;
+		for (int t = 0; t < nthreads; t++) {
+			memcpy(tmp + m, heaps + ((size_t)t * nq + j) * k, (size_t)hn[(size_t)t * nq + j] * sizeof(hit_t));
+			m += hn[(size_t)t * nq + j];
+		}
+		qsort(tmp, (size_t)m, sizeof(hit_t), cmp_hit);
+		int c = m < k ? m : k;
+		out_counts[j] = c;
+		for (int i = 0; i < k; i++) {
+			out_labels[(size_t)j * k + i] = i < c ? tmp[i].l : -1;
+			out_dist[(size_t)j * k + i] = i < c ? tmp[i].d : NAN;
+		}
+	}
+	free(tmp);
+	free(qn2);
+	free(heaps);
+	free(hn);
+	return 0;
+}
+
+/* exact distances of all rows to one query (checker for size-independent tests) */
+void oracle_distances(const float *base, int64_t n, int32_t d, const float *q, int32_t metric, float *out) {
+	double qn2 = 0;
+	for (int32_t i = 0; i < d; i++) qn2 += (double)q[i] * q[i];
+#pragma omp parallel for schedule(static)
+	for (int64_t r = 0; r < n; r++) out[r] = dist64(base + (size_t)r * d, q, d, metric, qn2);
+}

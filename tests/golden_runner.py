@@ -1,0 +1,117 @@
+"""Runs the reference's SQL goldens (tests/golden/sql_goldens.json) against an
+index implementation: the CPU oracle (``oracle.flat_knn``) or the product
+(``lance_hip`` over the HIP C-ABI).  Shared by the CPU and GPU test files so
+both read like the reference's own sqllogictests."""
+from __future__ import annotations
+
+import json
+import math
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+
+
+def load_sql_goldens():
+    with open(os.path.join(GOLDEN, "sql_goldens.json")) as f:
+        return json.load(f)["cases"]
+
+
+def hnsw_rows(n):
+    # lance_hnsw.test:13-15: [sin(i::FLOAT), cos(i::FLOAT), (i % 10)::FLOAT / 10.0]
+    i = np.arange(n, dtype=np.float32)
+    return np.stack([np.sin(i), np.cos(i), (np.arange(n) % 10).astype(np.float32) / 10.0], 1).astype(np.float32)
+
+
+def _close(a, b):
+    return math.isclose(a, b, rel_tol=1e-4, abs_tol=1e-6)
+
+
+def run_index_case(case, make_index, restart):
+    """make_index(dim) -> object with Append/Delete/Search(q, dim, k);
+    restart(ix) -> reopened index (CHECKPOINT + restart)."""
+    ix = make_index(case["dim"])
+    for st in case["steps"]:
+        op = st["op"]
+        where = st.get("ref", case["ref"])
+        if op == "append":
+            ix.Append(np.array(st["rows"], np.float32), st["row_ids"])
+        elif op == "append_hnsw_rows":
+            rows = hnsw_rows(st["n"])
+            ix.Append(rows, list(range(st["n"])))
+        elif op == "create_hnsw":
+            ix.CreateHnswIndex(st["m"], st["ef"])
+        elif op == "delete":
+            ix.Delete(st["row_ids"])
+        elif op == "restart":
+            ix = restart(ix)
+        elif op in ("search", "count_search"):
+            q = np.array(st["q"], np.float32)
+            res = ix.Search(q, q.shape[0], st["k"])
+            if "expect" in st:
+                assert len(res) == len(st["expect"]), (where, res)
+                for (rid, d), (erid, ed) in zip(res, st["expect"]):
+                    assert rid == erid and _close(d, ed), (where, res, st["expect"])
+            if "expect_ids" in st:
+                assert [r for r, _ in res] == st["expect_ids"], (where, res)
+            if "expect_count" in st:
+                assert len(res) == st["expect_count"], (where, res)
+            if "expect_count_gt" in st:
+                assert len(res) > st["expect_count_gt"], (where, res)
+        else:
+            raise ValueError(op)
+    return ix
+
+
+def eval_predicate(where, lang, score):
+    """Evaluates the Lance SQL predicates the optimizer pushes down in
+    lance_optimizer_filter.test (ExpressionToLancePredicate output,
+    lance_optimizer.cpp:204-344)."""
+    if where is None:
+        return True
+    if where == "lang = 'en'":
+        return lang == "en"
+    if where == "score > 20":
+        return score > 20
+    if where == "lang = 'es'":
+        return lang == "es"
+    if where == "lang IS NOT NULL":
+        return lang is not None
+    if where == "lang IN ('en', 'fr')":
+        return lang in ("en", "fr")
+    if where == "NOT (lang = 'en')":
+        return not (lang == "en")
+    raise ValueError(where)
+
+
+def check_filter_result(query, got_ids):
+    """The (distance, label) order of this build vs LanceDB's heap order at a
+    tie on the cut-off (lance_optimizer_filter.test:36-44): accept either tied id."""
+    exp = query["expect_ids"]
+    if "tie_at_cutoff" in query:
+        assert got_ids[:-1] == exp[:-1], (query, got_ids)
+        assert got_ids[-1] in query["tie_at_cutoff"], (query, got_ids)
+    else:
+        assert got_ids == exp, (query, got_ids)
+
+
+def load_seeded():
+    with open(os.path.join(GOLDEN, "seeded_cases.json")) as f:
+        return json.load(f)
+
+
+def gen(seed, n, d):
+    return np.random.default_rng(seed).standard_normal((n, d), dtype=np.float32)
+
+
+def seeded_inputs(spec):
+    import hashlib
+
+    X = gen(spec["seed_base"], spec["n"], spec["d"])
+    Q = gen(spec["seed_q"], spec["nq"], spec["d"])
+    assert hashlib.sha256(X.tobytes()).hexdigest() == spec["sha_base"], "generator drift (base)"
+    assert hashlib.sha256(Q.tobytes()).hexdigest() == spec["sha_q"], "generator drift (queries)"
+    exp = np.load(os.path.join(GOLDEN, spec["name"] + ".npz"))
+    return X, Q, exp

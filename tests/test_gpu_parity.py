@@ -1,0 +1,313 @@
+"""GPU parity: the HIP path through the C-ABI vs the oracle and the reference's
+goldens.  Bar (BASELINE.json north_star): returned labels bit-exact, distances
+within 1e-4 relative (f32); the canonical order is (distance, label)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import c_oracle, flat_knn
+from tests.golden_runner import load_seeded, load_sql_goldens, run_index_case, seeded_inputs
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-4
+ATOL = 1e-5
+
+
+def assert_same(gl, gd, gc, el, ed, ec=None):
+    gl, gd = np.asarray(gl), np.asarray(gd)
+    el, ed = np.asarray(el), np.asarray(ed)
+    if ec is not None:
+        np.testing.assert_array_equal(gc, ec)
+    for i in range(el.shape[0]):
+        n = int(gc[i]) if gc is not None else el.shape[1]
+        np.testing.assert_array_equal(gl[i, :n], el[i, :n], err_msg=f"query {i}")
+        np.testing.assert_allclose(gd[i, :n], ed[i, :n], rtol=RTOL, atol=ATOL, err_msg=f"query {i}")
+
+
+@pytest.fixture
+def mk(hip, tmp_path):
+    made = []
+
+    def make(dim, metric="l2", path=None, table="vectors"):
+        h = hip.LanceCreateDetached(str(path if path is not None else tmp_path), dim, metric, table)
+        made.append(h)
+        return h
+
+    yield make
+    for h in made:
+        hip.LanceFreeDetached(h)
+
+
+# ---------------------------------------------------------------------------
+# the reference's own goldens through the LanceIndex mirror
+# ---------------------------------------------------------------------------
+INDEX_CASES = [c for c in load_sql_goldens() if "steps" in c and not c["name"].startswith("rust_")]
+
+
+@pytest.mark.parametrize("case", INDEX_CASES, ids=[c["name"] for c in INDEX_CASES])
+def test_sql_goldens(hip, tmp_path, case):
+    def make(dim):
+        return hip.LanceIndex(case["name"], dim, {}, lance_path=str(tmp_path / "db.lance" / case["name"]))
+
+    def restart(ix):
+        meta = ix.Serialize()
+        ix.CommitDrop()
+        return hip.LanceIndex.LoadFromStorage(ix.name, meta)
+
+    run_index_case(case, make, restart)
+
+
+def test_filter_golden_unfiltered_query(hip, tmp_path):
+    # lance_optimizer_filter.test:47-54 (no WHERE): top-2 of [1,0,0] -> ids 1,2
+    case = next(c for c in load_sql_goldens() if c["name"] == "filter_pushdown")
+    ix = hip.LanceIndex("docs_idx", 3, {}, lance_path=str(tmp_path))
+    ix.Append(np.array(case["rows"], np.float32), list(range(5)))
+    res = ix.Search(np.array([1, 0, 0], np.float32), 3, 2)
+    assert [case["ids"][r] for r, _ in res] == [1, 2]
+    with pytest.raises(hip.IOException, match="predicate"):
+        ix.Search(np.array([1, 0, 0], np.float32), 3, 2, predicate="lang = 'en'")
+
+
+def test_rust_label_semantics(hip, tmp_path):
+    p = str(tmp_path / "t.lance")
+    h = hip.LanceCreateDetached(p, 3, "l2", "vectors")
+    labs = [hip.LanceDetachedAdd(h, np.array([i, 0, 0], np.float32), 3) for i in range(5)]
+    assert labs == [0, 1, 2, 3, 4]                                     # lance_manager.rs:786-790
+    hip.LanceDetachedDelete(h, 1)
+    hip.LanceDetachedDelete(h, 2)
+    hip.LanceFreeDetached(h)
+    h = hip.LanceOpenDetached(p, "vectors", "l2")
+    assert hip.LanceDetachedAdd(h, np.array([99, 0, 0], np.float32), 3) >= 5   # :796-803
+    hip.LanceFreeDetached(h)
+    # empty reopen -> label 0 (:806-818)
+    p2 = str(tmp_path / "e.lance")
+    hip.LanceFreeDetached(hip.LanceCreateDetached(p2, 2, "l2", "vectors"))
+    h = hip.LanceOpenDetached(p2, "vectors", "l2")
+    assert hip.LanceDetachedAdd(h, np.array([1, 2], np.float32), 2) == 0
+    hip.LanceFreeDetached(h)
+    # two tables in one dataset stay independent (:843-867)
+    p3 = str(tmp_path / "tbl.lance")
+    a = hip.LanceCreateDetached(p3, 2, "l2", "idx_a")
+    b = hip.LanceCreateDetached(p3, 2, "l2", "idx_b")
+    hip.LanceDetachedAdd(a, np.array([1, 0], np.float32), 2)
+    hip.LanceDetachedAdd(a, np.array([2, 0], np.float32), 2)
+    hip.LanceDetachedAdd(b, np.array([10, 0], np.float32), 2)
+    assert hip.LanceDetachedCount(a) == 2 and hip.LanceDetachedCount(b) == 1
+    hip.LanceFreeDetached(a)
+    hip.LanceFreeDetached(b)
+    a = hip.LanceOpenDetached(p3, "idx_a", "l2")
+    b = hip.LanceOpenDetached(p3, "idx_b", "l2")
+    assert hip.LanceDetachedCount(a) == 2 and hip.LanceDetachedCount(b) == 1
+    hip.LanceFreeDetached(a)
+    hip.LanceFreeDetached(b)
+
+
+def test_reopen_reuses_max_label_like_reference(hip, tmp_path):
+    # lance_manager.rs:157-158 next_label = MAX(live label)+1: deleting the max
+    # label then reopening re-issues it; the store must stay consistent.
+    p = str(tmp_path)
+    h = hip.LanceCreateDetached(p, 2, "l2", "vectors")
+    hip.LanceDetachedAddBatch(h, np.array([[0, 0], [1, 0], [2, 0]], np.float32), 3, 2)
+    hip.LanceDetachedDelete(h, 2)
+    hip.LanceFreeDetached(h)
+    h = hip.LanceOpenDetached(p, "vectors", "l2")
+    assert hip.LanceDetachedAdd(h, np.array([5, 0], np.float32), 2) == 2
+    l, d = hip.LanceDetachedSearch(h, np.array([5, 0], np.float32), 2, 3)
+    assert list(l) == [2, 1, 0] and d[0] == 0.0
+    hip.LanceFreeDetached(h)
+    h = hip.LanceOpenDetached(p, "vectors", "l2")
+    l, d = hip.LanceDetachedSearch(h, np.array([5, 0], np.float32), 2, 3)
+    assert list(l) == [2, 1, 0]
+    np.testing.assert_array_equal(hip.LanceDetachedGetVector(h, 2, 2), [5, 0])
+    hip.LanceFreeDetached(h)
+
+
+# ---------------------------------------------------------------------------
+# C-ABI behaviour
+# ---------------------------------------------------------------------------
+def test_dimension_mismatch_is_error_at_ffi_and_empty_at_index(hip, mk):
+    h = mk(3)
+    hip.LanceDetachedAddBatch(h, np.eye(3, dtype=np.float32), 3, 3)
+    with pytest.raises(hip.IOException, match="expected query dimension 3, got 2"):
+        hip.LanceDetachedSearch(h, np.zeros(2, np.float32), 2, 1)
+
+
+def test_k_and_empty_edge_cases(hip, mk):
+    h = mk(4)
+    l, d = hip.LanceDetachedSearch(h, np.zeros(4, np.float32), 4, 5)   # empty table
+    assert l.size == 0
+    hip.LanceDetachedAddBatch(h, np.eye(4, dtype=np.float32), 4, 4)
+    l, d = hip.LanceDetachedSearch(h, np.zeros(4, np.float32), 4, 0)
+    assert l.size == 0
+    l, d = hip.LanceDetachedSearch(h, np.array([1, 0, 0, 0], np.float32), 4, 10)  # k > n
+    assert list(l) == [0, 1, 2, 3]
+    np.testing.assert_allclose(d, [0, 2, 2, 2])
+    hip.LanceDetachedDeleteBatch(h, [0, 1, 2, 3])
+    assert hip.LanceDetachedCount(h) == 0
+    l, d = hip.LanceDetachedSearch(h, np.array([1, 0, 0, 0], np.float32), 4, 10)
+    assert l.size == 0
+
+
+def test_get_vector_and_all_vectors(hip, mk):
+    h = mk(5)
+    X = np.random.default_rng(3).standard_normal((10, 5)).astype(np.float32)
+    hip.LanceDetachedAddBatch(h, X, 10, 5)
+    hip.LanceDetachedDeleteBatch(h, [3, 7])
+    np.testing.assert_array_equal(hip.LanceDetachedGetVector(h, 4, 5), X[4])
+    with pytest.raises(hip.IOException, match="not found"):
+        hip.LanceDetachedGetVector(h, 3, 5)
+    with pytest.raises(hip.IOException, match="too small"):
+        hip.LanceDetachedGetVector(h, 4, 2)
+    labs, vecs = hip.LanceDetachedGetAllVectors(h)
+    keep = [i for i in range(10) if i not in (3, 7)]
+    assert list(labs) == keep
+    np.testing.assert_array_equal(vecs, X[keep])
+
+
+def test_merge_assigns_fresh_labels(hip, mk, tmp_path):
+    a = mk(3, path=tmp_path / "a")
+    b = mk(3, path=tmp_path / "b")
+    hip.LanceDetachedAddBatch(a, np.eye(3, dtype=np.float32), 3, 3)
+    hip.LanceDetachedAddBatch(b, 2 * np.eye(3, dtype=np.float32), 3, 3)
+    old, new = hip.LanceDetachedMerge(a, b, [0, 2])
+    assert list(old) == [0, 2] and list(new) == [3, 4]
+    np.testing.assert_array_equal(hip.LanceDetachedGetVector(a, 4, 3), [0, 0, 2])
+
+
+def test_compact_keeps_labels(hip, mk):
+    h = mk(8)
+    X = np.random.default_rng(5).standard_normal((300, 8)).astype(np.float32)
+    hip.LanceDetachedAddBatch(h, X, 300, 8)
+    dead = list(range(0, 300, 3))
+    hip.LanceDetachedDeleteBatch(h, dead)
+    Q = np.random.default_rng(6).standard_normal((4, 8)).astype(np.float32)
+    before = hip.LanceDetachedSearchBatch(h, Q, 7)
+    hip.LanceDetachedCompact(h)
+    after = hip.LanceDetachedSearchBatch(h, Q, 7)
+    for x, y in zip(before, after):
+        np.testing.assert_array_equal(x, y)
+    live = np.ones(300, bool)
+    live[dead] = False
+    el, ed, ec = flat_knn.flat_search_batch(X, np.arange(300), live, Q, 7)
+    assert_same(*after, el, ed, ec)
+
+
+# ---------------------------------------------------------------------------
+# numerics vs the oracle
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("metric", ["l2", "dot", "cosine"])
+def test_small_fixture(hip, mk, metric):
+    z = np.load("tests/golden/knn_small.npz")
+    X, Q, live = z["X"], z["Q"], z["live"]
+    h = mk(16, metric)
+    hip.LanceDetachedAddBatch(h, X, len(X), 16)
+    hip.LanceDetachedDeleteBatch(h, np.nonzero(~live)[0])
+    gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 5)
+    assert_same(gl, gd, gc, z[f"{metric}_labels"], z[f"{metric}_dists"])
+    # single-query entry point returns the same
+    for i in range(len(Q)):
+        l, d = hip.LanceDetachedSearch(h, Q[i], 16, 5)
+        np.testing.assert_array_equal(l, gl[i])
+
+
+def test_ties_by_label(hip, mk):
+    z = np.load("tests/golden/knn_ties.npz")
+    h = mk(4)
+    hip.LanceDetachedAddBatch(h, z["X"], 40, 4)
+    gl, gd, gc = hip.LanceDetachedSearchBatch(h, z["Q"], 12)
+    assert_same(gl, gd, gc, z["labels"], z["dists"], z["counts"])
+
+
+@pytest.mark.parametrize("spec", load_seeded(), ids=lambda s: s["name"])
+def test_seeded_fixtures(hip, mk, spec):
+    X, Q, exp = seeded_inputs(spec)
+    h = mk(spec["d"], spec["metric"])
+    for s in range(0, len(X), 2048):   # DuckDB sink chunks (lance_index.cpp:940-946)
+        hip.LanceDetachedAddBatch(h, X[s:s + 2048], len(X[s:s + 2048]), spec["d"])
+    gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, spec["k"])
+    assert_same(gl, gd, gc, exp["labels"], exp["dists"], exp["counts"])
+    st = hip.LanceHipLastSearchStats(h)
+    assert st["fallback_queries"] == 0, st      # certificate holds on continuous data
+
+
+@pytest.mark.parametrize("dim", [1, 3, 17, 100, 129, 1000])
+def test_odd_dimensions(hip, mk, dim):
+    rng = np.random.default_rng(dim)
+    X = rng.standard_normal((3000, dim)).astype(np.float32)
+    Q = rng.standard_normal((9, dim)).astype(np.float32)
+    h = mk(dim)
+    hip.LanceDetachedAddBatch(h, X, len(X), dim)
+    gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 10)
+    el, ed, ec = flat_knn.flat_search_batch(X, np.arange(len(X)), np.ones(len(X), bool), Q, 10)
+    assert_same(gl, gd, gc, el, ed, ec)
+
+
+def test_sampled_path_with_deletes_and_many_queries(hip, mk):
+    # > 65536 rows takes the sample + threshold-scan path; 600 queries = 3 query tiles
+    rng = np.random.default_rng(99)
+    n, d = 150_000, 96
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Q = rng.standard_normal((600, d)).astype(np.float32)
+    h = mk(d)
+    hip.LanceDetachedAddBatch(h, X, n, d)
+    dead = rng.choice(n, 20_000, replace=False)
+    hip.LanceDetachedDeleteBatch(h, dead)
+    live = np.ones(n, bool)
+    live[dead] = False
+    gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 10)
+    st = hip.LanceHipLastSearchStats(h)
+    assert not st["dense_path"]
+    el, ed, ec = c_oracle.flat_search_batch(X, Q, 10, "l2", live=live, acc64=True, nthreads=16)
+    assert_same(gl, gd, gc, el, ed, ec)
+
+
+def test_duplicates_force_exact_fallback(hip, mk):
+    # 100k identical rows: every lower bound ties, the certificate cannot hold,
+    # the exact fallback must return the k smallest labels
+    n, d = 100_000, 32
+    X = np.ones((n, d), np.float32)
+    h = mk(d)
+    hip.LanceDetachedAddBatch(h, X, n, d)
+    hip.LanceDetachedDeleteBatch(h, [0, 5])
+    gl, gd, gc = hip.LanceDetachedSearchBatch(h, np.ones((2, d), np.float32), 10)
+    assert list(gl[0]) == [1, 2, 3, 4, 6, 7, 8, 9, 10, 11]
+    assert np.all(gd == 0)
+    assert hip.LanceHipLastSearchStats(h)["fallback_queries"] == 2
+
+
+def test_metric_quirk_ranks_by_l2(hip, mk):
+    rng = np.random.default_rng(1)
+    X = rng.standard_normal((500, 8)).astype(np.float32)
+    Q = rng.standard_normal((3, 8)).astype(np.float32)
+    h = mk(8, "dot")
+    hip.LanceDetachedAddBatch(h, X, 500, 8)
+    gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 5)
+    el, ed, _ = flat_knn.flat_search_batch(X, np.arange(500), np.ones(500, bool), Q, 5, "dot")
+    assert_same(gl, gd, gc, el, ed)
+    hip.LanceHipSetOption(h, "metric_quirk", "1")
+    gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 5)
+    el, ed, _ = flat_knn.flat_search_batch(X, np.arange(500), np.ones(500, bool), Q, 5, "l2")
+    assert_same(gl, gd, gc, el, ed)
+
+
+def test_merge_topk_kernel(hip):
+    rng = np.random.default_rng(4)
+    nshard, nq, k = 4, 5, 7
+    pl = np.full((nshard, nq, k), -1, np.int64)
+    pd = np.full((nshard, nq, k), np.nan, np.float32)
+    pc = rng.integers(0, k + 1, (nshard, nq)).astype(np.int32)
+    for s in range(nshard):
+        for q in range(nq):
+            c = pc[s, q]
+            d = np.sort(rng.integers(0, 20, c).astype(np.float32))
+            pd[s, q, :c] = d
+            pl[s, q, :c] = s * 1000 + np.arange(c)
+    ol, od, oc = hip.LanceHipMergeTopk(pl, pd, pc)
+    for q in range(nq):
+        items = [(pd[s, q, i], pl[s, q, i]) for s in range(nshard) for i in range(pc[s, q])]
+        items.sort()
+        items = items[:k]
+        assert oc[q] == len(items)
+        assert list(ol[q, :oc[q]]) == [l for _, l in items]
