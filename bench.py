@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""Headline benchmark: BASELINE.json metric "kNN queries/sec + recall@10,
+1M x 768 f32 flat; GB/s vs HBM roofline" on configs[1] (C2): flat squared-L2,
+N = 1,000,000 x d = 768 f32 base, k = 10, query batch B = 256.
+
+One step = one batch of 256 queries searched through the C-ABI
+(lance_hip_search_batch_device) against the whole base, inputs resident in HBM.
+With --gpus N (one process per GPU, launched by torch.distributed.run) the base
+is row-sharded over the ranks (fixed N: strong scaling); every rank searches
+its shard for the same batch, the per-shard top-k lists are all-gathered over
+RCCL and merged on the device (lance_hip_merge_topk_device).
+
+Prints ONE JSON line on rank 0 (driver contract).  The CPU baseline (rank 0,
+N = 1 only) times oracle/flat_knn.c — the port of the reference's flat search
+(rust_lib/src/lance_manager.rs:393-451 -> lance flat KNN) — on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "duckdb-lancedb_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import lance_hip  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+GEN_CHUNK = 65536
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--metric", default="l2")
+    ap.add_argument("--recall-queries", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-recall", action="store_true")
+    return ap.parse_args()
+
+
+def gen_rows(start, stop, dim, device, seed=1234):
+    """Rows [start, stop) of the synthetic N(0,1) base, identical whatever the
+    sharding: chunk c of GEN_CHUNK rows comes from generator seed (seed, c)."""
+    out = torch.empty((stop - start, dim), dtype=torch.float32, device=device)
+    c0, c1 = start // GEN_CHUNK, (stop - 1) // GEN_CHUNK
+    g = torch.Generator(device=device)
+    for c in range(c0, c1 + 1):
+        g.manual_seed(seed * 1_000_003 + c)
+        chunk = torch.randn((GEN_CHUNK, dim), generator=g, device=device, dtype=torch.float32)
+        lo, hi = max(start, c * GEN_CHUNK), min(stop, (c + 1) * GEN_CHUNK)
+        out[lo - start:hi - start] = chunk[lo - c * GEN_CHUNK:hi - c * GEN_CHUNK]
+    return out
+
+
+def err_buf():
+    return ctypes.create_string_buffer(2048)
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+    L = lance_hip.lib()
+
+    N, D, K, B = a.n, a.dim, a.k, a.batch
+    s0, s1 = rank * N // world, (rank + 1) * N // world
+    n_local = s1 - s0
+
+    # ---- build the shard (device-resident base) --------------------------
+    e = err_buf()
+    h = L.lance_create_detached(b"", D, a.metric.encode(), b"bench", e, 2048)
+    if not h:
+        raise RuntimeError(e.value.decode())
+    lance_hip.LanceHipSetOption(h, "reserve_rows", str(n_local))
+    for lo in range(s0, s1, 1 << 18):
+        hi = min(s1, lo + (1 << 18))
+        X = gen_rows(lo, hi, D, dev)
+        torch.cuda.synchronize()
+        r = L.lance_hip_add_batch_device(h, X.data_ptr(), hi - lo, D, e, 2048)
+        if r < 0:
+            raise RuntimeError(e.value.decode())
+        del X
+    g = torch.Generator(device=dev)
+    g.manual_seed(5678)
+    Q = torch.randn((B, D), generator=g, device=dev, dtype=torch.float32)
+    out_l = torch.empty((B, K), dtype=torch.int64, device=dev)
+    out_d = torch.empty((B, K), dtype=torch.float32, device=dev)
+    out_c = torch.empty((B,), dtype=torch.int32, device=dev)
+    if world > 1:
+        gl = torch.empty((world, B, K), dtype=torch.int64, device=dev)
+        gd = torch.empty((world, B, K), dtype=torch.float32, device=dev)
+        gc = torch.empty((world, B), dtype=torch.int32, device=dev)
+        ml = torch.empty((B, K), dtype=torch.int64, device=dev)
+        md = torch.empty((B, K), dtype=torch.float32, device=dev)
+        mc = torch.empty((B,), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    def step():
+        r = L.lance_hip_search_batch_device(h, Q.data_ptr(), B, D, K, 20, 1, out_l.data_ptr(), out_d.data_ptr(),
+                                            out_c.data_ptr(), e, 2048)
+        if r < 0:
+            raise RuntimeError(e.value.decode())
+        if world == 1:
+            return out_l, out_d, out_c
+        out_l.add_(s0)  # shard-local label -> global label (labels are dense, row-range shards)
+        dist.all_gather_into_tensor(gl, out_l)
+        dist.all_gather_into_tensor(gd, out_d)
+        dist.all_gather_into_tensor(gc, out_c)
+        r = L.lance_hip_merge_topk_device(world, B, K, gl.data_ptr(), gd.data_ptr(), gc.data_ptr(), ml.data_ptr(),
+                                          md.data_ptr(), mc.data_ptr(), e, 2048)
+        if r < 0:
+            raise RuntimeError(e.value.decode())
+        return ml, md, mc
+
+    for _ in range(a.warmup):
+        step()
+    lance_hip.LanceHipSetOption(h, "time_kernels", "1")
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    t = float(elapsed.item())
+    kt = lance_hip.LanceHipKernelTimes(h)
+    st = lance_hip.LanceHipLastSearchStats(h)
+    lance_hip.LanceHipSetOption(h, "time_kernels", "0")
+    res_l = res[0].cpu().numpy()
+    res_d = res[1].cpu().numpy()
+
+    # ---- recall@10 vs exact (CPU oracle, float64) on a query subset ----------
+    recall = None
+    cpu = None
+    if rank == 0 and not a.no_recall:
+        sys.path.insert(0, ROOT)
+        from oracle import c_oracle, flat_knn
+
+        Xh = np.empty((N, D), np.float32)
+        for lo in range(0, N, 1 << 18):
+            hi = min(N, lo + (1 << 18))
+            Xh[lo:hi] = gen_rows(lo, hi, D, dev).cpu().numpy()
+        Qh = Q.cpu().numpy()
+        nr = min(a.recall_queries, B)
+        nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        el, ed, _ = c_oracle.flat_search_batch(Xh, Qh[:nr], K, a.metric, acc64=True, nthreads=nthreads)
+        recall = flat_knn.recall_at_k(res_l[:nr], el, min(10, K))
+        exact_ids = bool((res_l[:nr] == el).all())
+        max_rel = float(np.max(np.abs(res_d[:nr] - ed) / np.maximum(np.abs(ed), 1e-30)))
+        if world == 1 and not a.no_cpu_baseline:
+            # bounded sample: one query per call (the reference API, lance_search.cpp:73-74)
+            done, t_cpu0 = 0, time.perf_counter()
+            while True:
+                c_oracle.flat_search_batch(Xh, Qh[done % B:done % B + 1], K, a.metric, acc64=False,
+                                           nthreads=nthreads)
+                done += 1
+                if time.perf_counter() - t_cpu0 >= a.cpu_seconds and done >= 2:
+                    break
+            t_cpu = time.perf_counter() - t_cpu0
+            cpu = {"value": done / t_cpu, "unit": "queries/s", "cores": nthreads, "kind": "port",
+                   "sample": f"{done} queries, one per call, each an exact f32 scan of all {N}x{D} rows "
+                             f"({t_cpu:.1f} s, oracle/flat_knn.c, {nthreads} OpenMP threads)"}
+        del Xh
+
+    if rank == 0:
+        ms_step = 1000.0 * t / a.steps
+        value = B * a.steps / t
+        roof = None
+        if kt["scan_launches"] > 0:
+            ld = ((D + 63) // 64) * 64
+            avg_ms = kt["scan_ms_total"] / kt["scan_launches"]
+            bytes_launch = kt["scan_rows"] * (ld * 4 + 16) + kt["scan_qpad"] * ld * 2
+            ach = bytes_launch / (avg_ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "scan_kernel<L2,append>",
+                    "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(bytes_launch)}
+        line = {
+            "metric": "kNN queries/sec + recall@10, 1Mx768 f32 flat; GB/s vs HBM roofline",
+            "value": round(value, 1),
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic N(0,1) base (seeded torch Philox), independent N(0,1) queries",
+            "config": {"workload": f"C2 flat {a.metric} {N}x{D} f32 k={K} query-batch={B}", "n": N, "dim": D,
+                       "k": K, "global_batch": B, "metric": a.metric, "parallelism": f"rowshard{world}"},
+            "recall_at_10": recall,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "search_stats": st,
+        }
+        if recall is not None:
+            line["exact_ids_on_recall_subset"] = exact_ids
+            line["max_rel_dist_err"] = max_rel
+        print(json.dumps(line), flush=True)
+    L.lance_free_detached(h)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -207,10 +207,15 @@ void launch_prep_queries(const float *Q, int nq, int dim, int ld, int nq_pad, in
 // Global loads of step k+1 are issued before the MFMAs of step k.
 // ---------------------------------------------------------------------------
 constexpr int BR = SCAN_BR, BQ = SCAN_BQ, BK = SCAN_BK;
-constexpr int XS_BYTES = BR * BK * 2;  // 16 KiB
-constexpr int QS_BYTES = BQ * BK * 2;  // 32 KiB
-constexpr int SCAN_LDS = XS_BYTES + QS_BYTES + BR * 16;
+constexpr int XS_BYTES = BR * BK * 2;  // 16 KiB bf16 base tile
+constexpr int QS_BYTES = BQ * BK * 2;  // 32 KiB bf16 query tile
+constexpr int RA_BYTES = BR * 16;      // row aux of the tile
+constexpr int EP_BYTES = BQ * 8;       // epilogue per-query counters + pool bases
+constexpr int SCAN_LDS = XS_BYTES + QS_BYTES + RA_BYTES + EP_BYTES;
 
+// byte offset of 16 B chunk `chunk` (0..7) of row `row` in a [rows][64] bf16
+// LDS image: chunk index XOR-ed with (row>>1)&7 so that the ds_read_b128
+// fragment loads of 32 consecutive rows hit distinct bank groups
 __device__ __forceinline__ int swz(int row, int chunk) {
 	return row * (BK * 2) + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
@@ -225,17 +230,40 @@ __device__ __forceinline__ float lower_bound(float s, float4 ra, float4 qa) {
 	return v + qa.w;
 }
 
+__device__ __forceinline__ uint2 cvt4(float4 v, bool ok) {
+	uint2 r = make_uint2(pk_bf16(v.x, v.y), pk_bf16(v.z, v.w));
+	return ok ? r : make_uint2(0u, 0u);
+}
+
+// ---------------------------------------------------------------------------
+// scan kernel
+//
+// Workgroup = 512 threads = 8 waves, 2 (base rows) x 4 (queries); each wave owns
+// a 64-row x 64-query sub-tile = 2x2 v_mfma_f32_32x32x16_bf16 tiles (A = base
+// rows, B = queries: accumulator column = lane&31 = query, the 16 registers
+// walk base rows).  Per 64-deep k-step the workgroup pulls a 128 x 64 f32 base
+// tile from HBM (16 B per lane, 256 contiguous bytes per row), converts it to
+// bf16 in registers (v_cvt_pk_bf16_f32) and a 256 x 64 bf16 query tile from L2,
+// into XOR-swizzled LDS.  Loads of step k+1 are in flight during the MFMAs of
+// step k; <=128 VGPRs keeps two workgroups (16 waves) per CU so one
+// workgroup's MFMAs cover the other's load latency.
+// Epilogue: each accumulator becomes a rigorous lower bound of the exact
+// distance; dense mode stores it, append mode keeps (LB, slot) if LB <= tau[q]
+// with one global pool reservation per (tile, query) instead of per candidate.
+// ---------------------------------------------------------------------------
 template <int METRIC, int MODE>
-__global__ __launch_bounds__(512) void scan_kernel(const float *__restrict__ X, const float4 *__restrict__ rowaux,
-                                                   int64_t n_slots, int ld, const uint16_t *__restrict__ Qb,
-                                                   const float4 *__restrict__ qaux, int nq, int64_t tile_stride,
-                                                   float *__restrict__ dense, int64_t ld_out,
-                                                   const float *__restrict__ tau, uint2 *__restrict__ pool,
-                                                   int *__restrict__ pool_cnt, int cap) {
+__global__ __launch_bounds__(512, 2) void scan_kernel(const float *__restrict__ X, const float4 *__restrict__ rowaux,
+                                                      int64_t n_slots, int ld, const uint16_t *__restrict__ Qb,
+                                                      const float4 *__restrict__ qaux, int nq, int64_t tile_stride,
+                                                      float *__restrict__ dense, int64_t ld_out,
+                                                      const float *__restrict__ tau, uint2 *__restrict__ pool,
+                                                      int *__restrict__ pool_cnt, int cap) {
 	__shared__ __attribute__((aligned(16))) uint8_t smem[SCAN_LDS];
 	uint8_t *Xs = smem;
 	uint8_t *Qs = smem + XS_BYTES;
 	float4 *RA = reinterpret_cast<float4 *>(smem + XS_BYTES + QS_BYTES);
+	unsigned *ep_cnt = reinterpret_cast<unsigned *>(smem + XS_BYTES + QS_BYTES + RA_BYTES);
+	unsigned *ep_base = ep_cnt + BQ;
 
 	const int tid = threadIdx.x;
 	const int lane = tid & 63;
@@ -249,110 +277,197 @@ __global__ __launch_bounds__(512) void scan_kernel(const float *__restrict__ X, 
 		int64_t r = row0 + tid;
 		RA[tid] = (r < n_slots) ? rowaux[r] : make_float4(F_INF, 0.f, 0.f, 0.f);
 	}
+	if (MODE == 1 && tid < BQ) ep_cnt[tid] = 0u;
 
-	// staging assignment: X chunks c = tid, tid+512 (row = c>>3, 16 B bf16 chunk = c&7)
-	const int xr0 = tid >> 3, xc = tid & 7;
-	const int xr1 = xr0 + 64;
-	const bool xv0 = row0 + xr0 < n_slots, xv1 = row0 + xr1 < n_slots;
-	const float *xp0 = X + (xv0 ? (row0 + xr0) * (int64_t)ld : 0) + xc * 8;
-	const float *xp1 = X + (xv1 ? (row0 + xr1) * (int64_t)ld : 0) + xc * 8;
-	// Q chunks c = tid + 512*i, i < 4: row = c>>3 (= (tid>>3) + 64 i), chunk = tid&7
-	const uint16_t *qp = Qb + (int64_t)(q0 + (tid >> 3)) * ld + xc * 8;
-	const int64_t qstep = (int64_t)64 * ld;
+	// X staging: float4 f = tid + 512 i (i < 4) of the 128 x 16 float4 tile:
+	// row = (tid >> 4) + 32 i, float4 column c4 = tid & 15
+	const int xr = tid >> 4, xc4 = tid & 15;
+	uint32_t xmask = 0;
+#pragma unroll
+	for (int i = 0; i < 4; ++i) xmask |= (row0 + xr + 32 * i < n_slots) ? (1u << i) : 0u;
+	// rows past the end are clamped to the last slot (valid memory) and zeroed
+	const int64_t last = n_slots - 1;
+	const float *xq0 = X + min(row0 + xr, last) * ld + xc4 * 4;
+	const float *xq1 = X + min(row0 + xr + 32, last) * ld + xc4 * 4;
+	const float *xq2 = X + min(row0 + xr + 64, last) * ld + xc4 * 4;
+	const float *xq3 = X + min(row0 + xr + 96, last) * ld + xc4 * 4;
+	// Q staging: 16 B chunk f = tid + 512 i: row = (tid >> 3) + 64 i, chunk = tid & 7
+	const int qr = tid >> 3, qc = tid & 7;
+	const uint16_t *qp = Qb + (int64_t)(q0 + qr) * ld + qc * 8;
+	const int64_t qstride = (int64_t)64 * ld;
 
-	float4 xa0, xa1, xb0, xb1;
-	uint4 qv[4];
-	auto gload = [&](int kt) {
-		const int ko = kt * BK;
-		if (xv0) {
-			xa0 = *reinterpret_cast<const float4 *>(xp0 + ko);
-			xa1 = *reinterpret_cast<const float4 *>(xp0 + ko + 4);
-		} else {
-			xa0 = xa1 = make_float4(0.f, 0.f, 0.f, 0.f);
-		}
-		if (xv1) {
-			xb0 = *reinterpret_cast<const float4 *>(xp1 + ko);
-			xb1 = *reinterpret_cast<const float4 *>(xp1 + ko + 4);
-		} else {
-			xb0 = xb1 = make_float4(0.f, 0.f, 0.f, 0.f);
-		}
-#pragma unroll
-		for (int i = 0; i < 4; ++i) qv[i] = *reinterpret_cast<const uint4 *>(qp + i * qstep + ko);
-	};
-	auto swrite = [&]() {
-		uint4 p0 = make_uint4(pk_bf16(xa0.x, xa0.y), pk_bf16(xa0.z, xa0.w), pk_bf16(xa1.x, xa1.y),
-		                      pk_bf16(xa1.z, xa1.w));
-		uint4 p1 = make_uint4(pk_bf16(xb0.x, xb0.y), pk_bf16(xb0.z, xb0.w), pk_bf16(xb1.x, xb1.y),
-		                      pk_bf16(xb1.z, xb1.w));
-		*reinterpret_cast<uint4 *>(Xs + swz(xr0, xc)) = p0;
-		*reinterpret_cast<uint4 *>(Xs + swz(xr1, xc)) = p1;
-#pragma unroll
-		for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4 *>(Qs + swz(xr0 + 64 * i, xc)) = qv[i];
-	};
+	// LDS destinations of this thread's staged data
+	const int xdst0 = swz(xr, xc4 >> 1) + (xc4 & 1) * 8;
+	const int qdst0 = swz(qr, qc);
 
-	f32x16 acc[2][2];
+	f32x16 acc00, acc01, acc10, acc11;
 #pragma unroll
-	for (int a = 0; a < 2; ++a)
-#pragma unroll
-		for (int b = 0; b < 2; ++b)
-#pragma unroll
-			for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+	for (int r = 0; r < 16; ++r) {
+		acc00[r] = 0.f;
+		acc01[r] = 0.f;
+		acc10[r] = 0.f;
+		acc11[r] = 0.f;
+	}
 
+	float4 x0, x1, x2, x3;
+	uint4 y0, y1, y2, y3;
 	const int KT = ld / BK;
-	gload(0);
+	x0 = *reinterpret_cast<const float4 *>(xq0);
+	x1 = *reinterpret_cast<const float4 *>(xq1);
+	x2 = *reinterpret_cast<const float4 *>(xq2);
+	x3 = *reinterpret_cast<const float4 *>(xq3);
+	y0 = *reinterpret_cast<const uint4 *>(qp);
+	y1 = *reinterpret_cast<const uint4 *>(qp + qstride);
+	y2 = *reinterpret_cast<const uint4 *>(qp + 2 * qstride);
+	y3 = *reinterpret_cast<const uint4 *>(qp + 3 * qstride);
 	for (int kt = 0; kt < KT; ++kt) {
-		swrite();
+		// stage the landed step into LDS
+		*reinterpret_cast<uint2 *>(Xs + xdst0) = cvt4(x0, xmask & 1u);
+		*reinterpret_cast<uint2 *>(Xs + xdst0 + 32 * 128) = cvt4(x1, xmask & 2u);
+		*reinterpret_cast<uint2 *>(Xs + xdst0 + 64 * 128) = cvt4(x2, xmask & 4u);
+		*reinterpret_cast<uint2 *>(Xs + xdst0 + 96 * 128) = cvt4(x3, xmask & 8u);
+		*reinterpret_cast<uint4 *>(Qs + qdst0) = y0;
+		*reinterpret_cast<uint4 *>(Qs + qdst0 + 64 * 128) = y1;
+		*reinterpret_cast<uint4 *>(Qs + qdst0 + 128 * 128) = y2;
+		*reinterpret_cast<uint4 *>(Qs + qdst0 + 192 * 128) = y3;
 		__syncthreads();
-		if (kt + 1 < KT) gload(kt + 1);
+		// issue the next step's loads before this step's MFMAs
+		if (kt + 1 < KT) {
+			const int ko = (kt + 1) * BK;
+			x0 = *reinterpret_cast<const float4 *>(xq0 + ko);
+			x1 = *reinterpret_cast<const float4 *>(xq1 + ko);
+			x2 = *reinterpret_cast<const float4 *>(xq2 + ko);
+			x3 = *reinterpret_cast<const float4 *>(xq3 + ko);
+			y0 = *reinterpret_cast<const uint4 *>(qp + ko);
+			y1 = *reinterpret_cast<const uint4 *>(qp + qstride + ko);
+			y2 = *reinterpret_cast<const uint4 *>(qp + 2 * qstride + ko);
+			y3 = *reinterpret_cast<const uint4 *>(qp + 3 * qstride + ko);
+		}
 #pragma unroll
 		for (int ks = 0; ks < BK / 16; ++ks) {
 			const int kc = ks * 2 + hi;
-			bf16x8 af[2], bfr[2];
-#pragma unroll
-			for (int tr = 0; tr < 2; ++tr)
-				af[tr] = *reinterpret_cast<const bf16x8 *>(Xs + swz(wr * 64 + tr * 32 + li, kc));
-#pragma unroll
-			for (int tq = 0; tq < 2; ++tq)
-				bfr[tq] = *reinterpret_cast<const bf16x8 *>(Qs + swz(wq * 64 + tq * 32 + li, kc));
-#pragma unroll
-			for (int tr = 0; tr < 2; ++tr)
-#pragma unroll
-				for (int tq = 0; tq < 2; ++tq)
-					acc[tr][tq] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tr], bfr[tq], acc[tr][tq], 0, 0, 0);
+			const bf16x8 a0 = *reinterpret_cast<const bf16x8 *>(Xs + swz(wr * 64 + li, kc));
+			const bf16x8 a1 = *reinterpret_cast<const bf16x8 *>(Xs + swz(wr * 64 + 32 + li, kc));
+			const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(Qs + swz(wq * 64 + li, kc));
+			const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(Qs + swz(wq * 64 + 32 + li, kc));
+			acc00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc00, 0, 0, 0);
+			acc01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc01, 0, 0, 0);
+			acc10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc10, 0, 0, 0);
+			acc11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc11, 0, 0, 0);
 		}
 		__syncthreads();
 	}
 
-	// epilogue: lane holds query q = q0 + wq*64 + tq*32 + li and, in register
-	// reg, base row wr*64 + tr*32 + (reg&3) + 8*(reg>>2) + 4*hi.
+	// ---- epilogue -------------------------------------------------------------
+	// lane: query q = q0 + wq*64 + tq*32 + li; register reg of acc<tr><tq> holds
+	// base row wr*64 + tr*32 + (reg&3) + 8*(reg>>2) + 4*hi.
+	const int ql0 = wq * 64 + li, ql1 = ql0 + 32;  // tile-local queries
+	const bool qv0 = q0 + ql0 < nq, qv1 = q0 + ql1 < nq;
+	const float4 qa0 = qaux[q0 + ql0];
+	const float4 qa1 = qaux[q0 + ql1];
+	const int rb = wr * 64 + 4 * hi;  // + tr*32 + 8g + j
+
+	if (MODE == 0) {
 #pragma unroll
-	for (int tq = 0; tq < 2; ++tq) {
-		const int q = q0 + wq * 64 + tq * 32 + li;
-		if (q >= nq) continue;
-		const float4 qa = qaux[q];
-		float t = 0.f;
-		if (MODE == 1) t = tau[q];
+		for (int g = 0; g < 4; ++g) {
+			const int r0 = rb + 8 * g, r1 = rb + 32 + 8 * g;
+			float4 o;
+			if (qv0) {
+				float *dst = dense + (int64_t)(q0 + ql0) * ld_out + (int64_t)blockIdx.x * BR;
+				o = make_float4(lower_bound<METRIC>(acc00[4 * g + 0], RA[r0 + 0], qa0),
+				                lower_bound<METRIC>(acc00[4 * g + 1], RA[r0 + 1], qa0),
+				                lower_bound<METRIC>(acc00[4 * g + 2], RA[r0 + 2], qa0),
+				                lower_bound<METRIC>(acc00[4 * g + 3], RA[r0 + 3], qa0));
+				*reinterpret_cast<float4 *>(dst + r0) = o;
+				o = make_float4(lower_bound<METRIC>(acc10[4 * g + 0], RA[r1 + 0], qa0),
+				                lower_bound<METRIC>(acc10[4 * g + 1], RA[r1 + 1], qa0),
+				                lower_bound<METRIC>(acc10[4 * g + 2], RA[r1 + 2], qa0),
+				                lower_bound<METRIC>(acc10[4 * g + 3], RA[r1 + 3], qa0));
+				*reinterpret_cast<float4 *>(dst + r1) = o;
+			}
+			if (qv1) {
+				float *dst = dense + (int64_t)(q0 + ql1) * ld_out + (int64_t)blockIdx.x * BR;
+				o = make_float4(lower_bound<METRIC>(acc01[4 * g + 0], RA[r0 + 0], qa1),
+				                lower_bound<METRIC>(acc01[4 * g + 1], RA[r0 + 1], qa1),
+				                lower_bound<METRIC>(acc01[4 * g + 2], RA[r0 + 2], qa1),
+				                lower_bound<METRIC>(acc01[4 * g + 3], RA[r0 + 3], qa1));
+				*reinterpret_cast<float4 *>(dst + r0) = o;
+				o = make_float4(lower_bound<METRIC>(acc11[4 * g + 0], RA[r1 + 0], qa1),
+				                lower_bound<METRIC>(acc11[4 * g + 1], RA[r1 + 1], qa1),
+				                lower_bound<METRIC>(acc11[4 * g + 2], RA[r1 + 2], qa1),
+				                lower_bound<METRIC>(acc11[4 * g + 3], RA[r1 + 3], qa1));
+				*reinterpret_cast<float4 *>(dst + r1) = o;
+			}
+		}
+		return;
+	}
+
+	// append mode, pass A: count survivors per (lane, query) and reserve a
+	// contiguous local range in the tile's per-query LDS counter
+	const float t0 = qv0 ? tau[q0 + ql0] : -F_INF;
+	const float t1 = qv1 ? tau[q0 + ql1] : -F_INF;
+	uint32_t m00 = 0, m01 = 0, m10 = 0, m11 = 0;  // survivor bitmasks per accumulator
 #pragma unroll
-		for (int tr = 0; tr < 2; ++tr) {
+	for (int r = 0; r < 16; ++r) {
+		const int rl0 = rb + (r & 3) + 8 * (r >> 2), rl1 = rl0 + 32;
+		const float4 ra0 = RA[rl0], ra1 = RA[rl1];
+		float l;
+		l = lower_bound<METRIC>(acc00[r], ra0, qa0);
+		m00 |= (l <= t0 && l < F_INF) ? (1u << r) : 0u;
+		l = lower_bound<METRIC>(acc10[r], ra1, qa0);
+		m10 |= (l <= t0 && l < F_INF) ? (1u << r) : 0u;
+		l = lower_bound<METRIC>(acc01[r], ra0, qa1);
+		m01 |= (l <= t1 && l < F_INF) ? (1u << r) : 0u;
+		l = lower_bound<METRIC>(acc11[r], ra1, qa1);
+		m11 |= (l <= t1 && l < F_INF) ? (1u << r) : 0u;
+	}
+	const unsigned c0 = __popc(m00) + __popc(m10), c1 = __popc(m01) + __popc(m11);
+	unsigned off0 = 0, off1 = 0;
+	if (c0) off0 = atomicAdd(&ep_cnt[ql0], c0);
+	if (c1) off1 = atomicAdd(&ep_cnt[ql1], c1);
+	__syncthreads();
+	// one pool reservation per (tile, query)
+	if (tid < BQ) {
+		const unsigned c = ep_cnt[tid];
+		ep_base[tid] = c ? (unsigned)atomicAdd(&pool_cnt[q0 + tid], (int)c) : 0u;
+	}
+	__syncthreads();
+	if ((c0 | c1) == 0) return;
+	// pass B: write the survivors
+	const uint32_t slot0 = (uint32_t)(row0 + rb);
+	if (c0) {
+		unsigned pos = ep_base[ql0] + off0;
+		uint2 *dst = pool + (int64_t)(q0 + ql0) * cap;
 #pragma unroll
-			for (int g = 0; g < 4; ++g) {
-				const int rl = wr * 64 + tr * 32 + 8 * g + 4 * hi;
-				float lb[4];
+		for (int r = 0; r < 16; ++r) {
+			const int rl = (r & 3) + 8 * (r >> 2);
+			if (m00 & (1u << r)) {
+				if (pos < (unsigned)cap)
+					dst[pos] = make_uint2(fkey(lower_bound<METRIC>(acc00[r], RA[rb + rl], qa0)), slot0 + rl);
+				++pos;
+			}
+			if (m10 & (1u << r)) {
+				if (pos < (unsigned)cap)
+					dst[pos] = make_uint2(fkey(lower_bound<METRIC>(acc10[r], RA[rb + 32 + rl], qa0)), slot0 + 32 + rl);
+				++pos;
+			}
+		}
+	}
+	if (c1) {
+		unsigned pos = ep_base[ql1] + off1;
+		uint2 *dst = pool + (int64_t)(q0 + ql1) * cap;
 #pragma unroll
-				for (int j = 0; j < 4; ++j) lb[j] = lower_bound<METRIC>(acc[tr][tq][4 * g + j], RA[rl + j], qa);
-				if (MODE == 0) {
-					float *o = dense + (int64_t)q * ld_out + (int64_t)blockIdx.x * BR + rl;
-					*reinterpret_cast<float4 *>(o) = make_float4(lb[0], lb[1], lb[2], lb[3]);
-				} else {
-#pragma unroll
-					for (int j = 0; j < 4; ++j) {
-						if (lb[j] <= t && lb[j] < F_INF) {
-							int pos = atomicAdd(&pool_cnt[q], 1);
-							if (pos < cap)
-								pool[(int64_t)q * cap + pos] = make_uint2(fkey(lb[j]), (uint32_t)(row0 + rl + j));
-						}
-					}
-				}
+		for (int r = 0; r < 16; ++r) {
+			const int rl = (r & 3) + 8 * (r >> 2);
+			if (m01 & (1u << r)) {
+				if (pos < (unsigned)cap)
+					dst[pos] = make_uint2(fkey(lower_bound<METRIC>(acc01[r], RA[rb + rl], qa1)), slot0 + rl);
+				++pos;
+			}
+			if (m11 & (1u << r)) {
+				if (pos < (unsigned)cap)
+					dst[pos] = make_uint2(fkey(lower_bound<METRIC>(acc11[r], RA[rb + 32 + rl], qa1)), slot0 + 32 + rl);
+				++pos;
 			}
 		}
 	}

@@ -131,6 +131,13 @@ struct Index {
 
 	int64_t last_stats[4] = {0, 0, 0, 0};
 
+	// optional HIP-event timing of the scan kernels, on the stream they run on
+	bool time_kernels = false;
+	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+	double kt_append_ms = 0.0, kt_dense_ms = 0.0;
+	int64_t kt_append_n = 0, kt_dense_n = 0;
+	int64_t kt_append_rows = 0, kt_append_qpad = 0;
+
 	~Index() {
 		if (log) fclose(log);
 		(void)hipSetDevice(device);
@@ -138,7 +145,19 @@ struct Index {
 		if (rowaux) (void)hipFree(rowaux);
 		if (rowaux_l2) (void)hipFree(rowaux_l2);
 		if (dlabels) (void)hipFree(dlabels);
+		for (auto &e : ev)
+			if (e) (void)hipEventDestroy(e);
 		if (stream) (void)hipStreamDestroy(stream);
+	}
+
+	void tic(int i) {
+		if (time_kernels) HIPCHK(hipEventRecord(ev[i], stream));
+	}
+	float toc_ms(int a, int b) {
+		float ms = 0.f;
+		HIPCHK(hipEventSynchronize(ev[b]));
+		HIPCHK(hipEventElapsedTime(&ms, ev[a], ev[b]));
+		return ms;
 	}
 
 	void init_device(int dev) {
@@ -390,12 +409,18 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		last_stats[3] = 1;
 		const int64_t cols = n_tiles * SCAN_BR;
 		ws.dense.need((size_t)nq * cols);
+		tic(0);
 		launch_scan_dense(sv, qv, n_tiles, 1, ws.dense.p, cols, stream);
+		tic(1);
 		launch_select(ws.dense.p, cols, cols, 1, nullptr, nullptr, 0, nullptr, nq, Mfinal, ws.cand_slot.p,
 		              ws.cand_cnt.p, ws.cut.p, stream);
 		launch_refine(sv, qv, ws.cand_slot.p, ws.cand_cnt.p, Mfinal, ws.cand_dist.p, stream);
 		launch_finalize(sv, ws.cand_slot.p, ws.cand_cnt.p, ws.cand_dist.p, ws.cut.p, nq, Mfinal, k, 1, 0, nullptr, dL,
 		                dD, dC, ws.cert.p, stream);
+		if (time_kernels) {
+			kt_dense_ms += toc_ms(0, 1);
+			kt_dense_n += 1;
+		}
 	} else if (fast_ok) {
 		// 1) sample pass: dense LB over every stride-th tile -> tau[q]
 		const int64_t n_sample = std::min<int64_t>(n_tiles, std::max<int64_t>((n_tiles + 63) / 64, 32));
@@ -414,7 +439,9 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		ws.pool.need((size_t)nq * cap_pool);
 		ws.pool_cnt.need(nq);
 		HIPCHK(hipMemsetAsync(ws.pool_cnt.p, 0, (size_t)nq * sizeof(int), stream));
+		tic(2);
 		launch_scan_append(sv, qv, ws.tau.p, ws.pool.p, ws.pool_cnt.p, cap_pool, stream);
+		tic(3);
 		// 3) top-M by LB, exact refine, certificate
 		launch_select(nullptr, 0, 0, 1, ws.pool.p, ws.pool_cnt.p, cap_pool, ws.tau.p, nq, Mfinal, ws.cand_slot.p,
 		              ws.cand_cnt.p, ws.cut.p, stream);
@@ -425,6 +452,12 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		HIPCHK(hipMemcpyAsync(pc.data(), ws.pool_cnt.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, stream));
 		HIPCHK(hipStreamSynchronize(stream));
 		for (int v : pc) last_stats[2] = std::max<int64_t>(last_stats[2], v);
+		if (time_kernels) {
+			kt_append_ms += toc_ms(2, 3);
+			kt_append_n += 1;
+			kt_append_rows = n_slots;
+			kt_append_qpad = nq_pad;
+		}
 	}
 	HIPCHK(hipGetLastError());
 
@@ -951,6 +984,15 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			ix->metric_quirk = on;
 			return 0;
 		}
+		if (k == "time_kernels") {
+			ix->bind();
+			ix->time_kernels = (v == "1" || v == "true");
+			for (auto &e : ix->ev)
+				if (!e) HIPCHK(hipEventCreate(&e));
+			ix->kt_append_ms = ix->kt_dense_ms = 0.0;
+			ix->kt_append_n = ix->kt_dense_n = 0;
+			return 0;
+		}
 		if (k == "reserve_rows") {
 			ix->bind();
 			ix->reserve(std::stoll(v));
@@ -966,6 +1008,19 @@ int32_t lance_hip_last_search_stats(void *handle, int64_t *out, int32_t n) {
 	Index *ix = as_index(handle);
 	std::lock_guard<std::mutex> g(ix->mu);
 	for (int32_t i = 0; i < n && i < 4; ++i) out[i] = ix->last_stats[i];
+	return 0;
+}
+
+// out[0] = total ms of threshold-scan launches, out[1] = their count,
+// out[2] = rows scanned per launch, out[3] = padded queries per launch,
+// out[4] = total ms of small-store dense scans, out[5] = their count.
+int32_t lance_hip_kernel_times(void *handle, double *out, int32_t n) {
+	if (!handle || !out) return -1;
+	Index *ix = as_index(handle);
+	std::lock_guard<std::mutex> g(ix->mu);
+	double v[6] = {ix->kt_append_ms, (double)ix->kt_append_n, (double)ix->kt_append_rows,
+	               (double)ix->kt_append_qpad, ix->kt_dense_ms, (double)ix->kt_dense_n};
+	for (int32_t i = 0; i < n && i < 6; ++i) out[i] = v[i];
 	return 0;
 }
 

@@ -71,6 +71,7 @@ _SIGNATURES = [
     ("lance_hip_add_batch_device", i64, [c_void_p, c_void_p, i64, i32, c_char_p, c_int]),
     ("lance_hip_search_batch_device", i32,
      [c_void_p, c_void_p, i32, i32, i32, i32, i32, c_void_p, c_void_p, c_void_p, c_char_p, c_int]),
+    ("lance_hip_kernel_times", i32, [c_void_p, c_void_p, i32]),
     ("lance_hip_merge_topk_device", i32,
      [i32, i32, i32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_char_p, c_int]),
 ]
@@ -311,6 +312,13 @@ def LanceHipLastSearchStats(handle) -> dict:
     lib().lance_hip_last_search_stats(handle, out.ctypes.data, 4)
     return {"fallback_queries": int(out[0]), "refined": int(out[1]), "max_pool": int(out[2]),
             "dense_path": bool(out[3])}
+
+
+def LanceHipKernelTimes(handle) -> dict:
+    out = np.zeros(6, np.float64)
+    lib().lance_hip_kernel_times(handle, out.ctypes.data, 6)
+    return {"scan_ms_total": float(out[0]), "scan_launches": int(out[1]), "scan_rows": int(out[2]),
+            "scan_qpad": int(out[3]), "dense_ms_total": float(out[4]), "dense_launches": int(out[5])}
 
 
 def LanceHipMergeTopk(part_labels, part_dists, part_counts):

@@ -159,6 +159,30 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
  * out[3] = 1 if the dense (small-N) path ran.  Returns 0 or -1. */
 int32_t lance_hip_last_search_stats(void *handle, int64_t *out, int32_t n);
 
+/* Per-handle HIP-event timings of the scan kernels (enable with option
+ * "time_kernels"="1"; events recorded on the handle's stream around each launch):
+ * out[0] total ms of threshold-scan launches, out[1] their count, out[2] rows
+ * per launch, out[3] padded queries per launch, out[4] total ms of small-store
+ * dense scans, out[5] their count.  Returns 0 or -1. */
+int32_t lance_hip_kernel_times(void *handle, double *out, int32_t n);
+
+/* Device-pointer ingest: num x dim row-major f32 already on the handle's device.
+ * Labels [returned, returned+num).  Returns the first label or -1. */
+int64_t lance_hip_add_batch_device(void *handle, const float *d_vectors, int64_t num, int32_t dim, char *err_buf,
+                                   int err_buf_len);
+
+/* Device-pointer batched search (inputs resident in HBM; synchronous: returns
+ * once the device outputs are written).  Same semantics as
+ * lance_detached_search_batch.  Returns nq or -1. */
+int32_t lance_hip_search_batch_device(void *handle, const float *d_queries, int32_t nq, int32_t dim, int32_t k,
+                                      int32_t nprobes, int32_t refine_factor, int64_t *d_out_labels,
+                                      float *d_out_distances, int32_t *d_out_counts, char *err_buf, int err_buf_len);
+
+/* Device-pointer variant of lance_hip_merge_topk (current device, null stream). */
+int32_t lance_hip_merge_topk_device(int32_t nshard, int32_t nq, int32_t k, const int64_t *d_part_labels,
+                                    const float *d_part_dists, const int32_t *d_part_counts, int64_t *d_out_labels,
+                                    float *d_out_dists, int32_t *d_out_counts, char *err_buf, int err_buf_len);
+
 /* Merge per-shard partial top-k lists into a global top-k, on the device of
  * the handle (multi-GPU path: shards all-gathered over RCCL).
  * part_labels / part_dists: nshard x nq x k (host pointers), part_counts:
