@@ -512,7 +512,7 @@ void launch_scan_append(const StoreView &s, const QueryView &q, const float *tau
 // select: per-query radix select of the M smallest lower bounds
 // One 256-thread workgroup per query; 11/11/10-bit digits over ordered keys.
 // ---------------------------------------------------------------------------
-constexpr int SEL_THREADS = 256;
+constexpr int SEL_THREADS = 512;
 constexpr int SEL_BINS = 2048;
 
 struct SelSrc {
@@ -533,7 +533,7 @@ struct SelSrc {
 };
 
 // exclusive scan of one value per thread across the 256-thread block
-__device__ __forceinline__ unsigned block_excl_scan(unsigned v, unsigned *sh /*[8]*/, unsigned &total) {
+__device__ __forceinline__ unsigned block_excl_scan(unsigned v, unsigned *sh /*[SEL_THREADS/64]*/, unsigned &total) {
 	const int t = threadIdx.x, lane = t & 63, w = t >> 6;
 	unsigned x = v;
 #pragma unroll
@@ -543,34 +543,111 @@ __device__ __forceinline__ unsigned block_excl_scan(unsigned v, unsigned *sh /*[
 	}
 	if (lane == 63) sh[w] = x;
 	__syncthreads();
-	unsigned base = 0;
-	for (int i = 0; i < w; ++i) base += sh[i];
-	total = sh[0] + sh[1] + sh[2] + sh[3];
+	unsigned base = 0, tot = 0;
+#pragma unroll
+	for (int i = 0; i < SEL_THREADS / 64; ++i) {
+		base += (i < w) ? sh[i] : 0u;
+		tot += sh[i];
+	}
+	total = tot;
 	__syncthreads();
 	return base + x - v;
 }
+
+__device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) v = min(v, (unsigned)__shfl_xor(v, o, 64));
+	return v;
+}
+
+// LDS-resident variant: the whole list of one query is staged once (16 B
+// vector loads, several in flight per thread), every radix pass then reads LDS.
+constexpr int SEL_LDS_KEYS = 16384;  // dense lists (keys only) up to 16K entries
+constexpr int SEL_LDS_PAIRS = 8192;  // pool lists (key, slot) up to 8K entries
 
 __global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const int *__restrict__ pool_cnt,
                                                              const float *__restrict__ tau, int M,
                                                              uint32_t *__restrict__ cand_slot,
                                                              int *__restrict__ cand_cnt, float *__restrict__ cut) {
+	__shared__ __attribute__((aligned(16))) uint32_t s_keys[SEL_LDS_KEYS];
 	__shared__ unsigned hist[SEL_BINS];
-	__shared__ unsigned sh[8];
+	__shared__ unsigned sh[SEL_THREADS / 64];
 	__shared__ unsigned s_digit, s_rem, s_nlt, s_neq, s_minex;
 	const int q = blockIdx.x;
 	const int t = threadIdx.x;
 	int64_t n;
 	bool overflow = false;
-	if (src.dense) {
+	const bool dense = src.dense != nullptr;
+	if (dense) {
 		n = src.n_entries;
 	} else {
 		int c = pool_cnt[q];
 		overflow = c > src.cap;
 		n = c < src.cap ? c : src.cap;
 	}
-	const float ftau = src.dense ? F_INF : tau[q];
+	const float ftau = dense ? F_INF : tau[q];
+	const bool in_lds = dense ? (n <= SEL_LDS_KEYS) : (n <= SEL_LDS_PAIRS);
+	uint32_t *s_slots = s_keys + SEL_LDS_PAIRS;  // pool mode: [keys 8K | slots 8K]
 
-	// pass 1: histogram of the top 11 bits (also counts +inf / NaN keys)
+	// stage (LDS path)
+	if (in_lds) {
+		if (dense) {
+			const float *row = src.dense + (int64_t)q * src.ld_dense;
+			const int n4 = (int)(n >> 2);
+			constexpr int U = 8;  // loads in flight per thread
+			for (int i0 = 0; i0 < n4; i0 += U * SEL_THREADS) {
+				float4 v[U];
+#pragma unroll
+				for (int u = 0; u < U; ++u) {
+					const int i = i0 + u * SEL_THREADS + t;
+					v[u] = i < n4 ? reinterpret_cast<const float4 *>(row)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+				}
+#pragma unroll
+				for (int u = 0; u < U; ++u) {
+					const int i = i0 + u * SEL_THREADS + t;
+					if (i < n4)
+						reinterpret_cast<uint4 *>(s_keys)[i] =
+						    make_uint4(fkey(v[u].x), fkey(v[u].y), fkey(v[u].z), fkey(v[u].w));
+				}
+			}
+			for (int64_t i = (int64_t)n4 * 4 + t; i < n; i += SEL_THREADS) s_keys[i] = fkey(row[i]);
+		} else {
+			const uint2 *pl = src.pool + (int64_t)q * src.cap;
+			constexpr int U = 8;
+			for (int i0 = 0; i0 < n; i0 += U * SEL_THREADS) {
+				uint2 e[U];
+#pragma unroll
+				for (int u = 0; u < U; ++u) {
+					const int i = i0 + u * SEL_THREADS + t;
+					e[u] = i < n ? pl[i] : make_uint2(0u, 0u);
+				}
+#pragma unroll
+				for (int u = 0; u < U; ++u) {
+					const int i = i0 + u * SEL_THREADS + t;
+					if (i < n) {
+						s_keys[i] = e[u].x;
+						s_slots[i] = e[u].y;
+					}
+				}
+			}
+		}
+	}
+	auto key_at = [&](int64_t i) -> uint32_t {
+		if (in_lds) return s_keys[i];
+		uint32_t k, sl;
+		src.get(q, i, k, sl);
+		return k;
+	};
+	auto slot_at = [&](int64_t i) -> uint32_t {
+		if (in_lds) {
+			if (dense) return (uint32_t)((i / BR) * src.tile_stride * BR + (i % BR));
+			return s_slots[i];
+		}
+		uint32_t k, sl;
+		src.get(q, i, k, sl);
+		return sl;
+	};
+
 	for (int i = t; i < SEL_BINS; i += SEL_THREADS) hist[i] = 0;
 	if (t == 0) {
 		s_nlt = 0;
@@ -578,58 +655,49 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const i
 		s_minex = 0xFFFFFFFFu;
 	}
 	__syncthreads();
-	for (int64_t i = t; i < n; i += SEL_THREADS) {
-		uint32_t k, sl;
-		src.get(q, i, k, sl);
-		atomicAdd(&hist[k >> 21], 1u);
-	}
+	// pass 1: histogram of the top 11 bits (also counts +inf / NaN keys)
+	for (int64_t i = t; i < n; i += SEL_THREADS) atomicAdd(&hist[key_at(i) >> 21], 1u);
 	__syncthreads();
 	const unsigned n_nan = hist[SEL_BINS - 1];
 	const unsigned n_inf = hist[KEY_INF >> 21];  // bin 0x7FC holds +inf only
 	const int64_t n_fin = n - n_nan - n_inf;
 	float c_out;
 	if (n_fin <= M) {
-		// take every finite entry
 		for (int64_t i = t; i < n; i += SEL_THREADS) {
-			uint32_t k, sl;
-			src.get(q, i, k, sl);
-			if (k < KEY_INF) {
+			if (key_at(i) < KEY_INF) {
 				unsigned p = atomicAdd(&s_nlt, 1u);
-				cand_slot[(int64_t)q * M + p] = sl;
+				cand_slot[(int64_t)q * M + p] = slot_at(i);
 			}
 		}
 		__syncthreads();
 		c_out = ftau;
 	} else {
 		unsigned prefix = 0, mask = 0, rem = (unsigned)M;
-		const int shifts[3] = {21, 10, 0};
-		const int widths[3] = {11, 11, 10};
 #pragma unroll 1
 		for (int p = 0; p < 3; ++p) {
-			const int sh_ = shifts[p];
-			const unsigned dmask = (1u << widths[p]) - 1u;
+			const int sh_ = p == 0 ? 21 : (p == 1 ? 10 : 0);
+			const unsigned dmask = p == 2 ? 0x3FFu : 0x7FFu;
 			if (p > 0) {
 				for (int i = t; i < SEL_BINS; i += SEL_THREADS) hist[i] = 0;
 				__syncthreads();
 				for (int64_t i = t; i < n; i += SEL_THREADS) {
-					uint32_t k, sl;
-					src.get(q, i, k, sl);
+					const uint32_t k = key_at(i);
 					if ((k & mask) == prefix) atomicAdd(&hist[(k >> sh_) & dmask], 1u);
 				}
 				__syncthreads();
 			}
-			// each thread owns 8 consecutive bins
+			constexpr int BPT = SEL_BINS / SEL_THREADS;
 			unsigned local = 0;
 #pragma unroll
-			for (int j = 0; j < 8; ++j) local += hist[t * 8 + j];
+			for (int j = 0; j < BPT; ++j) local += hist[t * BPT + j];
 			unsigned total;
 			unsigned excl = block_excl_scan(local, sh, total);
 			if (excl < rem && rem <= excl + local) {
 				unsigned c = excl;
-				for (int j = 0; j < 8; ++j) {
-					unsigned h = hist[t * 8 + j];
+				for (int j = 0; j < BPT; ++j) {
+					unsigned h = hist[t * BPT + j];
 					if (rem <= c + h) {
-						s_digit = (unsigned)(t * 8 + j);
+						s_digit = (unsigned)(t * BPT + j);
 						s_rem = rem - c;
 						break;
 					}
@@ -642,24 +710,26 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const i
 			rem = s_rem;
 			__syncthreads();
 		}
-		const uint32_t T = prefix;          // key of the M-th smallest
+		const uint32_t T = prefix;                // key of the M-th smallest
 		const unsigned n_lt = (unsigned)M - rem;  // entries strictly below T
+		unsigned my_min = 0xFFFFFFFFu;            // smallest key left out
 		for (int64_t i = t; i < n; i += SEL_THREADS) {
-			uint32_t k, sl;
-			src.get(q, i, k, sl);
+			const uint32_t k = key_at(i);
 			if (k < T) {
 				unsigned p = atomicAdd(&s_nlt, 1u);
-				cand_slot[(int64_t)q * M + p] = sl;
+				cand_slot[(int64_t)q * M + p] = slot_at(i);
 			} else if (k == T) {
 				unsigned p = atomicAdd(&s_neq, 1u);
 				if (p < rem)
-					cand_slot[(int64_t)q * M + n_lt + p] = sl;
+					cand_slot[(int64_t)q * M + n_lt + p] = slot_at(i);
 				else
-					atomicMin(&s_minex, k);
+					my_min = min(my_min, k);
 			} else if (k < KEY_INF) {
-				atomicMin(&s_minex, k);
+				my_min = min(my_min, k);
 			}
 		}
+		my_min = wave_min_u32(my_min);
+		if ((t & 63) == 0 && my_min != 0xFFFFFFFFu) atomicMin(&s_minex, my_min);
 		__syncthreads();
 		c_out = (s_minex == 0xFFFFFFFFu) ? F_INF : fkey_inv(s_minex);
 		if (ftau < c_out) c_out = ftau;

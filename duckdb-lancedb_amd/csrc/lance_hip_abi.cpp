@@ -86,11 +86,22 @@ struct Workspace {
 	DevBuf<uint16_t> Qb;
 	DevBuf<float4> qaux;
 	DevBuf<uint2> pool;
-	DevBuf<int> pool_cnt, cand_cnt, out_c, cert;
+	DevBuf<int> status, out_c;  // status = [cert | cand_cnt | pool_cnt] x nq
+	int *h_status = nullptr;    // pinned mirror of status
+	size_t h_status_n = 0;
 	DevBuf<uint32_t> cand_slot;
 	DevBuf<int64_t> out_l, fb_vals, fb_vals2, idx;
 	DevBuf<uint8_t> sort_tmp;
-	std::vector<int> h_cert;
+	~Workspace() {
+		if (h_status) (void)hipHostFree(h_status);
+	}
+	void need_host_status(size_t n) {
+		if (n <= h_status_n) return;
+		if (h_status) HIPCHK(hipHostFree(h_status));
+		h_status = nullptr;
+		HIPCHK(hipHostMalloc(&h_status, n * sizeof(int)));
+		h_status_n = n;
+	}
 };
 
 // ---------------------------------------------------------------------------
@@ -392,9 +403,11 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	ws.tau.need(nq);
 	ws.cut.need(nq);
 	ws.cand_slot.need((size_t)nq * MAX_CAND);
-	ws.cand_cnt.need(nq);
 	ws.cand_dist.need((size_t)nq * MAX_CAND);
-	ws.cert.need(nq);
+	ws.status.need((size_t)3 * nq);
+	ws.need_host_status((size_t)3 * nq);
+	int *d_cert = ws.status.p, *d_cand_cnt = ws.status.p + nq, *d_pool_cnt = ws.status.p + 2 * nq;
+	HIPCHK(hipMemsetAsync(ws.status.p, 0, (size_t)3 * nq * sizeof(int), stream));
 	launch_prep_queries(dQ, nq, dim, ld, nq_pad, eff_metric, ma, mu, ws.Qf.p, ws.Qb.p, ws.qaux.p, stream);
 	QueryView qv{ws.Qf.p, ws.Qb.p, ws.qaux.p, nq, nq_pad};
 
@@ -413,10 +426,10 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		launch_scan_dense(sv, qv, n_tiles, 1, ws.dense.p, cols, stream);
 		tic(1);
 		launch_select(ws.dense.p, cols, cols, 1, nullptr, nullptr, 0, nullptr, nq, Mfinal, ws.cand_slot.p,
-		              ws.cand_cnt.p, ws.cut.p, stream);
-		launch_refine(sv, qv, ws.cand_slot.p, ws.cand_cnt.p, Mfinal, ws.cand_dist.p, stream);
-		launch_finalize(sv, ws.cand_slot.p, ws.cand_cnt.p, ws.cand_dist.p, ws.cut.p, nq, Mfinal, k, 1, 0, nullptr, dL,
-		                dD, dC, ws.cert.p, stream);
+		              d_cand_cnt, ws.cut.p, stream);
+		launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Mfinal, ws.cand_dist.p, stream);
+		launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Mfinal, k, 1, 0, nullptr, dL,
+		                dD, dC, d_cert, stream);
 		if (time_kernels) {
 			kt_dense_ms += toc_ms(0, 1);
 			kt_dense_n += 1;
@@ -430,48 +443,42 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		ws.dense.need((size_t)nq * cols);
 		launch_scan_dense(sv, qv, n_sample, stride, ws.dense.p, cols, stream);
 		launch_select(ws.dense.p, cols, cols, stride, nullptr, nullptr, 0, nullptr, nq, Ms, ws.cand_slot.p,
-		              ws.cand_cnt.p, ws.cut.p, stream);
-		launch_refine(sv, qv, ws.cand_slot.p, ws.cand_cnt.p, Ms, ws.cand_dist.p, stream);
-		launch_finalize(sv, ws.cand_slot.p, ws.cand_cnt.p, ws.cand_dist.p, ws.cut.p, nq, Ms, k, 0, k + 1, ws.tau.p,
+		              d_cand_cnt, ws.cut.p, stream);
+		launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Ms, ws.cand_dist.p, stream);
+		launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Ms, k, 0, k + 1, ws.tau.p,
 		                nullptr, nullptr, nullptr, nullptr, stream);
 		// 2) threshold scan over every row
 		const int cap_pool = std::max(8192, 256 * (k + 8));
 		ws.pool.need((size_t)nq * cap_pool);
-		ws.pool_cnt.need(nq);
-		HIPCHK(hipMemsetAsync(ws.pool_cnt.p, 0, (size_t)nq * sizeof(int), stream));
 		tic(2);
-		launch_scan_append(sv, qv, ws.tau.p, ws.pool.p, ws.pool_cnt.p, cap_pool, stream);
+		launch_scan_append(sv, qv, ws.tau.p, ws.pool.p, d_pool_cnt, cap_pool, stream);
 		tic(3);
 		// 3) top-M by LB, exact refine, certificate
-		launch_select(nullptr, 0, 0, 1, ws.pool.p, ws.pool_cnt.p, cap_pool, ws.tau.p, nq, Mfinal, ws.cand_slot.p,
-		              ws.cand_cnt.p, ws.cut.p, stream);
-		launch_refine(sv, qv, ws.cand_slot.p, ws.cand_cnt.p, Mfinal, ws.cand_dist.p, stream);
-		launch_finalize(sv, ws.cand_slot.p, ws.cand_cnt.p, ws.cand_dist.p, ws.cut.p, nq, Mfinal, k, 1, 0, nullptr, dL,
-		                dD, dC, ws.cert.p, stream);
-		std::vector<int> pc((size_t)nq);
-		HIPCHK(hipMemcpyAsync(pc.data(), ws.pool_cnt.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, stream));
-		HIPCHK(hipStreamSynchronize(stream));
-		for (int v : pc) last_stats[2] = std::max<int64_t>(last_stats[2], v);
-		if (time_kernels) {
-			kt_append_ms += toc_ms(2, 3);
-			kt_append_n += 1;
-			kt_append_rows = n_slots;
-			kt_append_qpad = nq_pad;
-		}
+		launch_select(nullptr, 0, 0, 1, ws.pool.p, d_pool_cnt, cap_pool, ws.tau.p, nq, Mfinal, ws.cand_slot.p,
+		              d_cand_cnt, ws.cut.p, stream);
+		launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Mfinal, ws.cand_dist.p, stream);
+		launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Mfinal, k, 1, 0, nullptr, dL,
+		                dD, dC, d_cert, stream);
 	}
 	HIPCHK(hipGetLastError());
 
-	ws.h_cert.assign((size_t)nq, 0);
-	if (!all_fallback) {
-		HIPCHK(hipMemcpyAsync(ws.h_cert.data(), ws.cert.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, stream));
-		std::vector<int> cc((size_t)nq);
-		HIPCHK(hipMemcpyAsync(cc.data(), ws.cand_cnt.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, stream));
-		HIPCHK(hipStreamSynchronize(stream));
-		for (int v : cc) last_stats[1] += v;
+	// one pinned readback of [cert | cand_cnt | pool_cnt]
+	HIPCHK(hipMemcpyAsync(ws.h_status, ws.status.p, (size_t)3 * nq * sizeof(int), hipMemcpyDeviceToHost, stream));
+	HIPCHK(hipStreamSynchronize(stream));
+	if (time_kernels && !all_fallback && last_stats[3] == 0) {
+		kt_append_ms += toc_ms(2, 3);
+		kt_append_n += 1;
+		kt_append_rows = n_slots;
+		kt_append_qpad = nq_pad;
+	}
+	const int *h_cert = ws.h_status;
+	for (int q = 0; q < nq; ++q) {
+		last_stats[1] += ws.h_status[nq + q];
+		last_stats[2] = std::max<int64_t>(last_stats[2], ws.h_status[2 * nq + q]);
 	}
 	// exact fallback for every query whose certificate failed
 	for (int q = 0; q < nq; ++q) {
-		if (ws.h_cert[(size_t)q]) continue;
+		if (!all_fallback && h_cert[q]) continue;
 		last_stats[0] += 1;
 		ws.fb_keys.need((size_t)n_slots);
 		ws.fb_keys2.need((size_t)n_slots);
