@@ -207,18 +207,45 @@ void launch_prep_queries(const float *Q, int nq, int dim, int ld, int nq_pad, in
 // Global loads of step k+1 are issued before the MFMAs of step k.
 // ---------------------------------------------------------------------------
 constexpr int BR = SCAN_BR, BQ = SCAN_BQ, BK = SCAN_BK;
-constexpr int XS_BYTES = BR * BK * 2;  // 16 KiB bf16 base tile
-constexpr int QS_BYTES = BQ * BK * 2;  // 32 KiB bf16 query tile
-constexpr int RA_BYTES = BR * 16;      // row aux of the tile
-constexpr int EP_BYTES = BQ * 8;       // epilogue per-query counters + pool bases
-constexpr int SCAN_LDS = XS_BYTES + QS_BYTES + RA_BYTES + EP_BYTES;
 
-// byte offset of 16 B chunk `chunk` (0..7) of row `row` in a [rows][64] bf16
-// LDS image: chunk index XOR-ed with (row>>1)&7 so that the ds_read_b128
-// fragment loads of 32 consecutive rows hit distinct bank groups
-__device__ __forceinline__ int swz(int row, int chunk) {
-	return row * (BK * 2) + ((chunk ^ ((row >> 1) & 7)) << 4);
-}
+// ---------------------------------------------------------------------------
+// scan kernel (LDS-DMA ring)
+//
+// Workgroup = 1024 threads = 16 waves laid out 4 (base rows) x 4 (queries);
+// each wave owns a 64-row x 64-query sub-tile = 2x2 v_mfma_f32_32x32x16_bf16
+// tiles (A = base rows, B = queries: accumulator column = lane&31 = query,
+// the 16 registers walk base rows).  Tile = 256 base rows x 256 queries, one
+// workgroup (4 waves per SIMD) per CU: every base byte crosses HBM once and
+// the query tile (L2-resident) costs half a byte per base byte.
+//
+// The k dimension streams through a ring of NSTAGE LDS stages of SK = 32:
+//   X stage: 256 rows x 32 f32 (32 KiB) straight from HBM by
+//            global_load_lds_dwordx4 (no VGPR staging), rows 128 B,
+//            16 B chunk c of row r stored at c ^ ((r>>1)&7);
+//   Q stage: 256 queries x 32 bf16 (16 KiB) from L2, rows 64 B,
+//            chunk c of row r stored at c ^ ((r>>2)&3).
+// LDS-DMA writes lane-linear, so the swizzle is applied on the per-lane SOURCE
+// address and undone on the ds_read_b128 fragment reads (conflict-free for
+// the b128 lane groups).  A fragments are converted f32 -> bf16 after the read.
+// Per stage each thread issues 3 DMA instructions; NSTAGE-1 stages stay in
+// flight; one raw s_barrier per stage behind a counted s_waitcnt vmcnt.
+// The store is zero-padded to a multiple of BR rows, so no row is clamped.
+// ---------------------------------------------------------------------------
+constexpr int SCAN_THREADS = 1024;
+constexpr int SK = 32;
+constexpr int NSTAGE = 3;
+constexpr int XST_BYTES = BR * SK * 4;                 // 32 KiB
+constexpr int QST_BYTES = BQ * SK * 2;                 // 16 KiB
+constexpr int STAGE_BYTES = XST_BYTES + QST_BYTES;     // 48 KiB
+constexpr int RING_BYTES = NSTAGE * STAGE_BYTES;       // 144 KiB
+constexpr int RA_BYTES = BR * 16;
+constexpr int EP_BYTES = BQ * 8 + 64;  // per-query counters + pool bases + list counter + overflow bits
+constexpr int SCAN_LDS = RING_BYTES + RA_BYTES + EP_BYTES;
+static_assert(SCAN_LDS <= 160 * 1024, "LDS budget");
+static_assert(XST_BYTES / 1024 == 2 * (SCAN_THREADS / 64), "2 X DMA instructions per wave per stage");
+static_assert(QST_BYTES / 1024 == SCAN_THREADS / 64, "1 Q DMA instruction per wave per stage");
+
+typedef __attribute__((address_space(3))) void lds_void;
 
 template <int METRIC>
 __device__ __forceinline__ float lower_bound(float s, float4 ra, float4 qa) {
@@ -230,75 +257,70 @@ __device__ __forceinline__ float lower_bound(float s, float4 ra, float4 qa) {
 	return v + qa.w;
 }
 
-__device__ __forceinline__ uint2 cvt4(float4 v, bool ok) {
-	uint2 r = make_uint2(pk_bf16(v.x, v.y), pk_bf16(v.z, v.w));
-	return ok ? r : make_uint2(0u, 0u);
+// One global_load_lds_dwordx4: 64 lanes x 16 B land lane-linearly at the
+// wave-uniform LDS byte address in M0.  Issued through inline asm so the
+// compiler does not see an LDS write in flight: it would otherwise put a
+// vmcnt(0) in front of every ds_read of the ring (any stage may alias) and
+// serialise the pipeline.  Ordering is ours: counted vmcnt + s_barrier.
+// M0 is written here and nowhere else in the kernel.
+__device__ __forceinline__ void dma16(const void *g, uint32_t lds_addr) {
+	asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_addr), "v"(g) : "memory", "m0");
 }
 
-// ---------------------------------------------------------------------------
-// scan kernel
-//
-// Workgroup = 512 threads = 8 waves, 2 (base rows) x 4 (queries); each wave owns
-// a 64-row x 64-query sub-tile = 2x2 v_mfma_f32_32x32x16_bf16 tiles (A = base
-// rows, B = queries: accumulator column = lane&31 = query, the 16 registers
-// walk base rows).  Per 64-deep k-step the workgroup pulls a 128 x 64 f32 base
-// tile from HBM (16 B per lane, 256 contiguous bytes per row), converts it to
-// bf16 in registers (v_cvt_pk_bf16_f32) and a 256 x 64 bf16 query tile from L2,
-// into XOR-swizzled LDS.  Loads of step k+1 are in flight during the MFMAs of
-// step k; <=128 VGPRs keeps two workgroups (16 waves) per CU so one
-// workgroup's MFMAs cover the other's load latency.
-// Epilogue: each accumulator becomes a rigorous lower bound of the exact
-// distance; dense mode stores it, append mode keeps (LB, slot) if LB <= tau[q]
-// with one global pool reservation per (tile, query) instead of per candidate.
-// ---------------------------------------------------------------------------
+__device__ __forceinline__ bf16x8 ld_afrag(const uint8_t *xs, int r, int c) {
+	const int f = (r >> 1) & 7;
+	const float4 lo = *reinterpret_cast<const float4 *>(xs + r * 128 + ((c ^ f) << 4));
+	const float4 hi = *reinterpret_cast<const float4 *>(xs + r * 128 + (((c + 1) ^ f) << 4));
+	bf16x8 v;
+	v[0] = (__bf16)lo.x;
+	v[1] = (__bf16)lo.y;
+	v[2] = (__bf16)lo.z;
+	v[3] = (__bf16)lo.w;
+	v[4] = (__bf16)hi.x;
+	v[5] = (__bf16)hi.y;
+	v[6] = (__bf16)hi.z;
+	v[7] = (__bf16)hi.w;
+	return v;
+}
+
+__device__ __forceinline__ bf16x8 ld_bfrag(const uint8_t *qs, int r, int c) {
+	return *reinterpret_cast<const bf16x8 *>(qs + r * 64 + ((c ^ ((r >> 2) & 3)) << 4));
+}
+
+#define LHIP_WAIT_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+
 template <int METRIC, int MODE>
-__global__ __launch_bounds__(512, 2) void scan_kernel(const float *__restrict__ X, const float4 *__restrict__ rowaux,
-                                                      int64_t n_slots, int ld, const uint16_t *__restrict__ Qb,
-                                                      const float4 *__restrict__ qaux, int nq, int64_t tile_stride,
-                                                      float *__restrict__ dense, int64_t ld_out,
-                                                      const float *__restrict__ tau, uint2 *__restrict__ pool,
-                                                      int *__restrict__ pool_cnt, int cap) {
+__global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(const float *__restrict__ X,
+                                                            const float4 *__restrict__ rowaux, int64_t n_slots, int ld,
+                                                            const uint16_t *__restrict__ Qb,
+                                                            const float4 *__restrict__ qaux, int nq,
+                                                            int64_t tile_stride, float *__restrict__ dense,
+                                                            int64_t ld_out, const float *__restrict__ tau,
+                                                            uint2 *__restrict__ pool, int *__restrict__ pool_cnt,
+                                                            int cap) {
 	__shared__ __attribute__((aligned(16))) uint8_t smem[SCAN_LDS];
-	uint8_t *Xs = smem;
-	uint8_t *Qs = smem + XS_BYTES;
-	float4 *RA = reinterpret_cast<float4 *>(smem + XS_BYTES + QS_BYTES);
-	unsigned *ep_cnt = reinterpret_cast<unsigned *>(smem + XS_BYTES + QS_BYTES + RA_BYTES);
+	float4 *RA = reinterpret_cast<float4 *>(smem + RING_BYTES);
+	unsigned *ep_cnt = reinterpret_cast<unsigned *>(smem + RING_BYTES + RA_BYTES);
 	unsigned *ep_base = ep_cnt + BQ;
 
 	const int tid = threadIdx.x;
 	const int lane = tid & 63;
 	const int w = tid >> 6;
-	const int wr = w & 1, wq = w >> 1;
+	const int wr = w & 3, wq = w >> 2;
 	const int li = lane & 31, hi = lane >> 5;
 	const int64_t row0 = (int64_t)blockIdx.x * tile_stride * BR;
 	const int q0 = blockIdx.y * BQ;
 
-	if (tid < BR) {
-		int64_t r = row0 + tid;
-		RA[tid] = (r < n_slots) ? rowaux[r] : make_float4(F_INF, 0.f, 0.f, 0.f);
-	}
-	if (MODE == 1 && tid < BQ) ep_cnt[tid] = 0u;
-
-	// X staging: float4 f = tid + 512 i (i < 4) of the 128 x 16 float4 tile:
-	// row = (tid >> 4) + 32 i, float4 column c4 = tid & 15
-	const int xr = tid >> 4, xc4 = tid & 15;
-	uint32_t xmask = 0;
-#pragma unroll
-	for (int i = 0; i < 4; ++i) xmask |= (row0 + xr + 32 * i < n_slots) ? (1u << i) : 0u;
-	// rows past the end are clamped to the last slot (valid memory) and zeroed
-	const int64_t last = n_slots - 1;
-	const float *xq0 = X + min(row0 + xr, last) * ld + xc4 * 4;
-	const float *xq1 = X + min(row0 + xr + 32, last) * ld + xc4 * 4;
-	const float *xq2 = X + min(row0 + xr + 64, last) * ld + xc4 * 4;
-	const float *xq3 = X + min(row0 + xr + 96, last) * ld + xc4 * 4;
-	// Q staging: 16 B chunk f = tid + 512 i: row = (tid >> 3) + 64 i, chunk = tid & 7
-	const int qr = tid >> 3, qc = tid & 7;
-	const uint16_t *qp = Qb + (int64_t)(q0 + qr) * ld + qc * 8;
-	const int64_t qstride = (int64_t)64 * ld;
-
-	// LDS destinations of this thread's staged data
-	const int xdst0 = swz(xr, xc4 >> 1) + (xc4 & 1) * 8;
-	const int qdst0 = swz(qr, qc);
+	// DMA sources.  X: wave instruction j (0,1) covers rows (2w+j)*8 + lane/8,
+	// physical 16 B chunk lane%8 (logical chunk = physical ^ ((row>>1)&7)).
+	// Q: one instruction covers queries w*16 + lane/4, physical chunk lane%4.
+	const int xr0 = (2 * w) * 8 + (lane >> 3), xr1 = xr0 + 8;
+	const float *xsrc0 = X + (row0 + xr0) * ld + (((lane & 7) ^ ((xr0 >> 1) & 7)) << 2);
+	const float *xsrc1 = X + (row0 + xr1) * ld + (((lane & 7) ^ ((xr1 >> 1) & 7)) << 2);
+	const int qr = w * 16 + (lane >> 2);
+	const uint16_t *qsrc = Qb + (int64_t)(q0 + qr) * ld + (((lane & 3) ^ ((qr >> 2) & 3)) << 3);
+	const int xdst0 = (2 * w) * 1024, xdst1 = xdst0 + 1024;
+	const int qdst = XST_BYTES + w * 1024;
 
 	f32x16 acc00, acc01, acc10, acc11;
 #pragma unroll
@@ -309,56 +331,55 @@ __global__ __launch_bounds__(512, 2) void scan_kernel(const float *__restrict__ 
 		acc11[r] = 0.f;
 	}
 
-	float4 x0, x1, x2, x3;
-	uint4 y0, y1, y2, y3;
-	const int KT = ld / BK;
-	x0 = *reinterpret_cast<const float4 *>(xq0);
-	x1 = *reinterpret_cast<const float4 *>(xq1);
-	x2 = *reinterpret_cast<const float4 *>(xq2);
-	x3 = *reinterpret_cast<const float4 *>(xq3);
-	y0 = *reinterpret_cast<const uint4 *>(qp);
-	y1 = *reinterpret_cast<const uint4 *>(qp + qstride);
-	y2 = *reinterpret_cast<const uint4 *>(qp + 2 * qstride);
-	y3 = *reinterpret_cast<const uint4 *>(qp + 3 * qstride);
-	for (int kt = 0; kt < KT; ++kt) {
-		// stage the landed step into LDS
-		*reinterpret_cast<uint2 *>(Xs + xdst0) = cvt4(x0, xmask & 1u);
-		*reinterpret_cast<uint2 *>(Xs + xdst0 + 32 * 128) = cvt4(x1, xmask & 2u);
-		*reinterpret_cast<uint2 *>(Xs + xdst0 + 64 * 128) = cvt4(x2, xmask & 4u);
-		*reinterpret_cast<uint2 *>(Xs + xdst0 + 96 * 128) = cvt4(x3, xmask & 8u);
-		*reinterpret_cast<uint4 *>(Qs + qdst0) = y0;
-		*reinterpret_cast<uint4 *>(Qs + qdst0 + 64 * 128) = y1;
-		*reinterpret_cast<uint4 *>(Qs + qdst0 + 128 * 128) = y2;
-		*reinterpret_cast<uint4 *>(Qs + qdst0 + 192 * 128) = y3;
-		__syncthreads();
-		// issue the next step's loads before this step's MFMAs
-		if (kt + 1 < KT) {
-			const int ko = (kt + 1) * BK;
-			x0 = *reinterpret_cast<const float4 *>(xq0 + ko);
-			x1 = *reinterpret_cast<const float4 *>(xq1 + ko);
-			x2 = *reinterpret_cast<const float4 *>(xq2 + ko);
-			x3 = *reinterpret_cast<const float4 *>(xq3 + ko);
-			y0 = *reinterpret_cast<const uint4 *>(qp + ko);
-			y1 = *reinterpret_cast<const uint4 *>(qp + qstride + ko);
-			y2 = *reinterpret_cast<const uint4 *>(qp + 2 * qstride + ko);
-			y3 = *reinterpret_cast<const uint4 *>(qp + 3 * qstride + ko);
-		}
-#pragma unroll
-		for (int ks = 0; ks < BK / 16; ++ks) {
-			const int kc = ks * 2 + hi;
-			const bf16x8 a0 = *reinterpret_cast<const bf16x8 *>(Xs + swz(wr * 64 + li, kc));
-			const bf16x8 a1 = *reinterpret_cast<const bf16x8 *>(Xs + swz(wr * 64 + 32 + li, kc));
-			const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(Qs + swz(wq * 64 + li, kc));
-			const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(Qs + swz(wq * 64 + 32 + li, kc));
+	const int S = ld / SK;  // >= 2 (ld is a multiple of 64)
+	const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
+#define LHIP_ISSUE(st_)                                                                                             \
+	do {                                                                                                            \
+		const uint32_t base_ = lds0 + ((st_) % NSTAGE) * STAGE_BYTES;                                               \
+		const int ko_ = (st_) * SK;                                                                                 \
+		dma16(xsrc0 + ko_, __builtin_amdgcn_readfirstlane(base_ + xdst0));                                          \
+		dma16(xsrc1 + ko_, __builtin_amdgcn_readfirstlane(base_ + xdst1));                                          \
+		dma16(qsrc + ko_, __builtin_amdgcn_readfirstlane(base_ + qdst));                                            \
+	} while (0)
+
+	LHIP_ISSUE(0);
+	LHIP_ISSUE(1);
+	const int ra0 = wr * 64 + li, ra1 = ra0 + 32;
+	const int qb0 = wq * 64 + li, qb1 = qb0 + 32;
+	for (int st = 0; st < S; ++st) {
+		if (st + 1 < S)
+			LHIP_WAIT_VM(3);  // stage st+1 (3 DMA instructions) may stay in flight
+		else
+			LHIP_WAIT_VM(0);
+		__builtin_amdgcn_s_barrier();
+		asm volatile("" ::: "memory");
+		if (st + 2 < S) LHIP_ISSUE(st + 2);
+		const uint8_t *xs = smem + (st % NSTAGE) * STAGE_BYTES;
+		const uint8_t *qs = xs + XST_BYTES;
+#pragma unroll 1
+		for (int kk = 0; kk < SK / 16; ++kk) {
+			const int ca = 4 * kk + 2 * hi;  // logical 16 B chunk (4 f32) of the A fragment
+			const int cb = 2 * kk + hi;      // logical 16 B chunk (8 bf16) of the B fragment
+			const bf16x8 a0 = ld_afrag(xs, ra0, ca);
+			const bf16x8 a1 = ld_afrag(xs, ra1, ca);
+			const bf16x8 b0 = ld_bfrag(qs, qb0, cb);
+			const bf16x8 b1 = ld_bfrag(qs, qb1, cb);
 			acc00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc00, 0, 0, 0);
 			acc01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc01, 0, 0, 0);
 			acc10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc10, 0, 0, 0);
 			acc11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc11, 0, 0, 0);
 		}
-		__syncthreads();
+		asm volatile("" ::: "memory");
 	}
+#undef LHIP_ISSUE
 
 	// ---- epilogue -------------------------------------------------------------
+	if (tid < BR) {
+		int64_t r = row0 + tid;
+		RA[tid] = (r < n_slots) ? rowaux[r] : make_float4(F_INF, 0.f, 0.f, 0.f);
+	}
+	if (MODE == 1 && tid < BQ) ep_cnt[tid] = 0u;
+	__syncthreads();
 	// lane: query q = q0 + wq*64 + tq*32 + li; register reg of acc<tr><tq> holds
 	// base row wr*64 + tr*32 + (reg&3) + 8*(reg>>2) + 4*hi.
 	const int ql0 = wq * 64 + li, ql1 = ql0 + 32;  // tile-local queries
@@ -402,74 +423,54 @@ __global__ __launch_bounds__(512, 2) void scan_kernel(const float *__restrict__ 
 		return;
 	}
 
-	// append mode, pass A: count survivors per (lane, query) and reserve a
-	// contiguous local range in the tile's per-query LDS counter
+	// append mode.  Survivors (LB <= tau[q]) go to an LDS list in the (now
+	// idle) ring: entry = (ordered key, slot, query, offset within the query's
+	// tile range).  Then one pool reservation per (tile, query), then copy-out.
+	// A list overflow (adversarial data) marks the query so its pool counter
+	// exceeds cap: select then reports the certificate as unknown (fallback).
+	uint4 *list = reinterpret_cast<uint4 *>(smem);
+	constexpr unsigned LIST_CAP = RING_BYTES / 16;
+	unsigned &s_list_n = ep_base[BQ];   // all LDS lives in the one smem array
+	unsigned *s_over = ep_base + BQ + 1;  // BQ/32 overflow bit words
+	if (tid == 0) s_list_n = 0u;
+	if (tid < BQ / 32) s_over[tid] = 0u;
+	__syncthreads();
 	const float t0 = qv0 ? tau[q0 + ql0] : -F_INF;
 	const float t1 = qv1 ? tau[q0 + ql1] : -F_INF;
-	uint32_t m00 = 0, m01 = 0, m10 = 0, m11 = 0;  // survivor bitmasks per accumulator
-#pragma unroll
-	for (int r = 0; r < 16; ++r) {
-		const int rl0 = rb + (r & 3) + 8 * (r >> 2), rl1 = rl0 + 32;
-		const float4 ra0 = RA[rl0], ra1 = RA[rl1];
-		float l;
-		l = lower_bound<METRIC>(acc00[r], ra0, qa0);
-		m00 |= (l <= t0 && l < F_INF) ? (1u << r) : 0u;
-		l = lower_bound<METRIC>(acc10[r], ra1, qa0);
-		m10 |= (l <= t0 && l < F_INF) ? (1u << r) : 0u;
-		l = lower_bound<METRIC>(acc01[r], ra0, qa1);
-		m01 |= (l <= t1 && l < F_INF) ? (1u << r) : 0u;
-		l = lower_bound<METRIC>(acc11[r], ra1, qa1);
-		m11 |= (l <= t1 && l < F_INF) ? (1u << r) : 0u;
-	}
-	const unsigned c0 = __popc(m00) + __popc(m10), c1 = __popc(m01) + __popc(m11);
-	unsigned off0 = 0, off1 = 0;
-	if (c0) off0 = atomicAdd(&ep_cnt[ql0], c0);
-	if (c1) off1 = atomicAdd(&ep_cnt[ql1], c1);
+	const uint32_t slot0 = (uint32_t)(row0 + rb);
+#define LHIP_PUSH(accv, rlo, qa, tt, qloc)                                                                          \
+	do {                                                                                                           \
+		_Pragma("unroll") for (int r = 0; r < 16; ++r) {                                                           \
+			const int rl_ = (rlo) + (r & 3) + 8 * (r >> 2);                                                        \
+			const float l_ = lower_bound<METRIC>(accv[r], RA[rb + rl_], qa);                                       \
+			if (l_ <= (tt) && l_ < F_INF) {                                                                        \
+				const unsigned off_ = atomicAdd(&ep_cnt[qloc], 1u);                                                \
+				const unsigned p_ = atomicAdd(&s_list_n, 1u);                                                      \
+				if (p_ < LIST_CAP)                                                                                 \
+					list[p_] = make_uint4(fkey(l_), slot0 + rl_, (unsigned)(qloc), off_);                          \
+				else                                                                                               \
+					atomicOr(&s_over[(qloc) >> 5], 1u << ((qloc)&31));                                             \
+			}                                                                                                      \
+		}                                                                                                          \
+	} while (0)
+	LHIP_PUSH(acc00, 0, qa0, t0, ql0);
+	LHIP_PUSH(acc10, 32, qa0, t0, ql0);
+	LHIP_PUSH(acc01, 0, qa1, t1, ql1);
+	LHIP_PUSH(acc11, 32, qa1, t1, ql1);
+#undef LHIP_PUSH
 	__syncthreads();
 	// one pool reservation per (tile, query)
 	if (tid < BQ) {
 		const unsigned c = ep_cnt[tid];
-		ep_base[tid] = c ? (unsigned)atomicAdd(&pool_cnt[q0 + tid], (int)c) : 0u;
+		const bool over = (s_over[tid >> 5] >> (tid & 31)) & 1u;
+		ep_base[tid] = c ? (unsigned)atomicAdd(&pool_cnt[q0 + tid], (int)c + (over ? cap + 1 : 0)) : 0u;
 	}
 	__syncthreads();
-	if ((c0 | c1) == 0) return;
-	// pass B: write the survivors
-	const uint32_t slot0 = (uint32_t)(row0 + rb);
-	if (c0) {
-		unsigned pos = ep_base[ql0] + off0;
-		uint2 *dst = pool + (int64_t)(q0 + ql0) * cap;
-#pragma unroll
-		for (int r = 0; r < 16; ++r) {
-			const int rl = (r & 3) + 8 * (r >> 2);
-			if (m00 & (1u << r)) {
-				if (pos < (unsigned)cap)
-					dst[pos] = make_uint2(fkey(lower_bound<METRIC>(acc00[r], RA[rb + rl], qa0)), slot0 + rl);
-				++pos;
-			}
-			if (m10 & (1u << r)) {
-				if (pos < (unsigned)cap)
-					dst[pos] = make_uint2(fkey(lower_bound<METRIC>(acc10[r], RA[rb + 32 + rl], qa0)), slot0 + 32 + rl);
-				++pos;
-			}
-		}
-	}
-	if (c1) {
-		unsigned pos = ep_base[ql1] + off1;
-		uint2 *dst = pool + (int64_t)(q0 + ql1) * cap;
-#pragma unroll
-		for (int r = 0; r < 16; ++r) {
-			const int rl = (r & 3) + 8 * (r >> 2);
-			if (m01 & (1u << r)) {
-				if (pos < (unsigned)cap)
-					dst[pos] = make_uint2(fkey(lower_bound<METRIC>(acc01[r], RA[rb + rl], qa1)), slot0 + rl);
-				++pos;
-			}
-			if (m11 & (1u << r)) {
-				if (pos < (unsigned)cap)
-					dst[pos] = make_uint2(fkey(lower_bound<METRIC>(acc11[r], RA[rb + 32 + rl], qa1)), slot0 + 32 + rl);
-				++pos;
-			}
-		}
+	const unsigned n_list = min(s_list_n, LIST_CAP);
+	for (unsigned i = tid; i < n_list; i += SCAN_THREADS) {
+		const uint4 e = list[i];
+		const unsigned pos = ep_base[e.z] + e.w;
+		if (pos < (unsigned)cap) pool[(int64_t)(q0 + e.z) * cap + pos] = make_uint2(e.x, e.y);
 	}
 }
 
@@ -477,7 +478,7 @@ template <int MODE>
 static void scan_dispatch(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, float *dense,
                           int64_t ld_out, const float *tau, uint2 *pool, int *pool_cnt, int cap, hipStream_t st) {
 	dim3 grid((unsigned)n_tiles, (unsigned)(q.nq_pad / BQ));
-	dim3 block(512);
+	dim3 block(SCAN_THREADS);
 	switch (s.metric) {
 	case METRIC_L2:
 		scan_kernel<METRIC_L2, MODE><<<grid, block, 0, st>>>(s.X, s.rowaux, s.n_slots, s.ld, q.Qb, q.qaux, q.nq,

@@ -189,7 +189,9 @@ struct Index {
 	// grow the device store to hold at least `want` slots (contents preserved)
 	void reserve(int64_t want) {
 		if (want <= cap) return;
-		int64_t c = std::max<int64_t>(want, std::max<int64_t>(4096, cap * 2));
+		// capacity is a multiple of the scan tile and the tail past n_slots is
+		// zero: the scan kernel streams whole tiles without clamping rows
+		int64_t c = round_up(std::max<int64_t>(want, std::max<int64_t>(4096, cap * 2)), SCAN_BR);
 		float *nX = nullptr;
 		float4 *na = nullptr, *na2 = nullptr;
 		int64_t *nl = nullptr;
@@ -205,6 +207,7 @@ struct Index {
 				HIPCHK(hipMemcpyAsync(na2, rowaux_l2, (size_t)n_slots * sizeof(float4), hipMemcpyDeviceToDevice,
 				                      stream));
 		}
+		HIPCHK(hipMemsetAsync(nX + n_slots * ld, 0, (size_t)(c - n_slots) * ld * sizeof(float), stream));
 		HIPCHK(hipStreamSynchronize(stream));
 		if (X) HIPCHK(hipFree(X));
 		if (rowaux) HIPCHK(hipFree(rowaux));
@@ -301,7 +304,7 @@ struct Index {
 		for (int64_t s = 0; s < n_slots; ++s)
 			if (live[(size_t)s]) keep.push_back(s);
 		const int64_t n = (int64_t)keep.size();
-		const int64_t c = std::max<int64_t>(4096, n);
+		const int64_t c = round_up(std::max<int64_t>(4096, n), SCAN_BR);
 		float *nX = nullptr;
 		float4 *na = nullptr, *na2 = nullptr;
 		int64_t *nl = nullptr;
@@ -316,6 +319,7 @@ struct Index {
 			if (rowaux_l2) launch_gather_rows(X, rowaux_l2, dlabels, ws.idx.p, n, ld, nX, na2, nl, stream);
 			HIPCHK(hipGetLastError());
 		}
+		HIPCHK(hipMemsetAsync(nX + n * ld, 0, (size_t)(c - n) * ld * sizeof(float), stream));
 		HIPCHK(hipStreamSynchronize(stream));
 		HIPCHK(hipFree(X));
 		HIPCHK(hipFree(rowaux));
