@@ -108,34 +108,14 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(5678)
     Q = torch.randn((B, D), generator=g, device=dev, dtype=torch.float32)
-    out_l = torch.empty((B, K), dtype=torch.int64, device=dev)
-    out_d = torch.empty((B, K), dtype=torch.float32, device=dev)
-    out_c = torch.empty((B,), dtype=torch.int32, device=dev)
-    if world > 1:
-        gl = torch.empty((world, B, K), dtype=torch.int64, device=dev)
-        gd = torch.empty((world, B, K), dtype=torch.float32, device=dev)
-        gc = torch.empty((world, B), dtype=torch.int32, device=dev)
-        ml = torch.empty((B, K), dtype=torch.int64, device=dev)
-        md = torch.empty((B, K), dtype=torch.float32, device=dev)
-        mc = torch.empty((B,), dtype=torch.int32, device=dev)
+    from lance_hip.sharded import ShardedSearch, hip_device_merge, hip_device_search
+
+    searcher = ShardedSearch(hip_device_search(L, h, D), hip_device_merge(L), label_offset=s0, dist=dist,
+                             world=world)
     torch.cuda.synchronize()
 
     def step():
-        r = L.lance_hip_search_batch_device(h, Q.data_ptr(), B, D, K, 20, 1, out_l.data_ptr(), out_d.data_ptr(),
-                                            out_c.data_ptr(), e, 2048)
-        if r < 0:
-            raise RuntimeError(e.value.decode())
-        if world == 1:
-            return out_l, out_d, out_c
-        out_l.add_(s0)  # shard-local label -> global label (labels are dense, row-range shards)
-        dist.all_gather_into_tensor(gl, out_l)
-        dist.all_gather_into_tensor(gd, out_d)
-        dist.all_gather_into_tensor(gc, out_c)
-        r = L.lance_hip_merge_topk_device(world, B, K, gl.data_ptr(), gd.data_ptr(), gc.data_ptr(), ml.data_ptr(),
-                                          md.data_ptr(), mc.data_ptr(), e, 2048)
-        if r < 0:
-            raise RuntimeError(e.value.decode())
-        return ml, md, mc
+        return searcher.search(Q, K)
 
     for _ in range(a.warmup):
         step()

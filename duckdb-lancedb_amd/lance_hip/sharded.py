@@ -1,0 +1,110 @@
+"""Row-sharded search over several GPUs.
+
+The base of one LANCE index is split into contiguous row ranges, one per rank
+(one process per GPU).  Because the reference's labels are dense consecutive
+integers (``rust_lib/src/lance_manager.rs:232-233``), shard ``r`` holding
+global rows ``[s0, s1)`` stores them under local labels ``[0, s1-s0)`` and the
+global label is ``s0 + local`` — no id translation table.  Every rank searches
+its shard for the same query batch; the per-shard top-k lists are exchanged by
+ONE all-gather (RCCL over xGMI on GPUs, gloo in CPU tests) and merged on the
+device by ``lance_hip_merge_topk_device`` under the (distance, label) order.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Tuple
+
+
+def shard_range(n_total: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous, balanced row range of ``rank`` (sizes differ by at most 1)."""
+    return rank * n_total // world, (rank + 1) * n_total // world
+
+
+class ShardedSearch:
+    """One rank's view of a sharded index.
+
+    ``local_search(Q, k) -> (labels[nq,k] int64, dists[nq,k] f32, counts[nq] i32)``
+    searches this rank's shard (local labels).  ``merge(gl, gd, gc) -> same``
+    merges ``world`` gathered lists; ``dist`` is ``torch.distributed`` (or None
+    for a single shard).  Tensors may live on the GPU (RCCL) or the CPU (gloo).
+    """
+
+    def __init__(self, local_search: Callable, merge: Callable, label_offset: int, dist=None,
+                 world: int = 1):
+        self.local_search = local_search
+        self.merge = merge
+        self.label_offset = int(label_offset)
+        self.dist = dist
+        self.world = int(world)
+        self._bufs = None
+
+    def _gather_bufs(self, like_l, like_d, like_c):
+        import torch
+
+        # flat [world * n, ...] outputs: the layout both RCCL and gloo accept
+        key = (tuple(like_l.shape), like_l.device)
+        if self._bufs is None or self._bufs[0] != key:
+            gl = torch.empty((self.world * like_l.shape[0],) + tuple(like_l.shape[1:]), dtype=like_l.dtype,
+                             device=like_l.device)
+            gd = torch.empty((self.world * like_d.shape[0],) + tuple(like_d.shape[1:]), dtype=like_d.dtype,
+                             device=like_d.device)
+            gc = torch.empty((self.world * like_c.shape[0],), dtype=like_c.dtype, device=like_c.device)
+            self._bufs = (key, gl, gd, gc)
+        return self._bufs[1:]
+
+    def search(self, Q, k: int):
+        lab, dis, cnt = self.local_search(Q, k)
+        if self.world == 1:
+            return lab, dis, cnt
+        # local -> global labels (unused slots stay -1)
+        import torch
+
+        lab = torch.where(lab >= 0, lab + self.label_offset, lab)  # no host sync
+        gl, gd, gc = self._gather_bufs(lab, dis, cnt)
+        self.dist.all_gather_into_tensor(gl, lab.contiguous())
+        self.dist.all_gather_into_tensor(gd, dis.contiguous())
+        self.dist.all_gather_into_tensor(gc, cnt.contiguous())
+        nq = lab.shape[0]
+        return self.merge(gl.view(self.world, nq, -1), gd.view(self.world, nq, -1), gc.view(self.world, nq))
+
+
+def hip_device_merge(lib, err_len: int = 2048):
+    """The product merge: ``lance_hip_merge_topk_device`` on the current device."""
+    import ctypes
+
+    import torch
+
+    def merge(gl, gd, gc):
+        world, nq, k = gl.shape
+        ol = torch.empty((nq, k), dtype=torch.int64, device=gl.device)
+        od = torch.empty((nq, k), dtype=torch.float32, device=gl.device)
+        oc = torch.empty((nq,), dtype=torch.int32, device=gl.device)
+        e = ctypes.create_string_buffer(err_len)
+        r = lib.lance_hip_merge_topk_device(world, nq, k, gl.data_ptr(), gd.data_ptr(), gc.data_ptr(),
+                                            ol.data_ptr(), od.data_ptr(), oc.data_ptr(), e, err_len)
+        if r < 0:
+            raise RuntimeError(e.value.decode())
+        return ol, od, oc
+
+    return merge
+
+
+def hip_device_search(lib, handle, dim: int, nprobes: int = 20, refine_factor: int = 1, err_len: int = 2048):
+    """The product shard search: ``lance_hip_search_batch_device`` (inputs in HBM)."""
+    import ctypes
+
+    import torch
+
+    def search(Q, k):
+        nq = Q.shape[0]
+        ol = torch.empty((nq, k), dtype=torch.int64, device=Q.device)
+        od = torch.empty((nq, k), dtype=torch.float32, device=Q.device)
+        oc = torch.empty((nq,), dtype=torch.int32, device=Q.device)
+        e = ctypes.create_string_buffer(err_len)
+        torch.cuda.current_stream().synchronize()
+        r = lib.lance_hip_search_batch_device(handle, Q.data_ptr(), nq, dim, k, nprobes, refine_factor,
+                                              ol.data_ptr(), od.data_ptr(), oc.data_ptr(), e, err_len)
+        if r < 0:
+            raise RuntimeError(e.value.decode())
+        return ol, od, oc
+
+    return search

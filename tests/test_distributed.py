@@ -1,0 +1,151 @@
+"""Multi-rank sharded search, world_size 2-3 over gloo.
+
+CPU tests: the exchange/merge logic of ``lance_hip.sharded`` with the oracle as
+each rank's shard searcher and a reference merge; the result on every rank must
+equal the unsharded oracle.  GPU test: two ranks on one device, each searching
+its shard through the C-ABI, gathered over gloo, merged by the HIP merge kernel.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from lance_hip.sharded import ShardedSearch, shard_range
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def ref_merge(gl, gd, gc):
+    """Reference merge under the (distance, label) order (test-side, numpy)."""
+    world, nq, k = gl.shape
+    ol = torch.full((nq, k), -1, dtype=torch.int64)
+    od = torch.full((nq, k), float("nan"), dtype=torch.float32)
+    oc = torch.zeros(nq, dtype=torch.int32)
+    for q in range(nq):
+        items = []
+        for s in range(world):
+            for i in range(int(gc[s, q])):
+                items.append((float(gd[s, q, i]), int(gl[s, q, i])))
+        items.sort()
+        items = items[:k]
+        oc[q] = len(items)
+        for i, (d, l) in enumerate(items):
+            ol[q, i] = l
+            od[q, i] = d
+    return ol, od, oc
+
+
+def _cpu_worker(rank, world, port, n, d, k, q, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from oracle import flat_knn
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(7)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Q = rng.standard_normal((q, d)).astype(np.float32)
+    s0, s1 = shard_range(n, world, rank)
+    Xs = X[s0:s1]
+
+    def local_search(Qt, kk):
+        l, dd, c = flat_knn.flat_search_batch(Xs, np.arange(s1 - s0), np.ones(s1 - s0, bool), Qt.numpy(), kk)
+        return torch.from_numpy(l), torch.from_numpy(dd), torch.from_numpy(c)
+
+    s = ShardedSearch(local_search, ref_merge, label_offset=s0, dist=dist, world=world)
+    l, dd, c = s.search(torch.from_numpy(Q), k)
+    out[rank] = (l.numpy(), dd.numpy(), c.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 1000), (3, 1001)])
+def test_sharded_merge_equals_unsharded_cpu(world, n):
+    from oracle import flat_knn
+
+    d, k, q = 8, 6, 5
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_cpu_worker, args=(world, _free_port(), n, d, k, q, out), nprocs=world, join=True)
+    rng = np.random.default_rng(7)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Q = rng.standard_normal((q, d)).astype(np.float32)
+    el, ed, ec = flat_knn.flat_search_batch(X, np.arange(n), np.ones(n, bool), Q, k)
+    for r in range(world):
+        l, dd, c = out[r]
+        np.testing.assert_array_equal(l, el)
+        np.testing.assert_array_equal(c, ec)
+        np.testing.assert_allclose(dd, ed, rtol=1e-6)
+
+
+def test_shard_range_partitions_exactly():
+    for n in (0, 1, 7, 1000, 1_000_000):
+        for world in (1, 2, 3, 8):
+            rs = [shard_range(n, world, r) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            for (a0, a1), (b0, b1) in zip(rs, rs[1:]):
+                assert a1 == b0
+            sizes = [b - a for a, b in rs]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def _gpu_worker(rank, world, port, n, d, k, q, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    import lance_hip
+    from lance_hip.sharded import hip_device_merge, hip_device_search
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    L = lance_hip.lib()
+    rng = np.random.default_rng(11)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Q = rng.standard_normal((q, d)).astype(np.float32)
+    s0, s1 = shard_range(n, world, rank)
+    h = lance_hip.LanceCreateDetached("", d, "l2", f"shard{rank}")
+    lance_hip.LanceDetachedAddBatch(h, X[s0:s1], s1 - s0, d)
+    dev_search = hip_device_search(L, h, d)
+    dev_merge = hip_device_merge(L)
+
+    def local_search(Qt, kk):  # GPU search, results moved to the CPU for gloo
+        l, dd, c = dev_search(Qt.cuda(), kk)
+        return l.cpu(), dd.cpu(), c.cpu()
+
+    def merge(gl, gd, gc):  # HIP merge kernel on the device
+        l, dd, c = dev_merge(gl.cuda(), gd.cuda(), gc.cuda())
+        return l.cpu(), dd.cpu(), c.cpu()
+
+    s = ShardedSearch(local_search, merge, label_offset=s0, dist=dist, world=world)
+    l, dd, c = s.search(torch.from_numpy(Q), k)
+    out[rank] = (l.numpy(), dd.numpy(), c.numpy())
+    lance_hip.LanceFreeDetached(h)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_hip_search_two_ranks_one_gpu():
+    from oracle import flat_knn
+
+    world, n, d, k, q = 2, 90_000, 64, 10, 40   # 45k rows per shard: dense path on each
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_gpu_worker, args=(world, _free_port(), n, d, k, q, out), nprocs=world, join=True)
+    rng = np.random.default_rng(11)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Q = rng.standard_normal((q, d)).astype(np.float32)
+    el, ed, ec = flat_knn.flat_search_batch(X, np.arange(n), np.ones(n, bool), Q, k)
+    for r in range(world):
+        l, dd, c = out[r]
+        np.testing.assert_array_equal(l, el)
+        np.testing.assert_allclose(dd, ed, rtol=1e-4, atol=1e-5)
