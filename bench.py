@@ -69,6 +69,24 @@ def gen_rows(start, stop, dim, device, seed=1234):
     return out
 
 
+def measured_traffic(n, dim, batch):
+    """Per-launch HBM bytes of the scan kernel from the committed rocprofv3 PMC
+    passes (profiles/*_scan_traffic.json, made by tools/pmc_traffic.py from
+    separate FETCH_SIZE / WRITE_SIZE runs of this bench) for the same shape."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_scan_traffic.json"))):
+        try:
+            with open(f) as fh:
+                t = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if (t.get("n"), t.get("dim"), t.get("batch")) == (n, dim, batch):
+            best = t
+    return None if best is None else int(best["traffic_bytes_per_launch"])
+
+
 def err_buf():
     return ctypes.create_string_buffer(2048)
 
@@ -182,8 +200,9 @@ def main():
             avg_ms = kt["scan_ms_total"] / kt["scan_launches"]
             bytes_launch = kt["scan_rows"] * (ld * 4 + 16) + kt["scan_qpad"] * ld * 2
             ach = bytes_launch / (avg_ms * 1e-3) / 1e9
+            traffic = measured_traffic(N // world, D, B)
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "scan_kernel<L2,append>",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "scan_kernel<L2,append>",
                     "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(bytes_launch)}
         line = {
             "metric": "kNN queries/sec + recall@10, 1Mx768 f32 flat; GB/s vs HBM roofline",
