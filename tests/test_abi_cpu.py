@@ -107,3 +107,16 @@ def test_arrow_paths_report_unsupported():
 def test_create_without_gpu_fails_cleanly():
     with pytest.raises(lance_hip.IOException, match="no HIP device"):
         lance_hip.LanceCreateDetached("", 3, "l2", "vectors")
+
+
+def test_cpp_caller_links_against_library(tmp_path):
+    """A C++ caller with the reference's extern "C" declarations (rust_ffi.cpp:7-42)
+    compiles, links against liblancedb_hip.so and runs (no GPU needed)."""
+    src = os.path.join(ROOT, "tests", "cpp", "abi_caller.cpp")
+    exe = str(tmp_path / "abi_caller")
+    libdir = os.path.dirname(lance_hip.LIB_PATH)
+    subprocess.run(["g++", "-std=c++17", "-O1", src, "-o", exe, f"-L{libdir}", "-llancedb_hip",
+                    f"-Wl,-rpath,{libdir}"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.strip().endswith("OK")
