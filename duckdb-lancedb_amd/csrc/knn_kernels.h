@@ -48,6 +48,9 @@ struct QueryView {
 void launch_rowaux(const float *X, int ld, int dim, int metric, int64_t s0, int64_t n, float4 *rowaux,
                    unsigned *stats, hipStream_t st);
 
+// rowaux[from, to) = (+inf, 0, 0, 0): padding rows past the last slot.
+void launch_fill_rowaux(float4 *rowaux, int64_t from, int64_t to, hipStream_t st);
+
 // Marks the listed slots dead (rowaux.x = +inf).
 void launch_tombstone(float4 *rowaux, const int64_t *slots, int n, hipStream_t st);
 
@@ -60,19 +63,27 @@ void launch_prep_queries(const float *Q, int nq, int dim, int ld, int nq_pad, in
 void launch_scan_dense(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, float *out,
                        int64_t ld_out, hipStream_t st);
 
-// Threshold scan over all rows: append (orderedkey(LB), slot) for LB <= tau[q]
-// into pool[q][0..cap); pool_cnt[q] counts every pass (may exceed cap).
-void launch_scan_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *pool, int *pool_cnt,
-                        int cap, hipStream_t st);
+// Threshold scan over all rows (persistent: scan_grid(n_tiles) workgroups):
+// workgroup g appends (orderedkey(LB), slot) for LB <= tau[q] into its own
+// segment seg_pool[(g*nq + q)*seg_cap ..], count in seg_cnt[g*nq + q] (may
+// exceed seg_cap: overflow is reported by select).
+void launch_scan_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
+                        int seg_cap, hipStream_t st);
 
-// Per-query top-M selection by LB.  Source is either a dense LB matrix
-// (dense != null: n_entries per query, entry i -> slot (i/BR)*stride*BR + i%BR)
-// or the append pools.  Writes cand_slot[q][0..M), cand_cnt[q] and the cut
-// cut[q] = a lower bound on the true distance of every live row not selected
-// (+inf when nothing live was left out; -inf when unknown -> certificate fails).
-void launch_select(const float *dense, int64_t ld_dense, int64_t n_entries, int64_t tile_stride,
-                   const uint2 *pool, const int *pool_cnt, int cap, const float *tau, int nq, int M,
-                   uint32_t *cand_slot, int *cand_cnt, float *cut, hipStream_t st);
+// Workgroups a scan over n_tiles tiles launches (= min(n_tiles, CUs)).
+int scan_grid(int64_t n_tiles);
+
+// Per-query top-M selection by LB.  Writes cand_slot[q][0..M), cand_cnt[q] and
+// the cut cut[q] = a lower bound on the true distance of every live row not
+// selected (+inf when nothing live was left out; -inf when unknown -> the
+// certificate fails).  Dense source: n_entries per query, entry i -> slot
+// (i/BR)*stride*BR + i%BR.  Segment source: the append scan's output;
+// pool_total[q] = entries seen (-1 on overflow).
+void launch_select_dense(const float *dense, int64_t ld_dense, int64_t n_entries, int64_t tile_stride, int nq, int M,
+                         uint32_t *cand_slot, int *cand_cnt, float *cut, hipStream_t st);
+void launch_select_segments(const uint2 *seg_pool, const int *seg_cnt, int seg_cap, int n_seg, const float *tau,
+                            int nq, int M, uint32_t *cand_slot, int *cand_cnt, float *cut, int *pool_total,
+                            hipStream_t st);
 
 // Exact distances (f64 accumulation, rounded to f32) of the candidates.
 void launch_refine(const StoreView &s, const QueryView &q, const uint32_t *cand_slot, const int *cand_cnt, int M,

@@ -23,6 +23,7 @@
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 
@@ -120,6 +121,16 @@ void launch_rowaux(const float *X, int ld, int dim, int metric, int64_t s0, int6
 	rowaux_kernel<<<dim3((unsigned)blocks), dim3(256), 0, st>>>(X, ld, dim, metric, s0, n, rowaux, stats);
 }
 
+__global__ void fill_rowaux_kernel(float4 *rowaux, int64_t from, int64_t to) {
+	const int64_t i = from + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < to) rowaux[i] = make_float4(F_INF, 0.f, 0.f, 0.f);
+}
+
+void launch_fill_rowaux(float4 *rowaux, int64_t from, int64_t to, hipStream_t st) {
+	if (to <= from) return;
+	fill_rowaux_kernel<<<dim3((unsigned)((to - from + 255) / 256)), dim3(256), 0, st>>>(rowaux, from, to);
+}
+
 __global__ void tombstone_kernel(float4 *rowaux, const int64_t *slots, int n) {
 	int i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i < n) rowaux[slots[i]].x = F_INF;
@@ -209,28 +220,46 @@ void launch_prep_queries(const float *Q, int nq, int dim, int ld, int nq_pad, in
 constexpr int BR = SCAN_BR, BQ = SCAN_BQ, BK = SCAN_BK;
 
 // ---------------------------------------------------------------------------
-// scan kernel (LDS-DMA ring)
+// scan kernel (persistent, LDS-DMA ring)
 //
-// Workgroup = 1024 threads = 16 waves laid out 4 (base rows) x 4 (queries);
-// each wave owns a 64-row x 64-query sub-tile = 2x2 v_mfma_f32_32x32x16_bf16
-// tiles (A = base rows, B = queries: accumulator column = lane&31 = query,
-// the 16 registers walk base rows).  Tile = 256 base rows x 256 queries, one
-// workgroup (4 waves per SIMD) per CU: every base byte crosses HBM once and
-// the query tile (L2-resident) costs half a byte per base byte.
+// Tile = 256 base rows x 256 queries.  Workgroup = 1024 threads = 16 waves laid
+// out 4 (base rows) x 4 (queries); each wave owns a 64-row x 64-query sub-tile
+// = 2x2 v_mfma_f32_32x32x16_bf16 tiles (A = base rows, B = queries:
+// accumulator column = lane&31 = query, the 16 registers walk base rows).
+// One workgroup per CU; it walks tiles blockIdx.x, +gridDim.x, ... and the
+// k-stream never stops at a tile boundary: stages of the next tile are
+// already in flight while the current tile's epilogue runs.
 //
 // The k dimension streams through a ring of NSTAGE LDS stages of SK = 32:
 //   X stage: 256 rows x 32 f32 (32 KiB) straight from HBM by
 //            global_load_lds_dwordx4 (no VGPR staging), rows 128 B,
 //            16 B chunk c of row r stored at c ^ ((r>>1)&7);
 //   Q stage: 256 queries x 32 bf16 (16 KiB) from L2, rows 64 B,
-//            chunk c of row r stored at c ^ ((r>>2)&3).
+//            chunk c of row r stored at c ^ ((r>>2)&3);
+//   with stage 0 of a tile: the tile's 256 row-aux float4 (4 KiB, 2 slots).
 // LDS-DMA writes lane-linear, so the swizzle is applied on the per-lane SOURCE
 // address and undone on the ds_read_b128 fragment reads (conflict-free for
 // the b128 lane groups).  A fragments are converted f32 -> bf16 after the read.
-// Per stage each thread issues 3 DMA instructions; NSTAGE-1 stages stay in
-// flight; one raw s_barrier per stage behind a counted s_waitcnt vmcnt.
-// The store is zero-padded to a multiple of BR rows, so no row is clamped.
+// NSTAGE-1 stages stay in flight; one raw s_barrier per stage behind a counted
+// s_waitcnt vmcnt.  The store is zero-padded (rows) and +inf-padded (row aux)
+// to a multiple of BR rows, so no row is clamped.
+//
+// Epilogue per tile: each accumulator becomes a rigorous lower bound of the
+// exact distance (4 FMAs).  Dense mode stores it.  Append mode keeps (LB, slot)
+// when LB <= tau[q] in the workgroup's private segment for q: the position
+// comes from an LDS counter, the store is fire-and-forget — no global atomic,
+// no barrier, nothing that would drain the DMA queue.
 // ---------------------------------------------------------------------------
+// development-only ablation switches (timing experiments; results are wrong when set)
+#ifndef LHIP_ABL_NO_Q
+#define LHIP_ABL_NO_Q 0
+#endif
+#ifndef LHIP_ABL_NO_MFMA
+#define LHIP_ABL_NO_MFMA 0
+#endif
+#ifndef LHIP_ABL_NO_EPILOGUE
+#define LHIP_ABL_NO_EPILOGUE 0
+#endif
 constexpr int SCAN_THREADS = 1024;
 constexpr int SK = 32;
 constexpr int NSTAGE = 3;
@@ -238,14 +267,15 @@ constexpr int XST_BYTES = BR * SK * 4;                 // 32 KiB
 constexpr int QST_BYTES = BQ * SK * 2;                 // 16 KiB
 constexpr int STAGE_BYTES = XST_BYTES + QST_BYTES;     // 48 KiB
 constexpr int RING_BYTES = NSTAGE * STAGE_BYTES;       // 144 KiB
-constexpr int RA_BYTES = BR * 16;
-constexpr int EP_BYTES = BQ * 8 + 64;  // per-query counters + pool bases + list counter + overflow bits
-constexpr int SCAN_LDS = RING_BYTES + RA_BYTES + EP_BYTES;
+constexpr int RA_SLOT = BR * 16;                       // 4 KiB
+constexpr int RA_BYTES = 2 * RA_SLOT;
+constexpr int CNT_BYTES = BQ * 4;
+constexpr int QA_BYTES = BQ * 16 + BQ * 4;             // per-query bound constants + tau
+constexpr int SCAN_LDS = RING_BYTES + RA_BYTES + CNT_BYTES + QA_BYTES;
 static_assert(SCAN_LDS <= 160 * 1024, "LDS budget");
 static_assert(XST_BYTES / 1024 == 2 * (SCAN_THREADS / 64), "2 X DMA instructions per wave per stage");
 static_assert(QST_BYTES / 1024 == SCAN_THREADS / 64, "1 Q DMA instruction per wave per stage");
-
-typedef __attribute__((address_space(3))) void lds_void;
+static_assert(RA_SLOT / 1024 == 4, "row aux: one DMA instruction on waves 0..3");
 
 template <int METRIC>
 __device__ __forceinline__ float lower_bound(float s, float4 ra, float4 qa) {
@@ -265,6 +295,18 @@ __device__ __forceinline__ float lower_bound(float s, float4 ra, float4 qa) {
 // M0 is written here and nowhere else in the kernel.
 __device__ __forceinline__ void dma16(const void *g, uint32_t lds_addr) {
 	asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_addr), "v"(g) : "memory", "m0");
+}
+// saddr form: wave-uniform 64-bit base in SGPRs + 32-bit per-lane byte offset
+// (no 64-bit per-lane address registers)
+__device__ __forceinline__ void dma16s(const void *sbase, uint32_t voff, uint32_t lds_addr) {
+	// readfirstlane returns int: go through uint32_t so the low word is not
+	// sign-extended into the high word of the address
+	const uint64_t b = (uint64_t)(uintptr_t)sbase;
+	const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+	const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32));
+	const uint64_t ub = ((uint64_t)hi << 32) | (uint64_t)lo;
+	asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds_addr), "v"(voff), "s"(ub)
+	             : "memory", "m0");
 }
 
 __device__ __forceinline__ bf16x8 ld_afrag(const uint8_t *xs, int r, int c) {
@@ -291,36 +333,71 @@ __device__ __forceinline__ bf16x8 ld_bfrag(const uint8_t *qs, int r, int c) {
 
 template <int METRIC, int MODE>
 __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(const float *__restrict__ X,
-                                                            const float4 *__restrict__ rowaux, int64_t n_slots, int ld,
+                                                            const float4 *__restrict__ rowaux, int ld,
                                                             const uint16_t *__restrict__ Qb,
-                                                            const float4 *__restrict__ qaux, int nq,
-                                                            int64_t tile_stride, float *__restrict__ dense,
+                                                            const float4 *__restrict__ qaux, int nq, int n_tiles,
+                                                            int tile_stride, float *__restrict__ dense,
                                                             int64_t ld_out, const float *__restrict__ tau,
-                                                            uint2 *__restrict__ pool, int *__restrict__ pool_cnt,
-                                                            int cap) {
+                                                            uint2 *__restrict__ seg_pool, int *__restrict__ seg_cnt,
+                                                            int seg_cap) {
 	__shared__ __attribute__((aligned(16))) uint8_t smem[SCAN_LDS];
-	float4 *RA = reinterpret_cast<float4 *>(smem + RING_BYTES);
-	unsigned *ep_cnt = reinterpret_cast<unsigned *>(smem + RING_BYTES + RA_BYTES);
-	unsigned *ep_base = ep_cnt + BQ;
+	unsigned *CNT = reinterpret_cast<unsigned *>(smem + RING_BYTES + RA_BYTES);
+	float4 *QA = reinterpret_cast<float4 *>(smem + RING_BYTES + RA_BYTES + CNT_BYTES);
+	float *TAU = reinterpret_cast<float *>(smem + RING_BYTES + RA_BYTES + CNT_BYTES + BQ * 16);
 
 	const int tid = threadIdx.x;
 	const int lane = tid & 63;
-	const int w = tid >> 6;
+	const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR math
 	const int wr = w & 3, wq = w >> 2;
 	const int li = lane & 31, hi = lane >> 5;
-	const int64_t row0 = (int64_t)blockIdx.x * tile_stride * BR;
 	const int q0 = blockIdx.y * BQ;
+	const int S = ld / SK;  // >= 2 (ld is a multiple of 64)
+	const int my_tiles = (n_tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+	const int G = my_tiles * S;
+
+	// per-query constants of this query tile -> LDS (read in the epilogues)
+	if (tid < BQ) {
+		const int q = q0 + tid;
+		QA[tid] = qaux[q];
+		TAU[tid] = (MODE == 1 && q < nq) ? tau[q] : -F_INF;
+		if (MODE == 1) CNT[tid] = 0u;
+	}
+	LHIP_WAIT_VM(0);  // the ordinary loads above, before any counted DMA wait
+	__syncthreads();
 
 	// DMA sources.  X: wave instruction j (0,1) covers rows (2w+j)*8 + lane/8,
 	// physical 16 B chunk lane%8 (logical chunk = physical ^ ((row>>1)&7)).
 	// Q: one instruction covers queries w*16 + lane/4, physical chunk lane%4.
+	// Row aux (stage 0 only): waves 0..3, rows w*64 + lane.
+	// per-lane byte offsets (32-bit); the tile / stage base is wave-uniform
 	const int xr0 = (2 * w) * 8 + (lane >> 3), xr1 = xr0 + 8;
-	const float *xsrc0 = X + (row0 + xr0) * ld + (((lane & 7) ^ ((xr0 >> 1) & 7)) << 2);
-	const float *xsrc1 = X + (row0 + xr1) * ld + (((lane & 7) ^ ((xr1 >> 1) & 7)) << 2);
+	const uint32_t xoff0 = (uint32_t)(xr0 * ld + (((lane & 7) ^ ((xr0 >> 1) & 7)) << 2)) * 4u;
+	const uint32_t xoff1 = (uint32_t)(xr1 * ld + (((lane & 7) ^ ((xr1 >> 1) & 7)) << 2)) * 4u;
 	const int qr = w * 16 + (lane >> 2);
-	const uint16_t *qsrc = Qb + (int64_t)(q0 + qr) * ld + (((lane & 3) ^ ((qr >> 2) & 3)) << 3);
-	const int xdst0 = (2 * w) * 1024, xdst1 = xdst0 + 1024;
-	const int qdst = XST_BYTES + w * 1024;
+	const uint32_t qoff = (uint32_t)(qr * ld + (((lane & 3) ^ ((qr >> 2) & 3)) << 3)) * 2u;
+	const uint16_t *qbase = Qb + (int64_t)q0 * ld;
+	const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
+
+	auto issue = [&](int ti, int st, int slot) {
+		const int64_t row0 = (int64_t)((int)blockIdx.x + ti * (int)gridDim.x) * tile_stride * BR;
+		const uint32_t base = lds0 + (uint32_t)slot * STAGE_BYTES;
+		if (st == 0 && w < 4) {
+			// lane id rematerialised here instead of kept live across the loop
+			uint32_t ln;
+			asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+			dma16s(rowaux + row0 + w * 64, ln * 16u,
+			       __builtin_amdgcn_readfirstlane(lds0 + RING_BYTES + (uint32_t)(ti & 1) * RA_SLOT + w * 1024));
+		}
+		const float *xt = X + row0 * ld + st * SK;
+		dma16s(xt, xoff0, __builtin_amdgcn_readfirstlane(base + (2 * w) * 1024));
+		dma16s(xt, xoff1, __builtin_amdgcn_readfirstlane(base + (2 * w + 1) * 1024));
+		if (!LHIP_ABL_NO_Q) dma16s(qbase + st * SK, qoff, __builtin_amdgcn_readfirstlane(base + XST_BYTES + w * 1024));
+	};
+
+	const int ql0 = wq * 64 + li, ql1 = ql0 + 32;  // tile-local queries of this lane
+	const int rb = wr * 64 + 4 * hi;                // + tr*32 + 8g + j
+	const int ra0 = wr * 64 + li, ra1 = ra0 + 32;
+	const int qb0 = wq * 64 + li, qb1 = qb0 + 32;
 
 	f32x16 acc00, acc01, acc10, acc11;
 #pragma unroll
@@ -331,30 +408,40 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(const float *__restr
 		acc11[r] = 0.f;
 	}
 
-	const int S = ld / SK;  // >= 2 (ld is a multiple of 64)
-	const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
-#define LHIP_ISSUE(st_)                                                                                             \
-	do {                                                                                                            \
-		const uint32_t base_ = lds0 + ((st_) % NSTAGE) * STAGE_BYTES;                                               \
-		const int ko_ = (st_) * SK;                                                                                 \
-		dma16(xsrc0 + ko_, __builtin_amdgcn_readfirstlane(base_ + xdst0));                                          \
-		dma16(xsrc1 + ko_, __builtin_amdgcn_readfirstlane(base_ + xdst1));                                          \
-		dma16(qsrc + ko_, __builtin_amdgcn_readfirstlane(base_ + qdst));                                            \
-	} while (0)
-
-	LHIP_ISSUE(0);
-	LHIP_ISSUE(1);
-	const int ra0 = wr * 64 + li, ra1 = ra0 + 32;
-	const int qb0 = wq * 64 + li, qb1 = qb0 + 32;
-	for (int st = 0; st < S; ++st) {
-		if (st + 1 < S)
-			LHIP_WAIT_VM(3);  // stage st+1 (3 DMA instructions) may stay in flight
-		else
+	// issue cursor (tile, stage) runs two stages ahead of the compute cursor
+	int iss_t = 0, iss_s = 0;
+	auto advance_issue = [&]() {
+		if (++iss_s == S) {
+			iss_s = 0;
+			++iss_t;
+		}
+	};
+	issue(iss_t, iss_s, 0);
+	advance_issue();
+	if (G > 1) {
+		issue(iss_t, iss_s, 1);
+		advance_issue();
+	}
+	int cur_t = 0, cur_s = 0, slot = 0, iss_slot = 2;
+	for (int g = 0; g < G; ++g) {
+		if (g + 1 < G) {
+			// this wave's DMA instructions of stage g+1 may stay in flight
+			const bool next_has_ra = (cur_s + 1 == S) && w < 4;
+			if (next_has_ra)
+				LHIP_WAIT_VM(4);
+			else
+				LHIP_WAIT_VM(3);
+		} else {
 			LHIP_WAIT_VM(0);
+		}
 		__builtin_amdgcn_s_barrier();
 		asm volatile("" ::: "memory");
-		if (st + 2 < S) LHIP_ISSUE(st + 2);
-		const uint8_t *xs = smem + (st % NSTAGE) * STAGE_BYTES;
+		if (g + 2 < G) {
+			issue(iss_t, iss_s, iss_slot);
+			advance_issue();
+			iss_slot = iss_slot == NSTAGE - 1 ? 0 : iss_slot + 1;
+		}
+		const uint8_t *xs = smem + slot * STAGE_BYTES;
 		const uint8_t *qs = xs + XST_BYTES;
 #pragma unroll 1
 		for (int kk = 0; kk < SK / 16; ++kk) {
@@ -364,134 +451,147 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(const float *__restr
 			const bf16x8 a1 = ld_afrag(xs, ra1, ca);
 			const bf16x8 b0 = ld_bfrag(qs, qb0, cb);
 			const bf16x8 b1 = ld_bfrag(qs, qb1, cb);
-			acc00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc00, 0, 0, 0);
-			acc01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc01, 0, 0, 0);
-			acc10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc10, 0, 0, 0);
-			acc11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc11, 0, 0, 0);
+			if (LHIP_ABL_NO_MFMA) {
+				asm volatile("" ::"v"(a0), "v"(a1), "v"(b0), "v"(b1));
+			} else {
+				acc00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc00, 0, 0, 0);
+				acc01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc01, 0, 0, 0);
+				acc10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc10, 0, 0, 0);
+				acc11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc11, 0, 0, 0);
+			}
 		}
 		asm volatile("" ::: "memory");
-	}
-#undef LHIP_ISSUE
+		slot = slot == NSTAGE - 1 ? 0 : slot + 1;
+		if (++cur_s != S) continue;
+		cur_s = 0;
+		const int ti = cur_t++;
 
-	// ---- epilogue -------------------------------------------------------------
-	if (tid < BR) {
-		int64_t r = row0 + tid;
-		RA[tid] = (r < n_slots) ? rowaux[r] : make_float4(F_INF, 0.f, 0.f, 0.f);
-	}
-	if (MODE == 1 && tid < BQ) ep_cnt[tid] = 0u;
-	__syncthreads();
-	// lane: query q = q0 + wq*64 + tq*32 + li; register reg of acc<tr><tq> holds
-	// base row wr*64 + tr*32 + (reg&3) + 8*(reg>>2) + 4*hi.
-	const int ql0 = wq * 64 + li, ql1 = ql0 + 32;  // tile-local queries
-	const bool qv0 = q0 + ql0 < nq, qv1 = q0 + ql1 < nq;
-	const float4 qa0 = qaux[q0 + ql0];
-	const float4 qa1 = qaux[q0 + ql1];
-	const int rb = wr * 64 + 4 * hi;  // + tr*32 + 8g + j
-
-	if (MODE == 0) {
+		// ---- epilogue of tile ti (its row aux landed with its stage 0) ------
+		const int64_t tile = (int64_t)blockIdx.x + (int64_t)ti * gridDim.x;
+		const int64_t row0 = tile * tile_stride * BR;
+		const float4 *RA = reinterpret_cast<const float4 *>(smem + RING_BYTES + (ti & 1) * RA_SLOT);
+		const float4 qa0 = QA[ql0], qa1 = QA[ql1];
+		if (LHIP_ABL_NO_EPILOGUE) {
+			if (acc00[0] == 12345.f && acc11[3] == 54321.f && acc01[1] == acc10[2]) seg_cnt[0] = 1;
+		} else if (MODE == 0) {
+			const bool qv0 = q0 + ql0 < nq, qv1 = q0 + ql1 < nq;
 #pragma unroll
-		for (int g = 0; g < 4; ++g) {
-			const int r0 = rb + 8 * g, r1 = rb + 32 + 8 * g;
-			float4 o;
-			if (qv0) {
-				float *dst = dense + (int64_t)(q0 + ql0) * ld_out + (int64_t)blockIdx.x * BR;
-				o = make_float4(lower_bound<METRIC>(acc00[4 * g + 0], RA[r0 + 0], qa0),
-				                lower_bound<METRIC>(acc00[4 * g + 1], RA[r0 + 1], qa0),
-				                lower_bound<METRIC>(acc00[4 * g + 2], RA[r0 + 2], qa0),
-				                lower_bound<METRIC>(acc00[4 * g + 3], RA[r0 + 3], qa0));
-				*reinterpret_cast<float4 *>(dst + r0) = o;
-				o = make_float4(lower_bound<METRIC>(acc10[4 * g + 0], RA[r1 + 0], qa0),
-				                lower_bound<METRIC>(acc10[4 * g + 1], RA[r1 + 1], qa0),
-				                lower_bound<METRIC>(acc10[4 * g + 2], RA[r1 + 2], qa0),
-				                lower_bound<METRIC>(acc10[4 * g + 3], RA[r1 + 3], qa0));
-				*reinterpret_cast<float4 *>(dst + r1) = o;
+			for (int gq = 0; gq < 4; ++gq) {
+				const int r0 = rb + 8 * gq, r1 = rb + 32 + 8 * gq;
+				if (qv0) {
+					float *dst = dense + (int64_t)(q0 + ql0) * ld_out + tile * BR;
+					*reinterpret_cast<float4 *>(dst + r0) =
+					    make_float4(lower_bound<METRIC>(acc00[4 * gq + 0], RA[r0 + 0], qa0),
+					                lower_bound<METRIC>(acc00[4 * gq + 1], RA[r0 + 1], qa0),
+					                lower_bound<METRIC>(acc00[4 * gq + 2], RA[r0 + 2], qa0),
+					                lower_bound<METRIC>(acc00[4 * gq + 3], RA[r0 + 3], qa0));
+					*reinterpret_cast<float4 *>(dst + r1) =
+					    make_float4(lower_bound<METRIC>(acc10[4 * gq + 0], RA[r1 + 0], qa0),
+					                lower_bound<METRIC>(acc10[4 * gq + 1], RA[r1 + 1], qa0),
+					                lower_bound<METRIC>(acc10[4 * gq + 2], RA[r1 + 2], qa0),
+					                lower_bound<METRIC>(acc10[4 * gq + 3], RA[r1 + 3], qa0));
+				}
+				if (qv1) {
+					float *dst = dense + (int64_t)(q0 + ql1) * ld_out + tile * BR;
+					*reinterpret_cast<float4 *>(dst + r0) =
+					    make_float4(lower_bound<METRIC>(acc01[4 * gq + 0], RA[r0 + 0], qa1),
+					                lower_bound<METRIC>(acc01[4 * gq + 1], RA[r0 + 1], qa1),
+					                lower_bound<METRIC>(acc01[4 * gq + 2], RA[r0 + 2], qa1),
+					                lower_bound<METRIC>(acc01[4 * gq + 3], RA[r0 + 3], qa1));
+					*reinterpret_cast<float4 *>(dst + r1) =
+					    make_float4(lower_bound<METRIC>(acc11[4 * gq + 0], RA[r1 + 0], qa1),
+					                lower_bound<METRIC>(acc11[4 * gq + 1], RA[r1 + 1], qa1),
+					                lower_bound<METRIC>(acc11[4 * gq + 2], RA[r1 + 2], qa1),
+					                lower_bound<METRIC>(acc11[4 * gq + 3], RA[r1 + 3], qa1));
+				}
 			}
-			if (qv1) {
-				float *dst = dense + (int64_t)(q0 + ql1) * ld_out + (int64_t)blockIdx.x * BR;
-				o = make_float4(lower_bound<METRIC>(acc01[4 * g + 0], RA[r0 + 0], qa1),
-				                lower_bound<METRIC>(acc01[4 * g + 1], RA[r0 + 1], qa1),
-				                lower_bound<METRIC>(acc01[4 * g + 2], RA[r0 + 2], qa1),
-				                lower_bound<METRIC>(acc01[4 * g + 3], RA[r0 + 3], qa1));
-				*reinterpret_cast<float4 *>(dst + r0) = o;
-				o = make_float4(lower_bound<METRIC>(acc11[4 * g + 0], RA[r1 + 0], qa1),
-				                lower_bound<METRIC>(acc11[4 * g + 1], RA[r1 + 1], qa1),
-				                lower_bound<METRIC>(acc11[4 * g + 2], RA[r1 + 2], qa1),
-				                lower_bound<METRIC>(acc11[4 * g + 3], RA[r1 + 3], qa1));
-				*reinterpret_cast<float4 *>(dst + r1) = o;
+		} else {
+			// epilogue-only values are made opaque here so the compiler cannot
+			// hoist them out of the tile loop (they would stay live through the
+			// MFMA loop and spill at the 128-VGPR cap of a 1024-thread block)
+			int segc = seg_cap, nqq = nq;
+			asm volatile("" : "+s"(segc), "+s"(nqq));
+			const float t0 = TAU[ql0], t1 = TAU[ql1];
+			const uint32_t slot0 = (uint32_t)(row0 + rb);
+			const int64_t sb0 = ((int64_t)blockIdx.x * nqq + q0 + ql0) * segc;
+			const int64_t sb1 = sb0 + (int64_t)32 * segc;
+#pragma unroll
+			for (int r = 0; r < 16; ++r) {
+				const int rl = (r & 3) + 8 * (r >> 2);
+				const float4 x0 = RA[rb + rl], x1 = RA[rb + 32 + rl];
+				float l;
+				l = lower_bound<METRIC>(acc00[r], x0, qa0);
+				if (l <= t0 && l < F_INF) {
+					const unsigned p = atomicAdd(&CNT[ql0], 1u);
+					if (p < (unsigned)segc) seg_pool[sb0 + p] = make_uint2(fkey(l), slot0 + rl);
+				}
+				l = lower_bound<METRIC>(acc10[r], x1, qa0);
+				if (l <= t0 && l < F_INF) {
+					const unsigned p = atomicAdd(&CNT[ql0], 1u);
+					if (p < (unsigned)segc) seg_pool[sb0 + p] = make_uint2(fkey(l), slot0 + 32 + rl);
+				}
+				l = lower_bound<METRIC>(acc01[r], x0, qa1);
+				if (l <= t1 && l < F_INF) {
+					const unsigned p = atomicAdd(&CNT[ql1], 1u);
+					if (p < (unsigned)segc) seg_pool[sb1 + p] = make_uint2(fkey(l), slot0 + rl);
+				}
+				l = lower_bound<METRIC>(acc11[r], x1, qa1);
+				if (l <= t1 && l < F_INF) {
+					const unsigned p = atomicAdd(&CNT[ql1], 1u);
+					if (p < (unsigned)segc) seg_pool[sb1 + p] = make_uint2(fkey(l), slot0 + 32 + rl);
+				}
 			}
 		}
-		return;
+#pragma unroll
+		for (int r = 0; r < 16; ++r) {
+			acc00[r] = 0.f;
+			acc01[r] = 0.f;
+			acc10[r] = 0.f;
+			acc11[r] = 0.f;
+		}
 	}
-
-	// append mode.  Survivors (LB <= tau[q]) go to an LDS list in the (now
-	// idle) ring: entry = (ordered key, slot, query, offset within the query's
-	// tile range).  Then one pool reservation per (tile, query), then copy-out.
-	// A list overflow (adversarial data) marks the query so its pool counter
-	// exceeds cap: select then reports the certificate as unknown (fallback).
-	uint4 *list = reinterpret_cast<uint4 *>(smem);
-	constexpr unsigned LIST_CAP = RING_BYTES / 16;
-	unsigned &s_list_n = ep_base[BQ];   // all LDS lives in the one smem array
-	unsigned *s_over = ep_base + BQ + 1;  // BQ/32 overflow bit words
-	if (tid == 0) s_list_n = 0u;
-	if (tid < BQ / 32) s_over[tid] = 0u;
-	__syncthreads();
-	const float t0 = qv0 ? tau[q0 + ql0] : -F_INF;
-	const float t1 = qv1 ? tau[q0 + ql1] : -F_INF;
-	const uint32_t slot0 = (uint32_t)(row0 + rb);
-#define LHIP_PUSH(accv, rlo, qa, tt, qloc)                                                                          \
-	do {                                                                                                           \
-		_Pragma("unroll") for (int r = 0; r < 16; ++r) {                                                           \
-			const int rl_ = (rlo) + (r & 3) + 8 * (r >> 2);                                                        \
-			const float l_ = lower_bound<METRIC>(accv[r], RA[rb + rl_], qa);                                       \
-			if (l_ <= (tt) && l_ < F_INF) {                                                                        \
-				const unsigned off_ = atomicAdd(&ep_cnt[qloc], 1u);                                                \
-				const unsigned p_ = atomicAdd(&s_list_n, 1u);                                                      \
-				if (p_ < LIST_CAP)                                                                                 \
-					list[p_] = make_uint4(fkey(l_), slot0 + rl_, (unsigned)(qloc), off_);                          \
-				else                                                                                               \
-					atomicOr(&s_over[(qloc) >> 5], 1u << ((qloc)&31));                                             \
-			}                                                                                                      \
-		}                                                                                                          \
-	} while (0)
-	LHIP_PUSH(acc00, 0, qa0, t0, ql0);
-	LHIP_PUSH(acc10, 32, qa0, t0, ql0);
-	LHIP_PUSH(acc01, 0, qa1, t1, ql1);
-	LHIP_PUSH(acc11, 32, qa1, t1, ql1);
-#undef LHIP_PUSH
-	__syncthreads();
-	// one pool reservation per (tile, query)
-	if (tid < BQ) {
-		const unsigned c = ep_cnt[tid];
-		const bool over = (s_over[tid >> 5] >> (tid & 31)) & 1u;
-		ep_base[tid] = c ? (unsigned)atomicAdd(&pool_cnt[q0 + tid], (int)c + (over ? cap + 1 : 0)) : 0u;
-	}
-	__syncthreads();
-	const unsigned n_list = min(s_list_n, LIST_CAP);
-	for (unsigned i = tid; i < n_list; i += SCAN_THREADS) {
-		const uint4 e = list[i];
-		const unsigned pos = ep_base[e.z] + e.w;
-		if (pos < (unsigned)cap) pool[(int64_t)(q0 + e.z) * cap + pos] = make_uint2(e.x, e.y);
+	if (MODE == 1) {
+		__syncthreads();
+		if (tid < BQ && q0 + tid < nq) seg_cnt[(int64_t)blockIdx.x * nq + q0 + tid] = (int)CNT[tid];
 	}
 }
 
+static int num_cus() {
+	static int n = 0;
+	if (n == 0) {
+		int dev = 0, v = 0;
+		if (hipGetDevice(&dev) == hipSuccess &&
+		    hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+			n = v;
+		else
+			n = 256;
+	}
+	return n;
+}
+
+int scan_grid(int64_t n_tiles) { return (int)std::min<int64_t>(n_tiles, (int64_t)num_cus()); }
+
 template <int MODE>
 static void scan_dispatch(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, float *dense,
-                          int64_t ld_out, const float *tau, uint2 *pool, int *pool_cnt, int cap, hipStream_t st) {
-	dim3 grid((unsigned)n_tiles, (unsigned)(q.nq_pad / BQ));
+                          int64_t ld_out, const float *tau, uint2 *seg_pool, int *seg_cnt, int seg_cap,
+                          hipStream_t st) {
+	dim3 grid((unsigned)scan_grid(n_tiles), (unsigned)(q.nq_pad / BQ));
 	dim3 block(SCAN_THREADS);
 	switch (s.metric) {
 	case METRIC_L2:
-		scan_kernel<METRIC_L2, MODE><<<grid, block, 0, st>>>(s.X, s.rowaux, s.n_slots, s.ld, q.Qb, q.qaux, q.nq,
-		                                                      tile_stride, dense, ld_out, tau, pool, pool_cnt, cap);
+		scan_kernel<METRIC_L2, MODE><<<grid, block, 0, st>>>(s.X, s.rowaux, s.ld, q.Qb, q.qaux, q.nq, (int)n_tiles,
+		                                                      (int)tile_stride, dense, ld_out, tau, seg_pool, seg_cnt,
+		                                                      seg_cap);
 		break;
 	case METRIC_DOT:
-		scan_kernel<METRIC_DOT, MODE><<<grid, block, 0, st>>>(s.X, s.rowaux, s.n_slots, s.ld, q.Qb, q.qaux, q.nq,
-		                                                       tile_stride, dense, ld_out, tau, pool, pool_cnt, cap);
+		scan_kernel<METRIC_DOT, MODE><<<grid, block, 0, st>>>(s.X, s.rowaux, s.ld, q.Qb, q.qaux, q.nq, (int)n_tiles,
+		                                                       (int)tile_stride, dense, ld_out, tau, seg_pool, seg_cnt,
+		                                                       seg_cap);
 		break;
 	default:
-		scan_kernel<METRIC_COSINE, MODE><<<grid, block, 0, st>>>(s.X, s.rowaux, s.n_slots, s.ld, q.Qb, q.qaux,
-		                                                          q.nq, tile_stride, dense, ld_out, tau, pool,
-		                                                          pool_cnt, cap);
+		scan_kernel<METRIC_COSINE, MODE><<<grid, block, 0, st>>>(s.X, s.rowaux, s.ld, q.Qb, q.qaux, q.nq,
+		                                                          (int)n_tiles, (int)tile_stride, dense, ld_out, tau, seg_pool, seg_cnt,
+		                                                          seg_cap);
 		break;
 	}
 }
@@ -502,38 +602,36 @@ void launch_scan_dense(const StoreView &s, const QueryView &q, int64_t n_tiles, 
 	scan_dispatch<0>(s, q, n_tiles, tile_stride, out, ld_out, nullptr, nullptr, nullptr, 0, st);
 }
 
-void launch_scan_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *pool, int *pool_cnt,
-                        int cap, hipStream_t st) {
+void launch_scan_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
+                        int seg_cap, hipStream_t st) {
 	int64_t n_tiles = (s.n_slots + BR - 1) / BR;
 	if (n_tiles <= 0) return;
-	scan_dispatch<1>(s, q, n_tiles, 1, nullptr, 0, tau, pool, pool_cnt, cap, st);
+	scan_dispatch<1>(s, q, n_tiles, 1, nullptr, 0, tau, seg_pool, seg_cnt, seg_cap, st);
 }
 
 // ---------------------------------------------------------------------------
 // select: per-query radix select of the M smallest lower bounds
-// One 256-thread workgroup per query; 11/11/10-bit digits over ordered keys.
+// One 512-thread workgroup per query; 11/11/10-bit digits over ordered keys.
+// Sources: a dense LB matrix (sample pass / small stores) or the append scan's
+// per-(workgroup, query) segments.  Lists that fit are staged in LDS once and
+// every pass reads LDS; larger dense lists stream from global memory with
+// 8 loads in flight per thread.
 // ---------------------------------------------------------------------------
 constexpr int SEL_THREADS = 512;
 constexpr int SEL_BINS = 2048;
+constexpr int SEL_LDS_KEYS = 32768;   // dense lists (keys only)
+constexpr int SEL_LDS_PAIRS = 16384;  // segment lists (key, slot)
+constexpr int SEL_U = 8;
 
 struct SelSrc {
 	const float *dense;
 	int64_t ld_dense, n_entries, tile_stride;
-	const uint2 *pool;
-	int cap;
-	__device__ __forceinline__ void get(int q, int64_t i, uint32_t &key, uint32_t &slot) const {
-		if (dense) {
-			key = fkey(dense[(int64_t)q * ld_dense + i]);
-			slot = (uint32_t)((i / BR) * tile_stride * BR + (i % BR));
-		} else {
-			uint2 e = pool[(int64_t)q * cap + i];
-			key = e.x;
-			slot = e.y;
-		}
-	}
+	const uint2 *seg_pool;
+	const int *seg_cnt;
+	int seg_cap, n_seg;
 };
 
-// exclusive scan of one value per thread across the 256-thread block
+// exclusive scan of one value per thread across the block
 __device__ __forceinline__ unsigned block_excl_scan(unsigned v, unsigned *sh /*[SEL_THREADS/64]*/, unsigned &total) {
 	const int t = threadIdx.x, lane = t & 63, w = t >> 6;
 	unsigned x = v;
@@ -561,50 +659,66 @@ __device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
 	return v;
 }
 
-// LDS-resident variant: the whole list of one query is staged once (16 B
-// vector loads, several in flight per thread), every radix pass then reads LDS.
-constexpr int SEL_LDS_KEYS = 16384;  // dense lists (keys only) up to 16K entries
-constexpr int SEL_LDS_PAIRS = 8192;  // pool lists (key, slot) up to 8K entries
+// calls f(i, key) for every entry of this query's list
+template <typename F>
+__device__ __forceinline__ void sel_for_each(bool in_lds, const uint32_t *s_keys, const float *row, int64_t n, F f) {
+	const int t = threadIdx.x;
+	if (in_lds) {
+		for (int64_t i = t; i < n; i += SEL_THREADS) f(i, s_keys[i]);
+		return;
+	}
+	for (int64_t i0 = 0; i0 < n; i0 += (int64_t)SEL_U * SEL_THREADS) {
+		uint32_t k[SEL_U];
+#pragma unroll
+		for (int u = 0; u < SEL_U; ++u) {
+			const int64_t i = i0 + u * SEL_THREADS + t;
+			k[u] = i < n ? fkey(row[i]) : KEY_NAN;
+		}
+#pragma unroll
+		for (int u = 0; u < SEL_U; ++u) {
+			const int64_t i = i0 + u * SEL_THREADS + t;
+			if (i < n) f(i, k[u]);
+		}
+	}
+}
 
-__global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const int *__restrict__ pool_cnt,
-                                                             const float *__restrict__ tau, int M,
+__global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const float *__restrict__ tau, int nq, int M,
                                                              uint32_t *__restrict__ cand_slot,
-                                                             int *__restrict__ cand_cnt, float *__restrict__ cut) {
+                                                             int *__restrict__ cand_cnt, float *__restrict__ cut,
+                                                             int *__restrict__ pool_total) {
 	__shared__ __attribute__((aligned(16))) uint32_t s_keys[SEL_LDS_KEYS];
 	__shared__ unsigned hist[SEL_BINS];
 	__shared__ unsigned sh[SEL_THREADS / 64];
-	__shared__ unsigned s_digit, s_rem, s_nlt, s_neq, s_minex;
+	__shared__ unsigned s_digit, s_rem, s_nlt, s_neq, s_minex, s_over;
 	const int q = blockIdx.x;
 	const int t = threadIdx.x;
-	int64_t n;
-	bool overflow = false;
 	const bool dense = src.dense != nullptr;
+	uint32_t *s_slots = s_keys + SEL_LDS_PAIRS;  // segment mode: [keys 16K | slots 16K]
+	const float *row = dense ? src.dense + (int64_t)q * src.ld_dense : nullptr;
+	if (t == 0) {
+		s_nlt = 0;
+		s_neq = 0;
+		s_minex = 0xFFFFFFFFu;
+		s_over = 0;
+	}
+	__syncthreads();
+
+	int64_t n;
+	bool in_lds;
 	if (dense) {
 		n = src.n_entries;
-	} else {
-		int c = pool_cnt[q];
-		overflow = c > src.cap;
-		n = c < src.cap ? c : src.cap;
-	}
-	const float ftau = dense ? F_INF : tau[q];
-	const bool in_lds = dense ? (n <= SEL_LDS_KEYS) : (n <= SEL_LDS_PAIRS);
-	uint32_t *s_slots = s_keys + SEL_LDS_PAIRS;  // pool mode: [keys 8K | slots 8K]
-
-	// stage (LDS path)
-	if (in_lds) {
-		if (dense) {
-			const float *row = src.dense + (int64_t)q * src.ld_dense;
+		in_lds = n <= SEL_LDS_KEYS;
+		if (in_lds) {
 			const int n4 = (int)(n >> 2);
-			constexpr int U = 8;  // loads in flight per thread
-			for (int i0 = 0; i0 < n4; i0 += U * SEL_THREADS) {
-				float4 v[U];
+			for (int i0 = 0; i0 < n4; i0 += SEL_U * SEL_THREADS) {
+				float4 v[SEL_U];
 #pragma unroll
-				for (int u = 0; u < U; ++u) {
+				for (int u = 0; u < SEL_U; ++u) {
 					const int i = i0 + u * SEL_THREADS + t;
 					v[u] = i < n4 ? reinterpret_cast<const float4 *>(row)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
 				}
 #pragma unroll
-				for (int u = 0; u < U; ++u) {
+				for (int u = 0; u < SEL_U; ++u) {
 					const int i = i0 + u * SEL_THREADS + t;
 					if (i < n4)
 						reinterpret_cast<uint4 *>(s_keys)[i] =
@@ -612,64 +726,65 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const i
 				}
 			}
 			for (int64_t i = (int64_t)n4 * 4 + t; i < n; i += SEL_THREADS) s_keys[i] = fkey(row[i]);
-		} else {
-			const uint2 *pl = src.pool + (int64_t)q * src.cap;
-			constexpr int U = 8;
-			for (int i0 = 0; i0 < n; i0 += U * SEL_THREADS) {
-				uint2 e[U];
-#pragma unroll
-				for (int u = 0; u < U; ++u) {
-					const int i = i0 + u * SEL_THREADS + t;
-					e[u] = i < n ? pl[i] : make_uint2(0u, 0u);
-				}
-#pragma unroll
-				for (int u = 0; u < U; ++u) {
-					const int i = i0 + u * SEL_THREADS + t;
-					if (i < n) {
-						s_keys[i] = e[u].x;
-						s_slots[i] = e[u].y;
-					}
-				}
+		}
+	} else {
+		// segments: thread s < n_seg owns segment s of this query
+		unsigned c = 0;
+		if (t < src.n_seg) {
+			const int cs = src.seg_cnt[(int64_t)t * nq + q];
+			if (cs > src.seg_cap) s_over = 1u;
+			c = (unsigned)min(cs, src.seg_cap);
+		}
+		unsigned total;
+		const unsigned off = block_excl_scan(c, sh, total);
+		n = total;
+		in_lds = true;
+		if (total > (unsigned)SEL_LDS_PAIRS) {
+			s_over = 1u;
+			n = 0;
+		} else if (c) {
+			const uint2 *seg = src.seg_pool + ((int64_t)t * nq + q) * src.seg_cap;
+			unsigned i = 0;
+			for (; i + 4 <= c; i += 4) {
+				uint2 e0 = seg[i], e1 = seg[i + 1], e2 = seg[i + 2], e3 = seg[i + 3];
+				s_keys[off + i] = e0.x;
+				s_slots[off + i] = e0.y;
+				s_keys[off + i + 1] = e1.x;
+				s_slots[off + i + 1] = e1.y;
+				s_keys[off + i + 2] = e2.x;
+				s_slots[off + i + 2] = e2.y;
+				s_keys[off + i + 3] = e3.x;
+				s_slots[off + i + 3] = e3.y;
+			}
+			for (; i < c; ++i) {
+				uint2 e = seg[i];
+				s_keys[off + i] = e.x;
+				s_slots[off + i] = e.y;
 			}
 		}
 	}
-	auto key_at = [&](int64_t i) -> uint32_t {
-		if (in_lds) return s_keys[i];
-		uint32_t k, sl;
-		src.get(q, i, k, sl);
-		return k;
-	};
+	const float ftau = dense ? F_INF : tau[q];
 	auto slot_at = [&](int64_t i) -> uint32_t {
-		if (in_lds) {
-			if (dense) return (uint32_t)((i / BR) * src.tile_stride * BR + (i % BR));
-			return s_slots[i];
-		}
-		uint32_t k, sl;
-		src.get(q, i, k, sl);
-		return sl;
+		if (dense) return (uint32_t)((i / BR) * src.tile_stride * BR + (i % BR));
+		return s_slots[i];
 	};
 
 	for (int i = t; i < SEL_BINS; i += SEL_THREADS) hist[i] = 0;
-	if (t == 0) {
-		s_nlt = 0;
-		s_neq = 0;
-		s_minex = 0xFFFFFFFFu;
-	}
 	__syncthreads();
 	// pass 1: histogram of the top 11 bits (also counts +inf / NaN keys)
-	for (int64_t i = t; i < n; i += SEL_THREADS) atomicAdd(&hist[key_at(i) >> 21], 1u);
+	sel_for_each(in_lds, s_keys, row, n, [&](int64_t, uint32_t k) { atomicAdd(&hist[k >> 21], 1u); });
 	__syncthreads();
 	const unsigned n_nan = hist[SEL_BINS - 1];
 	const unsigned n_inf = hist[KEY_INF >> 21];  // bin 0x7FC holds +inf only
 	const int64_t n_fin = n - n_nan - n_inf;
 	float c_out;
 	if (n_fin <= M) {
-		for (int64_t i = t; i < n; i += SEL_THREADS) {
-			if (key_at(i) < KEY_INF) {
+		sel_for_each(in_lds, s_keys, row, n, [&](int64_t i, uint32_t k) {
+			if (k < KEY_INF) {
 				unsigned p = atomicAdd(&s_nlt, 1u);
 				cand_slot[(int64_t)q * M + p] = slot_at(i);
 			}
-		}
+		});
 		__syncthreads();
 		c_out = ftau;
 	} else {
@@ -681,10 +796,9 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const i
 			if (p > 0) {
 				for (int i = t; i < SEL_BINS; i += SEL_THREADS) hist[i] = 0;
 				__syncthreads();
-				for (int64_t i = t; i < n; i += SEL_THREADS) {
-					const uint32_t k = key_at(i);
+				sel_for_each(in_lds, s_keys, row, n, [&](int64_t, uint32_t k) {
 					if ((k & mask) == prefix) atomicAdd(&hist[(k >> sh_) & dmask], 1u);
-				}
+				});
 				__syncthreads();
 			}
 			constexpr int BPT = SEL_BINS / SEL_THREADS;
@@ -714,8 +828,7 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const i
 		const uint32_t T = prefix;                // key of the M-th smallest
 		const unsigned n_lt = (unsigned)M - rem;  // entries strictly below T
 		unsigned my_min = 0xFFFFFFFFu;            // smallest key left out
-		for (int64_t i = t; i < n; i += SEL_THREADS) {
-			const uint32_t k = key_at(i);
+		sel_for_each(in_lds, s_keys, row, n, [&](int64_t i, uint32_t k) {
 			if (k < T) {
 				unsigned p = atomicAdd(&s_nlt, 1u);
 				cand_slot[(int64_t)q * M + p] = slot_at(i);
@@ -728,7 +841,7 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const i
 			} else if (k < KEY_INF) {
 				my_min = min(my_min, k);
 			}
-		}
+		});
 		my_min = wave_min_u32(my_min);
 		if ((t & 63) == 0 && my_min != 0xFFFFFFFFu) atomicMin(&s_minex, my_min);
 		__syncthreads();
@@ -738,17 +851,24 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const i
 		__syncthreads();
 	}
 	if (t == 0) {
-		if (overflow || n_nan > 0) c_out = -F_INF;
+		if (s_over || n_nan > 0) c_out = -F_INF;
 		cand_cnt[q] = (int)s_nlt;
 		cut[q] = c_out;
+		if (pool_total) pool_total[q] = s_over ? -1 : (int)n;
 	}
 }
 
-void launch_select(const float *dense, int64_t ld_dense, int64_t n_entries, int64_t tile_stride, const uint2 *pool,
-                   const int *pool_cnt, int cap, const float *tau, int nq, int M, uint32_t *cand_slot,
-                   int *cand_cnt, float *cut, hipStream_t st) {
-	SelSrc s{dense, ld_dense, n_entries, tile_stride, pool, cap};
-	select_kernel<<<dim3(nq), dim3(SEL_THREADS), 0, st>>>(s, pool_cnt, tau, M, cand_slot, cand_cnt, cut);
+void launch_select_dense(const float *dense, int64_t ld_dense, int64_t n_entries, int64_t tile_stride, int nq, int M,
+                         uint32_t *cand_slot, int *cand_cnt, float *cut, hipStream_t st) {
+	SelSrc s{dense, ld_dense, n_entries, tile_stride, nullptr, nullptr, 0, 0};
+	select_kernel<<<dim3(nq), dim3(SEL_THREADS), 0, st>>>(s, nullptr, nq, M, cand_slot, cand_cnt, cut, nullptr);
+}
+
+void launch_select_segments(const uint2 *seg_pool, const int *seg_cnt, int seg_cap, int n_seg, const float *tau,
+                            int nq, int M, uint32_t *cand_slot, int *cand_cnt, float *cut, int *pool_total,
+                            hipStream_t st) {
+	SelSrc s{nullptr, 0, 0, 1, seg_pool, seg_cnt, seg_cap, n_seg};
+	select_kernel<<<dim3(nq), dim3(SEL_THREADS), 0, st>>>(s, tau, nq, M, cand_slot, cand_cnt, cut, pool_total);
 }
 
 // ---------------------------------------------------------------------------

@@ -85,7 +85,8 @@ struct Workspace {
 	DevBuf<float> Qin, Qf, tau, cut, dense, cand_dist, out_d, fb_keys, fb_keys2;
 	DevBuf<uint16_t> Qb;
 	DevBuf<float4> qaux;
-	DevBuf<uint2> pool;
+	DevBuf<uint2> seg_pool;
+	DevBuf<int> seg_cnt;
 	DevBuf<int> status, out_c;  // status = [cert | cand_cnt | pool_cnt] x nq
 	int *h_status = nullptr;    // pinned mirror of status
 	size_t h_status_n = 0;
@@ -208,6 +209,8 @@ struct Index {
 				                      stream));
 		}
 		HIPCHK(hipMemsetAsync(nX + n_slots * ld, 0, (size_t)(c - n_slots) * ld * sizeof(float), stream));
+		launch_fill_rowaux(na, n_slots, c, stream);
+		if (na2) launch_fill_rowaux(na2, n_slots, c, stream);
 		HIPCHK(hipStreamSynchronize(stream));
 		if (X) HIPCHK(hipFree(X));
 		if (rowaux) HIPCHK(hipFree(rowaux));
@@ -320,6 +323,8 @@ struct Index {
 			HIPCHK(hipGetLastError());
 		}
 		HIPCHK(hipMemsetAsync(nX + n * ld, 0, (size_t)(c - n) * ld * sizeof(float), stream));
+		launch_fill_rowaux(na, n, c, stream);
+		if (na2) launch_fill_rowaux(na2, n, c, stream);
 		HIPCHK(hipStreamSynchronize(stream));
 		HIPCHK(hipFree(X));
 		HIPCHK(hipFree(rowaux));
@@ -429,8 +434,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		tic(0);
 		launch_scan_dense(sv, qv, n_tiles, 1, ws.dense.p, cols, stream);
 		tic(1);
-		launch_select(ws.dense.p, cols, cols, 1, nullptr, nullptr, 0, nullptr, nq, Mfinal, ws.cand_slot.p,
-		              d_cand_cnt, ws.cut.p, stream);
+		launch_select_dense(ws.dense.p, cols, cols, 1, nq, Mfinal, ws.cand_slot.p, d_cand_cnt, ws.cut.p, stream);
 		launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Mfinal, ws.cand_dist.p, stream);
 		launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Mfinal, k, 1, 0, nullptr, dL,
 		                dD, dC, d_cert, stream);
@@ -446,20 +450,23 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		const int Ms = k + 8;
 		ws.dense.need((size_t)nq * cols);
 		launch_scan_dense(sv, qv, n_sample, stride, ws.dense.p, cols, stream);
-		launch_select(ws.dense.p, cols, cols, stride, nullptr, nullptr, 0, nullptr, nq, Ms, ws.cand_slot.p,
-		              d_cand_cnt, ws.cut.p, stream);
+		launch_select_dense(ws.dense.p, cols, cols, stride, nq, Ms, ws.cand_slot.p, d_cand_cnt, ws.cut.p, stream);
 		launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Ms, ws.cand_dist.p, stream);
 		launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Ms, k, 0, k + 1, ws.tau.p,
 		                nullptr, nullptr, nullptr, nullptr, stream);
-		// 2) threshold scan over every row
-		const int cap_pool = std::max(8192, 256 * (k + 8));
-		ws.pool.need((size_t)nq * cap_pool);
+		// 2) threshold scan over every row into per-(workgroup, query) segments;
+		//    a segment holds ~4x its expected share of the (k+8)*N/sample pool
+		const int n_seg = scan_grid(n_tiles);
+		const int64_t expect = (int64_t)(k + 8) * ((n_tiles + n_sample - 1) / n_sample);
+		const int seg_cap = (int)std::min<int64_t>(1024, round_up(std::max<int64_t>(64, 4 * expect / n_seg), 32));
+		ws.seg_pool.need((size_t)n_seg * nq * seg_cap);
+		ws.seg_cnt.need((size_t)n_seg * nq);
 		tic(2);
-		launch_scan_append(sv, qv, ws.tau.p, ws.pool.p, d_pool_cnt, cap_pool, stream);
+		launch_scan_append(sv, qv, ws.tau.p, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, stream);
 		tic(3);
 		// 3) top-M by LB, exact refine, certificate
-		launch_select(nullptr, 0, 0, 1, ws.pool.p, d_pool_cnt, cap_pool, ws.tau.p, nq, Mfinal, ws.cand_slot.p,
-		              d_cand_cnt, ws.cut.p, stream);
+		launch_select_segments(ws.seg_pool.p, ws.seg_cnt.p, seg_cap, n_seg, ws.tau.p, nq, Mfinal, ws.cand_slot.p,
+		                       d_cand_cnt, ws.cut.p, d_pool_cnt, stream);
 		launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Mfinal, ws.cand_dist.p, stream);
 		launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Mfinal, k, 1, 0, nullptr, dL,
 		                dD, dC, d_cert, stream);
