@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-recall", action="store_true")
+    ap.add_argument("--sample-div", type=int, default=None, help="index option sample_div (default: library's)")
     return ap.parse_args()
 
 
@@ -115,6 +116,8 @@ def main():
     if not h:
         raise RuntimeError(e.value.decode())
     lance_hip.LanceHipSetOption(h, "reserve_rows", str(n_local))
+    if a.sample_div:
+        lance_hip.LanceHipSetOption(h, "sample_div", str(a.sample_div))
     for lo in range(s0, s1, 1 << 18):
         hi = min(s1, lo + (1 << 18))
         X = gen_rows(lo, hi, D, dev)

@@ -24,7 +24,7 @@ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 //   w = sc    (1 for l2/dot, 1/|x| for cosine)
 struct StoreView {
 	const float *X;          // [n_slots][ld] f32 rows, zero padded to ld
-	const float4 *rowaux;    // [n_slots]
+	const float4 *rowaux;    // [n_slots rounded up to SCAN_BR], tile-blocked SoA (raix() in knn_kernels.hip)
 	const int64_t *labels;   // [n_slots] slot -> label
 	int64_t n_slots;
 	int ld;                  // padded row stride (floats), multiple of DPAD

@@ -24,6 +24,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
+#include <stdexcept>
 #include <cfloat>
 #include <cmath>
 
@@ -33,6 +34,7 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 static constexpr float F_INF = __builtin_huge_valf();
+static constexpr float F_MAX = 3.40282347e+38f;
 static constexpr uint32_t KEY_INF = 0xFF800000u;  // ordered key of +inf
 static constexpr uint32_t KEY_NAN = 0xFFFFFFFFu;  // every NaN is canonicalised to this
 
@@ -74,6 +76,12 @@ __device__ __forceinline__ bool hit_less(float da, int64_t la, float db, int64_t
 // accumulation that truncates instead of rounding.
 static constexpr double U_BOUND = 1.1920928955078125e-07;
 
+// Row aux layout: tile-blocked SoA, 16 B per slot.  For slot r of tile
+// T = r / 256 the four terms live at floats [T*1024 + c*256 + r%256],
+// c = 0 alpha, 1 xn, 2 ux, 3 sc.  A tile's block is the 4 KiB the scan DMAs
+// into LDS, and four consecutive rows' terms are one 16 B read.
+__host__ __device__ __forceinline__ int64_t raix(int64_t r, int c) { return ((r >> 8) << 10) | ((int64_t)c << 8) | (r & 255); }
+
 // ---------------------------------------------------------------------------
 // ingest: per-row auxiliary data
 // ---------------------------------------------------------------------------
@@ -108,7 +116,11 @@ __global__ __launch_bounds__(256) void rowaux_kernel(const float *__restrict__ X
 				a = make_float4(__builtin_nanf(""), 0.0f, 0.0f, 0.0f);  // cosine undefined: exact fallback
 			}
 		}
-		rowaux[s0 + r] = a;
+		float *ra = reinterpret_cast<float *>(rowaux);
+		ra[raix(s0 + r, 0)] = a.x;
+		ra[raix(s0 + r, 1)] = a.y;
+		ra[raix(s0 + r, 2)] = a.z;
+		ra[raix(s0 + r, 3)] = a.w;
 		if (a.x == a.x) atomicMax(&stats[0], __float_as_uint(fabsf(a.x)));
 		atomicMax(&stats[1], __float_as_uint(a.z));
 	}
@@ -123,7 +135,13 @@ void launch_rowaux(const float *X, int ld, int dim, int metric, int64_t s0, int6
 
 __global__ void fill_rowaux_kernel(float4 *rowaux, int64_t from, int64_t to) {
 	const int64_t i = from + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	if (i < to) rowaux[i] = make_float4(F_INF, 0.f, 0.f, 0.f);
+	if (i < to) {
+		float *ra = reinterpret_cast<float *>(rowaux);
+		ra[raix(i, 0)] = F_INF;
+		ra[raix(i, 1)] = 0.f;
+		ra[raix(i, 2)] = 0.f;
+		ra[raix(i, 3)] = 0.f;
+	}
 }
 
 void launch_fill_rowaux(float4 *rowaux, int64_t from, int64_t to, hipStream_t st) {
@@ -133,7 +151,7 @@ void launch_fill_rowaux(float4 *rowaux, int64_t from, int64_t to, hipStream_t st
 
 __global__ void tombstone_kernel(float4 *rowaux, const int64_t *slots, int n) {
 	int i = blockIdx.x * blockDim.x + threadIdx.x;
-	if (i < n) rowaux[slots[i]].x = F_INF;
+	if (i < n) reinterpret_cast<float *>(rowaux)[raix(slots[i], 0)] = F_INF;
 }
 
 void launch_tombstone(float4 *rowaux, const int64_t *slots, int n, hipStream_t st) {
@@ -156,7 +174,10 @@ __global__ __launch_bounds__(256) void prep_queries_kernel(const float *__restri
 		float v = (q < nq && i < dim) ? Q[(int64_t)q * dim + i] : 0.0f;
 		Qf[(int64_t)q * ld + i] = v;
 		uint16_t b = bf16_bits(v);
-		Qb[(int64_t)q * ld + i] = b;
+		// L2 / dot: the scan accumulates S*s directly (S = -2 / -1, a power of
+		// two: bf16(S*v) == S*bf16(v) exactly), see scan_kernel's bound fold
+		Qb[(int64_t)q * ld + i] =
+		    metric == METRIC_L2 ? bf16_bits(-2.0f * v) : metric == METRIC_DOT ? bf16_bits(-v) : b;
 		float e = v - __uint_as_float((uint32_t)b << 16);
 		s2 += (double)v * v;
 		e2 += (double)e * e;
@@ -179,12 +200,18 @@ __global__ __launch_bounds__(256) void prep_queries_kernel(const float *__restri
 	const double gamma = 2.0 * ld * u;  // accumulation of ld exact bf16 products in f32
 	const double qn = sqrt(s2), eq = sqrt(e2);
 	const double uq = (qn + eq) * (1.0 + 4.0 * u);
+	// L2 / dot fold the row/query terms into the accumulator before the k
+	// loop (scan_kernel): the ld/16 MFMA k-steps then each round at the
+	// magnitude of the whole bound, not of the partial dot product, and
+	// the slack's evaluation budget grows from 16 to ld/16 + 16 unit roundoffs
+	// of the same magnitudes.
+	const double ev = (double)ld / 16.0 + 16.0;
 	float4 a;
 	if (metric == METRIC_L2) {
-		double slack = 16.0 * u * ((double)max_alpha + s2 + 7.0 * (double)max_ux * uq) + 1e-30;
+		double slack = ev * u * ((double)max_alpha + s2 + 7.0 * (double)max_ux * uq) + 1e-30;
 		a = make_float4(-2.0f, (float)(-2.0 * (1.0 + gamma) * uq), (float)(2.0 * qn), (float)(s2 - slack));
 	} else if (metric == METRIC_DOT) {
-		double slack = 16.0 * u * (1.0 + 7.0 * (double)max_ux * uq) + 1e-30;
+		double slack = ev * u * (1.0 + 7.0 * (double)max_ux * uq) + 1e-30;
 		a = make_float4(-1.0f, (float)(-(1.0 + gamma) * uq), (float)qn, (float)(1.0 - slack));
 	} else {
 		if (qn > 0.0) {
@@ -260,7 +287,44 @@ constexpr int BR = SCAN_BR, BQ = SCAN_BQ, BK = SCAN_BK;
 #ifndef LHIP_ABL_NO_EPILOGUE
 #define LHIP_ABL_NO_EPILOGUE 0
 #endif
-constexpr int SCAN_THREADS = 1024;
+#ifndef LHIP_ABL_NO_SLOW
+#define LHIP_ABL_NO_SLOW 0  // survivors are tested but not written
+#endif
+#ifndef LHIP_ABL_NO_FLUSH
+#define LHIP_ABL_NO_FLUSH 0  // survivor lists are not written out
+#endif
+// development-only phase timer: per-wave s_memtime cycles in the DMA wait, the
+// barrier, the stage's fragment reads + MFMA issue and the epilogue, summed over
+// all waves into lhip_prof[MODE*8 + 0..3] ([4] waves, [5] stages, [6] tiles)
+#ifndef LHIP_PROF
+#define LHIP_PROF 0
+#endif
+#if LHIP_PROF
+__device__ unsigned long long lhip_prof[24];
+extern "C" int lhip_prof_read(unsigned long long *out, int reset) {
+	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lhip_prof), sizeof(unsigned long long) * 24) != hipSuccess) return -1;
+	if (reset) {
+		unsigned long long z[24] = {};
+		if (hipMemcpyToSymbol(HIP_SYMBOL(lhip_prof), z, sizeof(z)) != hipSuccess) return -1;
+	}
+	return 0;
+}
+#define PROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define PROF_T(v)
+#endif
+// tuning switches (both variants are correct)
+#ifndef LHIP_EARLY_REFILL
+#define LHIP_EARLY_REFILL 1  // refill the last stage's slot before a tile's epilogue
+#endif
+#ifndef LHIP_READS_FIRST
+#define LHIP_READS_FIRST 1  // issue all fragment reads of a stage before its MFMAs
+#endif
+#ifndef LHIP_X_NT
+#define LHIP_X_NT 1  // non-temporal policy on the once-read base stream
+#endif
+constexpr int SCAN_THREADS = 512;
+constexpr int SCAN_WAVES = SCAN_THREADS / 64;          // 8: 2 per SIMD, 256 registers each
 constexpr int SK = 32;
 constexpr int NSTAGE = 3;
 constexpr int XST_BYTES = BR * SK * 4;                 // 32 KiB
@@ -271,11 +335,20 @@ constexpr int RA_SLOT = BR * 16;                       // 4 KiB
 constexpr int RA_BYTES = 2 * RA_SLOT;
 constexpr int CNT_BYTES = BQ * 4;
 constexpr int QA_BYTES = BQ * 16 + BQ * 4;             // per-query bound constants + tau
-constexpr int SCAN_LDS = RING_BYTES + RA_BYTES + CNT_BYTES + QA_BYTES;
+constexpr int WLIST = 32;                              // survivor list entries (8 B) per wave and tile
+constexpr int LIST_BYTES = 8 * WLIST * 8;
+constexpr int SCAN_LDS = RING_BYTES + RA_BYTES + CNT_BYTES + QA_BYTES + LIST_BYTES;
+constexpr int X_DMA_PER_WAVE = XST_BYTES / 1024 / SCAN_WAVES;  // 4
+constexpr int Q_DMA_PER_WAVE = QST_BYTES / 1024 / SCAN_WAVES;  // 2
+constexpr int DMA_PER_STAGE = X_DMA_PER_WAVE + Q_DMA_PER_WAVE; // + 1 row-aux on waves 0..3 at stage 0
 static_assert(SCAN_LDS <= 160 * 1024, "LDS budget");
-static_assert(XST_BYTES / 1024 == 2 * (SCAN_THREADS / 64), "2 X DMA instructions per wave per stage");
-static_assert(QST_BYTES / 1024 == SCAN_THREADS / 64, "1 Q DMA instruction per wave per stage");
-static_assert(RA_SLOT / 1024 == 4, "row aux: one DMA instruction on waves 0..3");
+static_assert(X_DMA_PER_WAVE * SCAN_WAVES * 1024 == XST_BYTES, "X stage = whole DMA instructions");
+static_assert(Q_DMA_PER_WAVE * SCAN_WAVES * 1024 == QST_BYTES, "Q stage = whole DMA instructions");
+static_assert(RA_SLOT / 1024 == 4 && SCAN_WAVES >= 4, "row aux: one DMA instruction on waves 0..3");
+static_assert(DMA_PER_STAGE == 6, "wait counts below assume 6 (+1) DMA instructions per wave and stage");
+static_assert(SCAN_WAVES == 8 && WLIST <= 64, "one list of WLIST entries per wave; a flush is one instruction");
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int METRIC>
 __device__ __forceinline__ float lower_bound(float s, float4 ra, float4 qa) {
@@ -292,12 +365,9 @@ __device__ __forceinline__ float lower_bound(float s, float4 ra, float4 qa) {
 // compiler does not see an LDS write in flight: it would otherwise put a
 // vmcnt(0) in front of every ds_read of the ring (any stage may alias) and
 // serialise the pipeline.  Ordering is ours: counted vmcnt + s_barrier.
-// M0 is written here and nowhere else in the kernel.
-__device__ __forceinline__ void dma16(const void *g, uint32_t lds_addr) {
-	asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_addr), "v"(g) : "memory", "m0");
-}
-// saddr form: wave-uniform 64-bit base in SGPRs + 32-bit per-lane byte offset
-// (no 64-bit per-lane address registers)
+// M0 is written here and nowhere else in the kernel.  saddr form: wave-uniform
+// 64-bit base in SGPRs + 32-bit per-lane byte offset.
+template <bool NT = false>
 __device__ __forceinline__ void dma16s(const void *sbase, uint32_t voff, uint32_t lds_addr) {
 	// readfirstlane returns int: go through uint32_t so the low word is not
 	// sign-extended into the high word of the address
@@ -305,10 +375,16 @@ __device__ __forceinline__ void dma16s(const void *sbase, uint32_t voff, uint32_
 	const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
 	const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32));
 	const uint64_t ub = ((uint64_t)hi << 32) | (uint64_t)lo;
-	asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds_addr), "v"(voff), "s"(ub)
-	             : "memory", "m0");
+	if (NT)
+		asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2 nt" ::"s"(lds_addr), "v"(voff), "s"(ub)
+		             : "memory", "m0");
+	else
+		asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds_addr), "v"(voff), "s"(ub)
+		             : "memory", "m0");
 }
 
+// A fragment (32 base rows x 16 k) from the f32 X stage: two ds_read_b128 of
+// logical chunks c, c+1 of row r, converted to bf16 in registers.
 __device__ __forceinline__ bf16x8 ld_afrag(const uint8_t *xs, int r, int c) {
 	const int f = (r >> 1) & 7;
 	const float4 lo = *reinterpret_cast<const float4 *>(xs + r * 128 + ((c ^ f) << 4));
@@ -325,31 +401,76 @@ __device__ __forceinline__ bf16x8 ld_afrag(const uint8_t *xs, int r, int c) {
 	return v;
 }
 
+// B fragment (16 k x 32 queries) from the bf16 Q stage: one ds_read_b128.
 __device__ __forceinline__ bf16x8 ld_bfrag(const uint8_t *qs, int r, int c) {
 	return *reinterpret_cast<const bf16x8 *>(qs + r * 64 + ((c ^ ((r >> 2) & 3)) << 4));
 }
 
 #define LHIP_WAIT_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 
+// Lane id through volatile asm: not loop-invariant to the compiler, so values
+// derived from it are recomputed where used instead of hoisted out of the
+// tile loop and kept live across the MFMA loop.
+__device__ __forceinline__ int lane_id_fresh() {
+	uint32_t ln;
+	asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+	return (int)ln;
+}
+
+// ---------------------------------------------------------------------------
+// scan kernel (persistent, LDS-DMA ring)
+//
+// Tile = 256 base rows x 256 queries.  Workgroup = 512 threads = 8 waves, two
+// per SIMD with 256 registers each, laid out 4 (base rows) x 2 (queries): a
+// wave owns 64 rows x 128 queries = 2 x 4 v_mfma_f32_32x32x16_bf16 tiles
+// (A = base rows, B = queries: accumulator column = lane&31 = query, the 16
+// registers walk base rows).  Per 32-deep stage a wave reads 4 A fragments
+// (f32, converted to bf16) and 8 B fragments from LDS for 16 MFMAs — all
+// fragments of a stage are read before its first MFMA.  One workgroup per CU
+// walks tiles blockIdx.x, +gridDim.x, ...; the k-stream never stops at a tile
+// boundary.
+//
+// The k dimension streams through a ring of NSTAGE LDS stages of SK = 32:
+//   X stage: 256 rows x 32 f32 (32 KiB) straight from HBM by
+//            global_load_lds_dwordx4 (nt: read once), rows 128 B,
+//            16 B chunk c of row r stored at c ^ ((r>>1)&7);
+//   Q stage: 256 queries x 32 bf16 (16 KiB) from L2, rows 64 B,
+//            chunk c of row r stored at c ^ ((r>>2)&3);
+//   with stage 0 of a tile: the tile's 256 row-aux float4 (4 KiB, 2 slots).
+// LDS-DMA writes lane-linearly, so the swizzle is applied on the per-lane
+// SOURCE address and undone on the ds_read_b128 fragment reads (conflict-free
+// for the b128 lane groups).  NSTAGE-1 stages stay in flight; one raw
+// s_barrier per stage behind a counted s_waitcnt vmcnt.  The store is
+// zero-padded (rows) and +inf-padded (row aux) to a multiple of BR rows.
+//
+// Epilogue per tile: each accumulator becomes a rigorous lower bound of the
+// exact distance (4 FMAs).  Dense mode stores it.  Append mode keeps (LB,
+// row) when LB <= tau[q]: survivors are appended to the wave's own LDS list
+// by wave ballots (no atomics); at the next stage, ahead of that stage's DMA,
+// the wave assigns each entry its position in the workgroup's segment for q
+// with one ds_add_rtn over the whole list and writes it out, so no global
+// store sits behind in-flight DMA in the in-order vmcnt queue.
+// ---------------------------------------------------------------------------
 template <int METRIC, int MODE>
-__global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(const float *__restrict__ X,
-                                                            const float4 *__restrict__ rowaux, int ld,
-                                                            const uint16_t *__restrict__ Qb,
-                                                            const float4 *__restrict__ qaux, int nq, int n_tiles,
-                                                            int tile_stride, float *__restrict__ dense,
-                                                            int64_t ld_out, const float *__restrict__ tau,
-                                                            uint2 *__restrict__ seg_pool, int *__restrict__ seg_cnt,
-                                                            int seg_cap) {
+__global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const float *__restrict__ X,
+                                                               const float4 *__restrict__ rowaux, int ld,
+                                                               const uint16_t *__restrict__ Qb,
+                                                               const float4 *__restrict__ qaux, int nq,
+                                                               int n_tiles, int tile_stride,
+                                                               float *__restrict__ dense, int64_t ld_out,
+                                                               const float *__restrict__ tau,
+                                                               uint2 *__restrict__ seg_pool,
+                                                               int *__restrict__ seg_cnt, int seg_cap) {
 	__shared__ __attribute__((aligned(16))) uint8_t smem[SCAN_LDS];
 	unsigned *CNT = reinterpret_cast<unsigned *>(smem + RING_BYTES + RA_BYTES);
 	float4 *QA = reinterpret_cast<float4 *>(smem + RING_BYTES + RA_BYTES + CNT_BYTES);
 	float *TAU = reinterpret_cast<float *>(smem + RING_BYTES + RA_BYTES + CNT_BYTES + BQ * 16);
+	uint2 *LIST = reinterpret_cast<uint2 *>(smem + RING_BYTES + RA_BYTES + CNT_BYTES + QA_BYTES);
 
 	const int tid = threadIdx.x;
 	const int lane = tid & 63;
 	const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR math
 	const int wr = w & 3, wq = w >> 2;
-	const int li = lane & 31, hi = lane >> 5;
 	const int q0 = blockIdx.y * BQ;
 	const int S = ld / SK;  // >= 2 (ld is a multiple of 64)
 	const int my_tiles = (n_tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
@@ -365,193 +486,426 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(const float *__restr
 	LHIP_WAIT_VM(0);  // the ordinary loads above, before any counted DMA wait
 	__syncthreads();
 
-	// DMA sources.  X: wave instruction j (0,1) covers rows (2w+j)*8 + lane/8,
+	// DMA sources.  X: wave instruction j covers rows (4w+j)*8 + lane/8,
 	// physical 16 B chunk lane%8 (logical chunk = physical ^ ((row>>1)&7)).
-	// Q: one instruction covers queries w*16 + lane/4, physical chunk lane%4.
-	// Row aux (stage 0 only): waves 0..3, rows w*64 + lane.
-	// per-lane byte offsets (32-bit); the tile / stage base is wave-uniform
-	const int xr0 = (2 * w) * 8 + (lane >> 3), xr1 = xr0 + 8;
-	const uint32_t xoff0 = (uint32_t)(xr0 * ld + (((lane & 7) ^ ((xr0 >> 1) & 7)) << 2)) * 4u;
-	const uint32_t xoff1 = (uint32_t)(xr1 * ld + (((lane & 7) ^ ((xr1 >> 1) & 7)) << 2)) * 4u;
-	const int qr = w * 16 + (lane >> 2);
-	const uint32_t qoff = (uint32_t)(qr * ld + (((lane & 3) ^ ((qr >> 2) & 3)) << 3)) * 2u;
+	// Q: instruction j covers queries (2w+j)*16 + lane/4, physical chunk lane%4.
+	// Row aux (stage 0 only): waves 0..3, rows w*64 + lane.  Per-lane byte
+	// offsets are recomputed at every issue from a fresh lane id (a few VALU
+	// ops per stage) rather than kept live across the loop.
 	const uint16_t *qbase = Qb + (int64_t)q0 * ld;
 	const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
 
 	auto issue = [&](int ti, int st, int slot) {
 		const int64_t row0 = (int64_t)((int)blockIdx.x + ti * (int)gridDim.x) * tile_stride * BR;
 		const uint32_t base = lds0 + (uint32_t)slot * STAGE_BYTES;
-		if (st == 0 && w < 4) {
-			// lane id rematerialised here instead of kept live across the loop
-			uint32_t ln;
-			asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-			dma16s(rowaux + row0 + w * 64, ln * 16u,
+		const int ln = lane_id_fresh();
+		if (st == 0 && w < 4)
+			dma16s(rowaux + row0 + w * 64, (uint32_t)ln * 16u,
 			       __builtin_amdgcn_readfirstlane(lds0 + RING_BYTES + (uint32_t)(ti & 1) * RA_SLOT + w * 1024));
-		}
 		const float *xt = X + row0 * ld + st * SK;
-		dma16s(xt, xoff0, __builtin_amdgcn_readfirstlane(base + (2 * w) * 1024));
-		dma16s(xt, xoff1, __builtin_amdgcn_readfirstlane(base + (2 * w + 1) * 1024));
-		if (!LHIP_ABL_NO_Q) dma16s(qbase + st * SK, qoff, __builtin_amdgcn_readfirstlane(base + XST_BYTES + w * 1024));
+#pragma unroll
+		for (int j = 0; j < X_DMA_PER_WAVE; ++j) {
+			const int xr = (X_DMA_PER_WAVE * w + j) * 8 + (ln >> 3);
+			const uint32_t xoff = (uint32_t)(xr * ld + (((ln & 7) ^ ((xr >> 1) & 7)) << 2)) * 4u;
+			dma16s<LHIP_X_NT>(xt, xoff, __builtin_amdgcn_readfirstlane(base + (X_DMA_PER_WAVE * w + j) * 1024));
+		}
+		if (!LHIP_ABL_NO_Q) {
+#pragma unroll
+			for (int j = 0; j < Q_DMA_PER_WAVE; ++j) {
+				const int qr = (Q_DMA_PER_WAVE * w + j) * 16 + (ln >> 2);
+				const uint32_t qoff = (uint32_t)(qr * ld + (((ln & 3) ^ ((qr >> 2) & 3)) << 3)) * 2u;
+				dma16s(qbase + st * SK, qoff,
+				       __builtin_amdgcn_readfirstlane(base + XST_BYTES + (Q_DMA_PER_WAVE * w + j) * 1024));
+			}
+		}
 	};
 
-	const int ql0 = wq * 64 + li, ql1 = ql0 + 32;  // tile-local queries of this lane
-	const int rb = wr * 64 + 4 * hi;                // + tr*32 + 8g + j
-	const int ra0 = wr * 64 + li, ra1 = ra0 + 32;
-	const int qb0 = wq * 64 + li, qb1 = qb0 + 32;
-
-	f32x16 acc00, acc01, acc10, acc11;
+	// accumulators: acc[t][u] = rows wr*64 + 32t + (reg layout), queries wq*128 + 32u + lane&31.
+	// Set at each tile's stage 0: L2 / dot start from the bound's row/query
+	// terms (FOLD: alpha + C + xn*B + ux*A by two exact f32 MFMAs) and the
+	// bf16 MFMAs add S*s (queries pre-scaled by S), so at the tile end the
+	// accumulator IS the lower bound; cosine (per-row scale) starts at 0.
+	constexpr bool FOLD = METRIC != METRIC_COSINE;
+	f32x16 acc[2][4];
+	auto init_acc = [&](int ti) {
+		if (!FOLD) {
 #pragma unroll
-	for (int r = 0; r < 16; ++r) {
-		acc00[r] = 0.f;
-		acc01[r] = 0.f;
-		acc10[r] = 0.f;
-		acc11[r] = 0.f;
-	}
+			for (int t = 0; t < 2; ++t)
+#pragma unroll
+				for (int u = 0; u < 4; ++u)
+#pragma unroll
+					for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
+			return;
+		}
+		const float *RAs = reinterpret_cast<const float *>(smem + RING_BYTES + (ti & 1) * RA_SLOT);
+		const int ln = lane_id_fresh();
+		const int li = ln & 31, hk = ln >> 5;  // f32 32x32x2 operands: lane = (row or column, k)
+		f32x16 zero;
+#pragma unroll
+		for (int r = 0; r < 16; ++r) zero[r] = 0.f;
+		float bq[4], cq[4];
+#pragma unroll
+		for (int u = 0; u < 4; ++u) {
+			const float4 qa = QA[wq * 128 + 32 * u + li];
+			bq[u] = hk ? qa.y : qa.z;  // k0: B, k1: A
+			cq[u] = hk ? qa.w : 1.0f;  // k0: 1, k1: C
+		}
+#pragma unroll
+		for (int t = 0; t < 2; ++t) {
+			const int r = wr * 64 + 32 * t + li;
+			const float axu = RAs[(1 + hk) * BR + r];  // k0: xn, k1: ux
+			const float aal = hk ? 1.0f : RAs[r];     // k0: alpha, k1: 1
+#pragma unroll
+			for (int u = 0; u < 4; ++u) {
+				acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(axu, bq[u], zero, 0, 0, 0);
+				acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(aal, cq[u], acc[t][u], 0, 0, 0);
+			}
+		}
+	};
 
-	// issue cursor (tile, stage) runs two stages ahead of the compute cursor
-	int iss_t = 0, iss_s = 0;
-	auto advance_issue = [&]() {
+	// Issue cursor: global stage iss_g = (tile iss_t, stage iss_s) into ring
+	// slot iss_slot.  Stage h may be issued once every wave has finished
+	// computing stage h-NSTAGE (its slot): right after the barrier of
+	// iteration h-2.
+	int iss_g = 0, iss_t = 0, iss_s = 0, iss_slot = 0;
+	auto issue_next = [&]() {
+		issue(iss_t, iss_s, iss_slot);
+		++iss_g;
 		if (++iss_s == S) {
 			iss_s = 0;
 			++iss_t;
 		}
+		iss_slot = iss_slot == NSTAGE - 1 ? 0 : iss_slot + 1;
 	};
-	issue(iss_t, iss_s, 0);
-	advance_issue();
-	if (G > 1) {
-		issue(iss_t, iss_s, 1);
-		advance_issue();
-	}
-	int cur_t = 0, cur_s = 0, slot = 0, iss_slot = 2;
-	for (int g = 0; g < G; ++g) {
-		if (g + 1 < G) {
-			// this wave's DMA instructions of stage g+1 may stay in flight
-			const bool next_has_ra = (cur_s + 1 == S) && w < 4;
-			if (next_has_ra)
-				LHIP_WAIT_VM(4);
-			else
-				LHIP_WAIT_VM(3);
-		} else {
-			LHIP_WAIT_VM(0);
+	issue_next();
+	if (G > 1) issue_next();
+	int cur_t = 0, cur_s = 0, slot = 0;
+	// This wave's survivor list: n_list entries (wave-uniform) of the tile
+	// finished last.  Entry = (key, query << 18 | tile row << 10).  Written
+	// out with segment positions from the per-query LDS counters: one
+	// ds_add_rtn for the whole list.
+	uint2 *wlist = LIST + w * WLIST;
+	int n_list = 0;
+	auto write_list = [&](int ti_prev) {
+		const int ln = lane_id_fresh();
+		if (ln < n_list) {
+			const uint2 e = wlist[ln];
+			const int qloc = (int)(e.y >> 18), rloc = (int)((e.y >> 10) & 255u);
+			const unsigned p = atomicAdd(&CNT[qloc], 1u);
+			if (p < (unsigned)seg_cap) {
+				const int64_t prow0 = ((int64_t)blockIdx.x + (int64_t)ti_prev * gridDim.x) * tile_stride * BR;
+				seg_pool[((int64_t)blockIdx.x * nq + q0 + qloc) * seg_cap + p] =
+				    make_uint2(fkey(__uint_as_float(e.x)), (uint32_t)(prow0 + rloc));
+			}
 		}
+		n_list = 0;
+	};
+	// a bound whose survivors do not fit the wave's list: straight to the
+	// segment (position from the LDS counter); out of line, rare
+	auto overflow = [&](uint64_t mm, float lb, int qv, int rr, int64_t row0) {
+		if ((mm >> lane_id_fresh()) & 1ull) {
+			const unsigned p = atomicAdd(&CNT[qv], 1u);
+			if (p < (unsigned)seg_cap)
+				seg_pool[((int64_t)blockIdx.x * nq + q0 + qv) * seg_cap + p] = make_uint2(fkey(lb), (uint32_t)(row0 + rr));
+		}
+	};
+#if LHIP_PROF
+	uint64_t pw = 0, pb = 0, pc = 0, pe = 0;
+	uint64_t prof_surv = 0, prof_over = 0, prof_slow = 0, prof_slown = 0;
+#endif
+	for (int g = 0; g < G; ++g) {
+		PROF_T(t0);
+		// Stage g must have landed; this wave's DMA instructions of the stages
+		// after it (one, or two after an early refill) may stay in flight: 6
+		// each, +1 for a tile's stage 0 on waves 0..3 (row aux).
+		{
+			const int ahead = iss_g - 1 - g;
+			const int s1 = cur_s + 1 == S ? 0 : cur_s + 1;
+			const int n1 = DMA_PER_STAGE + ((s1 == 0) & (w < 4));
+			const int n2 = DMA_PER_STAGE + (((s1 + 1 == S) | (S == 1)) & (w < 4));
+			const int n = ahead <= 0 ? 0 : (ahead == 1 ? n1 : n1 + n2);
+			if (n == 0)
+				LHIP_WAIT_VM(0);
+			else if (n == 6)
+				LHIP_WAIT_VM(6);
+			else if (n == 7)
+				LHIP_WAIT_VM(7);
+			else if (n == 12)
+				LHIP_WAIT_VM(12);
+			else
+				LHIP_WAIT_VM(13);
+		}
+		PROF_T(t1);
 		__builtin_amdgcn_s_barrier();
 		asm volatile("" ::: "memory");
-		if (g + 2 < G) {
-			issue(iss_t, iss_s, iss_slot);
-			advance_issue();
-			iss_slot = iss_slot == NSTAGE - 1 ? 0 : iss_slot + 1;
+		PROF_T(t2);
+		const bool tile_end = cur_s + 1 == S;
+		// write out the survivor list of the tile finished last iteration:
+		// these stores enter the vmcnt queue ahead of this iteration's DMA, so
+		// the next counted wait finds them a whole stage old
+		if (MODE == 1 && n_list > 0) {
+			if (LHIP_ABL_NO_FLUSH)
+				n_list = 0;
+			else
+				write_list(cur_t - 1);
 		}
-		const uint8_t *xs = smem + slot * STAGE_BYTES;
-		const uint8_t *qs = xs + XST_BYTES;
-#pragma unroll 1
-		for (int kk = 0; kk < SK / 16; ++kk) {
-			const int ca = 4 * kk + 2 * hi;  // logical 16 B chunk (4 f32) of the A fragment
-			const int cb = 2 * kk + hi;      // logical 16 B chunk (8 bf16) of the B fragment
-			const bf16x8 a0 = ld_afrag(xs, ra0, ca);
-			const bf16x8 a1 = ld_afrag(xs, ra1, ca);
-			const bf16x8 b0 = ld_bfrag(qs, qb0, cb);
-			const bf16x8 b1 = ld_bfrag(qs, qb1, cb);
-			if (LHIP_ABL_NO_MFMA) {
-				asm volatile("" ::"v"(a0), "v"(a1), "v"(b0), "v"(b1));
-			} else {
-				acc00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc00, 0, 0, 0);
-				acc01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc01, 0, 0, 0);
-				acc10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc10, 0, 0, 0);
-				acc11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc11, 0, 0, 0);
+		if (iss_g < G && iss_g <= g + 2) issue_next();
+
+		// ---- stage g: all fragment reads first, then 16 MFMAs --------------
+		if (cur_s == 0) init_acc(cur_t);
+		{
+			const uint8_t *xs = smem + slot * STAGE_BYTES;
+			const uint8_t *qs = xs + XST_BYTES;
+			const int ln = lane_id_fresh();
+			const int li = ln & 31, hh = ln >> 5;
+			// every fragment read of the stage is issued before the first
+			// convert / MFMA: one exposed LDS latency per stage, not three
+			float4 ar[2][2][2];
+			bf16x8 a[2][2], b[2][4];
+#pragma unroll
+			for (int kk = 0; kk < SK / 16; ++kk) {
+#pragma unroll
+				for (int t = 0; t < 2; ++t) {
+					const int r = wr * 64 + 32 * t + li, c = 4 * kk + 2 * hh, f = (r >> 1) & 7;
+					ar[kk][t][0] = *reinterpret_cast<const float4 *>(xs + r * 128 + ((c ^ f) << 4));
+					ar[kk][t][1] = *reinterpret_cast<const float4 *>(xs + r * 128 + (((c + 1) ^ f) << 4));
+				}
+#pragma unroll
+				for (int u = 0; u < 4; ++u) b[kk][u] = ld_bfrag(qs, wq * 128 + 32 * u + li, 2 * kk + hh);
+			}
+			if (LHIP_READS_FIRST) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+			for (int kk = 0; kk < SK / 16; ++kk)
+#pragma unroll
+				for (int t = 0; t < 2; ++t) {
+					const float4 lo = ar[kk][t][0], hi = ar[kk][t][1];
+					bf16x8 v;
+					v[0] = (__bf16)lo.x;
+					v[1] = (__bf16)lo.y;
+					v[2] = (__bf16)lo.z;
+					v[3] = (__bf16)lo.w;
+					v[4] = (__bf16)hi.x;
+					v[5] = (__bf16)hi.y;
+					v[6] = (__bf16)hi.z;
+					v[7] = (__bf16)hi.w;
+					a[kk][t] = v;
+				}
+#pragma unroll
+			for (int kk = 0; kk < SK / 16; ++kk) {
+#pragma unroll
+				for (int t = 0; t < 2; ++t)
+#pragma unroll
+					for (int u = 0; u < 4; ++u) {
+						if (LHIP_ABL_NO_MFMA)
+							asm volatile("" ::"v"(a[kk][t]), "v"(b[kk][u]));
+						else
+							acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kk][t], b[kk][u], acc[t][u], 0, 0, 0);
+					}
 			}
 		}
 		asm volatile("" ::: "memory");
+		PROF_T(t3);
+#if LHIP_PROF
+		pw += t1 - t0;
+		pb += t2 - t1;
+		pc += t3 - t2;
+#endif
 		slot = slot == NSTAGE - 1 ? 0 : slot + 1;
-		if (++cur_s != S) continue;
+		if (!tile_end) {
+			++cur_s;
+			continue;
+		}
 		cur_s = 0;
 		const int ti = cur_t++;
+		if (LHIP_EARLY_REFILL && S > 2 && iss_g < G && iss_g == g + 3) {
+			// every wave is done with this stage's slot: refill it before the
+			// epilogue, so all NSTAGE slots stream while the epilogue runs.
+			// (S > 2: stage g+3 is then stage 2 of the next tile, carrying no
+			// row aux; with S == 2 it would be stage 0 of tile ti+2, whose row
+			// aux DMA targets the slot this epilogue reads.)
+			__builtin_amdgcn_s_barrier();
+			asm volatile("" ::: "memory");
+			issue_next();
+		}
 
 		// ---- epilogue of tile ti (its row aux landed with its stage 0) ------
 		const int64_t tile = (int64_t)blockIdx.x + (int64_t)ti * gridDim.x;
 		const int64_t row0 = tile * tile_stride * BR;
-		const float4 *RA = reinterpret_cast<const float4 *>(smem + RING_BYTES + (ti & 1) * RA_SLOT);
-		const float4 qa0 = QA[ql0], qa1 = QA[ql1];
+		// row aux of the tile (SoA): alpha [0,256), xn [256,512), ux [512,768), sc [768,1024)
+		const float *RAs = reinterpret_cast<const float *>(smem + RING_BYTES + (ti & 1) * RA_SLOT);
+		auto ra4 = [&](int r0, int c) { return *reinterpret_cast<const float4 *>(RAs + c * BR + r0); };
+		const int eln = lane_id_fresh();
+		const int qlb = wq * 128 + (eln & 31);  // tile-local query of acc[.][u]: qlb + 32u
+		const int rb = wr * 64 + 4 * (eln >> 5); // tile-local row of acc[t][.] reg r: rb + 32t + (r&3) + 8(r>>2)
 		if (LHIP_ABL_NO_EPILOGUE) {
-			if (acc00[0] == 12345.f && acc11[3] == 54321.f && acc01[1] == acc10[2]) seg_cnt[0] = 1;
+			if (acc[0][0][0] == 12345.f && acc[1][3][3] == 54321.f && acc[0][1][1] == acc[1][2][2]) seg_cnt[0] = 1;
 		} else if (MODE == 0) {
-			const bool qv0 = q0 + ql0 < nq, qv1 = q0 + ql1 < nq;
 #pragma unroll
-			for (int gq = 0; gq < 4; ++gq) {
-				const int r0 = rb + 8 * gq, r1 = rb + 32 + 8 * gq;
-				if (qv0) {
-					float *dst = dense + (int64_t)(q0 + ql0) * ld_out + tile * BR;
-					*reinterpret_cast<float4 *>(dst + r0) =
-					    make_float4(lower_bound<METRIC>(acc00[4 * gq + 0], RA[r0 + 0], qa0),
-					                lower_bound<METRIC>(acc00[4 * gq + 1], RA[r0 + 1], qa0),
-					                lower_bound<METRIC>(acc00[4 * gq + 2], RA[r0 + 2], qa0),
-					                lower_bound<METRIC>(acc00[4 * gq + 3], RA[r0 + 3], qa0));
-					*reinterpret_cast<float4 *>(dst + r1) =
-					    make_float4(lower_bound<METRIC>(acc10[4 * gq + 0], RA[r1 + 0], qa0),
-					                lower_bound<METRIC>(acc10[4 * gq + 1], RA[r1 + 1], qa0),
-					                lower_bound<METRIC>(acc10[4 * gq + 2], RA[r1 + 2], qa0),
-					                lower_bound<METRIC>(acc10[4 * gq + 3], RA[r1 + 3], qa0));
-				}
-				if (qv1) {
-					float *dst = dense + (int64_t)(q0 + ql1) * ld_out + tile * BR;
-					*reinterpret_cast<float4 *>(dst + r0) =
-					    make_float4(lower_bound<METRIC>(acc01[4 * gq + 0], RA[r0 + 0], qa1),
-					                lower_bound<METRIC>(acc01[4 * gq + 1], RA[r0 + 1], qa1),
-					                lower_bound<METRIC>(acc01[4 * gq + 2], RA[r0 + 2], qa1),
-					                lower_bound<METRIC>(acc01[4 * gq + 3], RA[r0 + 3], qa1));
-					*reinterpret_cast<float4 *>(dst + r1) =
-					    make_float4(lower_bound<METRIC>(acc11[4 * gq + 0], RA[r1 + 0], qa1),
-					                lower_bound<METRIC>(acc11[4 * gq + 1], RA[r1 + 1], qa1),
-					                lower_bound<METRIC>(acc11[4 * gq + 2], RA[r1 + 2], qa1),
-					                lower_bound<METRIC>(acc11[4 * gq + 3], RA[r1 + 3], qa1));
-				}
+			for (int u = 0; u < 4; ++u) {
+				const int ql = qlb + 32 * u;
+				if (q0 + ql >= nq) continue;
+				const float4 qa = QA[ql];
+				float *dst = dense + (int64_t)(q0 + ql) * ld_out + tile * BR;
+#pragma unroll
+				for (int t = 0; t < 2; ++t)
+#pragma unroll
+					for (int gq = 0; gq < 4; ++gq) {
+						const int r0 = rb + 32 * t + 8 * gq;
+						if (FOLD) {
+							*reinterpret_cast<float4 *>(dst + r0) = make_float4(
+							    acc[t][u][4 * gq + 0], acc[t][u][4 * gq + 1], acc[t][u][4 * gq + 2], acc[t][u][4 * gq + 3]);
+							continue;
+						}
+						const float4 al = ra4(r0, 0), xn = ra4(r0, 1), ux = ra4(r0, 2), sc = ra4(r0, 3);
+						*reinterpret_cast<float4 *>(dst + r0) = make_float4(
+						    lower_bound<METRIC>(acc[t][u][4 * gq + 0], make_float4(al.x, xn.x, ux.x, sc.x), qa),
+						    lower_bound<METRIC>(acc[t][u][4 * gq + 1], make_float4(al.y, xn.y, ux.y, sc.y), qa),
+						    lower_bound<METRIC>(acc[t][u][4 * gq + 2], make_float4(al.z, xn.z, ux.z, sc.z), qa),
+						    lower_bound<METRIC>(acc[t][u][4 * gq + 3], make_float4(al.w, xn.w, ux.w, sc.w), qa));
+					}
 			}
 		} else {
-			// epilogue-only values are made opaque here so the compiler cannot
-			// hoist them out of the tile loop (they would stay live through the
-			// MFMA loop and spill at the 128-VGPR cap of a 1024-thread block)
-			int segc = seg_cap, nqq = nq;
-			asm volatile("" : "+s"(segc), "+s"(nqq));
-			const float t0 = TAU[ql0], t1 = TAU[ql1];
-			const uint32_t slot0 = (uint32_t)(row0 + rb);
-			const int64_t sb0 = ((int64_t)blockIdx.x * nqq + q0 + ql0) * segc;
-			const int64_t sb1 = sb0 + (int64_t)32 * segc;
+			// tau = +inf (fewer live sample rows than needed) must still drop
+			// dead rows (LB = +inf): compare against min(tau, FLT_MAX)
+			float4 qa[4];
+			float tq[4];
 #pragma unroll
-			for (int r = 0; r < 16; ++r) {
-				const int rl = (r & 3) + 8 * (r >> 2);
-				const float4 x0 = RA[rb + rl], x1 = RA[rb + 32 + rl];
-				float l;
-				l = lower_bound<METRIC>(acc00[r], x0, qa0);
-				if (l <= t0 && l < F_INF) {
-					const unsigned p = atomicAdd(&CNT[ql0], 1u);
-					if (p < (unsigned)segc) seg_pool[sb0 + p] = make_uint2(fkey(l), slot0 + rl);
-				}
-				l = lower_bound<METRIC>(acc10[r], x1, qa0);
-				if (l <= t0 && l < F_INF) {
-					const unsigned p = atomicAdd(&CNT[ql0], 1u);
-					if (p < (unsigned)segc) seg_pool[sb0 + p] = make_uint2(fkey(l), slot0 + 32 + rl);
-				}
-				l = lower_bound<METRIC>(acc01[r], x0, qa1);
-				if (l <= t1 && l < F_INF) {
-					const unsigned p = atomicAdd(&CNT[ql1], 1u);
-					if (p < (unsigned)segc) seg_pool[sb1 + p] = make_uint2(fkey(l), slot0 + rl);
-				}
-				l = lower_bound<METRIC>(acc11[r], x1, qa1);
-				if (l <= t1 && l < F_INF) {
-					const unsigned p = atomicAdd(&CNT[ql1], 1u);
-					if (p < (unsigned)segc) seg_pool[sb1 + p] = make_uint2(fkey(l), slot0 + 32 + rl);
-				}
+			for (int u = 0; u < 4; ++u) {
+				qa[u] = QA[qlb + 32 * u];
+				tq[u] = fminf(TAU[qlb + 32 * u], F_MAX);
 			}
-		}
+			// Per group of 4 rows x 4 queries (16 bounds per lane): the bounds
+			// of two consecutive rows are one v_pk_fma_f32 chain (row terms are
+			// SoA; per-lane results identical to the scalar formula), one
+			// ballot per bound; positions in the wave's list from mbcnt.  A
+			// list that fills (rare) sends further survivors straight to their
+			// segment.
+			int nl = 0;  // survivors of this tile so far (wave-uniform)
+			int nw = 0;  // of which in the list: entries [0, nw) are written
 #pragma unroll
-		for (int r = 0; r < 16; ++r) {
-			acc00[r] = 0.f;
-			acc01[r] = 0.f;
-			acc10[r] = 0.f;
-			acc11[r] = 0.f;
+			for (int t = 0; t < 2; ++t)
+#pragma unroll
+				for (int gq = 0; gq < 4; ++gq) {
+					const int r0 = rb + 32 * t + 8 * gq;
+					float l[4][4];
+					uint64_t m[4][4], any = 0;
+					if (FOLD) {
+#pragma unroll
+						for (int j = 0; j < 4; ++j)
+#pragma unroll
+							for (int u = 0; u < 4; ++u) {
+								l[j][u] = acc[t][u][4 * gq + j];
+								m[j][u] = __builtin_amdgcn_ballot_w64(l[j][u] <= tq[u]);
+								any |= m[j][u];
+							}
+					}
+					const float4 al = FOLD ? make_float4(0.f, 0.f, 0.f, 0.f) : ra4(r0, 0);
+					const float4 xn = FOLD ? al : ra4(r0, 1), ux = FOLD ? al : ra4(r0, 2);
+					const float4 sc = (METRIC == METRIC_COSINE) ? ra4(r0, 3) : make_float4(1.f, 1.f, 1.f, 1.f);
+#pragma unroll
+					for (int u = 0; u < 4 && !FOLD; ++u) {
+						const f32x2 Bq = {qa[u].z, qa[u].z}, Aq = {qa[u].y, qa[u].y}, Sq = {qa[u].x, qa[u].x};
+						const f32x2 Cq = {qa[u].w, qa[u].w};
+#pragma unroll
+						for (int p = 0; p < 2; ++p) {
+							const f32x2 a2 = p ? f32x2{al.z, al.w} : f32x2{al.x, al.y};
+							const f32x2 x2 = p ? f32x2{xn.z, xn.w} : f32x2{xn.x, xn.y};
+							const f32x2 u2 = p ? f32x2{ux.z, ux.w} : f32x2{ux.x, ux.y};
+							f32x2 s2 = {acc[t][u][4 * gq + 2 * p], acc[t][u][4 * gq + 2 * p + 1]};
+							if (METRIC == METRIC_COSINE) s2 = s2 * (p ? f32x2{sc.z, sc.w} : f32x2{sc.x, sc.y});
+							// = lower_bound(): alpha + xn*B + ux*A + (s*sc)*S + C
+							f32x2 y = __builtin_elementwise_fma(x2, Bq, a2);
+							y = __builtin_elementwise_fma(u2, Aq, y);
+							y = __builtin_elementwise_fma(s2, Sq, y);
+							y = y + Cq;
+							l[2 * p][u] = y.x;
+							l[2 * p + 1][u] = y.y;
+							m[2 * p][u] = __builtin_amdgcn_ballot_w64(y.x <= tq[u]);
+							m[2 * p + 1][u] = __builtin_amdgcn_ballot_w64(y.y <= tq[u]);
+							any |= m[2 * p][u] | m[2 * p + 1][u];
+						}
+					}
+					if (LHIP_ABL_NO_SLOW) {
+						asm volatile("" ::"s"(any));  // masks computed, nothing written
+					} else if (any) {
+#if LHIP_PROF
+						const uint64_t ts0 = __builtin_amdgcn_s_memtime();
+#endif
+						// Rare: each bound with a survivor in the wave appends the
+						// raw LB bits of its lanes at nl + (lanes below); the key
+						// conversion happens at write-out.  A scalar loop over the
+						// bounds that have survivors, with a uniform switch picking
+						// the bound: compact code (the epilogue must stay resident
+						// in the instruction cache; 16 unrolled copies per group
+						// would not).
+						uint32_t kmask = 0;
+#pragma unroll
+						for (int k = 0; k < 16; ++k) kmask |= (m[k >> 2][k & 3] != 0ull ? 1u : 0u) << k;
+						while (kmask) {
+							const int k = __builtin_ctz(kmask);
+							kmask &= kmask - 1;
+							uint64_t mm = 0;
+							float lv = 0.f;
+							switch (k) {
+#define LHIP_PICK(K)                         \
+	case K:                                  \
+		mm = m[(K) >> 2][(K)&3];             \
+		lv = l[(K) >> 2][(K)&3];             \
+		break;
+								LHIP_PICK(0) LHIP_PICK(1) LHIP_PICK(2) LHIP_PICK(3) LHIP_PICK(4) LHIP_PICK(5)
+								LHIP_PICK(6) LHIP_PICK(7) LHIP_PICK(8) LHIP_PICK(9) LHIP_PICK(10) LHIP_PICK(11)
+								LHIP_PICK(12) LHIP_PICK(13) LHIP_PICK(14) LHIP_PICK(15)
+#undef LHIP_PICK
+							}
+							const int qv = qlb + 32 * (k & 3), rr = r0 + (k >> 2);
+							const int cntm = __builtin_popcountll(mm);
+							if (nl + cntm <= WLIST) {
+								const int pos = nl + __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32),
+								                                               __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+								if ((mm >> eln) & 1ull)
+									wlist[pos] = make_uint2(__float_as_uint(lv), ((uint32_t)qv << 18) | ((uint32_t)rr << 10));
+								nw = nl + cntm;
+							} else {
+								overflow(mm, lv, qv, rr, row0);
+							}
+							nl += cntm;
+						}
+#if LHIP_PROF
+						prof_slow += __builtin_amdgcn_s_memtime() - ts0;
+						++prof_slown;
+#endif
+					}
+					__builtin_amdgcn_sched_barrier(0);
+				}
+			n_list = nw;
+#if LHIP_PROF
+			prof_surv += nl;
+			prof_over += nl > WLIST ? nl - WLIST : 0;
+#endif
 		}
+#if LHIP_PROF
+		PROF_T(t4);
+		pe += t4 - t3;
+#endif
 	}
+#if LHIP_PROF
+	if (lane == 0) {
+		atomicAdd(&lhip_prof[MODE * 8 + 0], (unsigned long long)pw);
+		atomicAdd(&lhip_prof[MODE * 8 + 1], (unsigned long long)pb);
+		atomicAdd(&lhip_prof[MODE * 8 + 2], (unsigned long long)pc);
+		atomicAdd(&lhip_prof[MODE * 8 + 3], (unsigned long long)pe);
+		atomicAdd(&lhip_prof[MODE * 8 + 4], 1ull);
+		atomicAdd(&lhip_prof[MODE * 8 + 5], (unsigned long long)G);
+		atomicAdd(&lhip_prof[MODE * 8 + 6], (unsigned long long)cur_t);
+		atomicAdd(&lhip_prof[16 + MODE * 2 + 0], (unsigned long long)prof_surv);
+		atomicAdd(&lhip_prof[16 + MODE * 2 + 1], (unsigned long long)prof_over);
+		atomicAdd(&lhip_prof[20 + MODE * 2 + 0], (unsigned long long)prof_slow);
+		atomicAdd(&lhip_prof[20 + MODE * 2 + 1], (unsigned long long)prof_slown);
+	}
+#endif
 	if (MODE == 1) {
-		__syncthreads();
+		if (n_list > 0) write_list(cur_t - 1);  // the last tile's survivors
+		__syncthreads();                         // every wave's counter updates
 		if (tid < BQ && q0 + tid < nq) seg_cnt[(int64_t)blockIdx.x * nq + q0 + tid] = (int)CNT[tid];
 	}
 }
@@ -606,6 +960,7 @@ void launch_scan_append(const StoreView &s, const QueryView &q, const float *tau
                         int seg_cap, hipStream_t st) {
 	int64_t n_tiles = (s.n_slots + BR - 1) / BR;
 	if (n_tiles <= 0) return;
+	if (seg_cap <= 0 || seg_cap > 1024) throw std::runtime_error("scan: segment capacity must be in [1, 1024]");
 	scan_dispatch<1>(s, q, n_tiles, 1, nullptr, 0, tau, seg_pool, seg_cnt, seg_cap, st);
 }
 
@@ -967,15 +1322,22 @@ __global__ __launch_bounds__(256) void finalize_kernel(const int64_t *__restrict
 	if (t == 0) s_dk = F_INF;
 	__syncthreads();
 	if (mode == 0) {
-		// tau = largest exact distance among the candidates (they are real rows)
-		if (t == 0) {
-			float mx = -F_INF;
-			bool nan = false;
-			for (int i = 0; i < m; ++i) {
-				if (__builtin_isnan(sd[i])) nan = true;
-				mx = fmaxf(mx, sd[i]);
-			}
-			tau[q] = (m >= need_for_tau && m > 0) ? (nan ? __builtin_nanf("") : mx) : F_INF;
+		// tau = the need_for_tau-th smallest exact distance among the
+		// candidates: they are real rows, so any need_for_tau (>= k) of them
+		// bound the true k-th distance from above.  Fewer than that: +inf; a
+		// NaN distance: NaN (nothing survives; the certificate sends the query
+		// to the exact fallback).
+		bool nan = false;
+		for (int i = 0; i < m; ++i) nan |= __builtin_isnan(sd[i]);
+		if (m < need_for_tau || m == 0 || nan) {
+			if (t == 0) tau[q] = nan ? __builtin_nanf("") : F_INF;
+			return;
+		}
+		for (int i = t; i < m; i += 256) {
+			int rank = 0;
+			const float d = sd[i];
+			for (int j = 0; j < m; ++j) rank += (sd[j] < d || (sd[j] == d && j < i)) ? 1 : 0;
+			if (rank == need_for_tau - 1) tau[q] = d;
 		}
 		return;
 	}
@@ -1030,7 +1392,7 @@ __global__ __launch_bounds__(256) void exact_all_kernel(const float *__restrict_
 	if (r >= n) return;
 	float d = exact_distance<METRIC>(X + r * ld, q, dim, lane);
 	if (lane == 0) {
-		const float a = rowaux[r].x;
+		const float a = reinterpret_cast<const float *>(rowaux)[raix(r, 0)];
 		const bool dead = (a == F_INF);
 		keys[r] = dead ? __uint_as_float(0x7FFFFFFFu) : d;
 		vals[r] = labels[r];
@@ -1151,7 +1513,10 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float *__restric
 	for (int i = lane * 4; i < ld; i += 256)
 		*reinterpret_cast<float4 *>(Xo + r * ld + i) = *reinterpret_cast<const float4 *>(X + s * ld + i);
 	if (lane == 0) {
-		rowaux_o[r] = rowaux[s];
+		const float *ri = reinterpret_cast<const float *>(rowaux);
+		float *ro = reinterpret_cast<float *>(rowaux_o);
+#pragma unroll
+		for (int c = 0; c < 4; ++c) ro[raix(r, c)] = ri[raix(s, c)];
 		labels_o[r] = labels[s];
 	}
 }

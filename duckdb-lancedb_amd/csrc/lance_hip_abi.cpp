@@ -145,6 +145,7 @@ struct Index {
 
 	// optional HIP-event timing of the scan kernels, on the stream they run on
 	bool time_kernels = false;
+	int sample_div = 32;  // sample pass covers ~1/sample_div of the tiles (>= 32 tiles)
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 	double kt_append_ms = 0.0, kt_dense_ms = 0.0;
 	int64_t kt_append_n = 0, kt_dense_n = 0;
@@ -202,11 +203,12 @@ struct Index {
 		if (rowaux_l2 || (metric_quirk && metric != METRIC_L2)) HIPCHK(hipMalloc(&na2, (size_t)c * sizeof(float4)));
 		if (n_slots > 0) {
 			HIPCHK(hipMemcpyAsync(nX, X, (size_t)n_slots * ld * sizeof(float), hipMemcpyDeviceToDevice, stream));
-			HIPCHK(hipMemcpyAsync(na, rowaux, (size_t)n_slots * sizeof(float4), hipMemcpyDeviceToDevice, stream));
+			// row aux is tile-blocked SoA: move whole tile blocks (cap is a
+			// multiple of SCAN_BR, so they exist in the old buffer)
+			const size_t aux_bytes = (size_t)round_up(n_slots, SCAN_BR) * sizeof(float4);
+			HIPCHK(hipMemcpyAsync(na, rowaux, aux_bytes, hipMemcpyDeviceToDevice, stream));
 			HIPCHK(hipMemcpyAsync(nl, dlabels, (size_t)n_slots * sizeof(int64_t), hipMemcpyDeviceToDevice, stream));
-			if (na2 && rowaux_l2)
-				HIPCHK(hipMemcpyAsync(na2, rowaux_l2, (size_t)n_slots * sizeof(float4), hipMemcpyDeviceToDevice,
-				                      stream));
+			if (na2 && rowaux_l2) HIPCHK(hipMemcpyAsync(na2, rowaux_l2, aux_bytes, hipMemcpyDeviceToDevice, stream));
 		}
 		HIPCHK(hipMemsetAsync(nX + n_slots * ld, 0, (size_t)(c - n_slots) * ld * sizeof(float), stream));
 		launch_fill_rowaux(na, n_slots, c, stream);
@@ -444,7 +446,8 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		}
 	} else if (fast_ok) {
 		// 1) sample pass: dense LB over every stride-th tile -> tau[q]
-		const int64_t n_sample = std::min<int64_t>(n_tiles, std::max<int64_t>((n_tiles + 63) / 64, 32));
+		const int64_t n_sample =
+		    std::min<int64_t>(n_tiles, std::max<int64_t>((n_tiles + sample_div - 1) / sample_div, 32));
 		const int64_t stride = std::max<int64_t>(1, n_tiles / n_sample);
 		const int64_t cols = n_sample * SCAN_BR;
 		const int Ms = k + 8;
@@ -452,12 +455,12 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		launch_scan_dense(sv, qv, n_sample, stride, ws.dense.p, cols, stream);
 		launch_select_dense(ws.dense.p, cols, cols, stride, nq, Ms, ws.cand_slot.p, d_cand_cnt, ws.cut.p, stream);
 		launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Ms, ws.cand_dist.p, stream);
-		launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Ms, k, 0, k + 1, ws.tau.p,
+		launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Ms, k, 0, k, ws.tau.p,
 		                nullptr, nullptr, nullptr, nullptr, stream);
 		// 2) threshold scan over every row into per-(workgroup, query) segments;
 		//    a segment holds ~4x its expected share of the (k+8)*N/sample pool
 		const int n_seg = scan_grid(n_tiles);
-		const int64_t expect = (int64_t)(k + 8) * ((n_tiles + n_sample - 1) / n_sample);
+		const int64_t expect = (int64_t)(k + 4) * ((n_tiles + n_sample - 1) / n_sample);
 		const int seg_cap = (int)std::min<int64_t>(1024, round_up(std::max<int64_t>(64, 4 * expect / n_seg), 32));
 		ws.seg_pool.need((size_t)n_seg * nq * seg_cap);
 		ws.seg_cnt.need((size_t)n_seg * nq);
@@ -1009,6 +1012,12 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 				if (!e) HIPCHK(hipEventCreate(&e));
 			ix->kt_append_ms = ix->kt_dense_ms = 0.0;
 			ix->kt_append_n = ix->kt_dense_n = 0;
+			return 0;
+		}
+		if (k == "sample_div") {
+			const int d = std::stoi(v);
+			if (d < 1) throw Error("sample_div must be >= 1");
+			ix->sample_div = d;
 			return 0;
 		}
 		if (k == "reserve_rows") {

@@ -28,7 +28,7 @@ import numpy as np
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "lib", "liblancedb_hip.so")
 # development override (ablation builds); the shipped path is LIB_PATH
-LIB_PATH = os.environ.get("LANCE_HIP_LIB", LIB_PATH)
+LIB_PATH = os.environ.get("LANCE_HIP_LIB") or LIB_PATH
 ERR_BUF_LEN = 2048  # rust_ffi.cpp:44
 
 _lib = None

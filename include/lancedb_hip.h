@@ -145,11 +145,16 @@ const char *lance_hip_version(void);
 /* Number of HIP devices visible to the library (0 when none / no driver). */
 int32_t lance_hip_device_count(void);
 
-/* Per-handle options, key/value strings:
- *   "device"       HIP device ordinal for the store (default: current device)
+/* Per-handle options, key/value strings (unknown keys: error, -1):
  *   "metric_quirk" "1" = rank every search by squared L2 whatever the index
  *                  metric, exactly as the reference does (lance_manager.rs:
  *                  411-418 never sets distance_type); default "0"
+ *   "reserve_rows" pre-size the device store for this many rows
+ *   "sample_div"   the threshold sample pass covers ~1/sample_div of the row
+ *                  tiles (at least 32 tiles); default "32"
+ *   "time_kernels" "1" = record HIP events around scan launches
+ *                  (lance_hip_kernel_times); default "0"
+ * The handle is bound to the HIP device current when it was created.
  * Returns 0 or -1. */
 int32_t lance_hip_set_option(void *handle, const char *key, const char *value, char *err_buf, int err_buf_len);
 

@@ -1,0 +1,34 @@
+#!/bin/bash
+# Development-only: builds timing-ablation variants of the scan kernel into abl/
+# (results are wrong by design; used with LANCE_HIP_LIB=abl/lib_<NAME>.so bench.py)
+set -e
+cd "$(dirname "$0")/.."
+D=duckdb-lancedb_amd
+F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-inline-asm -Wno-unused-result"
+hipcc $F -c $D/csrc/lance_hip_abi.cpp -o abl/abi.o
+build() { # name defines...
+	local n=$1; shift
+	hipcc $F "$@" -c $D/csrc/knn_kernels.hip -o abl/k_$n.o
+	hipcc -shared -o abl/lib_$n.so abl/k_$n.o abl/abi.o
+}
+for v in "$@"; do
+	case $v in
+	NO_EPILOGUE) build NO_EPILOGUE -DLHIP_ABL_NO_EPILOGUE=1 ;;
+	NO_MFMA) build NO_MFMA -DLHIP_ABL_NO_MFMA=1 ;;
+	NO_Q) build NO_Q -DLHIP_ABL_NO_Q=1 ;;
+	DMA_ONLY) build DMA_ONLY -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_EPILOGUE=1 ;;
+	NT0) build NT0 -DLHIP_X_NT=0 ;;
+	PROF) build PROF -DLHIP_PROF=1 ;;
+	NOSLOW) build NOSLOW -DLHIP_ABL_NO_SLOW=1 ;;
+	NOFLUSH) build NOFLUSH -DLHIP_ABL_NO_FLUSH=1 ;;
+	PROFER0) build PROFER0 -DLHIP_PROF=1 -DLHIP_EARLY_REFILL=0 ;;
+	ER1) build ER1 -DLHIP_EARLY_REFILL=1 ;;
+	ER0) build ER0 -DLHIP_EARLY_REFILL=0 ;;
+	RF0) build RF0 -DLHIP_READS_FIRST=0 ;;
+	PREV) # the committed (HEAD) kernel file, for same-box A/B timing
+		git show HEAD:$D/csrc/knn_kernels.hip > abl/prev_kernels.hip
+		hipcc $F -I$D/csrc -c abl/prev_kernels.hip -o abl/k_PREV.o
+		hipcc -shared -o abl/lib_PREV.so abl/k_PREV.o abl/abi.o ;;
+	*) echo "unknown $v"; exit 1 ;;
+	esac
+done
