@@ -35,6 +35,15 @@ for _p in (ROOT, PKG):
 import lance_hip  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+MFMA_BF16_PEAK_TFS = 2500.0  # dense bf16 MFMA (no sparsity), same table
+
+# --config presets (BASELINE.json configs): c2 is the headline line the driver
+# runs; c3 = "Flat inner-product bf16 on MFMA, 10Mx768, k=100" (bf16-stored base,
+# L2-normalized base and queries so that IP and L2 rankings coincide).
+CONFIGS = {
+    "c2": dict(n=1_000_000, dim=768, k=10, batch=256, metric="l2", storage="f32", normalize=False),
+    "c3": dict(n=10_000_000, dim=768, k=100, batch=256, metric="dot", storage="bf16", normalize=True),
+}
 GEN_CHUNK = 65536
 
 
@@ -43,22 +52,28 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=1_000_000)
-    ap.add_argument("--dim", type=int, default=768)
-    ap.add_argument("--k", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--metric", default="l2")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--dim", type=int, default=None)
+    ap.add_argument("--k", type=int, default=None)
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--metric", default=None)
     ap.add_argument("--recall-queries", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-recall", action="store_true")
     ap.add_argument("--sample-div", type=int, default=None, help="index option sample_div (default: library's)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    for key, v in CONFIGS[a.config].items():
+        if getattr(a, key, None) is None:
+            setattr(a, key, v)
+    return a
 
 
-def gen_rows(start, stop, dim, device, seed=1234):
+def gen_rows(start, stop, dim, device, seed=1234, normalize=False):
     """Rows [start, stop) of the synthetic N(0,1) base, identical whatever the
-    sharding: chunk c of GEN_CHUNK rows comes from generator seed (seed, c)."""
+    sharding: chunk c of GEN_CHUNK rows comes from generator seed (seed, c).
+    normalize: each row scaled to unit L2 norm (C3)."""
     out = torch.empty((stop - start, dim), dtype=torch.float32, device=device)
     c0, c1 = start // GEN_CHUNK, (stop - 1) // GEN_CHUNK
     g = torch.Generator(device=device)
@@ -67,6 +82,8 @@ def gen_rows(start, stop, dim, device, seed=1234):
         chunk = torch.randn((GEN_CHUNK, dim), generator=g, device=device, dtype=torch.float32)
         lo, hi = max(start, c * GEN_CHUNK), min(stop, (c + 1) * GEN_CHUNK)
         out[lo - start:hi - start] = chunk[lo - c * GEN_CHUNK:hi - c * GEN_CHUNK]
+    if normalize:
+        out /= torch.linalg.vector_norm(out, dim=1, keepdim=True)
     return out
 
 
@@ -115,12 +132,13 @@ def main():
     h = L.lance_create_detached(b"", D, a.metric.encode(), b"bench", e, 2048)
     if not h:
         raise RuntimeError(e.value.decode())
+    lance_hip.LanceHipSetOption(h, "storage", a.storage)
     lance_hip.LanceHipSetOption(h, "reserve_rows", str(n_local))
     if a.sample_div:
         lance_hip.LanceHipSetOption(h, "sample_div", str(a.sample_div))
     for lo in range(s0, s1, 1 << 18):
         hi = min(s1, lo + (1 << 18))
-        X = gen_rows(lo, hi, D, dev)
+        X = gen_rows(lo, hi, D, dev, normalize=a.normalize)
         torch.cuda.synchronize()
         r = L.lance_hip_add_batch_device(h, X.data_ptr(), hi - lo, D, e, 2048)
         if r < 0:
@@ -129,6 +147,8 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(5678)
     Q = torch.randn((B, D), generator=g, device=dev, dtype=torch.float32)
+    if a.normalize:
+        Q /= torch.linalg.vector_norm(Q, dim=1, keepdim=True)
     from lance_hip.sharded import ShardedSearch, hip_device_merge, hip_device_search
 
     searcher = ShardedSearch(hip_device_search(L, h, D), hip_device_merge(L), label_offset=s0, dist=dist,
@@ -171,12 +191,17 @@ def main():
         Xh = np.empty((N, D), np.float32)
         for lo in range(0, N, 1 << 18):
             hi = min(N, lo + (1 << 18))
-            Xh[lo:hi] = gen_rows(lo, hi, D, dev).cpu().numpy()
+            Xr = gen_rows(lo, hi, D, dev, normalize=a.normalize)
+            if a.storage == "bf16":  # the stored rows: nearest-even bf16 of the added rows
+                Xr = Xr.to(torch.bfloat16).float()
+            Xh[lo:hi] = Xr.cpu().numpy()
+            del Xr
         Qh = Q.cpu().numpy()
         nr = min(a.recall_queries, B)
         nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
         el, ed, _ = c_oracle.flat_search_batch(Xh, Qh[:nr], K, a.metric, acc64=True, nthreads=nthreads)
         recall = flat_knn.recall_at_k(res_l[:nr], el, min(10, K))
+        recall_k = flat_knn.recall_at_k(res_l[:nr], el, K)
         exact_ids = bool((res_l[:nr] == el).all())
         max_rel = float(np.max(np.abs(res_d[:nr] - ed) / np.maximum(np.abs(ed), 1e-30)))
         if world == 1 and not a.no_cpu_baseline:
@@ -190,8 +215,8 @@ def main():
                     break
             t_cpu = time.perf_counter() - t_cpu0
             cpu = {"value": done / t_cpu, "unit": "queries/s", "cores": nthreads, "kind": "port",
-                   "sample": f"{done} queries, one per call, each an exact f32 scan of all {N}x{D} rows "
-                             f"({t_cpu:.1f} s, oracle/flat_knn.c, {nthreads} OpenMP threads)"}
+                   "sample": f"{done} queries, one per call, each an exact f32 {a.metric} scan of all {N}x{D} "
+                             f"rows ({t_cpu:.1f} s, oracle/flat_knn.c, {nthreads} OpenMP threads)"}
         del Xh
 
     if rank == 0:
@@ -200,15 +225,23 @@ def main():
         roof = None
         if kt["scan_launches"] > 0:
             ld = ((D + 63) // 64) * 64
+            esz = 2 if a.storage == "bf16" else 4
             avg_ms = kt["scan_ms_total"] / kt["scan_launches"]
-            bytes_launch = kt["scan_rows"] * (ld * 4 + 16) + kt["scan_qpad"] * ld * 2
+            # algorithmic bytes per launch: every base row (ld elements + 16 B row aux) + the bf16 query tile
+            bytes_launch = kt["scan_rows"] * (ld * esz + 16) + kt["scan_qpad"] * ld * 2
             ach = bytes_launch / (avg_ms * 1e-3) / 1e9
-            traffic = measured_traffic(N // world, D, B)
+            traffic = measured_traffic(N // world, D, B) if a.config == "c2" else None
+            mfma_tfs = 2.0 * kt["scan_rows"] * D * B / (avg_ms * 1e-3) / 1e12
+            kname = {"l2": "L2", "dot": "DOT", "cosine": "COSINE"}[a.metric]
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "scan_kernel<L2,append>",
-                    "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(bytes_launch)}
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "kernel": f"scan_kernel<{kname},append,{a.storage}>",
+                    "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(bytes_launch),
+                    "mfma_tflops": round(mfma_tfs, 1), "mfma_frac": round(mfma_tfs / MFMA_BF16_PEAK_TFS, 4)}
+        metric_name = ("kNN queries/sec + recall@10, 1Mx768 f32 flat; GB/s vs HBM roofline" if a.config == "c2" else
+                       f"kNN queries/sec + recall@{K}, {N // 1_000_000}Mx{D} {a.storage} flat IP; GB/s vs HBM roofline")
         line = {
-            "metric": "kNN queries/sec + recall@10, 1Mx768 f32 flat; GB/s vs HBM roofline",
+            "metric": metric_name,
             "value": round(value, 1),
             "unit": "queries/s",
             "n_gpus": world,
@@ -218,16 +251,19 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic N(0,1) base (seeded torch Philox), independent N(0,1) queries",
-            "config": {"workload": f"C2 flat {a.metric} {N}x{D} f32 k={K} query-batch={B}", "n": N, "dim": D,
-                       "k": K, "global_batch": B, "metric": a.metric, "parallelism": f"rowshard{world}"},
+            "dtype": a.storage,
+            "data": "synthetic N(0,1) base (seeded torch Philox), independent N(0,1) queries"
+                    + (", rows and queries L2-normalized; base stored as bf16 (RNE)" if a.config == "c3" else ""),
+            "config": {"workload": f"{a.config.upper()} flat {a.metric} {N}x{D} {a.storage} k={K} query-batch={B}",
+                       "n": N, "dim": D, "k": K, "global_batch": B, "metric": a.metric, "storage": a.storage,
+                       "parallelism": f"rowshard{world}"},
             "recall_at_10": recall,
             "roofline": roof,
             "cpu_baseline": cpu,
             "search_stats": st,
         }
         if recall is not None:
+            line[f"recall_at_{K}"] = recall_k
             line["exact_ids_on_recall_subset"] = exact_ids
             line["max_rel_dist_err"] = max_rel
         print(json.dumps(line), flush=True)

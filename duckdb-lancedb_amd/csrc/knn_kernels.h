@@ -17,19 +17,20 @@ constexpr int MAX_CAND = 256; // max refined candidates per query per pass
 
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
-// Per-row auxiliary data kept beside the f32 rows (one float4 per slot):
+// Per-row auxiliary data kept beside the rows (16 B per slot, tile-blocked SoA):
 //   x = alpha (f32 |x|^2 for l2, 0 otherwise; +inf = tombstone / padding)
 //   y = xn    (|x| for l2/dot, 0 for cosine)
 //   z = ux    (upper bound of |bf16(x)| + |x - bf16(x)|; cosine: divided by |x|)
 //   w = sc    (1 for l2/dot, 1/|x| for cosine)
 struct StoreView {
-	const float *X;          // [n_slots][ld] f32 rows, zero padded to ld
+	const void *X;           // [n_slots][ld] rows, zero padded to ld: f32, or bf16 bits when xbf16
 	const float4 *rowaux;    // [n_slots rounded up to SCAN_BR], tile-blocked SoA (raix() in knn_kernels.hip)
 	const int64_t *labels;   // [n_slots] slot -> label
 	int64_t n_slots;
 	int ld;                  // padded row stride (floats), multiple of DPAD
 	int dim;
 	int metric;
+	int xbf16;               // base stored as bf16 (storage option "bf16")
 };
 
 // Per-query constants for the lower-bound epilogue:
@@ -45,8 +46,13 @@ struct QueryView {
 // ---- ingest ------------------------------------------------------------------
 // Computes rowaux for slots [s0, s0+n) of a store (f64 norms, bf16 error norms),
 // and folds max(alpha), max(ux) into stats[0], stats[1] (as float bits).
-void launch_rowaux(const float *X, int ld, int dim, int metric, int64_t s0, int64_t n, float4 *rowaux,
+// X holds f32 rows, or bf16 bits when xbf16.
+void launch_rowaux(const void *X, int xbf16, int ld, int dim, int metric, int64_t s0, int64_t n, float4 *rowaux,
                    unsigned *stats, hipStream_t st);
+
+// Rounds n f32 rows (stride src_ld) to bf16 (round to nearest even) into
+// dst rows of stride ld, zero-filling columns [dim, ld).
+void launch_rows_to_bf16(const float *src, int64_t src_ld, int64_t n, int dim, int ld, uint16_t *dst, hipStream_t st);
 
 // rowaux[from, to) = (+inf, 0, 0, 0): padding rows past the last slot.
 void launch_fill_rowaux(float4 *rowaux, int64_t from, int64_t to, hipStream_t st);
@@ -116,7 +122,7 @@ void launch_copy_fallback(const float *keys, const int64_t *vals, int64_t n_live
 
 // Gathers slots idx[0..n) of a store into a new store (same ld), in order.
 // Used by lance_detached_compact (drops tombstones, keeps label order).
-void launch_gather_rows(const float *X, const float4 *rowaux, const int64_t *labels, const int64_t *idx, int64_t n,
-                        int ld, float *Xo, float4 *rowaux_o, int64_t *labels_o, hipStream_t st);
+void launch_gather_rows(const void *X, int xbf16, const float4 *rowaux, const int64_t *labels, const int64_t *idx,
+                        int64_t n, int ld, void *Xo, float4 *rowaux_o, int64_t *labels_o, hipStream_t st);
 
 }  // namespace lhip

@@ -76,6 +76,10 @@ __device__ __forceinline__ bool hit_less(float da, int64_t la, float db, int64_t
 // accumulation that truncates instead of rounding.
 static constexpr double U_BOUND = 1.1920928955078125e-07;
 
+// a base element as f32: the store holds f32, or bf16 bits (uint16_t)
+__device__ __forceinline__ float xval(const float *p, int64_t i) { return p[i]; }
+__device__ __forceinline__ float xval(const uint16_t *p, int64_t i) { return __uint_as_float((uint32_t)p[i] << 16); }
+
 // Row aux layout: tile-blocked SoA, 16 B per slot.  For slot r of tile
 // T = r / 256 the four terms live at floats [T*1024 + c*256 + r%256],
 // c = 0 alpha, 1 xn, 2 ux, 3 sc.  A tile's block is the 4 KiB the scan DMAs
@@ -85,16 +89,17 @@ __host__ __device__ __forceinline__ int64_t raix(int64_t r, int c) { return ((r 
 // ---------------------------------------------------------------------------
 // ingest: per-row auxiliary data
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void rowaux_kernel(const float *__restrict__ X, int ld, int dim, int metric,
+template <typename T>
+__global__ __launch_bounds__(256) void rowaux_kernel(const T *__restrict__ X, int ld, int dim, int metric,
                                                      int64_t s0, int64_t n, float4 *__restrict__ rowaux,
                                                      unsigned *__restrict__ stats) {
 	const int lane = threadIdx.x & 63;
 	const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
 	if (r >= n) return;
-	const float *x = X + (s0 + r) * (int64_t)ld;
+	const T *x = X + (s0 + r) * (int64_t)ld;
 	double s2 = 0.0, e2 = 0.0;
 	for (int i = lane; i < dim; i += 64) {
-		float v = x[i];
+		float v = xval(x, i);
 		float e = v - bf16_round(v);
 		s2 += (double)v * v;
 		e2 += (double)e * e;
@@ -126,11 +131,29 @@ __global__ __launch_bounds__(256) void rowaux_kernel(const float *__restrict__ X
 	}
 }
 
-void launch_rowaux(const float *X, int ld, int dim, int metric, int64_t s0, int64_t n, float4 *rowaux,
+void launch_rowaux(const void *X, int xbf16, int ld, int dim, int metric, int64_t s0, int64_t n, float4 *rowaux,
                    unsigned *stats, hipStream_t st) {
 	if (n <= 0) return;
 	int64_t blocks = (n + 3) / 4;
-	rowaux_kernel<<<dim3((unsigned)blocks), dim3(256), 0, st>>>(X, ld, dim, metric, s0, n, rowaux, stats);
+	if (xbf16)
+		rowaux_kernel<<<dim3((unsigned)blocks), dim3(256), 0, st>>>((const uint16_t *)X, ld, dim, metric, s0, n, rowaux,
+		                                                            stats);
+	else
+		rowaux_kernel<<<dim3((unsigned)blocks), dim3(256), 0, st>>>((const float *)X, ld, dim, metric, s0, n, rowaux,
+		                                                            stats);
+}
+
+__global__ __launch_bounds__(256) void rows_to_bf16_kernel(const float *__restrict__ src, int64_t src_ld, int64_t n,
+                                                           int dim, int ld, uint16_t *__restrict__ dst) {
+	const int64_t r = (int64_t)blockIdx.x;
+	if (r >= n) return;
+	for (int i = threadIdx.x; i < ld; i += blockDim.x)
+		dst[r * ld + i] = i < dim ? bf16_bits(src[r * src_ld + i]) : (uint16_t)0;
+}
+
+void launch_rows_to_bf16(const float *src, int64_t src_ld, int64_t n, int dim, int ld, uint16_t *dst, hipStream_t st) {
+	if (n <= 0) return;
+	rows_to_bf16_kernel<<<dim3((unsigned)n), dim3(256), 0, st>>>(src, src_ld, n, dim, ld, dst);
 }
 
 __global__ void fill_rowaux_kernel(float4 *rowaux, int64_t from, int64_t to) {
@@ -244,46 +267,41 @@ void launch_prep_queries(const float *Q, int nq, int dim, int ld, int nq_pad, in
 // makes the ds_read_b128 fragment loads of 32 consecutive rows conflict-free).
 // Global loads of step k+1 are issued before the MFMAs of step k.
 // ---------------------------------------------------------------------------
-constexpr int BR = SCAN_BR, BQ = SCAN_BQ, BK = SCAN_BK;
+constexpr int BR = SCAN_BR, BQ = SCAN_BQ;
 
 // ---------------------------------------------------------------------------
 // scan kernel (persistent, LDS-DMA ring)
 //
-// Tile = 256 base rows x 256 queries.  Workgroup = 1024 threads = 16 waves laid
-// out 4 (base rows) x 4 (queries); each wave owns a 64-row x 64-query sub-tile
-// = 2x2 v_mfma_f32_32x32x16_bf16 tiles (A = base rows, B = queries:
-// accumulator column = lane&31 = query, the 16 registers walk base rows).
-// One workgroup per CU; it walks tiles blockIdx.x, +gridDim.x, ... and the
-// k-stream never stops at a tile boundary: stages of the next tile are
-// already in flight while the current tile's epilogue runs.
+// Tile = 256 base rows x 256 queries.  Workgroup = 512 threads = 8 waves, two
+// per SIMD, laid out 4 (base rows) x 2 (queries): a wave owns 64 rows x 128
+// queries = 2 x 4 v_mfma_f32_32x32x16_bf16 tiles (128 accumulator registers;
+// A = base rows, B = queries: accumulator column = lane&31 = query, the 16
+// registers walk base rows).  One workgroup per CU walks tiles blockIdx.x,
+// +gridDim.x, ...; the k-stream never stops at a tile boundary.
 //
-// The k dimension streams through a ring of NSTAGE LDS stages of SK = 32:
-//   X stage: 256 rows x 32 f32 (32 KiB) straight from HBM by
-//            global_load_lds_dwordx4 (no VGPR staging), rows 128 B,
-//            16 B chunk c of row r stored at c ^ ((r>>1)&7);
-//   Q stage: 256 queries x 32 bf16 (16 KiB) from L2, rows 64 B,
-//            chunk c of row r stored at c ^ ((r>>2)&3);
-//   with stage 0 of a tile: the tile's 256 row-aux float4 (4 KiB, 2 slots).
-// LDS-DMA writes lane-linear, so the swizzle is applied on the per-lane SOURCE
-// address and undone on the ds_read_b128 fragment reads (conflict-free for
-// the b128 lane groups).  A fragments are converted f32 -> bf16 after the read.
-// NSTAGE-1 stages stay in flight; one raw s_barrier per stage behind a counted
-// s_waitcnt vmcnt.  The store is zero-padded (rows) and +inf-padded (row aux)
-// to a multiple of BR rows, so no row is clamped.
+// The k dimension streams in stages of SK = 32 through a ring of NST LDS
+// slots, straight from HBM by global_load_lds_dwordx4 (no VGPR staging):
+//   X stage: 256 rows x 32 base elements: f32 store 32 KiB (rows 128 B, chunk
+//            c of row r at c ^ ((r>>1)&7), nt policy: read once), 3 slots;
+//            bf16 store 16 KiB (rows 64 B, chunk c at c ^ ((r>>2)&3)), 4 slots;
+//   Q stage: 256 queries x 32 bf16 (16 KiB, L2-resident), rows 64 B, chunk c at
+//            c ^ ((r>>2)&3);
+//   with stage 0 of a tile: the tile's row-aux block (4 KiB SoA, 2 slots).
+// LDS-DMA writes lane-linearly, so the swizzle is applied on the per-lane
+// SOURCE address and undone on the ds_read_b128 fragment reads (conflict-free
+// per 16-lane group).  f32 A fragments are converted to bf16 after the read.
+// Stage g is computed while stages g+1 .. g+NST-1 stream; one raw s_barrier
+// per stage behind a counted s_waitcnt vmcnt.  The store is zero-padded (rows)
+// and +inf-padded (row aux) to a multiple of BR rows, so no row is clamped.
 //
-// Epilogue per tile: each accumulator becomes a rigorous lower bound of the
-// exact distance (4 FMAs).  Dense mode stores it.  Append mode keeps (LB, slot)
-// when LB <= tau[q] in the workgroup's private segment for q: the position
-// comes from an LDS counter, the store is fire-and-forget — no global atomic,
-// no barrier, nothing that would drain the DMA queue.
+// L2 / dot fold the bound: each tile's accumulators start at the row/query
+// terms alpha + C + xn*B + ux*A (two exact f32 MFMAs) and the bf16 MFMAs add
+// S*s (queries pre-scaled by S): at the tile end the accumulator IS the
+// rigorous lower bound.  Dense mode stores it; append mode keeps (LB, row)
+// when LB <= tau[q]: one ballot per bound, survivors appended to the wave's
+// LDS list, written out at the next stage ahead of that stage's DMA.
 // ---------------------------------------------------------------------------
 // development-only ablation switches (timing experiments; results are wrong when set)
-#ifndef LHIP_ABL_NO_Q
-#define LHIP_ABL_NO_Q 0
-#endif
-#ifndef LHIP_ABL_NO_MFMA
-#define LHIP_ABL_NO_MFMA 0
-#endif
 #ifndef LHIP_ABL_NO_EPILOGUE
 #define LHIP_ABL_NO_EPILOGUE 0
 #endif
@@ -313,40 +331,45 @@ extern "C" int lhip_prof_read(unsigned long long *out, int reset) {
 #else
 #define PROF_T(v)
 #endif
-// tuning switches (both variants are correct)
-#ifndef LHIP_EARLY_REFILL
-#define LHIP_EARLY_REFILL 1  // refill the last stage's slot before a tile's epilogue
-#endif
-#ifndef LHIP_READS_FIRST
-#define LHIP_READS_FIRST 1  // issue all fragment reads of a stage before its MFMAs
-#endif
 #ifndef LHIP_X_NT
 #define LHIP_X_NT 1  // non-temporal policy on the once-read base stream
 #endif
+
 constexpr int SCAN_THREADS = 512;
 constexpr int SCAN_WAVES = SCAN_THREADS / 64;          // 8: 2 per SIMD, 256 registers each
 constexpr int SK = 32;
-constexpr int NSTAGE = 3;
-constexpr int XST_BYTES = BR * SK * 4;                 // 32 KiB
 constexpr int QST_BYTES = BQ * SK * 2;                 // 16 KiB
-constexpr int STAGE_BYTES = XST_BYTES + QST_BYTES;     // 48 KiB
-constexpr int RING_BYTES = NSTAGE * STAGE_BYTES;       // 144 KiB
 constexpr int RA_SLOT = BR * 16;                       // 4 KiB
 constexpr int RA_BYTES = 2 * RA_SLOT;
 constexpr int CNT_BYTES = BQ * 4;
 constexpr int QA_BYTES = BQ * 16 + BQ * 4;             // per-query bound constants + tau
 constexpr int WLIST = 32;                              // survivor list entries (8 B) per wave and tile
-constexpr int LIST_BYTES = 8 * WLIST * 8;
-constexpr int SCAN_LDS = RING_BYTES + RA_BYTES + CNT_BYTES + QA_BYTES + LIST_BYTES;
-constexpr int X_DMA_PER_WAVE = XST_BYTES / 1024 / SCAN_WAVES;  // 4
+constexpr int LIST_BYTES = SCAN_WAVES * WLIST * 8;
 constexpr int Q_DMA_PER_WAVE = QST_BYTES / 1024 / SCAN_WAVES;  // 2
-constexpr int DMA_PER_STAGE = X_DMA_PER_WAVE + Q_DMA_PER_WAVE; // + 1 row-aux on waves 0..3 at stage 0
-static_assert(SCAN_LDS <= 160 * 1024, "LDS budget");
-static_assert(X_DMA_PER_WAVE * SCAN_WAVES * 1024 == XST_BYTES, "X stage = whole DMA instructions");
 static_assert(Q_DMA_PER_WAVE * SCAN_WAVES * 1024 == QST_BYTES, "Q stage = whole DMA instructions");
 static_assert(RA_SLOT / 1024 == 4 && SCAN_WAVES >= 4, "row aux: one DMA instruction on waves 0..3");
-static_assert(DMA_PER_STAGE == 6, "wait counts below assume 6 (+1) DMA instructions per wave and stage");
 static_assert(SCAN_WAVES == 8 && WLIST <= 64, "one list of WLIST entries per wave; a flush is one instruction");
+
+// per base element type: f32 store (XB = false) or bf16 store (XB = true)
+template <bool XB>
+struct ScanCfg {
+	static constexpr int XE = XB ? 2 : 4;                      // bytes per base element
+	static constexpr int XROW = SK * XE;                       // bytes per row and stage: 64 / 128
+	static constexpr int XCH = XROW / 16;                      // 16 B chunks per row: 4 / 8
+	static constexpr int XST = BR * XROW;                      // 16 / 32 KiB
+	static constexpr int NST = XB ? 4 : 3;                     // ring slots
+	static constexpr int STAGE = XST + QST_BYTES;
+	static constexpr int RING = NST * STAGE;                   // 128 / 144 KiB
+	static constexpr int XDMA = XST / 1024 / SCAN_WAVES;       // X DMA instructions per wave and stage: 2 / 4
+	static constexpr int ROWS_PER_DMA = 1024 / XROW;           // 16 / 8
+	static constexpr int DMA = XDMA + Q_DMA_PER_WAVE;          // + 1 row aux on waves 0..3 at a tile's stage 0
+	static constexpr int LDS = RING + RA_BYTES + CNT_BYTES + QA_BYTES + LIST_BYTES;
+	static_assert(LDS <= 160 * 1024, "LDS budget");
+	static_assert(XDMA * SCAN_WAVES * 1024 == XST, "X stage = whole DMA instructions");
+	// 16 B chunk c of row r lives at physical chunk xswz(r, c) (an involution)
+	__device__ static __forceinline__ int xswz(int r, int c) { return XB ? c ^ ((r >> 2) & 3) : c ^ ((r >> 1) & 7); }
+};
+__device__ __forceinline__ int qswz(int r, int c) { return c ^ ((r >> 2) & 3); }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -383,30 +406,36 @@ __device__ __forceinline__ void dma16s(const void *sbase, uint32_t voff, uint32_
 		             : "memory", "m0");
 }
 
-// A fragment (32 base rows x 16 k) from the f32 X stage: two ds_read_b128 of
-// logical chunks c, c+1 of row r, converted to bf16 in registers.
-__device__ __forceinline__ bf16x8 ld_afrag(const uint8_t *xs, int r, int c) {
-	const int f = (r >> 1) & 7;
-	const float4 lo = *reinterpret_cast<const float4 *>(xs + r * 128 + ((c ^ f) << 4));
-	const float4 hi = *reinterpret_cast<const float4 *>(xs + r * 128 + (((c + 1) ^ f) << 4));
-	bf16x8 v;
-	v[0] = (__bf16)lo.x;
-	v[1] = (__bf16)lo.y;
-	v[2] = (__bf16)lo.z;
-	v[3] = (__bf16)lo.w;
-	v[4] = (__bf16)hi.x;
-	v[5] = (__bf16)hi.y;
-	v[6] = (__bf16)hi.z;
-	v[7] = (__bf16)hi.w;
-	return v;
-}
-
-// B fragment (16 k x 32 queries) from the bf16 Q stage: one ds_read_b128.
-__device__ __forceinline__ bf16x8 ld_bfrag(const uint8_t *qs, int r, int c) {
-	return *reinterpret_cast<const bf16x8 *>(qs + r * 64 + ((c ^ ((r >> 2) & 3)) << 4));
-}
-
 #define LHIP_WAIT_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+
+template <int N>
+__device__ __forceinline__ void wait_vm_c() {
+	asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// s_waitcnt vmcnt takes an immediate: dispatch the counts that can occur
+__device__ __forceinline__ void wait_vm(int n) {
+	switch (n) {
+	case 0: LHIP_WAIT_VM(0); break;
+	case 1: LHIP_WAIT_VM(1); break;
+	case 2: LHIP_WAIT_VM(2); break;
+	case 3: LHIP_WAIT_VM(3); break;
+	case 4: LHIP_WAIT_VM(4); break;
+	case 5: LHIP_WAIT_VM(5); break;
+	case 6: LHIP_WAIT_VM(6); break;
+	case 7: LHIP_WAIT_VM(7); break;
+	case 8: LHIP_WAIT_VM(8); break;
+	case 9: LHIP_WAIT_VM(9); break;
+	case 10: LHIP_WAIT_VM(10); break;
+	case 11: LHIP_WAIT_VM(11); break;
+	case 12: LHIP_WAIT_VM(12); break;
+	case 13: LHIP_WAIT_VM(13); break;
+	case 14: LHIP_WAIT_VM(14); break;
+	case 15: LHIP_WAIT_VM(15); break;
+	case 16: LHIP_WAIT_VM(16); break;
+	default: LHIP_WAIT_VM(0); break;  // (not reached) conservative
+	}
+}
 
 // Lane id through volatile asm: not loop-invariant to the compiler, so values
 // derived from it are recomputed where used instead of hoisted out of the
@@ -417,42 +446,8 @@ __device__ __forceinline__ int lane_id_fresh() {
 	return (int)ln;
 }
 
-// ---------------------------------------------------------------------------
-// scan kernel (persistent, LDS-DMA ring)
-//
-// Tile = 256 base rows x 256 queries.  Workgroup = 512 threads = 8 waves, two
-// per SIMD with 256 registers each, laid out 4 (base rows) x 2 (queries): a
-// wave owns 64 rows x 128 queries = 2 x 4 v_mfma_f32_32x32x16_bf16 tiles
-// (A = base rows, B = queries: accumulator column = lane&31 = query, the 16
-// registers walk base rows).  Per 32-deep stage a wave reads 4 A fragments
-// (f32, converted to bf16) and 8 B fragments from LDS for 16 MFMAs — all
-// fragments of a stage are read before its first MFMA.  One workgroup per CU
-// walks tiles blockIdx.x, +gridDim.x, ...; the k-stream never stops at a tile
-// boundary.
-//
-// The k dimension streams through a ring of NSTAGE LDS stages of SK = 32:
-//   X stage: 256 rows x 32 f32 (32 KiB) straight from HBM by
-//            global_load_lds_dwordx4 (nt: read once), rows 128 B,
-//            16 B chunk c of row r stored at c ^ ((r>>1)&7);
-//   Q stage: 256 queries x 32 bf16 (16 KiB) from L2, rows 64 B,
-//            chunk c of row r stored at c ^ ((r>>2)&3);
-//   with stage 0 of a tile: the tile's 256 row-aux float4 (4 KiB, 2 slots).
-// LDS-DMA writes lane-linearly, so the swizzle is applied on the per-lane
-// SOURCE address and undone on the ds_read_b128 fragment reads (conflict-free
-// for the b128 lane groups).  NSTAGE-1 stages stay in flight; one raw
-// s_barrier per stage behind a counted s_waitcnt vmcnt.  The store is
-// zero-padded (rows) and +inf-padded (row aux) to a multiple of BR rows.
-//
-// Epilogue per tile: each accumulator becomes a rigorous lower bound of the
-// exact distance (4 FMAs).  Dense mode stores it.  Append mode keeps (LB,
-// row) when LB <= tau[q]: survivors are appended to the wave's own LDS list
-// by wave ballots (no atomics); at the next stage, ahead of that stage's DMA,
-// the wave assigns each entry its position in the workgroup's segment for q
-// with one ds_add_rtn over the whole list and writes it out, so no global
-// store sits behind in-flight DMA in the in-order vmcnt queue.
-// ---------------------------------------------------------------------------
-template <int METRIC, int MODE>
-__global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const float *__restrict__ X,
+template <int METRIC, int MODE, bool XB>
+__global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__restrict__ Xv,
                                                                const float4 *__restrict__ rowaux, int ld,
                                                                const uint16_t *__restrict__ Qb,
                                                                const float4 *__restrict__ qaux, int nq,
@@ -461,16 +456,18 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const float *__re
                                                                const float *__restrict__ tau,
                                                                uint2 *__restrict__ seg_pool,
                                                                int *__restrict__ seg_cnt, int seg_cap) {
-	__shared__ __attribute__((aligned(16))) uint8_t smem[SCAN_LDS];
-	unsigned *CNT = reinterpret_cast<unsigned *>(smem + RING_BYTES + RA_BYTES);
-	float4 *QA = reinterpret_cast<float4 *>(smem + RING_BYTES + RA_BYTES + CNT_BYTES);
-	float *TAU = reinterpret_cast<float *>(smem + RING_BYTES + RA_BYTES + CNT_BYTES + BQ * 16);
-	uint2 *LIST = reinterpret_cast<uint2 *>(smem + RING_BYTES + RA_BYTES + CNT_BYTES + QA_BYTES);
+	using C = ScanCfg<XB>;
+	__shared__ __attribute__((aligned(16))) uint8_t smem[C::LDS];
+	unsigned *CNT = reinterpret_cast<unsigned *>(smem + C::RING + RA_BYTES);
+	float4 *QA = reinterpret_cast<float4 *>(smem + C::RING + RA_BYTES + CNT_BYTES);
+	float *TAU = reinterpret_cast<float *>(smem + C::RING + RA_BYTES + CNT_BYTES + BQ * 16);
+	uint2 *LIST = reinterpret_cast<uint2 *>(smem + C::RING + RA_BYTES + CNT_BYTES + QA_BYTES);
+	const uint8_t *X = reinterpret_cast<const uint8_t *>(Xv);
 
 	const int tid = threadIdx.x;
-	const int lane = tid & 63;
+	[[maybe_unused]] const int lane = tid & 63;
 	const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR math
-	const int wr = w & 3, wq = w >> 2;
+	const int wr = w & 3, wq = w >> 2;                      // 64-row quarter, 128-query half
 	const int q0 = blockIdx.y * BQ;
 	const int S = ld / SK;  // >= 2 (ld is a multiple of 64)
 	const int my_tiles = (n_tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
@@ -486,37 +483,55 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const float *__re
 	LHIP_WAIT_VM(0);  // the ordinary loads above, before any counted DMA wait
 	__syncthreads();
 
-	// DMA sources.  X: wave instruction j covers rows (4w+j)*8 + lane/8,
-	// physical 16 B chunk lane%8 (logical chunk = physical ^ ((row>>1)&7)).
-	// Q: instruction j covers queries (2w+j)*16 + lane/4, physical chunk lane%4.
-	// Row aux (stage 0 only): waves 0..3, rows w*64 + lane.  Per-lane byte
-	// offsets are recomputed at every issue from a fresh lane id (a few VALU
-	// ops per stage) rather than kept live across the loop.
-	const uint16_t *qbase = Qb + (int64_t)q0 * ld;
+	// DMA sources.  X: wave instruction j covers rows (XDMA*w+j)*ROWS_PER_DMA +
+	// lane/XCH, physical chunk lane%XCH.  Q: instruction j covers queries
+	// (2w+j)*16 + lane/4, physical chunk lane%4.  Row aux (stage 0 only): waves
+	// 0..3, rows w*64 + lane.  The per-lane source offsets are loop-invariant
+	// (VGPRs, computed once); the wave-uniform parts — source pointers of the
+	// next stage to issue and its LDS slot — run in SGPRs and advance by
+	// constants, so a stage's issue costs a handful of scalar instructions.
 	const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
-
-	auto issue = [&](int ti, int st, int slot) {
-		const int64_t row0 = (int64_t)((int)blockIdx.x + ti * (int)gridDim.x) * tile_stride * BR;
-		const uint32_t base = lds0 + (uint32_t)slot * STAGE_BYTES;
-		const int ln = lane_id_fresh();
-		if (st == 0 && w < 4)
-			dma16s(rowaux + row0 + w * 64, (uint32_t)ln * 16u,
-			       __builtin_amdgcn_readfirstlane(lds0 + RING_BYTES + (uint32_t)(ti & 1) * RA_SLOT + w * 1024));
-		const float *xt = X + row0 * ld + st * SK;
+	uint32_t xoff[C::XDMA], qoff[Q_DMA_PER_WAVE];
 #pragma unroll
-		for (int j = 0; j < X_DMA_PER_WAVE; ++j) {
-			const int xr = (X_DMA_PER_WAVE * w + j) * 8 + (ln >> 3);
-			const uint32_t xoff = (uint32_t)(xr * ld + (((ln & 7) ^ ((xr >> 1) & 7)) << 2)) * 4u;
-			dma16s<LHIP_X_NT>(xt, xoff, __builtin_amdgcn_readfirstlane(base + (X_DMA_PER_WAVE * w + j) * 1024));
-		}
-		if (!LHIP_ABL_NO_Q) {
+	for (int j = 0; j < C::XDMA; ++j) {
+		const int xr = (C::XDMA * w + j) * C::ROWS_PER_DMA + lane / C::XCH;
+		xoff[j] = (uint32_t)(xr * ld * C::XE + (C::xswz(xr, lane % C::XCH) << 4));
+	}
 #pragma unroll
-			for (int j = 0; j < Q_DMA_PER_WAVE; ++j) {
-				const int qr = (Q_DMA_PER_WAVE * w + j) * 16 + (ln >> 2);
-				const uint32_t qoff = (uint32_t)(qr * ld + (((ln & 3) ^ ((qr >> 2) & 3)) << 3)) * 2u;
-				dma16s(qbase + st * SK, qoff,
-				       __builtin_amdgcn_readfirstlane(base + XST_BYTES + (Q_DMA_PER_WAVE * w + j) * 1024));
-			}
+	for (int j = 0; j < Q_DMA_PER_WAVE; ++j) {
+		const int qr = (Q_DMA_PER_WAVE * w + j) * 16 + (lane >> 2);
+		qoff[j] = (uint32_t)(qr * ld + (qswz(qr, lane & 3) << 3)) * 2u;
+	}
+	const uint32_t raoff = (uint32_t)lane * 16u;
+	const int64_t tile_rows_step = (int64_t)gridDim.x * tile_stride * BR;  // rows between this workgroup's tiles
+	const uint16_t *qbase = Qb + (int64_t)q0 * ld;
+	const uint8_t *iss_xtile = X + (int64_t)blockIdx.x * tile_stride * BR * ld * C::XE;
+	const uint8_t *iss_xt = iss_xtile;
+	const float4 *iss_ra = rowaux + (int64_t)blockIdx.x * tile_stride * BR;
+	const uint16_t *iss_q = qbase;
+	uint32_t iss_lds = lds0;  // LDS slot of the next stage to issue
+	int iss_g = 0, iss_s = 0, iss_t = 0;
+	auto issue_one = [&]() {
+		if (iss_s == 0 && w < 4)
+			dma16s(iss_ra + w * 64, raoff, lds0 + C::RING + (uint32_t)(iss_t & 1) * RA_SLOT + (uint32_t)w * 1024u);
+#pragma unroll
+		for (int j = 0; j < C::XDMA; ++j)
+			dma16s<LHIP_X_NT>(iss_xt, xoff[j], iss_lds + (uint32_t)(C::XDMA * w + j) * 1024u);
+#pragma unroll
+		for (int j = 0; j < Q_DMA_PER_WAVE; ++j)
+			dma16s(iss_q, qoff[j], iss_lds + (uint32_t)C::XST + (uint32_t)(Q_DMA_PER_WAVE * w + j) * 1024u);
+		++iss_g;
+		iss_lds = iss_lds + C::STAGE == lds0 + C::RING ? lds0 : iss_lds + C::STAGE;
+		if (++iss_s == S) {
+			iss_s = 0;
+			++iss_t;
+			iss_xtile += tile_rows_step * ld * C::XE;
+			iss_xt = iss_xtile;
+			iss_ra += tile_rows_step;
+			iss_q = qbase;
+		} else {
+			iss_xt += SK * C::XE;
+			iss_q += SK;
 		}
 	};
 
@@ -537,7 +552,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const float *__re
 					for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
 			return;
 		}
-		const float *RAs = reinterpret_cast<const float *>(smem + RING_BYTES + (ti & 1) * RA_SLOT);
+		const float *RAs = reinterpret_cast<const float *>(smem + C::RING + (ti & 1) * RA_SLOT);
 		const int ln = lane_id_fresh();
 		const int li = ln & 31, hk = ln >> 5;  // f32 32x32x2 operands: lane = (row or column, k)
 		f32x16 zero;
@@ -563,23 +578,30 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const float *__re
 		}
 	};
 
-	// Issue cursor: global stage iss_g = (tile iss_t, stage iss_s) into ring
-	// slot iss_slot.  Stage h may be issued once every wave has finished
-	// computing stage h-NSTAGE (its slot): right after the barrier of
-	// iteration h-2.
-	int iss_g = 0, iss_t = 0, iss_s = 0, iss_slot = 0;
-	auto issue_next = [&]() {
-		issue(iss_t, iss_s, iss_slot);
-		++iss_g;
-		if (++iss_s == S) {
-			iss_s = 0;
-			++iss_t;
-		}
-		iss_slot = iss_slot == NSTAGE - 1 ? 0 : iss_slot + 1;
+	// Stage h may be issued once every wave is done reading stage h-NST (its
+	// slot), i.e. after the barrier of iteration h-NST; and a tile's stage 0
+	// (which carries its row aux into RA slot tile&1) only once the epilogue of
+	// tile-2 is done (matters when S < NST).
+	int tiles_done = 0;
+	const bool ra_wave = w < 4;  // waves that issue a row-aux DMA with a tile's stage 0
+	auto pump = [&](int limit) {
+		while (iss_g < G && iss_g <= limit && !(iss_s == 0 && iss_t >= tiles_done + 2)) issue_one();
 	};
-	issue_next();
-	if (G > 1) issue_next();
-	int cur_t = 0, cur_s = 0, slot = 0;
+	// s_waitcnt vmcnt for "stage h landed": this wave's DMA instructions of the
+	// m = iss_g-1-h stages issued after it may stay in flight — DMA each, +1 on
+	// waves 0..3 for each of them that is a tile's stage 0 (sh = in-tile index
+	// of stage h).  The steady-state counts are immediates.
+	auto wait_stage = [&](int h, int sh) {
+		const int m = iss_g - 1 - h;
+		if (m <= 0) {
+			LHIP_WAIT_VM(0);
+			return;
+		}
+		const int d0 = S - 1 - sh;  // stages after h up to the next tile start, exclusive
+		const int n0 = ra_wave ? (d0 < m) + (d0 + S < m) : 0;
+		wait_vm(m * C::DMA + n0);
+	};
+
 	// This wave's survivor list: n_list entries (wave-uniform) of the tile
 	// finished last.  Entry = (key, query << 18 | tile row << 10).  Written
 	// out with segment positions from the per-query LDS counters: one
@@ -609,37 +631,106 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const float *__re
 				seg_pool[((int64_t)blockIdx.x * nq + q0 + qv) * seg_cap + p] = make_uint2(fkey(lb), (uint32_t)(row0 + rr));
 		}
 	};
+	// Fragments of one 16-deep k-half of a stage: A raw (f32: two 16 B reads
+	// per fragment, converted at use; bf16: one), B bf16.  F0 holds (g, kk0)
+	// and F1 (g, kk1); each half's MFMAs run while the other half loads.
+	struct Frag {
+		float4 a[2][2];  // [t][lo/hi] raw 16 B reads (bf16: [t][0] only)
+		bf16x8 b[4];
+	};
+	// per-lane fragment byte offsets inside a stage (loop-invariant VGPRs)
+	uint32_t aoff[2][2][2], boff[2][4];
+#pragma unroll
+	for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+		for (int t = 0; t < 2; ++t) {
+			const int r = wr * 64 + 32 * t + (lane & 31), hh = lane >> 5;
+			if (XB) {
+				aoff[kk][t][0] = aoff[kk][t][1] = (uint32_t)(r * C::XROW + (C::xswz(r, 2 * kk + hh) << 4));
+			} else {
+				const int c = 4 * kk + 2 * hh;
+				aoff[kk][t][0] = (uint32_t)(r * C::XROW + (C::xswz(r, c) << 4));
+				aoff[kk][t][1] = (uint32_t)(r * C::XROW + (C::xswz(r, c + 1) << 4));
+			}
+		}
+#pragma unroll
+		for (int u = 0; u < 4; ++u) {
+			const int q = wq * 128 + 32 * u + (lane & 31);
+			boff[kk][u] = (uint32_t)(C::XST + q * 64 + (qswz(q, 2 * kk + (lane >> 5)) << 4));
+		}
+	}
+	auto read_half = [&](Frag &f, const uint8_t *st_base, int kk) {
+#pragma unroll
+		for (int t = 0; t < 2; ++t) {
+			f.a[t][0] = *reinterpret_cast<const float4 *>(st_base + aoff[kk][t][0]);
+			if (!XB) f.a[t][1] = *reinterpret_cast<const float4 *>(st_base + aoff[kk][t][1]);
+		}
+#pragma unroll
+		for (int u = 0; u < 4; ++u) f.b[u] = *reinterpret_cast<const bf16x8 *>(st_base + boff[kk][u]);
+	};
+	auto mfma_half = [&](const Frag &f) {
+#pragma unroll
+		for (int t = 0; t < 2; ++t) {
+			bf16x8 av;
+			if (XB) {
+				av = __builtin_bit_cast(bf16x8, f.a[t][0]);
+			} else {
+				const float4 lo = f.a[t][0], hi = f.a[t][1];
+				av[0] = (__bf16)lo.x;
+				av[1] = (__bf16)lo.y;
+				av[2] = (__bf16)lo.z;
+				av[3] = (__bf16)lo.w;
+				av[4] = (__bf16)hi.x;
+				av[5] = (__bf16)hi.y;
+				av[6] = (__bf16)hi.z;
+				av[7] = (__bf16)hi.w;
+			}
+#pragma unroll
+			for (int u = 0; u < 4; ++u) acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, f.b[u], acc[t][u], 0, 0, 0);
+		}
+	};
+
+	// prologue: stages 0 .. NST-1 in flight; (0, kk0) into registers
+	pump(C::NST - 1);
+	wait_stage(0, 0);
+	__builtin_amdgcn_s_barrier();
+	asm volatile("" ::: "memory");
+	Frag F0, F1;
+	read_half(F0, smem, 0);
+
 #if LHIP_PROF
 	uint64_t pw = 0, pb = 0, pc = 0, pe = 0;
 	uint64_t prof_surv = 0, prof_over = 0, prof_slow = 0, prof_slown = 0;
 #endif
+	int cur_t = 0, cur_s = 0;
+	const uint8_t *rd = smem;  // LDS slot of stage g
 	for (int g = 0; g < G; ++g) {
 		PROF_T(t0);
-		// Stage g must have landed; this wave's DMA instructions of the stages
-		// after it (one, or two after an early refill) may stay in flight: 6
-		// each, +1 for a tile's stage 0 on waves 0..3 (row aux).
-		{
-			const int ahead = iss_g - 1 - g;
-			const int s1 = cur_s + 1 == S ? 0 : cur_s + 1;
-			const int n1 = DMA_PER_STAGE + ((s1 == 0) & (w < 4));
-			const int n2 = DMA_PER_STAGE + (((s1 + 1 == S) | (S == 1)) & (w < 4));
-			const int n = ahead <= 0 ? 0 : (ahead == 1 ? n1 : n1 + n2);
-			if (n == 0)
-				LHIP_WAIT_VM(0);
-			else if (n == 6)
-				LHIP_WAIT_VM(6);
-			else if (n == 7)
-				LHIP_WAIT_VM(7);
-			else if (n == 12)
-				LHIP_WAIT_VM(12);
+		const bool tile_end = cur_s + 1 == S;
+		const uint8_t *rd_next = rd + C::STAGE == smem + C::RING ? smem : rd + C::STAGE;
+		if (cur_s == 0) init_acc(cur_t);
+		// (g, kk1) loads while (g, kk0) multiplies
+		read_half(F1, rd, 1);
+		mfma_half(F0);
+		// stage g+1 must have landed (the stages issued after it may stay in
+		// flight); this wave's reads of stage g are complete before the
+		// barrier, so after it slot g % NST is free for stage g+NST
+		if (iss_g == g + C::NST) {
+			// steady state: stages g+2 .. g+NST-1 in flight after g+1; the one
+			// extra DMA on waves 0..3 if one of them is a tile's stage 0
+			const bool st0 = cur_s + 2 == S || (C::NST == 4 && (cur_s + 3 == S || (S == 2 && cur_s == 1)));
+			if (ra_wave && st0)
+				wait_vm_c<(C::NST - 2) * C::DMA + 1>();
 			else
-				LHIP_WAIT_VM(13);
+				wait_vm_c<(C::NST - 2) * C::DMA>();
+		} else if (g + 1 < G) {
+			wait_stage(g + 1, tile_end ? 0 : cur_s + 1);  // the last stages, or a held-back issue
 		}
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 		PROF_T(t1);
 		__builtin_amdgcn_s_barrier();
 		asm volatile("" ::: "memory");
 		PROF_T(t2);
-		const bool tile_end = cur_s + 1 == S;
 		// write out the survivor list of the tile finished last iteration:
 		// these stores enter the vmcnt queue ahead of this iteration's DMA, so
 		// the next counted wait finds them a whole stage old
@@ -649,60 +740,12 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const float *__re
 			else
 				write_list(cur_t - 1);
 		}
-		if (iss_g < G && iss_g <= g + 2) issue_next();
-
-		// ---- stage g: all fragment reads first, then 16 MFMAs --------------
-		if (cur_s == 0) init_acc(cur_t);
-		{
-			const uint8_t *xs = smem + slot * STAGE_BYTES;
-			const uint8_t *qs = xs + XST_BYTES;
-			const int ln = lane_id_fresh();
-			const int li = ln & 31, hh = ln >> 5;
-			// every fragment read of the stage is issued before the first
-			// convert / MFMA: one exposed LDS latency per stage, not three
-			float4 ar[2][2][2];
-			bf16x8 a[2][2], b[2][4];
-#pragma unroll
-			for (int kk = 0; kk < SK / 16; ++kk) {
-#pragma unroll
-				for (int t = 0; t < 2; ++t) {
-					const int r = wr * 64 + 32 * t + li, c = 4 * kk + 2 * hh, f = (r >> 1) & 7;
-					ar[kk][t][0] = *reinterpret_cast<const float4 *>(xs + r * 128 + ((c ^ f) << 4));
-					ar[kk][t][1] = *reinterpret_cast<const float4 *>(xs + r * 128 + (((c + 1) ^ f) << 4));
-				}
-#pragma unroll
-				for (int u = 0; u < 4; ++u) b[kk][u] = ld_bfrag(qs, wq * 128 + 32 * u + li, 2 * kk + hh);
-			}
-			if (LHIP_READS_FIRST) __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-			for (int kk = 0; kk < SK / 16; ++kk)
-#pragma unroll
-				for (int t = 0; t < 2; ++t) {
-					const float4 lo = ar[kk][t][0], hi = ar[kk][t][1];
-					bf16x8 v;
-					v[0] = (__bf16)lo.x;
-					v[1] = (__bf16)lo.y;
-					v[2] = (__bf16)lo.z;
-					v[3] = (__bf16)lo.w;
-					v[4] = (__bf16)hi.x;
-					v[5] = (__bf16)hi.y;
-					v[6] = (__bf16)hi.z;
-					v[7] = (__bf16)hi.w;
-					a[kk][t] = v;
-				}
-#pragma unroll
-			for (int kk = 0; kk < SK / 16; ++kk) {
-#pragma unroll
-				for (int t = 0; t < 2; ++t)
-#pragma unroll
-					for (int u = 0; u < 4; ++u) {
-						if (LHIP_ABL_NO_MFMA)
-							asm volatile("" ::"v"(a[kk][t]), "v"(b[kk][u]));
-						else
-							acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kk][t], b[kk][u], acc[t][u], 0, 0, 0);
-					}
-			}
-		}
+		pump(g + C::NST);  // into slot g % NST
+		// (g+1, kk0) loads while (g, kk1) multiplies (unconditional: on the
+		// last stage it reads a stale, stable slot; the values are unused)
+		read_half(F0, rd_next, 0);
+		mfma_half(F1);
+		rd = rd_next;
 		asm volatile("" ::: "memory");
 		PROF_T(t3);
 #if LHIP_PROF
@@ -710,29 +753,18 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const float *__re
 		pb += t2 - t1;
 		pc += t3 - t2;
 #endif
-		slot = slot == NSTAGE - 1 ? 0 : slot + 1;
 		if (!tile_end) {
 			++cur_s;
 			continue;
 		}
 		cur_s = 0;
 		const int ti = cur_t++;
-		if (LHIP_EARLY_REFILL && S > 2 && iss_g < G && iss_g == g + 3) {
-			// every wave is done with this stage's slot: refill it before the
-			// epilogue, so all NSTAGE slots stream while the epilogue runs.
-			// (S > 2: stage g+3 is then stage 2 of the next tile, carrying no
-			// row aux; with S == 2 it would be stage 0 of tile ti+2, whose row
-			// aux DMA targets the slot this epilogue reads.)
-			__builtin_amdgcn_s_barrier();
-			asm volatile("" ::: "memory");
-			issue_next();
-		}
 
 		// ---- epilogue of tile ti (its row aux landed with its stage 0) ------
 		const int64_t tile = (int64_t)blockIdx.x + (int64_t)ti * gridDim.x;
 		const int64_t row0 = tile * tile_stride * BR;
 		// row aux of the tile (SoA): alpha [0,256), xn [256,512), ux [512,768), sc [768,1024)
-		const float *RAs = reinterpret_cast<const float *>(smem + RING_BYTES + (ti & 1) * RA_SLOT);
+		const float *RAs = reinterpret_cast<const float *>(smem + C::RING + (ti & 1) * RA_SLOT);
 		auto ra4 = [&](int r0, int c) { return *reinterpret_cast<const float4 *>(RAs + c * BR + r0); };
 		const int eln = lane_id_fresh();
 		const int qlb = wq * 128 + (eln & 31);  // tile-local query of acc[.][u]: qlb + 32u
@@ -883,6 +915,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const float *__re
 			prof_over += nl > WLIST ? nl - WLIST : 0;
 #endif
 		}
+		tiles_done = cur_t;
+		pump(g + C::NST);  // stages held back for this tile's row-aux slot
 #if LHIP_PROF
 		PROF_T(t4);
 		pe += t4 - t3;
@@ -925,29 +959,39 @@ static int num_cus() {
 
 int scan_grid(int64_t n_tiles) { return (int)std::min<int64_t>(n_tiles, (int64_t)num_cus()); }
 
-template <int MODE>
-static void scan_dispatch(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, float *dense,
-                          int64_t ld_out, const float *tau, uint2 *seg_pool, int *seg_cnt, int seg_cap,
-                          hipStream_t st) {
+template <int MODE, bool XB>
+static void scan_dispatch_x(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, float *dense,
+                            int64_t ld_out, const float *tau, uint2 *seg_pool, int *seg_cnt, int seg_cap,
+                            hipStream_t st) {
 	dim3 grid((unsigned)scan_grid(n_tiles), (unsigned)(q.nq_pad / BQ));
 	dim3 block(SCAN_THREADS);
 	switch (s.metric) {
 	case METRIC_L2:
-		scan_kernel<METRIC_L2, MODE><<<grid, block, 0, st>>>(s.X, s.rowaux, s.ld, q.Qb, q.qaux, q.nq, (int)n_tiles,
-		                                                      (int)tile_stride, dense, ld_out, tau, seg_pool, seg_cnt,
-		                                                      seg_cap);
+		scan_kernel<METRIC_L2, MODE, XB><<<grid, block, 0, st>>>(s.X, s.rowaux, s.ld, q.Qb, q.qaux, q.nq, (int)n_tiles,
+		                                                          (int)tile_stride, dense, ld_out, tau, seg_pool,
+		                                                          seg_cnt, seg_cap);
 		break;
 	case METRIC_DOT:
-		scan_kernel<METRIC_DOT, MODE><<<grid, block, 0, st>>>(s.X, s.rowaux, s.ld, q.Qb, q.qaux, q.nq, (int)n_tiles,
-		                                                       (int)tile_stride, dense, ld_out, tau, seg_pool, seg_cnt,
-		                                                       seg_cap);
+		scan_kernel<METRIC_DOT, MODE, XB><<<grid, block, 0, st>>>(s.X, s.rowaux, s.ld, q.Qb, q.qaux, q.nq, (int)n_tiles,
+		                                                           (int)tile_stride, dense, ld_out, tau, seg_pool,
+		                                                           seg_cnt, seg_cap);
 		break;
 	default:
-		scan_kernel<METRIC_COSINE, MODE><<<grid, block, 0, st>>>(s.X, s.rowaux, s.ld, q.Qb, q.qaux, q.nq,
-		                                                          (int)n_tiles, (int)tile_stride, dense, ld_out, tau, seg_pool, seg_cnt,
-		                                                          seg_cap);
+		scan_kernel<METRIC_COSINE, MODE, XB><<<grid, block, 0, st>>>(s.X, s.rowaux, s.ld, q.Qb, q.qaux, q.nq,
+		                                                              (int)n_tiles, (int)tile_stride, dense, ld_out,
+		                                                              tau, seg_pool, seg_cnt, seg_cap);
 		break;
 	}
+}
+
+template <int MODE>
+static void scan_dispatch(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, float *dense,
+                          int64_t ld_out, const float *tau, uint2 *seg_pool, int *seg_cnt, int seg_cap,
+                          hipStream_t st) {
+	if (s.xbf16)
+		scan_dispatch_x<MODE, true>(s, q, n_tiles, tile_stride, dense, ld_out, tau, seg_pool, seg_cnt, seg_cap, st);
+	else
+		scan_dispatch_x<MODE, false>(s, q, n_tiles, tile_stride, dense, ld_out, tau, seg_pool, seg_cnt, seg_cap, st);
 }
 
 void launch_scan_dense(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, float *out,
@@ -1229,12 +1273,12 @@ void launch_select_segments(const uint2 *seg_pool, const int *seg_cnt, int seg_c
 // ---------------------------------------------------------------------------
 // refine: one wave per (query, candidate), f64 accumulation
 // ---------------------------------------------------------------------------
-template <int METRIC>
-__device__ __forceinline__ float exact_distance(const float *__restrict__ x, const float *__restrict__ q, int dim,
+template <int METRIC, typename T>
+__device__ __forceinline__ float exact_distance(const T *__restrict__ x, const float *__restrict__ q, int dim,
                                                 int lane) {
 	double a = 0.0, b = 0.0, c = 0.0;
 	for (int i = lane; i < dim; i += 64) {
-		double xv = x[i], qv = q[i];
+		double xv = xval(x, i), qv = q[i];
 		if (METRIC == METRIC_L2) {
 			double d = xv - qv;
 			a += d * d;
@@ -1263,8 +1307,8 @@ __device__ __forceinline__ float exact_distance(const float *__restrict__ x, con
 	return f;
 }
 
-template <int METRIC>
-__global__ __launch_bounds__(256) void refine_kernel(const float *__restrict__ X, int ld, int dim,
+template <int METRIC, typename T>
+__global__ __launch_bounds__(256) void refine_kernel(const T *__restrict__ X, int ld, int dim,
                                                      const float *__restrict__ Qf,
                                                      const uint32_t *__restrict__ cand_slot,
                                                      const int *__restrict__ cand_cnt, int nq, int M,
@@ -1275,26 +1319,36 @@ __global__ __launch_bounds__(256) void refine_kernel(const float *__restrict__ X
 	const int q = (int)(g / M), m = (int)(g % M);
 	if (m >= cand_cnt[q]) return;
 	const uint32_t slot = cand_slot[(int64_t)q * M + m];
-	float d = exact_distance<METRIC>(X + (int64_t)slot * ld, Qf + (int64_t)q * ld, dim, lane);
+	float d = exact_distance<METRIC, T>(X + (int64_t)slot * ld, Qf + (int64_t)q * ld, dim, lane);
 	if (lane == 0) cand_dist[(int64_t)q * M + m] = d;
+}
+
+template <typename T>
+static void refine_dispatch(const StoreView &s, const QueryView &q, const uint32_t *cand_slot, const int *cand_cnt,
+                            int M, float *cand_dist, hipStream_t st) {
+	int64_t waves = (int64_t)q.nq * M;
+	dim3 grid((unsigned)((waves + 3) / 4));
+	const T *X = static_cast<const T *>(s.X);
+	switch (s.metric) {
+	case METRIC_L2:
+		refine_kernel<METRIC_L2, T><<<grid, 256, 0, st>>>(X, s.ld, s.dim, q.Qf, cand_slot, cand_cnt, q.nq, M, cand_dist);
+		break;
+	case METRIC_DOT:
+		refine_kernel<METRIC_DOT, T><<<grid, 256, 0, st>>>(X, s.ld, s.dim, q.Qf, cand_slot, cand_cnt, q.nq, M, cand_dist);
+		break;
+	default:
+		refine_kernel<METRIC_COSINE, T><<<grid, 256, 0, st>>>(X, s.ld, s.dim, q.Qf, cand_slot, cand_cnt, q.nq, M,
+		                                                       cand_dist);
+		break;
+	}
 }
 
 void launch_refine(const StoreView &s, const QueryView &q, const uint32_t *cand_slot, const int *cand_cnt, int M,
                    float *cand_dist, hipStream_t st) {
-	int64_t waves = (int64_t)q.nq * M;
-	dim3 grid((unsigned)((waves + 3) / 4));
-	switch (s.metric) {
-	case METRIC_L2:
-		refine_kernel<METRIC_L2><<<grid, 256, 0, st>>>(s.X, s.ld, s.dim, q.Qf, cand_slot, cand_cnt, q.nq, M, cand_dist);
-		break;
-	case METRIC_DOT:
-		refine_kernel<METRIC_DOT><<<grid, 256, 0, st>>>(s.X, s.ld, s.dim, q.Qf, cand_slot, cand_cnt, q.nq, M, cand_dist);
-		break;
-	default:
-		refine_kernel<METRIC_COSINE><<<grid, 256, 0, st>>>(s.X, s.ld, s.dim, q.Qf, cand_slot, cand_cnt, q.nq, M,
-		                                                    cand_dist);
-		break;
-	}
+	if (s.xbf16)
+		refine_dispatch<uint16_t>(s, q, cand_slot, cand_cnt, M, cand_dist, st);
+	else
+		refine_dispatch<float>(s, q, cand_slot, cand_cnt, M, cand_dist, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -1382,15 +1436,15 @@ void launch_finalize(const StoreView &s, const uint32_t *cand_slot, const int *c
 // ---------------------------------------------------------------------------
 // exact fallback
 // ---------------------------------------------------------------------------
-template <int METRIC>
-__global__ __launch_bounds__(256) void exact_all_kernel(const float *__restrict__ X, const float4 *__restrict__ rowaux,
+template <int METRIC, typename T>
+__global__ __launch_bounds__(256) void exact_all_kernel(const T *__restrict__ X, const float4 *__restrict__ rowaux,
                                                         const int64_t *__restrict__ labels, int64_t n, int ld,
                                                         int dim, const float *__restrict__ q,
                                                         float *__restrict__ keys, int64_t *__restrict__ vals) {
 	const int lane = threadIdx.x & 63;
 	const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
 	if (r >= n) return;
-	float d = exact_distance<METRIC>(X + r * ld, q, dim, lane);
+	float d = exact_distance<METRIC, T>(X + r * ld, q, dim, lane);
 	if (lane == 0) {
 		const float a = reinterpret_cast<const float *>(rowaux)[raix(r, 0)];
 		const bool dead = (a == F_INF);
@@ -1399,24 +1453,34 @@ __global__ __launch_bounds__(256) void exact_all_kernel(const float *__restrict_
 	}
 }
 
-void launch_exact_all(const StoreView &s, const QueryView &q, int qi, float *keys, int64_t *vals, hipStream_t st) {
-	if (s.n_slots <= 0) return;
+template <typename T>
+static void exact_all_dispatch(const StoreView &s, const QueryView &q, int qi, float *keys, int64_t *vals,
+                               hipStream_t st) {
 	dim3 grid((unsigned)((s.n_slots + 3) / 4));
 	const float *qq = q.Qf + (int64_t)qi * s.ld;
+	const T *X = static_cast<const T *>(s.X);
 	switch (s.metric) {
 	case METRIC_L2:
-		exact_all_kernel<METRIC_L2><<<grid, 256, 0, st>>>(s.X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim, qq, keys,
-		                                                   vals);
+		exact_all_kernel<METRIC_L2, T><<<grid, 256, 0, st>>>(X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim, qq, keys,
+		                                                      vals);
 		break;
 	case METRIC_DOT:
-		exact_all_kernel<METRIC_DOT><<<grid, 256, 0, st>>>(s.X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim, qq, keys,
-		                                                    vals);
+		exact_all_kernel<METRIC_DOT, T><<<grid, 256, 0, st>>>(X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim, qq, keys,
+		                                                       vals);
 		break;
 	default:
-		exact_all_kernel<METRIC_COSINE><<<grid, 256, 0, st>>>(s.X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim, qq,
-		                                                       keys, vals);
+		exact_all_kernel<METRIC_COSINE, T><<<grid, 256, 0, st>>>(X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim, qq,
+		                                                          keys, vals);
 		break;
 	}
+}
+
+void launch_exact_all(const StoreView &s, const QueryView &q, int qi, float *keys, int64_t *vals, hipStream_t st) {
+	if (s.n_slots <= 0) return;
+	if (s.xbf16)
+		exact_all_dispatch<uint16_t>(s, q, qi, keys, vals, st);
+	else
+		exact_all_dispatch<float>(s, q, qi, keys, vals, st);
 }
 
 int sort_pairs(void *temp, size_t &temp_bytes, const float *keys_in, float *keys_out, const int64_t *vals_in,
@@ -1501,17 +1565,18 @@ void launch_merge_topk(int nshard, int nq, int k, const int64_t *part_labels, co
 // ---------------------------------------------------------------------------
 // compaction gather
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void gather_rows_kernel(const float *__restrict__ X, const float4 *__restrict__ rowaux,
+// rows are moved as 16 B units: ld * element size is a multiple of 128 B
+__global__ __launch_bounds__(256) void gather_rows_kernel(const uint4 *__restrict__ X, int row_u4,
+                                                          const float4 *__restrict__ rowaux,
                                                           const int64_t *__restrict__ labels,
-                                                          const int64_t *__restrict__ idx, int64_t n, int ld,
-                                                          float *__restrict__ Xo, float4 *__restrict__ rowaux_o,
+                                                          const int64_t *__restrict__ idx, int64_t n,
+                                                          uint4 *__restrict__ Xo, float4 *__restrict__ rowaux_o,
                                                           int64_t *__restrict__ labels_o) {
 	const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
 	const int lane = threadIdx.x & 63;
 	if (r >= n) return;
 	const int64_t s = idx[r];
-	for (int i = lane * 4; i < ld; i += 256)
-		*reinterpret_cast<float4 *>(Xo + r * ld + i) = *reinterpret_cast<const float4 *>(X + s * ld + i);
+	for (int i = lane; i < row_u4; i += 64) Xo[r * row_u4 + i] = X[s * row_u4 + i];
 	if (lane == 0) {
 		const float *ri = reinterpret_cast<const float *>(rowaux);
 		float *ro = reinterpret_cast<float *>(rowaux_o);
@@ -1521,11 +1586,12 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float *__restric
 	}
 }
 
-void launch_gather_rows(const float *X, const float4 *rowaux, const int64_t *labels, const int64_t *idx, int64_t n,
-                        int ld, float *Xo, float4 *rowaux_o, int64_t *labels_o, hipStream_t st) {
+void launch_gather_rows(const void *X, int xbf16, const float4 *rowaux, const int64_t *labels, const int64_t *idx,
+                        int64_t n, int ld, void *Xo, float4 *rowaux_o, int64_t *labels_o, hipStream_t st) {
 	if (n <= 0) return;
-	gather_rows_kernel<<<dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st>>>(X, rowaux, labels, idx, n, ld, Xo,
-	                                                                       rowaux_o, labels_o);
+	const int row_u4 = ld * (xbf16 ? 2 : 4) / 16;
+	gather_rows_kernel<<<dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st>>>(
+	    static_cast<const uint4 *>(X), row_u4, rowaux, labels, idx, n, static_cast<uint4 *>(Xo), rowaux_o, labels_o);
 }
 
 }  // namespace lhip

@@ -82,7 +82,7 @@ struct DevBuf {
 };
 
 struct Workspace {
-	DevBuf<float> Qin, Qf, tau, cut, dense, cand_dist, out_d, fb_keys, fb_keys2;
+	DevBuf<float> Qin, Qf, tau, cut, dense, cand_dist, out_d, fb_keys, fb_keys2, stage;
 	DevBuf<uint16_t> Qb;
 	DevBuf<float4> qaux;
 	DevBuf<uint2> seg_pool;
@@ -124,8 +124,11 @@ struct Index {
 	std::vector<uint8_t> live;
 	int64_t n_live = 0;
 
-	// device store
-	float *X = nullptr;
+	// device store: rows of `ld` elements, f32, or bf16 bits with storage "bf16"
+	void *X = nullptr;
+	bool xbf16 = false;
+	size_t xes() const { return xbf16 ? 2 : 4; }
+	uint8_t *xrow(int64_t s) const { return static_cast<uint8_t *>(X) + (size_t)s * ld * xes(); }
 	float4 *rowaux = nullptr;  // aux for `metric`
 	float4 *rowaux_l2 = nullptr;  // aux for L2 when metric_quirk is on and metric != l2
 	int64_t *dlabels = nullptr;
@@ -194,15 +197,15 @@ struct Index {
 		// capacity is a multiple of the scan tile and the tail past n_slots is
 		// zero: the scan kernel streams whole tiles without clamping rows
 		int64_t c = round_up(std::max<int64_t>(want, std::max<int64_t>(4096, cap * 2)), SCAN_BR);
-		float *nX = nullptr;
+		void *nX = nullptr;
 		float4 *na = nullptr, *na2 = nullptr;
 		int64_t *nl = nullptr;
-		HIPCHK(hipMalloc(&nX, (size_t)c * ld * sizeof(float)));
+		HIPCHK(hipMalloc(&nX, (size_t)c * ld * xes()));
 		HIPCHK(hipMalloc(&na, (size_t)c * sizeof(float4)));
 		HIPCHK(hipMalloc(&nl, (size_t)c * sizeof(int64_t)));
 		if (rowaux_l2 || (metric_quirk && metric != METRIC_L2)) HIPCHK(hipMalloc(&na2, (size_t)c * sizeof(float4)));
 		if (n_slots > 0) {
-			HIPCHK(hipMemcpyAsync(nX, X, (size_t)n_slots * ld * sizeof(float), hipMemcpyDeviceToDevice, stream));
+			HIPCHK(hipMemcpyAsync(nX, X, (size_t)n_slots * ld * xes(), hipMemcpyDeviceToDevice, stream));
 			// row aux is tile-blocked SoA: move whole tile blocks (cap is a
 			// multiple of SCAN_BR, so they exist in the old buffer)
 			const size_t aux_bytes = (size_t)round_up(n_slots, SCAN_BR) * sizeof(float4);
@@ -210,7 +213,8 @@ struct Index {
 			HIPCHK(hipMemcpyAsync(nl, dlabels, (size_t)n_slots * sizeof(int64_t), hipMemcpyDeviceToDevice, stream));
 			if (na2 && rowaux_l2) HIPCHK(hipMemcpyAsync(na2, rowaux_l2, aux_bytes, hipMemcpyDeviceToDevice, stream));
 		}
-		HIPCHK(hipMemsetAsync(nX + n_slots * ld, 0, (size_t)(c - n_slots) * ld * sizeof(float), stream));
+		HIPCHK(hipMemsetAsync(static_cast<uint8_t *>(nX) + (size_t)n_slots * ld * xes(), 0,
+		                      (size_t)(c - n_slots) * ld * xes(), stream));
 		launch_fill_rowaux(na, n_slots, c, stream);
 		if (na2) launch_fill_rowaux(na2, n_slots, c, stream);
 		HIPCHK(hipStreamSynchronize(stream));
@@ -242,8 +246,8 @@ struct Index {
 		for (int64_t i = 0; i < num; ++i) labs[(size_t)i] = first + i;
 		HIPCHK(hipMemcpyAsync(dlabels + n_slots, labs.data(), (size_t)num * sizeof(int64_t), hipMemcpyHostToDevice,
 		                      stream));
-		launch_rowaux(X, ld, dim, metric, n_slots, num, rowaux, stats.p, stream);
-		if (rowaux_l2) launch_rowaux(X, ld, dim, METRIC_L2, n_slots, num, rowaux_l2, stats.p + 2, stream);
+		launch_rowaux(X, xbf16, ld, dim, metric, n_slots, num, rowaux, stats.p, stream);
+		if (rowaux_l2) launch_rowaux(X, xbf16, ld, dim, METRIC_L2, n_slots, num, rowaux_l2, stats.p + 2, stream);
 		HIPCHK(hipGetLastError());
 		HIPCHK(hipStreamSynchronize(stream));
 		refresh_stats();
@@ -257,20 +261,72 @@ struct Index {
 
 	int64_t add_host(const float *v, int64_t num) {
 		reserve(n_slots + num);
-		float *dst = X + n_slots * ld;
-		if (ld != dim) HIPCHK(hipMemsetAsync(dst, 0, (size_t)num * ld * sizeof(float), stream));
-		HIPCHK(hipMemcpy2DAsync(dst, (size_t)ld * sizeof(float), v, (size_t)dim * sizeof(float),
-		                        (size_t)dim * sizeof(float), (size_t)num, hipMemcpyHostToDevice, stream));
+		if (!xbf16) {
+			float *dst = reinterpret_cast<float *>(xrow(n_slots));
+			if (ld != dim) HIPCHK(hipMemsetAsync(dst, 0, (size_t)num * ld * sizeof(float), stream));
+			HIPCHK(hipMemcpy2DAsync(dst, (size_t)ld * sizeof(float), v, (size_t)dim * sizeof(float),
+			                        (size_t)dim * sizeof(float), (size_t)num, hipMemcpyHostToDevice, stream));
+		} else {
+			// bf16 store: f32 rows through a bounded device staging buffer
+			const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(num, (int64_t)(64 << 20) / (dim * 4)));
+			ws.stage.need((size_t)chunk * dim);
+			for (int64_t i = 0; i < num; i += chunk) {
+				const int64_t m = std::min<int64_t>(chunk, num - i);
+				HIPCHK(hipMemcpyAsync(ws.stage.p, v + i * dim, (size_t)m * dim * sizeof(float), hipMemcpyHostToDevice,
+				                      stream));
+				launch_rows_to_bf16(ws.stage.p, dim, m, dim, ld, reinterpret_cast<uint16_t *>(xrow(n_slots + i)),
+				                    stream);
+				HIPCHK(hipStreamSynchronize(stream));  // staging buffer reused
+			}
+		}
 		return commit_rows(num);
 	}
 
 	int64_t add_device(const float *v, int64_t num) {
 		reserve(n_slots + num);
-		float *dst = X + n_slots * ld;
-		if (ld != dim) HIPCHK(hipMemsetAsync(dst, 0, (size_t)num * ld * sizeof(float), stream));
-		HIPCHK(hipMemcpy2DAsync(dst, (size_t)ld * sizeof(float), v, (size_t)dim * sizeof(float),
-		                        (size_t)dim * sizeof(float), (size_t)num, hipMemcpyDeviceToDevice, stream));
+		if (!xbf16) {
+			float *dst = reinterpret_cast<float *>(xrow(n_slots));
+			if (ld != dim) HIPCHK(hipMemsetAsync(dst, 0, (size_t)num * ld * sizeof(float), stream));
+			HIPCHK(hipMemcpy2DAsync(dst, (size_t)ld * sizeof(float), v, (size_t)dim * sizeof(float),
+			                        (size_t)dim * sizeof(float), (size_t)num, hipMemcpyDeviceToDevice, stream));
+		} else {
+			launch_rows_to_bf16(v, dim, num, dim, ld, reinterpret_cast<uint16_t *>(xrow(n_slots)), stream);
+		}
 		return commit_rows(num);
+	}
+
+	// rows [s0, s0+n) as f32 (dim columns) into host memory
+	void read_rows(int64_t s0, int64_t n, float *out) {
+		if (n <= 0) return;
+		if (!xbf16) {
+			HIPCHK(hipMemcpy2D(out, (size_t)dim * sizeof(float), xrow(s0), (size_t)ld * sizeof(float),
+			                   (size_t)dim * sizeof(float), (size_t)n, hipMemcpyDeviceToHost));
+			return;
+		}
+		std::vector<uint16_t> b((size_t)n * dim);
+		HIPCHK(hipMemcpy2D(b.data(), (size_t)dim * 2, xrow(s0), (size_t)ld * 2, (size_t)dim * 2, (size_t)n,
+		                   hipMemcpyDeviceToHost));
+		for (size_t i = 0; i < b.size(); ++i) {
+			const uint32_t u = (uint32_t)b[i] << 16;
+			memcpy(out + i, &u, 4);
+		}
+	}
+
+	// storage "f32" | "bf16"; only while the store holds no rows
+	void set_storage(bool bf16) {
+		if (n_slots > 0) throw Error("storage can only be changed on an empty table");
+		if (bf16 == xbf16) return;
+		if (X) {
+			HIPCHK(hipFree(X));
+			HIPCHK(hipFree(rowaux));
+			HIPCHK(hipFree(dlabels));
+			if (rowaux_l2) HIPCHK(hipFree(rowaux_l2));
+			X = nullptr;
+			rowaux = rowaux_l2 = nullptr;
+			dlabels = nullptr;
+			cap = 0;
+		}
+		xbf16 = bf16;
 	}
 
 	int64_t slot_of(int64_t label) const {
@@ -310,21 +366,22 @@ struct Index {
 			if (live[(size_t)s]) keep.push_back(s);
 		const int64_t n = (int64_t)keep.size();
 		const int64_t c = round_up(std::max<int64_t>(4096, n), SCAN_BR);
-		float *nX = nullptr;
+		void *nX = nullptr;
 		float4 *na = nullptr, *na2 = nullptr;
 		int64_t *nl = nullptr;
-		HIPCHK(hipMalloc(&nX, (size_t)c * ld * sizeof(float)));
+		HIPCHK(hipMalloc(&nX, (size_t)c * ld * xes()));
 		HIPCHK(hipMalloc(&na, (size_t)c * sizeof(float4)));
 		HIPCHK(hipMalloc(&nl, (size_t)c * sizeof(int64_t)));
 		if (rowaux_l2) HIPCHK(hipMalloc(&na2, (size_t)c * sizeof(float4)));
 		if (n > 0) {
 			ws.idx.need((size_t)n);
 			HIPCHK(hipMemcpyAsync(ws.idx.p, keep.data(), (size_t)n * sizeof(int64_t), hipMemcpyHostToDevice, stream));
-			launch_gather_rows(X, rowaux, dlabels, ws.idx.p, n, ld, nX, na, nl, stream);
-			if (rowaux_l2) launch_gather_rows(X, rowaux_l2, dlabels, ws.idx.p, n, ld, nX, na2, nl, stream);
+			launch_gather_rows(X, xbf16, rowaux, dlabels, ws.idx.p, n, ld, nX, na, nl, stream);
+			if (rowaux_l2) launch_gather_rows(X, xbf16, rowaux_l2, dlabels, ws.idx.p, n, ld, nX, na2, nl, stream);
 			HIPCHK(hipGetLastError());
 		}
-		HIPCHK(hipMemsetAsync(nX + n * ld, 0, (size_t)(c - n) * ld * sizeof(float), stream));
+		HIPCHK(hipMemsetAsync(static_cast<uint8_t *>(nX) + (size_t)n * ld * xes(), 0, (size_t)(c - n) * ld * xes(),
+		                      stream));
 		launch_fill_rowaux(na, n, c, stream);
 		if (na2) launch_fill_rowaux(na2, n, c, stream);
 		HIPCHK(hipStreamSynchronize(stream));
@@ -377,6 +434,13 @@ struct Index {
 		fwrite(v, sizeof(float), (size_t)num * dim, log);
 		fflush(log);
 	}
+	void log_storage() {
+		if (!log) return;
+		uint8_t tag = 3, v = xbf16 ? 1 : 0;
+		fwrite(&tag, 1, 1, log);
+		fwrite(&v, 1, 1, log);
+		fflush(log);
+	}
 	void log_del(const std::vector<int64_t> &labs) {
 		if (!log || labs.empty()) return;
 		uint8_t tag = 2;
@@ -406,7 +470,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	const float4 *aux = (metric_quirk && metric != METRIC_L2) ? rowaux_l2 : rowaux;
 	const float ma = (metric_quirk && metric != METRIC_L2) ? max_alpha_l2 : max_alpha;
 	const float mu = (metric_quirk && metric != METRIC_L2) ? max_ux_l2 : max_ux;
-	StoreView sv{X, aux, dlabels, n_slots, ld, dim, eff_metric};
+	StoreView sv{X, aux, dlabels, n_slots, ld, dim, eff_metric, xbf16 ? 1 : 0};
 	const int nq_pad = (int)round_up(nq, SCAN_BQ);
 	ws.Qf.need((size_t)nq_pad * ld);
 	ws.Qb.need((size_t)nq_pad * ld);
@@ -446,8 +510,11 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		}
 	} else if (fast_ok) {
 		// 1) sample pass: dense LB over every stride-th tile -> tau[q]
-		const int64_t n_sample =
-		    std::min<int64_t>(n_tiles, std::max<int64_t>((n_tiles + sample_div - 1) / sample_div, 32));
+		// ~1/sample_div of the tiles, at least 32, at most one tile per CU
+		// (the dense LB matrix and its select grow with the sample)
+		const int64_t n_sample = std::min<int64_t>(
+		    n_tiles, std::max<int64_t>(std::min<int64_t>((n_tiles + sample_div - 1) / sample_div, scan_grid(1 << 30)),
+		                               32));
 		const int64_t stride = std::max<int64_t>(1, n_tiles / n_sample);
 		const int64_t cols = n_sample * SCAN_BR;
 		const int Ms = k + 8;
@@ -540,6 +607,10 @@ static void replay_log(Index *ix, const std::string &path) {
 			if (ix->n_slots > 0 && first <= ix->slot_label.back()) ix->compact();
 			ix->next_label = first;
 			ix->add_host(buf.data(), num);
+		} else if (tag == 3) {
+			uint8_t v;
+			if (fread(&v, 1, 1, f) != 1) break;
+			ix->set_storage(v == 1);
 		} else if (tag == 2) {
 			int64_t n;
 			if (fread(&n, 8, 1, f) != 1) break;
@@ -745,8 +816,7 @@ int32_t lance_detached_merge(void *target_handle, void *source_handle, const int
 			for (int64_t l : want) {
 				int64_t s = src->slot_of(l);
 				if (s < 0 || !src->live[(size_t)s]) continue;
-				HIPCHK(hipMemcpy(row.data(), src->X + s * src->ld, (size_t)src->dim * sizeof(float),
-				                 hipMemcpyDeviceToHost));
+				src->read_rows(s, 1, row.data());
 				vecs.insert(vecs.end(), row.begin(), row.end());
 				olds.push_back(l);
 			}
@@ -936,7 +1006,7 @@ int32_t lance_detached_get_vector(void *handle, int64_t label, float *out_vec, i
 			return -1;
 		}
 		ix->bind();
-		HIPCHK(hipMemcpy(out_vec, ix->X + s * ix->ld, (size_t)ix->dim * sizeof(float), hipMemcpyDeviceToHost));
+		ix->read_rows(s, 1, out_vec);
 		return ix->dim;
 	}
 	API_GUARD("get_vector failed: ", -1)
@@ -955,8 +1025,7 @@ int32_t lance_detached_get_all_vectors(void *handle, int64_t *out_labels, float 
 		if (out_labels && out_vectors && ix->n_live > 0) {
 			ix->bind();
 			std::vector<float> all((size_t)ix->n_slots * ix->dim);
-			HIPCHK(hipMemcpy2D(all.data(), (size_t)ix->dim * sizeof(float), ix->X, (size_t)ix->ld * sizeof(float),
-			                   (size_t)ix->dim * sizeof(float), (size_t)ix->n_slots, hipMemcpyDeviceToHost));
+			ix->read_rows(0, ix->n_slots, all.data());
 			int64_t j = 0;
 			for (int64_t s = 0; s < ix->n_slots; ++s) {
 				if (!ix->live[(size_t)s]) continue;
@@ -986,7 +1055,7 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 				ix->bind();
 				HIPCHK(hipMalloc(&ix->rowaux_l2, (size_t)std::max<int64_t>(ix->cap, 1) * sizeof(float4)));
 				if (ix->n_slots > 0) {
-					lhip::launch_rowaux(ix->X, ix->ld, ix->dim, lhip::METRIC_L2, 0, ix->n_slots, ix->rowaux_l2,
+					lhip::launch_rowaux(ix->X, ix->xbf16, ix->ld, ix->dim, lhip::METRIC_L2, 0, ix->n_slots, ix->rowaux_l2,
 					                    ix->stats.p + 2, ix->stream);
 					// re-apply tombstones
 					std::vector<int64_t> dead;
@@ -1012,6 +1081,14 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 				if (!e) HIPCHK(hipEventCreate(&e));
 			ix->kt_append_ms = ix->kt_dense_ms = 0.0;
 			ix->kt_append_n = ix->kt_dense_n = 0;
+			return 0;
+		}
+		if (k == "storage") {
+			if (v != "f32" && v != "bf16") throw Error("storage must be 'f32' or 'bf16'");
+			ix->bind();
+			const bool was = ix->xbf16;
+			ix->set_storage(v == "bf16");
+			if (was != ix->xbf16) ix->log_storage();
 			return 0;
 		}
 		if (k == "sample_div") {
