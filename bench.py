@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--metric", default=None)
+    ap.add_argument("--storage", choices=["f32", "bf16"], default=None, help="index option storage")
+    ap.add_argument("--scan-copy", choices=["on", "off"], default="on", help="index option scan_copy")
     ap.add_argument("--recall-queries", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -87,7 +89,7 @@ def gen_rows(start, stop, dim, device, seed=1234, normalize=False):
     return out
 
 
-def measured_traffic(n, dim, batch):
+def measured_traffic(n, dim, batch, elem_bytes):
     """Per-launch HBM bytes of the scan kernel from the committed rocprofv3 PMC
     passes (profiles/*_scan_traffic.json, made by tools/pmc_traffic.py from
     separate FETCH_SIZE / WRITE_SIZE runs of this bench) for the same shape."""
@@ -100,7 +102,7 @@ def measured_traffic(n, dim, batch):
                 t = json.load(fh)
         except (OSError, ValueError):
             continue
-        if (t.get("n"), t.get("dim"), t.get("batch")) == (n, dim, batch):
+        if (t.get("n"), t.get("dim"), t.get("batch"), t.get("scan_elem_bytes", 4)) == (n, dim, batch, elem_bytes):
             best = t
     return None if best is None else int(best["traffic_bytes_per_launch"])
 
@@ -133,6 +135,7 @@ def main():
     if not h:
         raise RuntimeError(e.value.decode())
     lance_hip.LanceHipSetOption(h, "storage", a.storage)
+    lance_hip.LanceHipSetOption(h, "scan_copy", a.scan_copy)
     lance_hip.LanceHipSetOption(h, "reserve_rows", str(n_local))
     if a.sample_div:
         lance_hip.LanceHipSetOption(h, "sample_div", str(a.sample_div))
@@ -225,17 +228,17 @@ def main():
         roof = None
         if kt["scan_launches"] > 0:
             ld = ((D + 63) // 64) * 64
-            esz = 2 if a.storage == "bf16" else 4
+            esz = kt.get("scan_elem_bytes") or (2 if a.storage == "bf16" else 4)
             avg_ms = kt["scan_ms_total"] / kt["scan_launches"]
             # algorithmic bytes per launch: every base row (ld elements + 16 B row aux) + the bf16 query tile
             bytes_launch = kt["scan_rows"] * (ld * esz + 16) + kt["scan_qpad"] * ld * 2
             ach = bytes_launch / (avg_ms * 1e-3) / 1e9
-            traffic = measured_traffic(N // world, D, B) if a.config == "c2" else None
+            traffic = measured_traffic(N // world, D, B, esz) if a.config == "c2" else None
             mfma_tfs = 2.0 * kt["scan_rows"] * D * B / (avg_ms * 1e-3) / 1e12
             kname = {"l2": "L2", "dot": "DOT", "cosine": "COSINE"}[a.metric]
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": f"scan_kernel<{kname},append,{a.storage}>",
+                    "kernel": f"scan_kernel<{kname},append,{'bf16' if esz == 2 else 'f32'}>",
                     "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(bytes_launch),
                     "mfma_tflops": round(mfma_tfs, 1), "mfma_frac": round(mfma_tfs / MFMA_BF16_PEAK_TFS, 4)}
         metric_name = ("kNN queries/sec + recall@10, 1Mx768 f32 flat; GB/s vs HBM roofline" if a.config == "c2" else

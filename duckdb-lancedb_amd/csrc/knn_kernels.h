@@ -31,6 +31,11 @@ struct StoreView {
 	int dim;
 	int metric;
 	int xbf16;               // base stored as bf16 (storage option "bf16")
+	// What the scan kernels stream: the bf16 scan copy of an f32 store, the
+	// bf16 store itself, or (scan_copy off) the f32 rows.  The row aux bounds
+	// hold for either: ux covers |x - bf16(x)| with the same RNE rounding.
+	const void *Xscan;
+	int scan_bf16;
 };
 
 // Per-query constants for the lower-bound epilogue:

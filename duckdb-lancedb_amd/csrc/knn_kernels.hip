@@ -305,6 +305,12 @@ constexpr int BR = SCAN_BR, BQ = SCAN_BQ;
 #ifndef LHIP_ABL_NO_EPILOGUE
 #define LHIP_ABL_NO_EPILOGUE 0
 #endif
+#ifndef LHIP_ABL_NO_MFMA
+#define LHIP_ABL_NO_MFMA 0  // fragments read, no MFMA
+#endif
+#ifndef LHIP_ABL_NO_READS
+#define LHIP_ABL_NO_READS 0  // no fragment reads (MFMAs on stale registers)
+#endif
 #ifndef LHIP_ABL_NO_SLOW
 #define LHIP_ABL_NO_SLOW 0  // survivors are tested but not written
 #endif
@@ -660,6 +666,17 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 		}
 	}
 	auto read_half = [&](Frag &f, const uint8_t *st_base, int kk) {
+		if (LHIP_ABL_NO_READS) {
+			float4 z;
+			bf16x8 zb;
+			asm volatile("" : "=v"(z));
+			asm volatile("" : "=v"(zb));
+#pragma unroll
+			for (int t = 0; t < 2; ++t) f.a[t][0] = f.a[t][1] = z;
+#pragma unroll
+			for (int u = 0; u < 4; ++u) f.b[u] = zb;
+			return;
+		}
 #pragma unroll
 		for (int t = 0; t < 2; ++t) {
 			f.a[t][0] = *reinterpret_cast<const float4 *>(st_base + aoff[kk][t][0]);
@@ -686,7 +703,12 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 				av[7] = (__bf16)hi.w;
 			}
 #pragma unroll
-			for (int u = 0; u < 4; ++u) acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, f.b[u], acc[t][u], 0, 0, 0);
+			for (int u = 0; u < 4; ++u) {
+				if (LHIP_ABL_NO_MFMA)
+					asm volatile("" ::"v"(av), "v"(f.b[u]));
+				else
+					acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, f.b[u], acc[t][u], 0, 0, 0);
+			}
 		}
 	};
 
@@ -800,11 +822,12 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 			// tau = +inf (fewer live sample rows than needed) must still drop
 			// dead rows (LB = +inf): compare against min(tau, FLT_MAX)
 			float4 qa[4];
-			float tq[4];
+			float tq[4], tqs[4];
 #pragma unroll
 			for (int u = 0; u < 4; ++u) {
 				qa[u] = QA[qlb + 32 * u];
 				tq[u] = fminf(TAU[qlb + 32 * u], F_MAX);
+				tqs[u] = fmaxf(tq[u], -F_MAX);
 			}
 			// Per group of 4 rows x 4 queries (16 bounds per lane): the bounds
 			// of two consecutive rows are one v_pk_fma_f32 chain (row terms are
@@ -820,16 +843,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 				for (int gq = 0; gq < 4; ++gq) {
 					const int r0 = rb + 32 * t + 8 * gq;
 					float l[4][4];
-					uint64_t m[4][4], any = 0;
 					if (FOLD) {
 #pragma unroll
 						for (int j = 0; j < 4; ++j)
 #pragma unroll
-							for (int u = 0; u < 4; ++u) {
-								l[j][u] = acc[t][u][4 * gq + j];
-								m[j][u] = __builtin_amdgcn_ballot_w64(l[j][u] <= tq[u]);
-								any |= m[j][u];
-							}
+							for (int u = 0; u < 4; ++u) l[j][u] = acc[t][u][4 * gq + j];
 					}
 					const float4 al = FOLD ? make_float4(0.f, 0.f, 0.f, 0.f) : ra4(r0, 0);
 					const float4 xn = FOLD ? al : ra4(r0, 1), ux = FOLD ? al : ra4(r0, 2);
@@ -852,11 +870,19 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 							y = y + Cq;
 							l[2 * p][u] = y.x;
 							l[2 * p + 1][u] = y.y;
-							m[2 * p][u] = __builtin_amdgcn_ballot_w64(y.x <= tq[u]);
-							m[2 * p + 1][u] = __builtin_amdgcn_ballot_w64(y.y <= tq[u]);
-							any |= m[2 * p][u] | m[2 * p + 1][u];
 						}
 					}
+					// Screen: one ballot per group.  min_j l[j][u] - tq[u] <= 0
+					// iff some l[j][u] <= tq[u] (exact sign of the rounded
+					// difference; a flushed denormal only adds a false
+					// positive, rechecked below; NaN bounds never pass either
+					// test; tq clamped to >= -FLT_MAX so -inf - -inf = NaN
+					// cannot hide a -inf bound).
+					float scr = F_MAX;
+#pragma unroll
+					for (int u = 0; u < 4; ++u)
+						scr = fminf(scr, fminf(fminf(l[0][u], l[1][u]), fminf(l[2][u], l[3][u])) - tqs[u]);
+					const uint64_t any = __builtin_amdgcn_ballot_w64(scr <= 0.f);
 					if (LHIP_ABL_NO_SLOW) {
 						asm volatile("" ::"s"(any));  // masks computed, nothing written
 					} else if (any) {
@@ -870,9 +896,13 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 						// the bound: compact code (the epilogue must stay resident
 						// in the instruction cache; 16 unrolled copies per group
 						// would not).
+						uint64_t m[4][4];
 						uint32_t kmask = 0;
 #pragma unroll
-						for (int k = 0; k < 16; ++k) kmask |= (m[k >> 2][k & 3] != 0ull ? 1u : 0u) << k;
+						for (int k = 0; k < 16; ++k) {
+							m[k >> 2][k & 3] = __builtin_amdgcn_ballot_w64(l[k >> 2][k & 3] <= tq[k & 3]);
+							kmask |= (m[k >> 2][k & 3] != 0ull ? 1u : 0u) << k;
+						}
 						while (kmask) {
 							const int k = __builtin_ctz(kmask);
 							kmask &= kmask - 1;
@@ -967,17 +997,17 @@ static void scan_dispatch_x(const StoreView &s, const QueryView &q, int64_t n_ti
 	dim3 block(SCAN_THREADS);
 	switch (s.metric) {
 	case METRIC_L2:
-		scan_kernel<METRIC_L2, MODE, XB><<<grid, block, 0, st>>>(s.X, s.rowaux, s.ld, q.Qb, q.qaux, q.nq, (int)n_tiles,
+		scan_kernel<METRIC_L2, MODE, XB><<<grid, block, 0, st>>>(s.Xscan, s.rowaux, s.ld, q.Qb, q.qaux, q.nq, (int)n_tiles,
 		                                                          (int)tile_stride, dense, ld_out, tau, seg_pool,
 		                                                          seg_cnt, seg_cap);
 		break;
 	case METRIC_DOT:
-		scan_kernel<METRIC_DOT, MODE, XB><<<grid, block, 0, st>>>(s.X, s.rowaux, s.ld, q.Qb, q.qaux, q.nq, (int)n_tiles,
+		scan_kernel<METRIC_DOT, MODE, XB><<<grid, block, 0, st>>>(s.Xscan, s.rowaux, s.ld, q.Qb, q.qaux, q.nq, (int)n_tiles,
 		                                                           (int)tile_stride, dense, ld_out, tau, seg_pool,
 		                                                           seg_cnt, seg_cap);
 		break;
 	default:
-		scan_kernel<METRIC_COSINE, MODE, XB><<<grid, block, 0, st>>>(s.X, s.rowaux, s.ld, q.Qb, q.qaux, q.nq,
+		scan_kernel<METRIC_COSINE, MODE, XB><<<grid, block, 0, st>>>(s.Xscan, s.rowaux, s.ld, q.Qb, q.qaux, q.nq,
 		                                                              (int)n_tiles, (int)tile_stride, dense, ld_out,
 		                                                              tau, seg_pool, seg_cnt, seg_cap);
 		break;
@@ -988,7 +1018,7 @@ template <int MODE>
 static void scan_dispatch(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, float *dense,
                           int64_t ld_out, const float *tau, uint2 *seg_pool, int *seg_cnt, int seg_cap,
                           hipStream_t st) {
-	if (s.xbf16)
+	if (s.scan_bf16)
 		scan_dispatch_x<MODE, true>(s, q, n_tiles, tile_stride, dense, ld_out, tau, seg_pool, seg_cnt, seg_cap, st);
 	else
 		scan_dispatch_x<MODE, false>(s, q, n_tiles, tile_stride, dense, ld_out, tau, seg_pool, seg_cnt, seg_cap, st);

@@ -129,6 +129,11 @@ struct Index {
 	bool xbf16 = false;
 	size_t xes() const { return xbf16 ? 2 : 4; }
 	uint8_t *xrow(int64_t s) const { return static_cast<uint8_t *>(X) + (size_t)s * ld * xes(); }
+	// bf16 scan copy of an f32 store (option scan_copy, default on): the scan
+	// streams 2 B per element; refine, get_vector and compact use the f32 rows
+	uint16_t *Xs = nullptr;
+	bool scan_copy = true;
+	bool has_scan_copy() const { return !xbf16 && scan_copy; }
 	float4 *rowaux = nullptr;  // aux for `metric`
 	float4 *rowaux_l2 = nullptr;  // aux for L2 when metric_quirk is on and metric != l2
 	int64_t *dlabels = nullptr;
@@ -158,6 +163,7 @@ struct Index {
 		if (log) fclose(log);
 		(void)hipSetDevice(device);
 		if (X) (void)hipFree(X);
+		if (Xs) (void)hipFree(Xs);
 		if (rowaux) (void)hipFree(rowaux);
 		if (rowaux_l2) (void)hipFree(rowaux_l2);
 		if (dlabels) (void)hipFree(dlabels);
@@ -198,14 +204,17 @@ struct Index {
 		// zero: the scan kernel streams whole tiles without clamping rows
 		int64_t c = round_up(std::max<int64_t>(want, std::max<int64_t>(4096, cap * 2)), SCAN_BR);
 		void *nX = nullptr;
+		uint16_t *nXs = nullptr;
 		float4 *na = nullptr, *na2 = nullptr;
 		int64_t *nl = nullptr;
 		HIPCHK(hipMalloc(&nX, (size_t)c * ld * xes()));
+		if (has_scan_copy()) HIPCHK(hipMalloc(&nXs, (size_t)c * ld * 2));
 		HIPCHK(hipMalloc(&na, (size_t)c * sizeof(float4)));
 		HIPCHK(hipMalloc(&nl, (size_t)c * sizeof(int64_t)));
 		if (rowaux_l2 || (metric_quirk && metric != METRIC_L2)) HIPCHK(hipMalloc(&na2, (size_t)c * sizeof(float4)));
 		if (n_slots > 0) {
 			HIPCHK(hipMemcpyAsync(nX, X, (size_t)n_slots * ld * xes(), hipMemcpyDeviceToDevice, stream));
+			if (nXs) HIPCHK(hipMemcpyAsync(nXs, Xs, (size_t)n_slots * ld * 2, hipMemcpyDeviceToDevice, stream));
 			// row aux is tile-blocked SoA: move whole tile blocks (cap is a
 			// multiple of SCAN_BR, so they exist in the old buffer)
 			const size_t aux_bytes = (size_t)round_up(n_slots, SCAN_BR) * sizeof(float4);
@@ -215,10 +224,13 @@ struct Index {
 		}
 		HIPCHK(hipMemsetAsync(static_cast<uint8_t *>(nX) + (size_t)n_slots * ld * xes(), 0,
 		                      (size_t)(c - n_slots) * ld * xes(), stream));
+		if (nXs) HIPCHK(hipMemsetAsync(nXs + (size_t)n_slots * ld, 0, (size_t)(c - n_slots) * ld * 2, stream));
 		launch_fill_rowaux(na, n_slots, c, stream);
 		if (na2) launch_fill_rowaux(na2, n_slots, c, stream);
 		HIPCHK(hipStreamSynchronize(stream));
 		if (X) HIPCHK(hipFree(X));
+		if (Xs) HIPCHK(hipFree(Xs));
+		Xs = nXs;
 		if (rowaux) HIPCHK(hipFree(rowaux));
 		if (dlabels) HIPCHK(hipFree(dlabels));
 		if (rowaux_l2) HIPCHK(hipFree(rowaux_l2));
@@ -239,6 +251,31 @@ struct Index {
 		memcpy(&max_ux_l2, &h[3], 4);
 	}
 
+	// scan copy rows [s0, s0+n) = bf16 (RNE) of the f32 rows of X (padding
+	// columns stay zero)
+	void fill_scan_copy(int64_t s0, int64_t n, uint16_t *dst) {
+		if (n > 0)
+			launch_rows_to_bf16(reinterpret_cast<const float *>(xrow(s0)), ld, n, dim, ld, dst + (size_t)s0 * ld,
+			                    stream);
+	}
+
+	// option scan_copy: build or drop the bf16 scan copy of an f32 store
+	void set_scan_copy(bool on) {
+		if (on == scan_copy) return;
+		scan_copy = on;
+		if (!on) {
+			if (Xs) HIPCHK(hipFree(Xs));
+			Xs = nullptr;
+			return;
+		}
+		if (xbf16 || !X) return;  // allocated with the store
+		HIPCHK(hipMalloc(&Xs, (size_t)cap * ld * 2));
+		HIPCHK(hipMemsetAsync(Xs, 0, (size_t)cap * ld * 2, stream));
+		fill_scan_copy(0, n_slots, Xs);
+		HIPCHK(hipGetLastError());
+		HIPCHK(hipStreamSynchronize(stream));
+	}
+
 	// append rows already resident on the device at X[n_slots .. n_slots+num)
 	int64_t commit_rows(int64_t num) {
 		const int64_t first = next_label;
@@ -246,6 +283,7 @@ struct Index {
 		for (int64_t i = 0; i < num; ++i) labs[(size_t)i] = first + i;
 		HIPCHK(hipMemcpyAsync(dlabels + n_slots, labs.data(), (size_t)num * sizeof(int64_t), hipMemcpyHostToDevice,
 		                      stream));
+		if (Xs) fill_scan_copy(n_slots, num, Xs);
 		launch_rowaux(X, xbf16, ld, dim, metric, n_slots, num, rowaux, stats.p, stream);
 		if (rowaux_l2) launch_rowaux(X, xbf16, ld, dim, METRIC_L2, n_slots, num, rowaux_l2, stats.p + 2, stream);
 		HIPCHK(hipGetLastError());
@@ -318,6 +356,8 @@ struct Index {
 		if (bf16 == xbf16) return;
 		if (X) {
 			HIPCHK(hipFree(X));
+			if (Xs) HIPCHK(hipFree(Xs));
+			Xs = nullptr;
 			HIPCHK(hipFree(rowaux));
 			HIPCHK(hipFree(dlabels));
 			if (rowaux_l2) HIPCHK(hipFree(rowaux_l2));
@@ -384,7 +424,17 @@ struct Index {
 		                      stream));
 		launch_fill_rowaux(na, n, c, stream);
 		if (na2) launch_fill_rowaux(na2, n, c, stream);
+		uint16_t *nXs = nullptr;
+		if (Xs) {
+			HIPCHK(hipMalloc(&nXs, (size_t)c * ld * 2));
+			HIPCHK(hipMemsetAsync(nXs, 0, (size_t)c * ld * 2, stream));
+			if (n > 0)
+				launch_rows_to_bf16(static_cast<const float *>(nX), ld, n, dim, ld, nXs, stream);
+			HIPCHK(hipGetLastError());
+		}
 		HIPCHK(hipStreamSynchronize(stream));
+		if (Xs) HIPCHK(hipFree(Xs));
+		Xs = nXs;
 		HIPCHK(hipFree(X));
 		HIPCHK(hipFree(rowaux));
 		HIPCHK(hipFree(dlabels));
@@ -470,7 +520,8 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	const float4 *aux = (metric_quirk && metric != METRIC_L2) ? rowaux_l2 : rowaux;
 	const float ma = (metric_quirk && metric != METRIC_L2) ? max_alpha_l2 : max_alpha;
 	const float mu = (metric_quirk && metric != METRIC_L2) ? max_ux_l2 : max_ux;
-	StoreView sv{X, aux, dlabels, n_slots, ld, dim, eff_metric, xbf16 ? 1 : 0};
+	StoreView sv{X, aux, dlabels, n_slots, ld, dim, eff_metric, xbf16 ? 1 : 0,
+	             Xs ? static_cast<const void *>(Xs) : X, (xbf16 || Xs) ? 1 : 0};
 	const int nq_pad = (int)round_up(nq, SCAN_BQ);
 	ws.Qf.need((size_t)nq_pad * ld);
 	ws.Qb.need((size_t)nq_pad * ld);
@@ -1091,6 +1142,12 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			if (was != ix->xbf16) ix->log_storage();
 			return 0;
 		}
+		if (k == "scan_copy") {
+			if (v != "on" && v != "off") throw Error("scan_copy must be 'on' or 'off'");
+			ix->bind();
+			ix->set_scan_copy(v == "on");
+			return 0;
+		}
 		if (k == "sample_div") {
 			const int d = std::stoi(v);
 			if (d < 1) throw Error("sample_div must be >= 1");
@@ -1117,14 +1174,16 @@ int32_t lance_hip_last_search_stats(void *handle, int64_t *out, int32_t n) {
 
 // out[0] = total ms of threshold-scan launches, out[1] = their count,
 // out[2] = rows scanned per launch, out[3] = padded queries per launch,
-// out[4] = total ms of small-store dense scans, out[5] = their count.
+// out[4] = total ms of small-store dense scans, out[5] = their count,
+// out[6] = bytes per element the scan streams (2: bf16 store or scan copy).
 int32_t lance_hip_kernel_times(void *handle, double *out, int32_t n) {
 	if (!handle || !out) return -1;
 	Index *ix = as_index(handle);
 	std::lock_guard<std::mutex> g(ix->mu);
-	double v[6] = {ix->kt_append_ms, (double)ix->kt_append_n, (double)ix->kt_append_rows,
-	               (double)ix->kt_append_qpad, ix->kt_dense_ms, (double)ix->kt_dense_n};
-	for (int32_t i = 0; i < n && i < 6; ++i) out[i] = v[i];
+	double v[7] = {ix->kt_append_ms, (double)ix->kt_append_n, (double)ix->kt_append_rows,
+		               (double)ix->kt_append_qpad, ix->kt_dense_ms, (double)ix->kt_dense_n,
+		               (ix->xbf16 || ix->Xs) ? 2.0 : 4.0};
+		for (int32_t i = 0; i < n && i < 7; ++i) out[i] = v[i];
 	return 0;
 }
 

@@ -317,10 +317,11 @@ def LanceHipLastSearchStats(handle) -> dict:
 
 
 def LanceHipKernelTimes(handle) -> dict:
-    out = np.zeros(6, np.float64)
-    lib().lance_hip_kernel_times(handle, out.ctypes.data, 6)
+    out = np.zeros(7, np.float64)
+    lib().lance_hip_kernel_times(handle, out.ctypes.data, 7)
     return {"scan_ms_total": float(out[0]), "scan_launches": int(out[1]), "scan_rows": int(out[2]),
-            "scan_qpad": int(out[3]), "dense_ms_total": float(out[4]), "dense_launches": int(out[5])}
+            "scan_qpad": int(out[3]), "dense_ms_total": float(out[4]), "dense_launches": int(out[5]),
+            "scan_elem_bytes": int(out[6])}
 
 
 def LanceHipMergeTopk(part_labels, part_dists, part_counts):

@@ -150,6 +150,14 @@ int32_t lance_hip_device_count(void);
  *                  metric, exactly as the reference does (lance_manager.rs:
  *                  411-418 never sets distance_type); default "0"
  *   "reserve_rows" pre-size the device store for this many rows
+ *   "storage"      "f32" (default) | "bf16": element type of the device store;
+ *                  bf16 keeps the nearest-even bf16 of each added row and every
+ *                  result is exact with respect to those stored rows.  Only
+ *                  while the table holds no rows.
+ *   "scan_copy"    "on" (default) | "off": an f32 store also keeps a bf16 copy
+ *                  of its rows that the scan streams (2 B per element instead
+ *                  of 4; +50% device memory); refine and get_vector read the
+ *                  f32 rows, results are unchanged
  *   "sample_div"   the threshold sample pass covers ~1/sample_div of the row
  *                  tiles (at least 32 tiles); default "32"
  *   "time_kernels" "1" = record HIP events around scan launches
@@ -168,7 +176,8 @@ int32_t lance_hip_last_search_stats(void *handle, int64_t *out, int32_t n);
  * "time_kernels"="1"; events recorded on the handle's stream around each launch):
  * out[0] total ms of threshold-scan launches, out[1] their count, out[2] rows
  * per launch, out[3] padded queries per launch, out[4] total ms of small-store
- * dense scans, out[5] their count.  Returns 0 or -1. */
+ * dense scans, out[5] their count, out[6] bytes per element the scan streams
+ * (2 with a bf16 store or scan copy, else 4).  Returns 0 or -1. */
 int32_t lance_hip_kernel_times(void *handle, double *out, int32_t n);
 
 /* Device-pointer ingest: num x dim row-major f32 already on the handle's device.

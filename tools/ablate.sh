@@ -20,6 +20,9 @@ for v in "$@"; do
 	NT0) build NT0 -DLHIP_X_NT=0 ;;
 	PROF) build PROF -DLHIP_PROF=1 ;;
 	NOSLOW) build NOSLOW -DLHIP_ABL_NO_SLOW=1 ;;
+	NOREADS) build NOREADS -DLHIP_ABL_NO_READS=1 ;;
+	NOMFMA_NOREADS) build NOMFMA_NOREADS -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 ;;
+	NOMFMA_NOREADS_NOEPI) build NOMFMA_NOREADS_NOEPI -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 -DLHIP_ABL_NO_EPILOGUE=1 ;;
 	NOFLUSH) build NOFLUSH -DLHIP_ABL_NO_FLUSH=1 ;;
 	PROFER0) build PROFER0 -DLHIP_PROF=1 -DLHIP_EARLY_REFILL=0 ;;
 	ER1) build ER1 -DLHIP_EARLY_REFILL=1 ;;

@@ -33,13 +33,14 @@ def main():
     ap.add_argument("--n", type=int, required=True)
     ap.add_argument("--dim", type=int, required=True)
     ap.add_argument("--batch", type=int, required=True)
+    ap.add_argument("--elem-bytes", type=int, default=4, help="bytes per element the scan streams")
     ap.add_argument("--kernel", default="scan_kernel<0, 1>")
     a = ap.parse_args()
     fk, nf = per_launch(a.fetch_dir, "FETCH_SIZE", a.kernel)
     wk, nw = per_launch(a.write_dir, "WRITE_SIZE", a.kernel)
     read_b = 2.0 * fk * 1024.0
     write_b = wk * 1024.0
-    out = {"kernel": a.kernel, "n": a.n, "dim": a.dim, "batch": a.batch, "launches": [nf, nw],
+    out = {"kernel": a.kernel, "n": a.n, "dim": a.dim, "batch": a.batch, "scan_elem_bytes": a.elem_bytes, "launches": [nf, nw],
            "fetch_size_kib_per_launch": fk, "write_size_kib_per_launch": wk,
            "hbm_read_bytes_corrected": read_b, "hbm_write_bytes": write_b,
            "traffic_bytes_per_launch": read_b + write_b,
