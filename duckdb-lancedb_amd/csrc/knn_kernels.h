@@ -81,6 +81,13 @@ void launch_scan_dense(const StoreView &s, const QueryView &q, int64_t n_tiles, 
 void launch_scan_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
                         int seg_cap, hipStream_t st);
 
+// Sample scan over row tiles t*tile_stride, t < n_tiles (persistent, scan_grid(n_tiles)
+// workgroups): for every tile, each 64-row quarter appends its smallest lower
+// bound per query, (orderedkey(LB), slot), to the workgroup's segment as
+// launch_scan_append does (4 entries per tile and query; +inf bounds skipped).
+void launch_scan_tilemin(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, uint2 *seg_pool,
+                         int *seg_cnt, int seg_cap, hipStream_t st);
+
 // Workgroups a scan over n_tiles tiles launches (= min(n_tiles, CUs)).
 int scan_grid(int64_t n_tiles);
 
@@ -89,7 +96,7 @@ int scan_grid(int64_t n_tiles);
 // selected (+inf when nothing live was left out; -inf when unknown -> the
 // certificate fails).  Dense source: n_entries per query, entry i -> slot
 // (i/BR)*stride*BR + i%BR.  Segment source: the append scan's output;
-// pool_total[q] = entries seen (-1 on overflow).
+// pool_total[q] = entries seen (-1 on overflow); tau may be null (= +inf).
 void launch_select_dense(const float *dense, int64_t ld_dense, int64_t n_entries, int64_t tile_stride, int nq, int M,
                          uint32_t *cand_slot, int *cand_cnt, float *cut, hipStream_t st);
 void launch_select_segments(const uint2 *seg_pool, const int *seg_cnt, int seg_cap, int n_seg, const float *tau,

@@ -311,6 +311,9 @@ constexpr int BR = SCAN_BR, BQ = SCAN_BQ;
 #ifndef LHIP_ABL_NO_READS
 #define LHIP_ABL_NO_READS 0  // no fragment reads (MFMAs on stale registers)
 #endif
+#ifndef LHIP_ABL_NO_QDMA
+#define LHIP_ABL_NO_QDMA 0  // query stages are not streamed (stale LDS)
+#endif
 #ifndef LHIP_ABL_NO_SLOW
 #define LHIP_ABL_NO_SLOW 0  // survivors are tested but not written
 #endif
@@ -338,7 +341,10 @@ extern "C" int lhip_prof_read(unsigned long long *out, int reset) {
 #define PROF_T(v)
 #endif
 #ifndef LHIP_X_NT
-#define LHIP_X_NT 1  // non-temporal policy on the once-read base stream
+#define LHIP_X_NT 0  // nt on the base stream: measured slower (bf16 scan 0.59 vs 0.525 ms)
+#endif
+#ifndef LHIP_NST_BF16
+#define LHIP_NST_BF16 3  // 3 measured faster than 4 (0.495 vs 0.511 ms) and 2 (0.552)
 #endif
 
 constexpr int SCAN_THREADS = 512;
@@ -363,12 +369,12 @@ struct ScanCfg {
 	static constexpr int XROW = SK * XE;                       // bytes per row and stage: 64 / 128
 	static constexpr int XCH = XROW / 16;                      // 16 B chunks per row: 4 / 8
 	static constexpr int XST = BR * XROW;                      // 16 / 32 KiB
-	static constexpr int NST = XB ? 4 : 3;                     // ring slots
+	static constexpr int NST = XB ? LHIP_NST_BF16 : 3;         // ring slots
 	static constexpr int STAGE = XST + QST_BYTES;
 	static constexpr int RING = NST * STAGE;                   // 128 / 144 KiB
 	static constexpr int XDMA = XST / 1024 / SCAN_WAVES;       // X DMA instructions per wave and stage: 2 / 4
 	static constexpr int ROWS_PER_DMA = 1024 / XROW;           // 16 / 8
-	static constexpr int DMA = XDMA + Q_DMA_PER_WAVE;          // + 1 row aux on waves 0..3 at a tile's stage 0
+	static constexpr int DMA = XDMA + (LHIP_ABL_NO_QDMA ? 0 : Q_DMA_PER_WAVE);  // + 1 row aux on waves 0..3 at a tile's stage 0
 	static constexpr int LDS = RING + RA_BYTES + CNT_BYTES + QA_BYTES + LIST_BYTES;
 	static_assert(LDS <= 160 * 1024, "LDS budget");
 	static_assert(XDMA * SCAN_WAVES * 1024 == XST, "X stage = whole DMA instructions");
@@ -484,7 +490,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 		const int q = q0 + tid;
 		QA[tid] = qaux[q];
 		TAU[tid] = (MODE == 1 && q < nq) ? tau[q] : -F_INF;
-		if (MODE == 1) CNT[tid] = 0u;
+		if (MODE >= 1) CNT[tid] = 0u;
 	}
 	LHIP_WAIT_VM(0);  // the ordinary loads above, before any counted DMA wait
 	__syncthreads();
@@ -524,7 +530,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 		for (int j = 0; j < C::XDMA; ++j)
 			dma16s<LHIP_X_NT>(iss_xt, xoff[j], iss_lds + (uint32_t)(C::XDMA * w + j) * 1024u);
 #pragma unroll
-		for (int j = 0; j < Q_DMA_PER_WAVE; ++j)
+		for (int j = 0; j < (LHIP_ABL_NO_QDMA ? 0 : Q_DMA_PER_WAVE); ++j)
 			dma16s(iss_q, qoff[j], iss_lds + (uint32_t)C::XST + (uint32_t)(Q_DMA_PER_WAVE * w + j) * 1024u);
 		++iss_g;
 		iss_lds = iss_lds + C::STAGE == lds0 + C::RING ? lds0 : iss_lds + C::STAGE;
@@ -740,7 +746,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 		if (iss_g == g + C::NST) {
 			// steady state: stages g+2 .. g+NST-1 in flight after g+1; the one
 			// extra DMA on waves 0..3 if one of them is a tile's stage 0
-			const bool st0 = cur_s + 2 == S || (C::NST == 4 && (cur_s + 3 == S || (S == 2 && cur_s == 1)));
+			static_assert(C::NST >= 2 && C::NST <= 4, "steady-state wait counts below");
+			const bool st0 = C::NST >= 3 && (cur_s + 2 == S || (C::NST == 4 && (cur_s + 3 == S || (S == 2 && cur_s == 1))));
 			if (ra_wave && st0)
 				wait_vm_c<(C::NST - 2) * C::DMA + 1>();
 			else
@@ -817,6 +824,46 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 						    lower_bound<METRIC>(acc[t][u][4 * gq + 2], make_float4(al.z, xn.z, ux.z, sc.z), qa),
 						    lower_bound<METRIC>(acc[t][u][4 * gq + 3], make_float4(al.w, xn.w, ux.w, sc.w), qa));
 					}
+			}
+		} else if (MODE == 2) {
+			// sample pass: per query, the smallest bound of this wave's 64 rows
+			// (lanes l and l^32 hold 32 rows each) -> one segment entry
+#pragma unroll
+			for (int u = 0; u < 4; ++u) {
+				const float4 qa = QA[qlb + 32 * u];
+				float mv = F_INF;
+				int mr = 0;
+#pragma unroll
+				for (int t = 0; t < 2; ++t)
+#pragma unroll
+					for (int gq = 0; gq < 4; ++gq) {
+						const int r0 = rb + 32 * t + 8 * gq;
+						float4 al, xn, ux, sc;
+						if (!FOLD) al = ra4(r0, 0), xn = ra4(r0, 1), ux = ra4(r0, 2), sc = ra4(r0, 3);
+#pragma unroll
+						for (int j = 0; j < 4; ++j) {
+							const float a = acc[t][u][4 * gq + j];
+							const float lb =
+							    FOLD ? a
+							         : lower_bound<METRIC>(a,
+							                               j == 0   ? make_float4(al.x, xn.x, ux.x, sc.x)
+							                               : j == 1 ? make_float4(al.y, xn.y, ux.y, sc.y)
+							                               : j == 2 ? make_float4(al.z, xn.z, ux.z, sc.z)
+							                                        : make_float4(al.w, xn.w, ux.w, sc.w),
+							                               qa);
+							if (lb < mv) mv = lb, mr = r0 + j;
+						}
+					}
+				const float ov = __shfl_xor(mv, 32, 64);
+				const int orr = __shfl_xor(mr, 32, 64);
+				if (ov < mv) mv = ov, mr = orr;
+				const int ql = qlb + 32 * u;
+				if (eln < 32 && q0 + ql < nq && mv < F_INF) {
+					const unsigned p = atomicAdd(&CNT[ql], 1u);
+					if (p < (unsigned)seg_cap)
+						seg_pool[((int64_t)blockIdx.x * nq + q0 + ql) * seg_cap + p] =
+						    make_uint2(fkey(mv), (uint32_t)(row0 + mr));
+				}
 			}
 		} else {
 			// tau = +inf (fewer live sample rows than needed) must still drop
@@ -954,20 +1001,20 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 	}
 #if LHIP_PROF
 	if (lane == 0) {
-		atomicAdd(&lhip_prof[MODE * 8 + 0], (unsigned long long)pw);
-		atomicAdd(&lhip_prof[MODE * 8 + 1], (unsigned long long)pb);
-		atomicAdd(&lhip_prof[MODE * 8 + 2], (unsigned long long)pc);
-		atomicAdd(&lhip_prof[MODE * 8 + 3], (unsigned long long)pe);
-		atomicAdd(&lhip_prof[MODE * 8 + 4], 1ull);
-		atomicAdd(&lhip_prof[MODE * 8 + 5], (unsigned long long)G);
-		atomicAdd(&lhip_prof[MODE * 8 + 6], (unsigned long long)cur_t);
-		atomicAdd(&lhip_prof[16 + MODE * 2 + 0], (unsigned long long)prof_surv);
-		atomicAdd(&lhip_prof[16 + MODE * 2 + 1], (unsigned long long)prof_over);
-		atomicAdd(&lhip_prof[20 + MODE * 2 + 0], (unsigned long long)prof_slow);
-		atomicAdd(&lhip_prof[20 + MODE * 2 + 1], (unsigned long long)prof_slown);
+		atomicAdd(&lhip_prof[(MODE == 1) * 8 + 0], (unsigned long long)pw);
+		atomicAdd(&lhip_prof[(MODE == 1) * 8 + 1], (unsigned long long)pb);
+		atomicAdd(&lhip_prof[(MODE == 1) * 8 + 2], (unsigned long long)pc);
+		atomicAdd(&lhip_prof[(MODE == 1) * 8 + 3], (unsigned long long)pe);
+		atomicAdd(&lhip_prof[(MODE == 1) * 8 + 4], 1ull);
+		atomicAdd(&lhip_prof[(MODE == 1) * 8 + 5], (unsigned long long)G);
+		atomicAdd(&lhip_prof[(MODE == 1) * 8 + 6], (unsigned long long)cur_t);
+		atomicAdd(&lhip_prof[16 + (MODE == 1) * 2 + 0], (unsigned long long)prof_surv);
+		atomicAdd(&lhip_prof[16 + (MODE == 1) * 2 + 1], (unsigned long long)prof_over);
+		atomicAdd(&lhip_prof[20 + (MODE == 1) * 2 + 0], (unsigned long long)prof_slow);
+		atomicAdd(&lhip_prof[20 + (MODE == 1) * 2 + 1], (unsigned long long)prof_slown);
 	}
 #endif
-	if (MODE == 1) {
+	if (MODE >= 1) {
 		if (n_list > 0) write_list(cur_t - 1);  // the last tile's survivors
 		__syncthreads();                         // every wave's counter updates
 		if (tid < BQ && q0 + tid < nq) seg_cnt[(int64_t)blockIdx.x * nq + q0 + tid] = (int)CNT[tid];
@@ -1028,6 +1075,13 @@ void launch_scan_dense(const StoreView &s, const QueryView &q, int64_t n_tiles, 
                        int64_t ld_out, hipStream_t st) {
 	if (n_tiles <= 0) return;
 	scan_dispatch<0>(s, q, n_tiles, tile_stride, out, ld_out, nullptr, nullptr, nullptr, 0, st);
+}
+
+void launch_scan_tilemin(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, uint2 *seg_pool,
+                         int *seg_cnt, int seg_cap, hipStream_t st) {
+	if (n_tiles <= 0) return;
+	if (seg_cap <= 0 || seg_cap > 1024) throw std::runtime_error("scan: segment capacity must be in [1, 1024]");
+	scan_dispatch<2>(s, q, n_tiles, tile_stride, nullptr, 0, nullptr, seg_pool, seg_cnt, seg_cap, st);
 }
 
 void launch_scan_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
@@ -1192,7 +1246,7 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const f
 			}
 		}
 	}
-	const float ftau = dense ? F_INF : tau[q];
+	const float ftau = (dense || !tau) ? F_INF : tau[q];
 	auto slot_at = [&](int64_t i) -> uint32_t {
 		if (dense) return (uint32_t)((i / BR) * src.tile_stride * BR + (i % BR));
 		return s_slots[i];

@@ -537,7 +537,9 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	launch_prep_queries(dQ, nq, dim, ld, nq_pad, eff_metric, ma, mu, ws.Qf.p, ws.Qb.p, ws.qaux.p, stream);
 	QueryView qv{ws.Qf.p, ws.Qb.p, ws.qaux.p, nq, nq_pad};
 
-	const int Mfinal = std::min(MAX_CAND, std::max(k * std::max(refine, 1), k + 32));
+	// refined candidates: k + max(32, k) — past k the bound slack (bf16 query
+	// rounding) spans more ranks as the neighbour distances crowd (C3: k = 100)
+	const int Mfinal = std::min(MAX_CAND, std::max(k * std::max(refine, 1), k + std::max(32, k)));
 	const int64_t n_tiles = (n_slots + SCAN_BR - 1) / SCAN_BR;
 	const bool fast_ok = (k + 8 <= MAX_CAND) && n_live > 0;
 	bool all_fallback = !fast_ok;
@@ -560,18 +562,22 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 			kt_dense_n += 1;
 		}
 	} else if (fast_ok) {
-		// 1) sample pass: dense LB over every stride-th tile -> tau[q]
-		// ~1/sample_div of the tiles, at least 32, at most one tile per CU
-		// (the dense LB matrix and its select grow with the sample)
+		// 1) sample pass over every stride-th tile (~1/sample_div of them, at
+		//    least 32 and (k+8)/2): per tile, query and 64-row quarter the row
+		//    of smallest bound -> top-(k+8) of those by bound -> exact
+		//    distances -> tau[q] = the k-th smallest (an upper bound on the
+		//    k-th nearest distance: k real rows lie within it)
 		const int64_t n_sample = std::min<int64_t>(
-		    n_tiles, std::max<int64_t>(std::min<int64_t>((n_tiles + sample_div - 1) / sample_div, scan_grid(1 << 30)),
-		                               32));
+		    n_tiles, std::max<int64_t>({(n_tiles + sample_div - 1) / sample_div, 32, (k + 9) / 2}));
 		const int64_t stride = std::max<int64_t>(1, n_tiles / n_sample);
-		const int64_t cols = n_sample * SCAN_BR;
 		const int Ms = k + 8;
-		ws.dense.need((size_t)nq * cols);
-		launch_scan_dense(sv, qv, n_sample, stride, ws.dense.p, cols, stream);
-		launch_select_dense(ws.dense.p, cols, cols, stride, nq, Ms, ws.cand_slot.p, d_cand_cnt, ws.cut.p, stream);
+		const int n_seg_s = scan_grid(n_sample);
+		const int cap_s = (int)round_up(4 * ((n_sample + n_seg_s - 1) / n_seg_s), 4);
+		ws.seg_pool.need((size_t)n_seg_s * nq * cap_s);
+		ws.seg_cnt.need((size_t)n_seg_s * nq);
+		launch_scan_tilemin(sv, qv, n_sample, stride, ws.seg_pool.p, ws.seg_cnt.p, cap_s, stream);
+		launch_select_segments(ws.seg_pool.p, ws.seg_cnt.p, cap_s, n_seg_s, nullptr, nq, Ms, ws.cand_slot.p,
+		                       d_cand_cnt, ws.cut.p, nullptr, stream);
 		launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Ms, ws.cand_dist.p, stream);
 		launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Ms, k, 0, k, ws.tau.p,
 		                nullptr, nullptr, nullptr, nullptr, stream);

@@ -15,19 +15,28 @@ for v in "$@"; do
 	case $v in
 	NO_EPILOGUE) build NO_EPILOGUE -DLHIP_ABL_NO_EPILOGUE=1 ;;
 	NO_MFMA) build NO_MFMA -DLHIP_ABL_NO_MFMA=1 ;;
-	NO_Q) build NO_Q -DLHIP_ABL_NO_Q=1 ;;
-	DMA_ONLY) build DMA_ONLY -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_EPILOGUE=1 ;;
-	NT0) build NT0 -DLHIP_X_NT=0 ;;
+	
+	
+	
 	PROF) build PROF -DLHIP_PROF=1 ;;
 	NOSLOW) build NOSLOW -DLHIP_ABL_NO_SLOW=1 ;;
 	NOREADS) build NOREADS -DLHIP_ABL_NO_READS=1 ;;
 	NOMFMA_NOREADS) build NOMFMA_NOREADS -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 ;;
 	NOMFMA_NOREADS_NOEPI) build NOMFMA_NOREADS_NOEPI -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 -DLHIP_ABL_NO_EPILOGUE=1 ;;
 	NOFLUSH) build NOFLUSH -DLHIP_ABL_NO_FLUSH=1 ;;
-	PROFER0) build PROFER0 -DLHIP_PROF=1 -DLHIP_EARLY_REFILL=0 ;;
-	ER1) build ER1 -DLHIP_EARLY_REFILL=1 ;;
-	ER0) build ER0 -DLHIP_EARLY_REFILL=0 ;;
-	RF0) build RF0 -DLHIP_READS_FIRST=0 ;;
+	SKEL) build SKEL -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 -DLHIP_ABL_NO_EPILOGUE=1 ;;
+	SKEL_NOQ) build SKEL_NOQ -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 -DLHIP_ABL_NO_EPILOGUE=1 -DLHIP_ABL_NO_QDMA=1 ;;
+	SKEL_NOQ_NT0) build SKEL_NOQ_NT0 -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 -DLHIP_ABL_NO_EPILOGUE=1 -DLHIP_ABL_NO_QDMA=1 -DLHIP_X_NT=0 ;;
+	NOQ) build NOQ -DLHIP_ABL_NO_QDMA=1 -DLHIP_ABL_NO_SLOW=1 ;;
+	SKEL_NT0) build SKEL_NT0 -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 -DLHIP_ABL_NO_EPILOGUE=1 -DLHIP_X_NT=0 ;;
+	NT0) build NT0 -DLHIP_X_NT=0 ;;
+	NST3) build NST3 -DLHIP_NST_BF16=3 ;;
+	NST2) build NST2 -DLHIP_NST_BF16=2 ;;
+	NOQ_NT0) build NOQ_NT0 -DLHIP_ABL_NO_QDMA=1 -DLHIP_ABL_NO_SLOW=1 -DLHIP_X_NT=0 ;;
+	
+	
+	
+	
 	PREV) # the committed (HEAD) kernel file, for same-box A/B timing
 		git show HEAD:$D/csrc/knn_kernels.hip > abl/prev_kernels.hip
 		hipcc $F -I$D/csrc -c abl/prev_kernels.hip -o abl/k_PREV.o
