@@ -66,8 +66,9 @@ void launch_fill_rowaux(float4 *rowaux, int64_t from, int64_t to, hipStream_t st
 void launch_tombstone(float4 *rowaux, const int64_t *slots, int n, hipStream_t st);
 
 // ---- search ------------------------------------------------------------------
+// Also zeroes zero3[0 .. 3*nq) when non-null (the search's status words).
 void launch_prep_queries(const float *Q, int nq, int dim, int ld, int nq_pad, int metric, float max_alpha,
-                         float max_ux, float *Qf, uint16_t *Qb, float4 *qaux, hipStream_t st);
+                         float max_ux, float *Qf, uint16_t *Qb, float4 *qaux, int *zero3, hipStream_t st);
 
 // Dense lower-bound scan over row tiles t*tile_stride, t < n_tiles:
 // out[q][t*BR + r] = LB(q, slot) (+inf for tombstones / rows past n_slots).
@@ -77,7 +78,8 @@ void launch_scan_dense(const StoreView &s, const QueryView &q, int64_t n_tiles, 
 // Threshold scan over all rows (persistent: scan_grid(n_tiles) workgroups):
 // workgroup g appends (orderedkey(LB), slot) for LB <= tau[q] into its own
 // segment seg_pool[(g*nq + q)*seg_cap ..], count in seg_cnt[g*nq + q] (may
-// exceed seg_cap: overflow is reported by select).
+// exceed seg_cap: overflow is reported by select).  seg_pool holds scan_grid(n_tiles) *
+// (nq_pad / SCAN_BQ) more entries past the segments: per-workgroup sink words.
 void launch_scan_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
                         int seg_cap, hipStream_t st);
 

@@ -188,10 +188,11 @@ void launch_tombstone(float4 *rowaux, const int64_t *slots, int n, hipStream_t s
 __global__ __launch_bounds__(256) void prep_queries_kernel(const float *__restrict__ Q, int nq, int dim, int ld,
                                                            int metric, float max_alpha, float max_ux,
                                                            float *__restrict__ Qf, uint16_t *__restrict__ Qb,
-                                                           float4 *__restrict__ qaux) {
+                                                           float4 *__restrict__ qaux, int *__restrict__ zero3) {
 	__shared__ double red[2][4];
 	const int q = blockIdx.x;
 	const int t = threadIdx.x;
+	if (zero3 && t < 3 && q < nq) zero3[t * nq + q] = 0;  // the search's status words
 	double s2 = 0.0, e2 = 0.0;
 	for (int i = t; i < ld; i += 256) {
 		float v = (q < nq && i < dim) ? Q[(int64_t)q * dim + i] : 0.0f;
@@ -249,24 +250,11 @@ __global__ __launch_bounds__(256) void prep_queries_kernel(const float *__restri
 }
 
 void launch_prep_queries(const float *Q, int nq, int dim, int ld, int nq_pad, int metric, float max_alpha,
-                         float max_ux, float *Qf, uint16_t *Qb, float4 *qaux, hipStream_t st) {
+                         float max_ux, float *Qf, uint16_t *Qb, float4 *qaux, int *zero3, hipStream_t st) {
 	prep_queries_kernel<<<dim3(nq_pad), dim3(256), 0, st>>>(Q, nq, dim, ld, metric, max_alpha, max_ux, Qf, Qb,
-	                                                           qaux);
+	                                                           qaux, zero3);
 }
 
-// ---------------------------------------------------------------------------
-// scan: bf16 MFMA lower-bound tiles
-//
-// Workgroup = 512 threads = 8 waves laid out 2 (base rows) x 4 (queries); each
-// wave owns a 64-row x 64-query sub-tile = 2x2 v_mfma_f32_32x32x16_bf16 tiles
-// (A = base rows, B = queries, so the accumulator column = lane&31 = query and
-// the 16 registers walk base rows).  Per 64-deep k-step the workgroup streams
-// a 128 x 64 f32 base tile from HBM (two 16 B loads per thread, converted to
-// bf16 in registers) and a 256 x 64 bf16 query tile from L2 into an
-// XOR-swizzled LDS image (16 B chunk c of row r stored at c ^ ((r>>1)&7), which
-// makes the ds_read_b128 fragment loads of 32 consecutive rows conflict-free).
-// Global loads of step k+1 are issued before the MFMAs of step k.
-// ---------------------------------------------------------------------------
 constexpr int BR = SCAN_BR, BQ = SCAN_BQ;
 
 // ---------------------------------------------------------------------------
@@ -317,6 +305,24 @@ constexpr int BR = SCAN_BR, BQ = SCAN_BQ;
 #ifndef LHIP_ABL_NO_SLOW
 #define LHIP_ABL_NO_SLOW 0  // survivors are tested but not written
 #endif
+#ifndef LHIP_ABL_SLOW_NEVER
+#define LHIP_ABL_SLOW_NEVER 0  // survivor path compiled in, never taken (runtime-false guard)
+#endif
+#ifndef LHIP_SLOW_UNROLL
+#define LHIP_SLOW_UNROLL 0  // survivor path: 16 unrolled uniform branches instead of mask loop + switch
+#endif
+#ifndef LHIP_ABL_DRAIN_EPI
+#define LHIP_ABL_DRAIN_EPI 0  // drain the DMA in flight before each epilogue
+#endif
+#ifndef LHIP_ABL_NO_LISTWRITE
+#define LHIP_ABL_NO_LISTWRITE 0  // survivor path runs, its LDS list writes do not
+#endif
+#ifndef LHIP_DEFER_LIST
+#define LHIP_DEFER_LIST 0  // measured slower (C2 0.49-0.50 vs 0.47 ms): survivor list writes at the next wait point
+#endif
+#ifndef LHIP_SLOW_VALU
+#define LHIP_SLOW_VALU 1  // survivor path: per-lane first hit by vector selects, one ballot + mbcnt
+#endif
 #ifndef LHIP_ABL_NO_FLUSH
 #define LHIP_ABL_NO_FLUSH 0  // survivor lists are not written out
 #endif
@@ -343,45 +349,56 @@ extern "C" int lhip_prof_read(unsigned long long *out, int reset) {
 #ifndef LHIP_X_NT
 #define LHIP_X_NT 0  // nt on the base stream: measured slower (bf16 scan 0.59 vs 0.525 ms)
 #endif
-#ifndef LHIP_NST_BF16
-#define LHIP_NST_BF16 3  // 3 measured faster than 4 (0.495 vs 0.511 ms) and 2 (0.552)
+#ifndef LHIP_SK_BF16
+#define LHIP_SK_BF16 64  // k per stage with a bf16 base: 64 (2 slots) or 32 (3 slots)
 #endif
 
 constexpr int SCAN_THREADS = 512;
 constexpr int SCAN_WAVES = SCAN_THREADS / 64;          // 8: 2 per SIMD, 256 registers each
-constexpr int SK = 32;
-constexpr int QST_BYTES = BQ * SK * 2;                 // 16 KiB
 constexpr int RA_SLOT = BR * 16;                       // 4 KiB
 constexpr int RA_BYTES = 2 * RA_SLOT;
 constexpr int CNT_BYTES = BQ * 4;
 constexpr int QA_BYTES = BQ * 16 + BQ * 4;             // per-query bound constants + tau
-constexpr int WLIST = 32;                              // survivor list entries (8 B) per wave and tile
-constexpr int LIST_BYTES = SCAN_WAVES * WLIST * 8;
-constexpr int Q_DMA_PER_WAVE = QST_BYTES / 1024 / SCAN_WAVES;  // 2
-static_assert(Q_DMA_PER_WAVE * SCAN_WAVES * 1024 == QST_BYTES, "Q stage = whole DMA instructions");
 static_assert(RA_SLOT / 1024 == 4 && SCAN_WAVES >= 4, "row aux: one DMA instruction on waves 0..3");
-static_assert(SCAN_WAVES == 8 && WLIST <= 64, "one list of WLIST entries per wave; a flush is one instruction");
+static_assert(SCAN_WAVES == 8, "8 waves: 4 row quarters x 2 query halves");
 
-// per base element type: f32 store (XB = false) or bf16 store (XB = true)
+// per base element type: f32 store (XB = false) or bf16 store / scan copy (XB = true)
 template <bool XB>
 struct ScanCfg {
+	static constexpr int SK = XB ? LHIP_SK_BF16 : 32;          // k per stage
+	static constexpr int KQ = SK / 16;                         // MFMA k-steps per stage: 4 / 2
 	static constexpr int XE = XB ? 2 : 4;                      // bytes per base element
-	static constexpr int XROW = SK * XE;                       // bytes per row and stage: 64 / 128
-	static constexpr int XCH = XROW / 16;                      // 16 B chunks per row: 4 / 8
-	static constexpr int XST = BR * XROW;                      // 16 / 32 KiB
-	static constexpr int NST = XB ? LHIP_NST_BF16 : 3;         // ring slots
-	static constexpr int STAGE = XST + QST_BYTES;
+	static constexpr int XROW = SK * XE;                       // bytes per row and stage: 128
+	static constexpr int XCH = XROW / 16;                      // 16 B chunks per row
+	static constexpr int XST = BR * XROW;                      // 32 KiB
+	static constexpr int QROW = SK * 2;                        // bytes per query and stage: 128 / 64
+	static constexpr int QCH = QROW / 16;
+	static constexpr int QST = BQ * QROW;                      // 32 / 16 KiB
+	static constexpr int NST = XB ? (SK == 64 ? 2 : 3) : 3;    // ring slots
+	static constexpr int STAGE = XST + QST;
 	static constexpr int RING = NST * STAGE;                   // 128 / 144 KiB
-	static constexpr int XDMA = XST / 1024 / SCAN_WAVES;       // X DMA instructions per wave and stage: 2 / 4
-	static constexpr int ROWS_PER_DMA = 1024 / XROW;           // 16 / 8
-	static constexpr int DMA = XDMA + (LHIP_ABL_NO_QDMA ? 0 : Q_DMA_PER_WAVE);  // + 1 row aux on waves 0..3 at a tile's stage 0
+	static constexpr int XDMA = XST / 1024 / SCAN_WAVES;       // X DMA instructions per wave and stage
+	static constexpr int QDMA = QST / 1024 / SCAN_WAVES;       // Q DMA instructions per wave and stage
+	static constexpr int ROWS_PER_DMA = 1024 / XROW;
+	static constexpr int QROWS_PER_DMA = 1024 / QROW;
+	static constexpr int DMA = XDMA + (LHIP_ABL_NO_QDMA ? 0 : QDMA);  // + 1 row aux on waves 0..3 at a tile's stage 0
+	// survivor list per wave (8 B entries): f32 32, flushed after every tile by
+	// one counted store; bf16 256, kept across tiles and flushed (drained)
+	// only past FLUSH_AT entries, or at the end
+	static constexpr int WLIST = XB ? 256 : 32;
+	static constexpr int FLUSH_AT = XB ? WLIST - 64 : 0;
+	static constexpr int LIST_BYTES = SCAN_WAVES * WLIST * 8;
 	static constexpr int LDS = RING + RA_BYTES + CNT_BYTES + QA_BYTES + LIST_BYTES;
 	static_assert(LDS <= 160 * 1024, "LDS budget");
-	static_assert(XDMA * SCAN_WAVES * 1024 == XST, "X stage = whole DMA instructions");
-	// 16 B chunk c of row r lives at physical chunk xswz(r, c) (an involution)
-	__device__ static __forceinline__ int xswz(int r, int c) { return XB ? c ^ ((r >> 2) & 3) : c ^ ((r >> 1) & 7); }
+	static_assert(XDMA * SCAN_WAVES * 1024 == XST && QDMA * SCAN_WAVES * 1024 == QST, "stages = whole DMA instructions");
+	static_assert(XROW == 128 && (QROW == 128 || QROW == 64), "swizzles below");
+	static_assert(XB || SK == 32, "f32 fragments: 2 k-steps per stage");
+	static_assert(KQ % 2 == 0, "k-step fragments alternate between two register sets");
+	// 16 B chunk c of row r lives at physical chunk xswz(r, c) (an involution):
+	// conflict-free ds_read_b128 fragment reads on 128 B (64 B) rows
+	__device__ static __forceinline__ int xswz(int r, int c) { return c ^ ((r >> 1) & 7); }
+	__device__ static __forceinline__ int qswz(int r, int c) { return QROW == 128 ? c ^ ((r >> 1) & 7) : c ^ ((r >> 2) & 3); }
 };
-__device__ __forceinline__ int qswz(int r, int c) { return c ^ ((r >> 2) & 3); }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -481,7 +498,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 	const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR math
 	const int wr = w & 3, wq = w >> 2;                      // 64-row quarter, 128-query half
 	const int q0 = blockIdx.y * BQ;
-	const int S = ld / SK;  // >= 2 (ld is a multiple of 64)
+	const int S = ld / C::SK;  // >= 1 (ld is a multiple of 64)
 	const int my_tiles = (n_tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
 	const int G = my_tiles * S;
 
@@ -503,16 +520,16 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 	// next stage to issue and its LDS slot — run in SGPRs and advance by
 	// constants, so a stage's issue costs a handful of scalar instructions.
 	const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
-	uint32_t xoff[C::XDMA], qoff[Q_DMA_PER_WAVE];
+	uint32_t xoff[C::XDMA], qoff[C::QDMA];
 #pragma unroll
 	for (int j = 0; j < C::XDMA; ++j) {
 		const int xr = (C::XDMA * w + j) * C::ROWS_PER_DMA + lane / C::XCH;
 		xoff[j] = (uint32_t)(xr * ld * C::XE + (C::xswz(xr, lane % C::XCH) << 4));
 	}
 #pragma unroll
-	for (int j = 0; j < Q_DMA_PER_WAVE; ++j) {
-		const int qr = (Q_DMA_PER_WAVE * w + j) * 16 + (lane >> 2);
-		qoff[j] = (uint32_t)(qr * ld + (qswz(qr, lane & 3) << 3)) * 2u;
+	for (int j = 0; j < C::QDMA; ++j) {
+		const int qr = (C::QDMA * w + j) * C::QROWS_PER_DMA + lane / C::QCH;
+		qoff[j] = (uint32_t)(qr * ld + (C::qswz(qr, lane % C::QCH) << 3)) * 2u;
 	}
 	const uint32_t raoff = (uint32_t)lane * 16u;
 	const int64_t tile_rows_step = (int64_t)gridDim.x * tile_stride * BR;  // rows between this workgroup's tiles
@@ -530,8 +547,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 		for (int j = 0; j < C::XDMA; ++j)
 			dma16s<LHIP_X_NT>(iss_xt, xoff[j], iss_lds + (uint32_t)(C::XDMA * w + j) * 1024u);
 #pragma unroll
-		for (int j = 0; j < (LHIP_ABL_NO_QDMA ? 0 : Q_DMA_PER_WAVE); ++j)
-			dma16s(iss_q, qoff[j], iss_lds + (uint32_t)C::XST + (uint32_t)(Q_DMA_PER_WAVE * w + j) * 1024u);
+		for (int j = 0; j < (LHIP_ABL_NO_QDMA ? 0 : C::QDMA); ++j)
+			dma16s(iss_q, qoff[j], iss_lds + (uint32_t)C::XST + (uint32_t)(C::QDMA * w + j) * 1024u);
 		++iss_g;
 		iss_lds = iss_lds + C::STAGE == lds0 + C::RING ? lds0 : iss_lds + C::STAGE;
 		if (++iss_s == S) {
@@ -542,8 +559,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 			iss_ra += tile_rows_step;
 			iss_q = qbase;
 		} else {
-			iss_xt += SK * C::XE;
-			iss_q += SK;
+			iss_xt += C::SK * C::XE;
+			iss_q += C::SK;
 		}
 	};
 
@@ -603,75 +620,103 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 	// m = iss_g-1-h stages issued after it may stay in flight — DMA each, +1 on
 	// waves 0..3 for each of them that is a tile's stage 0 (sh = in-tile index
 	// of stage h).  The steady-state counts are immediates.
+	// List flush stores: fpos1/fpos2 = iss_g when the latest two were issued
+	// (a store is younger than stage h iff its fpos > h).
+	int fpos1 = -1, fpos2 = -1;
+	auto fl_younger = [&](int h) { return (fpos1 > h ? 1 : 0) + (fpos2 > h ? 1 : 0); };
 	auto wait_stage = [&](int h, int sh) {
 		const int m = iss_g - 1 - h;
 		if (m <= 0) {
-			LHIP_WAIT_VM(0);
+			wait_vm(fl_younger(h));
 			return;
 		}
 		const int d0 = S - 1 - sh;  // stages after h up to the next tile start, exclusive
 		const int n0 = ra_wave ? (d0 < m) + (d0 + S < m) : 0;
-		wait_vm(m * C::DMA + n0);
+		wait_vm(m * C::DMA + n0 + fl_younger(h));
 	};
 
-	// This wave's survivor list: n_list entries (wave-uniform) of the tile
-	// finished last.  Entry = (key, query << 18 | tile row << 10).  Written
-	// out with segment positions from the per-query LDS counters: one
-	// ds_add_rtn for the whole list.
-	uint2 *wlist = LIST + w * WLIST;
+	// This wave's survivor list: n_list entries (wave-uniform), possibly of
+	// several tiles.  Entry = (raw LB bits, query << 24 | tile row << 16 |
+	// tile iteration).  Written out with segment positions from the per-query
+	// LDS counters.  A list of <= 64 entries goes out as exactly ONE
+	// global_store_dwordx2 of all 64 lanes (lanes without an entry, or past
+	// the segment capacity, write the workgroup's sink word past the
+	// segments), which the DMA waits count (issued after the stage's DMA, it
+	// never has to complete before a stage can be read); a longer list is
+	// written by plain stores and drained.
+	uint2 *wlist = LIST + w * C::WLIST;
 	int n_list = 0;
-	auto write_list = [&](int ti_prev) {
+	uint2 *const sink = seg_pool + (int64_t)gridDim.x * nq * seg_cap + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+	auto entry_out = [&](uint2 e, uint2 *&dst, uint2 &val) {
+		const int qloc = (int)(e.y >> 24), rloc = (int)((e.y >> 16) & 255u), ti = (int)(e.y & 0xFFFFu);
+		const unsigned p = atomicAdd(&CNT[qloc], 1u);
+		if (p < (unsigned)seg_cap) {
+			const int64_t prow0 = ((int64_t)blockIdx.x + (int64_t)ti * gridDim.x) * tile_stride * BR;
+			dst = seg_pool + ((int64_t)blockIdx.x * nq + q0 + qloc) * seg_cap + p;
+			val = make_uint2(fkey(__uint_as_float(e.x)), (uint32_t)(prow0 + rloc));
+		}
+	};
+	auto write_list_one = [&]() {  // n_list <= 64
 		const int ln = lane_id_fresh();
-		if (ln < n_list) {
-			const uint2 e = wlist[ln];
-			const int qloc = (int)(e.y >> 18), rloc = (int)((e.y >> 10) & 255u);
-			const unsigned p = atomicAdd(&CNT[qloc], 1u);
-			if (p < (unsigned)seg_cap) {
-				const int64_t prow0 = ((int64_t)blockIdx.x + (int64_t)ti_prev * gridDim.x) * tile_stride * BR;
-				seg_pool[((int64_t)blockIdx.x * nq + q0 + qloc) * seg_cap + p] =
-				    make_uint2(fkey(__uint_as_float(e.x)), (uint32_t)(prow0 + rloc));
+		uint2 *dst = sink;
+		uint2 val = make_uint2(0u, 0u);
+		if (ln < n_list) entry_out(wlist[ln], dst, val);
+		const uint64_t v64 = (uint64_t)val.x | ((uint64_t)val.y << 32);
+		asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(dst), "v"(v64) : "memory");
+		n_list = 0;
+	};
+	auto write_list_all = [&]() {
+		const int ln = lane_id_fresh();
+		for (int b = 0; b < n_list; b += 64) {
+			if (b + ln < n_list) {
+				uint2 *dst = nullptr;
+				uint2 val;
+				entry_out(wlist[b + ln], dst, val);
+				if (dst) *dst = val;
 			}
 		}
 		n_list = 0;
 	};
 	// a bound whose survivors do not fit the wave's list: straight to the
 	// segment (position from the LDS counter); out of line, rare
+	// per-lane form: each active lane its own (bound, query, row)
+	auto overflow_lane = [&](bool act, float lb, int qv, int rr, int64_t row0) {
+		if (act) {
+			const unsigned p = atomicAdd(&CNT[qv], 1u);
+			if (p < (unsigned)seg_cap)
+				seg_pool[((int64_t)blockIdx.x * nq + q0 + qv) * seg_cap + p] = make_uint2(fkey(lb), (uint32_t)(row0 + rr));
+		}
+		LHIP_WAIT_VM(0);
+	};
+	// (its store is not counted by the DMA waits: drained right away)
 	auto overflow = [&](uint64_t mm, float lb, int qv, int rr, int64_t row0) {
 		if ((mm >> lane_id_fresh()) & 1ull) {
 			const unsigned p = atomicAdd(&CNT[qv], 1u);
 			if (p < (unsigned)seg_cap)
 				seg_pool[((int64_t)blockIdx.x * nq + q0 + qv) * seg_cap + p] = make_uint2(fkey(lb), (uint32_t)(row0 + rr));
 		}
+		LHIP_WAIT_VM(0);
 	};
-	// Fragments of one 16-deep k-half of a stage: A raw (f32: two 16 B reads
-	// per fragment, converted at use; bf16: one), B bf16.  F0 holds (g, kk0)
-	// and F1 (g, kk1); each half's MFMAs run while the other half loads.
+	// Fragments of one 16-deep k-step of a stage: A raw (f32: two 16 B reads
+	// per fragment, converted at use; bf16: one), B bf16.  Two sets alternate:
+	// k-step j's MFMAs run while k-step j+1 loads.
 	struct Frag {
 		float4 a[2][2];  // [t][lo/hi] raw 16 B reads (bf16: [t][0] only)
 		bf16x8 b[4];
 	};
-	// per-lane fragment byte offsets inside a stage (loop-invariant VGPRs)
-	uint32_t aoff[2][2][2], boff[2][4];
-#pragma unroll
-	for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-		for (int t = 0; t < 2; ++t) {
-			const int r = wr * 64 + 32 * t + (lane & 31), hh = lane >> 5;
-			if (XB) {
-				aoff[kk][t][0] = aoff[kk][t][1] = (uint32_t)(r * C::XROW + (C::xswz(r, 2 * kk + hh) << 4));
-			} else {
-				const int c = 4 * kk + 2 * hh;
-				aoff[kk][t][0] = (uint32_t)(r * C::XROW + (C::xswz(r, c) << 4));
-				aoff[kk][t][1] = (uint32_t)(r * C::XROW + (C::xswz(r, c + 1) << 4));
-			}
-		}
-#pragma unroll
-		for (int u = 0; u < 4; ++u) {
-			const int q = wq * 128 + 32 * u + (lane & 31);
-			boff[kk][u] = (uint32_t)(C::XST + q * 64 + (qswz(q, 2 * kk + (lane >> 5)) << 4));
-		}
+	// Per-lane fragment byte offsets inside a stage.  Row r's chunk c sits at
+	// physical chunk c ^ f(r) and f is the same for r and r + 32, so every
+	// fragment of k-step kq is one base XOR (kq << 5) (f32: two chunks per
+	// fragment, kq << 6, the second chunk ^ 16) plus an immediate per 32-row
+	// (32-query) block.
+	uint32_t abase, bbase;
+	{
+		const int r = wr * 64 + (lane & 31), hh = lane >> 5;
+		abase = (uint32_t)(r * C::XROW + (C::xswz(r, XB ? hh : 2 * hh) << 4));
+		const int q = wq * 128 + (lane & 31);
+		bbase = (uint32_t)(C::XST + q * C::QROW + (C::qswz(q, hh) << 4));
 	}
-	auto read_half = [&](Frag &f, const uint8_t *st_base, int kk) {
+	auto read_k = [&](Frag &f, const uint8_t *st_base, int kq) {
 		if (LHIP_ABL_NO_READS) {
 			float4 z;
 			bf16x8 zb;
@@ -683,17 +728,19 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 			for (int u = 0; u < 4; ++u) f.b[u] = zb;
 			return;
 		}
+		const uint32_t ao = abase ^ ((uint32_t)kq << (XB ? 5 : 6));
 #pragma unroll
 		for (int t = 0; t < 2; ++t) {
-			f.a[t][0] = *reinterpret_cast<const float4 *>(st_base + aoff[kk][t][0]);
-			if (!XB) f.a[t][1] = *reinterpret_cast<const float4 *>(st_base + aoff[kk][t][1]);
+			f.a[t][0] = *reinterpret_cast<const float4 *>(st_base + ao + t * 32 * C::XROW);
+			if (!XB) f.a[t][1] = *reinterpret_cast<const float4 *>(st_base + (ao ^ 16u) + t * 32 * C::XROW);
 		}
+		const uint32_t bo = bbase ^ ((uint32_t)kq << 5);
 #pragma unroll
-		for (int u = 0; u < 4; ++u) f.b[u] = *reinterpret_cast<const bf16x8 *>(st_base + boff[kk][u]);
+		for (int u = 0; u < 4; ++u) f.b[u] = *reinterpret_cast<const bf16x8 *>(st_base + bo + u * 32 * C::QROW);
 	};
-	auto mfma_half = [&](const Frag &f) {
+	auto mfma_rows = [&](const Frag &f, int t_lo, int t_hi) {
 #pragma unroll
-		for (int t = 0; t < 2; ++t) {
+		for (int t = t_lo; t < t_hi; ++t) {
 			bf16x8 av;
 			if (XB) {
 				av = __builtin_bit_cast(bf16x8, f.a[t][0]);
@@ -717,19 +764,38 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 			}
 		}
 	};
+	auto mfma_k = [&](const Frag &f) { mfma_rows(f, 0, 2); };
 
 	// prologue: stages 0 .. NST-1 in flight; (0, kk0) into registers
 	pump(C::NST - 1);
 	wait_stage(0, 0);
 	__builtin_amdgcn_s_barrier();
 	asm volatile("" ::: "memory");
-	Frag F0, F1;
-	read_half(F0, smem, 0);
+	Frag F[2];
+	read_k(F[0], smem, 0);
 
 #if LHIP_PROF
 	uint64_t pw = 0, pb = 0, pc = 0, pe = 0;
 	uint64_t prof_surv = 0, prof_over = 0, prof_slow = 0, prof_slown = 0;
 #endif
+	// Survivor entries of the last epilogue, written into the list at the next
+	// stage's wait point: an LDS write issued while this wave's own LDS-DMA is
+	// in flight holds its later LDS accesses until that DMA lands (measured:
+	// one stage of pipelining lost per tile), so the epilogue only reserves
+	// the positions (ppos, -1 = none) and keeps the entries in registers.
+	// (L2 / dot; cosine keeps its row terms live in the epilogue and writes at
+	// once: the 24 registers would spill)
+	constexpr bool DEFER = LHIP_DEFER_LIST && LHIP_SLOW_VALU && FOLD;
+	int ppos[8];
+	float psv[8];
+	uint32_t ppl[8];
+	bool pend = false;
+	auto write_pending = [&]() {
+#pragma unroll
+		for (int gi = 0; gi < 8; ++gi)
+			if (ppos[gi] >= 0) wlist[ppos[gi]] = make_uint2(__float_as_uint(psv[gi]), ppl[gi]);
+		pend = false;
+	};
 	int cur_t = 0, cur_s = 0;
 	const uint8_t *rd = smem;  // LDS slot of stage g
 	for (int g = 0; g < G; ++g) {
@@ -737,9 +803,12 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 		const bool tile_end = cur_s + 1 == S;
 		const uint8_t *rd_next = rd + C::STAGE == smem + C::RING ? smem : rd + C::STAGE;
 		if (cur_s == 0) init_acc(cur_t);
-		// (g, kk1) loads while (g, kk0) multiplies
-		read_half(F1, rd, 1);
-		mfma_half(F0);
+		// (g, kq+1) loads while (g, kq) multiplies
+#pragma unroll
+		for (int kq = 0; kq + 1 < C::KQ; ++kq) {
+			read_k(F[(kq + 1) & 1], rd, kq + 1);
+			mfma_k(F[kq & 1]);
+		}
 		// stage g+1 must have landed (the stages issued after it may stay in
 		// flight); this wave's reads of stage g are complete before the
 		// barrier, so after it slot g % NST is free for stage g+NST
@@ -748,32 +817,40 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 			// extra DMA on waves 0..3 if one of them is a tile's stage 0
 			static_assert(C::NST >= 2 && C::NST <= 4, "steady-state wait counts below");
 			const bool st0 = C::NST >= 3 && (cur_s + 2 == S || (C::NST == 4 && (cur_s + 3 == S || (S == 2 && cur_s == 1))));
-			if (ra_wave && st0)
-				wait_vm_c<(C::NST - 2) * C::DMA + 1>();
-			else
-				wait_vm_c<(C::NST - 2) * C::DMA>();
+			switch ((ra_wave && st0 ? 1 : 0) + fl_younger(g + 1)) {
+			case 0: wait_vm_c<(C::NST - 2) * C::DMA>(); break;
+			case 1: wait_vm_c<(C::NST - 2) * C::DMA + 1>(); break;
+			case 2: wait_vm_c<(C::NST - 2) * C::DMA + 2>(); break;
+			default: wait_vm_c<(C::NST - 2) * C::DMA + 3>(); break;
+			}
 		} else if (g + 1 < G) {
 			wait_stage(g + 1, tile_end ? 0 : cur_s + 1);  // the last stages, or a held-back issue
 		}
+		if (MODE == 1 && DEFER && pend) write_pending();
 		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 		PROF_T(t1);
 		__builtin_amdgcn_s_barrier();
 		asm volatile("" ::: "memory");
 		PROF_T(t2);
-		// write out the survivor list of the tile finished last iteration:
-		// these stores enter the vmcnt queue ahead of this iteration's DMA, so
-		// the next counted wait finds them a whole stage old
-		if (MODE == 1 && n_list > 0) {
-			if (LHIP_ABL_NO_FLUSH)
+		// stage g+NST into slot g % NST, then the survivor list of the tile
+		// finished last iteration (its store younger than that DMA: counted)
+		pump(g + C::NST);
+		if (MODE == 1 && n_list > C::FLUSH_AT) {
+			if (LHIP_ABL_NO_FLUSH) {
 				n_list = 0;
-			else
-				write_list(cur_t - 1);
+			} else if (C::FLUSH_AT + 1 <= 64 && n_list <= 64) {
+				write_list_one();
+				fpos2 = fpos1;
+				fpos1 = iss_g;
+			} else {
+				write_list_all();
+				LHIP_WAIT_VM(0);  // rare: uncounted stores, drained here
+			}
 		}
-		pump(g + C::NST);  // into slot g % NST
-		// (g+1, kk0) loads while (g, kk1) multiplies (unconditional: on the
+		// (g+1, 0) loads while (g, KQ-1) multiplies (unconditional: on the
 		// last stage it reads a stale, stable slot; the values are unused)
-		read_half(F0, rd_next, 0);
-		mfma_half(F1);
+		read_k(F[0], rd_next, 0);
+		mfma_k(F[1]);
 		rd = rd_next;
 		asm volatile("" ::: "memory");
 		PROF_T(t3);
@@ -789,6 +866,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 		cur_s = 0;
 		const int ti = cur_t++;
 
+		if (LHIP_ABL_DRAIN_EPI) LHIP_WAIT_VM(0);
 		// ---- epilogue of tile ti (its row aux landed with its stage 0) ------
 		const int64_t tile = (int64_t)blockIdx.x + (int64_t)ti * gridDim.x;
 		const int64_t row0 = tile * tile_stride * BR;
@@ -882,8 +960,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 			// ballot per bound; positions in the wave's list from mbcnt.  A
 			// list that fills (rare) sends further survivors straight to their
 			// segment.
-			int nl = 0;  // survivors of this tile so far (wave-uniform)
-			int nw = 0;  // of which in the list: entries [0, nw) are written
+			[[maybe_unused]] const int nl0 = n_list;
+#pragma unroll
+			for (int gi = 0; gi < 8 && DEFER; ++gi) ppos[gi] = -1;
+			int nl = n_list;  // list entries + survivors of this tile so far (wave-uniform)
+			int nw = n_list;  // of which in the list: entries [0, nw) are written
 #pragma unroll
 			for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -932,7 +1013,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 					const uint64_t any = __builtin_amdgcn_ballot_w64(scr <= 0.f);
 					if (LHIP_ABL_NO_SLOW) {
 						asm volatile("" ::"s"(any));  // masks computed, nothing written
-					} else if (any) {
+					} else if (any && (!LHIP_ABL_SLOW_NEVER || seg_cap == 0x7FFFFFF3)) {
 #if LHIP_PROF
 						const uint64_t ts0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -943,6 +1024,95 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 						// the bound: compact code (the epilogue must stay resident
 						// in the instruction cache; 16 unrolled copies per group
 						// would not).
+#if LHIP_SLOW_VALU
+						// Vector side: each lane's first hit among its 16 bounds
+						// (k = 4 * row j + query u) by selects; one ballot gives
+						// the list positions.  Lanes with a second hit (rare)
+						// take the per-bound path below for the others.
+						int c = 0, sk = 0;
+						float sv = 0.f;
+#pragma unroll
+						for (int k = 0; k < 16; ++k) {
+							const bool hit = l[k >> 2][k & 3] <= tq[k & 3];
+							const bool first = hit && c == 0;
+							sv = first ? l[k >> 2][k & 3] : sv;
+							sk = first ? k : sk;
+							c += hit ? 1 : 0;
+						}
+						{
+							const uint64_t b1 = __builtin_amdgcn_ballot_w64(c > 0);
+							const int n1 = __builtin_popcountll(b1);
+							const int qv = qlb + 32 * (sk & 3), rr = r0 + (sk >> 2);
+							if (nl + n1 <= C::WLIST) {
+								const int pos = nl + __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32),
+								                                               __builtin_amdgcn_mbcnt_lo((uint32_t)b1, 0u));
+								if (LHIP_ABL_NO_LISTWRITE) {
+									asm volatile("" ::"v"(pos), "v"(sv), "v"(qv), "v"(rr));  // list stays as it was
+								} else {
+									const uint32_t pl = ((uint32_t)qv << 24) | ((uint32_t)rr << 16) | ((uint32_t)ti & 0xFFFFu);
+									if (DEFER) {
+										ppos[4 * t + gq] = c > 0 ? pos : -1;  // written at the next wait point
+										psv[4 * t + gq] = sv;
+										ppl[4 * t + gq] = pl;
+										pend = true;
+									} else if (c > 0) {
+										wlist[pos] = make_uint2(__float_as_uint(sv), pl);
+									}
+									nw = nl + n1;
+								}
+							} else {
+								overflow_lane(c > 0, sv, qv, rr, row0);
+							}
+							nl += n1;
+						}
+						if (!LHIP_ABL_NO_LISTWRITE && __builtin_amdgcn_ballot_w64(c > 1)) {
+#pragma unroll
+							for (int k = 0; k < 16; ++k) {
+								const uint64_t mm =
+								    __builtin_amdgcn_ballot_w64(l[k >> 2][k & 3] <= tq[k & 3] && k != sk);
+								if (mm) {
+									const float lv = l[k >> 2][k & 3];
+									const int qv = qlb + 32 * (k & 3), rr = r0 + (k >> 2);
+									const int cntm = __builtin_popcountll(mm);
+									if (nl + cntm <= C::WLIST) {
+										const int pos =
+										    nl + __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32),
+										                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+										if ((mm >> eln) & 1ull)
+											wlist[pos] = make_uint2(__float_as_uint(lv), ((uint32_t)qv << 24) |
+											                                                 ((uint32_t)rr << 16) |
+											                                                 ((uint32_t)ti & 0xFFFFu));
+										nw = nl + cntm;
+									} else {
+										overflow(mm, lv, qv, rr, row0);
+									}
+									nl += cntm;
+								}
+							}
+						}
+#elif LHIP_SLOW_UNROLL
+#pragma unroll
+						for (int k = 0; k < 16; ++k) {
+							const uint64_t mm = __builtin_amdgcn_ballot_w64(l[k >> 2][k & 3] <= tq[k & 3]);
+							if (mm) {
+								const float lv = l[k >> 2][k & 3];
+								const int qv = qlb + 32 * (k & 3), rr = r0 + (k >> 2);
+								const int cntm = __builtin_popcountll(mm);
+								if (nl + cntm <= C::WLIST) {
+									const int pos = nl + __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32),
+									                                               __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+									if ((mm >> eln) & 1ull)
+										wlist[pos] = make_uint2(__float_as_uint(lv), ((uint32_t)qv << 24) |
+										                                                 ((uint32_t)rr << 16) |
+										                                                 ((uint32_t)ti & 0xFFFFu));
+									nw = nl + cntm;
+								} else {
+									overflow(mm, lv, qv, rr, row0);
+								}
+								nl += cntm;
+							}
+						}
+#else
 						uint64_t m[4][4];
 						uint32_t kmask = 0;
 #pragma unroll
@@ -968,17 +1138,19 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 							}
 							const int qv = qlb + 32 * (k & 3), rr = r0 + (k >> 2);
 							const int cntm = __builtin_popcountll(mm);
-							if (nl + cntm <= WLIST) {
+							if (nl + cntm <= C::WLIST) {
 								const int pos = nl + __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32),
 								                                               __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
 								if ((mm >> eln) & 1ull)
-									wlist[pos] = make_uint2(__float_as_uint(lv), ((uint32_t)qv << 18) | ((uint32_t)rr << 10));
+									wlist[pos] = make_uint2(__float_as_uint(lv),
+									                        ((uint32_t)qv << 24) | ((uint32_t)rr << 16) | ((uint32_t)ti & 0xFFFFu));
 								nw = nl + cntm;
 							} else {
 								overflow(mm, lv, qv, rr, row0);
 							}
 							nl += cntm;
 						}
+#endif
 #if LHIP_PROF
 						prof_slow += __builtin_amdgcn_s_memtime() - ts0;
 						++prof_slown;
@@ -988,8 +1160,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 				}
 			n_list = nw;
 #if LHIP_PROF
-			prof_surv += nl;
-			prof_over += nl > WLIST ? nl - WLIST : 0;
+			prof_surv += nl - nl0;
+			prof_over += nl > C::WLIST ? nl - C::WLIST : 0;
 #endif
 		}
 		tiles_done = cur_t;
@@ -1015,7 +1187,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 	}
 #endif
 	if (MODE >= 1) {
-		if (n_list > 0) write_list(cur_t - 1);  // the last tile's survivors
+		if (DEFER && pend) write_pending();
+		if (n_list > 0) write_list_all();  // what is left in the list
 		__syncthreads();                         // every wave's counter updates
 		if (tid < BQ && q0 + tid < nq) seg_cnt[(int64_t)blockIdx.x * nq + q0 + tid] = (int)CNT[tid];
 	}
@@ -1089,6 +1262,8 @@ void launch_scan_append(const StoreView &s, const QueryView &q, const float *tau
 	int64_t n_tiles = (s.n_slots + BR - 1) / BR;
 	if (n_tiles <= 0) return;
 	if (seg_cap <= 0 || seg_cap > 1024) throw std::runtime_error("scan: segment capacity must be in [1, 1024]");
+	if ((n_tiles + scan_grid(n_tiles) - 1) / scan_grid(n_tiles) >= 65536)
+		throw std::runtime_error("scan: more than 65535 tiles per workgroup");  // 16-bit tile index in list entries
 	scan_dispatch<1>(s, q, n_tiles, 1, nullptr, 0, tau, seg_pool, seg_cnt, seg_cap, st);
 }
 

@@ -51,8 +51,8 @@ class ShardedSearch:
             self._bufs = (key, gl, gd, gc)
         return self._bufs[1:]
 
-    def search(self, Q, k: int):
-        lab, dis, cnt = self.local_search(Q, k)
+    def search(self, Q, k: int, **kw):
+        lab, dis, cnt = self.local_search(Q, k, **kw)
         if self.world == 1:
             return lab, dis, cnt
         # local -> global labels (unused slots stay -1)
@@ -94,15 +94,26 @@ def hip_device_search(lib, handle, dim: int, nprobes: int = 20, refine_factor: i
 
     import torch
 
-    def search(Q, k):
+    e = ctypes.create_string_buffer(err_len)
+    fn = lib.lance_hip_search_batch_device
+    cache = {}
+
+    def search(Q, k, reuse_outputs: bool = False):
+        """reuse_outputs: return the same output tensors on every call of this
+        shape (the caller consumes them before the next call)."""
         nq = Q.shape[0]
-        ol = torch.empty((nq, k), dtype=torch.int64, device=Q.device)
-        od = torch.empty((nq, k), dtype=torch.float32, device=Q.device)
-        oc = torch.empty((nq,), dtype=torch.int32, device=Q.device)
-        e = ctypes.create_string_buffer(err_len)
-        torch.cuda.current_stream().synchronize()
-        r = lib.lance_hip_search_batch_device(handle, Q.data_ptr(), nq, dim, k, nprobes, refine_factor,
-                                              ol.data_ptr(), od.data_ptr(), oc.data_ptr(), e, err_len)
+        key = (nq, k, Q.device)
+        outs = cache.get(key) if reuse_outputs else None
+        if outs is None:
+            outs = (torch.empty((nq, k), dtype=torch.int64, device=Q.device),
+                    torch.empty((nq, k), dtype=torch.float32, device=Q.device),
+                    torch.empty((nq,), dtype=torch.int32, device=Q.device))
+            if reuse_outputs:
+                cache[key] = outs
+        ol, od, oc = outs
+        torch.cuda.current_stream().synchronize()  # Q written on torch's stream
+        r = fn(handle, Q.data_ptr(), nq, dim, k, nprobes, refine_factor, ol.data_ptr(), od.data_ptr(), oc.data_ptr(),
+               e, err_len)
         if r < 0:
             raise RuntimeError(e.value.decode())
         return ol, od, oc

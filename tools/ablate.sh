@@ -19,19 +19,25 @@ for v in "$@"; do
 	
 	
 	PROF) build PROF -DLHIP_PROF=1 ;;
+	PROF_NOSLOW) build PROF_NOSLOW -DLHIP_PROF=1 -DLHIP_ABL_NO_SLOW=1 ;;
+	PROF_NOFLUSH) build PROF_NOFLUSH -DLHIP_PROF=1 -DLHIP_ABL_NO_FLUSH=1 ;;
 	NOSLOW) build NOSLOW -DLHIP_ABL_NO_SLOW=1 ;;
 	NOREADS) build NOREADS -DLHIP_ABL_NO_READS=1 ;;
 	NOMFMA_NOREADS) build NOMFMA_NOREADS -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 ;;
 	NOMFMA_NOREADS_NOEPI) build NOMFMA_NOREADS_NOEPI -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 -DLHIP_ABL_NO_EPILOGUE=1 ;;
 	NOFLUSH) build NOFLUSH -DLHIP_ABL_NO_FLUSH=1 ;;
+	SLOW_NEVER) build SLOW_NEVER -DLHIP_ABL_SLOW_NEVER=1 ;;
+	SLOW_UNROLL) build SLOW_UNROLL -DLHIP_SLOW_VALU=0 -DLHIP_SLOW_UNROLL=1 ;;
+	SLOW_SWITCH) build SLOW_SWITCH -DLHIP_SLOW_VALU=0 ;;
+	NOLISTWRITE) build NOLISTWRITE -DLHIP_ABL_NO_LISTWRITE=1 ;;
+	DRAIN) build DRAIN -DLHIP_ABL_DRAIN_EPI=1 ;;
+	NOSLOW_DRAIN) build NOSLOW_DRAIN -DLHIP_ABL_DRAIN_EPI=1 -DLHIP_ABL_NO_SLOW=1 ;;
 	SKEL) build SKEL -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 -DLHIP_ABL_NO_EPILOGUE=1 ;;
 	SKEL_NOQ) build SKEL_NOQ -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 -DLHIP_ABL_NO_EPILOGUE=1 -DLHIP_ABL_NO_QDMA=1 ;;
 	SKEL_NOQ_NT0) build SKEL_NOQ_NT0 -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 -DLHIP_ABL_NO_EPILOGUE=1 -DLHIP_ABL_NO_QDMA=1 -DLHIP_X_NT=0 ;;
 	NOQ) build NOQ -DLHIP_ABL_NO_QDMA=1 -DLHIP_ABL_NO_SLOW=1 ;;
 	SKEL_NT0) build SKEL_NT0 -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 -DLHIP_ABL_NO_EPILOGUE=1 -DLHIP_X_NT=0 ;;
 	NT0) build NT0 -DLHIP_X_NT=0 ;;
-	NST3) build NST3 -DLHIP_NST_BF16=3 ;;
-	NST2) build NST2 -DLHIP_NST_BF16=2 ;;
 	NOQ_NT0) build NOQ_NT0 -DLHIP_ABL_NO_QDMA=1 -DLHIP_ABL_NO_SLOW=1 -DLHIP_X_NT=0 ;;
 	
 	
