@@ -14,6 +14,7 @@ constexpr int SCAN_BQ = 256;  // queries per workgroup tile   (MFMA N)
 constexpr int SCAN_BK = 64;   // k-step
 constexpr int DPAD = 64;      // row stride of the device store is a multiple of this
 constexpr int MAX_CAND = 256; // max refined candidates per query per pass
+constexpr int MAX_PASS_Q = 2048; // queries per search pipeline pass (SCAN_BQ-query tiles per scan launch)
 
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 

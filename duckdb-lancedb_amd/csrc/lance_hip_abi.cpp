@@ -518,8 +518,10 @@ struct Index {
 
 void Index::search_device(const float *dQ, int nq, int k, int refine, int64_t *dL, float *dD, int *dC) {
 	last_stats[0] = last_stats[1] = last_stats[2] = last_stats[3] = 0;
-	for (int s = 0; s < nq; s += SCAN_BQ) {
-		int c = std::min(SCAN_BQ, nq - s);
+	// one pipeline pass covers up to MAX_PASS_Q queries (several query tiles
+	// per scan launch): the per-pass fixed cost is paid once per pass
+	for (int s = 0; s < nq; s += MAX_PASS_Q) {
+		int c = std::min(MAX_PASS_Q, nq - s);
 		search_chunk(dQ + (int64_t)s * dim, c, k, refine, dL + (int64_t)s * k, dD + (int64_t)s * k, dC + s);
 	}
 }
