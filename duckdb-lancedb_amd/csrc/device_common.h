@@ -1,0 +1,100 @@
+// Device helpers shared by the gfx950 kernel files (knn_kernels.hip: flat
+// path, ivf_kernels.hip: IVF_FLAT / IVF_PQ).  Canonical numerics of this build:
+// ordered float keys, the (distance, label) order, exact distances with f64
+// accumulation rounded once to f32 (DESIGN.md "Oracle and parity").
+#pragma once
+#include "knn_kernels.h"
+
+namespace lhip {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+static constexpr float F_INF = __builtin_huge_valf();
+static constexpr float F_MAX = 3.40282347e+38f;
+static constexpr uint32_t KEY_INF = 0xFF800000u;  // ordered key of +inf
+static constexpr uint32_t KEY_NAN = 0xFFFFFFFFu;  // every NaN is canonicalised to this
+
+// ---------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t fkey(float f) {
+	uint32_t u = __float_as_uint(f);
+	if ((u & 0x7FFFFFFFu) > 0x7F800000u) return KEY_NAN;
+	return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float fkey_inv(uint32_t k) {
+	uint32_t u = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+	return __uint_as_float(u);
+}
+__device__ __forceinline__ uint16_t bf16_bits(float f) {
+	__bf16 h = (__bf16)f;  // RNE: v_cvt_pk_bf16_f32 on gfx950
+	return __builtin_bit_cast(uint16_t, h);
+}
+__device__ __forceinline__ float bf16_round(float f) {
+	return (float)(__bf16)f;
+}
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+	return (uint32_t)bf16_bits(a) | ((uint32_t)bf16_bits(b) << 16);
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+	return v;
+}
+// (distance, label) total order used everywhere: NaN after +inf, then label.
+__device__ __forceinline__ bool hit_less(float da, int64_t la, float db, int64_t lb) {
+	bool an = __builtin_isnan(da), bn = __builtin_isnan(db);
+	if (an != bn) return bn;
+	if (!an && da != db) return da < db;
+	return la < lb;
+}
+// unit roundoff used by the bounds; 2^-23 (not 2^-24) leaves room for an
+// accumulation that truncates instead of rounding.
+static constexpr double U_BOUND = 1.1920928955078125e-07;
+
+// a base element as f32: the store holds f32, or bf16 bits (uint16_t)
+__device__ __forceinline__ float xval(const float *p, int64_t i) { return p[i]; }
+__device__ __forceinline__ float xval(const uint16_t *p, int64_t i) { return __uint_as_float((uint32_t)p[i] << 16); }
+
+// Row aux layout: tile-blocked SoA, 16 B per slot.  For slot r of tile
+// T = r / 256 the four terms live at floats [T*1024 + c*256 + r%256],
+// c = 0 alpha, 1 xn, 2 ux, 3 sc.  A tile's block is the 4 KiB the scan DMAs
+// into LDS, and four consecutive rows' terms are one 16 B read.
+__host__ __device__ __forceinline__ int64_t raix(int64_t r, int c) { return ((r >> 8) << 10) | ((int64_t)c << 8) | (r & 255); }
+
+template <int METRIC, typename T>
+__device__ __forceinline__ float exact_distance(const T *__restrict__ x, const float *__restrict__ q, int dim,
+                                                int lane) {
+	double a = 0.0, b = 0.0, c = 0.0;
+	for (int i = lane; i < dim; i += 64) {
+		double xv = xval(x, i), qv = q[i];
+		if (METRIC == METRIC_L2) {
+			double d = xv - qv;
+			a += d * d;
+		} else {
+			a += xv * qv;
+			if (METRIC == METRIC_COSINE) {
+				b += xv * xv;
+				c += qv * qv;
+			}
+		}
+	}
+	a = wave_sum_f64(a);
+	if (METRIC == METRIC_COSINE) {
+		b = wave_sum_f64(b);
+		c = wave_sum_f64(c);
+	}
+	double r;
+	if (METRIC == METRIC_L2)
+		r = a;
+	else if (METRIC == METRIC_DOT)
+		r = 1.0 - a;
+	else
+		r = 1.0 - a / (sqrt(b) * sqrt(c));
+	float f = (float)r + 0.0f;  // canonical +0
+	if (__builtin_isnan(f)) f = __builtin_nanf("");
+	return f;
+}
+
+}  // namespace lhip

@@ -1,0 +1,528 @@
+// Internal: the handle behind the C-ABI (lhip::Index), its device store and
+// workspace.  Shared by lance_hip_abi.cpp (flat path, C-ABI) and ivf_index.cpp
+// (IVF_FLAT / IVF_PQ, lance_manager.rs:483-515).  Not part of the public ABI.
+#pragma once
+#include "knn_kernels.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <sys/stat.h>
+#include <vector>
+
+namespace lhip {
+
+struct IvfState;            // ivf_index.cpp
+struct Index;
+void ivf_free(IvfState *s);  // ivf_index.cpp
+// compaction keeps slots `keep` (ascending old slots): carry the IVF list
+// assignment / PQ codes of the kept indexed rows over to their new slots
+void ivf_remap(Index *ix, const std::vector<int64_t> &keep);
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+struct Error : std::runtime_error {
+	using std::runtime_error::runtime_error;
+};
+
+#define HIPCHK(expr)                                                                                                   \
+	do {                                                                                                               \
+		hipError_t _e = (expr);                                                                                        \
+		if (_e != hipSuccess) throw Error(std::string("HIP error: ") + hipGetErrorString(_e) + " at " #expr);          \
+	} while (0)
+
+// Completion wait of a search: spins on the stream (a blocking wait costs tens
+// of microseconds of wake-up per call, ~10% of a C2 batch).
+inline void spin_sync(hipStream_t st) {
+	hipError_t e;
+	while ((e = hipStreamQuery(st)) == hipErrorNotReady) {
+	}
+	if (e != hipSuccess) throw Error(std::string("HIP error: ") + hipGetErrorString(e) + " at stream completion");
+}
+
+inline void write_err(char *buf, int len, const std::string &msg) {
+	if (!buf || len <= 0) return;
+	size_t n = std::min(msg.size(), (size_t)(len - 1));
+	memcpy(buf, msg.data(), n);
+	buf[n] = 0;
+}
+
+inline int metric_id(const std::string &m) {
+	// lance_manager.rs:493-497: cosine -> Cosine, dot|ip -> Dot, else L2
+	if (m == "cosine") return METRIC_COSINE;
+	if (m == "dot" || m == "ip") return METRIC_DOT;
+	return METRIC_L2;
+}
+
+// ---------------------------------------------------------------------------
+// device buffers
+// ---------------------------------------------------------------------------
+template <typename T>
+struct DevBuf {
+	T *p = nullptr;
+	size_t n = 0;  // capacity in elements
+	~DevBuf() { release(); }
+	void release() {
+		if (p) (void)hipFree(p);
+		p = nullptr;
+		n = 0;
+	}
+	// grow without preserving contents
+	void need(size_t m) {
+		if (m <= n) return;
+		release();
+		size_t c = std::max(m, (size_t)1);
+		HIPCHK(hipMalloc(&p, c * sizeof(T)));
+		n = c;
+	}
+};
+
+struct Workspace {
+	DevBuf<float> Qin, Qf, tau, cut, dense, cand_dist, out_d, fb_keys, fb_keys2, stage;
+	DevBuf<uint16_t> Qb;
+	DevBuf<float4> qaux;
+	DevBuf<uint2> seg_pool;
+	DevBuf<int> seg_cnt;
+	DevBuf<int> status, out_c;  // status = [cert | cand_cnt | pool_cnt] x nq
+	int *h_status = nullptr;    // pinned mirror of status
+	size_t h_status_n = 0;
+	DevBuf<uint32_t> cand_slot;
+	DevBuf<int64_t> out_l, fb_vals, fb_vals2, idx;
+	DevBuf<uint8_t> sort_tmp;
+	~Workspace() {
+		if (h_status) (void)hipHostFree(h_status);
+	}
+	void need_host_status(size_t n) {
+		if (n <= h_status_n) return;
+		if (h_status) HIPCHK(hipHostFree(h_status));
+		h_status = nullptr;
+		HIPCHK(hipHostMalloc(&h_status, n * sizeof(int)));
+		h_status_n = n;
+	}
+};
+
+// ---------------------------------------------------------------------------
+// the handle
+// ---------------------------------------------------------------------------
+struct Index {
+	std::string db_path, table, metric_name;
+	int metric = METRIC_L2;
+	int dim = 0;
+	int ld = 0;  // padded row stride
+	int device = 0;
+	bool metric_quirk = false;  // rank by L2 whatever the metric (reference behaviour)
+
+	std::mutex mu;
+	int64_t next_label = 0;
+
+	// host bookkeeping (slot order == ascending label order, always)
+	std::vector<int64_t> slot_label;
+	std::vector<uint8_t> live;
+	int64_t n_live = 0;
+
+	// device store: rows of `ld` elements, f32, or bf16 bits with storage "bf16"
+	void *X = nullptr;
+	bool xbf16 = false;
+	size_t xes() const { return xbf16 ? 2 : 4; }
+	uint8_t *xrow(int64_t s) const { return static_cast<uint8_t *>(X) + (size_t)s * ld * xes(); }
+	// bf16 scan copy of an f32 store (option scan_copy, default on): the scan
+	// streams 2 B per element; refine, get_vector and compact use the f32 rows
+	uint16_t *Xs = nullptr;
+	bool scan_copy = true;
+	bool has_scan_copy() const { return !xbf16 && scan_copy; }
+	float4 *rowaux = nullptr;  // aux for `metric`
+	float4 *rowaux_l2 = nullptr;  // aux for L2 when metric_quirk is on and metric != l2
+	int64_t *dlabels = nullptr;
+	int64_t cap = 0, n_slots = 0;
+	DevBuf<unsigned> stats;  // [0]=max alpha bits, [1]=max ux bits, [2],[3] for rowaux_l2
+	float max_alpha = 0.f, max_ux = 0.f, max_alpha_l2 = 0.f, max_ux_l2 = 0.f;
+	hipStream_t stream = nullptr;
+	Workspace ws;
+
+	// persistence
+	FILE *log = nullptr;
+
+	// IVF index (lance_detached_create_index, ivf_index.cpp); null = flat search.
+	// Options: index_type (IVF_PQ as lance_manager.rs:483-515 builds, or
+	// IVF_FLAT), k-means iterations and sampling seed.
+	IvfState *ivf = nullptr;
+	int ivf_type_opt = 1;  // 0 IVF_FLAT, 1 IVF_PQ
+	int kmeans_iters = 50;  // lance k-means max_iters default
+	uint64_t ivf_seed = 0x5eedULL;
+
+	int64_t last_stats[4] = {0, 0, 0, 0};
+
+	// optional HIP-event timing of the scan kernels, on the stream they run on
+	bool time_kernels = false;
+	int sample_div = 32;  // sample pass covers ~1/sample_div of the tiles (>= 32 tiles)
+	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+	double kt_append_ms = 0.0, kt_dense_ms = 0.0;
+	int64_t kt_append_n = 0, kt_dense_n = 0;
+	int64_t kt_append_rows = 0, kt_append_qpad = 0;
+
+	~Index() {
+		if (log) fclose(log);
+		ivf_free(ivf);
+		(void)hipSetDevice(device);
+		if (X) (void)hipFree(X);
+		if (Xs) (void)hipFree(Xs);
+		if (rowaux) (void)hipFree(rowaux);
+		if (rowaux_l2) (void)hipFree(rowaux_l2);
+		if (dlabels) (void)hipFree(dlabels);
+		for (auto &e : ev)
+			if (e) (void)hipEventDestroy(e);
+		if (stream) (void)hipStreamDestroy(stream);
+	}
+
+	void tic(int i) {
+		if (time_kernels) HIPCHK(hipEventRecord(ev[i], stream));
+	}
+	float toc_ms(int a, int b) {
+		float ms = 0.f;
+		HIPCHK(hipEventSynchronize(ev[b]));
+		HIPCHK(hipEventElapsedTime(&ms, ev[a], ev[b]));
+		return ms;
+	}
+
+	void init_device(int dev) {
+		int n = 0;
+		if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) throw Error("no HIP device available");
+		if (dev < 0) HIPCHK(hipGetDevice(&dev));
+		if (dev >= n) throw Error("HIP device " + std::to_string(dev) + " out of range");
+		device = dev;
+		HIPCHK(hipSetDevice(device));
+		HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+		stats.need(4);
+		HIPCHK(hipMemsetAsync(stats.p, 0, 4 * sizeof(unsigned), stream));
+		HIPCHK(hipStreamSynchronize(stream));
+	}
+
+	void bind() { HIPCHK(hipSetDevice(device)); }
+
+	// grow the device store to hold at least `want` slots (contents preserved)
+	void reserve(int64_t want) {
+		if (want <= cap) return;
+		// capacity is a multiple of the scan tile and the tail past n_slots is
+		// zero: the scan kernel streams whole tiles without clamping rows
+		int64_t c = round_up(std::max<int64_t>(want, std::max<int64_t>(4096, cap * 2)), SCAN_BR);
+		void *nX = nullptr;
+		uint16_t *nXs = nullptr;
+		float4 *na = nullptr, *na2 = nullptr;
+		int64_t *nl = nullptr;
+		HIPCHK(hipMalloc(&nX, (size_t)c * ld * xes()));
+		if (has_scan_copy()) HIPCHK(hipMalloc(&nXs, (size_t)c * ld * 2));
+		HIPCHK(hipMalloc(&na, (size_t)c * sizeof(float4)));
+		HIPCHK(hipMalloc(&nl, (size_t)c * sizeof(int64_t)));
+		if (rowaux_l2 || (metric_quirk && metric != METRIC_L2)) HIPCHK(hipMalloc(&na2, (size_t)c * sizeof(float4)));
+		if (n_slots > 0) {
+			HIPCHK(hipMemcpyAsync(nX, X, (size_t)n_slots * ld * xes(), hipMemcpyDeviceToDevice, stream));
+			if (nXs) HIPCHK(hipMemcpyAsync(nXs, Xs, (size_t)n_slots * ld * 2, hipMemcpyDeviceToDevice, stream));
+			// row aux is tile-blocked SoA: move whole tile blocks (cap is a
+			// multiple of SCAN_BR, so they exist in the old buffer)
+			const size_t aux_bytes = (size_t)round_up(n_slots, SCAN_BR) * sizeof(float4);
+			HIPCHK(hipMemcpyAsync(na, rowaux, aux_bytes, hipMemcpyDeviceToDevice, stream));
+			HIPCHK(hipMemcpyAsync(nl, dlabels, (size_t)n_slots * sizeof(int64_t), hipMemcpyDeviceToDevice, stream));
+			if (na2 && rowaux_l2) HIPCHK(hipMemcpyAsync(na2, rowaux_l2, aux_bytes, hipMemcpyDeviceToDevice, stream));
+		}
+		HIPCHK(hipMemsetAsync(static_cast<uint8_t *>(nX) + (size_t)n_slots * ld * xes(), 0,
+		                      (size_t)(c - n_slots) * ld * xes(), stream));
+		if (nXs) HIPCHK(hipMemsetAsync(nXs + (size_t)n_slots * ld, 0, (size_t)(c - n_slots) * ld * 2, stream));
+		launch_fill_rowaux(na, n_slots, c, stream);
+		if (na2) launch_fill_rowaux(na2, n_slots, c, stream);
+		HIPCHK(hipStreamSynchronize(stream));
+		if (X) HIPCHK(hipFree(X));
+		if (Xs) HIPCHK(hipFree(Xs));
+		Xs = nXs;
+		if (rowaux) HIPCHK(hipFree(rowaux));
+		if (dlabels) HIPCHK(hipFree(dlabels));
+		if (rowaux_l2) HIPCHK(hipFree(rowaux_l2));
+		X = nX;
+		rowaux = na;
+		dlabels = nl;
+		rowaux_l2 = na2;
+		cap = c;
+	}
+
+	void refresh_stats() {
+		unsigned h[4];
+		HIPCHK(hipMemcpyAsync(h, stats.p, sizeof(h), hipMemcpyDeviceToHost, stream));
+		HIPCHK(hipStreamSynchronize(stream));
+		memcpy(&max_alpha, &h[0], 4);
+		memcpy(&max_ux, &h[1], 4);
+		memcpy(&max_alpha_l2, &h[2], 4);
+		memcpy(&max_ux_l2, &h[3], 4);
+	}
+
+	// scan copy rows [s0, s0+n) = bf16 (RNE) of the f32 rows of X (padding
+	// columns stay zero)
+	void fill_scan_copy(int64_t s0, int64_t n, uint16_t *dst) {
+		if (n > 0)
+			launch_rows_to_bf16(reinterpret_cast<const float *>(xrow(s0)), ld, n, dim, ld, dst + (size_t)s0 * ld,
+			                    stream);
+	}
+
+	// option scan_copy: build or drop the bf16 scan copy of an f32 store
+	void set_scan_copy(bool on) {
+		if (on == scan_copy) return;
+		scan_copy = on;
+		if (!on) {
+			if (Xs) HIPCHK(hipFree(Xs));
+			Xs = nullptr;
+			return;
+		}
+		if (xbf16 || !X) return;  // allocated with the store
+		HIPCHK(hipMalloc(&Xs, (size_t)cap * ld * 2));
+		HIPCHK(hipMemsetAsync(Xs, 0, (size_t)cap * ld * 2, stream));
+		fill_scan_copy(0, n_slots, Xs);
+		HIPCHK(hipGetLastError());
+		HIPCHK(hipStreamSynchronize(stream));
+	}
+
+	// append rows already resident on the device at X[n_slots .. n_slots+num)
+	int64_t commit_rows(int64_t num) {
+		const int64_t first = next_label;
+		std::vector<int64_t> labs((size_t)num);
+		for (int64_t i = 0; i < num; ++i) labs[(size_t)i] = first + i;
+		HIPCHK(hipMemcpyAsync(dlabels + n_slots, labs.data(), (size_t)num * sizeof(int64_t), hipMemcpyHostToDevice,
+		                      stream));
+		if (Xs) fill_scan_copy(n_slots, num, Xs);
+		launch_rowaux(X, xbf16, ld, dim, metric, n_slots, num, rowaux, stats.p, stream);
+		if (rowaux_l2) launch_rowaux(X, xbf16, ld, dim, METRIC_L2, n_slots, num, rowaux_l2, stats.p + 2, stream);
+		HIPCHK(hipGetLastError());
+		HIPCHK(hipStreamSynchronize(stream));
+		refresh_stats();
+		slot_label.insert(slot_label.end(), labs.begin(), labs.end());
+		live.insert(live.end(), (size_t)num, 1);
+		n_slots += num;
+		n_live += num;
+		next_label = first + num;
+		return first;
+	}
+
+	int64_t add_host(const float *v, int64_t num) {
+		reserve(n_slots + num);
+		if (!xbf16) {
+			float *dst = reinterpret_cast<float *>(xrow(n_slots));
+			if (ld != dim) HIPCHK(hipMemsetAsync(dst, 0, (size_t)num * ld * sizeof(float), stream));
+			HIPCHK(hipMemcpy2DAsync(dst, (size_t)ld * sizeof(float), v, (size_t)dim * sizeof(float),
+			                        (size_t)dim * sizeof(float), (size_t)num, hipMemcpyHostToDevice, stream));
+		} else {
+			// bf16 store: f32 rows through a bounded device staging buffer
+			const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(num, (int64_t)(64 << 20) / (dim * 4)));
+			ws.stage.need((size_t)chunk * dim);
+			for (int64_t i = 0; i < num; i += chunk) {
+				const int64_t m = std::min<int64_t>(chunk, num - i);
+				HIPCHK(hipMemcpyAsync(ws.stage.p, v + i * dim, (size_t)m * dim * sizeof(float), hipMemcpyHostToDevice,
+				                      stream));
+				launch_rows_to_bf16(ws.stage.p, dim, m, dim, ld, reinterpret_cast<uint16_t *>(xrow(n_slots + i)),
+				                    stream);
+				HIPCHK(hipStreamSynchronize(stream));  // staging buffer reused
+			}
+		}
+		return commit_rows(num);
+	}
+
+	int64_t add_device(const float *v, int64_t num) {
+		reserve(n_slots + num);
+		if (!xbf16) {
+			float *dst = reinterpret_cast<float *>(xrow(n_slots));
+			if (ld != dim) HIPCHK(hipMemsetAsync(dst, 0, (size_t)num * ld * sizeof(float), stream));
+			HIPCHK(hipMemcpy2DAsync(dst, (size_t)ld * sizeof(float), v, (size_t)dim * sizeof(float),
+			                        (size_t)dim * sizeof(float), (size_t)num, hipMemcpyDeviceToDevice, stream));
+		} else {
+			launch_rows_to_bf16(v, dim, num, dim, ld, reinterpret_cast<uint16_t *>(xrow(n_slots)), stream);
+		}
+		return commit_rows(num);
+	}
+
+	// rows [s0, s0+n) as f32 (dim columns) into host memory
+	void read_rows(int64_t s0, int64_t n, float *out) {
+		if (n <= 0) return;
+		if (!xbf16) {
+			HIPCHK(hipMemcpy2D(out, (size_t)dim * sizeof(float), xrow(s0), (size_t)ld * sizeof(float),
+			                   (size_t)dim * sizeof(float), (size_t)n, hipMemcpyDeviceToHost));
+			return;
+		}
+		std::vector<uint16_t> b((size_t)n * dim);
+		HIPCHK(hipMemcpy2D(b.data(), (size_t)dim * 2, xrow(s0), (size_t)ld * 2, (size_t)dim * 2, (size_t)n,
+		                   hipMemcpyDeviceToHost));
+		for (size_t i = 0; i < b.size(); ++i) {
+			const uint32_t u = (uint32_t)b[i] << 16;
+			memcpy(out + i, &u, 4);
+		}
+	}
+
+	// storage "f32" | "bf16"; only while the store holds no rows
+	void set_storage(bool bf16) {
+		if (n_slots > 0) throw Error("storage can only be changed on an empty table");
+		if (bf16 == xbf16) return;
+		if (X) {
+			HIPCHK(hipFree(X));
+			if (Xs) HIPCHK(hipFree(Xs));
+			Xs = nullptr;
+			HIPCHK(hipFree(rowaux));
+			HIPCHK(hipFree(dlabels));
+			if (rowaux_l2) HIPCHK(hipFree(rowaux_l2));
+			X = nullptr;
+			rowaux = rowaux_l2 = nullptr;
+			dlabels = nullptr;
+			cap = 0;
+		}
+		xbf16 = bf16;
+	}
+
+	int64_t slot_of(int64_t label) const {
+		auto it = std::lower_bound(slot_label.begin(), slot_label.end(), label);
+		if (it == slot_label.end() || *it != label) return -1;
+		return (int64_t)(it - slot_label.begin());
+	}
+
+	// returns the labels actually deleted (live before the call)
+	std::vector<int64_t> remove(const int64_t *labels, int64_t n) {
+		std::vector<int64_t> slots, done;
+		for (int64_t i = 0; i < n; ++i) {
+			int64_t s = slot_of(labels[i]);
+			if (s < 0 || !live[(size_t)s]) continue;
+			live[(size_t)s] = 0;
+			--n_live;
+			slots.push_back(s);
+			done.push_back(labels[i]);
+		}
+		if (!slots.empty()) {
+			ws.idx.need(slots.size());
+			HIPCHK(hipMemcpyAsync(ws.idx.p, slots.data(), slots.size() * sizeof(int64_t), hipMemcpyHostToDevice,
+			                      stream));
+			launch_tombstone(rowaux, ws.idx.p, (int)slots.size(), stream);
+			if (rowaux_l2) launch_tombstone(rowaux_l2, ws.idx.p, (int)slots.size(), stream);
+			HIPCHK(hipGetLastError());
+			HIPCHK(hipStreamSynchronize(stream));
+		}
+		return done;
+	}
+
+	void compact() {
+		if (n_live == n_slots) return;
+		std::vector<int64_t> keep;
+		keep.reserve((size_t)n_live);
+		for (int64_t s = 0; s < n_slots; ++s)
+			if (live[(size_t)s]) keep.push_back(s);
+		const int64_t n = (int64_t)keep.size();
+		if (ivf) ivf_remap(this, keep);
+		const int64_t c = round_up(std::max<int64_t>(4096, n), SCAN_BR);
+		void *nX = nullptr;
+		float4 *na = nullptr, *na2 = nullptr;
+		int64_t *nl = nullptr;
+		HIPCHK(hipMalloc(&nX, (size_t)c * ld * xes()));
+		HIPCHK(hipMalloc(&na, (size_t)c * sizeof(float4)));
+		HIPCHK(hipMalloc(&nl, (size_t)c * sizeof(int64_t)));
+		if (rowaux_l2) HIPCHK(hipMalloc(&na2, (size_t)c * sizeof(float4)));
+		if (n > 0) {
+			ws.idx.need((size_t)n);
+			HIPCHK(hipMemcpyAsync(ws.idx.p, keep.data(), (size_t)n * sizeof(int64_t), hipMemcpyHostToDevice, stream));
+			launch_gather_rows(X, xbf16, rowaux, dlabels, ws.idx.p, n, ld, nX, na, nl, stream);
+			if (rowaux_l2) launch_gather_rows(X, xbf16, rowaux_l2, dlabels, ws.idx.p, n, ld, nX, na2, nl, stream);
+			HIPCHK(hipGetLastError());
+		}
+		HIPCHK(hipMemsetAsync(static_cast<uint8_t *>(nX) + (size_t)n * ld * xes(), 0, (size_t)(c - n) * ld * xes(),
+		                      stream));
+		launch_fill_rowaux(na, n, c, stream);
+		if (na2) launch_fill_rowaux(na2, n, c, stream);
+		uint16_t *nXs = nullptr;
+		if (Xs) {
+			HIPCHK(hipMalloc(&nXs, (size_t)c * ld * 2));
+			HIPCHK(hipMemsetAsync(nXs, 0, (size_t)c * ld * 2, stream));
+			if (n > 0)
+				launch_rows_to_bf16(static_cast<const float *>(nX), ld, n, dim, ld, nXs, stream);
+			HIPCHK(hipGetLastError());
+		}
+		HIPCHK(hipStreamSynchronize(stream));
+		if (Xs) HIPCHK(hipFree(Xs));
+		Xs = nXs;
+		HIPCHK(hipFree(X));
+		HIPCHK(hipFree(rowaux));
+		HIPCHK(hipFree(dlabels));
+		if (rowaux_l2) HIPCHK(hipFree(rowaux_l2));
+		X = nX;
+		rowaux = na;
+		dlabels = nl;
+		rowaux_l2 = na2;
+		cap = c;
+		std::vector<int64_t> nsl;
+		nsl.reserve((size_t)n);
+		for (int64_t s : keep) nsl.push_back(slot_label[(size_t)s]);
+		slot_label.swap(nsl);
+		live.assign((size_t)n, 1);
+		n_slots = n;
+		n_live = n;
+	}
+
+	// ---- persistence: append-only log <db_path>/<table>.lancehip ----------
+	std::string log_path() const { return db_path + "/" + table + ".lancehip"; }
+
+	void log_open(bool truncate) {
+		if (db_path.empty()) return;
+		// mkdir -p db_path
+		std::string acc;
+		for (size_t i = 0; i <= db_path.size(); ++i) {
+			if (i == db_path.size() || db_path[i] == '/') {
+				if (!acc.empty() && acc != "/") (void)mkdir(acc.c_str(), 0755);
+			}
+			if (i < db_path.size()) acc.push_back(db_path[i]);
+		}
+		log = fopen(log_path().c_str(), truncate ? "wb" : "ab");
+		if (!log) throw Error("cannot open " + log_path() + ": " + strerror(errno));
+		if (truncate) {
+			fwrite("LHIPLOG1", 1, 8, log);
+			int32_t d = dim;
+			fwrite(&d, 4, 1, log);
+			fflush(log);
+		}
+	}
+	void log_add(int64_t first, const float *v, int64_t num) {
+		if (!log) return;
+		uint8_t tag = 1;
+		fwrite(&tag, 1, 1, log);
+		fwrite(&first, 8, 1, log);
+		fwrite(&num, 8, 1, log);
+		fwrite(v, sizeof(float), (size_t)num * dim, log);
+		fflush(log);
+	}
+	void log_storage() {
+		if (!log) return;
+		uint8_t tag = 3, v = xbf16 ? 1 : 0;
+		fwrite(&tag, 1, 1, log);
+		fwrite(&v, 1, 1, log);
+		fflush(log);
+	}
+	void log_del(const std::vector<int64_t> &labs) {
+		if (!log || labs.empty()) return;
+		uint8_t tag = 2;
+		int64_t n = (int64_t)labs.size();
+		fwrite(&tag, 1, 1, log);
+		fwrite(&n, 8, 1, log);
+		fwrite(labs.data(), 8, labs.size(), log);
+		fflush(log);
+	}
+
+	// IVF model record (tag 4: type, nlist, m, centroids [nlist][dim], codebook)
+	// and optimize record (tag 5); bodies in ivf_index.cpp
+	void log_model();
+	void log_optimize();
+
+	// ---- search ------------------------------------------------------------
+	// IVF search when an index exists, else the exact flat path
+	void search_any(const float *dQ, int nq, int k, int nprobes, int refine, int64_t *dL, float *dD, int *dC);
+	// Device-side batched search; dQ [nq][dim] (device), outputs device.
+	void search_device(const float *dQ, int nq, int k, int refine, int64_t *dL, float *dD, int *dC);
+	void search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL, float *dD, int *dC);
+};
+
+}  // namespace lhip

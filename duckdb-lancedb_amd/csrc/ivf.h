@@ -1,0 +1,141 @@
+// IVF_FLAT / IVF_PQ indexes of the MI355X-native path (internal; not public ABI).
+//
+// Replaces what lance_manager.rs:483-515 (create_ann_index -> lancedb 0.15
+// IvfPqIndexBuilder -> lance-index 0.22 k-means + PQ training) builds and what
+// lance_manager.rs:411-418 (vector_search(..).nprobes(n).refine_factor(r))
+// searches, paths relative to /root/reference.  Layout and kernels: DESIGN.md
+// "IVF".  Canonical numerics (restated by oracle/ivf.py):
+//   coarse   exact distances to the centroids (f64 accumulate, f32 result),
+//            top-nprobe by (distance, list id)
+//   IVF_FLAT exact distance of every live row of the probed lists,
+//            top-k by (distance, label)
+//   IVF_PQ   ADC(q, row) = d0 + sum_j LUT[j][code_j], summed in f32 in j order,
+//            d0 = the coarse distance of the row's list, LUT = T[list] - 2 P[q]
+//            (L2 / cosine, residual PQ) or -P[q] (dot), with
+//              P[q][j][c] = sum_t q_{j,t} * y_{j,c,t}
+//              T[l][j][c] = sum_t y_{j,c,t} * (y_{j,c,t} + 2 c_{l,j,t})
+//            (f32, t in order, no fused multiply-add); top-(k*refine_factor)
+//            by (ADC, label) -> exact re-rank -> top-k by (distance, label)
+//   rows added after the build (slots >= n_indexed) are searched exactly and
+//   merged (LanceDB searches unindexed fragments flat); cosine works in the
+//   row-normalised space (k-means, residuals, P), exact cosine at the end.
+#pragma once
+#include "index.h"
+
+namespace lhip {
+
+enum IvfType : int { IVF_FLAT = 0, IVF_PQ = 1 };
+constexpr int PQ_K = 256;          // 8-bit codes (nbits = 8)
+constexpr int PQ_MAX_M = 128;      // LUT of m x 256 f32 must fit in LDS with the top-k buffer
+constexpr int PQ_MAX_DSUB = 64;    // codebook slice of one sub-space in LDS
+constexpr int IVF_TOPK_CAP = 2048; // LDS top-k buffer of the list scans / merges
+constexpr int IVF_MAX_K = 1024;    // k (and k * refine_factor) bound of the IVF path
+constexpr int FLAT_BLK = 256;      // rows per IVF_FLAT list-scan work item
+constexpr uint32_t SLOT_NONE = 0xFFFFFFFFu;
+
+struct IvfState {
+	int type = IVF_PQ;
+	int nlist = 0, m = 0, dsub = 0, mp = 0;  // mp = code bytes per row, multiple of 16
+	int metric = METRIC_L2;                  // index metric
+	int64_t n_indexed = 0;                   // slots [0, n_indexed) are in the lists
+	Index *coarse = nullptr;                 // centroid store (exact top-nprobe)
+	DevBuf<float> centroids;                 // [nlist][ld] f32, zero padded
+	DevBuf<float> codebook;                  // [m][256][dsub]
+	DevBuf<float> T;                         // [nlist][m][256] (L2 / cosine)
+	DevBuf<int> assign;                      // [n_indexed] list of each indexed slot
+	DevBuf<uint8_t> codes;                   // [n_indexed][mp] slot-major codes
+	// list layout (rebuilt when dirty): positions padded to 64 per list
+	bool dirty = true;
+	std::vector<int64_t> h_loff;             // [nlist+1]
+	DevBuf<int64_t> loff;
+	DevBuf<uint32_t> lslot;                  // [npos] slot, SLOT_NONE for padding
+	DevBuf<uint8_t> lcodes;                  // [npos/64][mp/16][64][16] blocked codes
+	DevBuf<int> blk_list, lblk0;             // IVF_FLAT work items (256 positions each)
+	DevBuf<int64_t> blk_pos0;
+	int nblk = 0, maxb = 1;
+	// search workspace
+	DevBuf<float> Qf, Qn, P, probe_d, tmpf;
+	DevBuf<int64_t> probe_l;
+	DevBuf<int> probe_c, lcnt, pstart, pairs;
+	DevBuf<uint64_t> keys, tkeys, cand_a, cand_b, best;
+	DevBuf<uint8_t> tmpb;
+	~IvfState();
+};
+
+// ---- host API (ivf_index.cpp) -----------------------------------------------
+// lance_detached_create_index: train (k-means on a seeded sample, PQ on the
+// residuals) and index every live row.  num_partitions / num_sub_vectors <= 0
+// take LanceDB's defaults (sqrt(rows); dim/16, dim/8 or 1).
+void ivf_build(Index *ix, int type, int num_partitions, int num_sub_vectors);
+// Install a given model (multi-GPU: rank 0 trains, every rank indexes its own
+// shard with the same centroids / codebook).  codebook may be null for IVF_FLAT.
+void ivf_set_model(Index *ix, int type, int nlist, int m, const float *centroids, const float *codebook);
+// lance_detached_compact (= optimize(All)): index the rows added since the build.
+void ivf_optimize(Index *ix);
+// Batched IVF search; device pointers, synchronous.
+void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refine, int64_t *dL, float *dD, int *dC);
+
+// Host copies of the model (centroids [nlist][dim], codebook [m][256][dsub]) and
+// of the per-slot list / codes (slots >= n_indexed: list -1, codes 0).
+void ivf_export_model(Index *ix, float *centroids, float *codebook);
+void ivf_export_slots(Index *ix, int32_t *slot_list, uint8_t *slot_codes);
+
+// ---- kernel launchers (ivf_kernels.hip) -------------------------------------
+void launch_gather_sample(const void *X, int xbf16, int ld, int dim, const int64_t *slots, int64_t n, int normalize,
+                          float *out_f32, uint16_t *out_bf16, hipStream_t st);
+void launch_centroid_prep(const float *C, int nc, int nc_pad, int ld, uint16_t *Cb, float *cnorm, hipStream_t st);
+// best[r] = min over centroids of (orderedkey(|c|^2 - 2 s_r x_r.c) << 32 | c), bf16 MFMA dot products.
+// Rows: X (f32 or bf16 bits, stride ld) rows r0 + r for r < n; s_r = 1 or the
+// row scale (rowaux w, cosine).  best must be pre-set to ~0.
+void launch_kmeans_assign(const void *X, int xbf16, int ld, int64_t r0, int64_t n, const float *row_scale_aux,
+                          const uint16_t *Cb, const float *cnorm, int nc_pad, uint64_t *best, hipStream_t st);
+// same with f32 centroids [nc_pad][ld] and exact-f32 MFMA products (row placement)
+void launch_kmeans_assign_f32(const void *X, int xbf16, int ld, int64_t r0, int64_t n, const float *row_scale_aux,
+                              const float *Cf, const float *cnorm, int nc_pad, uint64_t *best, hipStream_t st);
+// sum over rows of the winning score (f64, for the k-means stopping rule)
+void launch_score_sum(const uint64_t *best, int64_t n, double *out, hipStream_t st);
+void launch_sq_sum(const float *v, int64_t n, double *out, hipStream_t st);
+void launch_gather_bytes(const uint8_t *src, const int64_t *idx, int64_t n, int row_bytes, uint8_t *dst,
+                         hipStream_t st);
+void launch_best_to_assign(const uint64_t *best, int64_t n, int *assign, uint32_t *keys, uint32_t *vals,
+                           hipStream_t st);
+int sort_u32_pairs(void *temp, size_t &temp_bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
+                   uint32_t *vout, int64_t n, int end_bit, hipStream_t st);
+void launch_segments(const uint32_t *sorted_keys, int64_t n, int nseg, int *seg_start, hipStream_t st);
+void launch_centroid_mean(const float *S, int ld, int dim, const uint32_t *sorted_idx, const int *seg_start, int nc,
+                          float *C, hipStream_t st);
+void launch_residuals(const float *S, const int *assign, const float *C, int ld, int64_t n, float *R,
+                      hipStream_t st);
+void launch_pq_assign(const float *R, int ld, int64_t n, int m, int dsub, const float *cb, uint32_t *keys,
+                      uint32_t *vals, hipStream_t st);
+void launch_pq_mean(const float *R, int ld, const uint32_t *sorted_idx, const int *seg_start, int m, int dsub,
+                    float *cb, hipStream_t st);
+void launch_pq_encode(const void *X, int xbf16, int ld, int dim, int64_t s0, int64_t n, const float *rowaux_f,
+                      int normalize, const int *assign, const float *C, const float *cb, int m, int dsub, int mp,
+                      uint8_t *codes, hipStream_t st);
+void launch_pq_tables_T(const float *C, int ld, const float *cb, int nlist, int m, int dsub, float *T,
+                        hipStream_t st);
+void launch_pq_layout(const uint8_t *codes, const uint32_t *lslot, int64_t npos, int mp, uint8_t *lcodes,
+                      hipStream_t st);
+// search side
+void launch_ivf_prep(const float *Q, int nq, int dim, int ld, int normalize, float *Qf, float *Qn, hipStream_t st);
+void launch_invert(const int64_t *probe_l, int nq, int nprobe, int nlist, int *lcnt, int *pstart, int *pairs,
+                   hipStream_t st);
+void launch_flat_list_scan(const StoreView &s, const int *blk_list, const int64_t *blk_pos0, const int *lblk0,
+                           const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart, const int *pairs,
+                           int nprobe, int maxb, int64_t tail_s0, int64_t tail_n, int nq, const float *Qf, int kk,
+                           uint64_t *out, hipStream_t st);
+void launch_pq_P(const float *Q, int qld, int nq, const float *cb, int m, int dsub, float *P, hipStream_t st);
+void launch_pq_list_scan(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
+                         const float *rowaux_f, int nlist, const int *pstart, const int *pairs, int nprobe,
+                         const float *probe_d, const float *T, const float *P, int kk, uint64_t *out, hipStream_t st);
+// per query: top-K keys over the list-scan outputs of its probes (nblk_of
+// lists via lblk0, or 1 per probe when lblk0 is null) and/or a tail output.
+void launch_ivf_merge(int nq, int nprobe, const int64_t *probe_l, const int *lblk0, int maxb, int kk,
+                      const uint64_t *keys, int tail_nb, const uint64_t *tkeys, int K, uint64_t *out, hipStream_t st);
+void launch_keys_to_output(const uint64_t *keys, int nq, int K, int k, const int64_t *labels, int64_t *outL,
+                           float *outD, int *outC, hipStream_t st);
+void launch_ivf_refine_final(const StoreView &s, const float *Qf, const uint64_t *ca, int ka, const uint64_t *cb,
+                             int kb, int nq, int k, int64_t *outL, float *outD, int *outC, hipStream_t st);
+
+}  // namespace lhip

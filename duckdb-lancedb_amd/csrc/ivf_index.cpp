@@ -1,0 +1,559 @@
+// IVF_FLAT / IVF_PQ host side: training, indexing, list layout and the search
+// orchestration over the kernels of ivf_kernels.hip (contract in ivf.h).
+//
+// Reference behaviour restated (paths relative to /root/reference):
+//   rust_lib/src/lance_manager.rs:483-515  create_ann_index: IVF_PQ with the
+//       index metric (cosine / dot|ip / else L2), num_partitions and
+//       num_sub_vectors only when > 0 (LanceDB defaults otherwise), replace(true)
+//   rust_lib/src/lance_manager.rs:411-418  vector_search(q).limit(k)
+//       .nprobes(n).refine_factor(r): probe the n nearest partitions, rank by
+//       PQ distance, re-rank the top k*r exactly
+//   rust_lib/src/lance_manager.rs:557-561  compact = optimize(All): rows added
+//       after the build join the existing partitions
+//   src/lance_index.hpp:91-92              nprobes 20 / refine_factor 1 defaults
+// LanceDB-side defaults restated from lancedb 0.15 / lance-index 0.22 (not in
+// the container): num_partitions = sqrt(rows), num_sub_vectors = dim/16 (or
+// dim/8, else 1), k-means on a sample of 256 rows per centroid, <= 50
+// iterations, PQ trained on <= 256*256 residual rows, 8-bit codes.
+#include "ivf.h"
+
+#include <memory>
+#include <random>
+
+namespace lhip {
+
+IvfState::~IvfState() { delete coarse; }
+void ivf_free(IvfState *s) { delete s; }
+
+static StoreView store_view(Index *ix) {
+	return StoreView{ix->X,  ix->rowaux, ix->dlabels, ix->n_slots, ix->ld, ix->dim, ix->metric, ix->xbf16 ? 1 : 0,
+	                 ix->Xs ? static_cast<const void *>(ix->Xs) : ix->X, (ix->xbf16 || ix->Xs) ? 1 : 0};
+}
+
+static int bits_for(int64_t n) {
+	int b = 1;
+	while (((int64_t)1 << b) < n) ++b;
+	return b;
+}
+
+// grow a device buffer preserving its first `keep` elements
+template <typename T>
+static void grow_keep(DevBuf<T> &b, size_t want, size_t keep, hipStream_t st) {
+	if (want <= b.n) return;
+	T *p = nullptr;
+	HIPCHK(hipMalloc(&p, want * sizeof(T)));
+	if (keep > 0 && b.p) HIPCHK(hipMemcpyAsync(p, b.p, keep * sizeof(T), hipMemcpyDeviceToDevice, st));
+	HIPCHK(hipStreamSynchronize(st));
+	b.release();
+	b.p = p;
+	b.n = want;
+}
+
+// f32 centroids padded with zero rows to nc_pad (the f32 assignment kernel's tiles)
+static void pad_centroids(const float *C, int nc, int nc_pad, int ld, DevBuf<float> &Cf, hipStream_t st) {
+	Cf.need((size_t)nc_pad * ld);
+	HIPCHK(hipMemsetAsync(Cf.p, 0, (size_t)nc_pad * ld * sizeof(float), st));
+	HIPCHK(hipMemcpyAsync(Cf.p, C, (size_t)nc * ld * sizeof(float), hipMemcpyDeviceToDevice, st));
+}
+
+// scratch for the sort-based k-means updates
+struct SortBufs {
+	DevBuf<uint32_t> k0, v0, k1, v1;
+	DevBuf<int> seg;
+	DevBuf<uint8_t> tmp;
+	DevBuf<double> dsum;
+	void sort(int64_t n, int end_bit, hipStream_t st) {
+		size_t tb = 0;
+		HIPCHK((hipError_t)sort_u32_pairs(nullptr, tb, k0.p, k1.p, v0.p, v1.p, n, end_bit, st));
+		tmp.need(tb);
+		HIPCHK((hipError_t)sort_u32_pairs(tmp.p, tb, k0.p, k1.p, v0.p, v1.p, n, end_bit, st));
+	}
+};
+
+static double read_double(const double *d, hipStream_t st) {
+	double h = 0.0;
+	HIPCHK(hipMemcpyAsync(&h, d, sizeof(double), hipMemcpyDeviceToHost, st));
+	HIPCHK(hipStreamSynchronize(st));
+	return h;
+}
+
+// Lloyd k-means on n sample rows S (f32 + bf16 copies, stride ld): C[nc][ld]
+// initialised with the first nc sample rows (the sample is a seeded random
+// draw).  Stops after `iters` updates or when the total squared error moves by
+// less than 1e-4 relative.  Leaves the final assignment of the sample in assign.
+static void kmeans(const float *S, const uint16_t *Sb, int64_t n, int ld, int dim, int nc, int iters, float *C,
+                   int *assign, SortBufs &sb, hipStream_t st) {
+	const int nc_pad = (int)round_up(nc, 128);
+	DevBuf<uint16_t> Cb;
+	DevBuf<float> cnorm;
+	DevBuf<uint64_t> best;
+	Cb.need((size_t)nc_pad * ld);
+	cnorm.need(nc_pad);
+	best.need(n);
+	sb.k0.need(n);
+	sb.v0.need(n);
+	sb.k1.need(n);
+	sb.v1.need(n);
+	sb.seg.need((size_t)nc + 1);
+	sb.dsum.need(2);
+	HIPCHK(hipMemcpyAsync(C, S, (size_t)nc * ld * sizeof(float), hipMemcpyDeviceToDevice, st));
+	launch_sq_sum(S, n * ld, sb.dsum.p + 1, st);
+	const double sumx2 = read_double(sb.dsum.p + 1, st);
+	double prev = 0.0;
+	for (int it = 0;; ++it) {
+		launch_centroid_prep(C, nc, nc_pad, ld, Cb.p, cnorm.p, st);
+		HIPCHK(hipMemsetAsync(best.p, 0xFF, (size_t)n * sizeof(uint64_t), st));
+		launch_kmeans_assign(Sb, 1, ld, 0, n, nullptr, Cb.p, cnorm.p, nc_pad, best.p, st);
+		HIPCHK(hipGetLastError());
+		if (it >= iters) break;
+		launch_score_sum(best.p, n, sb.dsum.p, st);
+		const double loss = read_double(sb.dsum.p, st) + sumx2;  // sum |x - c|^2
+		if (it > 0 && std::fabs(prev - loss) <= 1e-4 * std::fabs(loss)) break;
+		prev = loss;
+		launch_best_to_assign(best.p, n, nullptr, sb.k0.p, sb.v0.p, st);
+		sb.sort(n, bits_for(nc), st);
+		launch_segments(sb.k1.p, n, nc, sb.seg.p, st);
+		launch_centroid_mean(S, ld, dim, sb.v1.p, sb.seg.p, nc, C, st);
+		HIPCHK(hipGetLastError());
+	}
+	// the sample's final lists (PQ residuals) with exact-f32 scores
+	DevBuf<float> Cf;
+	pad_centroids(C, nc, nc_pad, ld, Cf, st);
+	HIPCHK(hipMemsetAsync(best.p, 0xFF, (size_t)n * sizeof(uint64_t), st));
+	launch_kmeans_assign_f32(S, 0, ld, 0, n, nullptr, Cf.p, cnorm.p, nc_pad, best.p, st);
+	launch_best_to_assign(best.p, n, assign, nullptr, nullptr, st);
+	HIPCHK(hipGetLastError());
+	HIPCHK(hipStreamSynchronize(st));
+}
+
+// PQ codebook (m sub-spaces x 256 codes x dsub) by k-means on residual rows R
+static void pq_train(const float *R, int64_t n, int ld, int m, int dsub, int iters, float *cb, SortBufs &sb,
+                     hipStream_t st) {
+	// init: code c of sub-space j = residual row c's slice j
+	std::vector<float> h((size_t)PQ_K * ld), hc((size_t)m * PQ_K * dsub);
+	HIPCHK(hipMemcpyAsync(h.data(), R, h.size() * sizeof(float), hipMemcpyDeviceToHost, st));
+	HIPCHK(hipStreamSynchronize(st));
+	for (int j = 0; j < m; ++j)
+		for (int c = 0; c < PQ_K; ++c)
+			for (int t = 0; t < dsub; ++t) hc[((size_t)j * PQ_K + c) * dsub + t] = h[(size_t)c * ld + j * dsub + t];
+	HIPCHK(hipMemcpyAsync(cb, hc.data(), hc.size() * sizeof(float), hipMemcpyHostToDevice, st));
+	const int64_t tot = n * m;
+	sb.k0.need(tot);
+	sb.v0.need(tot);
+	sb.k1.need(tot);
+	sb.v1.need(tot);
+	sb.seg.need((size_t)m * PQ_K + 1);
+	for (int it = 0; it < iters; ++it) {
+		launch_pq_assign(R, ld, n, m, dsub, cb, sb.k0.p, sb.v0.p, st);
+		sb.sort(tot, bits_for((int64_t)m * PQ_K), st);
+		launch_segments(sb.k1.p, tot, m * PQ_K, sb.seg.p, st);
+		launch_pq_mean(R, ld, sb.v1.p, sb.seg.p, m, dsub, cb, st);
+		HIPCHK(hipGetLastError());
+	}
+	HIPCHK(hipStreamSynchronize(st));
+}
+
+// assign (and PQ-encode) slots [n_indexed, n_slots) with the installed model
+static void index_tail(Index *ix) {
+	IvfState *s = ix->ivf;
+	const int64_t n0 = s->n_indexed, n1 = ix->n_slots;
+	if (n1 <= n0) return;
+	hipStream_t st = ix->stream;
+	const int nc_pad = (int)round_up(s->nlist, 128);
+	DevBuf<uint16_t> Cb;
+	DevBuf<float> cnorm, Cf;
+	Cb.need((size_t)nc_pad * ix->ld);
+	cnorm.need(nc_pad);
+	launch_centroid_prep(s->centroids.p, s->nlist, nc_pad, ix->ld, Cb.p, cnorm.p, st);
+	pad_centroids(s->centroids.p, s->nlist, nc_pad, ix->ld, Cf, st);
+	grow_keep(s->assign, (size_t)std::max<int64_t>(n1, 1), (size_t)n0, st);
+	const bool cos = s->metric == METRIC_COSINE;
+	const float *ra = reinterpret_cast<const float *>(ix->rowaux);
+	// rows go to their nearest centroid by exact-f32 scores, read from the stored rows
+	const void *Xa = ix->X;
+	const int xab = ix->xbf16 ? 1 : 0;
+	// bounded chunks of rows keep the arg-min scratch small
+	const int64_t chunk = 1 << 22;
+	s->best.need((size_t)std::min<int64_t>(chunk, n1 - n0));
+	for (int64_t a = n0; a < n1; a += chunk) {
+		const int64_t n = std::min<int64_t>(chunk, n1 - a);
+		HIPCHK(hipMemsetAsync(s->best.p, 0xFF, (size_t)n * sizeof(uint64_t), st));
+		launch_kmeans_assign_f32(Xa, xab, ix->ld, a, n, cos ? ra : nullptr, Cf.p, cnorm.p, nc_pad, s->best.p, st);
+		launch_best_to_assign(s->best.p, n, s->assign.p + a, nullptr, nullptr, st);
+		HIPCHK(hipGetLastError());
+	}
+	if (s->type == IVF_PQ) {
+		grow_keep(s->codes, (size_t)std::max<int64_t>(n1, 1) * s->mp, (size_t)n0 * s->mp, st);
+		HIPCHK(hipMemsetAsync(s->codes.p + (size_t)n0 * s->mp, 0, (size_t)(n1 - n0) * s->mp, st));
+		launch_pq_encode(ix->X, ix->xbf16 ? 1 : 0, ix->ld, ix->dim, n0, n1 - n0, ra, cos ? 1 : 0, s->assign.p,
+		                 s->centroids.p, s->codebook.p, s->m, s->dsub, s->mp, s->codes.p, st);
+		HIPCHK(hipGetLastError());
+	}
+	HIPCHK(hipStreamSynchronize(st));
+	s->n_indexed = n1;
+	s->dirty = true;
+}
+
+// install a model given as device buffers (centroids [nlist][ld], codebook)
+static void install_model(Index *ix, int type, int nlist, int m, const float *dC, const float *dcb) {
+	hipStream_t st = ix->stream;
+	auto s = std::make_unique<IvfState>();
+	s->type = type;
+	s->nlist = nlist;
+	s->metric = ix->metric;
+	if (type == IVF_PQ) {
+		s->m = m;
+		s->dsub = ix->dim / m;
+		s->mp = (int)round_up(m, 16);
+	}
+	s->centroids.need((size_t)nlist * ix->ld);
+	HIPCHK(hipMemcpyAsync(s->centroids.p, dC, (size_t)nlist * ix->ld * sizeof(float), hipMemcpyDeviceToDevice, st));
+	if (type == IVF_PQ) {
+		const size_t ncb = (size_t)m * PQ_K * s->dsub;
+		s->codebook.need(ncb);
+		HIPCHK(hipMemcpyAsync(s->codebook.p, dcb, ncb * sizeof(float), hipMemcpyDeviceToDevice, st));
+		if (s->metric != METRIC_DOT) {
+			s->T.need((size_t)nlist * m * PQ_K);
+			launch_pq_tables_T(s->centroids.p, ix->ld, s->codebook.p, nlist, m, s->dsub, s->T.p, st);
+			HIPCHK(hipGetLastError());
+		}
+	}
+	// the centroid store: the exact flat path ranks the partitions (dot for a
+	// dot index, L2 otherwise; cosine probes with normalised queries)
+	auto co = std::make_unique<Index>();
+	co->table = "ivf_centroids";
+	co->metric = s->metric == METRIC_DOT ? METRIC_DOT : METRIC_L2;
+	co->dim = ix->dim;
+	co->ld = ix->ld;
+	co->init_device(ix->device);
+	{
+		DevBuf<float> packed;
+		packed.need((size_t)nlist * ix->dim);
+		HIPCHK(hipMemcpy2DAsync(packed.p, (size_t)ix->dim * sizeof(float), s->centroids.p, (size_t)ix->ld * sizeof(float),
+		                        (size_t)ix->dim * sizeof(float), (size_t)nlist, hipMemcpyDeviceToDevice, st));
+		HIPCHK(hipStreamSynchronize(st));
+		co->add_device(packed.p, nlist);
+	}
+	ix->bind();
+	s->coarse = co.release();
+	ivf_free(ix->ivf);
+	ix->ivf = s.release();
+	index_tail(ix);
+}
+
+static void check_params(Index *ix, int type, int nlist, int m) {
+	if (nlist <= 0) throw Error("num_partitions must be positive");
+	if (type == IVF_PQ) {
+		if (m <= 0 || ix->dim % m != 0)
+			throw Error("num_sub_vectors (" + std::to_string(m) + ") must divide the dimension " +
+			            std::to_string(ix->dim));
+		if (m > PQ_MAX_M) throw Error("num_sub_vectors > " + std::to_string(PQ_MAX_M) + " is not supported");
+		if (ix->dim / m > PQ_MAX_DSUB)
+			throw Error("sub-vectors longer than " + std::to_string(PQ_MAX_DSUB) +
+			            " dims are not supported; raise num_sub_vectors");
+	}
+}
+
+void ivf_build(Index *ix, int type, int num_partitions, int num_sub_vectors) {
+	if (ix->n_live <= 0) throw Error("cannot build an index on an empty table");
+	const int dim = ix->dim, ld = ix->ld;
+	const int nlist = num_partitions > 0 ? num_partitions : std::max(1, (int)std::sqrt((double)ix->n_live));
+	const int m = num_sub_vectors > 0 ? num_sub_vectors : (dim % 16 == 0 ? dim / 16 : dim % 8 == 0 ? dim / 8 : 1);
+	check_params(ix, type, nlist, m);
+	if (nlist > ix->n_live)
+		throw Error("KMeans: cannot train " + std::to_string(nlist) + " centroids with " +
+		            std::to_string(ix->n_live) + " vectors");
+	if (type == IVF_PQ && ix->n_live < PQ_K)
+		throw Error("PQ training needs at least 256 rows, the table has " + std::to_string(ix->n_live));
+	hipStream_t st = ix->stream;
+	// seeded uniform sample of the live rows (partial Fisher-Yates)
+	std::vector<int64_t> live_slots;
+	live_slots.reserve((size_t)ix->n_live);
+	for (int64_t s = 0; s < ix->n_slots; ++s)
+		if (ix->live[(size_t)s]) live_slots.push_back(s);
+	const int64_t nS = std::min<int64_t>((int64_t)live_slots.size(), (int64_t)nlist * 256);
+	std::mt19937_64 rng(ix->ivf_seed);
+	for (int64_t i = 0; i < nS; ++i) {
+		std::uniform_int_distribution<int64_t> u(i, (int64_t)live_slots.size() - 1);
+		std::swap(live_slots[(size_t)i], live_slots[(size_t)u(rng)]);
+	}
+	const bool cos = ix->metric == METRIC_COSINE;
+	DevBuf<int64_t> dslots;
+	DevBuf<float> S, C, R, cb;
+	DevBuf<uint16_t> Sb;
+	DevBuf<int> sassign;
+	dslots.need((size_t)nS);
+	S.need((size_t)nS * ld);
+	Sb.need((size_t)nS * ld);
+	C.need((size_t)nlist * ld);
+	sassign.need((size_t)nS);
+	HIPCHK(hipMemcpyAsync(dslots.p, live_slots.data(), (size_t)nS * sizeof(int64_t), hipMemcpyHostToDevice, st));
+	launch_gather_sample(ix->X, ix->xbf16 ? 1 : 0, ld, dim, dslots.p, nS, cos ? 1 : 0, S.p, Sb.p, st);
+	HIPCHK(hipGetLastError());
+	SortBufs sb;
+	kmeans(S.p, Sb.p, nS, ld, dim, nlist, ix->kmeans_iters, C.p, sassign.p, sb, st);
+	if (type == IVF_PQ) {
+		const int64_t nR = std::min<int64_t>(nS, (int64_t)PQ_K * PQ_K);
+		R.need((size_t)nR * ld);
+		launch_residuals(S.p, sassign.p, C.p, ld, nR, R.p, st);
+		cb.need((size_t)m * PQ_K * (dim / m));
+		pq_train(R.p, nR, ld, m, dim / m, ix->kmeans_iters, cb.p, sb, st);
+	}
+	HIPCHK(hipStreamSynchronize(st));
+	install_model(ix, type, nlist, m, C.p, type == IVF_PQ ? cb.p : nullptr);
+}
+
+void ivf_set_model(Index *ix, int type, int nlist, int m, const float *centroids, const float *codebook) {
+	check_params(ix, type, nlist, m);
+	if (type == IVF_PQ && !codebook) throw Error("IVF_PQ model needs a codebook");
+	hipStream_t st = ix->stream;
+	DevBuf<float> C, cb;
+	C.need((size_t)nlist * ix->ld);
+	HIPCHK(hipMemsetAsync(C.p, 0, (size_t)nlist * ix->ld * sizeof(float), st));
+	HIPCHK(hipMemcpy2DAsync(C.p, (size_t)ix->ld * sizeof(float), centroids, (size_t)ix->dim * sizeof(float),
+	                        (size_t)ix->dim * sizeof(float), (size_t)nlist, hipMemcpyHostToDevice, st));
+	if (type == IVF_PQ) {
+		const size_t ncb = (size_t)m * PQ_K * (ix->dim / m);
+		cb.need(ncb);
+		HIPCHK(hipMemcpyAsync(cb.p, codebook, ncb * sizeof(float), hipMemcpyHostToDevice, st));
+	}
+	HIPCHK(hipStreamSynchronize(st));
+	install_model(ix, type, nlist, m, C.p, type == IVF_PQ ? cb.p : nullptr);
+}
+
+void ivf_optimize(Index *ix) {
+	if (ix->ivf) index_tail(ix);
+}
+
+void ivf_remap(Index *ix, const std::vector<int64_t> &keep) {
+	IvfState *s = ix->ivf;
+	hipStream_t st = ix->stream;
+	const int64_t nk = std::lower_bound(keep.begin(), keep.end(), s->n_indexed) - keep.begin();
+	DevBuf<int64_t> idx;
+	idx.need((size_t)std::max<int64_t>(nk, 1));
+	HIPCHK(hipMemcpyAsync(idx.p, keep.data(), (size_t)nk * sizeof(int64_t), hipMemcpyHostToDevice, st));
+	{
+		std::vector<int> h((size_t)s->n_indexed), o((size_t)nk);
+		HIPCHK(hipMemcpyAsync(h.data(), s->assign.p, h.size() * sizeof(int), hipMemcpyDeviceToHost, st));
+		HIPCHK(hipStreamSynchronize(st));
+		for (int64_t i = 0; i < nk; ++i) o[(size_t)i] = h[(size_t)keep[(size_t)i]];
+		DevBuf<int> na;
+		na.need((size_t)std::max<int64_t>(nk, 1));
+		HIPCHK(hipMemcpyAsync(na.p, o.data(), (size_t)nk * sizeof(int), hipMemcpyHostToDevice, st));
+		HIPCHK(hipStreamSynchronize(st));
+		std::swap(s->assign.p, na.p);
+		std::swap(s->assign.n, na.n);
+	}
+	if (s->type == IVF_PQ) {
+		DevBuf<uint8_t> nc;
+		nc.need((size_t)std::max<int64_t>(nk, 1) * s->mp);
+		launch_gather_bytes(s->codes.p, idx.p, nk, s->mp, nc.p, st);
+		HIPCHK(hipGetLastError());
+		HIPCHK(hipStreamSynchronize(st));
+		std::swap(s->codes.p, nc.p);
+		std::swap(s->codes.n, nc.n);
+	}
+	s->n_indexed = nk;
+	s->dirty = true;
+}
+
+// list layout: positions grouped by list (ascending slot inside a list), each
+// list padded to a multiple of 64 positions; IVF_FLAT work items of 256
+// positions; IVF_PQ codes in the blocked order the list scan streams
+static void layout(Index *ix) {
+	IvfState *s = ix->ivf;
+	hipStream_t st = ix->stream;
+	const int nl = s->nlist;
+	std::vector<int> a((size_t)s->n_indexed);
+	if (s->n_indexed > 0)
+		HIPCHK(hipMemcpyAsync(a.data(), s->assign.p, a.size() * sizeof(int), hipMemcpyDeviceToHost, st));
+	HIPCHK(hipStreamSynchronize(st));
+	std::vector<int64_t> cnt((size_t)nl, 0);
+	for (int l : a) cnt[(size_t)l] += 1;
+	s->h_loff.assign((size_t)nl + 1, 0);
+	for (int l = 0; l < nl; ++l) s->h_loff[(size_t)l + 1] = s->h_loff[(size_t)l] + round_up(cnt[(size_t)l], 64);
+	const int64_t npos = s->h_loff[(size_t)nl];
+	std::vector<uint32_t> ls((size_t)std::max<int64_t>(npos, 1), SLOT_NONE);
+	std::vector<int64_t> cur(s->h_loff.begin(), s->h_loff.end() - 1);
+	for (int64_t sl = 0; sl < s->n_indexed; ++sl) ls[(size_t)cur[(size_t)a[(size_t)sl]]++] = (uint32_t)sl;
+	s->loff.need((size_t)nl + 1);
+	s->lslot.need(ls.size());
+	HIPCHK(hipMemcpyAsync(s->loff.p, s->h_loff.data(), ((size_t)nl + 1) * sizeof(int64_t), hipMemcpyHostToDevice, st));
+	HIPCHK(hipMemcpyAsync(s->lslot.p, ls.data(), ls.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+	if (s->type == IVF_FLAT) {
+		std::vector<int> bl, l0((size_t)nl + 1);
+		std::vector<int64_t> bp;
+		int maxb = 1;
+		for (int l = 0; l < nl; ++l) {
+			l0[(size_t)l] = (int)bl.size();
+			const int64_t len = s->h_loff[(size_t)l + 1] - s->h_loff[(size_t)l];
+			const int nb = (int)((len + FLAT_BLK - 1) / FLAT_BLK);
+			maxb = std::max(maxb, nb);
+			for (int b = 0; b < nb; ++b) {
+				bl.push_back(l);
+				bp.push_back(s->h_loff[(size_t)l] + (int64_t)b * FLAT_BLK);
+			}
+		}
+		l0[(size_t)nl] = (int)bl.size();
+		s->nblk = (int)bl.size();
+		s->maxb = maxb;
+		s->blk_list.need(std::max<size_t>(bl.size(), 1));
+		s->blk_pos0.need(std::max<size_t>(bp.size(), 1));
+		s->lblk0.need(l0.size());
+		if (!bl.empty()) {
+			HIPCHK(hipMemcpyAsync(s->blk_list.p, bl.data(), bl.size() * sizeof(int), hipMemcpyHostToDevice, st));
+			HIPCHK(hipMemcpyAsync(s->blk_pos0.p, bp.data(), bp.size() * sizeof(int64_t), hipMemcpyHostToDevice, st));
+		}
+		HIPCHK(hipMemcpyAsync(s->lblk0.p, l0.data(), l0.size() * sizeof(int), hipMemcpyHostToDevice, st));
+	} else {
+		s->lcodes.need((size_t)std::max<int64_t>(npos, 64) * s->mp);
+		launch_pq_layout(s->codes.p, s->lslot.p, npos, s->mp, s->lcodes.p, st);
+		HIPCHK(hipGetLastError());
+	}
+	HIPCHK(hipStreamSynchronize(st));
+	s->dirty = false;
+}
+
+void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refine, int64_t *dL, float *dD, int *dC) {
+	IvfState *s = ix->ivf;
+	hipStream_t st = ix->stream;
+	if (s->dirty) layout(ix);
+	if (k > IVF_MAX_K) throw Error("k > " + std::to_string(IVF_MAX_K) + " is not supported by the IVF path");
+	const int nprobe = std::min(s->nlist, nprobes > 0 ? nprobes : 20);  // lance_index.hpp:91 default
+	const int rf = std::max(refine, 1);
+	const int kp = (int)std::min<int64_t>((int64_t)k * rf, IVF_MAX_K);
+	const int kk = std::min(k, FLAT_BLK);
+	const int64_t tail_n = ix->n_slots - s->n_indexed;
+	const int tail_nb = (int)((tail_n + FLAT_BLK - 1) / FLAT_BLK);
+	const bool cos = s->metric == METRIC_COSINE;
+	const int ld = ix->ld, dim = ix->dim;
+	StoreView sv = store_view(ix);
+	// queries per pass: bounded by MAX_PASS_Q and ~1 GiB of list-scan keys
+	const int64_t per_q = s->type == IVF_FLAT ? (int64_t)nprobe * s->maxb * kk + (int64_t)tail_nb * kk
+	                                          : (int64_t)nprobe * kp + (int64_t)tail_nb * kk;
+	const int pass = (int)std::max<int64_t>(1, std::min<int64_t>(MAX_PASS_Q, (int64_t)(1 << 27) / std::max<int64_t>(per_q, 1)));
+	for (int q0 = 0; q0 < nq; q0 += pass) {
+		const int n = std::min(pass, nq - q0);
+		s->Qf.need((size_t)n * ld);
+		if (cos) s->Qn.need((size_t)n * dim);
+		launch_ivf_prep(dQ + (int64_t)q0 * dim, n, dim, ld, cos ? 1 : 0, s->Qf.p, cos ? s->Qn.p : nullptr, st);
+		HIPCHK(hipGetLastError());
+		HIPCHK(hipStreamSynchronize(st));
+		// coarse: exact top-nprobe partitions (synchronous on the centroid store's stream)
+		s->probe_l.need((size_t)n * nprobe);
+		s->probe_d.need((size_t)n * nprobe);
+		s->probe_c.need((size_t)n);
+		s->coarse->search_device(cos ? s->Qn.p : dQ + (int64_t)q0 * dim, n, nprobe, 1, s->probe_l.p, s->probe_d.p,
+		                         s->probe_c.p);
+		ix->bind();
+		s->lcnt.need((size_t)s->nlist);
+		s->pstart.need((size_t)s->nlist + 1);
+		s->pairs.need((size_t)n * nprobe);
+		launch_invert(s->probe_l.p, n, nprobe, s->nlist, s->lcnt.p, s->pstart.p, s->pairs.p, st);
+		int64_t *oL = dL + (int64_t)q0 * k;
+		float *oD = dD + (int64_t)q0 * k;
+		int *oC = dC + q0;
+		if (tail_n > 0) {
+			s->tkeys.need((size_t)n * tail_nb * kk);
+			launch_flat_list_scan(sv, nullptr, nullptr, nullptr, nullptr, nullptr, tail_nb, nullptr, nullptr, 1, 1,
+			                      s->n_indexed, tail_n, n, s->Qf.p, kk, s->tkeys.p, st);
+		}
+		if (s->type == IVF_FLAT) {
+			s->keys.need((size_t)n * nprobe * s->maxb * kk);
+			launch_flat_list_scan(sv, s->blk_list.p, s->blk_pos0.p, s->lblk0.p, s->loff.p, s->lslot.p, s->nblk,
+			                      s->pstart.p, s->pairs.p, nprobe, s->maxb, 0, 0, n, s->Qf.p, kk, s->keys.p, st);
+			s->cand_a.need((size_t)n * k);
+			launch_ivf_merge(n, nprobe, s->probe_l.p, s->lblk0.p, s->maxb, kk, s->keys.p, tail_nb,
+			                 tail_n > 0 ? s->tkeys.p : nullptr, k, s->cand_a.p, st);
+			launch_keys_to_output(s->cand_a.p, n, k, k, ix->dlabels, oL, oD, oC, st);
+		} else {
+			s->P.need((size_t)n * s->m * PQ_K);
+			launch_pq_P(cos ? s->Qn.p : s->Qf.p, cos ? dim : ld, n, s->codebook.p, s->m, s->dsub, s->P.p, st);
+			s->keys.need((size_t)n * nprobe * kp);
+			launch_pq_list_scan(s->lcodes.p, s->m, s->mp, s->loff.p, s->lslot.p,
+			                    reinterpret_cast<const float *>(ix->rowaux), s->nlist, s->pstart.p, s->pairs.p, nprobe,
+			                    s->probe_d.p, s->metric == METRIC_DOT ? nullptr : s->T.p, s->P.p, kp, s->keys.p, st);
+			s->cand_a.need((size_t)n * kp);
+			launch_ivf_merge(n, nprobe, s->probe_l.p, nullptr, 1, kp, s->keys.p, 0, nullptr, kp, s->cand_a.p, st);
+			if (tail_n > 0) {
+				s->cand_b.need((size_t)n * k);
+				launch_ivf_merge(n, 0, nullptr, nullptr, 1, kk, nullptr, tail_nb, s->tkeys.p, k, s->cand_b.p, st);
+			}
+			launch_ivf_refine_final(sv, s->Qf.p, s->cand_a.p, kp, tail_n > 0 ? s->cand_b.p : nullptr,
+			                        tail_n > 0 ? k : 0, n, k, oL, oD, oC, st);
+		}
+		HIPCHK(hipGetLastError());
+		spin_sync(st);
+	}
+}
+
+}  // namespace lhip
+
+namespace lhip {
+
+void Index::search_any(const float *dQ, int nq, int k, int nprobes, int refine, int64_t *dL, float *dD, int *dC) {
+	if (ivf)
+		ivf_search(this, dQ, nq, k, nprobes, refine, dL, dD, dC);
+	else
+		search_device(dQ, nq, k, refine, dL, dD, dC);
+}
+
+// model export as host arrays: centroids [nlist][dim], codebook [m][256][dsub]
+static void model_host(Index *ix, std::vector<float> &C, std::vector<float> &cb) {
+	IvfState *s = ix->ivf;
+	C.resize((size_t)s->nlist * ix->dim);
+	HIPCHK(hipMemcpy2D(C.data(), (size_t)ix->dim * sizeof(float), s->centroids.p, (size_t)ix->ld * sizeof(float),
+	                   (size_t)ix->dim * sizeof(float), (size_t)s->nlist, hipMemcpyDeviceToHost));
+	cb.clear();
+	if (s->type == IVF_PQ) {
+		cb.resize((size_t)s->m * PQ_K * s->dsub);
+		HIPCHK(hipMemcpy(cb.data(), s->codebook.p, cb.size() * sizeof(float), hipMemcpyDeviceToHost));
+	}
+}
+
+void ivf_export_model(Index *ix, float *centroids, float *codebook) {
+	std::vector<float> C, cb;
+	model_host(ix, C, cb);
+	if (centroids) memcpy(centroids, C.data(), C.size() * sizeof(float));
+	if (codebook && !cb.empty()) memcpy(codebook, cb.data(), cb.size() * sizeof(float));
+}
+
+void ivf_export_slots(Index *ix, int32_t *slot_list, uint8_t *slot_codes) {
+	IvfState *s = ix->ivf;
+	const int64_t n = ix->n_slots, ni = s->n_indexed;
+	if (slot_list) {
+		std::vector<int> a((size_t)ni);
+		if (ni > 0) HIPCHK(hipMemcpy(a.data(), s->assign.p, (size_t)ni * sizeof(int), hipMemcpyDeviceToHost));
+		for (int64_t i = 0; i < n; ++i) slot_list[i] = i < ni ? a[(size_t)i] : -1;
+	}
+	if (slot_codes) {
+		memset(slot_codes, 0, (size_t)n * (s->type == IVF_PQ ? s->m : 0));
+		if (s->type == IVF_PQ && ni > 0) {
+			std::vector<uint8_t> c((size_t)ni * s->mp);
+			HIPCHK(hipMemcpy(c.data(), s->codes.p, c.size(), hipMemcpyDeviceToHost));
+			for (int64_t i = 0; i < ni; ++i) memcpy(slot_codes + i * s->m, c.data() + i * s->mp, (size_t)s->m);
+		}
+	}
+}
+
+void Index::log_model() {
+	if (!log || !ivf) return;
+	std::vector<float> C, cb;
+	model_host(this, C, cb);
+	uint8_t tag = 4;
+	int32_t hdr[3] = {ivf->type, ivf->nlist, ivf->m};
+	fwrite(&tag, 1, 1, log);
+	fwrite(hdr, 4, 3, log);
+	fwrite(C.data(), sizeof(float), C.size(), log);
+	if (!cb.empty()) fwrite(cb.data(), sizeof(float), cb.size(), log);
+	fflush(log);
+}
+
+void Index::log_optimize() {
+	if (!log) return;
+	uint8_t tag = 5;
+	fwrite(&tag, 1, 1, log);
+	fflush(log);
+}
+
+}  // namespace lhip

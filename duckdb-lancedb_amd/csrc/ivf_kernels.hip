@@ -1,0 +1,1171 @@
+// gfx950 kernels of the IVF_FLAT / IVF_PQ path (ivf.h has the numerics contract).
+//
+// Replaces lance-index 0.22's IVF_PQ training and search (behind
+// rust_lib/src/lance_manager.rs:483-515 / :411-418, paths relative to
+// /root/reference):
+//   build   gather_sample -> kmeans_assign (bf16 MFMA |c|^2 - 2x.c, fused
+//           arg-min) -> sort-based deterministic centroid means; residual PQ
+//           k-means per sub-space (codebook slice in LDS); encode; T tables
+//   search  prep -> coarse (the exact flat path over the centroid store) ->
+//           invert probes into per-list query sets -> list scans:
+//             IVF_FLAT  256-row work items, rows staged through LDS, f64
+//                       exact distances for every query of the list, bitonic
+//                       top-k per (query, item)
+//             IVF_PQ    one workgroup per list, the (query, list) ADC LUT
+//                       (m x 256 f32) resident in LDS, codes streamed in a
+//                       64-row blocked layout (1 KiB per wave load), LDS
+//                       threshold top-k per (query, list)
+//           -> per-query merge -> exact re-rank (PQ) -> (distance, label) top-k
+#include "ivf.h"
+#include "device_common.h"
+
+#include <rocprim/device/device_radix_sort.hpp>
+
+namespace lhip {
+
+static constexpr uint64_t KEY64_NONE = ~0ull;
+
+__device__ __forceinline__ uint64_t key64(float d, uint32_t slot) { return ((uint64_t)fkey(d) << 32) | slot; }
+__device__ __forceinline__ float key64_dist(uint64_t k) { return fkey_inv((uint32_t)(k >> 32)); }
+// tombstones and padding rows carry alpha = +inf in the row aux
+__device__ __forceinline__ bool slot_alive(const float *rowaux_f, uint32_t slot) {
+	return rowaux_f[raix(slot, 0)] != F_INF;
+}
+
+// ---------------------------------------------------------------------------
+// workgroup-wide helpers (LDS)
+// ---------------------------------------------------------------------------
+// Bitonic sort of a[0..n), n a power of two, ascending.  All threads call it.
+__device__ void wg_bitonic_sort(uint64_t *a, int n) {
+	for (int size = 2; size <= n; size <<= 1) {
+		for (int stride = size >> 1; stride > 0; stride >>= 1) {
+			__syncthreads();
+			for (int i = threadIdx.x; i < (n >> 1); i += blockDim.x) {
+				const int lo = 2 * i - (i & (stride - 1));
+				const int hi = lo + stride;
+				const bool asc = (lo & size) == 0;
+				const uint64_t x = a[lo], y = a[hi];
+				if ((x > y) == asc) {
+					a[lo] = y;
+					a[hi] = x;
+				}
+			}
+		}
+	}
+	__syncthreads();
+}
+
+__device__ __forceinline__ int pow2_ceil(int v) {
+	int p = 2;
+	while (p < v) p <<= 1;
+	return p;
+}
+
+// Streaming top-K of 64-bit keys in LDS: every round each thread offers at
+// most one key; keys below the threshold are appended; when the buffer could
+// overflow in the next round it is sorted and cut to K (threshold = K-th key).
+struct TopK {
+	uint64_t *buf;
+	int *cnt;
+	uint64_t *thr;
+	int K;
+	__device__ void reset() {
+		if (threadIdx.x == 0) {
+			*cnt = 0;
+			*thr = KEY64_NONE;
+		}
+		__syncthreads();
+	}
+	__device__ void compact() {
+		__syncthreads();
+		const int c = *cnt;
+		const int n = pow2_ceil(c);
+		for (int i = c + threadIdx.x; i < n; i += blockDim.x) buf[i] = KEY64_NONE;
+		wg_bitonic_sort(buf, n);
+		if (threadIdx.x == 0) {
+			if (c >= K) {
+				*thr = buf[K - 1];
+				*cnt = K;
+			}
+		}
+		__syncthreads();
+	}
+	// all threads call; valid per thread
+	__device__ void offer(uint64_t key, bool valid) {
+		if (valid && key < *thr) {
+			const int p = atomicAdd(cnt, 1);
+			buf[p] = key;
+		}
+		__syncthreads();
+		if (*cnt > IVF_TOPK_CAP - (int)blockDim.x) compact();
+	}
+	// sorted result in buf[0 .. min(cnt, K))
+	__device__ int finish() {
+		compact();
+		const int c = *cnt;
+		return c < K ? c : K;
+	}
+};
+
+__device__ __forceinline__ float4 load4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ float4 load4(const uint16_t *p) {
+	const uint2 u = *reinterpret_cast<const uint2 *>(p);
+	return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xFFFF0000u), __uint_as_float(u.y << 16),
+	                   __uint_as_float(u.y & 0xFFFF0000u));
+}
+
+// ---------------------------------------------------------------------------
+// build: sample gather, centroid prep
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void gather_sample_kernel(const T *__restrict__ X, int ld, int dim,
+                                                            const int64_t *__restrict__ slots, int64_t n,
+                                                            int normalize, float *__restrict__ out,
+                                                            uint16_t *__restrict__ outb) {
+	const int lane = threadIdx.x & 63;
+	const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+	if (r >= n) return;
+	const T *x = X + slots[r] * (int64_t)ld;
+	float inv = 1.0f;
+	if (normalize) {
+		double ss = 0.0;
+		for (int i = lane; i < dim; i += 64) {
+			const double v = xval(x, i);
+			ss += v * v;
+		}
+		ss = wave_sum_f64(ss);
+		inv = ss > 0.0 ? (float)(1.0 / sqrt(ss)) : 0.0f;
+	}
+	for (int i = lane; i < ld; i += 64) {
+		const float v = i < dim ? xval(x, i) * inv : 0.0f;
+		out[r * ld + i] = v;
+		outb[r * ld + i] = bf16_bits(v);
+	}
+}
+
+void launch_gather_sample(const void *X, int xbf16, int ld, int dim, const int64_t *slots, int64_t n, int normalize,
+                          float *out_f32, uint16_t *out_bf16, hipStream_t st) {
+	dim3 grid((unsigned)((n + 3) / 4));
+	if (xbf16)
+		gather_sample_kernel<uint16_t><<<grid, 256, 0, st>>>(static_cast<const uint16_t *>(X), ld, dim, slots, n,
+		                                                      normalize, out_f32, out_bf16);
+	else
+		gather_sample_kernel<float><<<grid, 256, 0, st>>>(static_cast<const float *>(X), ld, dim, slots, n, normalize,
+		                                                   out_f32, out_bf16);
+}
+
+__global__ __launch_bounds__(256) void centroid_prep_kernel(const float *__restrict__ C, int nc, int nc_pad, int ld,
+                                                            uint16_t *__restrict__ Cb, float *__restrict__ cnorm) {
+	const int lane = threadIdx.x & 63;
+	const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+	if (c >= nc_pad) return;
+	double ss = 0.0;
+	for (int i = lane; i < ld; i += 64) {
+		const float v = c < nc ? C[(int64_t)c * ld + i] : 0.0f;
+		Cb[(int64_t)c * ld + i] = bf16_bits(v);
+		ss += (double)v * v;
+	}
+	ss = wave_sum_f64(ss);
+	if (lane == 0) cnorm[c] = c < nc ? (float)ss : F_INF;
+}
+
+void launch_centroid_prep(const float *C, int nc, int nc_pad, int ld, uint16_t *Cb, float *cnorm, hipStream_t st) {
+	centroid_prep_kernel<<<dim3((unsigned)((nc_pad + 3) / 4)), 256, 0, st>>>(C, nc, nc_pad, ld, Cb, cnorm);
+}
+
+// ---------------------------------------------------------------------------
+// k-means assignment: bf16 MFMA (v_mfma_f32_32x32x16_bf16) centroid x row
+// tiles of 128 x 128, K staged 32 at a time through padded LDS (80-B rows:
+// the 16-lane groups of ds_read_b128 hit 16 distinct 16-B bank slots).
+// A = centroids (MFMA rows), B = data rows (MFMA columns): a lane's 16
+// accumulator registers are 16 centroids of ONE data row, so the arg-min is
+// register-local plus one lane swap, then one 64-bit atomicMin per row.
+// ---------------------------------------------------------------------------
+constexpr int KM_T = 128;       // tile edge
+constexpr int KM_K = 32;        // k per stage
+constexpr int KM_ROWB = 80;     // LDS bytes per tile row (64 + 16 pad)
+
+template <typename T>
+__device__ __forceinline__ void km_load_rows(const T *__restrict__ X, int ld, int64_t r0, int64_t n, int k0,
+                                             uint4 (&reg)[4]);
+template <>
+__device__ __forceinline__ void km_load_rows<uint16_t>(const uint16_t *__restrict__ X, int ld, int64_t r0, int64_t n,
+                                                       int k0, uint4 (&reg)[4]) {
+#pragma unroll
+	for (int i = 0; i < 2; ++i) {
+		const int e = threadIdx.x + i * 256, row = e >> 2, seg = e & 3;
+		const int64_t r = r0 + row;
+		reg[i] = r < n ? *reinterpret_cast<const uint4 *>(X + r * ld + k0 + seg * 8) : make_uint4(0, 0, 0, 0);
+	}
+}
+template <>
+__device__ __forceinline__ void km_load_rows<float>(const float *__restrict__ X, int ld, int64_t r0, int64_t n, int k0,
+                                                    uint4 (&reg)[4]) {
+#pragma unroll
+	for (int i = 0; i < 4; ++i) {
+		const int e = threadIdx.x + i * 256, row = e >> 3, seg = e & 7;
+		const int64_t r = r0 + row;
+		float4 v = r < n ? *reinterpret_cast<const float4 *>(X + r * ld + k0 + seg * 4) : make_float4(0, 0, 0, 0);
+		reg[i] = make_uint4(pk_bf16(v.x, v.y), pk_bf16(v.z, v.w), 0, 0);
+	}
+}
+template <typename T>
+__device__ __forceinline__ void km_store_rows(uint8_t *Bs, const uint4 (&reg)[4]);
+template <>
+__device__ __forceinline__ void km_store_rows<uint16_t>(uint8_t *Bs, const uint4 (&reg)[4]) {
+#pragma unroll
+	for (int i = 0; i < 2; ++i) {
+		const int e = threadIdx.x + i * 256, row = e >> 2, seg = e & 3;
+		*reinterpret_cast<uint4 *>(Bs + row * KM_ROWB + seg * 16) = reg[i];
+	}
+}
+template <>
+__device__ __forceinline__ void km_store_rows<float>(uint8_t *Bs, const uint4 (&reg)[4]) {
+#pragma unroll
+	for (int i = 0; i < 4; ++i) {
+		const int e = threadIdx.x + i * 256, row = e >> 3, seg = e & 7;
+		*reinterpret_cast<uint2 *>(Bs + row * KM_ROWB + seg * 8) = make_uint2(reg[i].x, reg[i].y);
+	}
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void kmeans_assign_kernel(const T *__restrict__ X, int ld, int64_t r0, int64_t n,
+                                                            const float *__restrict__ row_scale_aux,
+                                                            const uint16_t *__restrict__ Cb,
+                                                            const float *__restrict__ cnorm,
+                                                            uint64_t *__restrict__ best) {
+	__shared__ __attribute__((aligned(16))) uint8_t As[2][KM_T * KM_ROWB];
+	__shared__ __attribute__((aligned(16))) uint8_t Bs[2][KM_T * KM_ROWB];
+	const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+	const int64_t rt0 = (int64_t)blockIdx.x * KM_T;  // first data row of the tile (relative)
+	const int c0 = blockIdx.y * KM_T;
+	const int cw = (w & 1) * 64, rw = (w >> 1) * 64;
+	const T *Xb = X + r0 * (int64_t)ld;
+	const int64_t nrel = n;
+	const int nst = ld / KM_K;
+
+	uint4 ra[2], rb[4];
+	auto load_a = [&](int k0) {
+#pragma unroll
+		for (int i = 0; i < 2; ++i) {
+			const int e = t + i * 256, row = e >> 2, seg = e & 3;
+			ra[i] = *reinterpret_cast<const uint4 *>(Cb + (int64_t)(c0 + row) * ld + k0 + seg * 8);
+		}
+	};
+	auto store_a = [&](uint8_t *A) {
+#pragma unroll
+		for (int i = 0; i < 2; ++i) {
+			const int e = t + i * 256, row = e >> 2, seg = e & 3;
+			*reinterpret_cast<uint4 *>(A + row * KM_ROWB + seg * 16) = ra[i];
+		}
+	};
+	f32x16 acc[2][2];
+#pragma unroll
+	for (int a = 0; a < 2; ++a)
+#pragma unroll
+		for (int b = 0; b < 2; ++b)
+#pragma unroll
+			for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+
+	load_a(0);
+	km_load_rows<T>(Xb, ld, rt0, nrel, 0, rb);
+	store_a(As[0]);
+	km_store_rows<T>(Bs[0], rb);
+	__syncthreads();
+	const int fr = lane & 31, fh = lane >> 5;
+	for (int s = 0; s < nst; ++s) {
+		const int cur = s & 1;
+		if (s + 1 < nst) {
+			load_a((s + 1) * KM_K);
+			km_load_rows<T>(Xb, ld, rt0, nrel, (s + 1) * KM_K, rb);
+		}
+#pragma unroll
+		for (int kk = 0; kk < 2; ++kk) {
+			bf16x8 av[2], bv[2];
+#pragma unroll
+			for (int mi = 0; mi < 2; ++mi)
+				av[mi] = *reinterpret_cast<const bf16x8 *>(As[cur] + (cw + mi * 32 + fr) * KM_ROWB + kk * 32 + fh * 16);
+#pragma unroll
+			for (int ni = 0; ni < 2; ++ni)
+				bv[ni] = *reinterpret_cast<const bf16x8 *>(Bs[cur] + (rw + ni * 32 + fr) * KM_ROWB + kk * 32 + fh * 16);
+#pragma unroll
+			for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+				for (int ni = 0; ni < 2; ++ni)
+					acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[mi], bv[ni], acc[mi][ni], 0, 0, 0);
+		}
+		if (s + 1 < nst) {
+			store_a(As[cur ^ 1]);
+			km_store_rows<T>(Bs[cur ^ 1], rb);
+		}
+		__syncthreads();
+	}
+	// epilogue: this lane's data row = rw + ni*32 + fr; centroids in registers
+#pragma unroll
+	for (int ni = 0; ni < 2; ++ni) {
+		const int64_t row = rt0 + rw + ni * 32 + fr;
+		const float sc = (row_scale_aux && row < nrel) ? row_scale_aux[raix(r0 + row, 3)] : 1.0f;
+		uint64_t bk = KEY64_NONE;
+#pragma unroll
+		for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+			for (int r = 0; r < 16; ++r) {
+				const int c = c0 + cw + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+				const float score = cnorm[c] - 2.0f * sc * acc[mi][ni][r];
+				const uint64_t kv = ((uint64_t)fkey(score) << 32) | (uint32_t)c;
+				bk = kv < bk ? kv : bk;
+			}
+		const uint64_t o = __shfl_xor(bk, 32, 64);
+		bk = o < bk ? o : bk;
+		if (fh == 0 && row < nrel) atomicMin((unsigned long long *)(best + row), (unsigned long long)bk);
+	}
+}
+
+void launch_kmeans_assign(const void *X, int xbf16, int ld, int64_t r0, int64_t n, const float *row_scale_aux,
+                          const uint16_t *Cb, const float *cnorm, int nc_pad, uint64_t *best, hipStream_t st) {
+	if (n <= 0) return;
+	dim3 grid((unsigned)((n + KM_T - 1) / KM_T), (unsigned)(nc_pad / KM_T));
+	if (xbf16)
+		kmeans_assign_kernel<uint16_t><<<grid, 256, 0, st>>>(static_cast<const uint16_t *>(X), ld, r0, n,
+		                                                      row_scale_aux, Cb, cnorm, best);
+	else
+		kmeans_assign_kernel<float><<<grid, 256, 0, st>>>(static_cast<const float *>(X), ld, r0, n, row_scale_aux, Cb,
+		                                                   cnorm, best);
+}
+
+// Exact-f32 variant for placing rows into lists (v_mfma_f32_32x32x2_f32:
+// f32 products and accumulation, ~1e-6 relative): the bf16 scores above are
+// good enough to train on, but near-equidistant rows would land in a
+// farther list.  Same tiling and epilogue; LDS rows of 33 floats (ds_read_b32
+// banks are mod 32: the 32 lanes of a half read 32 consecutive rows).
+constexpr int KF_ROW = KM_K + 1;
+
+template <typename T>
+__global__ __launch_bounds__(256) void kmeans_assign_f32_kernel(const T *__restrict__ X, int ld, int64_t r0, int64_t n,
+                                                                const float *__restrict__ row_scale_aux,
+                                                                const float *__restrict__ Cf,
+                                                                const float *__restrict__ cnorm,
+                                                                uint64_t *__restrict__ best) {
+	__shared__ float As[2][KM_T * KF_ROW];
+	__shared__ float Bs[2][KM_T * KF_ROW];
+	const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+	const int64_t rt0 = (int64_t)blockIdx.x * KM_T;
+	const int c0 = blockIdx.y * KM_T;
+	const int cw = (w & 1) * 64, rw = (w >> 1) * 64;
+	const T *Xb = X + r0 * (int64_t)ld;
+	const int nst = ld / KM_K;
+	float4 ra[4], rb[4];
+	auto load = [&](int k0) {
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			const int e = t + i * 256, row = e >> 3, seg = e & 7;
+			ra[i] = *reinterpret_cast<const float4 *>(Cf + (int64_t)(c0 + row) * ld + k0 + seg * 4);
+			const int64_t r = rt0 + row;
+			rb[i] = r < n ? load4(Xb + r * ld + k0 + seg * 4) : make_float4(0, 0, 0, 0);
+		}
+	};
+	auto store = [&](float *A, float *B) {
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			const int e = t + i * 256, row = e >> 3, seg = e & 7;
+			float *a = A + row * KF_ROW + seg * 4, *b = B + row * KF_ROW + seg * 4;
+			a[0] = ra[i].x, a[1] = ra[i].y, a[2] = ra[i].z, a[3] = ra[i].w;
+			b[0] = rb[i].x, b[1] = rb[i].y, b[2] = rb[i].z, b[3] = rb[i].w;
+		}
+	};
+	f32x16 acc[2][2];
+#pragma unroll
+	for (int a = 0; a < 2; ++a)
+#pragma unroll
+		for (int b = 0; b < 2; ++b)
+#pragma unroll
+			for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+	load(0);
+	store(As[0], Bs[0]);
+	__syncthreads();
+	const int fr = lane & 31, fh = lane >> 5;
+	for (int s = 0; s < nst; ++s) {
+		const int cur = s & 1;
+		if (s + 1 < nst) load((s + 1) * KM_K);
+#pragma unroll
+		for (int kk = 0; kk < KM_K / 2; ++kk) {
+			float av[2], bv[2];
+#pragma unroll
+			for (int mi = 0; mi < 2; ++mi) av[mi] = As[cur][(cw + mi * 32 + fr) * KF_ROW + 2 * kk + fh];
+#pragma unroll
+			for (int ni = 0; ni < 2; ++ni) bv[ni] = Bs[cur][(rw + ni * 32 + fr) * KF_ROW + 2 * kk + fh];
+#pragma unroll
+			for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+				for (int ni = 0; ni < 2; ++ni)
+					acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi], bv[ni], acc[mi][ni], 0, 0, 0);
+		}
+		if (s + 1 < nst) store(As[cur ^ 1], Bs[cur ^ 1]);
+		__syncthreads();
+	}
+#pragma unroll
+	for (int ni = 0; ni < 2; ++ni) {
+		const int64_t row = rt0 + rw + ni * 32 + fr;
+		const float sc = (row_scale_aux && row < n) ? row_scale_aux[raix(r0 + row, 3)] : 1.0f;
+		uint64_t bk = KEY64_NONE;
+#pragma unroll
+		for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+			for (int r = 0; r < 16; ++r) {
+				const int c = c0 + cw + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+				const float score = cnorm[c] - 2.0f * sc * acc[mi][ni][r];
+				const uint64_t kv = ((uint64_t)fkey(score) << 32) | (uint32_t)c;
+				bk = kv < bk ? kv : bk;
+			}
+		const uint64_t o = __shfl_xor(bk, 32, 64);
+		bk = o < bk ? o : bk;
+		if (fh == 0 && row < n) atomicMin((unsigned long long *)(best + row), (unsigned long long)bk);
+	}
+}
+
+void launch_kmeans_assign_f32(const void *X, int xbf16, int ld, int64_t r0, int64_t n, const float *row_scale_aux,
+                              const float *Cf, const float *cnorm, int nc_pad, uint64_t *best, hipStream_t st) {
+	if (n <= 0) return;
+	dim3 grid((unsigned)((n + KM_T - 1) / KM_T), (unsigned)(nc_pad / KM_T));
+	if (xbf16)
+		kmeans_assign_f32_kernel<uint16_t><<<grid, 256, 0, st>>>(static_cast<const uint16_t *>(X), ld, r0, n,
+		                                                          row_scale_aux, Cf, cnorm, best);
+	else
+		kmeans_assign_f32_kernel<float><<<grid, 256, 0, st>>>(static_cast<const float *>(X), ld, r0, n, row_scale_aux,
+		                                                       Cf, cnorm, best);
+}
+
+// deterministic sum (fixed per-thread strides + fixed tree) of the winning scores
+__global__ __launch_bounds__(1024) void score_sum_kernel(const uint64_t *__restrict__ best, int64_t n,
+                                                         double *__restrict__ out) {
+	__shared__ double sh[1024];
+	double s = 0.0;
+	for (int64_t i = threadIdx.x; i < n; i += 1024) s += (double)key64_dist(best[i]);
+	sh[threadIdx.x] = s;
+	__syncthreads();
+	for (int o = 512; o > 0; o >>= 1) {
+		if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+		__syncthreads();
+	}
+	if (threadIdx.x == 0) *out = sh[0];
+}
+
+void launch_score_sum(const uint64_t *best, int64_t n, double *out, hipStream_t st) {
+	score_sum_kernel<<<1, 1024, 0, st>>>(best, n, out);
+}
+
+// sum of squares of n f32 values (deterministic order), for the k-means stopping rule
+__global__ __launch_bounds__(1024) void sq_sum_kernel(const float *__restrict__ v, int64_t n, double *__restrict__ out) {
+	__shared__ double sh[1024];
+	double s = 0.0;
+	for (int64_t i = threadIdx.x; i < n; i += 1024) s += (double)v[i] * v[i];
+	sh[threadIdx.x] = s;
+	__syncthreads();
+	for (int o = 512; o > 0; o >>= 1) {
+		if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+		__syncthreads();
+	}
+	if (threadIdx.x == 0) *out = sh[0];
+}
+
+void launch_sq_sum(const float *v, int64_t n, double *out, hipStream_t st) { sq_sum_kernel<<<1, 1024, 0, st>>>(v, n, out); }
+
+// dst row i = src row idx[i] (rows of row_bytes, a multiple of 16)
+__global__ void gather_bytes_kernel(const uint8_t *__restrict__ src, const int64_t *__restrict__ idx, int64_t n,
+                                    int row_bytes, uint8_t *__restrict__ dst) {
+	const int nch = row_bytes >> 4;
+	const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (e >= n * nch) return;
+	const int64_t r = e / nch;
+	const int ch = (int)(e % nch);
+	*reinterpret_cast<uint4 *>(dst + r * row_bytes + ch * 16) =
+	    *reinterpret_cast<const uint4 *>(src + idx[r] * row_bytes + ch * 16);
+}
+
+void launch_gather_bytes(const uint8_t *src, const int64_t *idx, int64_t n, int row_bytes, uint8_t *dst,
+                         hipStream_t st) {
+	const int64_t tot = n * (row_bytes >> 4);
+	if (tot <= 0) return;
+	gather_bytes_kernel<<<dim3((unsigned)((tot + 255) / 256)), 256, 0, st>>>(src, idx, n, row_bytes, dst);
+}
+
+__global__ void best_to_assign_kernel(const uint64_t *__restrict__ best, int64_t n, int *__restrict__ assign,
+                                      uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+	const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	const uint32_t c = (uint32_t)best[i];
+	if (assign) assign[i] = (int)c;
+	if (keys) keys[i] = c;
+	if (vals) vals[i] = (uint32_t)i;
+}
+
+void launch_best_to_assign(const uint64_t *best, int64_t n, int *assign, uint32_t *keys, uint32_t *vals,
+                           hipStream_t st) {
+	if (n <= 0) return;
+	best_to_assign_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, st>>>(best, n, assign, keys, vals);
+}
+
+int sort_u32_pairs(void *temp, size_t &temp_bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
+                   uint32_t *vout, int64_t n, int end_bit, hipStream_t st) {
+	return (int)rocprim::radix_sort_pairs(temp, temp_bytes, kin, kout, vin, vout, (size_t)n, 0, end_bit, st);
+}
+
+__global__ void segments_kernel(const uint32_t *__restrict__ keys, int64_t n, int nseg, int *__restrict__ seg_start) {
+	const int c = blockIdx.x * blockDim.x + threadIdx.x;
+	if (c > nseg) return;
+	int64_t lo = 0, hi = n;  // first index with key >= c
+	while (lo < hi) {
+		const int64_t mid = (lo + hi) >> 1;
+		if (keys[mid] < (uint32_t)c)
+			lo = mid + 1;
+		else
+			hi = mid;
+	}
+	seg_start[c] = (int)lo;
+}
+
+void launch_segments(const uint32_t *sorted_keys, int64_t n, int nseg, int *seg_start, hipStream_t st) {
+	segments_kernel<<<dim3((unsigned)((nseg + 1 + 255) / 256)), 256, 0, st>>>(sorted_keys, n, nseg, seg_start);
+}
+
+// new centroid = mean of its members, summed in member order (f64); an empty
+// cluster keeps its previous centroid
+__global__ __launch_bounds__(256) void centroid_mean_kernel(const float *__restrict__ S, int ld, int dim,
+                                                            const uint32_t *__restrict__ idx,
+                                                            const int *__restrict__ seg_start, float *__restrict__ C) {
+	const int c = blockIdx.x;
+	const int a = seg_start[c], b = seg_start[c + 1];
+	if (b <= a) return;
+	const double inv = 1.0 / (double)(b - a);
+	for (int i = threadIdx.x; i < dim; i += 256) {
+		double s = 0.0;
+		for (int m = a; m < b; ++m) s += S[(int64_t)idx[m] * ld + i];
+		C[(int64_t)c * ld + i] = (float)(s * inv);
+	}
+}
+
+void launch_centroid_mean(const float *S, int ld, int dim, const uint32_t *sorted_idx, const int *seg_start, int nc,
+                          float *C, hipStream_t st) {
+	centroid_mean_kernel<<<dim3((unsigned)nc), 256, 0, st>>>(S, ld, dim, sorted_idx, seg_start, C);
+}
+
+__global__ void residuals_kernel(const float *__restrict__ S, const int *__restrict__ assign,
+                                 const float *__restrict__ C, int ld, int64_t n, float *__restrict__ R) {
+	const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (e >= n * ld) return;
+	const int64_t r = e / ld;
+	const int i = (int)(e % ld);
+	R[e] = S[e] - C[(int64_t)assign[r] * ld + i];
+}
+
+void launch_residuals(const float *S, const int *assign, const float *C, int ld, int64_t n, float *R,
+                      hipStream_t st) {
+	const int64_t tot = n * ld;
+	residuals_kernel<<<dim3((unsigned)((tot + 255) / 256)), 256, 0, st>>>(S, assign, C, ld, n, R);
+}
+
+// ---------------------------------------------------------------------------
+// PQ: per-sub-space assignment / means / encoding (codebook slice in LDS)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int pq_argmin(const float *cbs /*[256][dsub+1]*/, const float (&r)[PQ_MAX_DSUB],
+                                         int dsub) {
+	float bd = F_INF;
+	int bc = 0;
+	for (int c = 0; c < PQ_K; ++c) {
+		const float *y = cbs + c * (dsub + 1);
+		float d = 0.0f;
+#pragma unroll
+		for (int t = 0; t < PQ_MAX_DSUB; ++t) {
+			if (t < dsub) {
+				const float u = r[t] - y[t];
+				d += u * u;
+			}
+		}
+		if (d < bd) {  // strict: ties keep the lowest code
+			bd = d;
+			bc = c;
+		}
+	}
+	return bc;
+}
+
+__device__ __forceinline__ void pq_load_cb(const float *__restrict__ cb, int j, int dsub, float *cbs) {
+	for (int e = threadIdx.x; e < PQ_K * dsub; e += blockDim.x) {
+		const int c = e / dsub, t = e % dsub;
+		cbs[c * (dsub + 1) + t] = cb[((int64_t)j * PQ_K + c) * dsub + t];
+	}
+	__syncthreads();
+}
+
+__global__ __launch_bounds__(256) void pq_assign_kernel(const float *__restrict__ R, int ld, int64_t n, int m, int dsub,
+                                                        const float *__restrict__ cb, uint32_t *__restrict__ keys,
+                                                        uint32_t *__restrict__ vals) {
+	__shared__ float cbs[PQ_K * (PQ_MAX_DSUB + 1)];
+	const int j = blockIdx.y;
+	pq_load_cb(cb, j, dsub, cbs);
+	const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+	if (r >= n) return;
+	float v[PQ_MAX_DSUB];
+#pragma unroll
+	for (int t = 0; t < PQ_MAX_DSUB; ++t) v[t] = t < dsub ? R[r * ld + j * dsub + t] : 0.0f;
+	const int c = pq_argmin(cbs, v, dsub);
+	keys[(int64_t)j * n + r] = (uint32_t)(j * PQ_K + c);
+	vals[(int64_t)j * n + r] = (uint32_t)r;
+}
+
+void launch_pq_assign(const float *R, int ld, int64_t n, int m, int dsub, const float *cb, uint32_t *keys,
+                      uint32_t *vals, hipStream_t st) {
+	dim3 grid((unsigned)((n + 255) / 256), (unsigned)m);
+	pq_assign_kernel<<<grid, 256, 0, st>>>(R, ld, n, m, dsub, cb, keys, vals);
+}
+
+// one thread per (sub-space j, code c, component t): mean over the members in order
+__global__ void pq_mean_kernel(const float *__restrict__ R, int ld, const uint32_t *__restrict__ idx,
+                               const int *__restrict__ seg_start, int m, int dsub, float *__restrict__ cb) {
+	const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (e >= (int64_t)m * PQ_K * dsub) return;
+	const int seg = (int)(e / dsub), t = (int)(e % dsub);
+	const int j = seg / PQ_K;
+	const int a = seg_start[seg], b = seg_start[seg + 1];
+	if (b <= a) return;
+	double s = 0.0;
+	for (int i = a; i < b; ++i) s += R[(int64_t)idx[i] * ld + j * dsub + t];
+	cb[e] = (float)(s / (double)(b - a));
+}
+
+void launch_pq_mean(const float *R, int ld, const uint32_t *sorted_idx, const int *seg_start, int m, int dsub,
+                    float *cb, hipStream_t st) {
+	const int64_t tot = (int64_t)m * PQ_K * dsub;
+	pq_mean_kernel<<<dim3((unsigned)((tot + 255) / 256)), 256, 0, st>>>(R, ld, sorted_idx, seg_start, m, dsub, cb);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void pq_encode_kernel(const T *__restrict__ X, int ld, int64_t s0, int64_t n,
+                                                        const float *__restrict__ rowaux_f, int normalize,
+                                                        const int *__restrict__ assign, const float *__restrict__ C,
+                                                        const float *__restrict__ cb, int dsub, int mp,
+                                                        uint8_t *__restrict__ codes) {
+	__shared__ float cbs[PQ_K * (PQ_MAX_DSUB + 1)];
+	const int j = blockIdx.y;
+	pq_load_cb(cb, j, dsub, cbs);
+	const int64_t s = s0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+	if (s >= s0 + n) return;
+	const float sc = normalize ? rowaux_f[raix(s, 3)] : 1.0f;  // 1/|x| (cosine)
+	const float *c = C + (int64_t)assign[s] * ld + j * dsub;
+	const T *x = X + s * ld + j * dsub;
+	float v[PQ_MAX_DSUB];
+#pragma unroll
+	for (int t = 0; t < PQ_MAX_DSUB; ++t) v[t] = t < dsub ? xval(x, t) * sc - c[t] : 0.0f;
+	codes[s * mp + j] = (uint8_t)pq_argmin(cbs, v, dsub);
+}
+
+void launch_pq_encode(const void *X, int xbf16, int ld, int dim, int64_t s0, int64_t n, const float *rowaux_f,
+                      int normalize, const int *assign, const float *C, const float *cb, int m, int dsub, int mp,
+                      uint8_t *codes, hipStream_t st) {
+	if (n <= 0) return;
+	dim3 grid((unsigned)((n + 255) / 256), (unsigned)m);
+	if (xbf16)
+		pq_encode_kernel<uint16_t><<<grid, 256, 0, st>>>(static_cast<const uint16_t *>(X), ld, s0, n, rowaux_f,
+		                                                  normalize, assign, C, cb, dsub, mp, codes);
+	else
+		pq_encode_kernel<float><<<grid, 256, 0, st>>>(static_cast<const float *>(X), ld, s0, n, rowaux_f, normalize,
+		                                               assign, C, cb, dsub, mp, codes);
+}
+
+// T[l][j][c] = sum_t y (y + 2 c_l)  (f32, t in order, no contraction)
+__global__ __launch_bounds__(256) void pq_T_kernel(const float *__restrict__ C, int ld, const float *__restrict__ cb,
+                                                   int m, int dsub, float *__restrict__ T) {
+	const int l = blockIdx.x, j = blockIdx.y, c = threadIdx.x;
+	const float *y = cb + ((int64_t)j * PQ_K + c) * dsub;
+	const float *cl = C + (int64_t)l * ld + j * dsub;
+	float acc = 0.0f;
+	for (int t = 0; t < dsub; ++t) acc = __fadd_rn(acc, __fmul_rn(y[t], __fadd_rn(y[t], 2.0f * cl[t])));
+	T[((int64_t)l * m + j) * PQ_K + c] = acc;
+}
+
+void launch_pq_tables_T(const float *C, int ld, const float *cb, int nlist, int m, int dsub, float *T,
+                        hipStream_t st) {
+	pq_T_kernel<<<dim3((unsigned)nlist, (unsigned)m), PQ_K, 0, st>>>(C, ld, cb, m, dsub, T);
+}
+
+__global__ void pq_layout_kernel(const uint8_t *__restrict__ codes, const uint32_t *__restrict__ lslot, int64_t npos,
+                                 int mp, uint8_t *__restrict__ lcodes) {
+	const int nch = mp >> 4;
+	const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (e >= npos * nch) return;
+	const int64_t pos = e / nch;
+	const int ch = (int)(e % nch);
+	const uint32_t slot = lslot[pos];
+	uint4 v = make_uint4(0, 0, 0, 0);
+	if (slot != SLOT_NONE) v = *reinterpret_cast<const uint4 *>(codes + (int64_t)slot * mp + ch * 16);
+	*reinterpret_cast<uint4 *>(lcodes + (((pos >> 6) * nch + ch) * 64 + (pos & 63)) * 16) = v;
+}
+
+void launch_pq_layout(const uint8_t *codes, const uint32_t *lslot, int64_t npos, int mp, uint8_t *lcodes,
+                      hipStream_t st) {
+	const int64_t tot = npos * (mp >> 4);
+	if (tot <= 0) return;
+	pq_layout_kernel<<<dim3((unsigned)((tot + 255) / 256)), 256, 0, st>>>(codes, lslot, npos, mp, lcodes);
+}
+
+// ---------------------------------------------------------------------------
+// search: query prep, probe inversion
+// ---------------------------------------------------------------------------
+// Qf = zero-padded f32 queries; Qn = normalised queries (cosine):
+// q^ = q / f32(sqrt(sum q^2)) with an IEEE f32 division (oracle/ivf.py)
+__global__ __launch_bounds__(256) void ivf_prep_kernel(const float *__restrict__ Q, int dim, int ld, int normalize,
+                                                       float *__restrict__ Qf, float *__restrict__ Qn) {
+	__shared__ double sh[256];
+	const int q = blockIdx.x, t = threadIdx.x;
+	const float *x = Q + (int64_t)q * dim;
+	double ss = 0.0;
+	for (int i = t; i < ld; i += 256) {
+		const float v = i < dim ? x[i] : 0.0f;
+		Qf[(int64_t)q * ld + i] = v;
+		ss += (double)v * v;
+	}
+	if (!normalize) return;
+	sh[t] = ss;
+	__syncthreads();
+	for (int o = 128; o > 0; o >>= 1) {
+		if (t < o) sh[t] += sh[t + o];
+		__syncthreads();
+	}
+	const float nrm = (float)sqrt(sh[0]);
+	for (int i = t; i < dim; i += 256) Qn[(int64_t)q * dim + i] = nrm > 0.0f ? __fdiv_rn(x[i], nrm) : x[i];
+}
+
+void launch_ivf_prep(const float *Q, int nq, int dim, int ld, int normalize, float *Qf, float *Qn, hipStream_t st) {
+	ivf_prep_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(Q, dim, ld, normalize, Qf, Qn);
+}
+
+__global__ void invert_count_kernel(const int64_t *__restrict__ probe_l, int n, int *__restrict__ lcnt) {
+	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	const int64_t l = probe_l[i];
+	if (l >= 0) atomicAdd(lcnt + l, 1);
+}
+
+// exclusive scan of lcnt into pstart[0..nlist], then lcnt = 0 (fill cursors)
+__global__ __launch_bounds__(1024) void invert_scan_kernel(int *__restrict__ lcnt, int nlist, int *__restrict__ pstart) {
+	__shared__ int sh[1024];
+	const int t = threadIdx.x;
+	const int per = (nlist + 1023) / 1024;
+	const int a = t * per, b = min(nlist, a + per);
+	int s = 0;
+	for (int i = a; i < b; ++i) s += lcnt[i];
+	sh[t] = s;
+	__syncthreads();
+	for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+		const int v = t >= o ? sh[t - o] : 0;
+		__syncthreads();
+		sh[t] += v;
+		__syncthreads();
+	}
+	int run = sh[t] - s;
+	for (int i = a; i < b; ++i) {
+		pstart[i] = run;
+		run += lcnt[i];
+		lcnt[i] = 0;
+	}
+	if (t == 1023) pstart[nlist] = sh[1023];
+}
+
+__global__ void invert_fill_kernel(const int64_t *__restrict__ probe_l, int n, const int *__restrict__ pstart,
+                                   int *__restrict__ cursor, int *__restrict__ pairs) {
+	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	const int64_t l = probe_l[i];
+	if (l < 0) return;
+	const int p = atomicAdd(cursor + l, 1);
+	pairs[pstart[l] + p] = i;
+}
+
+void launch_invert(const int64_t *probe_l, int nq, int nprobe, int nlist, int *lcnt, int *pstart, int *pairs,
+                   hipStream_t st) {
+	const int n = nq * nprobe;
+	(void)hipMemsetAsync(lcnt, 0, (size_t)nlist * sizeof(int), st);
+	invert_count_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, st>>>(probe_l, n, lcnt);
+	invert_scan_kernel<<<1, 1024, 0, st>>>(lcnt, nlist, pstart);
+	invert_fill_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, st>>>(probe_l, n, pstart, lcnt, pairs);
+}
+
+// ---------------------------------------------------------------------------
+// IVF_FLAT list scan: work item = 256 positions of one list (or 256 rows of
+// the unindexed tail); every query probing the list, FS_G at a time: rows are
+// staged 32 dims at a time through LDS (coalesced 128-B row segments), each
+// thread owns one row and accumulates (x - q)^2 (or x.q) in f64.
+// ---------------------------------------------------------------------------
+constexpr int FS_G = 4;
+constexpr int FS_KC = 32;
+
+template <typename T>
+__device__ __forceinline__ void fs_stage(const T *__restrict__ X, int ld, const uint32_t *sslot, int d0,
+                                         float (*xs)[FS_KC + 1]) {
+	// 256 rows x 32 elements: 8 four-element pieces per row
+#pragma unroll
+	for (int i = 0; i < 8; ++i) {
+		const int e = threadIdx.x + i * 256, row = e >> 3, piece = e & 7;
+		const uint32_t s = sslot[row];
+		const float4 v = s != SLOT_NONE ? load4(X + (int64_t)s * ld + d0 + piece * 4) : make_float4(0, 0, 0, 0);
+		xs[row][piece * 4 + 0] = v.x;
+		xs[row][piece * 4 + 1] = v.y;
+		xs[row][piece * 4 + 2] = v.z;
+		xs[row][piece * 4 + 3] = v.w;
+	}
+}
+
+template <int METRIC, typename T>
+__global__ __launch_bounds__(256) void flat_list_scan_kernel(
+    const T *__restrict__ X, int ld, int dim, const float *__restrict__ rowaux_f, const int *__restrict__ blk_list,
+    const int64_t *__restrict__ blk_pos0, const int *__restrict__ lblk0, const int64_t *__restrict__ loff,
+    const uint32_t *__restrict__ lslot, const int *__restrict__ pstart, const int *__restrict__ pairs, int nprobe,
+    int maxb, int64_t tail_s0, int64_t tail_n, int nq, const float *__restrict__ Qf, int kk,
+    uint64_t *__restrict__ out) {
+	__shared__ float xs[FLAT_BLK][FS_KC + 1];
+	__shared__ double qs[FS_G][FS_KC];
+	__shared__ uint32_t sslot[FLAT_BLK];
+	__shared__ uint64_t sk[FLAT_BLK];
+	__shared__ int sq[FS_G], spair[FS_G];
+	const int t = threadIdx.x;
+	const int b = blockIdx.x;
+	const bool tail = tail_n > 0;
+	int pa, pb, bi = 0;
+	int64_t p0, p1;
+	if (tail) {
+		p0 = (int64_t)b * FLAT_BLK;
+		p1 = min<int64_t>(tail_n, p0 + FLAT_BLK);
+		pa = 0;
+		pb = nq;
+	} else {
+		const int l = blk_list[b];
+		p0 = blk_pos0[b];
+		p1 = min<int64_t>(loff[l + 1], p0 + FLAT_BLK);
+		pa = pstart[l];
+		pb = pstart[l + 1];
+		bi = b - lblk0[l];
+	}
+	if (pa >= pb) return;
+	{
+		uint32_t s = SLOT_NONE;
+		if (p0 + t < p1) {
+			s = tail ? (uint32_t)(tail_s0 + p0 + t) : lslot[p0 + t];
+			if (s != SLOT_NONE && !slot_alive(rowaux_f, s)) s = SLOT_NONE;
+		}
+		sslot[t] = s;
+	}
+	const int tail_nb = (int)((tail_n + FLAT_BLK - 1) / FLAT_BLK);
+	for (int g0 = pa; g0 < pb; g0 += FS_G) {
+		const int ng = min(FS_G, pb - g0);
+		__syncthreads();
+		if (t < FS_G) {
+			const int pid = t < ng ? (tail ? g0 + t : pairs[g0 + t]) : -1;
+			spair[t] = pid;
+			sq[t] = pid < 0 ? 0 : (tail ? pid : pid / nprobe);
+		}
+		double acc[FS_G], aux[FS_G], xx = 0.0;
+#pragma unroll
+		for (int g = 0; g < FS_G; ++g) acc[g] = aux[g] = 0.0;
+		for (int d0 = 0; d0 < dim; d0 += FS_KC) {
+			__syncthreads();
+			fs_stage<T>(X, ld, sslot, d0, xs);
+			if (t < FS_G * FS_KC) {
+				const int g = t / FS_KC, c = t % FS_KC;
+				qs[g][c] = g < ng ? (double)Qf[(int64_t)sq[g] * ld + d0 + c] : 0.0;
+			}
+			__syncthreads();
+#pragma unroll 4
+			for (int c = 0; c < FS_KC; ++c) {
+				const double xv = xs[t][c];
+				if (METRIC == METRIC_COSINE) xx = fma(xv, xv, xx);
+#pragma unroll
+				for (int g = 0; g < FS_G; ++g) {
+					const double qv = qs[g][c];
+					if (METRIC == METRIC_L2) {
+						const double dd = xv - qv;
+						acc[g] = fma(dd, dd, acc[g]);
+					} else {
+						acc[g] = fma(xv, qv, acc[g]);
+						if (METRIC == METRIC_COSINE) aux[g] = fma(qv, qv, aux[g]);
+					}
+				}
+			}
+		}
+		const bool valid = sslot[t] != SLOT_NONE;
+		for (int g = 0; g < ng; ++g) {
+			double r;
+			if (METRIC == METRIC_L2)
+				r = acc[g];
+			else if (METRIC == METRIC_DOT)
+				r = 1.0 - acc[g];
+			else
+				r = 1.0 - acc[g] / (sqrt(xx) * sqrt(aux[g]));
+			float f = (float)r + 0.0f;
+			if (__builtin_isnan(f)) f = __builtin_nanf("");
+			__syncthreads();
+			sk[t] = valid ? key64(f, sslot[t]) : KEY64_NONE;
+			wg_bitonic_sort(sk, FLAT_BLK);
+			const int pid = spair[g];
+			uint64_t *o = tail ? out + ((int64_t)pid * tail_nb + b) * kk : out + ((int64_t)pid * maxb + bi) * kk;
+			for (int i = t; i < kk; i += 256) o[i] = i < FLAT_BLK ? sk[i] : KEY64_NONE;
+		}
+	}
+}
+
+template <typename T>
+static void flat_scan_dispatch(const StoreView &s, const int *blk_list, const int64_t *blk_pos0, const int *lblk0,
+                               const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart,
+                               const int *pairs, int nprobe, int maxb, int64_t tail_s0, int64_t tail_n, int nq,
+                               const float *Qf, int kk, uint64_t *out, hipStream_t st) {
+	const T *X = static_cast<const T *>(s.X);
+	const float *ra = reinterpret_cast<const float *>(s.rowaux);
+	dim3 grid((unsigned)nblk);
+#define FS_ARGS X, s.ld, s.dim, ra, blk_list, blk_pos0, lblk0, loff, lslot, pstart, pairs, nprobe, maxb, tail_s0, tail_n, nq, Qf, kk, out
+	switch (s.metric) {
+	case METRIC_L2: flat_list_scan_kernel<METRIC_L2, T><<<grid, 256, 0, st>>>(FS_ARGS); break;
+	case METRIC_DOT: flat_list_scan_kernel<METRIC_DOT, T><<<grid, 256, 0, st>>>(FS_ARGS); break;
+	default: flat_list_scan_kernel<METRIC_COSINE, T><<<grid, 256, 0, st>>>(FS_ARGS); break;
+	}
+#undef FS_ARGS
+}
+
+void launch_flat_list_scan(const StoreView &s, const int *blk_list, const int64_t *blk_pos0, const int *lblk0,
+                           const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart, const int *pairs,
+                           int nprobe, int maxb, int64_t tail_s0, int64_t tail_n, int nq, const float *Qf, int kk,
+                           uint64_t *out, hipStream_t st) {
+	if (nblk <= 0) return;
+	if (s.xbf16)
+		flat_scan_dispatch<uint16_t>(s, blk_list, blk_pos0, lblk0, loff, lslot, nblk, pstart, pairs, nprobe, maxb,
+		                             tail_s0, tail_n, nq, Qf, kk, out, st);
+	else
+		flat_scan_dispatch<float>(s, blk_list, blk_pos0, lblk0, loff, lslot, nblk, pstart, pairs, nprobe, maxb,
+		                          tail_s0, tail_n, nq, Qf, kk, out, st);
+}
+
+// ---------------------------------------------------------------------------
+// IVF_PQ
+// ---------------------------------------------------------------------------
+// P[q][j][c] = sum_t q_{j,t} y_{j,c,t}  (f32, t in order, no contraction)
+__global__ __launch_bounds__(256) void pq_P_kernel(const float *__restrict__ Q, int qld, const float *__restrict__ cb,
+                                                   int m, int dsub, float *__restrict__ P) {
+	const int q = blockIdx.x, j = blockIdx.y, c = threadIdx.x;
+	const float *x = Q + (int64_t)q * qld + j * dsub;
+	const float *y = cb + ((int64_t)j * PQ_K + c) * dsub;
+	float acc = 0.0f;
+	for (int t = 0; t < dsub; ++t) acc = __fadd_rn(acc, __fmul_rn(x[t], y[t]));
+	P[((int64_t)q * m + j) * PQ_K + c] = acc;
+}
+
+void launch_pq_P(const float *Q, int qld, int nq, const float *cb, int m, int dsub, float *P, hipStream_t st) {
+	pq_P_kernel<<<dim3((unsigned)nq, (unsigned)m), PQ_K, 0, st>>>(Q, qld, cb, m, dsub, P);
+}
+
+constexpr int PQ_THREADS = 512;
+
+__global__ __launch_bounds__(PQ_THREADS) void pq_list_scan_kernel(
+    const uint8_t *__restrict__ lcodes, int m, int mp, const int64_t *__restrict__ loff,
+    const uint32_t *__restrict__ lslot, const float *__restrict__ rowaux_f, const int *__restrict__ pstart,
+    const int *__restrict__ pairs, int nprobe, const float *__restrict__ probe_d, const float *__restrict__ T,
+    const float *__restrict__ P, int kk, uint64_t *__restrict__ out) {
+	__shared__ float lut[PQ_MAX_M * PQ_K];
+	__shared__ uint64_t buf[IVF_TOPK_CAP];
+	__shared__ int cnt;
+	__shared__ uint64_t thr;
+	const int l = blockIdx.x, t = threadIdx.x;
+	const int pa = pstart[l], pb = pstart[l + 1];
+	if (pa >= pb) return;
+	const int64_t q0 = loff[l], q1 = loff[l + 1];
+	const int nch = mp >> 4;
+	const int nlut = m * PQ_K;
+	TopK tk{buf, &cnt, &thr, kk};
+	for (int g = pa; g < pb; ++g) {
+		const int pid = pairs[g];
+		const int q = pid / nprobe;
+		const float d0 = probe_d[pid];
+		__syncthreads();
+		const float *Pq = P + (int64_t)q * nlut;
+		if (T) {
+			const float *Tl = T + (int64_t)l * nlut;
+			for (int e = t; e < nlut; e += PQ_THREADS) lut[e] = Tl[e] - 2.0f * Pq[e];
+		} else {
+			for (int e = t; e < nlut; e += PQ_THREADS) lut[e] = -Pq[e];
+		}
+		tk.reset();
+		for (int64_t base = q0; base < q1; base += PQ_THREADS) {
+			const int64_t pos = base + t;
+			bool valid = false;
+			uint64_t key = KEY64_NONE;
+			if (pos < q1) {
+				const uint32_t slot = lslot[pos];
+				if (slot != SLOT_NONE && slot_alive(rowaux_f, slot)) {
+					valid = true;
+					const uint8_t *cp = lcodes + ((pos >> 6) * nch * 64 + (pos & 63)) * 16;
+					float acc = d0;
+					for (int ch = 0; ch < nch; ++ch) {
+						const uint4 w = *reinterpret_cast<const uint4 *>(cp + (int64_t)ch * 64 * 16);
+						const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+						for (int u = 0; u < 16; ++u) {
+							const int j = ch * 16 + u;
+							if (j < m) acc = acc + lut[j * PQ_K + ((wd[u >> 2] >> (8 * (u & 3))) & 255u)];
+						}
+					}
+					key = key64(acc, slot);
+				}
+			}
+			tk.offer(key, valid);
+		}
+		const int nout = tk.finish();
+		uint64_t *o = out + (int64_t)pid * kk;
+		for (int i = t; i < kk; i += PQ_THREADS) o[i] = i < nout ? buf[i] : KEY64_NONE;
+	}
+}
+
+void launch_pq_list_scan(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
+                         const float *rowaux_f, int nlist, const int *pstart, const int *pairs, int nprobe,
+                         const float *probe_d, const float *T, const float *P, int kk, uint64_t *out, hipStream_t st) {
+	pq_list_scan_kernel<<<dim3((unsigned)nlist), PQ_THREADS, 0, st>>>(lcodes, m, mp, loff, lslot, rowaux_f, pstart,
+	                                                                   pairs, nprobe, probe_d, T, P, kk, out);
+}
+
+// ---------------------------------------------------------------------------
+// merge / output
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void ivf_merge_kernel(int nprobe, const int64_t *__restrict__ probe_l,
+                                                        const int *__restrict__ lblk0, int maxb, int kk,
+                                                        const uint64_t *__restrict__ keys, int tail_nb,
+                                                        const uint64_t *__restrict__ tkeys, int K,
+                                                        uint64_t *__restrict__ out) {
+	__shared__ uint64_t buf[IVF_TOPK_CAP];
+	__shared__ int cnt;
+	__shared__ uint64_t thr;
+	const int q = blockIdx.x, t = threadIdx.x;
+	TopK tk{buf, &cnt, &thr, K};
+	tk.reset();
+	if (keys) {
+		for (int p = 0; p < nprobe; ++p) {
+			const int64_t l = probe_l[(int64_t)q * nprobe + p];
+			if (l < 0) continue;
+			const int nb = lblk0 ? lblk0[l + 1] - (int)lblk0[l] : 1;
+			const uint64_t *src = keys + ((int64_t)q * nprobe + p) * maxb * kk;
+			const int tot = nb * kk;
+			for (int e0 = 0; e0 < tot; e0 += 256) {
+				const int e = e0 + t;
+				const uint64_t k = e < tot ? src[e] : KEY64_NONE;
+				tk.offer(k, k != KEY64_NONE);
+			}
+		}
+	}
+	if (tkeys) {
+		const uint64_t *src = tkeys + (int64_t)q * tail_nb * kk;
+		const int tot = tail_nb * kk;
+		for (int e0 = 0; e0 < tot; e0 += 256) {
+			const int e = e0 + t;
+			const uint64_t k = e < tot ? src[e] : KEY64_NONE;
+			tk.offer(k, k != KEY64_NONE);
+		}
+	}
+	const int nout = tk.finish();
+	for (int i = t; i < K; i += 256) out[(int64_t)q * K + i] = i < nout ? buf[i] : KEY64_NONE;
+}
+
+void launch_ivf_merge(int nq, int nprobe, const int64_t *probe_l, const int *lblk0, int maxb, int kk,
+                      const uint64_t *keys, int tail_nb, const uint64_t *tkeys, int K, uint64_t *out, hipStream_t st) {
+	ivf_merge_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(nprobe, probe_l, lblk0, maxb, kk, keys, tail_nb, tkeys, K,
+	                                                      out);
+}
+
+__global__ void keys_to_output_kernel(const uint64_t *__restrict__ keys, int K, int k,
+                                      const int64_t *__restrict__ labels, int64_t *__restrict__ outL,
+                                      float *__restrict__ outD, int *__restrict__ outC) {
+	const int q = blockIdx.x;
+	__shared__ int n;
+	if (threadIdx.x == 0) n = 0;
+	__syncthreads();
+	for (int i = threadIdx.x; i < k; i += blockDim.x) {
+		const uint64_t key = i < K ? keys[(int64_t)q * K + i] : KEY64_NONE;
+		if (key != KEY64_NONE) {
+			outL[(int64_t)q * k + i] = labels[(uint32_t)key];
+			outD[(int64_t)q * k + i] = key64_dist(key);
+			atomicAdd(&n, 1);
+		} else {
+			outL[(int64_t)q * k + i] = -1;
+			outD[(int64_t)q * k + i] = __builtin_nanf("");
+		}
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) outC[q] = n;
+}
+
+void launch_keys_to_output(const uint64_t *keys, int nq, int K, int k, const int64_t *labels, int64_t *outL,
+                           float *outD, int *outC, hipStream_t st) {
+	keys_to_output_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(keys, K, k, labels, outL, outD, outC);
+}
+
+// exact re-rank of the ADC candidates (+ the tail's exact candidates): one
+// wave per candidate (f64, the flat path's refine arithmetic), bitonic sort
+template <int METRIC, typename T>
+__global__ __launch_bounds__(256) void ivf_refine_final_kernel(const T *__restrict__ X, int ld, int dim,
+                                                               const float *__restrict__ Qf,
+                                                               const uint64_t *__restrict__ ca, int ka,
+                                                               const uint64_t *__restrict__ cbk, int kb, int k,
+                                                               const int64_t *__restrict__ labels,
+                                                               int64_t *__restrict__ outL, float *__restrict__ outD,
+                                                               int *__restrict__ outC) {
+	__shared__ uint64_t sk[IVF_TOPK_CAP];
+	__shared__ uint32_t ss[IVF_TOPK_CAP];
+	__shared__ int n;
+	const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+	if (t == 0) n = 0;
+	__syncthreads();
+	for (int i = t; i < ka + kb; i += 256) {
+		const uint64_t key = i < ka ? ca[(int64_t)q * ka + i] : cbk[(int64_t)q * kb + (i - ka)];
+		if (key != KEY64_NONE) ss[atomicAdd(&n, 1)] = (uint32_t)key;
+	}
+	__syncthreads();
+	const int nc = n;
+	for (int i = w; i < nc; i += 4) {
+		const uint32_t slot = ss[i];
+		const float d = exact_distance<METRIC, T>(X + (int64_t)slot * ld, Qf + (int64_t)q * ld, dim, lane);
+		if (lane == 0) sk[i] = key64(d, slot);
+	}
+	const int np = pow2_ceil(nc);
+	__syncthreads();
+	for (int i = nc + t; i < np; i += 256) sk[i] = KEY64_NONE;
+	wg_bitonic_sort(sk, np);
+	const int nout = nc < k ? nc : k;
+	for (int i = t; i < k; i += 256) {
+		if (i < nout) {
+			outL[(int64_t)q * k + i] = labels[(uint32_t)sk[i]];
+			outD[(int64_t)q * k + i] = key64_dist(sk[i]);
+		} else {
+			outL[(int64_t)q * k + i] = -1;
+			outD[(int64_t)q * k + i] = __builtin_nanf("");
+		}
+	}
+	if (t == 0) outC[q] = nout;
+}
+
+template <typename T>
+static void refine_final_dispatch(const StoreView &s, const float *Qf, const uint64_t *ca, int ka, const uint64_t *cb,
+                                  int kb, int nq, int k, int64_t *outL, float *outD, int *outC, hipStream_t st) {
+	const T *X = static_cast<const T *>(s.X);
+	dim3 grid((unsigned)nq);
+#define RF_ARGS X, s.ld, s.dim, Qf, ca, ka, cb, kb, k, s.labels, outL, outD, outC
+	switch (s.metric) {
+	case METRIC_L2: ivf_refine_final_kernel<METRIC_L2, T><<<grid, 256, 0, st>>>(RF_ARGS); break;
+	case METRIC_DOT: ivf_refine_final_kernel<METRIC_DOT, T><<<grid, 256, 0, st>>>(RF_ARGS); break;
+	default: ivf_refine_final_kernel<METRIC_COSINE, T><<<grid, 256, 0, st>>>(RF_ARGS); break;
+	}
+#undef RF_ARGS
+}
+
+void launch_ivf_refine_final(const StoreView &s, const float *Qf, const uint64_t *ca, int ka, const uint64_t *cb,
+                             int kb, int nq, int k, int64_t *outL, float *outD, int *outC, hipStream_t st) {
+	if (s.xbf16)
+		refine_final_dispatch<uint16_t>(s, Qf, ca, ka, cb, kb, nq, k, outL, outD, outC, st);
+	else
+		refine_final_dispatch<float>(s, Qf, ca, ka, cb, kb, nq, k, outL, outD, outC, st);
+}
+
+}  // namespace lhip

@@ -28,493 +28,10 @@
 #include <string>
 #include <sys/stat.h>
 #include <vector>
+#include "index.h"
+#include "ivf.h"
 
 namespace lhip {
-
-// ---------------------------------------------------------------------------
-// errors
-// ---------------------------------------------------------------------------
-struct Error : std::runtime_error {
-	using std::runtime_error::runtime_error;
-};
-
-#define HIPCHK(expr)                                                                                                   \
-	do {                                                                                                               \
-		hipError_t _e = (expr);                                                                                        \
-		if (_e != hipSuccess) throw Error(std::string("HIP error: ") + hipGetErrorString(_e) + " at " #expr);          \
-	} while (0)
-
-// Completion wait of a search: spins on the stream (a blocking wait costs tens
-// of microseconds of wake-up per call, ~10% of a C2 batch).
-static void spin_sync(hipStream_t st) {
-	hipError_t e;
-	while ((e = hipStreamQuery(st)) == hipErrorNotReady) {
-	}
-	if (e != hipSuccess) throw Error(std::string("HIP error: ") + hipGetErrorString(e) + " at stream completion");
-}
-
-static void write_err(char *buf, int len, const std::string &msg) {
-	if (!buf || len <= 0) return;
-	size_t n = std::min(msg.size(), (size_t)(len - 1));
-	memcpy(buf, msg.data(), n);
-	buf[n] = 0;
-}
-
-static int metric_id(const std::string &m) {
-	// lance_manager.rs:493-497: cosine -> Cosine, dot|ip -> Dot, else L2
-	if (m == "cosine") return METRIC_COSINE;
-	if (m == "dot" || m == "ip") return METRIC_DOT;
-	return METRIC_L2;
-}
-
-// ---------------------------------------------------------------------------
-// device buffers
-// ---------------------------------------------------------------------------
-template <typename T>
-struct DevBuf {
-	T *p = nullptr;
-	size_t n = 0;  // capacity in elements
-	~DevBuf() { release(); }
-	void release() {
-		if (p) (void)hipFree(p);
-		p = nullptr;
-		n = 0;
-	}
-	// grow without preserving contents
-	void need(size_t m) {
-		if (m <= n) return;
-		release();
-		size_t c = std::max(m, (size_t)1);
-		HIPCHK(hipMalloc(&p, c * sizeof(T)));
-		n = c;
-	}
-};
-
-struct Workspace {
-	DevBuf<float> Qin, Qf, tau, cut, dense, cand_dist, out_d, fb_keys, fb_keys2, stage;
-	DevBuf<uint16_t> Qb;
-	DevBuf<float4> qaux;
-	DevBuf<uint2> seg_pool;
-	DevBuf<int> seg_cnt;
-	DevBuf<int> status, out_c;  // status = [cert | cand_cnt | pool_cnt] x nq
-	int *h_status = nullptr;    // pinned mirror of status
-	size_t h_status_n = 0;
-	DevBuf<uint32_t> cand_slot;
-	DevBuf<int64_t> out_l, fb_vals, fb_vals2, idx;
-	DevBuf<uint8_t> sort_tmp;
-	~Workspace() {
-		if (h_status) (void)hipHostFree(h_status);
-	}
-	void need_host_status(size_t n) {
-		if (n <= h_status_n) return;
-		if (h_status) HIPCHK(hipHostFree(h_status));
-		h_status = nullptr;
-		HIPCHK(hipHostMalloc(&h_status, n * sizeof(int)));
-		h_status_n = n;
-	}
-};
-
-// ---------------------------------------------------------------------------
-// the handle
-// ---------------------------------------------------------------------------
-struct Index {
-	std::string db_path, table, metric_name;
-	int metric = METRIC_L2;
-	int dim = 0;
-	int ld = 0;  // padded row stride
-	int device = 0;
-	bool metric_quirk = false;  // rank by L2 whatever the metric (reference behaviour)
-
-	std::mutex mu;
-	int64_t next_label = 0;
-
-	// host bookkeeping (slot order == ascending label order, always)
-	std::vector<int64_t> slot_label;
-	std::vector<uint8_t> live;
-	int64_t n_live = 0;
-
-	// device store: rows of `ld` elements, f32, or bf16 bits with storage "bf16"
-	void *X = nullptr;
-	bool xbf16 = false;
-	size_t xes() const { return xbf16 ? 2 : 4; }
-	uint8_t *xrow(int64_t s) const { return static_cast<uint8_t *>(X) + (size_t)s * ld * xes(); }
-	// bf16 scan copy of an f32 store (option scan_copy, default on): the scan
-	// streams 2 B per element; refine, get_vector and compact use the f32 rows
-	uint16_t *Xs = nullptr;
-	bool scan_copy = true;
-	bool has_scan_copy() const { return !xbf16 && scan_copy; }
-	float4 *rowaux = nullptr;  // aux for `metric`
-	float4 *rowaux_l2 = nullptr;  // aux for L2 when metric_quirk is on and metric != l2
-	int64_t *dlabels = nullptr;
-	int64_t cap = 0, n_slots = 0;
-	DevBuf<unsigned> stats;  // [0]=max alpha bits, [1]=max ux bits, [2],[3] for rowaux_l2
-	float max_alpha = 0.f, max_ux = 0.f, max_alpha_l2 = 0.f, max_ux_l2 = 0.f;
-	hipStream_t stream = nullptr;
-	Workspace ws;
-
-	// persistence
-	FILE *log = nullptr;
-
-	// ANN parameters recorded by create_index (flat search stays exact)
-	int32_t ivf_partitions = 0, ivf_sub_vectors = 0;
-
-	int64_t last_stats[4] = {0, 0, 0, 0};
-
-	// optional HIP-event timing of the scan kernels, on the stream they run on
-	bool time_kernels = false;
-	int sample_div = 32;  // sample pass covers ~1/sample_div of the tiles (>= 32 tiles)
-	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-	double kt_append_ms = 0.0, kt_dense_ms = 0.0;
-	int64_t kt_append_n = 0, kt_dense_n = 0;
-	int64_t kt_append_rows = 0, kt_append_qpad = 0;
-
-	~Index() {
-		if (log) fclose(log);
-		(void)hipSetDevice(device);
-		if (X) (void)hipFree(X);
-		if (Xs) (void)hipFree(Xs);
-		if (rowaux) (void)hipFree(rowaux);
-		if (rowaux_l2) (void)hipFree(rowaux_l2);
-		if (dlabels) (void)hipFree(dlabels);
-		for (auto &e : ev)
-			if (e) (void)hipEventDestroy(e);
-		if (stream) (void)hipStreamDestroy(stream);
-	}
-
-	void tic(int i) {
-		if (time_kernels) HIPCHK(hipEventRecord(ev[i], stream));
-	}
-	float toc_ms(int a, int b) {
-		float ms = 0.f;
-		HIPCHK(hipEventSynchronize(ev[b]));
-		HIPCHK(hipEventElapsedTime(&ms, ev[a], ev[b]));
-		return ms;
-	}
-
-	void init_device(int dev) {
-		int n = 0;
-		if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) throw Error("no HIP device available");
-		if (dev < 0) HIPCHK(hipGetDevice(&dev));
-		if (dev >= n) throw Error("HIP device " + std::to_string(dev) + " out of range");
-		device = dev;
-		HIPCHK(hipSetDevice(device));
-		HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-		stats.need(4);
-		HIPCHK(hipMemsetAsync(stats.p, 0, 4 * sizeof(unsigned), stream));
-		HIPCHK(hipStreamSynchronize(stream));
-	}
-
-	void bind() { HIPCHK(hipSetDevice(device)); }
-
-	// grow the device store to hold at least `want` slots (contents preserved)
-	void reserve(int64_t want) {
-		if (want <= cap) return;
-		// capacity is a multiple of the scan tile and the tail past n_slots is
-		// zero: the scan kernel streams whole tiles without clamping rows
-		int64_t c = round_up(std::max<int64_t>(want, std::max<int64_t>(4096, cap * 2)), SCAN_BR);
-		void *nX = nullptr;
-		uint16_t *nXs = nullptr;
-		float4 *na = nullptr, *na2 = nullptr;
-		int64_t *nl = nullptr;
-		HIPCHK(hipMalloc(&nX, (size_t)c * ld * xes()));
-		if (has_scan_copy()) HIPCHK(hipMalloc(&nXs, (size_t)c * ld * 2));
-		HIPCHK(hipMalloc(&na, (size_t)c * sizeof(float4)));
-		HIPCHK(hipMalloc(&nl, (size_t)c * sizeof(int64_t)));
-		if (rowaux_l2 || (metric_quirk && metric != METRIC_L2)) HIPCHK(hipMalloc(&na2, (size_t)c * sizeof(float4)));
-		if (n_slots > 0) {
-			HIPCHK(hipMemcpyAsync(nX, X, (size_t)n_slots * ld * xes(), hipMemcpyDeviceToDevice, stream));
-			if (nXs) HIPCHK(hipMemcpyAsync(nXs, Xs, (size_t)n_slots * ld * 2, hipMemcpyDeviceToDevice, stream));
-			// row aux is tile-blocked SoA: move whole tile blocks (cap is a
-			// multiple of SCAN_BR, so they exist in the old buffer)
-			const size_t aux_bytes = (size_t)round_up(n_slots, SCAN_BR) * sizeof(float4);
-			HIPCHK(hipMemcpyAsync(na, rowaux, aux_bytes, hipMemcpyDeviceToDevice, stream));
-			HIPCHK(hipMemcpyAsync(nl, dlabels, (size_t)n_slots * sizeof(int64_t), hipMemcpyDeviceToDevice, stream));
-			if (na2 && rowaux_l2) HIPCHK(hipMemcpyAsync(na2, rowaux_l2, aux_bytes, hipMemcpyDeviceToDevice, stream));
-		}
-		HIPCHK(hipMemsetAsync(static_cast<uint8_t *>(nX) + (size_t)n_slots * ld * xes(), 0,
-		                      (size_t)(c - n_slots) * ld * xes(), stream));
-		if (nXs) HIPCHK(hipMemsetAsync(nXs + (size_t)n_slots * ld, 0, (size_t)(c - n_slots) * ld * 2, stream));
-		launch_fill_rowaux(na, n_slots, c, stream);
-		if (na2) launch_fill_rowaux(na2, n_slots, c, stream);
-		HIPCHK(hipStreamSynchronize(stream));
-		if (X) HIPCHK(hipFree(X));
-		if (Xs) HIPCHK(hipFree(Xs));
-		Xs = nXs;
-		if (rowaux) HIPCHK(hipFree(rowaux));
-		if (dlabels) HIPCHK(hipFree(dlabels));
-		if (rowaux_l2) HIPCHK(hipFree(rowaux_l2));
-		X = nX;
-		rowaux = na;
-		dlabels = nl;
-		rowaux_l2 = na2;
-		cap = c;
-	}
-
-	void refresh_stats() {
-		unsigned h[4];
-		HIPCHK(hipMemcpyAsync(h, stats.p, sizeof(h), hipMemcpyDeviceToHost, stream));
-		HIPCHK(hipStreamSynchronize(stream));
-		memcpy(&max_alpha, &h[0], 4);
-		memcpy(&max_ux, &h[1], 4);
-		memcpy(&max_alpha_l2, &h[2], 4);
-		memcpy(&max_ux_l2, &h[3], 4);
-	}
-
-	// scan copy rows [s0, s0+n) = bf16 (RNE) of the f32 rows of X (padding
-	// columns stay zero)
-	void fill_scan_copy(int64_t s0, int64_t n, uint16_t *dst) {
-		if (n > 0)
-			launch_rows_to_bf16(reinterpret_cast<const float *>(xrow(s0)), ld, n, dim, ld, dst + (size_t)s0 * ld,
-			                    stream);
-	}
-
-	// option scan_copy: build or drop the bf16 scan copy of an f32 store
-	void set_scan_copy(bool on) {
-		if (on == scan_copy) return;
-		scan_copy = on;
-		if (!on) {
-			if (Xs) HIPCHK(hipFree(Xs));
-			Xs = nullptr;
-			return;
-		}
-		if (xbf16 || !X) return;  // allocated with the store
-		HIPCHK(hipMalloc(&Xs, (size_t)cap * ld * 2));
-		HIPCHK(hipMemsetAsync(Xs, 0, (size_t)cap * ld * 2, stream));
-		fill_scan_copy(0, n_slots, Xs);
-		HIPCHK(hipGetLastError());
-		HIPCHK(hipStreamSynchronize(stream));
-	}
-
-	// append rows already resident on the device at X[n_slots .. n_slots+num)
-	int64_t commit_rows(int64_t num) {
-		const int64_t first = next_label;
-		std::vector<int64_t> labs((size_t)num);
-		for (int64_t i = 0; i < num; ++i) labs[(size_t)i] = first + i;
-		HIPCHK(hipMemcpyAsync(dlabels + n_slots, labs.data(), (size_t)num * sizeof(int64_t), hipMemcpyHostToDevice,
-		                      stream));
-		if (Xs) fill_scan_copy(n_slots, num, Xs);
-		launch_rowaux(X, xbf16, ld, dim, metric, n_slots, num, rowaux, stats.p, stream);
-		if (rowaux_l2) launch_rowaux(X, xbf16, ld, dim, METRIC_L2, n_slots, num, rowaux_l2, stats.p + 2, stream);
-		HIPCHK(hipGetLastError());
-		HIPCHK(hipStreamSynchronize(stream));
-		refresh_stats();
-		slot_label.insert(slot_label.end(), labs.begin(), labs.end());
-		live.insert(live.end(), (size_t)num, 1);
-		n_slots += num;
-		n_live += num;
-		next_label = first + num;
-		return first;
-	}
-
-	int64_t add_host(const float *v, int64_t num) {
-		reserve(n_slots + num);
-		if (!xbf16) {
-			float *dst = reinterpret_cast<float *>(xrow(n_slots));
-			if (ld != dim) HIPCHK(hipMemsetAsync(dst, 0, (size_t)num * ld * sizeof(float), stream));
-			HIPCHK(hipMemcpy2DAsync(dst, (size_t)ld * sizeof(float), v, (size_t)dim * sizeof(float),
-			                        (size_t)dim * sizeof(float), (size_t)num, hipMemcpyHostToDevice, stream));
-		} else {
-			// bf16 store: f32 rows through a bounded device staging buffer
-			const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(num, (int64_t)(64 << 20) / (dim * 4)));
-			ws.stage.need((size_t)chunk * dim);
-			for (int64_t i = 0; i < num; i += chunk) {
-				const int64_t m = std::min<int64_t>(chunk, num - i);
-				HIPCHK(hipMemcpyAsync(ws.stage.p, v + i * dim, (size_t)m * dim * sizeof(float), hipMemcpyHostToDevice,
-				                      stream));
-				launch_rows_to_bf16(ws.stage.p, dim, m, dim, ld, reinterpret_cast<uint16_t *>(xrow(n_slots + i)),
-				                    stream);
-				HIPCHK(hipStreamSynchronize(stream));  // staging buffer reused
-			}
-		}
-		return commit_rows(num);
-	}
-
-	int64_t add_device(const float *v, int64_t num) {
-		reserve(n_slots + num);
-		if (!xbf16) {
-			float *dst = reinterpret_cast<float *>(xrow(n_slots));
-			if (ld != dim) HIPCHK(hipMemsetAsync(dst, 0, (size_t)num * ld * sizeof(float), stream));
-			HIPCHK(hipMemcpy2DAsync(dst, (size_t)ld * sizeof(float), v, (size_t)dim * sizeof(float),
-			                        (size_t)dim * sizeof(float), (size_t)num, hipMemcpyDeviceToDevice, stream));
-		} else {
-			launch_rows_to_bf16(v, dim, num, dim, ld, reinterpret_cast<uint16_t *>(xrow(n_slots)), stream);
-		}
-		return commit_rows(num);
-	}
-
-	// rows [s0, s0+n) as f32 (dim columns) into host memory
-	void read_rows(int64_t s0, int64_t n, float *out) {
-		if (n <= 0) return;
-		if (!xbf16) {
-			HIPCHK(hipMemcpy2D(out, (size_t)dim * sizeof(float), xrow(s0), (size_t)ld * sizeof(float),
-			                   (size_t)dim * sizeof(float), (size_t)n, hipMemcpyDeviceToHost));
-			return;
-		}
-		std::vector<uint16_t> b((size_t)n * dim);
-		HIPCHK(hipMemcpy2D(b.data(), (size_t)dim * 2, xrow(s0), (size_t)ld * 2, (size_t)dim * 2, (size_t)n,
-		                   hipMemcpyDeviceToHost));
-		for (size_t i = 0; i < b.size(); ++i) {
-			const uint32_t u = (uint32_t)b[i] << 16;
-			memcpy(out + i, &u, 4);
-		}
-	}
-
-	// storage "f32" | "bf16"; only while the store holds no rows
-	void set_storage(bool bf16) {
-		if (n_slots > 0) throw Error("storage can only be changed on an empty table");
-		if (bf16 == xbf16) return;
-		if (X) {
-			HIPCHK(hipFree(X));
-			if (Xs) HIPCHK(hipFree(Xs));
-			Xs = nullptr;
-			HIPCHK(hipFree(rowaux));
-			HIPCHK(hipFree(dlabels));
-			if (rowaux_l2) HIPCHK(hipFree(rowaux_l2));
-			X = nullptr;
-			rowaux = rowaux_l2 = nullptr;
-			dlabels = nullptr;
-			cap = 0;
-		}
-		xbf16 = bf16;
-	}
-
-	int64_t slot_of(int64_t label) const {
-		auto it = std::lower_bound(slot_label.begin(), slot_label.end(), label);
-		if (it == slot_label.end() || *it != label) return -1;
-		return (int64_t)(it - slot_label.begin());
-	}
-
-	// returns the labels actually deleted (live before the call)
-	std::vector<int64_t> remove(const int64_t *labels, int64_t n) {
-		std::vector<int64_t> slots, done;
-		for (int64_t i = 0; i < n; ++i) {
-			int64_t s = slot_of(labels[i]);
-			if (s < 0 || !live[(size_t)s]) continue;
-			live[(size_t)s] = 0;
-			--n_live;
-			slots.push_back(s);
-			done.push_back(labels[i]);
-		}
-		if (!slots.empty()) {
-			ws.idx.need(slots.size());
-			HIPCHK(hipMemcpyAsync(ws.idx.p, slots.data(), slots.size() * sizeof(int64_t), hipMemcpyHostToDevice,
-			                      stream));
-			launch_tombstone(rowaux, ws.idx.p, (int)slots.size(), stream);
-			if (rowaux_l2) launch_tombstone(rowaux_l2, ws.idx.p, (int)slots.size(), stream);
-			HIPCHK(hipGetLastError());
-			HIPCHK(hipStreamSynchronize(stream));
-		}
-		return done;
-	}
-
-	void compact() {
-		if (n_live == n_slots) return;
-		std::vector<int64_t> keep;
-		keep.reserve((size_t)n_live);
-		for (int64_t s = 0; s < n_slots; ++s)
-			if (live[(size_t)s]) keep.push_back(s);
-		const int64_t n = (int64_t)keep.size();
-		const int64_t c = round_up(std::max<int64_t>(4096, n), SCAN_BR);
-		void *nX = nullptr;
-		float4 *na = nullptr, *na2 = nullptr;
-		int64_t *nl = nullptr;
-		HIPCHK(hipMalloc(&nX, (size_t)c * ld * xes()));
-		HIPCHK(hipMalloc(&na, (size_t)c * sizeof(float4)));
-		HIPCHK(hipMalloc(&nl, (size_t)c * sizeof(int64_t)));
-		if (rowaux_l2) HIPCHK(hipMalloc(&na2, (size_t)c * sizeof(float4)));
-		if (n > 0) {
-			ws.idx.need((size_t)n);
-			HIPCHK(hipMemcpyAsync(ws.idx.p, keep.data(), (size_t)n * sizeof(int64_t), hipMemcpyHostToDevice, stream));
-			launch_gather_rows(X, xbf16, rowaux, dlabels, ws.idx.p, n, ld, nX, na, nl, stream);
-			if (rowaux_l2) launch_gather_rows(X, xbf16, rowaux_l2, dlabels, ws.idx.p, n, ld, nX, na2, nl, stream);
-			HIPCHK(hipGetLastError());
-		}
-		HIPCHK(hipMemsetAsync(static_cast<uint8_t *>(nX) + (size_t)n * ld * xes(), 0, (size_t)(c - n) * ld * xes(),
-		                      stream));
-		launch_fill_rowaux(na, n, c, stream);
-		if (na2) launch_fill_rowaux(na2, n, c, stream);
-		uint16_t *nXs = nullptr;
-		if (Xs) {
-			HIPCHK(hipMalloc(&nXs, (size_t)c * ld * 2));
-			HIPCHK(hipMemsetAsync(nXs, 0, (size_t)c * ld * 2, stream));
-			if (n > 0)
-				launch_rows_to_bf16(static_cast<const float *>(nX), ld, n, dim, ld, nXs, stream);
-			HIPCHK(hipGetLastError());
-		}
-		HIPCHK(hipStreamSynchronize(stream));
-		if (Xs) HIPCHK(hipFree(Xs));
-		Xs = nXs;
-		HIPCHK(hipFree(X));
-		HIPCHK(hipFree(rowaux));
-		HIPCHK(hipFree(dlabels));
-		if (rowaux_l2) HIPCHK(hipFree(rowaux_l2));
-		X = nX;
-		rowaux = na;
-		dlabels = nl;
-		rowaux_l2 = na2;
-		cap = c;
-		std::vector<int64_t> nsl;
-		nsl.reserve((size_t)n);
-		for (int64_t s : keep) nsl.push_back(slot_label[(size_t)s]);
-		slot_label.swap(nsl);
-		live.assign((size_t)n, 1);
-		n_slots = n;
-		n_live = n;
-	}
-
-	// ---- persistence: append-only log <db_path>/<table>.lancehip ----------
-	std::string log_path() const { return db_path + "/" + table + ".lancehip"; }
-
-	void log_open(bool truncate) {
-		if (db_path.empty()) return;
-		// mkdir -p db_path
-		std::string acc;
-		for (size_t i = 0; i <= db_path.size(); ++i) {
-			if (i == db_path.size() || db_path[i] == '/') {
-				if (!acc.empty() && acc != "/") (void)mkdir(acc.c_str(), 0755);
-			}
-			if (i < db_path.size()) acc.push_back(db_path[i]);
-		}
-		log = fopen(log_path().c_str(), truncate ? "wb" : "ab");
-		if (!log) throw Error("cannot open " + log_path() + ": " + strerror(errno));
-		if (truncate) {
-			fwrite("LHIPLOG1", 1, 8, log);
-			int32_t d = dim;
-			fwrite(&d, 4, 1, log);
-			fflush(log);
-		}
-	}
-	void log_add(int64_t first, const float *v, int64_t num) {
-		if (!log) return;
-		uint8_t tag = 1;
-		fwrite(&tag, 1, 1, log);
-		fwrite(&first, 8, 1, log);
-		fwrite(&num, 8, 1, log);
-		fwrite(v, sizeof(float), (size_t)num * dim, log);
-		fflush(log);
-	}
-	void log_storage() {
-		if (!log) return;
-		uint8_t tag = 3, v = xbf16 ? 1 : 0;
-		fwrite(&tag, 1, 1, log);
-		fwrite(&v, 1, 1, log);
-		fflush(log);
-	}
-	void log_del(const std::vector<int64_t> &labs) {
-		if (!log || labs.empty()) return;
-		uint8_t tag = 2;
-		int64_t n = (int64_t)labs.size();
-		fwrite(&tag, 1, 1, log);
-		fwrite(&n, 8, 1, log);
-		fwrite(labs.data(), 8, labs.size(), log);
-		fflush(log);
-	}
-
-	// ---- search ------------------------------------------------------------
-	// Device-side batched search; dQ [nq][dim] (device), outputs device.
-	void search_device(const float *dQ, int nq, int k, int refine, int64_t *dL, float *dD, int *dC);
-	void search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL, float *dD, int *dC);
-};
 
 void Index::search_device(const float *dQ, int nq, int k, int refine, int64_t *dL, float *dD, int *dC) {
 	last_stats[0] = last_stats[1] = last_stats[2] = last_stats[3] = 0;
@@ -684,12 +201,29 @@ static void replay_log(Index *ix, const std::string &path) {
 			std::vector<int64_t> labs((size_t)n);
 			if (fread(labs.data(), 8, (size_t)n, f) != (size_t)n) break;
 			ix->remove(labs.data(), n);
+		} else if (tag == 4) {
+			// IVF model (lance_detached_create_index): re-index the rows present
+			// at that point of the log with the persisted centroids / codebook
+			int32_t hdr[3];
+			if (fread(hdr, 4, 3, f) != 3) break;
+			const int type = hdr[0], nl = hdr[1], m = hdr[2];
+			if (nl <= 0 || (type == IVF_PQ && (m <= 0 || d % m != 0))) break;
+			std::vector<float> C((size_t)nl * d), cb;
+			if (fread(C.data(), sizeof(float), C.size(), f) != C.size()) break;
+			if (type == IVF_PQ) {
+				cb.resize((size_t)m * PQ_K * (d / m));
+				if (fread(cb.data(), sizeof(float), cb.size(), f) != cb.size()) break;
+			}
+			ivf_set_model(ix, type, nl, m, C.data(), type == IVF_PQ ? cb.data() : nullptr);
+		} else if (tag == 5) {
+			ix->compact();
+			ivf_optimize(ix);
 		} else {
 			break;
 		}
 	}
 	fclose(f);
-	ix->compact();
+	ix->compact();  // rows added after the last create_index / optimize stay unindexed
 	// next_label = MAX(label)+1 over live rows, 0 when empty (lance_manager.rs:157-158, :662-696)
 	int64_t mx = -1;
 	for (int64_t s = 0; s < ix->n_slots; ++s)
@@ -935,7 +469,8 @@ int32_t lance_detached_search_batch(void *handle, const float *queries, int32_t 
 		ws.out_d.need((size_t)nq * k);
 		ws.out_c.need((size_t)nq);
 		HIPCHK(hipMemcpyAsync(ws.Qin.p, queries, (size_t)nq * dim * sizeof(float), hipMemcpyHostToDevice, ix->stream));
-		ix->search_device(ws.Qin.p, nq, k, refine_factor, ws.out_l.p, ws.out_d.p, ws.out_c.p);
+		HIPCHK(hipStreamSynchronize(ix->stream));
+		ix->search_any(ws.Qin.p, nq, k, nprobes, refine_factor, ws.out_l.p, ws.out_d.p, ws.out_c.p);
 		HIPCHK(hipMemcpyAsync(out_labels, ws.out_l.p, (size_t)nq * k * sizeof(int64_t), hipMemcpyDeviceToHost,
 		                      ix->stream));
 		HIPCHK(hipMemcpyAsync(out_distances, ws.out_d.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost,
@@ -1026,11 +561,15 @@ int32_t lance_detached_create_index(void *handle, int32_t num_partitions, int32_
 		lhip::write_err(err_buf, err_buf_len, "null handle");
 		return -1;
 	}
-	Index *ix = as_index(handle);
-	std::lock_guard<std::mutex> g(ix->mu);
-	ix->ivf_partitions = num_partitions;
-	ix->ivf_sub_vectors = num_sub_vectors;
-	return 0;
+	try {
+		Index *ix = as_index(handle);
+		std::lock_guard<std::mutex> g(ix->mu);
+		ix->bind();
+		lhip::ivf_build(ix, ix->ivf_type_opt, num_partitions, num_sub_vectors);
+		ix->log_model();
+		return 0;
+	}
+	API_GUARD("create_index failed: ", -1)
 }
 
 int32_t lance_detached_create_hnsw_index(void *handle, int32_t m, int32_t ef_construction, char *err_buf,
@@ -1052,6 +591,10 @@ int32_t lance_detached_compact(void *handle, char *err_buf, int err_buf_len) {
 		std::lock_guard<std::mutex> g(ix->mu);
 		ix->bind();
 		ix->compact();
+		if (ix->ivf) {
+			lhip::ivf_optimize(ix);  // optimize(All): unindexed rows join the partitions
+			ix->log_optimize();
+		}
 		return 0;
 	}
 	API_GUARD("compact failed: ", -1)
@@ -1170,6 +713,25 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			ix->sample_div = d;
 			return 0;
 		}
+		if (k == "index_type") {
+			if (v == "ivf_pq" || v == "IVF_PQ")
+				ix->ivf_type_opt = lhip::IVF_PQ;
+			else if (v == "ivf_flat" || v == "IVF_FLAT")
+				ix->ivf_type_opt = lhip::IVF_FLAT;
+			else
+				throw Error("index_type must be 'ivf_pq' or 'ivf_flat'");
+			return 0;
+		}
+		if (k == "kmeans_iters") {
+			const int it = std::stoi(v);
+			if (it < 0) throw Error("kmeans_iters must be >= 0");
+			ix->kmeans_iters = it;
+			return 0;
+		}
+		if (k == "ivf_seed") {
+			ix->ivf_seed = std::stoull(v);
+			return 0;
+		}
 		if (k == "reserve_rows") {
 			ix->bind();
 			ix->reserve(std::stoll(v));
@@ -1247,7 +809,7 @@ int32_t lance_hip_search_batch_device(void *handle, const float *d_queries, int3
 			HIPCHK(hipStreamSynchronize(ix->stream));
 			return nq;
 		}
-		ix->search_device(d_queries, nq, k, refine_factor, d_out_labels, d_out_distances, d_out_counts);
+		ix->search_any(d_queries, nq, k, nprobes, refine_factor, d_out_labels, d_out_distances, d_out_counts);
 		return nq;
 	}
 	API_GUARD("search failed: ", -1)
@@ -1306,6 +868,66 @@ int32_t lance_hip_merge_topk_device(int32_t nshard, int32_t nq, int32_t k, const
 		return nq;
 	}
 	API_GUARD("merge_topk failed: ", -1)
+}
+
+// ---- IVF model / layout (multi-GPU model broadcast, parity tests) ----------
+
+int32_t lance_hip_ivf_info(void *handle, int64_t *out, int32_t n) {
+	if (!handle || !out) return -1;
+	Index *ix = as_index(handle);
+	std::lock_guard<std::mutex> g(ix->mu);
+	int64_t v[6] = {-1, 0, 0, 0, 0, ix->n_slots};
+	if (ix->ivf) {
+		v[0] = ix->ivf->type;
+		v[1] = ix->ivf->nlist;
+		v[2] = ix->ivf->m;
+		v[3] = ix->ivf->dsub;
+		v[4] = ix->ivf->n_indexed;
+	}
+	for (int32_t i = 0; i < n && i < 6; ++i) out[i] = v[i];
+	return 0;
+}
+
+int32_t lance_hip_ivf_export(void *handle, float *centroids, float *codebook, int64_t *slot_labels,
+                             uint8_t *slot_live, int32_t *slot_list, uint8_t *slot_codes, char *err_buf,
+                             int err_buf_len) {
+	if (!handle) {
+		lhip::write_err(err_buf, err_buf_len, "null handle");
+		return -1;
+	}
+	try {
+		Index *ix = as_index(handle);
+		std::lock_guard<std::mutex> g(ix->mu);
+		if (!ix->ivf) throw Error("no IVF index");
+		ix->bind();
+		lhip::ivf_export_model(ix, centroids, codebook);
+		lhip::ivf_export_slots(ix, slot_list, slot_codes);
+		for (int64_t s = 0; s < ix->n_slots; ++s) {
+			if (slot_labels) slot_labels[s] = ix->slot_label[(size_t)s];
+			if (slot_live) slot_live[s] = ix->live[(size_t)s];
+		}
+		return 0;
+	}
+	API_GUARD("ivf_export failed: ", -1)
+}
+
+int32_t lance_hip_ivf_set_model(void *handle, int32_t index_type, int32_t num_partitions, int32_t num_sub_vectors,
+                                const float *centroids, const float *codebook, char *err_buf, int err_buf_len) {
+	if (!handle) {
+		lhip::write_err(err_buf, err_buf_len, "null handle");
+		return -1;
+	}
+	try {
+		Index *ix = as_index(handle);
+		std::lock_guard<std::mutex> g(ix->mu);
+		if (index_type != lhip::IVF_FLAT && index_type != lhip::IVF_PQ) throw Error("index_type must be 0 or 1");
+		if (!centroids) throw Error("null centroids");
+		ix->bind();
+		lhip::ivf_set_model(ix, index_type, num_partitions, num_sub_vectors, centroids, codebook);
+		ix->log_model();
+		return 0;
+	}
+	API_GUARD("ivf_set_model failed: ", -1)
 }
 
 }  // extern "C"

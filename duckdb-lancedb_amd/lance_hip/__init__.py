@@ -76,6 +76,10 @@ _SIGNATURES = [
     ("lance_hip_kernel_times", i32, [c_void_p, c_void_p, i32]),
     ("lance_hip_merge_topk_device", i32,
      [i32, i32, i32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_char_p, c_int]),
+    ("lance_hip_ivf_info", i32, [c_void_p, c_void_p, i32]),
+    ("lance_hip_ivf_export", i32,
+     [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_char_p, c_int]),
+    ("lance_hip_ivf_set_model", i32, [c_void_p, i32, i32, i32, c_void_p, c_void_p, c_char_p, c_int]),
 ]
 
 EXPORTED_SYMBOLS = [s[0] for s in _SIGNATURES]
@@ -322,6 +326,58 @@ def LanceHipKernelTimes(handle) -> dict:
     return {"scan_ms_total": float(out[0]), "scan_launches": int(out[1]), "scan_rows": int(out[2]),
             "scan_qpad": int(out[3]), "dense_ms_total": float(out[4]), "dense_launches": int(out[5]),
             "scan_elem_bytes": int(out[6])}
+
+
+IVF_TYPES = {-1: None, 0: "ivf_flat", 1: "ivf_pq"}
+
+
+def LanceHipIvfInfo(handle) -> dict:
+    """IVF state of a handle: type (None when the table has no index), nlist,
+    m (sub-vectors), dsub, rows indexed, slots."""
+    out = np.zeros(6, np.int64)
+    lib().lance_hip_ivf_info(handle, out.ctypes.data, 6)
+    return {"type": IVF_TYPES[int(out[0])], "nlist": int(out[1]), "m": int(out[2]), "dsub": int(out[3]),
+            "n_indexed": int(out[4]), "n_slots": int(out[5])}
+
+
+def LanceHipIvfExport(handle) -> dict:
+    """Host copy of the IVF model and of the per-slot layout (for the oracle):
+    centroids [nlist, dim], codebook [m, 256, dsub] (IVF_PQ), and per slot:
+    label, live flag, list (-1 = not indexed yet), codes [m]."""
+    info = LanceHipIvfInfo(handle)
+    if info["type"] is None:
+        raise IOException("Lance ivf_export: no IVF index")
+    dim = LanceDetachedDimension(handle)
+    ns = info["n_slots"]
+    C = np.zeros((info["nlist"], dim), np.float32)
+    pq = info["type"] == "ivf_pq"
+    cb = np.zeros((info["m"], 256, info["dsub"]), np.float32) if pq else None
+    labels = np.zeros(ns, np.int64)
+    live = np.zeros(ns, np.uint8)
+    lists = np.zeros(ns, np.int32)
+    codes = np.zeros((ns, max(info["m"], 1)), np.uint8)
+    e = _err()
+    r = lib().lance_hip_ivf_export(handle, C.ctypes.data, cb.ctypes.data if pq else None, labels.ctypes.data,
+                                   live.ctypes.data, lists.ctypes.data, codes.ctypes.data if pq else None, e,
+                                   ERR_BUF_LEN)
+    if r != 0:
+        raise IOException("Lance ivf_export: " + e.value.decode())
+    return {**info, "centroids": C, "codebook": cb, "labels": labels, "live": live.astype(bool), "lists": lists,
+            "codes": codes if pq else None}
+
+
+def LanceHipIvfSetModel(handle, index_type: str, centroids, codebook=None) -> None:
+    """Install a trained IVF model (rank 0's, on every rank) and index this
+    handle's rows with it."""
+    C = np.ascontiguousarray(centroids, dtype=np.float32)
+    t = {"ivf_flat": 0, "ivf_pq": 1}[index_type]
+    cb = None if codebook is None else np.ascontiguousarray(codebook, dtype=np.float32)
+    m = 0 if cb is None else cb.shape[0]
+    e = _err()
+    r = lib().lance_hip_ivf_set_model(handle, t, C.shape[0], m, C.ctypes.data, None if cb is None else cb.ctypes.data,
+                                      e, ERR_BUF_LEN)
+    if r != 0:
+        raise IOException("Lance ivf_set_model: " + e.value.decode())
 
 
 def LanceHipMergeTopk(part_labels, part_dists, part_counts):

@@ -111,8 +111,13 @@ int32_t lance_detached_delete_batch(void *handle, const int64_t *labels, int32_t
 
 /* ---- ANN index / maintenance --------------------------------------------- */
 
-/* ffi.rs:403-423 (rust_ffi.cpp:168).  IVF build: not in this build yet; the
- * flat path stays exact, so this returns 0 and records the parameters. */
+/* ffi.rs:403-423 (rust_ffi.cpp:168), lance_manager.rs:483-515.  Trains and
+ * builds an IVF index over the live rows (replace = true): IVF_PQ (default, as
+ * the reference builds) or IVF_FLAT (option "index_type").  num_partitions /
+ * num_sub_vectors <= 0 take LanceDB's defaults (sqrt(rows); dim/16, dim/8 or 1).
+ * Later searches probe `nprobes` partitions and re-rank k*refine_factor PQ
+ * candidates exactly; rows added afterwards are searched exactly until
+ * lance_detached_compact (= optimize) indexes them.  0 or -1. */
 int32_t lance_detached_create_index(void *handle, int32_t num_partitions, int32_t num_sub_vectors, char *err_buf,
                                     int err_buf_len);
 
@@ -160,6 +165,9 @@ int32_t lance_hip_device_count(void);
  *                  f32 rows, results are unchanged
  *   "sample_div"   the threshold sample pass covers ~1/sample_div of the row
  *                  tiles (at least 32 tiles); default "32"
+ *   "index_type"   "ivf_pq" (default) | "ivf_flat": what create_index builds
+ *   "kmeans_iters" k-means iterations (coarse and PQ), default "50"
+ *   "ivf_seed"     seed of the k-means training sample, default 24301
  *   "time_kernels" "1" = record HIP events around scan launches
  *                  (lance_hip_kernel_times); default "0"
  * The handle is bound to the HIP device current when it was created.
@@ -204,6 +212,24 @@ int32_t lance_hip_merge_topk_device(int32_t nshard, int32_t nq, int32_t k, const
 int32_t lance_hip_merge_topk(int32_t nshard, int32_t nq, int32_t k, const int64_t *part_labels,
                              const float *part_dists, const int32_t *part_counts, int64_t *out_labels,
                              float *out_dists, int32_t *out_counts, char *err_buf, int err_buf_len);
+
+/* NEW — IVF state: out[0] type (-1 none, 0 IVF_FLAT, 1 IVF_PQ), out[1] nlist,
+ * out[2] m, out[3] dsub, out[4] rows indexed, out[5] slots.  0 or -1. */
+int32_t lance_hip_ivf_info(void *handle, int64_t *out, int32_t n);
+
+/* NEW — host copy of the IVF model and per-slot layout (any pointer may be
+ * NULL): centroids [nlist][dim], codebook [m][256][dsub], and for every slot
+ * (the ascending-label storage order, deleted rows included until compaction):
+ * label, live flag, list (-1 = not indexed yet), codes [m].  0 or -1. */
+int32_t lance_hip_ivf_export(void *handle, float *centroids, float *codebook, int64_t *slot_labels,
+                             uint8_t *slot_live, int32_t *slot_list, uint8_t *slot_codes, char *err_buf,
+                             int err_buf_len);
+
+/* NEW — install a trained model (multi-GPU: rank 0 trains, every rank indexes
+ * its shard with the same centroids / codebook).  index_type 0 IVF_FLAT, 1
+ * IVF_PQ; codebook [m][256][dim/m] (NULL for IVF_FLAT).  0 or -1. */
+int32_t lance_hip_ivf_set_model(void *handle, int32_t index_type, int32_t num_partitions, int32_t num_sub_vectors,
+                                const float *centroids, const float *codebook, char *err_buf, int err_buf_len);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,168 @@
+"""CPU ORACLE for the IVF_FLAT / IVF_PQ search — test infrastructure only.
+
+Only ``tests/`` (and ``bench.py``'s recall check) may use this module, and only
+as the *checker*; the product path is the HIP library
+(``duckdb-lancedb_amd/csrc/ivf_index.cpp`` + ``ivf_kernels.hip``).
+
+What it restates (reference paths relative to ``/root/reference``):
+
+* ``rust_lib/src/lance_manager.rs:411-418`` — ``vector_search(q).limit(k)
+  .nprobes(n).refine_factor(r)`` on a table with an IVF_PQ index
+  (``:483-515``): probe the ``n`` partitions nearest to the query, rank the
+  rows of those partitions by their PQ (ADC) distance, re-rank the best
+  ``k * r`` exactly and return the top ``k``; rows not covered by the index
+  yet are searched exactly (LanceDB scans unindexed fragments flat) and merged.
+* the published algorithms of the third-party ``lance-index 0.22.0`` (IVF
+  partition search, residual product quantisation with 8-bit codes and an
+  asymmetric-distance lookup table); the crate source is not in the container,
+  so parity with LanceDB itself is UNPINNED for IVF (no reference test builds
+  or searches an IVF index) and this oracle pins the HIP path to
+  the build's own canonical numerics, given the same trained model:
+
+  coarse    exact distances (f64 accumulate, f32 result) to the centroids —
+            dot for a dot index, L2 otherwise (cosine: L2 between the
+            normalised query and the centroids) — top-nprobe by (dist, id)
+  IVF_FLAT  exact distance of every live row of the probed lists
+  IVF_PQ    ADC = d0 + sum_j LUT[j][code_j] in f32, j ascending, d0 = the
+            coarse distance; LUT = T[l] - 2 P[q] (L2/cosine) or -P[q] (dot),
+            P[j][c] = sum_t q_t y_t, T[l][j][c] = sum_t y_t (y_t + 2 c_t), each
+            an f32 sum in t order of f32 products (no fused multiply-add);
+            top-(k*r) by (ADC, label), exact re-rank, top-k by (dist, label)
+  cosine    q^ = q / f32(sqrt(sum q^2)) (an f32 division) for the coarse
+            search and P; the final distances are exact cosine distances.
+
+The model (centroids, codebook) and the layout (list and codes of every row)
+come from the library (``lance_hip_ivf_export``): training is checked
+separately (assignments near-nearest, recall).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import flat_knn
+
+F32 = np.float32
+
+
+def normalize_queries(Q):
+    """q^ = q / f32(sqrt(f64 sum q^2)) per row (zero rows unchanged)."""
+    Q = np.asarray(Q, F32)
+    nrm = np.sqrt(np.einsum("ij,ij->i", Q.astype(np.float64), Q.astype(np.float64))).astype(F32)
+    out = Q.copy()
+    nz = nrm > 0
+    out[nz] = (Q[nz] / nrm[nz, None]).astype(F32)
+    return out
+
+
+def coarse_probes(C, Q, metric, nprobe):
+    """Top-``nprobe`` partitions per query: (ids [nq, nprobe], dists f32)."""
+    metric = flat_knn.normalize_metric(metric)
+    cm = "dot" if metric == "dot" else "l2"
+    Qc = normalize_queries(Q) if metric == "cosine" else np.asarray(Q, F32)
+    nl = C.shape[0]
+    nprobe = min(nprobe, nl)
+    ids = np.zeros((Qc.shape[0], nprobe), np.int64)
+    ds = np.zeros((Qc.shape[0], nprobe), F32)
+    lab = np.arange(nl, dtype=np.int64)
+    for i, q in enumerate(Qc):
+        d = flat_knn.exact_distances(C, q, cm)
+        o = flat_knn._order(d, lab)[:nprobe]
+        ids[i], ds[i] = o, d[o]
+    return ids, ds
+
+
+def _topk_exact(X, labels, slots, q, k, metric):
+    if slots.size == 0:
+        return np.zeros(0, np.int64), np.zeros(0, F32)
+    d = flat_knn.exact_distances(X[slots], q, metric)
+    o = flat_knn._order(d, labels[slots])[:k]
+    return slots[o], d[o]
+
+
+def ivf_flat_search(X, labels, live, lists, C, Q, k, nprobe, metric="l2"):
+    """IVF_FLAT: exact top-k over the live rows of the probed lists plus the
+    live rows not indexed yet (``lists == -1``).  X / labels / live / lists
+    are per slot (ascending labels).  Returns (labels [nq,k] -1 padded,
+    dists [nq,k] NaN padded, counts)."""
+    X = np.asarray(X, F32)
+    labels = np.asarray(labels, np.int64)
+    live = np.asarray(live, bool)
+    lists = np.asarray(lists, np.int64)
+    probes, _ = coarse_probes(C, Q, metric, nprobe)
+    nq = len(Q)
+    out_l = np.full((nq, k), -1, np.int64)
+    out_d = np.full((nq, k), np.nan, F32)
+    cnt = np.zeros(nq, np.int32)
+    tail = live & (lists < 0)
+    for i, q in enumerate(np.asarray(Q, F32)):
+        sel = live & np.isin(lists, probes[i])
+        slots = np.nonzero(sel | tail)[0]
+        s, d = _topk_exact(X, labels, slots, q, k, metric)
+        n = len(s)
+        out_l[i, :n], out_d[i, :n], cnt[i] = labels[s], d, n
+    return out_l, out_d, cnt
+
+
+def pq_tables(C, codebook, Qp, metric):
+    """P [nq, m, 256] and T [nlist, m, 256] (None for dot) per the canonical
+    f32 sequential definitions."""
+    cb = np.asarray(codebook, F32)
+    m, K, dsub = cb.shape
+    Qp = np.asarray(Qp, F32).reshape(len(Qp), m, dsub)
+    P = np.zeros((len(Qp), m, K), F32)
+    for t in range(dsub):
+        P = (P + (Qp[:, :, t][:, :, None] * cb[None, :, :, t]).astype(F32)).astype(F32)
+    T = None
+    if flat_knn.normalize_metric(metric) != "dot":
+        Cr = np.asarray(C, F32).reshape(len(C), m, dsub)
+        T = np.zeros((len(C), m, K), F32)
+        for t in range(dsub):
+            y = cb[None, :, :, t]
+            twoc = (F32(2.0) * Cr[:, :, t])[:, :, None]
+            T = (T + (y * (y + twoc).astype(F32)).astype(F32)).astype(F32)
+    return P, T
+
+
+def ivf_pq_search(X, labels, live, lists, codes, C, codebook, Q, k, nprobe, refine_factor=1, metric="l2"):
+    """IVF_PQ search (see the module docstring).  ``codes`` [slots, m] uint8."""
+    metric = flat_knn.normalize_metric(metric)
+    X = np.asarray(X, F32)
+    labels = np.asarray(labels, np.int64)
+    live = np.asarray(live, bool)
+    lists = np.asarray(lists, np.int64)
+    codes = np.asarray(codes, np.uint8)
+    Q = np.asarray(Q, F32)
+    probes, pd = coarse_probes(C, Q, metric, nprobe)
+    Qp = normalize_queries(Q) if metric == "cosine" else Q
+    P, T = pq_tables(C, codebook, Qp, metric)
+    m = codes.shape[1]
+    kp = k * max(1, refine_factor)
+    nq = len(Q)
+    out_l = np.full((nq, k), -1, np.int64)
+    out_d = np.full((nq, k), np.nan, F32)
+    cnt = np.zeros(nq, np.int32)
+    tail = np.nonzero(live & (lists < 0))[0]
+    for i in range(nq):
+        cand_adc, cand_slot = [], []
+        for p, l in enumerate(probes[i]):
+            rows = np.nonzero(live & (lists == l))[0]
+            if rows.size == 0:
+                continue
+            lut = (T[l] - F32(2.0) * P[i]).astype(F32) if T is not None else (-P[i]).astype(F32)
+            acc = np.full(rows.size, pd[i, p], F32)
+            for j in range(m):
+                acc = (acc + lut[j, codes[rows, j]]).astype(F32)
+            cand_adc.append(acc)
+            cand_slot.append(rows)
+        sel = np.zeros(0, np.int64)
+        if cand_adc:
+            a = np.concatenate(cand_adc)
+            s = np.concatenate(cand_slot)
+            o = flat_knn._order(a, labels[s])[:kp]
+            sel = s[o]
+        ts, _ = _topk_exact(X, labels, tail, Q[i], k, metric)
+        allc = np.concatenate([sel, ts])
+        s, d = _topk_exact(X, labels, allc, Q[i], k, metric)
+        n = len(s)
+        out_l[i, :n], out_d[i, :n], cnt[i] = labels[s], d, n
+    return out_l, out_d, cnt

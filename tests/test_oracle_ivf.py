@@ -1,0 +1,70 @@
+"""CPU checks of the IVF oracle (oracle/ivf.py) — the checker the GPU IVF
+tests compare against: with every list probed IVF_FLAT is the exact flat
+search, and IVF_PQ with a re-rank window covering every row is too; the ADC
+tables follow their f32 definitions."""
+import numpy as np
+
+from oracle import flat_knn, ivf
+
+
+def _model(rng, n, d, nlist, m):
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    C = X[rng.choice(n, nlist, replace=False)].copy()
+    lists = np.argmin(((X[:, None, :] - C[None]) ** 2).sum(-1), 1)
+    cb = rng.standard_normal((m, 256, d // m)).astype(np.float32) * 0.3
+    R = X - C[lists]
+    codes = np.stack([np.argmin(((R[:, j * (d // m):(j + 1) * (d // m)][:, None, :] - cb[j][None]) ** 2).sum(-1), 1)
+                      for j in range(m)], 1).astype(np.uint8)
+    return X, C, lists, cb, codes
+
+
+def test_flat_all_probes_equals_flat_search():
+    rng = np.random.default_rng(0)
+    X, C, lists, _, _ = _model(rng, 600, 16, 12, 4)
+    Q = rng.standard_normal((9, 16)).astype(np.float32)
+    n = len(X)
+    live = np.ones(n, bool)
+    live[::5] = False
+    lab = np.arange(n)
+    for metric in ("l2", "dot", "cosine"):
+        gl, gd, gc = ivf.ivf_flat_search(X, lab, live, lists, C, Q, 7, 12, metric)
+        el, ed, ec = flat_knn.flat_search_batch(X, lab, live, Q, 7, metric)
+        np.testing.assert_array_equal(gl, el)
+        np.testing.assert_array_equal(gc, ec)
+
+
+def test_pq_full_window_is_exact_and_tail_merges():
+    rng = np.random.default_rng(1)
+    X, C, lists, cb, codes = _model(rng, 500, 16, 8, 4)
+    Q = rng.standard_normal((6, 16)).astype(np.float32)
+    lab = np.arange(len(X))
+    live = np.ones(len(X), bool)
+    lists = lists.copy()
+    lists[450:] = -1  # the unindexed tail
+    gl, gd, gc = ivf.ivf_pq_search(X, lab, live, lists, codes, C, cb, Q, 5, 8, refine_factor=100)
+    el, ed, ec = flat_knn.flat_search_batch(X, lab, live, Q, 5)
+    np.testing.assert_array_equal(gl, el)
+    np.testing.assert_array_equal(gd, ed)
+
+
+def test_pq_tables_definition():
+    rng = np.random.default_rng(2)
+    _, C, _, cb, _ = _model(rng, 100, 8, 3, 2)
+    q = rng.standard_normal((1, 8)).astype(np.float32)
+    P, T = ivf.pq_tables(C, cb, q, "l2")
+    j, c, l = 1, 17, 2
+    acc = np.float32(0)
+    for t in range(4):
+        acc = np.float32(acc + np.float32(q[0, j * 4 + t] * cb[j, c, t]))
+    assert P[0, j, c] == acc
+    acc = np.float32(0)
+    for t in range(4):
+        y = cb[j, c, t]
+        acc = np.float32(acc + np.float32(y * np.float32(y + np.float32(2) * C[l, j * 4 + t])))
+    assert T[l, j, c] == acc
+    # L2 ADC approximates |q - c - y|^2 (T - 2P adds |q - c|^2 back through d0)
+    y = cb[:, 0, :].reshape(-1)
+    exact = ((q[0] - C[l] - y) ** 2).sum()
+    d0 = ((q[0] - C[l]) ** 2).sum()
+    adc = d0 + sum((T[l, jj, 0] - 2 * P[0, jj, 0]) for jj in range(2))
+    assert abs(adc - exact) < 1e-3 * max(1.0, exact)
