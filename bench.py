@@ -43,7 +43,16 @@ MFMA_BF16_PEAK_TFS = 2500.0  # dense bf16 MFMA (no sparsity), same table
 CONFIGS = {
     "c2": dict(n=1_000_000, dim=768, k=10, batch=256, metric="l2", storage="f32", normalize=False),
     "c3": dict(n=10_000_000, dim=768, k=100, batch=256, metric="dot", storage="bf16", normalize=True),
+    # IVF configs: n is ROWS PER GPU (the 8-GPU configs of BASELINE.json hold 100M rows,
+    # 12.5M per GPU; --gpus N runs N such shards), clustered synthetic rows
+    "c4": dict(n=12_500_000, dim=768, k=10, batch=256, metric="l2", storage="f32", normalize=False,
+               index_type="ivf_flat", nlist=4096, nprobe=64, m=0, refine=1),
+    "c5": dict(n=12_500_000, dim=768, k=10, batch=256, metric="l2", storage="f32", normalize=False,
+               index_type="ivf_pq", nlist=4096, nprobe=64, m=96, refine=10),
 }
+# clustered synthetic data of the IVF configs: NCENT Gaussian clusters, centers
+# N(0, 1) per dim (seed CENT_SEED), rows = center + SIGMA * N(0, 1)
+NCENT, SIGMA, CENT_SEED = 1024, 1.0, 777
 GEN_CHUNK = 65536
 
 
@@ -65,10 +74,16 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-recall", action="store_true")
     ap.add_argument("--sample-div", type=int, default=None, help="index option sample_div (default: library's)")
+    ap.add_argument("--nlist", type=int, default=None, help="IVF configs: num_partitions")
+    ap.add_argument("--nprobe", type=int, default=None, help="IVF configs: nprobes")
+    ap.add_argument("--m", type=int, default=None, help="IVF_PQ: num_sub_vectors")
+    ap.add_argument("--refine", type=int, default=None, help="IVF configs: refine_factor")
     a = ap.parse_args()
     for key, v in CONFIGS[a.config].items():
         if getattr(a, key, None) is None:
             setattr(a, key, v)
+    if not hasattr(a, "index_type"):
+        a.index_type = None
     return a
 
 
@@ -86,6 +101,28 @@ def gen_rows(start, stop, dim, device, seed=1234, normalize=False):
         out[lo - start:hi - start] = chunk[lo - c * GEN_CHUNK:hi - c * GEN_CHUNK]
     if normalize:
         out /= torch.linalg.vector_norm(out, dim=1, keepdim=True)
+    return out
+
+
+def cluster_centers(dim, device):
+    g = torch.Generator(device=device)
+    g.manual_seed(CENT_SEED)
+    return torch.randn((NCENT, dim), generator=g, device=device, dtype=torch.float32)
+
+
+def gen_clustered(start, stop, dim, device, centers, seed=1234):
+    """Rows [start, stop) of the clustered base (IVF configs); chunk c from
+    generator seed (seed, c) whatever the sharding."""
+    out = torch.empty((stop - start, dim), dtype=torch.float32, device=device)
+    c0, c1 = start // GEN_CHUNK, (stop - 1) // GEN_CHUNK
+    g = torch.Generator(device=device)
+    for c in range(c0, c1 + 1):
+        g.manual_seed(seed * 1_000_003 + c)
+        ids = torch.randint(0, NCENT, (GEN_CHUNK,), generator=g, device=device)
+        chunk = torch.randn((GEN_CHUNK, dim), generator=g, device=device, dtype=torch.float32)
+        chunk.mul_(SIGMA).add_(centers[ids])
+        lo, hi = max(start, c * GEN_CHUNK), min(stop, (c + 1) * GEN_CHUNK)
+        out[lo - start:hi - start] = chunk[lo - c * GEN_CHUNK:hi - c * GEN_CHUNK]
     return out
 
 
@@ -111,8 +148,183 @@ def err_buf():
     return ctypes.create_string_buffer(2048)
 
 
+def main_ivf(a):
+    """IVF configs (C4 IVF-Flat / C5 IVF-PQ of BASELINE.json): every rank holds
+    a shard of a.n rows (the 8-GPU configs' 100M rows = 8 x 12.5M), rank 0
+    trains the model (lance_detached_create_index), the others install it
+    (lance_hip_ivf_set_model) and index their shard; one step = one batch of
+    a.batch x world queries through lance_hip_search_batch_device with nprobes /
+    refine_factor, per-shard top-k all-gathered and merged on the device."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+    L = lance_hip.lib()
+    N, D, K, B = a.n, a.dim, a.k, a.batch
+    s0 = rank * N  # global label offset of this shard
+    e = err_buf()
+    h = L.lance_create_detached(b"", D, a.metric.encode(), b"bench_ivf", e, 2048)
+    if not h:
+        raise RuntimeError(e.value.decode())
+    lance_hip.LanceHipSetOption(h, "storage", a.storage)
+    lance_hip.LanceHipSetOption(h, "scan_copy", "off")
+    lance_hip.LanceHipSetOption(h, "reserve_rows", str(N))
+    lance_hip.LanceHipSetOption(h, "index_type", a.index_type)
+    centers = cluster_centers(D, dev)
+    t_gen = time.perf_counter()
+    for lo in range(s0, s0 + N, 1 << 18):
+        hi = min(s0 + N, lo + (1 << 18))
+        X = gen_clustered(lo, hi, D, dev, centers)
+        torch.cuda.synchronize()
+        if L.lance_hip_add_batch_device(h, X.data_ptr(), hi - lo, D, e, 2048) < 0:
+            raise RuntimeError(e.value.decode())
+        del X
+    t_build = time.perf_counter()
+    if rank == 0:
+        if L.lance_detached_create_index(h, a.nlist, a.m, e, 2048) != 0:
+            raise RuntimeError(e.value.decode())
+    if world > 1:
+        nsub = a.m if a.index_type == "ivf_pq" else 0
+        dsub = D // nsub if nsub else 0
+        Cm = torch.empty((a.nlist, D), dtype=torch.float32, device=dev)
+        CB = torch.empty((max(nsub, 1), 256, max(dsub, 1)), dtype=torch.float32, device=dev)
+        if rank == 0:
+            ex = lance_hip.LanceHipIvfExport(h)
+            Cm.copy_(torch.from_numpy(ex["centroids"]))
+            if nsub:
+                CB.copy_(torch.from_numpy(ex["codebook"]))
+        dist.broadcast(Cm, 0)
+        dist.broadcast(CB, 0)
+        if rank != 0:
+            lance_hip.LanceHipIvfSetModel(h, a.index_type, Cm.cpu().numpy(), CB.cpu().numpy() if nsub else None)
+    torch.cuda.synchronize()
+    build_s = time.perf_counter() - t_build
+    gen_s = t_build - t_gen
+    g = torch.Generator(device=dev)
+    g.manual_seed(5678)
+    BG = B * world
+    qids = torch.randint(0, NCENT, (BG,), generator=g, device=dev)
+    Q = (centers[qids] + SIGMA * torch.randn((BG, D), generator=g, device=dev, dtype=torch.float32)).contiguous()
+    from lance_hip.sharded import ShardedSearch, hip_device_merge, hip_device_search
+
+    searcher = ShardedSearch(hip_device_search(L, h, D, nprobes=a.nprobe, refine_factor=a.refine),
+                             hip_device_merge(L), label_offset=s0, dist=dist, world=world)
+    torch.cuda.synchronize()
+
+    def step():
+        return searcher.search(Q, K, reuse_outputs=True)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    t = float(elapsed.item())
+    lance_hip.LanceHipSetOption(h, "time_kernels", "1")
+    for _ in range(max(3, min(a.steps, 10))):
+        step()
+    torch.cuda.synchronize()
+    kt = lance_hip.LanceHipKernelTimes(h)
+    lance_hip.LanceHipSetOption(h, "time_kernels", "0")
+    res_l = res[0].cpu().numpy()
+
+    recall = cpu = None
+    if rank == 0 and world == 1 and not a.no_recall:
+        from oracle import c_oracle, flat_knn, ivf
+
+        Xh = np.empty((N, D), np.float32)
+        for lo in range(0, N, 1 << 18):
+            hi = min(N, lo + (1 << 18))
+            Xh[lo:hi] = gen_clustered(lo, hi, D, dev, centers).cpu().numpy()
+        Qh = Q.cpu().numpy()
+        nr = min(a.recall_queries, B)
+        nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        el, _, _ = c_oracle.flat_search_batch(Xh, Qh[:nr], K, a.metric, acc64=True, nthreads=nthreads)
+        recall = flat_knn.recall_at_k(res_l[:nr], el, min(10, K))
+        if not a.no_cpu_baseline:
+            # the same IVF search on the host (oracle/flat_knn.c's IVF port over the
+            # model and lists the GPU built), one query per call, f32 distances
+            ex = lance_hip.LanceHipIvfExport(h)
+            lay = c_oracle.IvfLayout(ex["lists"], ex["live"], a.nlist)
+            kw = {}
+            if a.index_type == "ivf_pq":
+                _, T = ivf.pq_tables(ex["centroids"], ex["codebook"], Qh[:1], a.metric)
+                kw = dict(codes=ex["codes"], codebook=ex["codebook"], T=T, refine_factor=a.refine)
+            done, tc0 = 0, time.perf_counter()
+            agree = 0
+            while True:
+                cl, _, _ = c_oracle.ivf_search_batch(Xh, ex["labels"], lay, ex["centroids"], Qh[done % B:done % B + 1],
+                                                     K, a.nprobe, a.metric, acc64=False, nthreads=nthreads, **kw)
+                agree += int(np.intersect1d(cl[0], res_l[done % B]).size)
+                done += 1
+                if time.perf_counter() - tc0 >= a.cpu_seconds and done >= 2:
+                    break
+            tcpu = time.perf_counter() - tc0
+            cpu = {"value": done / tcpu, "unit": "queries/s", "cores": nthreads, "kind": "port",
+                   "sample": f"{done} queries, one per call, {a.index_type} nprobes={a.nprobe} over the GPU-built "
+                             f"model and lists of {N}x{D} rows, f32 distances ({tcpu:.1f} s, oracle/flat_knn.c IVF "
+                             f"port, {nthreads} OpenMP threads)",
+                   "id_overlap_with_gpu": round(agree / (done * K), 4)}
+        del Xh
+
+    if rank == 0:
+        value = BG * a.steps / t
+        roof = None
+        if kt["ivf_scan_launches"] > 0:
+            avg_ms = kt["ivf_scan_ms_total"] / kt["ivf_scan_launches"]
+            bytes_launch = kt["ivf_scan_bytes"] / kt["ivf_scan_launches"]
+            ach = bytes_launch / (avg_ms * 1e-3) / 1e9
+            kname = "flat_list_scan_kernel" if a.index_type == "ivf_flat" else "pq_query_scan_kernel"
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
+                    "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(bytes_launch),
+                    "pair_rows_per_launch": int(kt["ivf_pair_rows"] / kt["ivf_scan_launches"]),
+                    "coarse_ms_per_batch": round(kt["ivf_coarse_ms_total"] / kt["ivf_scan_launches"], 4)}
+        what = "IVF-Flat" if a.index_type == "ivf_flat" else f"IVF-PQ m={a.m} nbits=8"
+        line = {
+            "metric": f"kNN queries/sec + recall@10, {what} nlist={a.nlist} nprobe={a.nprobe}, {N}x{D} f32 per GPU",
+            "value": round(value, 1), "unit": "queries/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(1000.0 * t / a.steps, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": a.storage,
+            "data": f"synthetic clustered rows: {NCENT} Gaussian clusters (centers N(0,1), sigma {SIGMA}), queries "
+                    "drawn the same way (seeded torch Philox)",
+            "config": {"workload": f"{a.config.upper()} {what} nlist={a.nlist} nprobe={a.nprobe} refine={a.refine} "
+                                   f"{N}x{D} f32 per GPU k={K} query-batch={BG}",
+                       "n_per_gpu": N, "n_total": N * world, "dim": D, "k": K, "global_batch": BG,
+                       "metric": a.metric, "index_type": a.index_type, "nlist": a.nlist, "nprobe": a.nprobe,
+                       "m": a.m, "refine_factor": a.refine, "parallelism": f"rowshard{world}"},
+            "recall_at_10": recall,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "build_s": round(build_s, 2), "gen_s": round(gen_s, 2),
+        }
+        print(json.dumps(line), flush=True)
+    L.lance_free_detached(h)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
+    if a.index_type:
+        return main_ivf(a)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

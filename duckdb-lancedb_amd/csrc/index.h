@@ -167,6 +167,11 @@ struct Index {
 	double kt_append_ms = 0.0, kt_dense_ms = 0.0;
 	int64_t kt_append_n = 0, kt_dense_n = 0;
 	int64_t kt_append_rows = 0, kt_append_qpad = 0;
+	// IVF list scans (ivf_search): launches, ms, and their algorithmic work:
+	// bytes = rows of every probed list once (row data or codes) + per-pair
+	// tables; pair_rows = sum over (query, list) pairs of the list's rows
+	double kt_ivf_ms = 0.0, kt_ivf_bytes = 0.0, kt_ivf_pair_rows = 0.0, kt_ivf_coarse_ms = 0.0;
+	int64_t kt_ivf_n = 0;
 
 	~Index() {
 		if (log) fclose(log);

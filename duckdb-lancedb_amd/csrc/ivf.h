@@ -47,6 +47,7 @@ struct IvfState {
 	// list layout (rebuilt when dirty): positions padded to 64 per list
 	bool dirty = true;
 	std::vector<int64_t> h_loff;             // [nlist+1]
+	std::vector<int64_t> h_lcnt;             // [nlist] rows per list (unpadded)
 	DevBuf<int64_t> loff;
 	DevBuf<uint32_t> lslot;                  // [npos] slot, SLOT_NONE for padding
 	DevBuf<uint8_t> lcodes;                  // [npos/64][mp/16][64][16] blocked codes
@@ -55,7 +56,7 @@ struct IvfState {
 	int nblk = 0, maxb = 1;
 	// search workspace
 	DevBuf<float> Qf, Qn, P, probe_d, tmpf;
-	DevBuf<int64_t> probe_l;
+	DevBuf<int64_t> probe_l, pref;
 	DevBuf<int> probe_c, lcnt, pstart, pairs;
 	DevBuf<uint64_t> keys, tkeys, cand_a, cand_b, best;
 	DevBuf<uint8_t> tmpb;
@@ -126,9 +127,16 @@ void launch_flat_list_scan(const StoreView &s, const int *blk_list, const int64_
                            int nprobe, int maxb, int64_t tail_s0, int64_t tail_n, int nq, const float *Qf, int kk,
                            uint64_t *out, hipStream_t st);
 void launch_pq_P(const float *Q, int qld, int nq, const float *cb, int m, int dsub, float *P, hipStream_t st);
-void launch_pq_list_scan(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
-                         const float *rowaux_f, int nlist, const int *pstart, const int *pairs, int nprobe,
-                         const float *probe_d, const float *T, const float *P, int kk, uint64_t *out, hipStream_t st);
+// pref [nq][nprobe+1]: exclusive prefix of the probed lists' padded lengths
+void launch_probe_prefix(const int64_t *probe_l, int nq, int nprobe, const int64_t *loff, int64_t *pref,
+                         hipStream_t st);
+// segments per query of the IVF_PQ scan (grid S x nq)
+int pq_segments(int nq);
+// out [nq][S][kk]: per (query, segment) top-kk (ADC, slot) keys
+void launch_pq_query_scan(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
+                          const float *rowaux_f, int nq, int nprobe, const int64_t *probe_l, const float *probe_d,
+                          const float *T, const float *P, const int64_t *pref, int S, int kk, uint64_t *out,
+                          hipStream_t st);
 // per query: top-K keys over the list-scan outputs of its probes (nblk_of
 // lists via lblk0, or 1 per probe when lblk0 is null) and/or a tail output.
 void launch_ivf_merge(int nq, int nprobe, const int64_t *probe_l, const int *lblk0, int maxb, int kk,

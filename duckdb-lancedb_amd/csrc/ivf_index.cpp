@@ -17,6 +17,8 @@
 // iterations, PQ trained on <= 256*256 residual rows, 8-bit codes.
 #include "ivf.h"
 
+#include <chrono>
+
 #include <memory>
 #include <random>
 
@@ -370,6 +372,7 @@ static void layout(Index *ix) {
 	HIPCHK(hipStreamSynchronize(st));
 	std::vector<int64_t> cnt((size_t)nl, 0);
 	for (int l : a) cnt[(size_t)l] += 1;
+	s->h_lcnt = cnt;
 	s->h_loff.assign((size_t)nl + 1, 0);
 	for (int l = 0; l < nl; ++l) s->h_loff[(size_t)l + 1] = s->h_loff[(size_t)l] + round_up(cnt[(size_t)l], 64);
 	const int64_t npos = s->h_loff[(size_t)nl];
@@ -414,6 +417,29 @@ static void layout(Index *ix) {
 	s->dirty = false;
 }
 
+// time_kernels: the list-scan launch (events 0/1 on the handle's stream) and
+// its algorithmic work: every probed list's rows (IVF_FLAT: dim x esz bytes;
+// IVF_PQ: m code bytes) once, plus the per-(query, list) LUT inputs of IVF_PQ
+// (T[l] and P[q], m x 256 f32 each); pair rows = sum over pairs of list rows.
+static void account_list_scan(Index *ix, int esz) {
+	IvfState *s = ix->ivf;
+	std::vector<int> ps((size_t)s->nlist + 1);
+	HIPCHK(hipMemcpy(ps.data(), s->pstart.p, ps.size() * sizeof(int), hipMemcpyDeviceToHost));
+	double bytes = 0.0, pair_rows = 0.0;
+	const double lut = (double)s->m * PQ_K * 4.0 * (s->metric == METRIC_DOT ? 1.0 : 2.0);
+	for (int l = 0; l < s->nlist; ++l) {
+		const int np = ps[(size_t)l + 1] - ps[(size_t)l];
+		if (np <= 0) continue;
+		const double rows = (double)s->h_lcnt[(size_t)l];
+		bytes += esz ? rows * ix->dim * esz : rows * s->m + np * lut;
+		pair_rows += rows * np;
+	}
+	ix->kt_ivf_ms += ix->toc_ms(0, 1);
+	ix->kt_ivf_n += 1;
+	ix->kt_ivf_bytes += bytes;
+	ix->kt_ivf_pair_rows += pair_rows;
+}
+
 void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refine, int64_t *dL, float *dD, int *dC) {
 	IvfState *s = ix->ivf;
 	hipStream_t st = ix->stream;
@@ -430,7 +456,7 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 	StoreView sv = store_view(ix);
 	// queries per pass: bounded by MAX_PASS_Q and ~1 GiB of list-scan keys
 	const int64_t per_q = s->type == IVF_FLAT ? (int64_t)nprobe * s->maxb * kk + (int64_t)tail_nb * kk
-	                                          : (int64_t)nprobe * kp + (int64_t)tail_nb * kk;
+	                                          : (int64_t)32 * kp + (int64_t)tail_nb * kk;
 	const int pass = (int)std::max<int64_t>(1, std::min<int64_t>(MAX_PASS_Q, (int64_t)(1 << 27) / std::max<int64_t>(per_q, 1)));
 	for (int q0 = 0; q0 < nq; q0 += pass) {
 		const int n = std::min(pass, nq - q0);
@@ -443,8 +469,12 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 		s->probe_l.need((size_t)n * nprobe);
 		s->probe_d.need((size_t)n * nprobe);
 		s->probe_c.need((size_t)n);
+		const auto tc0 = std::chrono::steady_clock::now();
 		s->coarse->search_device(cos ? s->Qn.p : dQ + (int64_t)q0 * dim, n, nprobe, 1, s->probe_l.p, s->probe_d.p,
 		                         s->probe_c.p);
+		if (ix->time_kernels)
+			ix->kt_ivf_coarse_ms +=
+			    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count();
 		ix->bind();
 		s->lcnt.need((size_t)s->nlist);
 		s->pstart.need((size_t)s->nlist + 1);
@@ -460,8 +490,10 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 		}
 		if (s->type == IVF_FLAT) {
 			s->keys.need((size_t)n * nprobe * s->maxb * kk);
+			ix->tic(0);
 			launch_flat_list_scan(sv, s->blk_list.p, s->blk_pos0.p, s->lblk0.p, s->loff.p, s->lslot.p, s->nblk,
 			                      s->pstart.p, s->pairs.p, nprobe, s->maxb, 0, 0, n, s->Qf.p, kk, s->keys.p, st);
+			ix->tic(1);
 			s->cand_a.need((size_t)n * k);
 			launch_ivf_merge(n, nprobe, s->probe_l.p, s->lblk0.p, s->maxb, kk, s->keys.p, tail_nb,
 			                 tail_n > 0 ? s->tkeys.p : nullptr, k, s->cand_a.p, st);
@@ -469,12 +501,18 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 		} else {
 			s->P.need((size_t)n * s->m * PQ_K);
 			launch_pq_P(cos ? s->Qn.p : s->Qf.p, cos ? dim : ld, n, s->codebook.p, s->m, s->dsub, s->P.p, st);
-			s->keys.need((size_t)n * nprobe * kp);
-			launch_pq_list_scan(s->lcodes.p, s->m, s->mp, s->loff.p, s->lslot.p,
-			                    reinterpret_cast<const float *>(ix->rowaux), s->nlist, s->pstart.p, s->pairs.p, nprobe,
-			                    s->probe_d.p, s->metric == METRIC_DOT ? nullptr : s->T.p, s->P.p, kp, s->keys.p, st);
+			const int S = pq_segments(n);
+			s->pref.need((size_t)n * (nprobe + 1));
+			launch_probe_prefix(s->probe_l.p, n, nprobe, s->loff.p, s->pref.p, st);
+			s->keys.need((size_t)n * S * kp);
+			ix->tic(0);
+			launch_pq_query_scan(s->lcodes.p, s->m, s->mp, s->loff.p, s->lslot.p,
+			                     reinterpret_cast<const float *>(ix->rowaux), n, nprobe, s->probe_l.p, s->probe_d.p,
+			                     s->metric == METRIC_DOT ? nullptr : s->T.p, s->P.p, s->pref.p, S, kp, s->keys.p, st);
+			ix->tic(1);
 			s->cand_a.need((size_t)n * kp);
-			launch_ivf_merge(n, nprobe, s->probe_l.p, nullptr, 1, kp, s->keys.p, 0, nullptr, kp, s->cand_a.p, st);
+			// the S segment lists of each query: the merge kernel's tail mode ([q][S][kp])
+			launch_ivf_merge(n, 0, nullptr, nullptr, 1, kp, nullptr, S, s->keys.p, kp, s->cand_a.p, st);
 			if (tail_n > 0) {
 				s->cand_b.need((size_t)n * k);
 				launch_ivf_merge(n, 0, nullptr, nullptr, 1, kk, nullptr, tail_nb, s->tkeys.p, k, s->cand_b.p, st);
@@ -484,6 +522,7 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 		}
 		HIPCHK(hipGetLastError());
 		spin_sync(st);
+		if (ix->time_kernels) account_list_scan(ix, s->type == IVF_FLAT ? (ix->xbf16 ? 2 : 4) : 0);
 	}
 }
 

@@ -792,26 +792,95 @@ void launch_invert(const int64_t *probe_l, int nq, int nprobe, int nlist, int *l
 
 // ---------------------------------------------------------------------------
 // IVF_FLAT list scan: work item = 256 positions of one list (or 256 rows of
-// the unindexed tail); every query probing the list, FS_G at a time: rows are
-// staged 32 dims at a time through LDS (coalesced 128-B row segments), each
-// thread owns one row and accumulates (x - q)^2 (or x.q) in f64.
+// the unindexed tail) x every query probing the list, FS_G at a time (one
+// pass for up to FS_G queries, so the rows stream from HBM once per item).
+// Rows arrive FS_KC dims at a time in coalesced 128-B row segments, the next
+// chunk prefetched into registers while the current one is consumed from LDS
+// (rows padded to FS_KC + 1 floats: conflict-free column reads); each thread
+// owns one row and accumulates (x - q)^2 (or x.q) in f64 for all FS_G queries.
 // ---------------------------------------------------------------------------
-constexpr int FS_G = 4;
+constexpr int FS_G = 16;
 constexpr int FS_KC = 32;
+constexpr int FS_PIECES = FLAT_BLK * FS_KC / 4 / 256;  // float4 pieces per thread and chunk (8)
 
 template <typename T>
-__device__ __forceinline__ void fs_stage(const T *__restrict__ X, int ld, const uint32_t *sslot, int d0,
-                                         float (*xs)[FS_KC + 1]) {
-	// 256 rows x 32 elements: 8 four-element pieces per row
+__device__ __forceinline__ void fs_fetch(const T *__restrict__ X, int ld, int dim, const uint32_t *sslot, int d0,
+                                         float4 (&v)[FS_PIECES]) {
 #pragma unroll
-	for (int i = 0; i < 8; ++i) {
+	for (int i = 0; i < FS_PIECES; ++i) {
 		const int e = threadIdx.x + i * 256, row = e >> 3, piece = e & 7;
 		const uint32_t s = sslot[row];
-		const float4 v = s != SLOT_NONE ? load4(X + (int64_t)s * ld + d0 + piece * 4) : make_float4(0, 0, 0, 0);
-		xs[row][piece * 4 + 0] = v.x;
-		xs[row][piece * 4 + 1] = v.y;
-		xs[row][piece * 4 + 2] = v.z;
-		xs[row][piece * 4 + 3] = v.w;
+		v[i] = (s != SLOT_NONE && d0 < dim) ? load4(X + (int64_t)s * ld + d0 + piece * 4) : make_float4(0, 0, 0, 0);
+	}
+}
+
+__device__ __forceinline__ void fs_store(float (*xs)[FS_KC + 1], const float4 (&v)[FS_PIECES]) {
+#pragma unroll
+	for (int i = 0; i < FS_PIECES; ++i) {
+		const int e = threadIdx.x + i * 256, row = e >> 3, piece = e & 7;
+		xs[row][piece * 4 + 0] = v[i].x;
+		xs[row][piece * 4 + 1] = v[i].y;
+		xs[row][piece * 4 + 2] = v[i].z;
+		xs[row][piece * 4 + 3] = v[i].w;
+	}
+}
+
+// one pass over the item's rows for G queries (sq / spair hold them)
+template <int METRIC, typename T, int G>
+__device__ __forceinline__ void fs_group(const T *__restrict__ X, int ld, int dim, const float *__restrict__ Qf,
+                                         int ng, const uint32_t *sslot, const int *sq, const int *spair,
+                                         float (*xs)[FS_KC + 1], double (*qs)[FS_G], uint64_t *sk, uint64_t *o0,
+                                         int64_t ostride, int kk) {
+	const int t = threadIdx.x;
+	double acc[G], aux[G], xx = 0.0;
+#pragma unroll
+	for (int g = 0; g < G; ++g) acc[g] = aux[g] = 0.0;
+	float4 v[FS_PIECES];
+	fs_fetch<T>(X, ld, dim, sslot, 0, v);
+	for (int d0 = 0; d0 < dim; d0 += FS_KC) {
+		__syncthreads();  // previous chunk consumed
+		fs_store(xs, v);
+		for (int e = t; e < G * FS_KC; e += 256) {
+			const int g = e / FS_KC, c = e % FS_KC;
+			qs[c][g] = g < ng ? (double)Qf[(int64_t)sq[g] * ld + d0 + c] : 0.0;
+		}
+		__syncthreads();
+		if (d0 + FS_KC < dim) fs_fetch<T>(X, ld, dim, sslot, d0 + FS_KC, v);  // in flight during the FMAs
+#pragma unroll 2
+		for (int c = 0; c < FS_KC; ++c) {
+			const double xv = xs[t][c];
+			if (METRIC == METRIC_COSINE) xx = fma(xv, xv, xx);
+#pragma unroll
+			for (int g = 0; g < G; ++g) {
+				const double qv = qs[c][g];
+				if (METRIC == METRIC_L2) {
+					const double dd = xv - qv;
+					acc[g] = fma(dd, dd, acc[g]);
+				} else {
+					acc[g] = fma(xv, qv, acc[g]);
+					if (METRIC == METRIC_COSINE) aux[g] = fma(qv, qv, aux[g]);
+				}
+			}
+		}
+	}
+	const bool valid = sslot[t] != SLOT_NONE;
+#pragma unroll
+	for (int g = 0; g < G; ++g) {
+		if (g >= ng) continue;  // ng is uniform: every thread skips together
+		double r;
+		if (METRIC == METRIC_L2)
+			r = acc[g];
+		else if (METRIC == METRIC_DOT)
+			r = 1.0 - acc[g];
+		else
+			r = 1.0 - acc[g] / (sqrt(xx) * sqrt(aux[g]));
+		float f = (float)r + 0.0f;
+		if (__builtin_isnan(f)) f = __builtin_nanf("");
+		__syncthreads();
+		sk[t] = valid ? key64(f, sslot[t]) : KEY64_NONE;
+		wg_bitonic_sort(sk, FLAT_BLK);
+		uint64_t *o = o0 + (int64_t)spair[g] * ostride;
+		for (int i = t; i < kk; i += 256) o[i] = i < FLAT_BLK ? sk[i] : KEY64_NONE;
 	}
 }
 
@@ -823,7 +892,7 @@ __global__ __launch_bounds__(256) void flat_list_scan_kernel(
     int maxb, int64_t tail_s0, int64_t tail_n, int nq, const float *__restrict__ Qf, int kk,
     uint64_t *__restrict__ out) {
 	__shared__ float xs[FLAT_BLK][FS_KC + 1];
-	__shared__ double qs[FS_G][FS_KC];
+	__shared__ double qs[FS_KC][FS_G];
 	__shared__ uint32_t sslot[FLAT_BLK];
 	__shared__ uint64_t sk[FLAT_BLK];
 	__shared__ int sq[FS_G], spair[FS_G];
@@ -855,6 +924,9 @@ __global__ __launch_bounds__(256) void flat_list_scan_kernel(
 		sslot[t] = s;
 	}
 	const int tail_nb = (int)((tail_n + FLAT_BLK - 1) / FLAT_BLK);
+	// output of pair pid: out + pid * ostride + o_off
+	uint64_t *o0 = tail ? out + (int64_t)b * kk : out + (int64_t)bi * kk;
+	const int64_t ostride = tail ? (int64_t)tail_nb * kk : (int64_t)maxb * kk;
 	for (int g0 = pa; g0 < pb; g0 += FS_G) {
 		const int ng = min(FS_G, pb - g0);
 		__syncthreads();
@@ -863,52 +935,16 @@ __global__ __launch_bounds__(256) void flat_list_scan_kernel(
 			spair[t] = pid;
 			sq[t] = pid < 0 ? 0 : (tail ? pid : pid / nprobe);
 		}
-		double acc[FS_G], aux[FS_G], xx = 0.0;
-#pragma unroll
-		for (int g = 0; g < FS_G; ++g) acc[g] = aux[g] = 0.0;
-		for (int d0 = 0; d0 < dim; d0 += FS_KC) {
-			__syncthreads();
-			fs_stage<T>(X, ld, sslot, d0, xs);
-			if (t < FS_G * FS_KC) {
-				const int g = t / FS_KC, c = t % FS_KC;
-				qs[g][c] = g < ng ? (double)Qf[(int64_t)sq[g] * ld + d0 + c] : 0.0;
-			}
-			__syncthreads();
-#pragma unroll 4
-			for (int c = 0; c < FS_KC; ++c) {
-				const double xv = xs[t][c];
-				if (METRIC == METRIC_COSINE) xx = fma(xv, xv, xx);
-#pragma unroll
-				for (int g = 0; g < FS_G; ++g) {
-					const double qv = qs[g][c];
-					if (METRIC == METRIC_L2) {
-						const double dd = xv - qv;
-						acc[g] = fma(dd, dd, acc[g]);
-					} else {
-						acc[g] = fma(xv, qv, acc[g]);
-						if (METRIC == METRIC_COSINE) aux[g] = fma(qv, qv, aux[g]);
-					}
-				}
-			}
-		}
-		const bool valid = sslot[t] != SLOT_NONE;
-		for (int g = 0; g < ng; ++g) {
-			double r;
-			if (METRIC == METRIC_L2)
-				r = acc[g];
-			else if (METRIC == METRIC_DOT)
-				r = 1.0 - acc[g];
-			else
-				r = 1.0 - acc[g] / (sqrt(xx) * sqrt(aux[g]));
-			float f = (float)r + 0.0f;
-			if (__builtin_isnan(f)) f = __builtin_nanf("");
-			__syncthreads();
-			sk[t] = valid ? key64(f, sslot[t]) : KEY64_NONE;
-			wg_bitonic_sort(sk, FLAT_BLK);
-			const int pid = spair[g];
-			uint64_t *o = tail ? out + ((int64_t)pid * tail_nb + b) * kk : out + ((int64_t)pid * maxb + bi) * kk;
-			for (int i = t; i < kk; i += 256) o[i] = i < FLAT_BLK ? sk[i] : KEY64_NONE;
-		}
+		__syncthreads();
+		// per-item query count decides the register block (f64 work scales with it)
+		if (ng <= 2)
+			fs_group<METRIC, T, 2>(X, ld, dim, Qf, ng, sslot, sq, spair, xs, qs, sk, o0, ostride, kk);
+		else if (ng <= 4)
+			fs_group<METRIC, T, 4>(X, ld, dim, Qf, ng, sslot, sq, spair, xs, qs, sk, o0, ostride, kk);
+		else if (ng <= 8)
+			fs_group<METRIC, T, 8>(X, ld, dim, Qf, ng, sslot, sq, spair, xs, qs, sk, o0, ostride, kk);
+		else
+			fs_group<METRIC, T, FS_G>(X, ld, dim, Qf, ng, sslot, sq, spair, xs, qs, sk, o0, ostride, kk);
 	}
 }
 
@@ -962,70 +998,157 @@ void launch_pq_P(const float *Q, int qld, int nq, const float *cb, int m, int ds
 
 constexpr int PQ_THREADS = 512;
 
-__global__ __launch_bounds__(PQ_THREADS) void pq_list_scan_kernel(
+// pref[q][p] = positions (padded list lengths) of probes 0..p-1 of query q,
+// pref[q][nprobe] = the total: the concatenation the IVF_PQ scan splits.
+__global__ __launch_bounds__(256) void probe_prefix_kernel(const int64_t *__restrict__ probe_l, int nprobe,
+                                                           const int64_t *__restrict__ loff,
+                                                           int64_t *__restrict__ pref) {
+	__shared__ int64_t sc[256];
+	__shared__ int64_t carry;
+	const int q = blockIdx.x, t = threadIdx.x;
+	if (t == 0) carry = 0;
+	for (int p0 = 0; p0 < nprobe; p0 += 256) {
+		const int p = p0 + t;
+		int64_t len = 0;
+		if (p < nprobe) {
+			const int64_t l = probe_l[(int64_t)q * nprobe + p];
+			if (l >= 0) len = loff[l + 1] - loff[l];
+		}
+		__syncthreads();
+		sc[t] = len;
+		__syncthreads();
+		for (int off = 1; off < 256; off <<= 1) {
+			const int64_t v = t >= off ? sc[t - off] : 0;
+			__syncthreads();
+			sc[t] += v;
+			__syncthreads();
+		}
+		if (p < nprobe) pref[(int64_t)q * (nprobe + 1) + p] = carry + sc[t] - len;
+		__syncthreads();
+		if (t == 255) carry += sc[255];
+	}
+	__syncthreads();
+	if (t == 0) pref[(int64_t)q * (nprobe + 1) + nprobe] = carry;
+}
+
+void launch_probe_prefix(const int64_t *probe_l, int nq, int nprobe, const int64_t *loff, int64_t *pref,
+                         hipStream_t st) {
+	probe_prefix_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(probe_l, nprobe, loff, pref);
+}
+
+// ADCs of PQ_R rows at list positions pos[i] (canonical f32 order: d0, then
+// j = 0..m-1), the PQ_R chains interleaved so their LDS lookups overlap
+constexpr int PQ_R = 4;
+__device__ __forceinline__ void pq_adc_r(const uint8_t *__restrict__ lcodes, int nch, int m, const int64_t (&pos)[PQ_R],
+                                         const float *lut, float d0, float (&acc)[PQ_R]) {
+	const uint8_t *cp[PQ_R];
+#pragma unroll
+	for (int i = 0; i < PQ_R; ++i) {
+		cp[i] = lcodes + ((pos[i] >> 6) * nch * 64 + (pos[i] & 63)) * 16;
+		acc[i] = d0;
+	}
+	for (int ch = 0; ch < nch; ++ch) {
+		uint32_t wd[PQ_R][4];
+#pragma unroll
+		for (int i = 0; i < PQ_R; ++i) {
+			const uint4 w = *reinterpret_cast<const uint4 *>(cp[i] + (int64_t)ch * 64 * 16);
+			wd[i][0] = w.x;
+			wd[i][1] = w.y;
+			wd[i][2] = w.z;
+			wd[i][3] = w.w;
+		}
+#pragma unroll
+		for (int u = 0; u < 16; ++u) {
+			const int j = ch * 16 + u;
+			if (j < m) {
+#pragma unroll
+				for (int i = 0; i < PQ_R; ++i) acc[i] = acc[i] + lut[j * PQ_K + ((wd[i][u >> 2] >> (8 * (u & 3))) & 255u)];
+			}
+		}
+	}
+}
+
+// IVF_PQ scan, query-major: workgroup (s, q) takes segment s of S of the
+// concatenation of query q's probed lists (balanced whatever the list sizes),
+// builds the (q, list) LUT = T[l] - 2 P[q] (or -P[q]) in LDS for each list it
+// enters, and keeps ONE streaming top-kk over its whole segment (the threshold
+// tightens across lists).  Rows stream as 16-B code pieces of the 64-row
+// blocked layout, PQ_R rows per thread per round.
+__global__ __launch_bounds__(PQ_THREADS) void pq_query_scan_kernel(
     const uint8_t *__restrict__ lcodes, int m, int mp, const int64_t *__restrict__ loff,
-    const uint32_t *__restrict__ lslot, const float *__restrict__ rowaux_f, const int *__restrict__ pstart,
-    const int *__restrict__ pairs, int nprobe, const float *__restrict__ probe_d, const float *__restrict__ T,
-    const float *__restrict__ P, int kk, uint64_t *__restrict__ out) {
+    const uint32_t *__restrict__ lslot, const float *__restrict__ rowaux_f, int nprobe,
+    const int64_t *__restrict__ probe_l, const float *__restrict__ probe_d, const float *__restrict__ T,
+    const float *__restrict__ P, const int64_t *__restrict__ pref, int S, int kk, uint64_t *__restrict__ out) {
 	__shared__ float lut[PQ_MAX_M * PQ_K];
 	__shared__ uint64_t buf[IVF_TOPK_CAP];
 	__shared__ int cnt;
 	__shared__ uint64_t thr;
-	const int l = blockIdx.x, t = threadIdx.x;
-	const int pa = pstart[l], pb = pstart[l + 1];
-	if (pa >= pb) return;
-	const int64_t q0 = loff[l], q1 = loff[l + 1];
+	__shared__ int sp0;
+	const int s = blockIdx.x, q = blockIdx.y, t = threadIdx.x;
+	const int64_t *pr = pref + (int64_t)q * (nprobe + 1);
+	const int64_t R = pr[nprobe];
+	const int64_t a = R * s / S, b = R * (s + 1) / S;
 	const int nch = mp >> 4;
 	const int nlut = m * PQ_K;
 	TopK tk{buf, &cnt, &thr, kk};
-	for (int g = pa; g < pb; ++g) {
-		const int pid = pairs[g];
-		const int q = pid / nprobe;
-		const float d0 = probe_d[pid];
-		__syncthreads();
-		const float *Pq = P + (int64_t)q * nlut;
-		if (T) {
-			const float *Tl = T + (int64_t)l * nlut;
-			for (int e = t; e < nlut; e += PQ_THREADS) lut[e] = Tl[e] - 2.0f * Pq[e];
-		} else {
-			for (int e = t; e < nlut; e += PQ_THREADS) lut[e] = -Pq[e];
-		}
-		tk.reset();
-		for (int64_t base = q0; base < q1; base += PQ_THREADS) {
-			const int64_t pos = base + t;
-			bool valid = false;
-			uint64_t key = KEY64_NONE;
-			if (pos < q1) {
-				const uint32_t slot = lslot[pos];
-				if (slot != SLOT_NONE && slot_alive(rowaux_f, slot)) {
-					valid = true;
-					const uint8_t *cp = lcodes + ((pos >> 6) * nch * 64 + (pos & 63)) * 16;
-					float acc = d0;
-					for (int ch = 0; ch < nch; ++ch) {
-						const uint4 w = *reinterpret_cast<const uint4 *>(cp + (int64_t)ch * 64 * 16);
-						const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-						for (int u = 0; u < 16; ++u) {
-							const int j = ch * 16 + u;
-							if (j < m) acc = acc + lut[j * PQ_K + ((wd[u >> 2] >> (8 * (u & 3))) & 255u)];
-						}
-					}
-					key = key64(acc, slot);
-				}
+	tk.reset();
+	if (a < b) {
+		if (t == 0) {  // last probe starting at or before a
+			int lo = 0, hi = nprobe - 1;
+			while (lo < hi) {
+				const int mid = (lo + hi + 1) >> 1;
+				if (pr[mid] <= a) lo = mid;
+				else hi = mid - 1;
 			}
-			tk.offer(key, valid);
+			sp0 = lo;
 		}
-		const int nout = tk.finish();
-		uint64_t *o = out + (int64_t)pid * kk;
-		for (int i = t; i < kk; i += PQ_THREADS) o[i] = i < nout ? buf[i] : KEY64_NONE;
+		__syncthreads();
+		for (int p = sp0; p < nprobe && pr[p] < b; ++p) {
+			const int64_t g0 = max(a, pr[p]), g1 = min(b, pr[p + 1]);
+			if (g0 >= g1) continue;
+			const int64_t l = probe_l[(int64_t)q * nprobe + p];
+			const float d0 = probe_d[(int64_t)q * nprobe + p];
+			__syncthreads();  // the previous list's LUT readers are done
+			const float *Pq = P + (int64_t)q * nlut;
+			if (T) {
+				const float *Tl = T + l * nlut;
+				for (int e = t; e < nlut; e += PQ_THREADS) lut[e] = Tl[e] - 2.0f * Pq[e];
+			} else {
+				for (int e = t; e < nlut; e += PQ_THREADS) lut[e] = -Pq[e];
+			}
+			__syncthreads();
+			const int64_t end = loff[l] + (g1 - pr[p]);
+			for (int64_t r0 = loff[l] + (g0 - pr[p]); r0 < end; r0 += PQ_R * PQ_THREADS) {
+				int64_t pos[PQ_R];
+				uint32_t sl[PQ_R];
+#pragma unroll
+				for (int i = 0; i < PQ_R; ++i) {
+					const int64_t ps = r0 + i * PQ_THREADS + t;
+					sl[i] = ps < end ? lslot[ps] : SLOT_NONE;
+					if (sl[i] != SLOT_NONE && !slot_alive(rowaux_f, sl[i])) sl[i] = SLOT_NONE;
+					pos[i] = ps < end ? ps : end - 1;  // in bounds; the key is dropped
+				}
+				float da[PQ_R];
+				pq_adc_r(lcodes, nch, m, pos, lut, d0, da);
+#pragma unroll
+				for (int i = 0; i < PQ_R; ++i)
+					tk.offer(sl[i] != SLOT_NONE ? key64(da[i], sl[i]) : KEY64_NONE, sl[i] != SLOT_NONE);
+			}
+		}
 	}
+	const int nout = tk.finish();
+	uint64_t *o = out + ((int64_t)q * S + s) * kk;
+	for (int i = t; i < kk; i += PQ_THREADS) o[i] = i < nout ? buf[i] : KEY64_NONE;
 }
 
-void launch_pq_list_scan(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
-                         const float *rowaux_f, int nlist, const int *pstart, const int *pairs, int nprobe,
-                         const float *probe_d, const float *T, const float *P, int kk, uint64_t *out, hipStream_t st) {
-	pq_list_scan_kernel<<<dim3((unsigned)nlist), PQ_THREADS, 0, st>>>(lcodes, m, mp, loff, lslot, rowaux_f, pstart,
-	                                                                   pairs, nprobe, probe_d, T, P, kk, out);
+int pq_segments(int nq) { return std::max(1, std::min(32, (4096 + nq - 1) / std::max(nq, 1))); }
+
+void launch_pq_query_scan(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
+                          const float *rowaux_f, int nq, int nprobe, const int64_t *probe_l, const float *probe_d,
+                          const float *T, const float *P, const int64_t *pref, int S, int kk, uint64_t *out,
+                          hipStream_t st) {
+	pq_query_scan_kernel<<<dim3((unsigned)S, (unsigned)nq), PQ_THREADS, 0, st>>>(
+	    lcodes, m, mp, loff, lslot, rowaux_f, nprobe, probe_l, probe_d, T, P, pref, S, kk, out);
 }
 
 // ---------------------------------------------------------------------------

@@ -691,6 +691,8 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 				if (!e) HIPCHK(hipEventCreate(&e));
 			ix->kt_append_ms = ix->kt_dense_ms = 0.0;
 			ix->kt_append_n = ix->kt_dense_n = 0;
+			ix->kt_ivf_ms = ix->kt_ivf_bytes = ix->kt_ivf_pair_rows = ix->kt_ivf_coarse_ms = 0.0;
+			ix->kt_ivf_n = 0;
 			return 0;
 		}
 		if (k == "storage") {
@@ -753,15 +755,19 @@ int32_t lance_hip_last_search_stats(void *handle, int64_t *out, int32_t n) {
 // out[0] = total ms of threshold-scan launches, out[1] = their count,
 // out[2] = rows scanned per launch, out[3] = padded queries per launch,
 // out[4] = total ms of small-store dense scans, out[5] = their count,
-// out[6] = bytes per element the scan streams (2: bf16 store or scan copy).
+// out[6] = bytes per element the scan streams (2: bf16 store or scan copy),
+// out[7] = total ms of IVF list-scan launches, out[8] = their count,
+// out[9] = their algorithmic bytes (summed), out[10] = (query, row) pairs
+// they scored (summed), out[11] = total ms of the IVF coarse searches.
 int32_t lance_hip_kernel_times(void *handle, double *out, int32_t n) {
 	if (!handle || !out) return -1;
 	Index *ix = as_index(handle);
 	std::lock_guard<std::mutex> g(ix->mu);
-	double v[7] = {ix->kt_append_ms, (double)ix->kt_append_n, (double)ix->kt_append_rows,
+	double v[12] = {ix->kt_append_ms, (double)ix->kt_append_n, (double)ix->kt_append_rows,
 		               (double)ix->kt_append_qpad, ix->kt_dense_ms, (double)ix->kt_dense_n,
-		               (ix->xbf16 || ix->Xs) ? 2.0 : 4.0};
-		for (int32_t i = 0; i < n && i < 7; ++i) out[i] = v[i];
+		               (ix->xbf16 || ix->Xs) ? 2.0 : 4.0, ix->kt_ivf_ms, (double)ix->kt_ivf_n,
+		               ix->kt_ivf_bytes, ix->kt_ivf_pair_rows, ix->kt_ivf_coarse_ms};
+		for (int32_t i = 0; i < n && i < 12; ++i) out[i] = v[i];
 	return 0;
 }
 

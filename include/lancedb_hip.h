@@ -185,7 +185,11 @@ int32_t lance_hip_last_search_stats(void *handle, int64_t *out, int32_t n);
  * out[0] total ms of threshold-scan launches, out[1] their count, out[2] rows
  * per launch, out[3] padded queries per launch, out[4] total ms of small-store
  * dense scans, out[5] their count, out[6] bytes per element the scan streams
- * (2 with a bf16 store or scan copy, else 4).  Returns 0 or -1. */
+ * (2 with a bf16 store or scan copy, else 4), out[7] total ms of IVF list-scan
+ * launches, out[8] their count, out[9] their algorithmic bytes (every probed
+ * list's rows or codes once + per-pair tables, summed), out[10] (query, row)
+ * pairs scored (summed), out[11] total ms of the IVF coarse searches.
+ * Returns 0 or -1. */
 int32_t lance_hip_kernel_times(void *handle, double *out, int32_t n);
 
 /* Device-pointer ingest: num x dim row-major f32 already on the handle's device.

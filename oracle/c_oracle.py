@@ -38,6 +38,10 @@ def lib():
         L.oracle_flat_search_batch.restype = ctypes.c_int
         L.oracle_distances.argtypes = [P, ctypes.c_int64, ctypes.c_int32, P, ctypes.c_int32, P]
         L.oracle_distances.restype = None
+        I32, I64 = ctypes.c_int32, ctypes.c_int64
+        L.oracle_ivf_search_batch.argtypes = [P, I32, P, P, P, I32, P, I64, P, P, I32, P, P, P, I32, I32, I32, I32,
+                                              I32, I32, I32, P, P, P]
+        L.oracle_ivf_search_batch.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -70,3 +74,48 @@ def distances(base, q, metric="l2"):
     out = np.empty(base.shape[0], np.float32)
     lib().oracle_distances(_ptr(base), base.shape[0], base.shape[1], _ptr(q), METRIC_IDS[metric], _ptr(out))
     return out
+
+
+class IvfLayout:
+    """CSR list layout of the LIVE indexed slots + the unindexed live tail, built
+    once from ``lance_hip_ivf_export`` output (slot lists / live flags)."""
+
+    def __init__(self, lists, live, nlist):
+        lists = np.asarray(lists, np.int64)
+        live = np.asarray(live, bool)
+        idx = np.nonzero(live & (lists >= 0))[0]
+        order = np.argsort(lists[idx], kind="stable")
+        self.lrows = np.ascontiguousarray(idx[order], np.int64)
+        cnt = np.bincount(lists[idx], minlength=nlist)
+        self.loff = np.zeros(nlist + 1, np.int64)
+        np.cumsum(cnt, out=self.loff[1:])
+        self.tail = np.ascontiguousarray(np.nonzero(live & (lists < 0))[0], np.int64)
+        self.nlist = nlist
+
+
+def ivf_search_batch(base, labels, layout, centroids, Q, k, nprobe, metric="l2", codes=None, codebook=None, T=None,
+                     refine_factor=1, acc64=True, nthreads=0):
+    """IVF_FLAT (codes None) / IVF_PQ search of oracle/flat_knn.c over a given
+    model and layout.  base / labels / codes are per slot.  l2 and dot only."""
+    base = np.ascontiguousarray(base, np.float32)
+    Q = np.ascontiguousarray(Q, np.float32)
+    labels = np.ascontiguousarray(labels, np.int64)
+    C = np.ascontiguousarray(centroids, np.float32)
+    nq, d = Q.shape
+    m = 0
+    if codes is not None:
+        codes = np.ascontiguousarray(codes, np.uint8)
+        codebook = np.ascontiguousarray(codebook, np.float32)
+        m = codes.shape[1]
+        T = None if T is None else np.ascontiguousarray(T, np.float32)
+    out_l = np.empty((nq, k), np.int64)
+    out_d = np.empty((nq, k), np.float32)
+    cnt = np.empty(nq, np.int32)
+    rc = lib().oracle_ivf_search_batch(_ptr(base), d, _ptr(labels), _ptr(layout.loff), _ptr(layout.lrows),
+                                       layout.nlist, _ptr(layout.tail), len(layout.tail), _ptr(C), _ptr(codes), m,
+                                       _ptr(codebook), _ptr(T), _ptr(Q), nq, k, nprobe, refine_factor,
+                                       METRIC_IDS[metric], 1 if acc64 else 0, int(nthreads), _ptr(out_l),
+                                       _ptr(out_d), _ptr(cnt))
+    if rc != 0:
+        raise ValueError(f"oracle_ivf_search_batch failed ({rc})")
+    return out_l, out_d, cnt

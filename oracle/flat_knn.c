@@ -213,3 +213,144 @@ void oracle_distances(const float *base, int64_t n, int32_t d, const float *q, i
 #pragma omp parallel for schedule(static)
 	for (int64_t r = 0; r < n; r++) out[r] = dist64(base + (size_t)r * d, q, d, metric, qn2);
 }
+
+/*
+ * IVF_FLAT / IVF_PQ search over a given model and list layout (the CPU port of
+ * the IVF path, oracle/ivf.py's numerics; timed as the cpu_baseline of the IVF
+ * bench configs and cross-checked against oracle/ivf.py in tests/).
+ * Reference: rust_lib/src/lance_manager.rs:411-418 (vector_search(q).limit(k)
+ * .nprobes(n).refine_factor(r)) over the IVF_PQ index of :483-515.
+ *
+ *   base [n][d] f32 rows by slot, labels [n]; lists as CSR over LIVE indexed
+ *   slots: loff [nlist+1], lrows [loff[nlist]] (ascending slots per list);
+ *   tail [ntail] live slots not indexed (searched exactly);
+ *   C [nlist][d] centroids; IVF_PQ when codes != NULL: codes [n][m] (by slot),
+ *   codebook cb [m][256][d/m], T [nlist][m][256] (NULL for dot).
+ *   metric 0 l2, 1 dot (cosine: -2, not ported).  acc64: f64 exact distances
+ *   (the checker) or f32 SIMD (the timed baseline) for the coarse / flat /
+ *   re-rank distances; the ADC is f32 in j order in both.
+ * Parallel over the probed lists of each query (per-thread heaps).
+ */
+static void topk_sel(const float *dv, int64_t n, int32_t np, int32_t *ids, float *ds) {
+	hit_t *h = (hit_t *)malloc((size_t)np * sizeof(hit_t));
+	int hn = 0;
+	for (int64_t i = 0; i < n; i++) {
+		hit_t x = {dv[i], i};
+		heap_push(h, &hn, np, x);
+	}
+	qsort(h, (size_t)hn, sizeof(hit_t), cmp_hit);
+	for (int i = 0; i < hn; i++) {
+		ids[i] = (int32_t)h[i].l;
+		ds[i] = h[i].d;
+	}
+	free(h);
+}
+
+int oracle_ivf_search_batch(const float *base, int32_t d, const int64_t *labels, const int64_t *loff,
+                            const int64_t *lrows, int32_t nlist, const int64_t *tail, int64_t ntail, const float *C,
+                            const uint8_t *codes, int32_t m, const float *cb, const float *T, const float *Q,
+                            int32_t nq, int32_t k, int32_t nprobe, int32_t refine, int32_t metric, int32_t acc64,
+                            int32_t nthreads, int64_t *out_labels, float *out_dist, int32_t *out_counts) {
+	if (metric != 0 && metric != 1) return -2;
+	if (nthreads <= 0) nthreads = omp_get_max_threads();
+	if (nprobe > nlist) nprobe = nlist;
+	const int pq = codes != NULL;
+	const int dsub = pq ? d / m : 0;
+	const int kp = pq ? k * (refine > 1 ? refine : 1) : k;
+	float *cd = (float *)malloc((size_t)nlist * sizeof(float));
+	int32_t *pid = (int32_t *)malloc((size_t)nprobe * sizeof(int32_t));
+	float *pd = (float *)malloc((size_t)nprobe * sizeof(float));
+	float *P = pq ? (float *)malloc((size_t)m * 256 * sizeof(float)) : NULL;
+	hit_t *heaps = (hit_t *)malloc((size_t)nthreads * kp * sizeof(hit_t));
+	int *hn = (int *)malloc((size_t)nthreads * sizeof(int));
+	hit_t *all = (hit_t *)malloc(((size_t)nthreads * kp + (size_t)k) * sizeof(hit_t));
+	if (!cd || !pid || !pd || (pq && !P) || !heaps || !hn || !all) return -1;
+	for (int32_t qi = 0; qi < nq; qi++) {
+		const float *q = Q + (size_t)qi * d;
+		double qn2 = 0.0;
+		for (int32_t i = 0; i < d; i++) qn2 += (double)q[i] * q[i];
+		/* coarse: dot for a dot index, l2 otherwise; top-nprobe by (dist, id) */
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+		for (int32_t l = 0; l < nlist; l++)
+			cd[l] = acc64 ? dist64(C + (size_t)l * d, q, d, metric, qn2) : dist32(C + (size_t)l * d, q, d, metric, (float)qn2);
+		topk_sel(cd, nlist, nprobe, pid, pd);
+		if (pq) {
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+			for (int32_t e = 0; e < m * 256; e++) {
+				const int j = e / 256;
+				const float *y = cb + (size_t)e * dsub;
+				float acc = 0.0f;
+				for (int t = 0; t < dsub; t++) acc = acc + q[j * dsub + t] * y[t];
+				P[e] = acc;
+			}
+		}
+		for (int t = 0; t < nthreads; t++) hn[t] = 0;
+#pragma omp parallel num_threads(nthreads)
+		{
+			const int t = omp_get_thread_num();
+			hit_t *my = heaps + (size_t)t * kp;
+			float *lut = pq ? (float *)malloc((size_t)m * 256 * sizeof(float)) : NULL;
+#pragma omp for schedule(dynamic, 1)
+			for (int32_t p = 0; p < nprobe; p++) {
+				const int32_t l = pid[p];
+				if (pq) {
+					for (int e = 0; e < m * 256; e++) lut[e] = T ? T[(size_t)l * m * 256 + e] - 2.0f * P[e] : -P[e];
+				}
+				for (int64_t i = loff[l]; i < loff[l + 1]; i++) {
+					const int64_t s = lrows[i];
+					float dd;
+					if (pq) {
+						const uint8_t *c = codes + (size_t)s * m;
+						float acc = pd[p];
+						for (int j = 0; j < m; j++) acc = acc + lut[j * 256 + c[j]];
+						dd = acc;
+					} else {
+						dd = acc64 ? dist64(base + (size_t)s * d, q, d, metric, qn2)
+						           : dist32(base + (size_t)s * d, q, d, metric, (float)qn2);
+					}
+					hit_t h = {dd, s}; /* by slot: slots ascend with labels, so ties go by label */
+					heap_push(my, &hn[t], kp, h);
+				}
+			}
+			free(lut);
+		}
+		int na = 0;
+		for (int t = 0; t < nthreads; t++) {
+			memcpy(all + na, heaps + (size_t)t * kp, (size_t)hn[t] * sizeof(hit_t));
+			na += hn[t];
+		}
+		qsort(all, (size_t)na, sizeof(hit_t), cmp_hit);
+		if (na > kp) na = kp;
+		/* re-rank (PQ) + the unindexed tail, exact */
+		int nc = 0;
+		hit_t *cand = (hit_t *)malloc(((size_t)na + (size_t)ntail + 1) * sizeof(hit_t));
+		for (int i = 0; i < na; i++) {
+			const int64_t s = all[i].l;
+			float dd = all[i].d;
+			if (pq) dd = acc64 ? dist64(base + (size_t)s * d, q, d, metric, qn2) : dist32(base + (size_t)s * d, q, d, metric, (float)qn2);
+			hit_t h = {dd, labels[s]};
+			cand[nc++] = h;
+		}
+		for (int64_t i = 0; i < ntail; i++) {
+			const int64_t s = tail[i];
+			hit_t h = {acc64 ? dist64(base + (size_t)s * d, q, d, metric, qn2) : dist32(base + (size_t)s * d, q, d, metric, (float)qn2), labels[s]};
+			cand[nc++] = h;
+		}
+		qsort(cand, (size_t)nc, sizeof(hit_t), cmp_hit);
+		const int c = nc < k ? nc : k;
+		out_counts[qi] = c;
+		for (int i = 0; i < k; i++) {
+			out_labels[(size_t)qi * k + i] = i < c ? cand[i].l : -1;
+			out_dist[(size_t)qi * k + i] = i < c ? cand[i].d : NAN;
+		}
+		free(cand);
+	}
+	free(cd);
+	free(pid);
+	free(pd);
+	free(P);
+	free(heaps);
+	free(hn);
+	free(all);
+	return 0;
+}

@@ -68,3 +68,35 @@ def test_pq_tables_definition():
     d0 = ((q[0] - C[l]) ** 2).sum()
     adc = d0 + sum((T[l, jj, 0] - 2 * P[0, jj, 0]) for jj in range(2))
     assert abs(adc - exact) < 1e-3 * max(1.0, exact)
+
+
+def test_c_ivf_port_matches_numpy_oracle():
+    """oracle/flat_knn.c's IVF port (the IVF benches' cpu_baseline) restates
+    oracle/ivf.py exactly in its f64 mode: same labels, same distances."""
+    from oracle import c_oracle
+
+    rng = np.random.default_rng(3)
+    n, d, nlist, m = 900, 32, 10, 8
+    X, C, lists, cb, codes = _model(rng, n, d, nlist, m)
+    Q = rng.standard_normal((7, d)).astype(np.float32)
+    lab = np.arange(n, dtype=np.int64) * 3 + 5  # ascending, not dense
+    live = np.ones(n, bool)
+    live[::7] = False
+    lists = lists.copy()
+    lists[850:] = -1  # unindexed tail
+    lay = c_oracle.IvfLayout(lists, live, nlist)
+    for metric in ("l2", "dot"):
+        for nprobe, k in [(3, 5), (10, 12), (1, 4)]:
+            el, ed, ec = ivf.ivf_flat_search(X, lab, live, lists, C, Q, k, nprobe, metric)
+            gl, gd, gc = c_oracle.ivf_search_batch(X, lab, lay, C, Q, k, nprobe, metric)
+            np.testing.assert_array_equal(gc, ec)
+            np.testing.assert_array_equal(gl, el)
+            np.testing.assert_array_equal(gd, ed)
+            for rf in (1, 3):
+                el, ed, ec = ivf.ivf_pq_search(X, lab, live, lists, codes, C, cb, Q, k, nprobe, rf, metric)
+                _, T = ivf.pq_tables(C, cb, Q[:1], metric)
+                gl, gd, gc = c_oracle.ivf_search_batch(X, lab, lay, C, Q, k, nprobe, metric, codes=codes, codebook=cb,
+                                                       T=T, refine_factor=rf)
+                np.testing.assert_array_equal(gc, ec)
+                np.testing.assert_array_equal(gl, el)
+                np.testing.assert_array_equal(gd, ed)
