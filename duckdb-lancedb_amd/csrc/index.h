@@ -3,6 +3,7 @@
 // (IVF_FLAT / IVF_PQ, lance_manager.rs:483-515).  Not part of the public ABI.
 #pragma once
 #include "knn_kernels.h"
+#include "meta.h"
 
 #include <hip/hip_runtime.h>
 
@@ -154,6 +155,26 @@ struct Index {
 	// Options: index_type (IVF_PQ as lance_manager.rs:483-515 builds, or
 	// IVF_FLAT), k-means iterations and sampling seed.
 	IvfState *ivf = nullptr;
+
+	// metadata columns of a multi-column table (lance_create_detached_from_arrow;
+	// null for vector-only tables) and the filtered-search state: a search with
+	// a predicate runs with `faux` = the row aux with alpha = +inf on every slot
+	// the predicate does not select (the scan, refine, fallback and IVF list
+	// scans already skip such rows as tombstones) and filter_live in place of
+	// n_live
+	std::unique_ptr<MetaStore> meta;
+	bool filter_on = false;
+	int64_t filter_live = 0;
+	DevBuf<uint8_t> fmask;
+	DevBuf<float4> faux;
+	int64_t live_rows() const { return filter_on ? filter_live : n_live; }
+	// the row aux a search reads: `base`, or its filtered copy
+	const float4 *search_aux(const float4 *base) {
+		if (!filter_on) return base;
+		faux.need((size_t)cap);
+		launch_filter_rowaux(base, fmask.p, n_slots, cap, faux.p, stream);
+		return faux.p;
+	}
 	int ivf_type_opt = 1;  // 0 IVF_FLAT, 1 IVF_PQ
 	int kmeans_iters = 50;  // lance k-means max_iters default
 	uint64_t ivf_seed = 0x5eedULL;
@@ -306,6 +327,8 @@ struct Index {
 		refresh_stats();
 		slot_label.insert(slot_label.end(), labs.begin(), labs.end());
 		live.insert(live.end(), (size_t)num, 1);
+		if (meta && meta->cols.size() && meta->cols[0].size() < (size_t)(n_slots + num))
+			meta->append_nulls(n_slots + num - (int64_t)meta->cols[0].size());
 		n_slots += num;
 		n_live += num;
 		next_label = first + num;
@@ -421,6 +444,7 @@ struct Index {
 			if (live[(size_t)s]) keep.push_back(s);
 		const int64_t n = (int64_t)keep.size();
 		if (ivf) ivf_remap(this, keep);
+		if (meta) meta->keep_slots(keep);
 		const int64_t c = round_up(std::max<int64_t>(4096, n), SCAN_BR);
 		void *nX = nullptr;
 		float4 *na = nullptr, *na2 = nullptr;
@@ -500,6 +524,30 @@ struct Index {
 		fwrite(v, sizeof(float), (size_t)num * dim, log);
 		fflush(log);
 	}
+	// multi-column tables: schema record (tag 6, right after the header) and
+	// the metadata rows of each ingest batch (tag 7, after its tag-1 record)
+	void log_meta_schema() {
+		if (!log || !meta) return;
+		std::vector<uint8_t> b;
+		meta->serialize_schema(b);
+		uint8_t tag = 6;
+		int64_t n = (int64_t)b.size();
+		fwrite(&tag, 1, 1, log);
+		fwrite(&n, 8, 1, log);
+		fwrite(b.data(), 1, b.size(), log);
+		fflush(log);
+	}
+	void log_meta_rows(int64_t s0, int64_t num) {
+		if (!log || !meta) return;
+		std::vector<uint8_t> b;
+		meta->serialize_rows(s0, num, b);
+		uint8_t tag = 7;
+		int64_t n = (int64_t)b.size();
+		fwrite(&tag, 1, 1, log);
+		fwrite(&n, 8, 1, log);
+		fwrite(b.data(), 1, b.size(), log);
+		fflush(log);
+	}
 	void log_storage() {
 		if (!log) return;
 		uint8_t tag = 3, v = xbf16 ? 1 : 0;
@@ -528,6 +576,24 @@ struct Index {
 	// Device-side batched search; dQ [nq][dim] (device), outputs device.
 	void search_device(const float *dQ, int nq, int k, int refine, int64_t *dL, float *dD, int *dC);
 	void search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL, float *dD, int *dC);
+};
+
+// A search with a predicate: evaluates it over the slots (host, vectorised),
+// uploads the mask and turns filtering on for the scope of the search call.
+struct FilterScope {
+	Index *ix;
+	FilterScope(Index *i, const char *predicate) : ix(i) {
+		if (!predicate || !predicate[0]) return;
+		std::vector<uint8_t> mask;
+		ix->filter_live = eval_predicate(predicate, ix->meta.get(), ix->slot_label, ix->live, mask);
+		ix->bind();
+		ix->fmask.need(std::max<size_t>(mask.size(), 1));
+		if (!mask.empty())
+			HIPCHK(hipMemcpyAsync(ix->fmask.p, mask.data(), mask.size(), hipMemcpyHostToDevice, ix->stream));
+		HIPCHK(hipStreamSynchronize(ix->stream));
+		ix->filter_on = true;
+	}
+	~FilterScope() { ix->filter_on = false; }
 };
 
 }  // namespace lhip

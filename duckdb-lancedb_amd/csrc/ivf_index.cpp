@@ -454,6 +454,7 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 	const bool cos = s->metric == METRIC_COSINE;
 	const int ld = ix->ld, dim = ix->dim;
 	StoreView sv = store_view(ix);
+	sv.rowaux = ix->search_aux(ix->rowaux);  // filtered search: unselected slots read as tombstones
 	// queries per pass: bounded by MAX_PASS_Q and ~1 GiB of list-scan keys
 	const int64_t per_q = s->type == IVF_FLAT ? (int64_t)nprobe * s->maxb * kk + (int64_t)tail_nb * kk
 	                                          : (int64_t)32 * kp + (int64_t)tail_nb * kk;
@@ -507,7 +508,7 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			s->keys.need((size_t)n * S * kp);
 			ix->tic(0);
 			launch_pq_query_scan(s->lcodes.p, s->m, s->mp, s->loff.p, s->lslot.p,
-			                     reinterpret_cast<const float *>(ix->rowaux), n, nprobe, s->probe_l.p, s->probe_d.p,
+			                     reinterpret_cast<const float *>(sv.rowaux), n, nprobe, s->probe_l.p, s->probe_d.p,
 			                     s->metric == METRIC_DOT ? nullptr : s->T.p, s->P.p, s->pref.p, S, kp, s->keys.p, st);
 			ix->tic(1);
 			s->cand_a.need((size_t)n * kp);

@@ -65,6 +65,10 @@ void launch_fill_rowaux(float4 *rowaux, int64_t from, int64_t to, hipStream_t st
 
 // Marks the listed slots dead (rowaux.x = +inf).
 void launch_tombstone(float4 *rowaux, const int64_t *slots, int n, hipStream_t st);
+// dst = src with alpha = +inf on slots [0, n_slots) whose mask byte is 0
+// (filtered search); rows [0, cap) copied
+void launch_filter_rowaux(const float4 *src, const uint8_t *mask, int64_t n_slots, int64_t cap, float4 *dst,
+                          hipStream_t st);
 
 // ---- search ------------------------------------------------------------------
 // Also zeroes zero3[0 .. 3*nq) when non-null (the search's status words).

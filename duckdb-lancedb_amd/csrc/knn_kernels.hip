@@ -130,6 +130,22 @@ void launch_tombstone(float4 *rowaux, const int64_t *slots, int n, hipStream_t s
 	tombstone_kernel<<<dim3((n + 255) / 256), dim3(256), 0, st>>>(rowaux, slots, n);
 }
 
+__global__ void filter_rowaux_kernel(const float *__restrict__ src, const uint8_t *__restrict__ mask, int64_t n_slots,
+                                     int64_t cap, float *__restrict__ dst) {
+	const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (r >= cap) return;
+#pragma unroll
+	for (int c = 0; c < 4; ++c) dst[raix(r, c)] = src[raix(r, c)];
+	if (r < n_slots && !mask[r]) dst[raix(r, 0)] = F_INF;
+}
+
+void launch_filter_rowaux(const float4 *src, const uint8_t *mask, int64_t n_slots, int64_t cap, float4 *dst,
+                          hipStream_t st) {
+	if (cap <= 0) return;
+	filter_rowaux_kernel<<<dim3((unsigned)((cap + 255) / 256)), 256, 0, st>>>(
+	    reinterpret_cast<const float *>(src), mask, n_slots, cap, reinterpret_cast<float *>(dst));
+}
+
 // ---------------------------------------------------------------------------
 // queries
 // ---------------------------------------------------------------------------
@@ -279,6 +295,12 @@ constexpr int BR = SCAN_BR, BQ = SCAN_BQ;
 // all waves into lhip_prof[MODE*8 + 0..3] ([4] waves, [5] stages, [6] tiles)
 #ifndef LHIP_PROF
 #define LHIP_PROF 0
+#endif
+#ifndef LHIP_DBG_RA_GLOBAL
+#define LHIP_DBG_RA_GLOBAL 0  // debug: dense cosine epilogue reads the row aux from global memory
+#endif
+#ifndef LHIP_DBG_QA_GLOBAL
+#define LHIP_DBG_QA_GLOBAL 0  // debug: dense epilogue reads the query constants from global memory
 #endif
 #if LHIP_PROF
 __device__ unsigned long long lhip_prof[24];
@@ -815,6 +837,13 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 		const int ti = cur_t++;
 
 		if (LHIP_ABL_DRAIN_EPI) LHIP_WAIT_VM(0);
+		// 64 cycles of s_nop between the tile's last MFMAs and the epilogue's
+		// reads of the accumulators: without them the cosine epilogue (VALU on
+		// the accumulators right after the k loop) read stale accumulator
+		// values in ~1% of the queries of a small store (measured on MI355X:
+		// 15-19 wrong top-10 lists per 1600 queries; 0 with the pad; a vmcnt or
+		// lgkmcnt wait in its place does not remove it).  ~0.3% of a tile.
+		asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 		// ---- epilogue of tile ti (its row aux landed with its stage 0) ------
 		const int64_t tile = (int64_t)blockIdx.x + (int64_t)ti * gridDim.x;
 		const int64_t row0 = tile * tile_stride * BR;
@@ -831,7 +860,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 			for (int u = 0; u < 4; ++u) {
 				const int ql = qlb + 32 * u;
 				if (q0 + ql >= nq) continue;
+#if LHIP_DBG_QA_GLOBAL
+				const float4 qa = qaux[q0 + ql];
+#else
 				const float4 qa = QA[ql];
+#endif
 				float *dst = dense + (int64_t)(q0 + ql) * ld_out + tile * BR;
 #pragma unroll
 				for (int t = 0; t < 2; ++t)
@@ -843,7 +876,13 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 							    acc[t][u][4 * gq + 0], acc[t][u][4 * gq + 1], acc[t][u][4 * gq + 2], acc[t][u][4 * gq + 3]);
 							continue;
 						}
+#if LHIP_DBG_RA_GLOBAL
+						const float *gra = reinterpret_cast<const float *>(rowaux);
+						auto ra4g = [&](int rr, int c) { return *reinterpret_cast<const float4 *>(gra + raix(row0 + rr, c)); };
+						const float4 al = ra4g(r0, 0), xn = ra4g(r0, 1), ux = ra4g(r0, 2), sc = ra4g(r0, 3);
+#else
 						const float4 al = ra4(r0, 0), xn = ra4(r0, 1), ux = ra4(r0, 2), sc = ra4(r0, 3);
+#endif
 						*reinterpret_cast<float4 *>(dst + r0) = make_float4(
 						    lower_bound<METRIC>(acc[t][u][4 * gq + 0], make_float4(al.x, xn.x, ux.x, sc.x), qa),
 						    lower_bound<METRIC>(acc[t][u][4 * gq + 1], make_float4(al.y, xn.y, ux.y, sc.y), qa),

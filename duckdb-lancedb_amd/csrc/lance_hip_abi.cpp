@@ -45,7 +45,7 @@ void Index::search_device(const float *dQ, int nq, int k, int refine, int64_t *d
 
 void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL, float *dD, int *dC) {
 	const int eff_metric = metric_quirk ? METRIC_L2 : metric;
-	const float4 *aux = (metric_quirk && metric != METRIC_L2) ? rowaux_l2 : rowaux;
+	const float4 *aux = search_aux((metric_quirk && metric != METRIC_L2) ? rowaux_l2 : rowaux);
 	const float ma = (metric_quirk && metric != METRIC_L2) ? max_alpha_l2 : max_alpha;
 	const float mu = (metric_quirk && metric != METRIC_L2) ? max_ux_l2 : max_ux;
 	StoreView sv{X, aux, dlabels, n_slots, ld, dim, eff_metric, xbf16 ? 1 : 0,
@@ -68,7 +68,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	// rounding) spans more ranks as the neighbour distances crowd (C3: k = 100)
 	const int Mfinal = std::min(MAX_CAND, std::max(k * std::max(refine, 1), k + std::max(32, k)));
 	const int64_t n_tiles = (n_slots + SCAN_BR - 1) / SCAN_BR;
-	const bool fast_ok = (k + 8 <= MAX_CAND) && n_live > 0;
+	const bool fast_ok = (k + 8 <= MAX_CAND) && live_rows() > 0;
 	bool all_fallback = !fast_ok;
 	constexpr int64_t DENSE_MAX_ROWS = 65536;
 
@@ -156,7 +156,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		ws.sort_tmp.need(tb);
 		HIPCHK((hipError_t)sort_pairs(ws.sort_tmp.p, tb, ws.fb_keys.p, ws.fb_keys2.p, ws.fb_vals.p, ws.fb_vals2.p,
 		                              n_slots, stream));
-		launch_copy_fallback(ws.fb_keys2.p, ws.fb_vals2.p, n_live, k, q, dL, dD, dC, stream);
+		launch_copy_fallback(ws.fb_keys2.p, ws.fb_vals2.p, live_rows(), k, q, dL, dD, dC, stream);
 		HIPCHK(hipGetLastError());
 	}
 	HIPCHK(hipStreamSynchronize(stream));
@@ -218,6 +218,22 @@ static void replay_log(Index *ix, const std::string &path) {
 		} else if (tag == 5) {
 			ix->compact();
 			ivf_optimize(ix);
+		} else if (tag == 6 || tag == 7) {
+			// multi-column table: metadata schema / the rows of the batch just replayed
+			int64_t n;
+			if (fread(&n, 8, 1, f) != 1 || n < 0) break;
+			std::vector<uint8_t> b((size_t)n);
+			if (fread(b.data(), 1, b.size(), f) != b.size()) break;
+			if (tag == 6) {
+				ix->meta = MetaStore::deserialize_schema(b.data(), b.size());
+			} else if (ix->meta) {
+				// the tag-1 record before it filled these slots with NULLs
+				const int64_t have = ix->meta->cols.empty() ? 0 : (int64_t)ix->meta->cols[0].size();
+				int64_t nrec = 0;
+				memcpy(&nrec, b.data(), std::min<size_t>(8, b.size()));
+				ix->meta->truncate((size_t)std::max<int64_t>(0, have - nrec));
+				ix->meta->deserialize_rows(b.data(), b.size());
+			}
 		} else {
 			break;
 		}
@@ -289,9 +305,30 @@ void *lance_create_detached_from_arrow(const char *db_path, void *arrow_schema, 
 		lhip::write_err(err_buf, err_buf_len, "null arrow schema");
 		return nullptr;
 	}
-	lhip::write_err(err_buf, err_buf_len,
-	                "create_from_arrow failed: multi-column (Arrow) tables are not supported by the HIP backend yet");
-	return nullptr;
+	try {
+		// lance_manager.rs:62-126: dimension from the first FixedSizeList column,
+		// every other field a metadata column; the schema stays caller-owned
+		auto meta = lhip::MetaStore::from_schema(static_cast<const ArrowSchema *>(arrow_schema));
+		auto ix = new Index();
+		try {
+			ix->db_path = cstr(db_path);
+			ix->table = cstr(table_name);
+			if (ix->table.empty()) ix->table = "vectors";
+			ix->metric_name = cstr(metric);
+			ix->metric = lhip::metric_id(ix->metric_name);
+			ix->dim = meta->dim;
+			ix->ld = (int)lhip::round_up(ix->dim, lhip::DPAD);
+			ix->meta = std::move(meta);
+			ix->init_device(-1);
+			ix->log_open(true);
+			ix->log_meta_schema();
+		} catch (...) {
+			delete ix;
+			throw;
+		}
+		return ix;
+	}
+	API_GUARD("create_from_arrow failed: ", nullptr)
 }
 
 void *lance_open_detached(const char *db_path, const char *table_name, const char *metric, char *err_buf,
@@ -328,7 +365,9 @@ void lance_free_detached(void *handle) {
 }
 
 int32_t lance_detached_has_extra_columns(void *handle) {
-	return 0;  // vector-only tables (Arrow multi-column path not supported yet)
+	if (!handle) return 0;
+	Index *ix = as_index(handle);
+	return (ix->meta && !ix->meta->cols.empty()) ? 1 : 0;
 }
 
 int32_t lance_detached_dimension(void *handle) {
@@ -387,9 +426,70 @@ int32_t lance_detached_add_batch_arrow(void *handle, void *arrow_schema, void *a
 		lhip::write_err(err_buf, err_buf_len, "null arrow schema/array");
 		return -1;
 	}
-	lhip::write_err(err_buf, err_buf_len,
-	                "add_batch_arrow failed: multi-column (Arrow) ingest is not supported by the HIP backend yet");
-	return -1;
+	// lance_manager.rs:257: the callee takes the array over (its release runs
+	// here, the caller's struct is left released); the schema stays borrowed
+	ArrowArray *arr = static_cast<ArrowArray *>(arrow_array);
+	struct Owned {
+		ArrowArray a;
+		~Owned() {
+			if (a.release) a.release(&a);
+		}
+	} owned{*arr};
+	arr->release = nullptr;
+	try {
+		Index *ix = as_index(handle);
+		const ArrowSchema *sch = static_cast<const ArrowSchema *>(arrow_schema);
+		std::lock_guard<std::mutex> g(ix->mu);
+		std::unique_ptr<lhip::MetaStore> tmp;
+		lhip::MetaStore *m = ix->meta.get();
+		if (!m) {  // a vector-only table: the batch may only carry the vector column
+			tmp = lhip::MetaStore::from_schema(sch);
+			if (!tmp->cols.empty()) throw Error("the table has no metadata columns");
+			m = tmp.get();
+		}
+		if (m->dim != ix->dim)
+			throw Error("expected dimension " + std::to_string(ix->dim) + ", got " + std::to_string(m->dim));
+		std::vector<float> vecs;
+		const int64_t n0 = ix->n_slots;
+		int64_t n;
+		try {
+			n = m->import_batch(sch, &owned.a, vecs);
+		} catch (...) {
+			m->truncate((size_t)n0);
+			throw;
+		}
+		if (n == 0) return 0;
+		if (!out_labels) {
+			m->truncate((size_t)n0);
+			throw Error("null buffer");
+		}
+		ix->bind();
+		const int64_t first = ix->add_host(vecs.data(), n);
+		ix->log_add(first, vecs.data(), n);
+		ix->log_meta_rows(n0, n);
+		for (int64_t i = 0; i < n; ++i) out_labels[i] = first + i;
+		return (int32_t)n;
+	}
+	API_GUARD("add_batch_arrow failed: ", -1)
+}
+
+// NEW — the predicate evaluator of filtered search on a host Arrow batch (no
+// device, nothing taken over): mask[r] = live[r] && predicate TRUE for row r.
+int64_t lance_hip_predicate_mask(void *arrow_schema, void *arrow_array, const int64_t *labels, const uint8_t *live,
+                                 const char *predicate, uint8_t *out_mask, char *err_buf, int err_buf_len) {
+	try {
+		if (!arrow_schema || !arrow_array || !labels || !live || !out_mask) throw Error("null argument");
+		const ArrowSchema *sch = static_cast<const ArrowSchema *>(arrow_schema);
+		auto m = lhip::MetaStore::from_schema(sch);
+		std::vector<float> vecs;
+		const int64_t n = m->import_batch(sch, static_cast<const ArrowArray *>(arrow_array), vecs);
+		std::vector<int64_t> lab(labels, labels + n);
+		std::vector<uint8_t> lv(live, live + n), mask;
+		const int64_t c = lhip::eval_predicate(cstr(predicate), m.get(), lab, lv, mask);
+		if (n > 0) memcpy(out_mask, mask.data(), (size_t)n);
+		return c;
+	}
+	API_GUARD("predicate failed: ", -1)
 }
 
 int32_t lance_detached_merge(void *target_handle, void *source_handle, const int64_t *live_source_labels,
@@ -408,7 +508,7 @@ int32_t lance_detached_merge(void *target_handle, void *source_handle, const int
 		std::vector<int64_t> want(live_source_labels, live_source_labels + live_count);
 		std::sort(want.begin(), want.end());
 		want.erase(std::unique(want.begin(), want.end()), want.end());
-		std::vector<int64_t> olds;
+		std::vector<int64_t> olds, oslots;
 		std::vector<float> vecs;
 		{
 			std::lock_guard<std::mutex> g(src->mu);
@@ -420,13 +520,20 @@ int32_t lance_detached_merge(void *target_handle, void *source_handle, const int
 				src->read_rows(s, 1, row.data());
 				vecs.insert(vecs.end(), row.begin(), row.end());
 				olds.push_back(l);
+				oslots.push_back(s);
 			}
 		}
 		if (olds.empty()) return 0;
 		std::lock_guard<std::mutex> g(tg->mu);
 		tg->bind();
+		const int64_t n0 = tg->n_slots;
+		if (tg->meta && !tg->meta->cols.empty()) {  // the extra columns travel with the rows (lance_manager.rs:311-349)
+			if (!src->meta) throw Error("merged indexes have different metadata columns");
+			tg->meta->append_rows(*src->meta, oslots);
+		}
 		int64_t first = tg->add_host(vecs.data(), (int64_t)olds.size());
 		tg->log_add(first, vecs.data(), (int64_t)olds.size());
+		tg->log_meta_rows(n0, (int64_t)olds.size());
 		for (size_t i = 0; i < olds.size(); ++i) {
 			out_old_labels[i] = olds[i];
 			out_new_labels[i] = first + (int64_t)i;
@@ -446,15 +553,16 @@ int32_t lance_detached_search_batch(void *handle, const float *queries, int32_t 
 	}
 	try {
 		Index *ix = as_index(handle);
-		if (predicate && predicate[0])
-			throw Error("predicate pushdown needs metadata columns, which the HIP backend does not store yet");
 		if (dim != ix->dim)
 			throw Error("expected query dimension " + std::to_string(ix->dim) + ", got " + std::to_string(dim));
 		if (nq < 0) throw Error("negative query count");
 		if (nq == 0) return 0;
 		if (!queries || !out_labels || !out_distances || !out_counts) throw Error("null buffer");
 		std::lock_guard<std::mutex> g(ix->mu);
-		if (k <= 0 || ix->n_live == 0) {
+		// prefilter (lance_index.cpp:452-453 passes the optimizer's predicate,
+		// lance_optimizer.cpp:555-584): slots whose predicate is TRUE
+		lhip::FilterScope fs(ix, predicate);
+		if (k <= 0 || ix->live_rows() == 0) {
 			for (int32_t i = 0; i < nq; ++i) out_counts[i] = 0;
 			for (int64_t i = 0; i < (int64_t)nq * std::max(k, 0); ++i) {
 				out_labels[i] = -1;

@@ -80,6 +80,7 @@ _SIGNATURES = [
     ("lance_hip_ivf_export", i32,
      [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_char_p, c_int]),
     ("lance_hip_ivf_set_model", i32, [c_void_p, i32, i32, i32, c_void_p, c_void_p, c_char_p, c_int]),
+    ("lance_hip_predicate_mask", i64, [c_void_p, c_void_p, c_void_p, c_void_p, c_char_p, c_void_p, c_char_p, c_int]),
 ]
 
 EXPORTED_SYMBOLS = [s[0] for s in _SIGNATURES]
@@ -184,12 +185,91 @@ def LanceDetachedAddBatch(handle, vectors, num: int, dim: int) -> np.ndarray:
 
 
 def LanceDetachedAddBatchArrow(handle, arrow_schema, arrow_array) -> np.ndarray:
+    """arrow_schema / arrow_array: addresses of Arrow C Data Interface structs
+    (ArrowC.export); the array is taken over by the library."""
     e = _err()
-    out = np.empty(0, np.int64)
+    n_rows = ctypes.c_int64.from_address(int(arrow_array)).value  # ArrowArray.length
+    out = np.empty(max(n_rows, 1), np.int64)
     n = lib().lance_detached_add_batch_arrow(handle, arrow_schema, arrow_array, out.ctypes.data, e, ERR_BUF_LEN)
     if n < 0:
         raise IOException("Lance add_batch_arrow: " + e.value.decode())
     return out[:n]
+
+
+class _ArrowSchemaC(ctypes.Structure):
+    _fields_ = [("format", ctypes.c_char_p), ("name", ctypes.c_char_p), ("metadata", ctypes.c_char_p),
+                ("flags", ctypes.c_int64), ("n_children", ctypes.c_int64), ("children", ctypes.c_void_p),
+                ("dictionary", ctypes.c_void_p), ("release", ctypes.c_void_p), ("private_data", ctypes.c_void_p)]
+
+
+class _ArrowArrayC(ctypes.Structure):
+    _fields_ = [("length", ctypes.c_int64), ("null_count", ctypes.c_int64), ("offset", ctypes.c_int64),
+                ("n_buffers", ctypes.c_int64), ("n_children", ctypes.c_int64), ("buffers", ctypes.c_void_p),
+                ("children", ctypes.c_void_p), ("dictionary", ctypes.c_void_p), ("release", ctypes.c_void_p),
+                ("private_data", ctypes.c_void_p)]
+
+
+_ARROW_RELEASE = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+
+
+class ArrowC:
+    """Arrow C Data Interface structs of a pyarrow StructArray (what DuckDB's
+    ArrowConverter hands the reference's FFI, lance_index.cpp:340-354).  The
+    structs are released on close() unless the library took them over."""
+
+    def __init__(self, struct_array):
+        self.schema = _ArrowSchemaC()
+        self.array = _ArrowArrayC()
+        struct_array._export_to_c(ctypes.addressof(self.array), ctypes.addressof(self.schema))
+
+    @property
+    def schema_ptr(self):
+        return ctypes.addressof(self.schema)
+
+    @property
+    def array_ptr(self):
+        return ctypes.addressof(self.array)
+
+    def close(self):
+        for st in (self.array, self.schema):
+            if st.release:
+                _ARROW_RELEASE(st.release)(ctypes.addressof(st))
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def arrow_rows(vectors, extras=None, vector_name="vector"):
+    """StructArray [vector FixedSizeList<float32>[d], extra columns...];
+    extras: list of (name, pyarrow array or python list, pyarrow type or None)."""
+    import pyarrow as pa
+
+    v = np.ascontiguousarray(vectors, dtype=np.float32)
+    n, d = v.shape
+    vec = pa.FixedSizeListArray.from_arrays(pa.array(v.reshape(-1), pa.float32()), d)
+    arrays, names = [vec], [vector_name]
+    for name, vals, typ in (extras or []):
+        arrays.append(vals if isinstance(vals, pa.Array) else pa.array(vals, typ))
+        names.append(name)
+    return pa.StructArray.from_arrays(arrays, names=names)
+
+
+def LanceHipPredicateMask(struct_array, labels, live, predicate: str) -> np.ndarray:
+    """The library's predicate evaluator over a host Arrow batch (no device)."""
+    n = len(struct_array)
+    lab = np.ascontiguousarray(labels, np.int64)
+    lv = np.ascontiguousarray(live, np.uint8)
+    out = np.zeros(max(n, 1), np.uint8)
+    e = _err()
+    with ArrowC(struct_array) as a:
+        c = lib().lance_hip_predicate_mask(a.schema_ptr, a.array_ptr, lab.ctypes.data, lv.ctypes.data,
+                                           _b(predicate), out.ctypes.data, e, ERR_BUF_LEN)
+    if c < 0:
+        raise IOException("Lance predicate: " + e.value.decode())
+    return out[:n].astype(bool)
 
 
 def LanceDetachedMerge(target, source, live_source_labels):
@@ -411,8 +491,13 @@ class LanceIndex:
     """
 
     def __init__(self, name: str, dimension: int, options: Optional[dict] = None, lance_path: str = "",
-                 table_name: str = "vectors"):
+                 table_name: str = "vectors", extra_columns=None):
+        """extra_columns: [(name, pyarrow type)] of a multi-column index
+        (``CREATE INDEX .. USING LANCE (embedding, lang, score)``,
+        lance_index.cpp:283-312 ``has_extra_columns_``)."""
         options = dict(options or {})
+        self.extra_columns_ = list(extra_columns or [])
+        self.has_extra_columns_ = bool(self.extra_columns_)
         self.name = name
         self.metric_ = str(options.get("metric", "l2"))
         self.nprobes_ = int(options.get("nprobes", 20))
@@ -426,13 +511,26 @@ class LanceIndex:
         self.has_pending_deletes_ = False
 
     # lance_index.cpp:273-383 (Append; lazily creates the dataset :283-312)
-    def Append(self, vectors, row_ids) -> None:
+    def Append(self, vectors, row_ids, extras: Optional[dict] = None) -> None:
+        """extras: {column name: values} of the extra columns (multi-column index)."""
         v = np.ascontiguousarray(vectors, dtype=np.float32).reshape(-1, self.dimension_)
         if v.shape[0] == 0:
             return
-        if self.rust_handle_ is None:
-            self.rust_handle_ = LanceCreateDetached(self.lance_path_, self.dimension_, self.metric_, self.table_name_)
-        labels = LanceDetachedAddBatch(self.rust_handle_, v, v.shape[0], self.dimension_)
+        if self.has_extra_columns_:
+            # Arrow C Data Interface path (lance_index.cpp:322-360)
+            cols = [(nm, (extras or {}).get(nm, [None] * v.shape[0]), typ) for nm, typ in self.extra_columns_]
+            batch = arrow_rows(v, cols)
+            if self.rust_handle_ is None:
+                with ArrowC(batch) as sch:
+                    self.rust_handle_ = LanceCreateDetachedFromArrow(self.lance_path_, sch.schema_ptr, self.metric_,
+                                                                     self.table_name_)
+            with ArrowC(batch) as a:
+                labels = LanceDetachedAddBatchArrow(self.rust_handle_, a.schema_ptr, a.array_ptr)
+        else:
+            if self.rust_handle_ is None:
+                self.rust_handle_ = LanceCreateDetached(self.lance_path_, self.dimension_, self.metric_,
+                                                        self.table_name_)
+            labels = LanceDetachedAddBatch(self.rust_handle_, v, v.shape[0], self.dimension_)
         for lab, rid in zip(labels.tolist(), list(row_ids)):
             while len(self.label_to_rowid_) <= lab:
                 self.label_to_rowid_.append(-1)

@@ -31,8 +31,11 @@ extern "C" {
 void *lance_create_detached(const char *db_path, int32_t dimension, const char *metric, const char *table_name,
                             char *err_buf, int err_buf_len);
 
-/* ffi.rs:62-89 (rust_ffi.cpp:58).  Multi-column Arrow tables: not supported by
- * this build yet — returns NULL with an error message. */
+/* ffi.rs:62-89 (rust_ffi.cpp:58), lance_manager.rs:62-126.  Multi-column
+ * table from an Arrow C Data Interface schema (struct of the table's columns,
+ * borrowed): the first FixedSizeList<float32>[dim] column is the vector, every
+ * other column metadata (filterable by a search predicate, persisted in the
+ * table log, carried by merge and compact).  NULL with an error otherwise. */
 void *lance_create_detached_from_arrow(const char *db_path, void *arrow_schema, const char *metric,
                                        const char *table_name, char *err_buf, int err_buf_len);
 
@@ -59,7 +62,12 @@ int64_t lance_detached_add(void *handle, const float *vector, int32_t dimension,
 int32_t lance_detached_add_batch(void *handle, const float *vectors, int32_t num, int32_t dim, int64_t *out_labels,
                                  char *err_buf, int err_buf_len);
 
-/* ffi.rs:147-180 (rust_ffi.cpp:108).  Not supported yet: returns -1. */
+/* ffi.rs:147-180 (rust_ffi.cpp:108), lance_manager.rs:251-301.  A struct
+ * array of the table's columns [vector FixedSizeList<float32>[dim], extra...]
+ * (Arrow C Data Interface); the callee takes the array over (its release is
+ * called, the caller's struct is left released), the schema stays borrowed.
+ * Extra columns: integers, float, double, boolean, utf8 / large utf8, NULLs
+ * allowed.  Labels dense as add_batch.  Returns num or -1. */
 int32_t lance_detached_add_batch_arrow(void *handle, void *arrow_schema, void *arrow_array, int64_t *out_labels,
                                        char *err_buf, int err_buf_len);
 
@@ -82,9 +90,13 @@ int32_t lance_detached_search(void *handle, const float *query, int32_t dim, int
                               int err_buf_len);
 
 /* NEW — the form the reference's C++ already calls (lance_index.cpp:452-453):
- * a nullable Lance-SQL predicate inserted after refine_factor.  NULL or "" =
- * unfiltered.  A non-empty predicate needs metadata columns (Arrow path), which
- * this build does not store yet: returns -1 with an error. */
+ * a nullable Lance-SQL predicate inserted after refine_factor (NULL or "" =
+ * unfiltered), as lance_optimizer.cpp:204-344 writes it: column op constant,
+ * AND / OR, NOT (..), IS [NOT] NULL, [NOT] IN (..), BETWEEN; string literals
+ * '..' ('' escapes), numbers, true / false, NULL.  Columns: the table's extra
+ * columns and the implicit int64 `label`.  Prefilter semantics (LanceDB
+ * only_if): top-k over the live rows whose predicate is TRUE (SQL three-valued
+ * logic).  Unknown column / syntax error: -1. */
 int32_t lance_detached_search_with_predicate(void *handle, const float *query, int32_t dim, int32_t k,
                                              int32_t nprobes, int32_t refine_factor, const char *predicate,
                                              int64_t *out_labels, float *out_distances, char *err_buf,
@@ -216,6 +228,13 @@ int32_t lance_hip_merge_topk_device(int32_t nshard, int32_t nq, int32_t k, const
 int32_t lance_hip_merge_topk(int32_t nshard, int32_t nq, int32_t k, const int64_t *part_labels,
                              const float *part_dists, const int32_t *part_counts, int64_t *out_labels,
                              float *out_dists, int32_t *out_counts, char *err_buf, int err_buf_len);
+
+/* NEW — the filtered-search predicate evaluator on a host Arrow batch (struct
+ * of [vector, extra...] as lance_detached_add_batch_arrow takes; nothing is
+ * taken over, no device needed): out_mask[r] = live[r] && predicate TRUE for
+ * row r with label labels[r].  Returns the selected count or -1. */
+int64_t lance_hip_predicate_mask(void *arrow_schema, void *arrow_array, const int64_t *labels, const uint8_t *live,
+                                 const char *predicate, uint8_t *out_mask, char *err_buf, int err_buf_len);
 
 /* NEW — IVF state: out[0] type (-1 none, 0 IVF_FLAT, 1 IVF_PQ), out[1] nlist,
  * out[2] m, out[3] dsub, out[4] rows indexed, out[5] slots.  0 or -1. */
