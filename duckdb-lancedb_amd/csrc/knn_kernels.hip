@@ -296,6 +296,12 @@ constexpr int BR = SCAN_BR, BQ = SCAN_BQ;
 #ifndef LHIP_PROF
 #define LHIP_PROF 0
 #endif
+#ifndef LHIP_NST_BF16_32
+#define LHIP_NST_BF16_32 3  // ring slots of a 32-deep bf16 stage (3 or 4)
+#endif
+#ifndef LHIP_PRIO_HI_HALF
+#define LHIP_PRIO_HI_HALF 0  // s_setprio 1 on waves 4..7 (the second-dispatched half) for the whole kernel
+#endif
 #ifndef LHIP_DBG_RA_GLOBAL
 #define LHIP_DBG_RA_GLOBAL 0  // debug: dense cosine epilogue reads the row aux from global memory
 #endif
@@ -344,7 +350,7 @@ struct ScanCfg {
 	static constexpr int QROW = SK * 2;                        // bytes per query and stage: 128 / 64
 	static constexpr int QCH = QROW / 16;
 	static constexpr int QST = BQ * QROW;                      // 32 / 16 KiB
-	static constexpr int NST = XB ? (SK == 64 ? 2 : 3) : 3;    // ring slots
+	static constexpr int NST = XB ? (SK == 64 ? 2 : LHIP_NST_BF16_32) : 3;  // ring slots
 	static constexpr int STAGE = XST + QST;
 	static constexpr int RING = NST * STAGE;                   // 128 / 144 KiB
 	static constexpr int XDMA = XST / 1024 / SCAN_WAVES;       // X DMA instructions per wave and stage
@@ -361,12 +367,12 @@ struct ScanCfg {
 	static constexpr int LDS = RING + RA_BYTES + CNT_BYTES + QA_BYTES + LIST_BYTES;
 	static_assert(LDS <= 160 * 1024, "LDS budget");
 	static_assert(XDMA * SCAN_WAVES * 1024 == XST && QDMA * SCAN_WAVES * 1024 == QST, "stages = whole DMA instructions");
-	static_assert(XROW == 128 && (QROW == 128 || QROW == 64), "swizzles below");
+	static_assert((XROW == 128 || XROW == 64) && (QROW == 128 || QROW == 64), "swizzles below");
 	static_assert(XB || SK == 32, "f32 fragments: 2 k-steps per stage");
 	static_assert(KQ % 2 == 0, "k-step fragments alternate between two register sets");
 	// 16 B chunk c of row r lives at physical chunk xswz(r, c) (an involution):
 	// conflict-free ds_read_b128 fragment reads on 128 B (64 B) rows
-	__device__ static __forceinline__ int xswz(int r, int c) { return c ^ ((r >> 1) & 7); }
+	__device__ static __forceinline__ int xswz(int r, int c) { return XROW == 128 ? c ^ ((r >> 1) & 7) : c ^ ((r >> 2) & 3); }
 	__device__ static __forceinline__ int qswz(int r, int c) { return QROW == 128 ? c ^ ((r >> 1) & 7) : c ^ ((r >> 2) & 3); }
 };
 
@@ -467,6 +473,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 	[[maybe_unused]] const int lane = tid & 63;
 	const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR math
 	const int wr = w & 3, wq = w >> 2;                      // 64-row quarter, 128-query half
+	if (LHIP_PRIO_HI_HALF && w >= 4) __builtin_amdgcn_s_setprio(1);
 	const int q0 = blockIdx.y * BQ;
 	const int S = ld / C::SK;  // >= 1 (ld is a multiple of 64)
 	const int my_tiles = (n_tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;

@@ -149,3 +149,74 @@ def test_sharded_hip_search_two_ranks_one_gpu():
         l, dd, c = out[r]
         np.testing.assert_array_equal(l, el)
         np.testing.assert_allclose(dd, ed, rtol=1e-4, atol=1e-5)
+
+
+def _gpu_ivf_worker(rank, world, port, n, d, k, q, nlist, nprobe, out):
+    # the bench's IVF multi-GPU flow (bench.py main_ivf): rank 0 trains, the model
+    # is broadcast, every other rank installs it and indexes its own shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    import lance_hip
+    from lance_hip.sharded import hip_device_merge, hip_device_search
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    L = lance_hip.lib()
+    rng = np.random.default_rng(12)
+    C = rng.standard_normal((24, d)).astype(np.float32)
+    X = (C[rng.integers(0, 24, n)] + 0.5 * rng.standard_normal((n, d))).astype(np.float32)
+    Q = (X[rng.choice(n, q, replace=False)] + 0.1 * rng.standard_normal((q, d))).astype(np.float32)
+    s0, s1 = shard_range(n, world, rank)
+    h = lance_hip.LanceCreateDetached("", d, "l2", f"ivfshard{rank}")
+    lance_hip.LanceHipSetOption(h, "index_type", "ivf_flat")
+    lance_hip.LanceDetachedAddBatch(h, X[s0:s1], s1 - s0, d)
+    Cm = torch.zeros((nlist, d), dtype=torch.float32)
+    if rank == 0:
+        lance_hip.LanceDetachedCreateIndex(h, nlist, 0)
+        Cm.copy_(torch.from_numpy(lance_hip.LanceHipIvfExport(h)["centroids"]))
+    dist.broadcast(Cm, 0)
+    if rank != 0:
+        lance_hip.LanceHipIvfSetModel(h, "ivf_flat", Cm.numpy())
+    ex = lance_hip.LanceHipIvfExport(h)
+    dev_search = hip_device_search(L, h, d, nprobes=nprobe)
+    dev_merge = hip_device_merge(L)
+
+    def local_search(Qt, kk):
+        l, dd, c = dev_search(Qt.cuda(), kk)
+        return l.cpu(), dd.cpu(), c.cpu()
+
+    def merge(gl, gd, gc):
+        l, dd, c = dev_merge(gl.cuda(), gd.cuda(), gc.cuda())
+        return l.cpu(), dd.cpu(), c.cpu()
+
+    s = ShardedSearch(local_search, merge, label_offset=s0, dist=dist, world=world)
+    l, dd, c = s.search(torch.from_numpy(Q), k)
+    out[rank] = (l.numpy(), dd.numpy(), c.numpy(), ex["lists"].copy(), Cm.numpy().copy())
+    lance_hip.LanceFreeDetached(h)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_ivf_flat_two_ranks_one_gpu():
+    # sharded IVF_FLAT over one broadcast model == unsharded IVF_FLAT with that
+    # model and the same row placement (PQ is not: each shard re-ranks its own
+    # k*refine_factor candidates, a superset of the unsharded re-rank window)
+    from oracle import ivf
+
+    world, n, d, k, q, nlist, nprobe = 2, 30_000, 32, 10, 24, 32, 5
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_gpu_ivf_worker, args=(world, _free_port(), n, d, k, q, nlist, nprobe, out), nprocs=world, join=True)
+    rng = np.random.default_rng(12)
+    C = rng.standard_normal((24, d)).astype(np.float32)
+    X = (C[rng.integers(0, 24, n)] + 0.5 * rng.standard_normal((n, d))).astype(np.float32)
+    Q = (X[rng.choice(n, q, replace=False)] + 0.1 * rng.standard_normal((q, d))).astype(np.float32)
+    lists = np.concatenate([out[r][3] for r in range(world)])
+    el, ed, ec = ivf.ivf_flat_search(X, np.arange(n), np.ones(n, bool), lists, out[0][4], Q, k, nprobe, "l2")
+    for r in range(world):
+        l, dd, c = out[r][:3]
+        np.testing.assert_array_equal(c, ec)
+        np.testing.assert_array_equal(l, el)
+        np.testing.assert_allclose(dd, ed, rtol=1e-4, atol=1e-5)

@@ -5,11 +5,13 @@ set -e
 cd "$(dirname "$0")/.."
 D=duckdb-lancedb_amd
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-inline-asm -Wno-unused-result"
-hipcc $F -c $D/csrc/lance_hip_abi.cpp -o abl/abi.o
+mkdir -p abl
+make -s -C $D  # the other objects of the library (lib/*.o)
+OTHERS="$D/lib/ivf_kernels.o $D/lib/lance_hip_abi.o $D/lib/ivf_index.o $D/lib/meta.o"
 build() { # name defines...
 	local n=$1; shift
 	hipcc $F "$@" -c $D/csrc/knn_kernels.hip -o abl/k_$n.o
-	hipcc -shared -o abl/lib_$n.so abl/k_$n.o abl/abi.o
+	hipcc -shared -o abl/lib_$n.so abl/k_$n.o $OTHERS
 }
 for v in "$@"; do
 	case $v in
@@ -31,6 +33,10 @@ for v in "$@"; do
 	SLOW_SWITCH) build SLOW_SWITCH -DLHIP_SLOW_VALU=0 ;;
 	NOLISTWRITE) build NOLISTWRITE -DLHIP_ABL_NO_LISTWRITE=1 ;;
 	DRAIN) build DRAIN -DLHIP_ABL_DRAIN_EPI=1 ;;
+	PRIO) build PRIO -DLHIP_PRIO_HI_HALF=1 ;;
+	SK32N3) build SK32N3 -DLHIP_SK_BF16=32 -DLHIP_NST_BF16_32=3 ;;
+	SK32N4) build SK32N4 -DLHIP_SK_BF16=32 -DLHIP_NST_BF16_32=4 ;;
+	SKEL_SK32N4) build SKEL_SK32N4 -DLHIP_SK_BF16=32 -DLHIP_NST_BF16_32=4 -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 -DLHIP_ABL_NO_EPILOGUE=1 ;;
 	NOSLOW_DRAIN) build NOSLOW_DRAIN -DLHIP_ABL_DRAIN_EPI=1 -DLHIP_ABL_NO_SLOW=1 ;;
 	SKEL) build SKEL -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 -DLHIP_ABL_NO_EPILOGUE=1 ;;
 	SKEL_NOQ) build SKEL_NOQ -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 -DLHIP_ABL_NO_EPILOGUE=1 -DLHIP_ABL_NO_QDMA=1 ;;
@@ -46,7 +52,7 @@ for v in "$@"; do
 	PREV) # the committed (HEAD) kernel file, for same-box A/B timing
 		git show HEAD:$D/csrc/knn_kernels.hip > abl/prev_kernels.hip
 		hipcc $F -I$D/csrc -c abl/prev_kernels.hip -o abl/k_PREV.o
-		hipcc -shared -o abl/lib_PREV.so abl/k_PREV.o abl/abi.o ;;
+		hipcc -shared -o abl/lib_PREV.so abl/k_PREV.o $OTHERS ;;
 	*) echo "unknown $v"; exit 1 ;;
 	esac
 done
