@@ -56,6 +56,7 @@ struct IvfState {
 	int nblk = 0, maxb = 1;
 	// search workspace
 	DevBuf<float> Qf, Qn, P, probe_d, tmpf;
+	DevBuf<double> Qd, qn2;
 	DevBuf<int64_t> probe_l, pref;
 	DevBuf<int> probe_c, lcnt, pstart, pairs;
 	DevBuf<uint64_t> keys, tkeys, cand_a, cand_b, best;
@@ -124,8 +125,10 @@ void launch_invert(const int64_t *probe_l, int nq, int nprobe, int nlist, int *l
                    hipStream_t st);
 void launch_flat_list_scan(const StoreView &s, const int *blk_list, const int64_t *blk_pos0, const int *lblk0,
                            const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart, const int *pairs,
-                           int nprobe, int maxb, int64_t tail_s0, int64_t tail_n, int nq, const float *Qf, int kk,
-                           uint64_t *out, hipStream_t st);
+                           int nprobe, int maxb, int64_t tail_s0, int64_t tail_n, int nq, const double *Qd,
+                           const double *qn2, int kk, uint64_t *out, hipStream_t st);
+// Qd [nq][ld] f64 copy of the padded f32 queries Qf, qn2 [nq] = sum of q^2 in element order
+void launch_ivf_qd(const float *Qf, int nq, int ld, int dim, double *Qd, double *qn2, hipStream_t st);
 void launch_pq_P(const float *Q, int qld, int nq, const float *cb, int m, int dsub, float *P, hipStream_t st);
 // pref [nq][nprobe+1]: exclusive prefix of the probed lists' padded lengths
 void launch_probe_prefix(const int64_t *probe_l, int nq, int nprobe, const int64_t *loff, int64_t *pref,

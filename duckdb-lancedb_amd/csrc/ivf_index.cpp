@@ -464,6 +464,9 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 		s->Qf.need((size_t)n * ld);
 		if (cos) s->Qn.need((size_t)n * dim);
 		launch_ivf_prep(dQ + (int64_t)q0 * dim, n, dim, ld, cos ? 1 : 0, s->Qf.p, cos ? s->Qn.p : nullptr, st);
+		s->Qd.need((size_t)n * ld);
+		s->qn2.need((size_t)n);
+		launch_ivf_qd(s->Qf.p, n, ld, dim, s->Qd.p, s->qn2.p, st);
 		HIPCHK(hipGetLastError());
 		HIPCHK(hipStreamSynchronize(st));
 		// coarse: exact top-nprobe partitions (synchronous on the centroid store's stream)
@@ -487,13 +490,13 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 		if (tail_n > 0) {
 			s->tkeys.need((size_t)n * tail_nb * kk);
 			launch_flat_list_scan(sv, nullptr, nullptr, nullptr, nullptr, nullptr, tail_nb, nullptr, nullptr, 1, 1,
-			                      s->n_indexed, tail_n, n, s->Qf.p, kk, s->tkeys.p, st);
+			                      s->n_indexed, tail_n, n, s->Qd.p, s->qn2.p, kk, s->tkeys.p, st);
 		}
 		if (s->type == IVF_FLAT) {
 			s->keys.need((size_t)n * nprobe * s->maxb * kk);
 			ix->tic(0);
 			launch_flat_list_scan(sv, s->blk_list.p, s->blk_pos0.p, s->lblk0.p, s->loff.p, s->lslot.p, s->nblk,
-			                      s->pstart.p, s->pairs.p, nprobe, s->maxb, 0, 0, n, s->Qf.p, kk, s->keys.p, st);
+			                      s->pstart.p, s->pairs.p, nprobe, s->maxb, 0, 0, n, s->Qd.p, s->qn2.p, kk, s->keys.p, st);
 			ix->tic(1);
 			s->cand_a.need((size_t)n * k);
 			launch_ivf_merge(n, nprobe, s->probe_l.p, s->lblk0.p, s->maxb, kk, s->keys.p, tail_nb,

@@ -739,6 +739,26 @@ void launch_ivf_prep(const float *Q, int nq, int dim, int ld, int normalize, flo
 	ivf_prep_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(Q, dim, ld, normalize, Qf, Qn);
 }
 
+// f64 copies of the padded f32 queries and their |q|^2 summed in element
+// order (the IVF_FLAT list scan reads them through scalar loads)
+__global__ __launch_bounds__(256) void ivf_qd_kernel(const float *__restrict__ Qf, int ld, int dim,
+                                                     double *__restrict__ Qd, double *__restrict__ qn2) {
+	const int q = blockIdx.x, t = threadIdx.x;
+	for (int i = t; i < ld; i += 256) Qd[(int64_t)q * ld + i] = (double)Qf[(int64_t)q * ld + i];
+	if (t == 0) {
+		double s = 0.0;
+		for (int i = 0; i < dim; ++i) {
+			const double v = (double)Qf[(int64_t)q * ld + i];
+			s = fma(v, v, s);
+		}
+		qn2[q] = s;
+	}
+}
+
+void launch_ivf_qd(const float *Qf, int nq, int ld, int dim, double *Qd, double *qn2, hipStream_t st) {
+	ivf_qd_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(Qf, ld, dim, Qd, qn2);
+}
+
 __global__ void invert_count_kernel(const int64_t *__restrict__ probe_l, int n, int *__restrict__ lcnt) {
 	const int i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n) return;
@@ -814,52 +834,50 @@ __device__ __forceinline__ void fs_fetch(const T *__restrict__ X, int ld, int di
 	}
 }
 
-__device__ __forceinline__ void fs_store(float (*xs)[FS_KC + 1], const float4 (&v)[FS_PIECES]) {
+// chunk of 32 dims of 256 rows as float4 pieces, piece p of row r at p ^ (r & 7):
+// one ds_write_b128 per loaded piece, one ds_read_b128 per 4 dims of a thread's row
+__device__ __forceinline__ void fs_store(float4 (*xs)[8], const float4 (&v)[FS_PIECES]) {
 #pragma unroll
 	for (int i = 0; i < FS_PIECES; ++i) {
 		const int e = threadIdx.x + i * 256, row = e >> 3, piece = e & 7;
-		xs[row][piece * 4 + 0] = v[i].x;
-		xs[row][piece * 4 + 1] = v[i].y;
-		xs[row][piece * 4 + 2] = v[i].z;
-		xs[row][piece * 4 + 3] = v[i].w;
+		xs[row][piece ^ (row & 7)] = v[i];
 	}
 }
 
-// one pass over the item's rows for G queries (sq / spair hold them)
+// one pass over the item's rows for G queries (sq / spair hold them).  The
+// query values come through scalar loads of their f64 copies (wave-uniform
+// addresses), the rows from LDS.  L2 as |x|^2 + |q|^2 - 2 x.q with every sum
+// in f64 in element order (one FMA per element and query; x == q gives
+// exactly 0): its f32 rounding equals the oracle's rounded sum of squared
+// differences except within f64 noise of an f32 rounding boundary.
 template <int METRIC, typename T, int G>
-__device__ __forceinline__ void fs_group(const T *__restrict__ X, int ld, int dim, const float *__restrict__ Qf,
-                                         int ng, const uint32_t *sslot, const int *sq, const int *spair,
-                                         float (*xs)[FS_KC + 1], double (*qs)[FS_G], uint64_t *sk, uint64_t *o0,
-                                         int64_t ostride, int kk) {
+__device__ __forceinline__ void fs_group(const T *__restrict__ X, int ld, int dim, const double *__restrict__ Qd,
+                                         const double *__restrict__ qn2, int ng, const uint32_t *sslot,
+                                         const int *sq, const int *spair, float4 (*xs)[8], uint64_t *sk,
+                                         uint64_t *o0, int64_t ostride, int kk) {
 	const int t = threadIdx.x;
-	double acc[G], aux[G], xx = 0.0;
+	const double *qp[G];
 #pragma unroll
-	for (int g = 0; g < G; ++g) acc[g] = aux[g] = 0.0;
+	for (int g = 0; g < G; ++g) qp[g] = Qd + (int64_t)__builtin_amdgcn_readfirstlane(sq[g < ng ? g : 0]) * ld;
+	double acc[G], xx = 0.0;
+#pragma unroll
+	for (int g = 0; g < G; ++g) acc[g] = 0.0;
 	float4 v[FS_PIECES];
 	fs_fetch<T>(X, ld, dim, sslot, 0, v);
 	for (int d0 = 0; d0 < dim; d0 += FS_KC) {
 		__syncthreads();  // previous chunk consumed
 		fs_store(xs, v);
-		for (int e = t; e < G * FS_KC; e += 256) {
-			const int g = e / FS_KC, c = e % FS_KC;
-			qs[c][g] = g < ng ? (double)Qf[(int64_t)sq[g] * ld + d0 + c] : 0.0;
-		}
 		__syncthreads();
 		if (d0 + FS_KC < dim) fs_fetch<T>(X, ld, dim, sslot, d0 + FS_KC, v);  // in flight during the FMAs
 #pragma unroll 2
-		for (int c = 0; c < FS_KC; ++c) {
-			const double xv = xs[t][c];
-			if (METRIC == METRIC_COSINE) xx = fma(xv, xv, xx);
+		for (int j = 0; j < 8; ++j) {
+			const float4 x4 = xs[t][j ^ (t & 7)];
+			const double xv[4] = {(double)x4.x, (double)x4.y, (double)x4.z, (double)x4.w};
 #pragma unroll
-			for (int g = 0; g < G; ++g) {
-				const double qv = qs[c][g];
-				if (METRIC == METRIC_L2) {
-					const double dd = xv - qv;
-					acc[g] = fma(dd, dd, acc[g]);
-				} else {
-					acc[g] = fma(xv, qv, acc[g]);
-					if (METRIC == METRIC_COSINE) aux[g] = fma(qv, qv, aux[g]);
-				}
+			for (int c = 0; c < 4; ++c) {
+				if (METRIC != METRIC_DOT) xx = fma(xv[c], xv[c], xx);
+#pragma unroll
+				for (int g = 0; g < G; ++g) acc[g] = fma(xv[c], qp[g][d0 + 4 * j + c], acc[g]);
 			}
 		}
 	}
@@ -867,13 +885,14 @@ __device__ __forceinline__ void fs_group(const T *__restrict__ X, int ld, int di
 #pragma unroll
 	for (int g = 0; g < G; ++g) {
 		if (g >= ng) continue;  // ng is uniform: every thread skips together
+		const double qq = METRIC == METRIC_DOT ? 0.0 : qn2[__builtin_amdgcn_readfirstlane(sq[g])];
 		double r;
 		if (METRIC == METRIC_L2)
-			r = acc[g];
+			r = fmax(fma(-2.0, acc[g], xx + qq), 0.0);
 		else if (METRIC == METRIC_DOT)
 			r = 1.0 - acc[g];
 		else
-			r = 1.0 - acc[g] / (sqrt(xx) * sqrt(aux[g]));
+			r = 1.0 - acc[g] / (sqrt(xx) * sqrt(qq));
 		float f = (float)r + 0.0f;
 		if (__builtin_isnan(f)) f = __builtin_nanf("");
 		__syncthreads();
@@ -889,10 +908,9 @@ __global__ __launch_bounds__(256) void flat_list_scan_kernel(
     const T *__restrict__ X, int ld, int dim, const float *__restrict__ rowaux_f, const int *__restrict__ blk_list,
     const int64_t *__restrict__ blk_pos0, const int *__restrict__ lblk0, const int64_t *__restrict__ loff,
     const uint32_t *__restrict__ lslot, const int *__restrict__ pstart, const int *__restrict__ pairs, int nprobe,
-    int maxb, int64_t tail_s0, int64_t tail_n, int nq, const float *__restrict__ Qf, int kk,
-    uint64_t *__restrict__ out) {
-	__shared__ float xs[FLAT_BLK][FS_KC + 1];
-	__shared__ double qs[FS_KC][FS_G];
+    int maxb, int64_t tail_s0, int64_t tail_n, int nq, const double *__restrict__ Qd, const double *__restrict__ qn2,
+    int kk, uint64_t *__restrict__ out) {
+	__shared__ float4 xs[FLAT_BLK][8];
 	__shared__ uint32_t sslot[FLAT_BLK];
 	__shared__ uint64_t sk[FLAT_BLK];
 	__shared__ int sq[FS_G], spair[FS_G];
@@ -937,14 +955,12 @@ __global__ __launch_bounds__(256) void flat_list_scan_kernel(
 		}
 		__syncthreads();
 		// per-item query count decides the register block (f64 work scales with it)
-		if (ng <= 2)
-			fs_group<METRIC, T, 2>(X, ld, dim, Qf, ng, sslot, sq, spair, xs, qs, sk, o0, ostride, kk);
-		else if (ng <= 4)
-			fs_group<METRIC, T, 4>(X, ld, dim, Qf, ng, sslot, sq, spair, xs, qs, sk, o0, ostride, kk);
-		else if (ng <= 8)
-			fs_group<METRIC, T, 8>(X, ld, dim, Qf, ng, sslot, sq, spair, xs, qs, sk, o0, ostride, kk);
-		else
-			fs_group<METRIC, T, FS_G>(X, ld, dim, Qf, ng, sslot, sq, spair, xs, qs, sk, o0, ostride, kk);
+#define FS_CALL(GG) fs_group<METRIC, T, GG>(X, ld, dim, Qd, qn2, ng, sslot, sq, spair, xs, sk, o0, ostride, kk)
+		if (ng <= 2) FS_CALL(2);
+		else if (ng <= 4) FS_CALL(4);
+		else if (ng <= 8) FS_CALL(8);
+		else FS_CALL(FS_G);
+#undef FS_CALL
 	}
 }
 
@@ -952,11 +968,11 @@ template <typename T>
 static void flat_scan_dispatch(const StoreView &s, const int *blk_list, const int64_t *blk_pos0, const int *lblk0,
                                const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart,
                                const int *pairs, int nprobe, int maxb, int64_t tail_s0, int64_t tail_n, int nq,
-                               const float *Qf, int kk, uint64_t *out, hipStream_t st) {
+                               const double *Qd, const double *qn2, int kk, uint64_t *out, hipStream_t st) {
 	const T *X = static_cast<const T *>(s.X);
 	const float *ra = reinterpret_cast<const float *>(s.rowaux);
 	dim3 grid((unsigned)nblk);
-#define FS_ARGS X, s.ld, s.dim, ra, blk_list, blk_pos0, lblk0, loff, lslot, pstart, pairs, nprobe, maxb, tail_s0, tail_n, nq, Qf, kk, out
+#define FS_ARGS X, s.ld, s.dim, ra, blk_list, blk_pos0, lblk0, loff, lslot, pstart, pairs, nprobe, maxb, tail_s0, tail_n, nq, Qd, qn2, kk, out
 	switch (s.metric) {
 	case METRIC_L2: flat_list_scan_kernel<METRIC_L2, T><<<grid, 256, 0, st>>>(FS_ARGS); break;
 	case METRIC_DOT: flat_list_scan_kernel<METRIC_DOT, T><<<grid, 256, 0, st>>>(FS_ARGS); break;
@@ -967,15 +983,15 @@ static void flat_scan_dispatch(const StoreView &s, const int *blk_list, const in
 
 void launch_flat_list_scan(const StoreView &s, const int *blk_list, const int64_t *blk_pos0, const int *lblk0,
                            const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart, const int *pairs,
-                           int nprobe, int maxb, int64_t tail_s0, int64_t tail_n, int nq, const float *Qf, int kk,
+                           int nprobe, int maxb, int64_t tail_s0, int64_t tail_n, int nq, const double *Qd, const double *qn2, int kk,
                            uint64_t *out, hipStream_t st) {
 	if (nblk <= 0) return;
 	if (s.xbf16)
 		flat_scan_dispatch<uint16_t>(s, blk_list, blk_pos0, lblk0, loff, lslot, nblk, pstart, pairs, nprobe, maxb,
-		                             tail_s0, tail_n, nq, Qf, kk, out, st);
+		                             tail_s0, tail_n, nq, Qd, qn2, kk, out, st);
 	else
 		flat_scan_dispatch<float>(s, blk_list, blk_pos0, lblk0, loff, lslot, nblk, pstart, pairs, nprobe, maxb,
-		                          tail_s0, tail_n, nq, Qf, kk, out, st);
+		                          tail_s0, tail_n, nq, Qd, qn2, kk, out, st);
 }
 
 // ---------------------------------------------------------------------------
