@@ -55,6 +55,21 @@ __device__ void wg_bitonic_sort(uint64_t *a, int n) {
 	__syncthreads();
 }
 
+// ascending bitonic sort of one 64-bit key per lane across the wave (no LDS, no barrier)
+__device__ __forceinline__ uint64_t wave_sort64(uint64_t k) {
+	const int lane = threadIdx.x & 63;
+#pragma unroll
+	for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+		for (int stride = size >> 1; stride > 0; stride >>= 1) {
+			const uint64_t o = __shfl_xor(k, stride, 64);
+			const bool asc = (lane & size) == 0, lower = (lane & stride) == 0;
+			k = (lower == asc) ? (o < k ? o : k) : (o > k ? o : k);
+		}
+	}
+	return k;
+}
+
 __device__ __forceinline__ int pow2_ceil(int v) {
 	int p = 2;
 	while (p < v) p <<= 1;
@@ -895,11 +910,26 @@ __device__ __forceinline__ void fs_group(const T *__restrict__ X, int ld, int di
 			r = 1.0 - acc[g] / (sqrt(xx) * sqrt(qq));
 		float f = (float)r + 0.0f;
 		if (__builtin_isnan(f)) f = __builtin_nanf("");
-		__syncthreads();
-		sk[t] = valid ? key64(f, sslot[t]) : KEY64_NONE;
-		wg_bitonic_sort(sk, FLAT_BLK);
+		const uint64_t key = valid ? key64(f, sslot[t]) : KEY64_NONE;
 		uint64_t *o = o0 + (int64_t)spair[g] * ostride;
-		for (int i = t; i < kk; i += 256) o[i] = i < FLAT_BLK ? sk[i] : KEY64_NONE;
+		__syncthreads();  // sk reuse
+		if (kk <= 16) {
+			// each wave sorts its 64 keys in registers; the 4 x kk leaders are
+			// sorted again by wave 0: two barriers instead of the 36 of a
+			// workgroup bitonic sort of 256 keys
+			const uint64_t ks = wave_sort64(key);
+			const int lane = t & 63, w = t >> 6;
+			if (lane < kk) sk[w * kk + lane] = ks;
+			__syncthreads();
+			if (w == 0) {
+				const uint64_t k2 = wave_sort64(lane < 4 * kk ? sk[lane] : KEY64_NONE);
+				if (lane < kk) o[lane] = k2;
+			}
+		} else {
+			sk[t] = key;
+			wg_bitonic_sort(sk, FLAT_BLK);
+			for (int i = t; i < kk; i += 256) o[i] = i < FLAT_BLK ? sk[i] : KEY64_NONE;
+		}
 	}
 }
 
