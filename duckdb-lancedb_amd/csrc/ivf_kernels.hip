@@ -1171,14 +1171,19 @@ __global__ __launch_bounds__(PQ_THREADS) void pq_query_scan_kernel(
 				for (int i = 0; i < PQ_R; ++i) {
 					const int64_t ps = r0 + i * PQ_THREADS + t;
 					sl[i] = ps < end ? lslot[ps] : SLOT_NONE;
-					if (sl[i] != SLOT_NONE && !slot_alive(rowaux_f, sl[i])) sl[i] = SLOT_NONE;
 					pos[i] = ps < end ? ps : end - 1;  // in bounds; the key is dropped
 				}
 				float da[PQ_R];
 				pq_adc_r(lcodes, nch, m, pos, lut, d0, da);
+				// liveness (a random 4-B read of the row aux) only for keys that
+				// pass the current threshold: most rows stop at the compare
+				const uint64_t th = *tk.thr;
 #pragma unroll
-				for (int i = 0; i < PQ_R; ++i)
-					tk.offer(sl[i] != SLOT_NONE ? key64(da[i], sl[i]) : KEY64_NONE, sl[i] != SLOT_NONE);
+				for (int i = 0; i < PQ_R; ++i) {
+					const uint64_t key = sl[i] != SLOT_NONE ? key64(da[i], sl[i]) : KEY64_NONE;
+					const bool ok = sl[i] != SLOT_NONE && key < th && slot_alive(rowaux_f, sl[i]);
+					tk.offer(key, ok);
+				}
 			}
 		}
 	}
