@@ -835,27 +835,32 @@ void launch_invert(const int64_t *probe_l, int nq, int nprobe, int nlist, int *l
 // owns one row and accumulates (x - q)^2 (or x.q) in f64 for all FS_G queries.
 // ---------------------------------------------------------------------------
 constexpr int FS_G = 16;
-constexpr int FS_KC = 32;
-constexpr int FS_PIECES = FLAT_BLK * FS_KC / 4 / 256;  // float4 pieces per thread and chunk (8)
+#ifndef LHIP_FS_KC
+#define LHIP_FS_KC 32
+#endif
+constexpr int FS_KC = LHIP_FS_KC;                       // dims per staged chunk (32 or 64)
+constexpr int FS_NP = FS_KC / 4;                        // float4 pieces per row and chunk
+constexpr int FS_PIECES = FLAT_BLK * FS_KC / 4 / 256;  // float4 pieces per thread and chunk
 
 template <typename T>
 __device__ __forceinline__ void fs_fetch(const T *__restrict__ X, int ld, int dim, const uint32_t *sslot, int d0,
                                          float4 (&v)[FS_PIECES]) {
 #pragma unroll
 	for (int i = 0; i < FS_PIECES; ++i) {
-		const int e = threadIdx.x + i * 256, row = e >> 3, piece = e & 7;
+		const int e = threadIdx.x + i * 256, row = e / FS_NP, piece = e % FS_NP;
 		const uint32_t s = sslot[row];
 		v[i] = (s != SLOT_NONE && d0 < dim) ? load4(X + (int64_t)s * ld + d0 + piece * 4) : make_float4(0, 0, 0, 0);
 	}
 }
 
-// chunk of 32 dims of 256 rows as float4 pieces, piece p of row r at p ^ (r & 7):
-// one ds_write_b128 per loaded piece, one ds_read_b128 per 4 dims of a thread's row
-__device__ __forceinline__ void fs_store(float4 (*xs)[8], const float4 (&v)[FS_PIECES]) {
+// chunk of FS_KC dims of 256 rows as float4 pieces, piece p of row r at
+// p ^ (r % FS_NP): one ds_write_b128 per loaded piece, one ds_read_b128 per 4
+// dims of a thread's row
+__device__ __forceinline__ void fs_store(float4 (*xs)[FS_NP], const float4 (&v)[FS_PIECES]) {
 #pragma unroll
 	for (int i = 0; i < FS_PIECES; ++i) {
-		const int e = threadIdx.x + i * 256, row = e >> 3, piece = e & 7;
-		xs[row][piece ^ (row & 7)] = v[i];
+		const int e = threadIdx.x + i * 256, row = e / FS_NP, piece = e % FS_NP;
+		xs[row][piece ^ (row % FS_NP)] = v[i];
 	}
 }
 
@@ -868,7 +873,7 @@ __device__ __forceinline__ void fs_store(float4 (*xs)[8], const float4 (&v)[FS_P
 template <int METRIC, typename T, int G>
 __device__ __forceinline__ void fs_group(const T *__restrict__ X, int ld, int dim, const double *__restrict__ Qd,
                                          const double *__restrict__ qn2, int ng, const uint32_t *sslot,
-                                         const int *sq, const int *spair, float4 (*xs)[8], uint64_t *sk,
+                                         const int *sq, const int *spair, float4 (*xs)[FS_NP], uint64_t *sk,
                                          uint64_t *o0, int64_t ostride, int kk) {
 	const int t = threadIdx.x;
 	const double *qp[G];
@@ -885,8 +890,8 @@ __device__ __forceinline__ void fs_group(const T *__restrict__ X, int ld, int di
 		__syncthreads();
 		if (d0 + FS_KC < dim) fs_fetch<T>(X, ld, dim, sslot, d0 + FS_KC, v);  // in flight during the FMAs
 #pragma unroll 2
-		for (int j = 0; j < 8; ++j) {
-			const float4 x4 = xs[t][j ^ (t & 7)];
+		for (int j = 0; j < FS_NP; ++j) {
+			const float4 x4 = xs[t][j ^ (t % FS_NP)];
 			const double xv[4] = {(double)x4.x, (double)x4.y, (double)x4.z, (double)x4.w};
 #pragma unroll
 			for (int c = 0; c < 4; ++c) {
@@ -940,7 +945,7 @@ __global__ __launch_bounds__(256) void flat_list_scan_kernel(
     const uint32_t *__restrict__ lslot, const int *__restrict__ pstart, const int *__restrict__ pairs, int nprobe,
     int maxb, int64_t tail_s0, int64_t tail_n, int nq, const double *__restrict__ Qd, const double *__restrict__ qn2,
     int kk, uint64_t *__restrict__ out) {
-	__shared__ float4 xs[FLAT_BLK][8];
+	__shared__ float4 xs[FLAT_BLK][FS_NP];
 	__shared__ uint32_t sslot[FLAT_BLK];
 	__shared__ uint64_t sk[FLAT_BLK];
 	__shared__ int sq[FS_G], spair[FS_G];
