@@ -144,6 +144,24 @@ def measured_traffic(n, dim, batch, elem_bytes):
     return None if best is None else int(best["traffic_bytes_per_launch"])
 
 
+def ivf_traffic(config, n, dim, batch):
+    """Per-launch HBM bytes of the IVF list scan from the committed rocprofv3
+    PMC passes of the same config (profiles/*_<config>_ivf_traffic.json, made by
+    tools/pmc_passes.sh + tools/pmc_traffic.py)."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_ivf_traffic.json"))):
+        try:
+            with open(f) as fh:
+                t = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if (t.get("n"), t.get("dim"), t.get("batch")) == (n, dim, batch):
+            best = t
+    return None if best is None else int(best["traffic_bytes_per_launch"])
+
+
 def err_buf():
     return ctypes.create_string_buffer(2048)
 
@@ -292,7 +310,7 @@ def main_ivf(a):
             ach = bytes_launch / (avg_ms * 1e-3) / 1e9
             kname = "flat_list_scan_kernel" if a.index_type == "ivf_flat" else "pq_query_scan_kernel"
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": ivf_traffic(a.config, N, D, BG), "kernel": kname,
                     "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(bytes_launch),
                     "pair_rows_per_launch": int(kt["ivf_pair_rows"] / kt["ivf_scan_launches"]),
                     "coarse_ms_per_batch": round(kt["ivf_coarse_ms_total"] / kt["ivf_scan_launches"], 4)}
