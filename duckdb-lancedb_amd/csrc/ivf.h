@@ -9,9 +9,10 @@
 //            top-nprobe by (distance, list id)
 //   IVF_FLAT exact distance of every live row of the probed lists,
 //            top-k by (distance, label)
-//   IVF_PQ   ADC(q, row) = d0 + sum_j LUT[j][code_j], summed in f32 in j order,
-//            d0 = the coarse distance of the row's list, LUT = T[list] - 2 P[q]
-//            (L2 / cosine, residual PQ) or -P[q] (dot), with
+//   IVF_PQ   ADC(q, row) = (d0 + tau_row) + sum_j LUT[j][code_j], summed in f32
+//            in j order, d0 = the coarse distance of the row's list, LUT =
+//            -2 P[q] and tau_row = sum_j T[list][j][code_j] (f32, j order, from
+//            0) for L2 / cosine (residual PQ); LUT = -P[q], tau = 0 for dot; with
 //              P[q][j][c] = sum_t q_{j,t} * y_{j,c,t}
 //              T[l][j][c] = sum_t y_{j,c,t} * (y_{j,c,t} + 2 c_{l,j,t})
 //            (f32, t in order, no fused multiply-add); top-(k*refine_factor)
@@ -51,6 +52,7 @@ struct IvfState {
 	DevBuf<int64_t> loff;
 	DevBuf<uint32_t> lslot;                  // [npos] slot, SLOT_NONE for padding
 	DevBuf<uint8_t> lcodes;                  // [npos/64][mp/16][64][16] blocked codes
+	DevBuf<float> ltau;                      // [npos] row term of the L2 / cosine ADC (list order)
 	DevBuf<int> blk_list, lblk0;             // IVF_FLAT work items (256 positions each)
 	DevBuf<int64_t> blk_pos0;
 	int nblk = 0, maxb = 1;
@@ -138,8 +140,11 @@ int pq_segments(int nq);
 // out [nq][S][kk]: per (query, segment) top-kk (ADC, slot) keys
 void launch_pq_query_scan(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
                           const float *rowaux_f, int nq, int nprobe, const int64_t *probe_l, const float *probe_d,
-                          const float *T, const float *P, const int64_t *pref, int S, int kk, uint64_t *out,
+                          const float *ltau, const float *P, const int64_t *pref, int S, int kk, uint64_t *out,
                           hipStream_t st);
+// ltau [npos]: per list position sum_j T[l][j][c_j] (f32, j ascending), 0 for padding
+void launch_pq_tau(const uint8_t *codes, const uint32_t *lslot, const int64_t *loff, int nlist, int64_t npos, int m,
+                   int mp, const float *T, float *ltau, hipStream_t st);
 // per query: top-K keys over the list-scan outputs of its probes (nblk_of
 // lists via lblk0, or 1 per probe when lblk0 is null) and/or a tail output.
 void launch_ivf_merge(int nq, int nprobe, const int64_t *probe_l, const int *lblk0, int maxb, int kk,

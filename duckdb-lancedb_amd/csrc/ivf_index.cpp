@@ -411,6 +411,10 @@ static void layout(Index *ix) {
 	} else {
 		s->lcodes.need((size_t)std::max<int64_t>(npos, 64) * s->mp);
 		launch_pq_layout(s->codes.p, s->lslot.p, npos, s->mp, s->lcodes.p, st);
+		if (s->metric != METRIC_DOT) {
+			s->ltau.need((size_t)std::max<int64_t>(npos, 1));
+			launch_pq_tau(s->codes.p, s->lslot.p, s->loff.p, nl, npos, s->m, s->mp, s->T.p, s->ltau.p, st);
+		}
 		HIPCHK(hipGetLastError());
 	}
 	HIPCHK(hipStreamSynchronize(st));
@@ -418,20 +422,21 @@ static void layout(Index *ix) {
 }
 
 // time_kernels: the list-scan launch (events 0/1 on the handle's stream) and
-// its algorithmic work: every probed list's rows (IVF_FLAT: dim x esz bytes;
-// IVF_PQ: m code bytes) once, plus the per-(query, list) LUT inputs of IVF_PQ
-// (T[l] and P[q], m x 256 f32 each); pair rows = sum over pairs of list rows.
-static void account_list_scan(Index *ix, int esz) {
+// its algorithmic work: every probed list's rows once (IVF_FLAT: dim x esz
+// bytes; IVF_PQ: m code bytes + the 4-B row term tau for L2 / cosine) plus, for
+// IVF_PQ, each query's LUT input P[q] (m x 256 f32) once; pair rows = sum over
+// (query, list) pairs of the list's rows.
+static void account_list_scan(Index *ix, int esz, int nq) {
 	IvfState *s = ix->ivf;
 	std::vector<int> ps((size_t)s->nlist + 1);
 	HIPCHK(hipMemcpy(ps.data(), s->pstart.p, ps.size() * sizeof(int), hipMemcpyDeviceToHost));
-	double bytes = 0.0, pair_rows = 0.0;
-	const double lut = (double)s->m * PQ_K * 4.0 * (s->metric == METRIC_DOT ? 1.0 : 2.0);
+	double bytes = esz ? 0.0 : (double)nq * s->m * PQ_K * 4.0, pair_rows = 0.0;
+	const double row_pq = (double)s->m + (s->metric == METRIC_DOT ? 0.0 : 4.0);
 	for (int l = 0; l < s->nlist; ++l) {
 		const int np = ps[(size_t)l + 1] - ps[(size_t)l];
 		if (np <= 0) continue;
 		const double rows = (double)s->h_lcnt[(size_t)l];
-		bytes += esz ? rows * ix->dim * esz : rows * s->m + np * lut;
+		bytes += esz ? rows * ix->dim * esz : rows * row_pq;
 		pair_rows += rows * np;
 	}
 	ix->kt_ivf_ms += ix->toc_ms(0, 1);
@@ -512,7 +517,7 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			ix->tic(0);
 			launch_pq_query_scan(s->lcodes.p, s->m, s->mp, s->loff.p, s->lslot.p,
 			                     reinterpret_cast<const float *>(sv.rowaux), n, nprobe, s->probe_l.p, s->probe_d.p,
-			                     s->metric == METRIC_DOT ? nullptr : s->T.p, s->P.p, s->pref.p, S, kp, s->keys.p, st);
+			                     s->metric == METRIC_DOT ? nullptr : s->ltau.p, s->P.p, s->pref.p, S, kp, s->keys.p, st);
 			ix->tic(1);
 			s->cand_a.need((size_t)n * kp);
 			// the S segment lists of each query: the merge kernel's tail mode ([q][S][kp])
@@ -526,7 +531,7 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 		}
 		HIPCHK(hipGetLastError());
 		spin_sync(st);
-		if (ix->time_kernels) account_list_scan(ix, s->type == IVF_FLAT ? (ix->xbf16 ? 2 : 4) : 0);
+		if (ix->time_kernels) account_list_scan(ix, s->type == IVF_FLAT ? (ix->xbf16 ? 2 : 4) : 0, n);
 	}
 }
 

@@ -723,6 +723,36 @@ void launch_pq_layout(const uint8_t *codes, const uint32_t *lslot, int64_t npos,
 	pq_layout_kernel<<<dim3((unsigned)((tot + 255) / 256)), 256, 0, st>>>(codes, lslot, npos, mp, lcodes);
 }
 
+// list-ordered row term of the L2 / cosine ADC: tau[pos] = sum_j T[l][j][c_j]
+// (f32, j ascending, from 0) of the row at pos in list l; 0 for padding
+__global__ void pq_tau_kernel(const uint8_t *__restrict__ codes, const uint32_t *__restrict__ lslot,
+                              const int64_t *__restrict__ loff, int nlist, int64_t npos, int m, int mp,
+                              const float *__restrict__ T, float *__restrict__ ltau) {
+	const int64_t pos = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (pos >= npos) return;
+	const uint32_t slot = lslot[pos];
+	float acc = 0.0f;
+	if (slot != SLOT_NONE) {
+		int lo = 0, hi = nlist - 1;  // list of pos: last l with loff[l] <= pos
+		while (lo < hi) {
+			const int mid = (lo + hi + 1) >> 1;
+			if (loff[mid] <= pos) lo = mid;
+			else hi = mid - 1;
+		}
+		const float *Tl = T + (int64_t)lo * m * PQ_K;
+		const uint8_t *c = codes + (int64_t)slot * mp;
+		for (int j = 0; j < m; ++j) acc = acc + Tl[j * PQ_K + c[j]];
+	}
+	ltau[pos] = acc;
+}
+
+void launch_pq_tau(const uint8_t *codes, const uint32_t *lslot, const int64_t *loff, int nlist, int64_t npos, int m,
+                   int mp, const float *T, float *ltau, hipStream_t st) {
+	if (npos <= 0) return;
+	pq_tau_kernel<<<dim3((unsigned)((npos + 255) / 256)), 256, 0, st>>>(codes, lslot, loff, nlist, npos, m, mp, T,
+	                                                                      ltau);
+}
+
 // ---------------------------------------------------------------------------
 // search: query prep, probe inversion
 // ---------------------------------------------------------------------------
@@ -1087,16 +1117,17 @@ void launch_probe_prefix(const int64_t *probe_l, int nq, int nprobe, const int64
 	probe_prefix_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(probe_l, nprobe, loff, pref);
 }
 
-// ADCs of PQ_R rows at list positions pos[i] (canonical f32 order: d0, then
-// j = 0..m-1), the PQ_R chains interleaved so their LDS lookups overlap
+// ADCs of PQ_R rows at list positions pos[i] (canonical f32 order: d0 + tau,
+// then j = 0..m-1), the PQ_R chains interleaved so their LDS lookups overlap
 constexpr int PQ_R = 4;
 __device__ __forceinline__ void pq_adc_r(const uint8_t *__restrict__ lcodes, int nch, int m, const int64_t (&pos)[PQ_R],
-                                         const float *lut, float d0, float (&acc)[PQ_R]) {
+                                         const float *lut, float d0, const float *__restrict__ ltau,
+                                         float (&acc)[PQ_R]) {
 	const uint8_t *cp[PQ_R];
 #pragma unroll
 	for (int i = 0; i < PQ_R; ++i) {
 		cp[i] = lcodes + ((pos[i] >> 6) * nch * 64 + (pos[i] & 63)) * 16;
-		acc[i] = d0;
+		acc[i] = ltau ? d0 + ltau[pos[i]] : d0;
 	}
 	for (int ch = 0; ch < nch; ++ch) {
 		uint32_t wd[PQ_R][4];
@@ -1121,14 +1152,15 @@ __device__ __forceinline__ void pq_adc_r(const uint8_t *__restrict__ lcodes, int
 
 // IVF_PQ scan, query-major: workgroup (s, q) takes segment s of S of the
 // concatenation of query q's probed lists (balanced whatever the list sizes),
-// builds the (q, list) LUT = T[l] - 2 P[q] (or -P[q]) in LDS for each list it
-// enters, and keeps ONE streaming top-kk over its whole segment (the threshold
-// tightens across lists).  Rows stream as 16-B code pieces of the 64-row
+// builds the query's LUT -2 P[q] (L2 / cosine; -P[q] for dot) in LDS ONCE (the
+// list term T[l][j][c_j] is folded into the per-row tau at index time), and
+// keeps ONE streaming top-kk over its whole segment (the threshold tightens
+// across lists).  Rows stream as 16-B code pieces of the 64-row
 // blocked layout, PQ_R rows per thread per round.
 __global__ __launch_bounds__(PQ_THREADS) void pq_query_scan_kernel(
     const uint8_t *__restrict__ lcodes, int m, int mp, const int64_t *__restrict__ loff,
     const uint32_t *__restrict__ lslot, const float *__restrict__ rowaux_f, int nprobe,
-    const int64_t *__restrict__ probe_l, const float *__restrict__ probe_d, const float *__restrict__ T,
+    const int64_t *__restrict__ probe_l, const float *__restrict__ probe_d, const float *__restrict__ ltau,
     const float *__restrict__ P, const int64_t *__restrict__ pref, int S, int kk, uint64_t *__restrict__ out) {
 	__shared__ float lut[PQ_MAX_M * PQ_K];
 	__shared__ uint64_t buf[IVF_TOPK_CAP];
@@ -1144,6 +1176,9 @@ __global__ __launch_bounds__(PQ_THREADS) void pq_query_scan_kernel(
 	TopK tk{buf, &cnt, &thr, kk};
 	tk.reset();
 	if (a < b) {
+		const float *Pq = P + (int64_t)q * nlut;
+		const float sP = ltau ? -2.0f : -1.0f;  // exact scaling
+		for (int e = t; e < nlut; e += PQ_THREADS) lut[e] = sP * Pq[e];
 		if (t == 0) {  // last probe starting at or before a
 			int lo = 0, hi = nprobe - 1;
 			while (lo < hi) {
@@ -1159,15 +1194,6 @@ __global__ __launch_bounds__(PQ_THREADS) void pq_query_scan_kernel(
 			if (g0 >= g1) continue;
 			const int64_t l = probe_l[(int64_t)q * nprobe + p];
 			const float d0 = probe_d[(int64_t)q * nprobe + p];
-			__syncthreads();  // the previous list's LUT readers are done
-			const float *Pq = P + (int64_t)q * nlut;
-			if (T) {
-				const float *Tl = T + l * nlut;
-				for (int e = t; e < nlut; e += PQ_THREADS) lut[e] = Tl[e] - 2.0f * Pq[e];
-			} else {
-				for (int e = t; e < nlut; e += PQ_THREADS) lut[e] = -Pq[e];
-			}
-			__syncthreads();
 			const int64_t end = loff[l] + (g1 - pr[p]);
 			for (int64_t r0 = loff[l] + (g0 - pr[p]); r0 < end; r0 += PQ_R * PQ_THREADS) {
 				int64_t pos[PQ_R];
@@ -1179,7 +1205,7 @@ __global__ __launch_bounds__(PQ_THREADS) void pq_query_scan_kernel(
 					pos[i] = ps < end ? ps : end - 1;  // in bounds; the key is dropped
 				}
 				float da[PQ_R];
-				pq_adc_r(lcodes, nch, m, pos, lut, d0, da);
+				pq_adc_r(lcodes, nch, m, pos, lut, d0, ltau, da);
 				// liveness (a random 4-B read of the row aux) only for keys that
 				// pass the current threshold: most rows stop at the compare
 				const uint64_t th = *tk.thr;
@@ -1201,10 +1227,10 @@ int pq_segments(int nq) { return std::max(1, std::min(32, (4096 + nq - 1) / std:
 
 void launch_pq_query_scan(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
                           const float *rowaux_f, int nq, int nprobe, const int64_t *probe_l, const float *probe_d,
-                          const float *T, const float *P, const int64_t *pref, int S, int kk, uint64_t *out,
+                          const float *ltau, const float *P, const int64_t *pref, int S, int kk, uint64_t *out,
                           hipStream_t st) {
 	pq_query_scan_kernel<<<dim3((unsigned)S, (unsigned)nq), PQ_THREADS, 0, st>>>(
-	    lcodes, m, mp, loff, lslot, rowaux_f, nprobe, probe_l, probe_d, T, P, pref, S, kk, out);
+	    lcodes, m, mp, loff, lslot, rowaux_f, nprobe, probe_l, probe_d, ltau, P, pref, S, kk, out);
 }
 
 // ---------------------------------------------------------------------------

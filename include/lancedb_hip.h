@@ -199,7 +199,7 @@ int32_t lance_hip_last_search_stats(void *handle, int64_t *out, int32_t n);
  * dense scans, out[5] their count, out[6] bytes per element the scan streams
  * (2 with a bf16 store or scan copy, else 4), out[7] total ms of IVF list-scan
  * launches, out[8] their count, out[9] their algorithmic bytes (every probed
- * list's rows or codes once + per-pair tables, summed), out[10] (query, row)
+ * list's rows or codes once + each query's PQ table, summed), out[10] (query, row)
  * pairs scored (summed), out[11] total ms of the IVF coarse searches.
  * Returns 0 or -1. */
 int32_t lance_hip_kernel_times(void *handle, double *out, int32_t n);

@@ -226,6 +226,8 @@ void oracle_distances(const float *base, int64_t n, int32_t d, const float *q, i
  *   tail [ntail] live slots not indexed (searched exactly);
  *   C [nlist][d] centroids; IVF_PQ when codes != NULL: codes [n][m] (by slot),
  *   codebook cb [m][256][d/m], T [nlist][m][256] (NULL for dot).
+ *   ADC = (d0 + tau) + sum_j LUT[j][c_j] (f32, j order), tau = sum_j
+ *   T[l][j][c_j] (f32 from 0), LUT = -2 P (l2) / -P and tau = 0 (dot).
  *   metric 0 l2, 1 dot (cosine: -2, not ported).  acc64: f64 exact distances
  *   (the checker) or f32 SIMD (the timed baseline) for the coarse / flat /
  *   re-rank distances; the ADC is f32 in j order in both.
@@ -294,7 +296,7 @@ int oracle_ivf_search_batch(const float *base, int32_t d, const int64_t *labels,
 			for (int32_t p = 0; p < nprobe; p++) {
 				const int32_t l = pid[p];
 				if (pq) {
-					for (int e = 0; e < m * 256; e++) lut[e] = T ? T[(size_t)l * m * 256 + e] - 2.0f * P[e] : -P[e];
+					for (int e = 0; e < m * 256; e++) lut[e] = T ? -2.0f * P[e] : -P[e];
 				}
 				for (int64_t i = loff[l]; i < loff[l + 1]; i++) {
 					const int64_t s = lrows[i];
@@ -302,6 +304,12 @@ int oracle_ivf_search_batch(const float *base, int32_t d, const int64_t *labels,
 					if (pq) {
 						const uint8_t *c = codes + (size_t)s * m;
 						float acc = pd[p];
+						if (T) { /* row term tau = sum_j T[l][j][c_j], then the query LUT */
+							const float *Tl = T + (size_t)l * m * 256;
+							float tau = 0.0f;
+							for (int j = 0; j < m; j++) tau = tau + Tl[j * 256 + c[j]];
+							acc = acc + tau;
+						}
 						for (int j = 0; j < m; j++) acc = acc + lut[j * 256 + c[j]];
 						dd = acc;
 					} else {

@@ -23,10 +23,13 @@ What it restates (reference paths relative to ``/root/reference``):
             dot for a dot index, L2 otherwise (cosine: L2 between the
             normalised query and the centroids) — top-nprobe by (dist, id)
   IVF_FLAT  exact distance of every live row of the probed lists
-  IVF_PQ    ADC = d0 + sum_j LUT[j][code_j] in f32, j ascending, d0 = the
-            coarse distance; LUT = T[l] - 2 P[q] (L2/cosine) or -P[q] (dot),
-            P[j][c] = sum_t q_t y_t, T[l][j][c] = sum_t y_t (y_t + 2 c_t), each
-            an f32 sum in t order of f32 products (no fused multiply-add);
+  IVF_PQ    ADC = (d0 + tau) + sum_j LUT[j][code_j] in f32, j ascending, d0 =
+            the coarse distance; L2/cosine: LUT = -2 P[q] and the row term
+            tau = sum_j T[l][j][code_j] (f32, j ascending, from 0; the HIP
+            path computes it once per row at index time); dot: LUT = -P[q],
+            tau = 0.  P[j][c] = sum_t q_t y_t, T[l][j][c] = sum_t y_t (y_t +
+            2 c_t), each an f32 sum in t order of f32 products (no fused
+            multiply-add);
             top-(k*r) by (ADC, label), exact re-rank, top-k by (dist, label)
   cosine    q^ = q / f32(sqrt(sum q^2)) (an f32 division) for the coarse
             search and P; the final distances are exact cosine distances.
@@ -148,8 +151,13 @@ def ivf_pq_search(X, labels, live, lists, codes, C, codebook, Q, k, nprobe, refi
             rows = np.nonzero(live & (lists == l))[0]
             if rows.size == 0:
                 continue
-            lut = (T[l] - F32(2.0) * P[i]).astype(F32) if T is not None else (-P[i]).astype(F32)
+            lut = (F32(-2.0) * P[i]).astype(F32) if T is not None else (-P[i]).astype(F32)
             acc = np.full(rows.size, pd[i, p], F32)
+            if T is not None:
+                tau = np.zeros(rows.size, F32)
+                for j in range(m):
+                    tau = (tau + T[l][j, codes[rows, j]]).astype(F32)
+                acc = (acc + tau).astype(F32)
             for j in range(m):
                 acc = (acc + lut[j, codes[rows, j]]).astype(F32)
             cand_adc.append(acc)

@@ -6,7 +6,7 @@ shift
 O=gpurun_out
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_ivf.py -x -v --timeout 120 --timeout-method thread > $O/${T}_pytest.log 2>&1 || { echo "ivf pytest FAILED"; tail -40 $O/${T}_pytest.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ivf.py tests/test_gpu_filter.py tests/test_distributed.py -x -v --timeout 120 --timeout-method thread > $O/${T}_pytest.log 2>&1 || { echo "ivf pytest FAILED"; tail -40 $O/${T}_pytest.log; exit 1; }
 tail -3 $O/${T}_pytest.log
 bash tools/gpu_ivf_bench.sh $T "$@"
 if [ -n "$IVF_PROF" ]; then
