@@ -548,6 +548,17 @@ struct Index {
 		fwrite(b.data(), 1, b.size(), log);
 		fflush(log);
 	}
+	void log_scalar_index(const std::string &col, const std::string &ty) {
+		if (!log) return;
+		uint8_t tag = 8;
+		uint32_t a = (uint32_t)col.size(), b = (uint32_t)ty.size();
+		fwrite(&tag, 1, 1, log);
+		fwrite(&a, 4, 1, log);
+		fwrite(col.data(), 1, a, log);
+		fwrite(&b, 4, 1, log);
+		fwrite(ty.data(), 1, b, log);
+		fflush(log);
+	}
 	void log_storage() {
 		if (!log) return;
 		uint8_t tag = 3, v = xbf16 ? 1 : 0;

@@ -218,6 +218,17 @@ static void replay_log(Index *ix, const std::string &path) {
 		} else if (tag == 5) {
 			ix->compact();
 			ivf_optimize(ix);
+		} else if (tag == 8) {
+			// scalar index record: column, type (rebuilt over the rows present here)
+			uint32_t a = 0, b = 0;
+			if (fread(&a, 4, 1, f) != 1 || a > 4096) break;
+			std::string col(a, '\0');
+			if (fread(&col[0], 1, a, f) != a || fread(&b, 4, 1, f) != 1 || b > 64) break;
+			std::string ty(b, '\0');
+			if (fread(&ty[0], 1, b, f) != b) break;
+			if (ix->meta)
+				for (auto &c : ix->meta->cols)
+					if (c.name == col) c.build_index(ty);
 		} else if (tag == 6 || tag == 7) {
 			// multi-column table: metadata schema / the rows of the batch just replayed
 			int64_t n;
@@ -476,13 +487,29 @@ int32_t lance_detached_add_batch_arrow(void *handle, void *arrow_schema, void *a
 // NEW — the predicate evaluator of filtered search on a host Arrow batch (no
 // device, nothing taken over): mask[r] = live[r] && predicate TRUE for row r.
 int64_t lance_hip_predicate_mask(void *arrow_schema, void *arrow_array, const int64_t *labels, const uint8_t *live,
-                                 const char *predicate, uint8_t *out_mask, char *err_buf, int err_buf_len) {
+                                 const char *predicate, const char *indexed_columns, uint8_t *out_mask, char *err_buf,
+                                 int err_buf_len) {
 	try {
 		if (!arrow_schema || !arrow_array || !labels || !live || !out_mask) throw Error("null argument");
 		const ArrowSchema *sch = static_cast<const ArrowSchema *>(arrow_schema);
 		auto m = lhip::MetaStore::from_schema(sch);
 		std::vector<float> vecs;
 		const int64_t n = m->import_batch(sch, static_cast<const ArrowArray *>(arrow_array), vecs);
+		// comma-separated columns to evaluate through a scalar index
+		const std::string ic = cstr(indexed_columns);
+		for (size_t a = 0; a < ic.size();) {
+			size_t b = ic.find(',', a);
+			if (b == std::string::npos) b = ic.size();
+			const std::string name = ic.substr(a, b - a);
+			bool found = false;
+			for (auto &c : m->cols)
+				if (c.name == name) {
+					c.build_index("BTREE");
+					found = true;
+				}
+			if (!found && !name.empty()) throw Error("no column named '" + name + "'");
+			a = b + 1;
+		}
 		std::vector<int64_t> lab(labels, labels + n);
 		std::vector<uint8_t> lv(live, live + n), mask;
 		const int64_t c = lhip::eval_predicate(cstr(predicate), m.get(), lab, lv, mask);
@@ -490,6 +517,38 @@ int64_t lance_hip_predicate_mask(void *arrow_schema, void *arrow_array, const in
 		return c;
 	}
 	API_GUARD("predicate failed: ", -1)
+}
+
+// The call the reference's C++ already makes (lance_index.cpp:481-486) with no
+// declaration or Rust export behind it: a scalar index on a
+// metadata column, used by search predicates that compare the column with a
+// literal.  index_type (case-insensitive): "BTREE" (default for NULL / "") or
+// "BITMAP"; `label` is implicitly ordered (no-op).  0 or -1.
+int32_t lance_detached_create_scalar_index(void *handle, const char *column, const char *index_type, char *err_buf,
+                                           int err_buf_len) {
+	if (!handle) {
+		lhip::write_err(err_buf, err_buf_len, "null handle");
+		return -1;
+	}
+	try {
+		Index *ix = as_index(handle);
+		std::lock_guard<std::mutex> g(ix->mu);
+		std::string ty = cstr(index_type);
+		for (auto &ch : ty) ch = (char)toupper((unsigned char)ch);
+		if (ty.empty()) ty = "BTREE";
+		if (ty != "BTREE" && ty != "BITMAP") throw Error("unsupported scalar index type '" + cstr(index_type) + "'");
+		const std::string col = cstr(column);
+		if (col == "label") return 0;
+		lhip::MetaColumn *mc = nullptr;
+		if (ix->meta)
+			for (auto &c : ix->meta->cols)
+				if (c.name == col) mc = &c;
+		if (!mc) throw Error("no column named '" + col + "'");
+		mc->build_index(ty);
+		ix->log_scalar_index(col, ty);
+		return 0;
+	}
+	API_GUARD("create_scalar_index failed: ", -1)
 }
 
 int32_t lance_detached_merge(void *target_handle, void *source_handle, const int64_t *live_source_labels,

@@ -168,7 +168,40 @@ void MetaStore::keep_slots(const std::vector<int64_t> &keep) {
 		c.i.swap(nc.i);
 		c.f.swap(nc.f);
 		c.s.swap(nc.s);
+		if (c.index) c.build_index(c.index->type);  // slots moved
 	}
+}
+
+// total order of the index: NaN after every number (DataFusion's order), ties by slot
+void MetaColumn::build_index(const std::string &ty) {
+	auto ix = std::make_shared<ColIndex>();
+	ix->type = ty;
+	ix->n_indexed = (int64_t)size();
+	for (int64_t r = 0; r < ix->n_indexed; ++r)
+		if (valid[(size_t)r]) ix->perm.push_back((uint32_t)r);
+	auto less = [&](uint32_t a, uint32_t b) {
+		switch (type) {
+		case COL_INT:
+		case COL_BOOL:
+			if (i[a] != i[b]) return i[a] < i[b];
+			break;
+		case COL_FLOAT: {
+			const double x = f[a], y = f[b];
+			const bool nx = std::isnan(x), ny = std::isnan(y);
+			if (nx != ny) return ny;
+			if (!nx && x != y) return x < y;
+			break;
+		}
+		case COL_STRING: {
+			const int c = s[a].compare(s[b]);
+			if (c != 0) return c < 0;
+			break;
+		}
+		}
+		return a < b;
+	};
+	std::sort(ix->perm.begin(), ix->perm.end(), less);
+	index = ix;
 }
 
 void MetaStore::append_rows(const MetaStore &src, const std::vector<int64_t> &src_slots) {
@@ -596,15 +629,16 @@ struct Eval {
 		const std::vector<double> *f = nullptr;
 		const std::vector<std::string> *s = nullptr;
 		const std::vector<uint8_t> *valid = nullptr;  // null = all valid
+		const ColIndex *index = nullptr;
 	};
 	ColRef column(const std::string &name) const {
 		if (meta)
 			for (auto &c : meta->cols)
-				if (c.name == name) return ColRef{c.type, &c.i, &c.f, &c.s, &c.valid};
+				if (c.name == name) return ColRef{c.type, &c.i, &c.f, &c.s, &c.valid, c.index.get()};
 		if (name == "label") return ColRef{COL_INT, &labels, nullptr, nullptr, nullptr};
 		if (meta)
 			for (auto &c : meta->cols)  // DataFusion folds unquoted identifiers to lower case
-				if (upper(c.name) == upper(name)) return ColRef{c.type, &c.i, &c.f, &c.s, &c.valid};
+				if (upper(c.name) == upper(name)) return ColRef{c.type, &c.i, &c.f, &c.s, &c.valid, c.index.get()};
 		throw Error("predicate: no column named '" + name + "'");
 	}
 	static Value at(const ColRef &c, size_t r) {
@@ -673,9 +707,54 @@ struct Eval {
 		}
 		throw Error("predicate: comparison operands must be columns or literals");
 	}
+	// indexed column vs literal: the rows of [0, n_indexed) that satisfy the
+	// comparison are one or two ranges of the sorted permutation
+	bool cmp_indexed(const ColRef &c, const Value &lit, const std::string &op, std::vector<uint8_t> &out) {
+		const ColIndex &ix = *c.index;
+		const bool str = c.type == COL_STRING, lstr = lit.kind == Value::STR;
+		if (str != lstr) return false;                                  // type error: generic path reports it
+		if ((c.type == COL_BOOL) != (lit.kind == Value::BOOL)) return false;
+		if (c.type == COL_INT && lit.kind == Value::FLT) return false;  // mixed int / float: generic path
+		// sign of (value of perm[p]) - literal, monotone in p
+		auto sgn = [&](uint32_t r) -> int {
+			if (str) {
+				const int k = (*c.s)[r].compare(lit.s);
+				return k < 0 ? -1 : k > 0;
+			}
+			if (c.type == COL_FLOAT) {
+				const double x = (*c.f)[r], y = lit.kind == Value::INT ? (double)lit.i : lit.f;
+				if (std::isnan(x) || std::isnan(y)) return std::isnan(x) && std::isnan(y) ? 0 : (std::isnan(x) ? 1 : -1);
+				return (x > y) - (x < y);
+			}
+			const int64_t x = (*c.i)[r], y = lit.i;
+			return (x > y) - (x < y);
+		};
+		const auto &pm = ix.perm;
+		const size_t lo = std::partition_point(pm.begin(), pm.end(), [&](uint32_t r) { return sgn(r) < 0; }) - pm.begin();
+		const size_t hi = std::partition_point(pm.begin() + lo, pm.end(), [&](uint32_t r) { return sgn(r) == 0; }) - pm.begin();
+		// [0, lo) < lit, [lo, hi) == lit, [hi, end) > lit
+		const size_t ni = (size_t)std::min<int64_t>(ix.n_indexed, (int64_t)n);
+		for (size_t r = 0; r < ni; ++r) out[r] = (!c.valid || (*c.valid)[r]) ? T_FALSE : T_NULL;
+		auto mark = [&](size_t a, size_t b) {
+			for (size_t p = a; p < b; ++p)
+				if (pm[p] < ni) out[pm[p]] = T_TRUE;
+		};
+		if (op == "=") mark(lo, hi);
+		else if (op == "!=") { mark(0, lo); mark(hi, pm.size()); }
+		else if (op == "<") mark(0, lo);
+		else if (op == "<=") mark(0, hi);
+		else if (op == ">") mark(hi, pm.size());
+		else mark(lo, pm.size());
+		for (size_t r = ni; r < n; ++r) {  // rows appended after the index was built
+			if (c.valid && !(*c.valid)[r]) continue;
+			out[r] = cmp_vals(at(c, r), lit, op) ? T_TRUE : T_FALSE;
+		}
+		return true;
+	}
 	std::vector<uint8_t> cmp_col_lit(const ColRef &c, const Value &lit, const std::string &op) {
 		std::vector<uint8_t> out(n, T_NULL);
 		if (lit.kind == Value::NUL) return out;
+		if (c.index && cmp_indexed(c, lit, op, out)) return out;
 		auto valid = [&](size_t r) { return !c.valid || (*c.valid)[r]; };
 		if (c.type == COL_INT && lit.kind == Value::INT) {  // exact int64 compare
 			const int64_t y = lit.i;

@@ -55,6 +55,17 @@ namespace lhip {
 
 enum ColType : int { COL_INT = 0, COL_FLOAT = 1, COL_BOOL = 2, COL_STRING = 3 };
 
+// scalar index of one column (lance_detached_create_scalar_index, the call at
+// lance_index.cpp:481-486; LanceDB BTREE / BITMAP): the non-NULL slots of
+// [0, n_indexed) sorted by (value, slot).  Comparisons of the column with a
+// literal take a binary-searched range of it instead of comparing every row;
+// slots appended later are compared one by one.
+struct ColIndex {
+	std::string type;            // "BTREE" | "BITMAP" (same structure here)
+	int64_t n_indexed = 0;
+	std::vector<uint32_t> perm;  // slots sorted by value
+};
+
 // one metadata column, values per slot (slot order = ascending label order)
 struct MetaColumn {
 	std::string name;
@@ -64,7 +75,9 @@ struct MetaColumn {
 	std::vector<double> f;     // COL_FLOAT
 	std::vector<std::string> s;  // COL_STRING
 	std::vector<uint8_t> valid;  // 1 = non-NULL
+	std::shared_ptr<ColIndex> index;  // scalar index, if created
 	size_t size() const { return valid.size(); }
+	void build_index(const std::string &type);  // over the current rows
 };
 
 struct MetaStore {

@@ -80,7 +80,9 @@ _SIGNATURES = [
     ("lance_hip_ivf_export", i32,
      [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_char_p, c_int]),
     ("lance_hip_ivf_set_model", i32, [c_void_p, i32, i32, i32, c_void_p, c_void_p, c_char_p, c_int]),
-    ("lance_hip_predicate_mask", i64, [c_void_p, c_void_p, c_void_p, c_void_p, c_char_p, c_void_p, c_char_p, c_int]),
+    ("lance_hip_predicate_mask", i64,
+     [c_void_p, c_void_p, c_void_p, c_void_p, c_char_p, c_char_p, c_void_p, c_char_p, c_int]),
+    ("lance_detached_create_scalar_index", i32, [c_void_p, c_char_p, c_char_p, c_char_p, c_int]),
 ]
 
 EXPORTED_SYMBOLS = [s[0] for s in _SIGNATURES]
@@ -257,8 +259,16 @@ def arrow_rows(vectors, extras=None, vector_name="vector"):
     return pa.StructArray.from_arrays(arrays, names=names)
 
 
-def LanceHipPredicateMask(struct_array, labels, live, predicate: str) -> np.ndarray:
-    """The library's predicate evaluator over a host Arrow batch (no device)."""
+def LanceDetachedCreateScalarIndex(handle, column: str, index_type: str = "BTREE") -> None:
+    """``LanceDetachedCreateScalarIndex`` as ``lance_index.cpp:481-486`` calls it."""
+    e = _err()
+    if lib().lance_detached_create_scalar_index(handle, _b(column), _b(index_type), e, ERR_BUF_LEN) != 0:
+        raise IOException("Lance create_scalar_index: " + e.value.decode())
+
+
+def LanceHipPredicateMask(struct_array, labels, live, predicate: str, indexed_columns=()) -> np.ndarray:
+    """The library's predicate evaluator over a host Arrow batch (no device);
+    indexed_columns go through a scalar index."""
     n = len(struct_array)
     lab = np.ascontiguousarray(labels, np.int64)
     lv = np.ascontiguousarray(live, np.uint8)
@@ -266,7 +276,8 @@ def LanceHipPredicateMask(struct_array, labels, live, predicate: str) -> np.ndar
     e = _err()
     with ArrowC(struct_array) as a:
         c = lib().lance_hip_predicate_mask(a.schema_ptr, a.array_ptr, lab.ctypes.data, lv.ctypes.data,
-                                           _b(predicate), out.ctypes.data, e, ERR_BUF_LEN)
+                                           _b(predicate), _b(",".join(indexed_columns)), out.ctypes.data, e,
+                                           ERR_BUF_LEN)
     if c < 0:
         raise IOException("Lance predicate: " + e.value.decode())
     return out[:n].astype(bool)
@@ -569,6 +580,12 @@ class LanceIndex:
         if self.rust_handle_ is None:
             raise IOException("Lance index not initialized")
         LanceDetachedCreateIndex(self.rust_handle_, num_partitions, num_sub_vectors)
+
+    # lance_index.cpp:481-486
+    def CreateScalarIndex(self, column: str, index_type: str) -> None:
+        if self.rust_handle_ is None:
+            raise IOException("Lance index not initialized")
+        LanceDetachedCreateScalarIndex(self.rust_handle_, column, index_type)
 
     def CreateHnswIndex(self, m: int, ef_construction: int) -> None:
         if self.rust_handle_ is None:

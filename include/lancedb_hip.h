@@ -133,6 +133,14 @@ int32_t lance_detached_delete_batch(void *handle, const int64_t *labels, int32_t
 int32_t lance_detached_create_index(void *handle, int32_t num_partitions, int32_t num_sub_vectors, char *err_buf,
                                     int err_buf_len);
 
+/* The call lance_index.cpp:481-486 already makes (LanceDetachedCreateScalarIndex,
+ * never declared nor exported by the reference): a scalar
+ * index ("BTREE" default, or "BITMAP") on a metadata column of a multi-column
+ * table; search predicates comparing the column with a literal use it.
+ * Persisted in the table log.  0 or -1. */
+int32_t lance_detached_create_scalar_index(void *handle, const char *column, const char *index_type, char *err_buf,
+                                           int err_buf_len);
+
 /* ffi.rs:425-445 (rust_ffi.cpp:176).  HNSW is out of scope:
  * returns 0 and keeps serving exact flat search (lance_hnsw.test pins only
  * result counts). */
@@ -232,9 +240,12 @@ int32_t lance_hip_merge_topk(int32_t nshard, int32_t nq, int32_t k, const int64_
 /* NEW — the filtered-search predicate evaluator on a host Arrow batch (struct
  * of [vector, extra...] as lance_detached_add_batch_arrow takes; nothing is
  * taken over, no device needed): out_mask[r] = live[r] && predicate TRUE for
- * row r with label labels[r].  Returns the selected count or -1. */
+ * row r with label labels[r]; indexed_columns (nullable, comma-separated) are
+ * evaluated through a scalar index as lance_detached_create_scalar_index builds
+ * it.  Returns the selected count or -1. */
 int64_t lance_hip_predicate_mask(void *arrow_schema, void *arrow_array, const int64_t *labels, const uint8_t *live,
-                                 const char *predicate, uint8_t *out_mask, char *err_buf, int err_buf_len);
+                                 const char *predicate, const char *indexed_columns, uint8_t *out_mask, char *err_buf,
+                                 int err_buf_len);
 
 /* NEW — IVF state: out[0] type (-1 none, 0 IVF_FLAT, 1 IVF_PQ), out[1] nlist,
  * out[2] m, out[3] dsub, out[4] rows indexed, out[5] slots.  0 or -1. */

@@ -218,3 +218,47 @@ def test_vector_only_table_label_predicate(hip, tmp_path):
         del live
     finally:
         hip.LanceFreeDetached(h)
+
+
+def test_scalar_index_filtered_search(hip, tmp_path):
+    # lance_index.cpp:481-486 CreateScalarIndex: same results through the index,
+    # for rows indexed and rows appended after it, and after a reopen
+    rng = np.random.default_rng(31)
+    n, d = 40_000, 32
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Q = rng.standard_normal((12, d)).astype(np.float32)
+    cols, types = _meta(rng, n)
+    h = _make(hip, X[:30_000], {k: v[:30_000] for k, v in cols.items()}, types, "l2", path=str(tmp_path))
+    hip.LanceDetachedCreateScalarIndex(h, "lang", "BITMAP")
+    hip.LanceDetachedCreateScalarIndex(h, "score", "btree")
+    hip.LanceDetachedCreateScalarIndex(h, "price", None)
+    hip.LanceDetachedCreateScalarIndex(h, "label", "BTREE")  # implicitly ordered: no-op
+    with pytest.raises(hip.IOException):
+        hip.LanceDetachedCreateScalarIndex(h, "nosuch", "BTREE")
+    with pytest.raises(hip.IOException):
+        hip.LanceDetachedCreateScalarIndex(h, "lang", "FTS")
+    batch = hip.arrow_rows(X[30_000:], [(nm, cols[nm][30_000:], t) for nm, t in types])
+    with hip.ArrowC(batch) as a:
+        hip.LanceDetachedAddBatchArrow(h, a.schema_ptr, a.array_ptr)
+    dead = rng.choice(n, 2000, replace=False)
+    hip.LanceDetachedDeleteBatch(h, dead)
+    live = np.ones(n, bool)
+    live[dead] = False
+    labels = np.arange(n)
+    preds = ["lang = 'fr'", "score >= 990 OR lang = 'it''s'", "price < 3.5 AND NOT (lang IN ('en', 'de'))",
+             "score BETWEEN 100 AND 105", "lang != 'en'"]
+    exp = {}
+    for pred in preds:
+        m = np.array(P.mask(pred, cols, labels, live))
+        exp[pred] = c_oracle.flat_search_batch(X, Q, 10, "l2", live=m, acc64=True)
+        assert_same(*hip.LanceDetachedSearchBatch(h, Q, 10, predicate=pred), *exp[pred])
+    hip.LanceDetachedCompact(h)  # indexes follow the compaction
+    for pred in preds:
+        assert_same(*hip.LanceDetachedSearchBatch(h, Q, 10, predicate=pred), *exp[pred])
+    hip.LanceFreeDetached(h)
+    h2 = hip.LanceOpenDetached(str(tmp_path), "filt", "l2")
+    try:
+        for pred in preds:
+            assert_same(*hip.LanceDetachedSearchBatch(h2, Q, 10, predicate=pred), *exp[pred])
+    finally:
+        hip.LanceFreeDetached(h2)

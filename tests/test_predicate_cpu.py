@@ -115,6 +115,23 @@ def test_random_predicates_match_oracle():
     assert checked == 400
 
 
+def test_scalar_index_path_matches_oracle():
+    # every column through the sorted-permutation scalar index
+    # (lance_detached_create_scalar_index): identical masks
+    rng = np.random.default_rng(9)
+    n = 700
+    cols, types = _table(rng, n)
+    X = rng.standard_normal((n, 4)).astype(np.float32)
+    batch = lance_hip.arrow_rows(X, [(k, cols[k], types[k]) for k in cols])
+    labels = np.arange(n, dtype=np.int64)
+    live = (rng.random(n) > 0.1).astype(np.uint8)
+    for _ in range(300):
+        pred = _pred(rng)
+        exp = P.mask(pred, cols, labels, live)
+        got = lance_hip.LanceHipPredicateMask(batch, labels, live, pred, indexed_columns=list(cols))
+        assert got.tolist() == exp, pred
+
+
 def test_literal_forms_and_offsets():
     # sliced struct arrays (non-zero Arrow offsets), large_string, quoted names,
     # keyword case, constant-only predicates
