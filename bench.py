@@ -41,6 +41,9 @@ MFMA_BF16_PEAK_TFS = 2500.0  # dense bf16 MFMA (no sparsity), same table
 # runs; c3 = "Flat inner-product bf16 on MFMA, 10Mx768, k=100" (bf16-stored base,
 # L2-normalized base and queries so that IP and L2 rankings coincide).
 CONFIGS = {
+    # C1: the reference's own CPU-runnable case through the reference API shape
+    # (lance_search(): one query per call, host buffers, lance_detached_search)
+    "c1": dict(n=10_000, dim=128, k=10, batch=1, metric="l2", storage="f32", normalize=False),
     "c2": dict(n=1_000_000, dim=768, k=10, batch=256, metric="l2", storage="f32", normalize=False),
     "c3": dict(n=10_000_000, dim=768, k=100, batch=256, metric="dot", storage="bf16", normalize=True),
     # IVF configs: n is ROWS PER GPU (the 8-GPU configs of BASELINE.json hold 100M rows,
@@ -339,8 +342,69 @@ def main_ivf(a):
         dist.destroy_process_group()
 
 
+def main_c1(a):
+    """C1 (BASELINE.json configs[0]): 10k x 128 f32, k = 10, one query per call
+    through lance_detached_search with host query / result buffers — the
+    lance_search() call pattern (lance_search.cpp:73-74 -> rust_ffi.cpp:130-139).
+    Latency-bound by construction (one 5 MB dense scan per call); a step = one
+    call.  Single GPU only."""
+    from oracle import c_oracle
+
+    torch.cuda.set_device(0)
+    L = lance_hip.lib()
+    N, D, K = a.n, a.dim, a.k
+    rng = np.random.default_rng(1234)
+    X = rng.standard_normal((N, D), dtype=np.float32)
+    Q = np.random.default_rng(5678).standard_normal((max(a.steps, 64), D), dtype=np.float32)
+    h = lance_hip.LanceCreateDetached("", D, a.metric, "c1")
+    lance_hip.LanceDetachedAddBatch(h, X, N, D)
+    for i in range(a.warmup):
+        lance_hip.LanceDetachedSearch(h, Q[i % len(Q)], D, K)
+    got = []
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        got.append(lance_hip.LanceDetachedSearch(h, Q[i % len(Q)], D, K)[0])
+    t = time.perf_counter() - t0
+    lance_hip.LanceHipSetOption(h, "time_kernels", "1")
+    for i in range(10):
+        lance_hip.LanceDetachedSearch(h, Q[i], D, K)
+    kt = lance_hip.LanceHipKernelTimes(h)
+    nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    nr = min(16, a.steps)
+    el, _, _ = c_oracle.flat_search_batch(X, Q[:nr], K, a.metric, acc64=True, nthreads=nthreads)
+    exact = all((got[i] == el[i]).all() for i in range(nr))
+    done, tc0 = 0, time.perf_counter()
+    while time.perf_counter() - tc0 < min(a.cpu_seconds, 5.0) or done < 2:
+        c_oracle.flat_search_batch(X, Q[done % len(Q):done % len(Q) + 1], K, a.metric, acc64=False, nthreads=nthreads)
+        done += 1
+    tcpu = time.perf_counter() - tc0
+    roof = None
+    if kt["dense_launches"]:
+        ms = kt["dense_ms_total"] / kt["dense_launches"]
+        ld = ((D + 63) // 64) * 64
+        byts = ((N + 255) // 256 * 256) * (ld * kt["scan_elem_bytes"] + 16) + 256 * ld * 2
+        roof = {"bound": "hbm", "achieved": round(byts / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "scan_kernel<L2,dense,bf16>", "avg_launch_ms": round(ms, 4), "bytes_per_launch": int(byts),
+                "note": "a 10k-row store is one short launch: latency, not bandwidth, sets the call time"}
+    line = {"metric": "lance_search() queries/sec, 10kx128 f32 flat L2 k=10, one query per call (C1)",
+            "value": round(a.steps / t, 1), "unit": "queries/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(1000.0 * t / a.steps, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic N(0,1) rows and queries (numpy default_rng)",
+            "config": {"workload": "C1 flat l2 10000x128 f32 k=10, lance_detached_search per query (host buffers)",
+                       "n": N, "dim": D, "k": K, "global_batch": 1, "parallelism": "single"},
+            "exact_ids": exact, "roofline": roof,
+            "cpu_baseline": {"value": done / tcpu, "unit": "queries/s", "cores": nthreads, "kind": "port",
+                             "sample": f"{done} queries, one per call, exact f32 l2 over {N}x{D} "
+                                       f"({tcpu:.1f} s, oracle/flat_knn.c, {nthreads} OpenMP threads)"}}
+    print(json.dumps(line), flush=True)
+    lance_hip.LanceFreeDetached(h)
+
+
 def main():
     a = parse()
+    if a.config == "c1":
+        return main_c1(a)
     if a.index_type:
         return main_ivf(a)
     rank = int(os.environ.get("RANK", "0"))
