@@ -77,6 +77,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-recall", action="store_true")
     ap.add_argument("--sample-div", type=int, default=None, help="index option sample_div (default: library's)")
+    ap.add_argument("--cand-extra", type=int, default=None, help="index option cand_extra (default: library's)")
     ap.add_argument("--nlist", type=int, default=None, help="IVF configs: num_partitions")
     ap.add_argument("--nprobe", type=int, default=None, help="IVF configs: nprobes")
     ap.add_argument("--m", type=int, default=None, help="IVF_PQ: num_sub_vectors")
@@ -433,6 +434,8 @@ def main():
     lance_hip.LanceHipSetOption(h, "reserve_rows", str(n_local))
     if a.sample_div:
         lance_hip.LanceHipSetOption(h, "sample_div", str(a.sample_div))
+    if a.cand_extra:
+        lance_hip.LanceHipSetOption(h, "cand_extra", str(a.cand_extra))
     for lo in range(s0, s1, 1 << 18):
         hi = min(s1, lo + (1 << 18))
         X = gen_rows(lo, hi, D, dev, normalize=a.normalize)

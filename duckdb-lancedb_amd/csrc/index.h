@@ -93,6 +93,7 @@ struct Workspace {
 	DevBuf<uint2> seg_pool;
 	DevBuf<int> seg_cnt;
 	DevBuf<int> status, out_c;  // status = [cert | cand_cnt | pool_cnt] x nq
+	DevBuf<int> selbig;         // per query: pool too large for the small select
 	int *h_status = nullptr;    // pinned mirror of status
 	size_t h_status_n = 0;
 	DevBuf<uint32_t> cand_slot;
@@ -184,6 +185,7 @@ struct Index {
 	// optional HIP-event timing of the scan kernels, on the stream they run on
 	bool time_kernels = false;
 	int sample_div = 32;  // sample pass covers ~1/sample_div of the tiles (>= 32 tiles)
+	int cand_extra = 32;  // refined candidates: max(k * refine_factor, k + max(cand_extra, k))
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 	double kt_append_ms = 0.0, kt_dense_ms = 0.0;
 	int64_t kt_append_n = 0, kt_dense_n = 0;

@@ -108,7 +108,7 @@ void launch_select_dense(const float *dense, int64_t ld_dense, int64_t n_entries
                          uint32_t *cand_slot, int *cand_cnt, float *cut, hipStream_t st);
 void launch_select_segments(const uint2 *seg_pool, const int *seg_cnt, int seg_cap, int n_seg, const float *tau,
                             int nq, int M, uint32_t *cand_slot, int *cand_cnt, float *cut, int *pool_total,
-                            hipStream_t st);
+                            int *big, hipStream_t st);
 
 // Exact distances (f64 accumulation, rounded to f32) of the candidates.
 void launch_refine(const StoreView &s, const QueryView &q, const uint32_t *cand_slot, const int *cand_cnt, int M,

@@ -66,7 +66,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 
 	// refined candidates: k + max(32, k) — past k the bound slack (bf16 query
 	// rounding) spans more ranks as the neighbour distances crowd (C3: k = 100)
-	const int Mfinal = std::min(MAX_CAND, std::max(k * std::max(refine, 1), k + std::max(32, k)));
+	const int Mfinal = std::min(MAX_CAND, std::max(k * std::max(refine, 1), k + std::max(cand_extra, k)));
 	const int64_t n_tiles = (n_slots + SCAN_BR - 1) / SCAN_BR;
 	const bool fast_ok = (k + 8 <= MAX_CAND) && live_rows() > 0;
 	bool all_fallback = !fast_ok;
@@ -103,8 +103,9 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		ws.seg_pool.need((size_t)n_seg_s * nq * cap_s + (size_t)n_seg_s * (nq_pad / SCAN_BQ));
 		ws.seg_cnt.need((size_t)n_seg_s * nq);
 		launch_scan_tilemin(sv, qv, n_sample, stride, ws.seg_pool.p, ws.seg_cnt.p, cap_s, stream);
+		ws.selbig.need((size_t)nq);
 		launch_select_segments(ws.seg_pool.p, ws.seg_cnt.p, cap_s, n_seg_s, nullptr, nq, Ms, ws.cand_slot.p,
-		                       d_cand_cnt, ws.cut.p, nullptr, stream);
+		                       d_cand_cnt, ws.cut.p, nullptr, ws.selbig.p, stream);
 		launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Ms, ws.cand_dist.p, stream);
 		launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Ms, k, 0, k, ws.tau.p,
 		                nullptr, nullptr, nullptr, nullptr, stream);
@@ -120,7 +121,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		tic(3);
 		// 3) top-M by LB, exact refine, certificate
 		launch_select_segments(ws.seg_pool.p, ws.seg_cnt.p, seg_cap, n_seg, ws.tau.p, nq, Mfinal, ws.cand_slot.p,
-		                       d_cand_cnt, ws.cut.p, d_pool_cnt, stream);
+		                       d_cand_cnt, ws.cut.p, d_pool_cnt, ws.selbig.p, stream);
 		launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Mfinal, ws.cand_dist.p, stream);
 		launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Mfinal, k, 1, 0, nullptr, dL,
 		                dD, dC, d_cert, stream);
@@ -874,6 +875,12 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			if (v != "on" && v != "off") throw Error("scan_copy must be 'on' or 'off'");
 			ix->bind();
 			ix->set_scan_copy(v == "on");
+			return 0;
+		}
+		if (k == "cand_extra") {
+			const int d = std::stoi(v);
+			if (d < 8 || d > 256) throw Error("cand_extra must be in [8, 256]");
+			ix->cand_extra = d;
 			return 0;
 		}
 		if (k == "sample_div") {

@@ -185,6 +185,8 @@ int32_t lance_hip_device_count(void);
  *                  f32 rows, results are unchanged
  *   "sample_div"   the threshold sample pass covers ~1/sample_div of the row
  *                  tiles (at least 32 tiles); default "32"
+ *   "cand_extra"   exact candidates re-ranked per query beyond k: max(k *
+ *                  refine_factor, k + max(cand_extra, k)), default "32"
  *   "index_type"   "ivf_pq" (default) | "ivf_flat": what create_index builds
  *   "kmeans_iters" k-means iterations (coarse and PQ), default "50"
  *   "ivf_seed"     seed of the k-means training sample, default 24301
