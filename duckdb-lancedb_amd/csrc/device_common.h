@@ -63,23 +63,47 @@ __device__ __forceinline__ float xval(const uint16_t *p, int64_t i) { return __u
 // into LDS, and four consecutive rows' terms are one 16 B read.
 __host__ __device__ __forceinline__ int64_t raix(int64_t r, int c) { return ((r >> 8) << 10) | ((int64_t)c << 8) | (r & 255); }
 
+// four consecutive base elements as f32 (16-B / 8-B aligned: rows are ld-padded)
+__device__ __forceinline__ float4 xval4(const float *p, int64_t i) { return *reinterpret_cast<const float4 *>(p + i); }
+__device__ __forceinline__ float4 xval4(const uint16_t *p, int64_t i) {
+	const uint2 u = *reinterpret_cast<const uint2 *>(p + i);
+	return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xFFFF0000u), __uint_as_float(u.y << 16),
+	                   __uint_as_float(u.y & 0xFFFF0000u));
+}
+
+template <int METRIC>
+__device__ __forceinline__ void exact_acc(double xv, double qv, double &a, double &b, double &c) {
+	if (METRIC == METRIC_L2) {
+		const double d = xv - qv;
+		a += d * d;
+	} else {
+		a += xv * qv;
+		if (METRIC == METRIC_COSINE) {
+			b += xv * xv;
+			c += qv * qv;
+		}
+	}
+}
+
+// Exact distance of one row to one query by one wave: f64 accumulation, f32
+// result.  Each lane takes 4 consecutive elements per step (one 16-B load of
+// the row, one of the query; the steps of a lane are independent loads, so a
+// row costs one memory latency, not dim/64 of them).
 template <int METRIC, typename T>
 __device__ __forceinline__ float exact_distance(const T *__restrict__ x, const float *__restrict__ q, int dim,
                                                 int lane) {
 	double a = 0.0, b = 0.0, c = 0.0;
-	for (int i = lane; i < dim; i += 64) {
-		double xv = xval(x, i), qv = q[i];
-		if (METRIC == METRIC_L2) {
-			double d = xv - qv;
-			a += d * d;
-		} else {
-			a += xv * qv;
-			if (METRIC == METRIC_COSINE) {
-				b += xv * xv;
-				c += qv * qv;
-			}
-		}
+	const int d4 = dim >> 2;
+#pragma unroll 4
+	for (int i4 = lane; i4 < d4; i4 += 64) {
+		const float4 xv = xval4(x, 4 * i4);
+		const float4 qv = *reinterpret_cast<const float4 *>(q + 4 * i4);
+		exact_acc<METRIC>(xv.x, qv.x, a, b, c);
+		exact_acc<METRIC>(xv.y, qv.y, a, b, c);
+		exact_acc<METRIC>(xv.z, qv.z, a, b, c);
+		exact_acc<METRIC>(xv.w, qv.w, a, b, c);
 	}
+	for (int i = 4 * d4 + lane; i < dim; i += 64) exact_acc<METRIC>(xval(x, i), q[i], a, b, c);
 	a = wave_sum_f64(a);
 	if (METRIC == METRIC_COSINE) {
 		b = wave_sum_f64(b);
