@@ -6,7 +6,8 @@ integers (``rust_lib/src/lance_manager.rs:232-233``), shard ``r`` holding
 global rows ``[s0, s1)`` stores them under local labels ``[0, s1-s0)`` and the
 global label is ``s0 + local`` — no id translation table.  Every rank searches
 its shard for the same query batch; the per-shard top-k lists are exchanged by
-ONE all-gather (RCCL over xGMI on GPUs, gloo in CPU tests) and merged on the
+ONE all-gather (RCCL over xGMI on GPUs, gloo in CPU tests; labels, distances
+and counts packed into one int32 buffer) and merged on the
 device by ``lance_hip_merge_topk_device`` under the (distance, label) order.
 """
 from __future__ import annotations
@@ -37,20 +38,6 @@ class ShardedSearch:
         self.world = int(world)
         self._bufs = None
 
-    def _gather_bufs(self, like_l, like_d, like_c):
-        import torch
-
-        # flat [world * n, ...] outputs: the layout both RCCL and gloo accept
-        key = (tuple(like_l.shape), like_l.device)
-        if self._bufs is None or self._bufs[0] != key:
-            gl = torch.empty((self.world * like_l.shape[0],) + tuple(like_l.shape[1:]), dtype=like_l.dtype,
-                             device=like_l.device)
-            gd = torch.empty((self.world * like_d.shape[0],) + tuple(like_d.shape[1:]), dtype=like_d.dtype,
-                             device=like_d.device)
-            gc = torch.empty((self.world * like_c.shape[0],), dtype=like_c.dtype, device=like_c.device)
-            self._bufs = (key, gl, gd, gc)
-        return self._bufs[1:]
-
     def search(self, Q, k: int, **kw):
         lab, dis, cnt = self.local_search(Q, k, **kw)
         if self.world == 1:
@@ -59,12 +46,23 @@ class ShardedSearch:
         import torch
 
         lab = torch.where(lab >= 0, lab + self.label_offset, lab)  # no host sync
-        gl, gd, gc = self._gather_bufs(lab, dis, cnt)
-        self.dist.all_gather_into_tensor(gl, lab.contiguous())
-        self.dist.all_gather_into_tensor(gd, dis.contiguous())
-        self.dist.all_gather_into_tensor(gc, cnt.contiguous())
-        nq = lab.shape[0]
-        return self.merge(gl.view(self.world, nq, -1), gd.view(self.world, nq, -1), gc.view(self.world, nq))
+        nq, kk = lab.shape
+        # ONE collective per batch: labels (int64 as 2 x int32), distances (f32
+        # bits) and counts packed into an int32 row per rank (collective latency,
+        # not bytes, is the cost at these sizes: 3 all-gathers would pay it 3x)
+        pack = torch.cat([lab.contiguous().view(torch.int32).reshape(-1),
+                          dis.contiguous().view(torch.int32).reshape(-1), cnt.to(torch.int32).reshape(-1)])
+        key = (pack.numel(), pack.device)
+        if self._bufs is None or self._bufs[0] != key:
+            self._bufs = (key, torch.empty((self.world * pack.numel(),), dtype=torch.int32, device=pack.device))
+        g = self._bufs[1]
+        self.dist.all_gather_into_tensor(g, pack)
+        g = g.view(self.world, -1)
+        nl, nd = 2 * nq * kk, nq * kk
+        gl = g[:, :nl].contiguous().view(torch.int64).view(self.world, nq, kk)
+        gd = g[:, nl:nl + nd].contiguous().view(torch.float32).view(self.world, nq, kk)
+        gc = g[:, nl + nd:].contiguous().view(self.world, nq).to(cnt.dtype)
+        return self.merge(gl, gd, gc)
 
 
 def hip_device_merge(lib, err_len: int = 2048):
