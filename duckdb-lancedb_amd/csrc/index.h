@@ -99,8 +99,20 @@ struct Workspace {
 	DevBuf<uint32_t> cand_slot;
 	DevBuf<int64_t> out_l, fb_vals, fb_vals2, idx;
 	DevBuf<uint8_t> sort_tmp;
+	uint8_t *h_io = nullptr;    // pinned staging of the host-buffer API (queries in, results out)
+	size_t h_io_n = 0;
 	~Workspace() {
 		if (h_status) (void)hipHostFree(h_status);
+		if (h_io) (void)hipHostFree(h_io);
+	}
+	uint8_t *need_host_io(size_t bytes) {
+		if (bytes > h_io_n) {
+			if (h_io) HIPCHK(hipHostFree(h_io));
+			h_io = nullptr;
+			HIPCHK(hipHostMalloc(&h_io, bytes));
+			h_io_n = bytes;
+		}
+		return h_io;
 	}
 	void need_host_status(size_t n) {
 		if (n <= h_status_n) return;

@@ -636,16 +636,20 @@ int32_t lance_detached_search_batch(void *handle, const float *queries, int32_t 
 		ws.out_l.need((size_t)nq * k);
 		ws.out_d.need((size_t)nq * k);
 		ws.out_c.need((size_t)nq);
-		HIPCHK(hipMemcpyAsync(ws.Qin.p, queries, (size_t)nq * dim * sizeof(float), hipMemcpyHostToDevice, ix->stream));
-		HIPCHK(hipStreamSynchronize(ix->stream));
+		// pinned staging: true async copies on the handle's stream, one wait at the end
+		const size_t qb = (size_t)nq * dim * sizeof(float), lb = (size_t)nq * k * sizeof(int64_t);
+		const size_t db = (size_t)nq * k * sizeof(float), cb = (size_t)nq * sizeof(int32_t);
+		uint8_t *io = ws.need_host_io(std::max(qb, lb + db + cb));
+		memcpy(io, queries, qb);
+		HIPCHK(hipMemcpyAsync(ws.Qin.p, io, qb, hipMemcpyHostToDevice, ix->stream));
 		ix->search_any(ws.Qin.p, nq, k, nprobes, refine_factor, ws.out_l.p, ws.out_d.p, ws.out_c.p);
-		HIPCHK(hipMemcpyAsync(out_labels, ws.out_l.p, (size_t)nq * k * sizeof(int64_t), hipMemcpyDeviceToHost,
-		                      ix->stream));
-		HIPCHK(hipMemcpyAsync(out_distances, ws.out_d.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost,
-		                      ix->stream));
-		HIPCHK(hipMemcpyAsync(out_counts, ws.out_c.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost,
-		                      ix->stream));
-		HIPCHK(hipStreamSynchronize(ix->stream));
+		HIPCHK(hipMemcpyAsync(io, ws.out_l.p, lb, hipMemcpyDeviceToHost, ix->stream));
+		HIPCHK(hipMemcpyAsync(io + lb, ws.out_d.p, db, hipMemcpyDeviceToHost, ix->stream));
+		HIPCHK(hipMemcpyAsync(io + lb + db, ws.out_c.p, cb, hipMemcpyDeviceToHost, ix->stream));
+		lhip::spin_sync(ix->stream);
+		memcpy(out_labels, io, lb);
+		memcpy(out_distances, io + lb, db);
+		memcpy(out_counts, io + lb + db, cb);
 		return nq;
 	}
 	API_GUARD("search failed: ", -1)
