@@ -94,6 +94,12 @@ struct Workspace {
 	DevBuf<int> seg_cnt;
 	DevBuf<int> status, out_c;  // status = [cert | cand_cnt | pool_cnt] x nq
 	DevBuf<int> selbig;         // per query: pool too large for the small select
+	// second threshold pass of uncertified queries (search_chunk)
+	DevBuf<float> rQf, rtau, rD;
+	DevBuf<uint16_t> rQb;
+	DevBuf<float4> rqaux;
+	DevBuf<int> rfq, rstat, rC;
+	DevBuf<int64_t> rL;
 	int *h_status = nullptr;    // pinned mirror of status
 	size_t h_status_n = 0;
 	DevBuf<uint32_t> cand_slot;
@@ -192,11 +198,12 @@ struct Index {
 	int kmeans_iters = 50;  // lance k-means max_iters default
 	uint64_t ivf_seed = 0x5eedULL;
 
-	int64_t last_stats[4] = {0, 0, 0, 0};
+	int64_t last_stats[5] = {0, 0, 0, 0, 0};
 
 	// optional HIP-event timing of the scan kernels, on the stream they run on
 	bool time_kernels = false;
 	int sample_div = 32;  // sample pass covers ~1/sample_div of the tiles (>= 32 tiles)
+	bool retry_pass = true;  // rerun uncertified queries with a tighter tau before the exact fallback
 	int cand_extra = 32;  // refined candidates: max(k * refine_factor, k + max(cand_extra, k))
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 	double kt_append_ms = 0.0, kt_dense_ms = 0.0;

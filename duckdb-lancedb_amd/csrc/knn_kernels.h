@@ -130,6 +130,18 @@ void launch_exact_all(const StoreView &s, const QueryView &q, int qi, float *key
 int sort_pairs(void *temp, size_t &temp_bytes, const float *keys_in, float *keys_out, const int64_t *vals_in,
                int64_t *vals_out, int64_t n, hipStream_t st);
 
+// Second threshold pass of failed queries fq[0..nf): packs their prepared
+// query rows into Qf2/Qb2/qaux2 (nf_pad rows, pads zero), tau2[i] = min(tau,
+// first-pass k-th exact distance), zeroes status2 = [cert | cnt | pool] x nf.
+void launch_retry_gather(const int *fq, int nf, int nf_pad, int ld, int k, const QueryView &q, const float *tau,
+                         const float *dists, float *Qf2, uint16_t *Qb2, float4 *qaux2, float *tau2, int *status2,
+                         hipStream_t st);
+// Writes back the rerun results of the queries the rerun certified; for the
+// others tau[q] = min(tau2, rerun k-th exact distance) for a further rerun.
+void launch_retry_scatter(const int *fq, int nf, int k, const int64_t *L2, const float *D2, const int *C2,
+                          const int *cert2, const float *tau2, int64_t *L, float *D, int *C, int *cert, float *tau,
+                          hipStream_t st);
+
 // Merge nshard partial top-k lists (device pointers) into the global top-k.
 void launch_merge_topk(int nshard, int nq, int k, const int64_t *part_labels, const float *part_dists,
                        const int *part_counts, int64_t *out_labels, float *out_dists, int *out_counts,

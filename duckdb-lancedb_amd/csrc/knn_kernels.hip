@@ -1391,12 +1391,15 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const f
 		}
 		unsigned total;
 		const unsigned off = block_excl_scan(c, sh, total);
-		n = total;
+		// a pool over the LDS capacity keeps its first SEL_LDS_PAIRS entries:
+		// the certificate fails (cut = -inf), but the candidates are still
+		// real rows, so their k-th exact distance bounds the second pass's tau
 		in_lds = true;
-		if (total > (unsigned)SEL_LDS_PAIRS) {
-			s_over = 1u;
-			n = 0;
-		} else if (c) {
+		if (total > (unsigned)SEL_LDS_PAIRS) s_over = 1u;
+		n = total < (unsigned)SEL_LDS_PAIRS ? total : (unsigned)SEL_LDS_PAIRS;
+		unsigned room = off < (unsigned)SEL_LDS_PAIRS ? (unsigned)SEL_LDS_PAIRS - off : 0u;
+		c = c < room ? c : room;
+		if (c) {
 			const uint2 *seg = src.seg_pool + ((int64_t)t * nq + q) * src.seg_cap;
 			unsigned i = 0;
 			for (; i + 4 <= c; i += 4) {
@@ -1826,6 +1829,78 @@ void launch_copy_fallback(const float *keys, const int64_t *vals, int64_t n_live
                           float *out_dists, int *out_counts, hipStream_t st) {
 	copy_fallback_kernel<<<dim3((k + 255) / 256), dim3(256), 0, st>>>(keys, vals, n_live, k, qi, out_labels,
 	                                                                   out_dists, out_counts);
+}
+
+// ---------------------------------------------------------------------------
+// second threshold pass for queries whose certificate failed (a segment
+// overflowed, or the sampled tau was loose): the failed queries are packed
+// into a batch of their own with tau = the k-th exact distance the first pass
+// found (k real live rows lie within it) and rerun with full segments
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void retry_gather_kernel(const int *__restrict__ fq, int nf, int ld, int k,
+                                                           const float *__restrict__ Qf,
+                                                           const uint16_t *__restrict__ Qb,
+                                                           const float4 *__restrict__ qaux,
+                                                           const float *__restrict__ tau,
+                                                           const float *__restrict__ dists, float *__restrict__ Qf2,
+                                                           uint16_t *__restrict__ Qb2, float4 *__restrict__ qaux2,
+                                                           float *__restrict__ tau2, int *__restrict__ status2) {
+	const int i = blockIdx.x;
+	const int t = threadIdx.x;
+	const int src = i < nf ? fq[i] : -1;
+	for (int j = t; j < ld; j += 256) {
+		Qf2[(int64_t)i * ld + j] = src >= 0 ? Qf[(int64_t)src * ld + j] : 0.0f;
+		Qb2[(int64_t)i * ld + j] = src >= 0 ? Qb[(int64_t)src * ld + j] : (uint16_t)0;
+	}
+	if (t != 0) return;
+	qaux2[i] = src >= 0 ? qaux[src] : make_float4(0.f, 0.f, 0.f, 0.f);
+	if (src < 0) return;
+	const float t0 = tau[src];
+	const float dk = dists[(int64_t)src * k + k - 1];  // NaN when fewer than k were found
+	tau2[i] = (dk < t0) ? dk : t0;
+	status2[i] = status2[nf + i] = status2[2 * nf + i] = 0;
+}
+
+void launch_retry_gather(const int *fq, int nf, int nf_pad, int ld, int k, const QueryView &q, const float *tau,
+                         const float *dists, float *Qf2, uint16_t *Qb2, float4 *qaux2, float *tau2, int *status2,
+                         hipStream_t st) {
+	retry_gather_kernel<<<dim3(nf_pad), dim3(256), 0, st>>>(fq, nf, ld, k, q.Qf, q.Qb, q.qaux, tau, dists, Qf2, Qb2,
+	                                                         qaux2, tau2, status2);
+}
+
+__global__ __launch_bounds__(64) void retry_scatter_kernel(const int *__restrict__ fq, int k,
+                                                           const int64_t *__restrict__ L2,
+                                                           const float *__restrict__ D2, const int *__restrict__ C2,
+                                                           const int *__restrict__ cert2,
+                                                           const float *__restrict__ tau2, int64_t *__restrict__ L,
+                                                           float *__restrict__ D, int *__restrict__ C,
+                                                           int *__restrict__ cert, float *__restrict__ tau) {
+	const int i = blockIdx.x;
+	const int dst = fq[i];
+	if (!cert2[i]) {
+		// still uncertified: keep the tighter bound for a further rerun (the
+		// exact fallback writes the results)
+		if (threadIdx.x == 0) {
+			const float dk = D2[(int64_t)i * k + k - 1];
+			const float t1 = tau2[i];
+			tau[dst] = (dk < t1) ? dk : t1;
+		}
+		return;
+	}
+	for (int j = threadIdx.x; j < k; j += 64) {
+		L[(int64_t)dst * k + j] = L2[(int64_t)i * k + j];
+		D[(int64_t)dst * k + j] = D2[(int64_t)i * k + j];
+	}
+	if (threadIdx.x == 0) {
+		C[dst] = C2[i];
+		cert[dst] = 1;
+	}
+}
+
+void launch_retry_scatter(const int *fq, int nf, int k, const int64_t *L2, const float *D2, const int *C2,
+                          const int *cert2, const float *tau2, int64_t *L, float *D, int *C, int *cert, float *tau,
+                          hipStream_t st) {
+	retry_scatter_kernel<<<dim3(nf), dim3(64), 0, st>>>(fq, k, L2, D2, C2, cert2, tau2, L, D, C, cert, tau);
 }
 
 // ---------------------------------------------------------------------------

@@ -34,7 +34,7 @@
 namespace lhip {
 
 void Index::search_device(const float *dQ, int nq, int k, int refine, int64_t *dL, float *dD, int *dC) {
-	last_stats[0] = last_stats[1] = last_stats[2] = last_stats[3] = 0;
+	last_stats[0] = last_stats[1] = last_stats[2] = last_stats[3] = last_stats[4] = 0;
 	// one pipeline pass covers up to MAX_PASS_Q queries (several query tiles
 	// per scan launch): the per-pass fixed cost is paid once per pass
 	for (int s = 0; s < nq; s += MAX_PASS_Q) {
@@ -141,6 +141,55 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	for (int q = 0; q < nq; ++q) {
 		last_stats[1] += ws.h_status[nq + q];
 		last_stats[2] = std::max<int64_t>(last_stats[2], ws.h_status[2 * nq + q]);
+	}
+	// threshold path: rerun the uncertified queries as a batch of their own,
+	// tau = their previous pass's k-th exact distance, full-size segments (up
+	// to two reruns: a pool over the selection's capacity still yields real
+	// candidates, so each rerun's tau tightens)
+	// A query that found no candidate at all (NaN bound: a zero cosine query)
+	// goes straight to the exact fallback.
+	std::vector<char> rerun(nq, 0);
+	for (int q = 0; q < nq; ++q) rerun[q] = !h_cert[q] && ws.h_status[nq + q] > 0;
+	for (int attempt = 0; attempt < 2 && fast_ok && n_slots > DENSE_MAX_ROWS && retry_pass; ++attempt) {
+		std::vector<int> fq;
+		for (int q = 0; q < nq; ++q)
+			if (rerun[q] && !h_cert[q]) fq.push_back(q);
+		const int nf = (int)fq.size();
+		if (nf == 0) break;
+		{
+			if (attempt == 0) last_stats[4] += nf;
+			const int nf_pad = (int)round_up(nf, SCAN_BQ);
+			ws.rfq.need(nf);
+			ws.rQf.need((size_t)nf_pad * ld);
+			ws.rQb.need((size_t)nf_pad * ld);
+			ws.rqaux.need(nf_pad);
+			ws.rtau.need(nf);
+			ws.rstat.need((size_t)3 * nf);
+			ws.rL.need((size_t)nf * k);
+			ws.rD.need((size_t)nf * k);
+			ws.rC.need(nf);
+			HIPCHK(hipMemcpyAsync(ws.rfq.p, fq.data(), (size_t)nf * sizeof(int), hipMemcpyHostToDevice, stream));
+			launch_retry_gather(ws.rfq.p, nf, nf_pad, ld, k, qv, ws.tau.p, dD, ws.rQf.p, ws.rQb.p, ws.rqaux.p,
+			                    ws.rtau.p, ws.rstat.p, stream);
+			const QueryView qv2{ws.rQf.p, ws.rQb.p, ws.rqaux.p, nf, nf_pad};
+			const int n_seg = scan_grid(n_tiles);
+			int cap2 = 1024;  // the scan's maximum, bounded to a 1 GiB pool
+			while (cap2 > 64 && (size_t)n_seg * nf * cap2 * sizeof(uint2) > ((size_t)1 << 30)) cap2 /= 2;
+			ws.seg_pool.need((size_t)n_seg * nf * cap2 + (size_t)n_seg * (nf_pad / SCAN_BQ));
+			ws.seg_cnt.need((size_t)n_seg * nf);
+			int *cert2 = ws.rstat.p, *cnt2 = ws.rstat.p + nf, *pool2 = ws.rstat.p + 2 * nf;
+			launch_scan_append(sv, qv2, ws.rtau.p, ws.seg_pool.p, ws.seg_cnt.p, cap2, stream);
+			launch_select_segments(ws.seg_pool.p, ws.seg_cnt.p, cap2, n_seg, ws.rtau.p, nf, Mfinal, ws.cand_slot.p,
+			                       cnt2, ws.cut.p, pool2, ws.selbig.p, stream);
+			launch_refine(sv, qv2, ws.cand_slot.p, cnt2, Mfinal, ws.cand_dist.p, stream);
+			launch_finalize(sv, ws.cand_slot.p, cnt2, ws.cand_dist.p, ws.cut.p, nf, Mfinal, k, 1, 0, nullptr, ws.rL.p,
+			                ws.rD.p, ws.rC.p, cert2, stream);
+			launch_retry_scatter(ws.rfq.p, nf, k, ws.rL.p, ws.rD.p, ws.rC.p, cert2, ws.rtau.p, dL, dD, dC, d_cert, ws.tau.p,
+			                     stream);
+			HIPCHK(hipGetLastError());
+			HIPCHK(hipMemcpyAsync(ws.h_status, d_cert, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, stream));
+			spin_sync(stream);
+		}
 	}
 	// exact fallback for every query whose certificate failed
 	for (int q = 0; q < nq; ++q) {
@@ -887,6 +936,10 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			ix->cand_extra = d;
 			return 0;
 		}
+		if (k == "retry_pass") {
+			ix->retry_pass = (v == "1" || v == "on" || v == "true");
+			return 0;
+		}
 		if (k == "sample_div") {
 			const int d = std::stoi(v);
 			if (d < 1) throw Error("sample_div must be >= 1");
@@ -926,7 +979,7 @@ int32_t lance_hip_last_search_stats(void *handle, int64_t *out, int32_t n) {
 	if (!handle || !out) return -1;
 	Index *ix = as_index(handle);
 	std::lock_guard<std::mutex> g(ix->mu);
-	for (int32_t i = 0; i < n && i < 4; ++i) out[i] = ix->last_stats[i];
+	for (int32_t i = 0; i < n && i < 5; ++i) out[i] = ix->last_stats[i];
 	return 0;
 }
 

@@ -187,6 +187,8 @@ int32_t lance_hip_device_count(void);
  *                  tiles (at least 32 tiles); default "32"
  *   "cand_extra"   exact candidates re-ranked per query beyond k: max(k *
  *                  refine_factor, k + max(cand_extra, k)), default "32"
+ *   "retry_pass"   "1" (default) | "0": rerun uncertified threshold-path
+ *                  queries with a tightened tau before the exact fallback
  *   "index_type"   "ivf_pq" (default) | "ivf_flat": what create_index builds
  *   "kmeans_iters" k-means iterations (coarse and PQ), default "50"
  *   "ivf_seed"     seed of the k-means training sample, default 24301
@@ -199,7 +201,10 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 /* Statistics of the last search on this handle (for benches/tests):
  * out[0] = queries whose exactness certificate failed and took the exact
  * fallback, out[1] = total candidates refined, out[2] = max pool size,
- * out[3] = 1 if the dense (small-N) path ran.  Returns 0 or -1. */
+ * out[3] = 1 if the dense (small-N) path ran, out[4] = queries rerun by the
+ * second threshold pass (option "retry_pass", default on: an uncertified
+ * query is rescanned with tau = its first-pass k-th exact distance and
+ * full-size segments before it may take the exact fallback).  Returns 0 or -1. */
 int32_t lance_hip_last_search_stats(void *handle, int64_t *out, int32_t n);
 
 /* Per-handle HIP-event timings of the scan kernels (enable with option

@@ -275,7 +275,38 @@ def test_duplicates_force_exact_fallback(hip, mk):
     gl, gd, gc = hip.LanceDetachedSearchBatch(h, np.ones((2, d), np.float32), 10)
     assert list(gl[0]) == [1, 2, 3, 4, 6, 7, 8, 9, 10, 11]
     assert np.all(gd == 0)
-    assert hip.LanceHipLastSearchStats(h)["fallback_queries"] == 2
+    st = hip.LanceHipLastSearchStats(h)
+    assert st["fallback_queries"] == 2 and st["retried_queries"] == 2
+
+
+@pytest.mark.parametrize("retry", ["1", "0"])
+def test_overflowed_segment_takes_second_pass(hip, mk, retry):
+    # the neighbours of three queries sit packed in tile 1 (rows 256..511),
+    # which the sample pass skips: the loose sampled tau overflows that tile's
+    # segment, the certificate fails, and the second threshold pass (tau = the
+    # first pass's k-th exact distance, full-size segments) recovers them
+    # without the exact fallback
+    rng = np.random.default_rng(5)
+    n, d, k = 120_000, 32, 10
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    q0 = rng.standard_normal(d).astype(np.float32)
+    dirs = rng.standard_normal((256, d))
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    X[256:512] = q0 + np.sqrt(rng.uniform(0, 40, 256))[:, None] * dirs
+    Q = np.concatenate([q0 + 0.01 * rng.standard_normal((3, d)), rng.standard_normal((5, d))]).astype(np.float32)
+    h = mk(d)
+    hip.LanceDetachedAddBatch(h, X, n, d)
+    hip.LanceHipSetOption(h, "sample_div", "100000")
+    hip.LanceHipSetOption(h, "retry_pass", retry)
+    gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, k)
+    st = hip.LanceHipLastSearchStats(h)
+    el, ed, ec = c_oracle.flat_search_batch(X, Q, k, "l2", acc64=True, nthreads=16)
+    assert_same(gl, gd, gc, el, ed, ec)
+    assert not st["dense_path"]
+    if retry == "1":
+        assert st["retried_queries"] >= 3 and st["fallback_queries"] == 0, st
+    else:
+        assert st["retried_queries"] == 0 and st["fallback_queries"] >= 3, st
 
 
 def test_metric_quirk_ranks_by_l2(hip, mk):
