@@ -370,6 +370,7 @@ def main_c1(a):
     for i in range(10):
         lance_hip.LanceDetachedSearch(h, Q[i], D, K)
     kt = lance_hip.LanceHipKernelTimes(h)
+    small = lance_hip.LanceHipLastSearchStats(h)["small_exact"]
     nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     nr = min(16, a.steps)
     el, _, _ = c_oracle.flat_search_batch(X, Q[:nr], K, a.metric, acc64=True, nthreads=nthreads)
@@ -383,10 +384,17 @@ def main_c1(a):
     if kt["dense_launches"]:
         ms = kt["dense_ms_total"] / kt["dense_launches"]
         ld = ((D + 63) // 64) * 64
-        byts = ((N + 255) // 256 * 256) * (ld * kt["scan_elem_bytes"] + 16) + 256 * ld * 2
+        if small:
+            # one-launch exact search: every row's dim f32 elements, its row-aux
+            # word and label (f32 store, the small path reads the rows themselves)
+            byts = N * (D * 4 + 4 + 8)
+            kern = f"small_exact_kernel<{a.metric.upper()},f32>"
+        else:
+            byts = ((N + 255) // 256 * 256) * (ld * kt["scan_elem_bytes"] + 16) + 256 * ld * 2
+            kern = "scan_kernel<L2,dense,bf16>"
         roof = {"bound": "hbm", "achieved": round(byts / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "scan_kernel<L2,dense,bf16>", "avg_launch_ms": round(ms, 4), "bytes_per_launch": int(byts),
+                "kernel": kern, "avg_launch_ms": round(ms, 4), "bytes_per_launch": int(byts),
                 "note": "a 10k-row store is one short launch: latency, not bandwidth, sets the call time"}
     line = {"metric": "lance_search() queries/sec, 10kx128 f32 flat L2 k=10, one query per call (C1)",
             "value": round(a.steps / t, 1), "unit": "queries/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,

@@ -94,6 +94,10 @@ struct Workspace {
 	DevBuf<int> seg_cnt;
 	DevBuf<int> status, out_c;  // status = [cert | cand_cnt | pool_cnt] x nq
 	DevBuf<int> selbig;         // per query: pool too large for the small select
+	// small exact search (search_chunk): per-workgroup partial top-k lists and
+	// the per-query completion counters (zeroed at allocation, left zeroed)
+	DevBuf<uint4> spart;
+	DevBuf<unsigned> scnt;
 	// second threshold pass of uncertified queries (search_chunk)
 	DevBuf<float> rQf, rtau, rD;
 	DevBuf<uint16_t> rQb;
@@ -104,7 +108,7 @@ struct Workspace {
 	size_t h_status_n = 0;
 	DevBuf<uint32_t> cand_slot;
 	DevBuf<int64_t> out_l, fb_vals, fb_vals2, idx;
-	DevBuf<uint8_t> sort_tmp;
+	DevBuf<uint8_t> sort_tmp, out_blk;
 	uint8_t *h_io = nullptr;    // pinned staging of the host-buffer API (queries in, results out)
 	size_t h_io_n = 0;
 	~Workspace() {
@@ -203,6 +207,8 @@ struct Index {
 	// optional HIP-event timing of the scan kernels, on the stream they run on
 	bool time_kernels = false;
 	int sample_div = 32;  // sample pass covers ~1/sample_div of the tiles (>= 32 tiles)
+	bool small_exact = true;  // one-launch exact search for <= 8 queries over <= 32768 slots
+	bool defer_sync = false;  // caller synchronizes the stream itself (host-buffer search)
 	bool retry_pass = true;  // rerun uncertified queries with a tighter tau before the exact fallback
 	int cand_extra = 32;  // refined candidates: max(k * refine_factor, k + max(cand_extra, k))
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};

@@ -130,6 +130,22 @@ void launch_exact_all(const StoreView &s, const QueryView &q, int qi, float *key
 int sort_pairs(void *temp, size_t &temp_bytes, const float *keys_in, float *keys_out, const int64_t *vals_in,
                int64_t *vals_out, int64_t n, hipStream_t st);
 
+// Small exact search (one launch): nq <= SMALL_MAX_Q queries (Q = [nq][dim]
+// f32, unpadded, device) over a store of <= SMALL_MAX_ROWS slots; exact f64
+// distances, per-workgroup top-k, last-workgroup merge.  part = 16 B x nq x
+// small_exact_grid(n_slots) x k scratch; counter = nq zeroed words (left
+// zeroed).  Writes labels/distances/counts like finalize.
+constexpr int SMALL_THREADS = 256;
+constexpr int SMALL_MAX_ROWS = 32768;
+constexpr int SMALL_MAX_DIM = 4096;
+constexpr int SMALL_MAX_Q = 8;
+constexpr int SMALL_MAX_K = 64;
+constexpr int SMALL_MAX_PART = 4096;
+bool small_exact_fits(int64_t n_slots, int dim, int nq, int k);
+int small_exact_grid(int64_t n_slots);
+void launch_small_exact(const StoreView &s, const float *Q, int nq, int k, void *part, unsigned *counter, int64_t *L,
+                        float *D, int *C, hipStream_t st);
+
 // Second threshold pass of failed queries fq[0..nf): packs their prepared
 // query rows into Qf2/Qb2/qaux2 (nf_pad rows, pads zero), tau2[i] = min(tau,
 // first-pass k-th exact distance), zeroes status2 = [cert | cnt | pool] x nf.

@@ -1832,6 +1832,161 @@ void launch_copy_fallback(const float *keys, const int64_t *vals, int64_t n_live
 }
 
 // ---------------------------------------------------------------------------
+// small exact search: one launch for a few queries over a small store
+// (the per-query lance_search call pattern, C1).  Thread = row: exact distance
+// in f64 (sequential over the dimension, rounded once to f32: the oracle's
+// definition); a bitonic sort of the workgroup's 256 rows by (distance,
+// label) puts its top-k in a partial list; the last workgroup of the query to
+// finish (device-scope counter) sorts the partial lists together and writes
+// the result.  No bounds, no certificate, no host round trip in between.
+// ---------------------------------------------------------------------------
+#ifndef LHIP_ABL_SMALL_NOFENCE
+#define LHIP_ABL_SMALL_NOFENCE 0  // timing ablation (tools/ablate.sh): results wrong by design
+#endif
+struct SHit {
+	float d;
+	int v;  // 1 = live row
+	int64_t l;
+};
+
+__device__ __forceinline__ bool shit_less(const SHit &a, const SHit &b) {
+	if (a.v != b.v) return a.v > b.v;
+	return hit_less(a.d, a.l, b.d, b.l);
+}
+
+// ascending bitonic sort of s[0..n) (n a power of two) by the whole block
+__device__ __forceinline__ void shit_sort(SHit *s, int n) {
+	const int t = threadIdx.x;
+	for (int size = 2; size <= n; size <<= 1) {
+		for (int j = size >> 1, lj = __builtin_ctz(size >> 1); j > 0; j >>= 1, --lj) {
+			for (int i = t; i < (n >> 1); i += SMALL_THREADS) {
+				const int lo = ((i >> lj) << (lj + 1)) | (i & (j - 1)), hi = lo + j;
+				const bool up = (lo & size) == 0;
+				const SHit a = s[lo], b = s[hi];
+				if (up ? shit_less(b, a) : shit_less(a, b)) {
+					s[lo] = b;
+					s[hi] = a;
+				}
+			}
+			__syncthreads();
+		}
+	}
+}
+
+template <int METRIC, typename T>
+__global__ __launch_bounds__(SMALL_THREADS) void small_exact_kernel(const T *__restrict__ X,
+                                                                    const float4 *__restrict__ rowaux,
+                                                                    const int64_t *__restrict__ labels, int64_t n,
+                                                                    int ld, int dim, const float *__restrict__ Q, int k,
+                                                                    SHit *__restrict__ part,
+                                                                    unsigned *__restrict__ counter,
+                                                                    int64_t *__restrict__ out_l,
+                                                                    float *__restrict__ out_d, int *__restrict__ out_c) {
+	__shared__ __attribute__((aligned(16))) float sq[SMALL_MAX_DIM];
+	__shared__ SHit s[SMALL_MAX_PART];
+	__shared__ int s_last;
+	const int q = blockIdx.y, G = gridDim.x, t = threadIdx.x;
+	for (int i = t; i < dim; i += SMALL_THREADS) sq[i] = Q[(int64_t)q * dim + i];
+	__syncthreads();
+	const int64_t r = (int64_t)blockIdx.x * SMALL_THREADS + t;
+	SHit h{F_INF, 0, INT64_MAX};
+	if (r < n && reinterpret_cast<const float *>(rowaux)[raix(r, 0)] != F_INF) {
+		const T *x = X + r * ld;
+		double a = 0.0, b = 0.0, c = 0.0;
+		const int d4 = dim >> 2;  // rows are padded to a multiple of 4 elements: aligned 16-B (8-B bf16) loads
+#pragma unroll 4
+		for (int i4 = 0; i4 < d4; ++i4) {
+			const float4 xv = xval4(x, 4 * i4);
+			const float4 qv = *reinterpret_cast<const float4 *>(sq + 4 * i4);
+			exact_acc<METRIC>(xv.x, qv.x, a, b, c);
+			exact_acc<METRIC>(xv.y, qv.y, a, b, c);
+			exact_acc<METRIC>(xv.z, qv.z, a, b, c);
+			exact_acc<METRIC>(xv.w, qv.w, a, b, c);
+		}
+		for (int i = 4 * d4; i < dim; ++i) exact_acc<METRIC>(xval(x, i), sq[i], a, b, c);
+		double v;
+		if (METRIC == METRIC_L2)
+			v = a;
+		else if (METRIC == METRIC_DOT)
+			v = 1.0 - a;
+		else
+			v = 1.0 - a / (sqrt(b) * sqrt(c));
+		float f = (float)v + 0.0f;
+		if (__builtin_isnan(f)) f = __builtin_nanf("");
+		h = SHit{f, 1, labels[r]};
+	}
+	s[t] = h;
+	__syncthreads();
+	// this workgroup's top-k: sorted by (distance, label)
+	shit_sort(s, SMALL_THREADS);
+	SHit *mine = part + ((int64_t)q * G + blockIdx.x) * k;
+	for (int i = t; i < k; i += SMALL_THREADS) mine[i] = s[i];
+	if (!LHIP_ABL_SMALL_NOFENCE) __threadfence();
+	__syncthreads();
+	if (t == 0) s_last = atomicAdd(&counter[q], 1u) == (unsigned)(G - 1);
+	__syncthreads();
+	if (!s_last) return;
+	if (!LHIP_ABL_SMALL_NOFENCE) __threadfence();
+	// merge: one sort of the G sorted k-lists (padded to a power of two)
+	const int P = G * k;
+	int P2 = SMALL_THREADS;
+	while (P2 < P) P2 <<= 1;
+	const SHit *all = part + (int64_t)q * G * k;
+	for (int i = t; i < P2; i += SMALL_THREADS) s[i] = i < P ? all[i] : SHit{F_INF, 0, INT64_MAX};
+	__syncthreads();
+	shit_sort(s, P2);
+	for (int i = t; i < k; i += SMALL_THREADS) {
+		out_l[(int64_t)q * k + i] = s[i].v ? s[i].l : -1;
+		out_d[(int64_t)q * k + i] = s[i].v ? s[i].d : __builtin_nanf("");
+	}
+	if (t == 0) {
+		int cnt = 0;
+		for (int i = 0; i < k; ++i) cnt += s[i].v;
+		out_c[q] = cnt;
+		counter[q] = 0u;  // ready for the next launch on this stream
+	}
+}
+
+int small_exact_grid(int64_t n_slots) { return (int)((n_slots + SMALL_THREADS - 1) / SMALL_THREADS); }
+
+bool small_exact_fits(int64_t n_slots, int dim, int nq, int k) {
+	const int64_t G = (n_slots + SMALL_THREADS - 1) / SMALL_THREADS;
+	return n_slots > 0 && n_slots <= SMALL_MAX_ROWS && dim <= SMALL_MAX_DIM && nq <= SMALL_MAX_Q && k <= SMALL_MAX_K &&
+	       G * k <= SMALL_MAX_PART;
+}
+
+template <typename T>
+static void small_exact_dispatch(const StoreView &s, const float *Q, int nq, int k, void *part, unsigned *counter,
+                                 int64_t *L, float *D, int *C, hipStream_t st) {
+	const dim3 grid((unsigned)small_exact_grid(s.n_slots), (unsigned)nq);
+	const T *X = static_cast<const T *>(s.X);
+	SHit *p = static_cast<SHit *>(part);
+	switch (s.metric) {
+	case METRIC_L2:
+		small_exact_kernel<METRIC_L2, T><<<grid, SMALL_THREADS, 0, st>>>(X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim, Q,
+		                                                                 k, p, counter, L, D, C);
+		break;
+	case METRIC_DOT:
+		small_exact_kernel<METRIC_DOT, T><<<grid, SMALL_THREADS, 0, st>>>(X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim,
+		                                                                  Q, k, p, counter, L, D, C);
+		break;
+	default:
+		small_exact_kernel<METRIC_COSINE, T><<<grid, SMALL_THREADS, 0, st>>>(X, s.rowaux, s.labels, s.n_slots, s.ld,
+		                                                                     s.dim, Q, k, p, counter, L, D, C);
+		break;
+	}
+}
+
+void launch_small_exact(const StoreView &s, const float *Q, int nq, int k, void *part, unsigned *counter, int64_t *L,
+                        float *D, int *C, hipStream_t st) {
+	if (!small_exact_fits(s.n_slots, s.dim, nq, k)) throw std::runtime_error("small exact search: shape out of range");
+	if (s.xbf16)
+		small_exact_dispatch<uint16_t>(s, Q, nq, k, part, counter, L, D, C, st);
+	else
+		small_exact_dispatch<float>(s, Q, nq, k, part, counter, L, D, C, st);
+}
+
+// ---------------------------------------------------------------------------
 // second threshold pass for queries whose certificate failed (a segment
 // overflowed, or the sampled tau was loose): the failed queries are packed
 // into a batch of their own with tau = the k-th exact distance the first pass

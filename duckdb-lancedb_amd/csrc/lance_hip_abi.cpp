@@ -50,6 +50,27 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	const float mu = (metric_quirk && metric != METRIC_L2) ? max_ux_l2 : max_ux;
 	StoreView sv{X, aux, dlabels, n_slots, ld, dim, eff_metric, xbf16 ? 1 : 0,
 	             Xs ? static_cast<const void *>(Xs) : X, (xbf16 || Xs) ? 1 : 0};
+	if (small_exact && small_exact_fits(n_slots, dim, nq, k)) {
+		// a few queries over a small store (one query per lance_search call):
+		// one launch of exact distances + merge, no bounds, no status readback
+		last_stats[3] = 2;
+		const size_t np = (size_t)nq * small_exact_grid(n_slots) * k;
+		ws.spart.need(np);
+		if (ws.scnt.n < (size_t)SMALL_MAX_Q) {
+			ws.scnt.need(SMALL_MAX_Q);
+			HIPCHK(hipMemsetAsync(ws.scnt.p, 0, ws.scnt.n * sizeof(unsigned), stream));
+		}
+		tic(0);
+		launch_small_exact(sv, dQ, nq, k, ws.spart.p, ws.scnt.p, dL, dD, dC, stream);
+		tic(1);
+		HIPCHK(hipGetLastError());
+		if (time_kernels) {
+			kt_dense_ms += toc_ms(0, 1);  // reported with the dense-path launches
+			kt_dense_n += 1;
+		}
+		if (!defer_sync) HIPCHK(hipStreamSynchronize(stream));
+		return;
+	}
 	const int nq_pad = (int)round_up(nq, SCAN_BQ);
 	ws.Qf.need((size_t)nq_pad * ld);
 	ws.Qb.need((size_t)nq_pad * ld);
@@ -682,19 +703,25 @@ int32_t lance_detached_search_batch(void *handle, const float *queries, int32_t 
 		ix->bind();
 		auto &ws = ix->ws;
 		ws.Qin.need((size_t)nq * dim);
-		ws.out_l.need((size_t)nq * k);
-		ws.out_d.need((size_t)nq * k);
-		ws.out_c.need((size_t)nq);
-		// pinned staging: true async copies on the handle's stream, one wait at the end
+		// pinned staging: true async copies on the handle's stream, one wait at
+		// the end; the results [labels | distances | counts] are one device
+		// block, read back by one copy
 		const size_t qb = (size_t)nq * dim * sizeof(float), lb = (size_t)nq * k * sizeof(int64_t);
 		const size_t db = (size_t)nq * k * sizeof(float), cb = (size_t)nq * sizeof(int32_t);
+		ws.out_blk.need(lb + db + cb);
+		int64_t *dL = reinterpret_cast<int64_t *>(ws.out_blk.p);
+		float *dD = reinterpret_cast<float *>(ws.out_blk.p + lb);
+		int32_t *dC = reinterpret_cast<int32_t *>(ws.out_blk.p + lb + db);
 		uint8_t *io = ws.need_host_io(std::max(qb, lb + db + cb));
 		memcpy(io, queries, qb);
 		HIPCHK(hipMemcpyAsync(ws.Qin.p, io, qb, hipMemcpyHostToDevice, ix->stream));
-		ix->search_any(ws.Qin.p, nq, k, nprobes, refine_factor, ws.out_l.p, ws.out_d.p, ws.out_c.p);
-		HIPCHK(hipMemcpyAsync(io, ws.out_l.p, lb, hipMemcpyDeviceToHost, ix->stream));
-		HIPCHK(hipMemcpyAsync(io + lb, ws.out_d.p, db, hipMemcpyDeviceToHost, ix->stream));
-		HIPCHK(hipMemcpyAsync(io + lb + db, ws.out_c.p, cb, hipMemcpyDeviceToHost, ix->stream));
+		struct DeferSync {
+			decltype(ix) p;
+			~DeferSync() { p->defer_sync = false; }
+		} defer{ix};
+		ix->defer_sync = true;  // the readback below waits for the search
+		ix->search_any(ws.Qin.p, nq, k, nprobes, refine_factor, dL, dD, dC);
+		HIPCHK(hipMemcpyAsync(io, ws.out_blk.p, lb + db + cb, hipMemcpyDeviceToHost, ix->stream));
 		lhip::spin_sync(ix->stream);
 		memcpy(out_labels, io, lb);
 		memcpy(out_distances, io + lb, db);
@@ -934,6 +961,10 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			const int d = std::stoi(v);
 			if (d < 8 || d > 256) throw Error("cand_extra must be in [8, 256]");
 			ix->cand_extra = d;
+			return 0;
+		}
+		if (k == "small_exact") {
+			ix->small_exact = (v == "1" || v == "on" || v == "true");
 			return 0;
 		}
 		if (k == "retry_pass") {

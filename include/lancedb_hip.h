@@ -187,6 +187,9 @@ int32_t lance_hip_device_count(void);
  *                  tiles (at least 32 tiles); default "32"
  *   "cand_extra"   exact candidates re-ranked per query beyond k: max(k *
  *                  refine_factor, k + max(cand_extra, k)), default "32"
+ *   "small_exact"  "1" (default) | "0": <= 8 queries over <= 32768 slots
+ *                  (k <= 64, dim <= 4096) take one launch of exact f64
+ *                  distances + merge instead of the bound/refine pipeline
  *   "retry_pass"   "1" (default) | "0": rerun uncertified threshold-path
  *                  queries with a tightened tau before the exact fallback
  *   "index_type"   "ivf_pq" (default) | "ivf_flat": what create_index builds
@@ -201,7 +204,9 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 /* Statistics of the last search on this handle (for benches/tests):
  * out[0] = queries whose exactness certificate failed and took the exact
  * fallback, out[1] = total candidates refined, out[2] = max pool size,
- * out[3] = 1 if the dense (small-N) path ran, out[4] = queries rerun by the
+ * out[3] = 1 if the dense (small-N) path ran, 2 if the one-launch small exact
+ * search ran (option "small_exact", default on: <= 8 queries, <= 32768 slots,
+ * k <= 64, dim <= 4096), out[4] = queries rerun by the
  * second threshold pass (option "retry_pass", default on: an uncertified
  * query is rescanned with tau = its first-pass k-th exact distance and
  * full-size segments before it may take the exact fallback).  Returns 0 or -1. */

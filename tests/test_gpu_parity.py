@@ -359,3 +359,53 @@ def test_cosine_repeated_searches_are_stable(hip, mk):
     el, ed, ec = c_oracle.flat_search_batch(X, Q, 10, "cosine", live=keep, acc64=True)
     for _ in range(40):
         assert_same(*hip.LanceDetachedSearchBatch(h, Q, 10), el, ed, ec)
+
+
+# ---------------------------------------------------------------------------
+# one-launch small exact search (<= 8 queries over <= 32768 slots)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("metric", ["l2", "dot", "cosine"])
+@pytest.mark.parametrize("n,dim,nq,k", [(1, 3, 1, 5), (300, 17, 2, 10), (10_000, 128, 1, 10), (10_000, 128, 8, 64),
+                                        (32_768, 129, 3, 7), (5_000, 1000, 4, 16)])
+def test_small_exact_path(hip, mk, metric, n, dim, nq, k):
+    rng = np.random.default_rng(n + dim + nq)
+    X = rng.standard_normal((n, dim)).astype(np.float32)
+    Q = rng.standard_normal((nq, dim)).astype(np.float32)
+    h = mk(dim, metric)
+    hip.LanceDetachedAddBatch(h, X, n, dim)
+    dead = rng.choice(n, n // 10, replace=False) if n > 10 else np.array([], np.int64)
+    if len(dead):
+        hip.LanceDetachedDeleteBatch(h, dead)
+    live = np.ones(n, bool)
+    live[dead] = False
+    gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, k)
+    assert hip.LanceHipLastSearchStats(h)["small_exact"]
+    el, ed, ec = c_oracle.flat_search_batch(X, Q, k, metric, live=live, acc64=True, nthreads=16)
+    assert_same(gl, gd, gc, el, ed, ec)
+    # the bound/refine pipeline returns the same
+    hip.LanceHipSetOption(h, "small_exact", "0")
+    pl, pd, pc = hip.LanceDetachedSearchBatch(h, Q, k)
+    assert not hip.LanceHipLastSearchStats(h)["small_exact"]
+    np.testing.assert_array_equal(pc, gc)
+    np.testing.assert_array_equal(pl, gl)
+    np.testing.assert_array_equal(pd, gd)
+
+
+def test_small_exact_limits_and_repeats(hip, mk):
+    # just past the slot limit takes the pipeline; 9 queries take the pipeline;
+    # repeated one-query calls reuse the completion counters
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((32_769, 8)).astype(np.float32)
+    h = mk(8)
+    hip.LanceDetachedAddBatch(h, X, len(X), 8)
+    hip.LanceDetachedSearchBatch(h, X[:2], 4)
+    assert not hip.LanceHipLastSearchStats(h)["small_exact"]
+    h2 = mk(8)
+    hip.LanceDetachedAddBatch(h2, X[:20_000], 20_000, 8)
+    hip.LanceDetachedSearchBatch(h2, X[:9], 4)
+    assert not hip.LanceHipLastSearchStats(h2)["small_exact"]
+    el, ed, ec = c_oracle.flat_search_batch(X[:20_000], X[100:140], 4, "l2", acc64=True, nthreads=16)
+    for i in range(40):
+        l, d = hip.LanceDetachedSearch(h2, X[100 + i], 8, 4)
+        assert hip.LanceHipLastSearchStats(h2)["small_exact"]
+        np.testing.assert_array_equal(l, el[i])
