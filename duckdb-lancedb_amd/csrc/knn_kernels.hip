@@ -1837,9 +1837,15 @@ void launch_copy_fallback(const float *keys, const int64_t *vals, int64_t n_live
 // in f64 (sequential over the dimension, rounded once to f32: the oracle's
 // definition); a bitonic sort of the workgroup's 256 rows by (distance,
 // label) puts its top-k in a partial list; the last workgroup of the query to
-// finish (device-scope counter) sorts the partial lists together and writes
-// the result.  No bounds, no certificate, no host round trip in between.
+// finish (device-scope counter) keeps the partial entries that can still
+// place and sorts those.  No bounds, no certificate, no host round trip in between.
 // ---------------------------------------------------------------------------
+#ifndef LHIP_ABL_SMALL_NOWGSORT
+#define LHIP_ABL_SMALL_NOWGSORT 0
+#endif
+#ifndef LHIP_ABL_SMALL_NOMERGE
+#define LHIP_ABL_SMALL_NOMERGE 0
+#endif
 #ifndef LHIP_ABL_SMALL_NOFENCE
 #define LHIP_ABL_SMALL_NOFENCE 0  // timing ablation (tools/ablate.sh): results wrong by design
 #endif
@@ -1883,8 +1889,10 @@ __global__ __launch_bounds__(SMALL_THREADS) void small_exact_kernel(const T *__r
                                                                     int64_t *__restrict__ out_l,
                                                                     float *__restrict__ out_d, int *__restrict__ out_c) {
 	__shared__ __attribute__((aligned(16))) float sq[SMALL_MAX_DIM];
-	__shared__ SHit s[SMALL_MAX_PART];
+	__shared__ SHit s_rows[SMALL_MAX_PART], s2[SMALL_MAX_PART], red[SMALL_THREADS];
+	__shared__ unsigned s_ns;
 	__shared__ int s_last;
+	SHit *s = s_rows;
 	const int q = blockIdx.y, G = gridDim.x, t = threadIdx.x;
 	for (int i = t; i < dim; i += SMALL_THREADS) sq[i] = Q[(int64_t)q * dim + i];
 	__syncthreads();
@@ -1918,7 +1926,7 @@ __global__ __launch_bounds__(SMALL_THREADS) void small_exact_kernel(const T *__r
 	s[t] = h;
 	__syncthreads();
 	// this workgroup's top-k: sorted by (distance, label)
-	shit_sort(s, SMALL_THREADS);
+	if (!LHIP_ABL_SMALL_NOWGSORT) shit_sort(s, SMALL_THREADS);
 	SHit *mine = part + ((int64_t)q * G + blockIdx.x) * k;
 	for (int i = t; i < k; i += SMALL_THREADS) mine[i] = s[i];
 	if (!LHIP_ABL_SMALL_NOFENCE) __threadfence();
@@ -1927,14 +1935,31 @@ __global__ __launch_bounds__(SMALL_THREADS) void small_exact_kernel(const T *__r
 	__syncthreads();
 	if (!s_last) return;
 	if (!LHIP_ABL_SMALL_NOFENCE) __threadfence();
-	// merge: one sort of the G sorted k-lists (padded to a power of two)
+	// merge: every list is sorted, so the k-th smallest overall is <= each
+	// list's k-th entry; only entries <= thr = the smallest of those can place
+	// (typically a few k of the G*k): they alone are sorted
 	const int P = G * k;
-	int P2 = SMALL_THREADS;
-	while (P2 < P) P2 <<= 1;
 	const SHit *all = part + (int64_t)q * G * k;
-	for (int i = t; i < P2; i += SMALL_THREADS) s[i] = i < P ? all[i] : SHit{F_INF, 0, INT64_MAX};
+	for (int i = t; i < P; i += SMALL_THREADS) s[i] = all[i];
+	if (t == 0) s_ns = 0;
 	__syncthreads();
-	shit_sort(s, P2);
+	if (t < G) red[t] = s[t * k + k - 1];
+	__syncthreads();
+	for (int w = 1; w < G; w <<= 1) {
+		if ((t & (2 * w - 1)) == 0 && t + w < G && shit_less(red[t + w], red[t])) red[t] = red[t + w];
+		__syncthreads();
+	}
+	const SHit thr = red[0];
+	for (int i = t; i < P; i += SMALL_THREADS)
+		if (!shit_less(thr, s[i])) s2[atomicAdd(&s_ns, 1u)] = s[i];
+	__syncthreads();
+	const int ns = (int)s_ns;
+	int n2 = 2;
+	while (n2 < ns) n2 <<= 1;
+	for (int i = ns + t; i < n2; i += SMALL_THREADS) s2[i] = SHit{F_INF, 0, INT64_MAX};
+	__syncthreads();
+	if (!LHIP_ABL_SMALL_NOMERGE) shit_sort(s2, n2);
+	s = s2;
 	for (int i = t; i < k; i += SMALL_THREADS) {
 		out_l[(int64_t)q * k + i] = s[i].v ? s[i].l : -1;
 		out_d[(int64_t)q * k + i] = s[i].v ? s[i].d : __builtin_nanf("");

@@ -29,6 +29,8 @@ for v in "$@"; do
 	NOMFMA_NOREADS_NOEPI) build NOMFMA_NOREADS_NOEPI -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 -DLHIP_ABL_NO_EPILOGUE=1 ;;
 	NOFLUSH) build NOFLUSH -DLHIP_ABL_NO_FLUSH=1 ;;
 	SNOFENCE) build SNOFENCE -DLHIP_ABL_SMALL_NOFENCE=1 ;;
+	SNOWGSORT) build SNOWGSORT -DLHIP_ABL_SMALL_NOWGSORT=1 ;;
+	SNOMERGE) build SNOMERGE -DLHIP_ABL_SMALL_NOMERGE=1 ;;
 	SLOW_NEVER) build SLOW_NEVER -DLHIP_ABL_SLOW_NEVER=1 ;;
 	SLOW_UNROLL) build SLOW_UNROLL -DLHIP_SLOW_VALU=0 -DLHIP_SLOW_UNROLL=1 ;;
 	SLOW_SWITCH) build SLOW_SWITCH -DLHIP_SLOW_VALU=0 ;;
