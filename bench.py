@@ -6,9 +6,14 @@ N = 1,000,000 x d = 768 f32 base, k = 10, query batch B = 256.
 One step = one batch of 256 queries searched through the C-ABI
 (lance_hip_search_batch_device) against the whole base, inputs resident in HBM.
 With --gpus N (one process per GPU, launched by torch.distributed.run) the base
-is row-sharded over the ranks (fixed N: strong scaling); every rank searches
-its shard for the same batch, the per-shard top-k lists are all-gathered over
-RCCL and merged on the device (lance_hip_merge_topk_device).
+is row-sharded over the ranks; every rank searches its shard for the same
+batch, the per-shard top-k lists are all-gathered over RCCL (one collective per
+batch) and merged on the device (lance_hip_merge_topk_device).
+  --scaling weak   (default) fixed N, global batch = B x world: per-GPU flops
+                   fixed as the GPU count grows ("scaling": "weak");
+  --scaling strong fixed N and fixed global batch B: each rank scans N/world
+                   rows for the same B queries ("scaling": "strong").
+--config nstar is the north_star target: flat L2 over 10M x 768 f32.
 
 Prints ONE JSON line on rank 0 (driver contract).  The CPU baseline (rank 0,
 N = 1 only) times oracle/flat_knn.c — the port of the reference's flat search
@@ -46,6 +51,8 @@ CONFIGS = {
     "c1": dict(n=10_000, dim=128, k=10, batch=1, metric="l2", storage="f32", normalize=False),
     "c2": dict(n=1_000_000, dim=768, k=10, batch=256, metric="l2", storage="f32", normalize=False),
     "c3": dict(n=10_000_000, dim=768, k=100, batch=256, metric="dot", storage="bf16", normalize=True),
+    # north_star target: ">= 70 % HBM roofline on flat-L2 scan at 10M x 768 f32, recall@10 >= 0.99"
+    "nstar": dict(n=10_000_000, dim=768, k=10, batch=256, metric="l2", storage="f32", normalize=False),
     # IVF configs: n is ROWS PER GPU (the 8-GPU configs of BASELINE.json hold 100M rows,
     # 12.5M per GPU; --gpus N runs N such shards), clustered synthetic rows
     "c4": dict(n=12_500_000, dim=768, k=10, batch=256, metric="l2", storage="f32", normalize=False,
@@ -72,7 +79,10 @@ def parse():
     ap.add_argument("--metric", default=None)
     ap.add_argument("--storage", choices=["f32", "bf16"], default=None, help="index option storage")
     ap.add_argument("--scan-copy", choices=["on", "off"], default="on", help="index option scan_copy")
-    ap.add_argument("--recall-queries", type=int, default=16)
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="multi-GPU: weak = global batch B x world, strong = global batch B")
+    ap.add_argument("--recall-queries", type=int, default=None, help="default: the whole batch")
+    ap.add_argument("--cpu-threads", type=int, default=None, help="default: every core this job may use")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-recall", action="store_true")
@@ -168,6 +178,40 @@ def ivf_traffic(config, n, dim, batch):
 
 def err_buf():
     return ctypes.create_string_buffer(2048)
+
+
+def host_cpus():
+    """The host cores this job may use (affinity mask, capped by a cgroup CPU
+    quota when one is set) and what they are: recorded with every CPU baseline."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    usable = min(aff, quota) if quota else aff
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota, "usable": usable, "model": model,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_threads(a):
+    return a.cpu_threads or host_cpus()["usable"]
 
 
 def main_ivf(a):
@@ -275,8 +319,8 @@ def main_ivf(a):
             hi = min(N, lo + (1 << 18))
             Xh[lo:hi] = gen_clustered(lo, hi, D, dev, centers).cpu().numpy()
         Qh = Q.cpu().numpy()
-        nr = min(a.recall_queries, B)
-        nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        nr = min(a.recall_queries or B, B)
+        nthreads = cpu_threads(a)
         el, _, _ = c_oracle.flat_search_batch(Xh, Qh[:nr], K, a.metric, acc64=True, nthreads=nthreads)
         recall = flat_knn.recall_at_k(res_l[:nr], el, min(10, K))
         if not a.no_cpu_baseline:
@@ -302,7 +346,7 @@ def main_ivf(a):
                    "sample": f"{done} queries, one per call, {a.index_type} nprobes={a.nprobe} over the GPU-built "
                              f"model and lists of {N}x{D} rows, f32 distances ({tcpu:.1f} s, oracle/flat_knn.c IVF "
                              f"port, {nthreads} OpenMP threads)",
-                   "id_overlap_with_gpu": round(agree / (done * K), 4)}
+                   "id_overlap_with_gpu": round(agree / (done * K), 4), "host": host_cpus()}
         del Xh
 
     if rank == 0:
@@ -371,7 +415,7 @@ def main_c1(a):
         lance_hip.LanceDetachedSearch(h, Q[i], D, K)
     kt = lance_hip.LanceHipKernelTimes(h)
     small = lance_hip.LanceHipLastSearchStats(h)["small_exact"]
-    nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    nthreads = cpu_threads(a)
     nr = min(16, a.steps)
     el, _, _ = c_oracle.flat_search_batch(X, Q[:nr], K, a.metric, acc64=True, nthreads=nthreads)
     exact = all((got[i] == el[i]).all() for i in range(nr))
@@ -454,7 +498,8 @@ def main():
         del X
     g = torch.Generator(device=dev)
     g.manual_seed(5678)
-    BG = B * world  # global batch (weak scaling over ranks)
+    # global batch: weak = B per rank (per-GPU flops fixed), strong = B in all
+    BG = B * world if a.scaling == "weak" else B
     Q = torch.randn((BG, D), generator=g, device=dev, dtype=torch.float32)
     if a.normalize:
         Q /= torch.linalg.vector_norm(Q, dim=1, keepdim=True)
@@ -515,8 +560,8 @@ def main():
             Xh[lo:hi] = Xr.cpu().numpy()
             del Xr
         Qh = Q.cpu().numpy()
-        nr = min(a.recall_queries, B)
-        nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        nr = min(a.recall_queries or BG, BG)
+        nthreads = cpu_threads(a)
         el, ed, _ = c_oracle.flat_search_batch(Xh, Qh[:nr], K, a.metric, acc64=True, nthreads=nthreads)
         recall = flat_knn.recall_at_k(res_l[:nr], el, min(10, K))
         recall_k = flat_knn.recall_at_k(res_l[:nr], el, K)
@@ -532,9 +577,22 @@ def main():
                 if time.perf_counter() - t_cpu0 >= a.cpu_seconds and done >= 2:
                     break
             t_cpu = time.perf_counter() - t_cpu0
+            # batched leg: one call for a block of queries (each 64-row block of the
+            # base reused from cache by every query of the call), bounded likewise
+            nbq = 8
+            while True:
+                tb0 = time.perf_counter()
+                c_oracle.flat_search_batch(Xh, Qh[:nbq], K, a.metric, acc64=False, nthreads=nthreads)
+                t_b = time.perf_counter() - tb0
+                if t_b >= a.cpu_seconds / 3 or nbq >= B:
+                    break
+                nbq = min(B, nbq * 4)
             cpu = {"value": done / t_cpu, "unit": "queries/s", "cores": nthreads, "kind": "port",
-                   "sample": f"{done} queries, one per call, each an exact f32 {a.metric} scan of all {N}x{D} "
-                             f"rows ({t_cpu:.1f} s, oracle/flat_knn.c, {nthreads} OpenMP threads)"}
+                   "sample": f"{done} queries, one per call (the reference API), each an exact f32 {a.metric} scan "
+                             f"of all {N}x{D} rows ({t_cpu:.1f} s, oracle/flat_knn.c, {nthreads} OpenMP threads)",
+                   "batched": {"value": nbq / t_b, "unit": "queries/s", "queries_per_call": nbq,
+                               "seconds": round(t_b, 2)},
+                   "host": host_cpus()}
         del Xh
 
     if rank == 0:
@@ -548,7 +606,7 @@ def main():
             # algorithmic bytes per launch: every base row (ld elements + 16 B row aux) + the bf16 query tile
             bytes_launch = kt["scan_rows"] * (ld * esz + 16) + kt["scan_qpad"] * ld * 2
             ach = bytes_launch / (avg_ms * 1e-3) / 1e9
-            traffic = measured_traffic(N // world, D, BG, esz) if a.config == "c2" else None
+            traffic = measured_traffic(N // world, D, BG, esz)
             mfma_tfs = 2.0 * kt["scan_rows"] * D * BG / (avg_ms * 1e-3) / 1e12
             kname = {"l2": "L2", "dot": "DOT", "cosine": "COSINE"}[a.metric]
             # the bounding roof: HBM time of the bytes vs dense-bf16 MFMA time of the flops
@@ -565,8 +623,13 @@ def main():
                     "kernel": f"scan_kernel<{kname},append,{'bf16' if esz == 2 else 'f32'}>",
                     "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(bytes_launch),
                     "mfma_tflops": round(mfma_tfs, 1), "mfma_frac": round(mfma_tfs / MFMA_BF16_PEAK_TFS, 4)})
-        metric_name = ("kNN queries/sec + recall@10, 1Mx768 f32 flat; GB/s vs HBM roofline" if a.config == "c2" else
-                       f"kNN queries/sec + recall@{K}, {N // 1_000_000}Mx{D} {a.storage} flat IP; GB/s vs HBM roofline")
+        if a.config == "c2":
+            metric_name = "kNN queries/sec + recall@10, 1Mx768 f32 flat; GB/s vs HBM roofline"
+        elif a.config == "nstar":
+            metric_name = f"kNN queries/sec + recall@10, {N // 1_000_000}Mx{D} f32 flat L2 (north_star); GB/s vs HBM roofline"
+        else:
+            metric_name = (f"kNN queries/sec + recall@{K}, {N // 1_000_000}Mx{D} {a.storage} flat "
+                           f"{'IP' if a.metric == 'dot' else a.metric}; GB/s vs HBM roofline")
         line = {
             "metric": metric_name,
             "value": round(value, 1),
@@ -576,15 +639,16 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": a.scaling,
             "vs_baseline": None,
             "dtype": a.storage,
             "data": "synthetic N(0,1) base (seeded torch Philox), independent N(0,1) queries"
                     + (", rows and queries L2-normalized; base stored as bf16 (RNE)" if a.config == "c3" else ""),
             "config": {"workload": f"{a.config.upper()} flat {a.metric} {N}x{D} {a.storage} k={K} query-batch={BG}",
                        "n": N, "dim": D, "k": K, "global_batch": BG, "batch_per_gpu": B, "metric": a.metric, "storage": a.storage,
-                       "parallelism": f"rowshard{world}"},
+                       "parallelism": f"rowshard{world}", "scan_copy": a.scan_copy},
             "recall_at_10": recall,
+            "recall_queries": None if recall is None else nr,
             "roofline": roof,
             "cpu_baseline": cpu,
             "search_stats": st,

@@ -253,7 +253,17 @@ constexpr int BR = SCAN_BR, BQ = SCAN_BQ;
 // when LB <= tau[q]: one ballot per bound, survivors appended to the wave's
 // LDS list, written out at the next stage ahead of that stage's DMA.
 // ---------------------------------------------------------------------------
-// development-only ablation switches (timing experiments; results are wrong when set)
+// Development-only ablation switches (timing experiments; results are WRONG
+// when set).  A release build refuses them: only tools/ablate.sh, which also
+// defines LHIP_ABLATION_BUILD, may turn them on.
+#if !defined(LHIP_ABLATION_BUILD) &&                                                                        \
+    (defined(LHIP_ABL_NO_EPILOGUE) || defined(LHIP_ABL_NO_MFMA) || defined(LHIP_ABL_NO_READS) ||             \
+     defined(LHIP_ABL_NO_QDMA) || defined(LHIP_ABL_NO_SLOW) || defined(LHIP_ABL_SLOW_NEVER) ||               \
+     defined(LHIP_ABL_DRAIN_EPI) || defined(LHIP_ABL_NO_LISTWRITE) || defined(LHIP_ABL_NO_FLUSH) ||          \
+     defined(LHIP_ABL_SMALL_NOWGSORT) || defined(LHIP_ABL_SMALL_NOMERGE) || defined(LHIP_ABL_SMALL_NOFENCE) || \
+     defined(LHIP_PROF))
+#error "LHIP_ABL_* / LHIP_PROF are timing ablations that break results: build them through tools/ablate.sh"
+#endif
 #ifndef LHIP_ABL_NO_EPILOGUE
 #define LHIP_ABL_NO_EPILOGUE 0
 #endif
@@ -301,12 +311,6 @@ constexpr int BR = SCAN_BR, BQ = SCAN_BQ;
 #endif
 #ifndef LHIP_PRIO_HI_HALF
 #define LHIP_PRIO_HI_HALF 0  // s_setprio 1 on waves 4..7 (the second-dispatched half) for the whole kernel
-#endif
-#ifndef LHIP_DBG_RA_GLOBAL
-#define LHIP_DBG_RA_GLOBAL 0  // debug: dense cosine epilogue reads the row aux from global memory
-#endif
-#ifndef LHIP_DBG_QA_GLOBAL
-#define LHIP_DBG_QA_GLOBAL 0  // debug: dense epilogue reads the query constants from global memory
 #endif
 #if LHIP_PROF
 __device__ unsigned long long lhip_prof[24];
@@ -586,8 +590,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 
 	// Stage h may be issued once every wave is done reading stage h-NST (its
 	// slot), i.e. after the barrier of iteration h-NST; and a tile's stage 0
-	// (which carries its row aux into RA slot tile&1) only once the epilogue of
-	// tile-2 is done (matters when S < NST).
+	// (which carries its row aux into RA slot tile&1) only once every wave is
+	// past the epilogue of tile-2 (matters when S < NST; see the end of the loop).
 	int tiles_done = 0;
 	const bool ra_wave = w < 4;  // waves that issue a row-aux DMA with a tile's stage 0
 	auto pump = [&](int limit) {
@@ -844,13 +848,6 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 		const int ti = cur_t++;
 
 		if (LHIP_ABL_DRAIN_EPI) LHIP_WAIT_VM(0);
-		// 64 cycles of s_nop between the tile's last MFMAs and the epilogue's
-		// reads of the accumulators: without them the cosine epilogue (VALU on
-		// the accumulators right after the k loop) read stale accumulator
-		// values in ~1% of the queries of a small store (measured on MI355X:
-		// 15-19 wrong top-10 lists per 1600 queries; 0 with the pad; a vmcnt or
-		// lgkmcnt wait in its place does not remove it).  ~0.3% of a tile.
-		asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 		// ---- epilogue of tile ti (its row aux landed with its stage 0) ------
 		const int64_t tile = (int64_t)blockIdx.x + (int64_t)ti * gridDim.x;
 		const int64_t row0 = tile * tile_stride * BR;
@@ -867,11 +864,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 			for (int u = 0; u < 4; ++u) {
 				const int ql = qlb + 32 * u;
 				if (q0 + ql >= nq) continue;
-#if LHIP_DBG_QA_GLOBAL
-				const float4 qa = qaux[q0 + ql];
-#else
 				const float4 qa = QA[ql];
-#endif
 				float *dst = dense + (int64_t)(q0 + ql) * ld_out + tile * BR;
 #pragma unroll
 				for (int t = 0; t < 2; ++t)
@@ -883,13 +876,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 							    acc[t][u][4 * gq + 0], acc[t][u][4 * gq + 1], acc[t][u][4 * gq + 2], acc[t][u][4 * gq + 3]);
 							continue;
 						}
-#if LHIP_DBG_RA_GLOBAL
-						const float *gra = reinterpret_cast<const float *>(rowaux);
-						auto ra4g = [&](int rr, int c) { return *reinterpret_cast<const float4 *>(gra + raix(row0 + rr, c)); };
-						const float4 al = ra4g(r0, 0), xn = ra4g(r0, 1), ux = ra4g(r0, 2), sc = ra4g(r0, 3);
-#else
 						const float4 al = ra4(r0, 0), xn = ra4(r0, 1), ux = ra4(r0, 2), sc = ra4(r0, 3);
-#endif
 						*reinterpret_cast<float4 *>(dst + r0) = make_float4(
 						    lower_bound<METRIC>(acc[t][u][4 * gq + 0], make_float4(al.x, xn.x, ux.x, sc.x), qa),
 						    lower_bound<METRIC>(acc[t][u][4 * gq + 1], make_float4(al.y, xn.y, ux.y, sc.y), qa),
@@ -1158,8 +1145,24 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 			prof_over += nl > C::WLIST ? nl - C::WLIST : 0;
 #endif
 		}
+		// A tile's stage 0 carries its row aux into RA slot tile&1, the slot
+		// tile-2's epilogue reads (cosine and the sample pass read the row terms
+		// from LDS there).  When S < NST that stage falls inside the pump limit
+		// before the epilogue of tile-2 is over, so pump holds it back (iss_t >=
+		// tiles_done + 2).  It may only go out once EVERY wave has left that
+		// epilogue: releasing it on this wave's own tiles_done let waves 0..3
+		// overwrite the slot while slower waves still read it (wrong cosine
+		// bounds in ~1% of the queries of small-dim stores).  So a stage held
+		// back here is issued behind a workgroup barrier.  The condition only
+		// depends on g, S, G and the tile count, so it is uniform over the
+		// workgroup and every wave takes the barrier or none does.
 		tiles_done = cur_t;
-		pump(g + C::NST);  // stages held back for this tile's row-aux slot
+		if (iss_g < G && iss_g <= g + C::NST && iss_s == 0 && iss_t < tiles_done + 2) {
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+			__builtin_amdgcn_s_barrier();
+			asm volatile("" ::: "memory");
+			pump(g + C::NST);
+		}
 #if LHIP_PROF
 		PROF_T(t4);
 		pe += t4 - t3;

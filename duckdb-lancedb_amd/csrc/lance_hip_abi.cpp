@@ -1070,6 +1070,9 @@ int32_t lance_hip_search_batch_device(void *handle, const float *d_queries, int3
 		if (dim != ix->dim)
 			throw Error("expected query dimension " + std::to_string(ix->dim) + ", got " + std::to_string(dim));
 		if (k <= 0) throw Error("k must be positive");
+		if (nq < 0) throw Error("negative query count");
+		if (nq == 0) return 0;
+		if (!d_queries || !d_out_labels || !d_out_distances || !d_out_counts) throw Error("null buffer");
 		std::lock_guard<std::mutex> g(ix->mu);
 		ix->bind();
 		if (ix->n_live == 0) {

@@ -361,6 +361,37 @@ def test_cosine_repeated_searches_are_stable(hip, mk):
         assert_same(*hip.LanceDetachedSearchBatch(h, Q, 10), el, ed, ec)
 
 
+@pytest.mark.parametrize("scan", ["copy", "f32", "bf16"])
+@pytest.mark.parametrize("d", [32, 64])
+def test_cosine_row_aux_slot_reuse(hip, mk, d, scan):
+    # regression (root cause of the case above): a tile's stage 0 carries its
+    # row aux into the LDS slot tile-2's epilogue reads; when a tile has fewer
+    # k-stages than the ring (small d) that DMA was released by each wave's
+    # own progress, not the workgroup's, and overwrote row terms slower waves
+    # were still reading.  Append mode (> 65536 rows), many tiles per
+    # workgroup, 80% deleted rows (alpha = +inf in the row aux), 1024 queries.
+    rng = np.random.default_rng(4100 + d)
+    n = 200_000
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Q = rng.standard_normal((1024, d)).astype(np.float32)
+    keep = rng.random(n) < 0.2
+    h = mk(d, "cosine")
+    if scan == "bf16":  # bf16 store: the scan streams the store itself
+        hip.LanceHipSetOption(h, "storage", "bf16")
+    elif scan == "f32":  # f32 store without its bf16 scan copy (32-deep f32 stages)
+        hip.LanceHipSetOption(h, "scan_copy", "off")
+    hip.LanceDetachedAddBatch(h, X, n, d)
+    hip.LanceDetachedDeleteBatch(h, np.nonzero(~keep)[0])
+    Xr = X
+    if scan == "bf16":  # a bf16 store holds the round-to-nearest-even roundings
+        u = X.view(np.uint32).astype(np.uint64)
+        Xr = ((((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16) & 0xFFFFFFFF).astype(np.uint32).view(np.float32)
+    el, ed, ec = c_oracle.flat_search_batch(Xr, Q, 10, "cosine", live=keep, acc64=True, nthreads=16)
+    gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 10)
+    assert not hip.LanceHipLastSearchStats(h)["dense_path"]
+    assert_same(gl, gd, gc, el, ed, ec)
+
+
 # ---------------------------------------------------------------------------
 # one-launch small exact search (<= 8 queries over <= 32768 slots)
 # ---------------------------------------------------------------------------
