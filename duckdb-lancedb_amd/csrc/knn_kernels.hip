@@ -446,13 +446,19 @@ __device__ __forceinline__ void wait_vm(int n) {
 	}
 }
 
-// Lane id through volatile asm: not loop-invariant to the compiler, so values
-// derived from it are recomputed where used instead of hoisted out of the
-// tile loop and kept live across the MFMA loop.
+// Lane id that is not loop-invariant to the compiler, so values derived from
+// it are recomputed where used instead of hoisted out of the tile loop and kept
+// live across the MFMA loop.  The mbcnt instructions are the compiler's own
+// (builtins): it pads their hazards.  They once sat inside the asm string,
+// where nothing is padded: the v_mbcnt could overwrite a VGPR that the tile's
+// last, still executing MFMA was reading as its A operand (register allocation
+// put the lane id there in the cosine kernels), which corrupted one 32 x 32
+// accumulator block now and then — wrong cosine bounds in ~1% of the queries.
+// Only the all-ones mask goes through an (empty) asm statement, as an SGPR.
 __device__ __forceinline__ int lane_id_fresh() {
-	uint32_t ln;
-	asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-	return (int)ln;
+	uint32_t m = 0xFFFFFFFFu;
+	asm volatile("" : "+s"(m));
+	return (int)__builtin_amdgcn_mbcnt_hi(m, __builtin_amdgcn_mbcnt_lo(m, 0u));
 }
 
 template <int METRIC, int MODE, bool XB>
