@@ -111,6 +111,8 @@ def test_c5_ivf_pq_m96_refine_sweep(hip, data, exact):
         # a wider exact re-rank window can only help (the ADC candidates of
         # refine r are a prefix of those of r' > r)
         assert recalls[1] <= recalls[10] + 1e-9 <= recalls[50] + 2e-9
-        assert recalls[50] >= 0.9
+        # measured on MI355X: 0.294 / 0.818 / 0.996 (profiles/r02_c_ivf_params.log)
+        assert recalls[10] >= 0.75
+        assert recalls[50] >= 0.98
     finally:
         hip.LanceFreeDetached(h)
