@@ -277,11 +277,7 @@ struct Index {
 		if (rowaux_l2 || (metric_quirk && metric != METRIC_L2)) HIPCHK(hipMalloc(&na2, (size_t)c * sizeof(float4)));
 		if (n_slots > 0) {
 			HIPCHK(hipMemcpyAsync(nX, X, (size_t)n_slots * ld * xes(), hipMemcpyDeviceToDevice, stream));
-			// blocked scan copy: rows [0, n_slots) live in the first whole
-			// tiles (their padding rows are zero in the old buffer too)
-			if (nXs)
-				HIPCHK(hipMemcpyAsync(nXs, Xs, (size_t)round_up(n_slots, SCAN_BR) * ld * 2, hipMemcpyDeviceToDevice,
-				                      stream));
+			if (nXs) HIPCHK(hipMemcpyAsync(nXs, Xs, (size_t)n_slots * ld * 2, hipMemcpyDeviceToDevice, stream));
 			// row aux is tile-blocked SoA: move whole tile blocks (cap is a
 			// multiple of SCAN_BR, so they exist in the old buffer)
 			const size_t aux_bytes = (size_t)round_up(n_slots, SCAN_BR) * sizeof(float4);
@@ -291,10 +287,7 @@ struct Index {
 		}
 		HIPCHK(hipMemsetAsync(static_cast<uint8_t *>(nX) + (size_t)n_slots * ld * xes(), 0,
 		                      (size_t)(c - n_slots) * ld * xes(), stream));
-		if (nXs) {
-			const size_t kept = (size_t)round_up(n_slots, SCAN_BR) * ld;
-			HIPCHK(hipMemsetAsync(nXs + kept, 0, (size_t)c * ld * 2 - kept * 2, stream));
-		}
+		if (nXs) HIPCHK(hipMemsetAsync(nXs + (size_t)n_slots * ld, 0, (size_t)(c - n_slots) * ld * 2, stream));
 		launch_fill_rowaux(na, n_slots, c, stream);
 		if (na2) launch_fill_rowaux(na2, n_slots, c, stream);
 		HIPCHK(hipStreamSynchronize(stream));
@@ -321,11 +314,12 @@ struct Index {
 		memcpy(&max_ux_l2, &h[3], 4);
 	}
 
-	// scan copy rows [s0, s0+n) = bf16 (RNE) of the f32 rows of X, in the
-	// tile-blocked layout the scan streams (padding columns stay zero)
+	// scan copy rows [s0, s0+n) = bf16 (RNE) of the f32 rows of X (padding
+	// columns stay zero)
 	void fill_scan_copy(int64_t s0, int64_t n, uint16_t *dst) {
 		if (n > 0)
-			launch_rows_to_bf16_blocked(reinterpret_cast<const float *>(xrow(s0)), ld, n, dim, ld, dst, s0, stream);
+			launch_rows_to_bf16(reinterpret_cast<const float *>(xrow(s0)), ld, n, dim, ld, dst + (size_t)s0 * ld,
+			                    stream);
 	}
 
 	// option scan_copy: build or drop the bf16 scan copy of an f32 store
@@ -501,7 +495,8 @@ struct Index {
 		if (Xs) {
 			HIPCHK(hipMalloc(&nXs, (size_t)c * ld * 2));
 			HIPCHK(hipMemsetAsync(nXs, 0, (size_t)c * ld * 2, stream));
-			if (n > 0) launch_rows_to_bf16_blocked(static_cast<const float *>(nX), ld, n, dim, ld, nXs, 0, stream);
+			if (n > 0)
+				launch_rows_to_bf16(static_cast<const float *>(nX), ld, n, dim, ld, nXs, stream);
 			HIPCHK(hipGetLastError());
 		}
 		HIPCHK(hipStreamSynchronize(stream));

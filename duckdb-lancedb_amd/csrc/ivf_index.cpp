@@ -29,8 +29,7 @@ void ivf_free(IvfState *s) { delete s; }
 
 static StoreView store_view(Index *ix) {
 	return StoreView{ix->X,  ix->rowaux, ix->dlabels, ix->n_slots, ix->ld, ix->dim, ix->metric, ix->xbf16 ? 1 : 0,
-	                 ix->Xs ? static_cast<const void *>(ix->Xs) : ix->X, (ix->xbf16 || ix->Xs) ? 1 : 0,
-	                 ix->Xs ? 1 : 0};
+	                 ix->Xs ? static_cast<const void *>(ix->Xs) : ix->X, (ix->xbf16 || ix->Xs) ? 1 : 0};
 }
 
 static int bits_for(int64_t n) {

@@ -37,17 +37,7 @@ struct StoreView {
 	// hold for either: ux covers |x - bf16(x)| with the same RNE rounding.
 	const void *Xscan;
 	int scan_bf16;
-	// Xscan is the tile-blocked bf16 scan copy (scan_block_offset()): each
-	// 64-deep k-stage of a 256-row tile is one contiguous 32 KiB block, so a
-	// scan stage streams sequential memory instead of 256 strided 128-B pieces.
-	// 0: row-major [n][ld] (a bf16 store, or f32 rows).
-	int scan_blocked;
 };
-
-// Element (row r, column e) of the tile-blocked scan copy, in elements:
-// [r / 256][e / 64][r % 256][e % 64].  ld is a multiple of 64, so a tile is
-// 256 * ld elements, as in the row-major layout.
-constexpr int SCAN_BLK_K = 64;
 
 // Per-query constants for the lower-bound epilogue:
 //   LB = alpha + xn*B + ux*A + (s*sc)*S + C      (s = bf16 MFMA dot)
@@ -69,10 +59,6 @@ void launch_rowaux(const void *X, int xbf16, int ld, int dim, int metric, int64_
 // Rounds n f32 rows (stride src_ld) to bf16 (round to nearest even) into
 // dst rows of stride ld, zero-filling columns [dim, ld).
 void launch_rows_to_bf16(const float *src, int64_t src_ld, int64_t n, int dim, int ld, uint16_t *dst, hipStream_t st);
-// Same rounding into the tile-blocked scan copy: source rows [0, n) become
-// rows [row0, row0 + n) of the blocked image at dst (columns [dim, ld) zero).
-void launch_rows_to_bf16_blocked(const float *src, int64_t src_ld, int64_t n, int dim, int ld, uint16_t *dst,
-                                 int64_t row0, hipStream_t st);
 
 // rowaux[from, to) = (+inf, 0, 0, 0): padding rows past the last slot.
 void launch_fill_rowaux(float4 *rowaux, int64_t from, int64_t to, hipStream_t st);

@@ -104,35 +104,6 @@ void launch_rows_to_bf16(const float *src, int64_t src_ld, int64_t n, int dim, i
 	rows_to_bf16_kernel<<<dim3((unsigned)n), dim3(256), 0, st>>>(src, src_ld, n, dim, ld, dst);
 }
 
-// one workgroup per 4 rows; thread = 4 consecutive columns of one row (8-byte
-// stores inside a row's 128-B block of each 64-deep stage)
-__global__ __launch_bounds__(256) void rows_to_bf16_blocked_kernel(const float *__restrict__ src, int64_t src_ld,
-                                                                   int64_t n, int dim, int ld,
-                                                                   uint16_t *__restrict__ dst, int64_t row0) {
-	const int per_row = ld / 4;  // threads per row
-	const int64_t i = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
-	for (int64_t r = i; r < n; r += (int64_t)gridDim.x * 4) {
-		const int64_t gr = row0 + r;
-		uint16_t *tile = dst + (gr / SCAN_BR) * (int64_t)SCAN_BR * ld + (gr % SCAN_BR) * SCAN_BLK_K;
-		for (int c4 = threadIdx.x % 64; c4 < per_row; c4 += 64) {
-			const int e = 4 * c4;
-			uint16_t v[4];
-#pragma unroll
-			for (int j = 0; j < 4; ++j) v[j] = e + j < dim ? bf16_bits(src[r * src_ld + e + j]) : (uint16_t)0;
-			const uint64_t w = (uint64_t)v[0] | ((uint64_t)v[1] << 16) | ((uint64_t)v[2] << 32) | ((uint64_t)v[3] << 48);
-			*reinterpret_cast<uint64_t *>(tile + (int64_t)(e / SCAN_BLK_K) * SCAN_BR * SCAN_BLK_K + e % SCAN_BLK_K) = w;
-		}
-	}
-}
-
-void launch_rows_to_bf16_blocked(const float *src, int64_t src_ld, int64_t n, int dim, int ld, uint16_t *dst,
-                                 int64_t row0, hipStream_t st) {
-	if (n <= 0) return;
-	if (ld % SCAN_BLK_K != 0) throw std::runtime_error("blocked scan copy: ld must be a multiple of 64");
-	const int64_t blocks = std::min<int64_t>((n + 3) / 4, 65536);
-	rows_to_bf16_blocked_kernel<<<dim3((unsigned)blocks), dim3(256), 0, st>>>(src, src_ld, n, dim, ld, dst, row0);
-}
-
 __global__ void fill_rowaux_kernel(float4 *rowaux, int64_t from, int64_t to) {
 	const int64_t i = from + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if (i < to) {
@@ -499,7 +470,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
                                                                float *__restrict__ dense, int64_t ld_out,
                                                                const float *__restrict__ tau,
                                                                uint2 *__restrict__ seg_pool,
-                                                               int *__restrict__ seg_cnt, int seg_cap, int xblk) {
+                                                               int *__restrict__ seg_cnt, int seg_cap) {
 	using C = ScanCfg<XB>;
 	__shared__ __attribute__((aligned(16))) uint8_t smem[C::LDS];
 	unsigned *CNT = reinterpret_cast<unsigned *>(smem + C::RING + RA_BYTES);
@@ -536,15 +507,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 	// next stage to issue and its LDS slot — run in SGPRs and advance by
 	// constants, so a stage's issue costs a handful of scalar instructions.
 	const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
-	// X rows: ld * XE bytes apart (row-major), or XROW (tile-blocked scan
-	// copy: a stage of the tile is one contiguous block of BR rows x XROW)
-	const int xrs = xblk ? C::XROW : ld * C::XE;
-	const int xstage = xblk ? C::XST : C::SK * C::XE;  // bytes between a tile's stages
 	uint32_t xoff[C::XDMA], qoff[C::QDMA];
 #pragma unroll
 	for (int j = 0; j < C::XDMA; ++j) {
 		const int xr = (C::XDMA * w + j) * C::ROWS_PER_DMA + lane / C::XCH;
-		xoff[j] = (uint32_t)(xr * xrs + (C::xswz(xr, lane % C::XCH) << 4));
+		xoff[j] = (uint32_t)(xr * ld * C::XE + (C::xswz(xr, lane % C::XCH) << 4));
 	}
 #pragma unroll
 	for (int j = 0; j < C::QDMA; ++j) {
@@ -579,7 +546,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 			iss_ra += tile_rows_step;
 			iss_q = qbase;
 		} else {
-			iss_xt += xstage;
+			iss_xt += C::SK * C::XE;
 			iss_q += C::SK;
 		}
 	};
@@ -1251,24 +1218,21 @@ static void scan_dispatch_x(const StoreView &s, const QueryView &q, int64_t n_ti
                             hipStream_t st) {
 	dim3 grid((unsigned)scan_grid(n_tiles), (unsigned)(q.nq_pad / BQ));
 	dim3 block(SCAN_THREADS);
-	const int xblk = s.scan_blocked ? 1 : 0;
-	if (xblk && !(XB && ScanCfg<XB>::SK == SCAN_BLK_K))
-		throw std::runtime_error("scan: the blocked scan copy needs 64-deep bf16 stages");
 	switch (s.metric) {
 	case METRIC_L2:
 		scan_kernel<METRIC_L2, MODE, XB><<<grid, block, 0, st>>>(s.Xscan, s.rowaux, s.ld, q.Qb, q.qaux, q.nq, (int)n_tiles,
 		                                                          (int)tile_stride, dense, ld_out, tau, seg_pool,
-		                                                          seg_cnt, seg_cap, xblk);
+		                                                          seg_cnt, seg_cap);
 		break;
 	case METRIC_DOT:
 		scan_kernel<METRIC_DOT, MODE, XB><<<grid, block, 0, st>>>(s.Xscan, s.rowaux, s.ld, q.Qb, q.qaux, q.nq, (int)n_tiles,
 		                                                           (int)tile_stride, dense, ld_out, tau, seg_pool,
-		                                                           seg_cnt, seg_cap, xblk);
+		                                                           seg_cnt, seg_cap);
 		break;
 	default:
 		scan_kernel<METRIC_COSINE, MODE, XB><<<grid, block, 0, st>>>(s.Xscan, s.rowaux, s.ld, q.Qb, q.qaux, q.nq,
 		                                                              (int)n_tiles, (int)tile_stride, dense, ld_out,
-		                                                              tau, seg_pool, seg_cnt, seg_cap, xblk);
+		                                                              tau, seg_pool, seg_cnt, seg_cap);
 		break;
 	}
 }

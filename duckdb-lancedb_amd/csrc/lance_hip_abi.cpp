@@ -49,7 +49,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	const float ma = (metric_quirk && metric != METRIC_L2) ? max_alpha_l2 : max_alpha;
 	const float mu = (metric_quirk && metric != METRIC_L2) ? max_ux_l2 : max_ux;
 	StoreView sv{X, aux, dlabels, n_slots, ld, dim, eff_metric, xbf16 ? 1 : 0,
-	             Xs ? static_cast<const void *>(Xs) : X, (xbf16 || Xs) ? 1 : 0, Xs ? 1 : 0};
+	             Xs ? static_cast<const void *>(Xs) : X, (xbf16 || Xs) ? 1 : 0};
 	if (small_exact && small_exact_fits(n_slots, dim, nq, k)) {
 		// a few queries over a small store (one query per lance_search call):
 		// one launch of exact distances + merge, no bounds, no status readback
