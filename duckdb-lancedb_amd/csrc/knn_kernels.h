@@ -125,6 +125,11 @@ void launch_finalize(const StoreView &s, const uint32_t *cand_slot, const int *c
 // (dead slots -> NaN with all-ones payload so they sort last), labels into vals.
 void launch_exact_all(const StoreView &s, const QueryView &q, int qi, float *keys, int64_t *vals, hipStream_t st);
 
+// Batched exact fallback: keys[i][r] (row stride ld_keys >= n_slots) = exact
+// distance of slot r to query i of q (the value refine computes), +inf for
+// dead / filtered slots; feeds launch_select_dense with tile_stride 1.
+void launch_exact_dense(const StoreView &s, const QueryView &q, float *keys, int64_t ld_keys, hipStream_t st);
+
 // Radix sort (key f32 asc, stable) of n pairs; temp sized by the first call with
 // temp == nullptr.  Returns hipError_t as int.
 int sort_pairs(void *temp, size_t &temp_bytes, const float *keys_in, float *keys_out, const int64_t *vals_in,

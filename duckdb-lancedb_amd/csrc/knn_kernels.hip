@@ -1805,6 +1805,55 @@ static void exact_all_dispatch(const StoreView &s, const QueryView &q, int qi, f
 	}
 }
 
+// Batched exact fallback: one wave per row computes the row's exact distance
+// to each of the nq queries with the same exact_distance() as refine (f64
+// accumulation, identical order), so a key equals the distance refine will
+// report; the row is read from HBM once and from L1/L2 for the other queries.
+// Dead / filtered slots get +inf (select_kernel leaves them out).
+template <int METRIC, typename T>
+__global__ __launch_bounds__(256) void exact_dense_kernel(const T *__restrict__ X, const float4 *__restrict__ rowaux,
+                                                          int64_t n, int ld, int dim, const float *__restrict__ Qf,
+                                                          int nq, float *__restrict__ keys, int64_t ld_keys) {
+	const int lane = threadIdx.x & 63;
+	const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+	if (r >= n) return;
+	const bool dead = reinterpret_cast<const float *>(rowaux)[raix(r, 0)] == F_INF;
+	for (int qi = 0; qi < nq; ++qi) {
+		float d = F_INF;
+		if (!dead) d = exact_distance<METRIC, T>(X + r * ld, Qf + (int64_t)qi * ld, dim, lane);
+		if (lane == 0) keys[(int64_t)qi * ld_keys + r] = d;
+	}
+}
+
+template <typename T>
+static void exact_dense_dispatch(const StoreView &s, const QueryView &q, float *keys, int64_t ld_keys, hipStream_t st) {
+	dim3 grid((unsigned)((s.n_slots + 3) / 4));
+	const T *X = static_cast<const T *>(s.X);
+	switch (s.metric) {
+	case METRIC_L2:
+		exact_dense_kernel<METRIC_L2, T><<<grid, 256, 0, st>>>(X, s.rowaux, s.n_slots, s.ld, s.dim, q.Qf, q.nq, keys,
+		                                                        ld_keys);
+		break;
+	case METRIC_DOT:
+		exact_dense_kernel<METRIC_DOT, T><<<grid, 256, 0, st>>>(X, s.rowaux, s.n_slots, s.ld, s.dim, q.Qf, q.nq, keys,
+		                                                         ld_keys);
+		break;
+	default:
+		exact_dense_kernel<METRIC_COSINE, T><<<grid, 256, 0, st>>>(X, s.rowaux, s.n_slots, s.ld, s.dim, q.Qf, q.nq,
+		                                                            keys, ld_keys);
+		break;
+	}
+}
+
+void launch_exact_dense(const StoreView &s, const QueryView &q, float *keys, int64_t ld_keys, hipStream_t st) {
+	if (s.n_slots <= 0 || q.nq <= 0) return;
+	if (ld_keys < s.n_slots) throw std::runtime_error("exact_dense: key rows shorter than the store");
+	if (s.xbf16)
+		exact_dense_dispatch<uint16_t>(s, q, keys, ld_keys, st);
+	else
+		exact_dense_dispatch<float>(s, q, keys, ld_keys, st);
+}
+
 void launch_exact_all(const StoreView &s, const QueryView &q, int qi, float *keys, int64_t *vals, hipStream_t st) {
 	if (s.n_slots <= 0) return;
 	if (s.xbf16)

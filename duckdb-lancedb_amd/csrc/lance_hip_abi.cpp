@@ -212,10 +212,67 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 			spin_sync(stream);
 		}
 	}
-	// exact fallback for every query whose certificate failed
-	for (int q = 0; q < nq; ++q) {
-		if (!all_fallback && h_cert[q]) continue;
-		last_stats[0] += 1;
+	// exact fallback for every query whose certificate failed: one batched
+	// pass — exact distances of every slot for a group of such queries, then
+	// the k smallest per query by (distance, slot) with the selection the scan
+	// uses (slots ascend with labels, so that is the (distance, label) order),
+	// refine + finalize for the outputs — instead of a full scan and an
+	// N-key radix sort per query.  A query whose selection comes up short of
+	// min(k, live rows) (NaN distances: a zero cosine query) and every query
+	// when k is past the selection's capacity take the per-query sort below.
+	std::vector<int> fbq;
+	for (int q = 0; q < nq; ++q)
+		if (all_fallback || !h_cert[q]) fbq.push_back(q);
+	last_stats[0] += (int64_t)fbq.size();
+	std::vector<int> slow;
+	if (!fbq.empty() && fast_ok) {
+		const int nf = (int)fbq.size();
+		const int nf_pad = (int)round_up(nf, SCAN_BQ);
+		ws.rfq.need(nf);
+		ws.rQf.need((size_t)nf_pad * ld);
+		ws.rQb.need((size_t)nf_pad * ld);
+		ws.rqaux.need(nf_pad);
+		ws.rtau.need(nf);
+		ws.rstat.need((size_t)3 * nf);
+		ws.rL.need((size_t)nf * k);
+		ws.rD.need((size_t)nf * k);
+		ws.rC.need(nf);
+		HIPCHK(hipMemcpyAsync(ws.rfq.p, fbq.data(), (size_t)nf * sizeof(int), hipMemcpyHostToDevice, stream));
+		launch_retry_gather(ws.rfq.p, nf, nf_pad, ld, k, qv, ws.tau.p, dD, ws.rQf.p, ws.rQb.p, ws.rqaux.p, ws.rtau.p,
+		                    ws.rstat.p, stream);
+		// keys of up to FB_GROUP queries at a time, within 1 GiB
+		constexpr int FB_GROUP = 16;
+		const int64_t cols = round_up(n_slots, 4);
+		const int G = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)FB_GROUP, (int64_t)nf,
+		                                                             ((int64_t)1 << 28) / cols}));
+		ws.fb_keys.need((size_t)G * cols);
+		int *cert2 = ws.rstat.p, *cnt2 = ws.rstat.p + nf;
+		for (int g0 = 0; g0 < nf; g0 += G) {
+			const int gq = std::min(G, nf - g0);
+			const QueryView qg{ws.rQf.p + (size_t)g0 * ld, ws.rQb.p + (size_t)g0 * ld, ws.rqaux.p + g0, gq,
+			                   (int)round_up(gq, SCAN_BQ)};
+			launch_exact_dense(sv, qg, ws.fb_keys.p, cols, stream);
+			launch_select_dense(ws.fb_keys.p, cols, n_slots, 1, gq, k, ws.cand_slot.p, cnt2 + g0, ws.cut.p, stream);
+			launch_refine(sv, qg, ws.cand_slot.p, cnt2 + g0, k, ws.cand_dist.p, stream);
+			launch_finalize(sv, ws.cand_slot.p, cnt2 + g0, ws.cand_dist.p, ws.cut.p, gq, k, k, 1, 0, nullptr,
+			                ws.rL.p + (size_t)g0 * k, ws.rD.p + (size_t)g0 * k, ws.rC.p + g0, cert2 + g0, stream);
+		}
+		// exact keys: the selection is the answer whatever the certificate
+		// says about ties at the cut
+		HIPCHK(hipMemsetAsync(cert2, 0x01, (size_t)nf * sizeof(int), stream));
+		launch_retry_scatter(ws.rfq.p, nf, k, ws.rL.p, ws.rD.p, ws.rC.p, cert2, ws.rtau.p, dL, dD, dC, d_cert,
+		                     ws.tau.p, stream);
+		HIPCHK(hipGetLastError());
+		std::vector<int> hc((size_t)nf);
+		HIPCHK(hipMemcpyAsync(hc.data(), ws.rC.p, (size_t)nf * sizeof(int), hipMemcpyDeviceToHost, stream));
+		HIPCHK(hipStreamSynchronize(stream));
+		const int64_t want = std::min<int64_t>(k, live_rows());
+		for (int i = 0; i < nf; ++i)
+			if (hc[(size_t)i] < want) slow.push_back(fbq[(size_t)i]);
+	} else {
+		slow = fbq;
+	}
+	for (int q : slow) {
 		ws.fb_keys.need((size_t)n_slots);
 		ws.fb_keys2.need((size_t)n_slots);
 		ws.fb_vals.need((size_t)n_slots);

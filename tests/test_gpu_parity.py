@@ -279,6 +279,33 @@ def test_duplicates_force_exact_fallback(hip, mk):
     assert st["fallback_queries"] == 2 and st["retried_queries"] == 2
 
 
+@pytest.mark.parametrize("metric", ["l2", "cosine"])
+def test_batched_exact_fallback_many_queries(hip, mk, metric):
+    # 50 vectors each repeated ~1600 times among 100k rows: a query equal to
+    # one of them ties at its nearest distance with ~1600 rows, so no
+    # certificate can hold; the 50 queries (4 groups of the batched fallback)
+    # must come back as the k smallest labels of their duplicates, as the
+    # oracle orders them; one zero query on top (cosine: NaN distances, the
+    # per-query fallback)
+    rng = np.random.default_rng(77)
+    n, d, k = 100_000, 32, 10
+    base = rng.standard_normal((50, d)).astype(np.float32)
+    X = base[rng.integers(0, 50, n)]
+    X[rng.random(n) < 0.2] = rng.standard_normal((1, d)).astype(np.float32)  # another tie group
+    Q = np.concatenate([base, np.zeros((1, d), np.float32)])
+    live = np.ones(n, bool)
+    live[rng.choice(n, 3000, replace=False)] = False
+    h = mk(d, metric)
+    hip.LanceDetachedAddBatch(h, X, n, d)
+    hip.LanceDetachedDeleteBatch(h, np.nonzero(~live)[0])
+    gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, k)
+    st = hip.LanceHipLastSearchStats(h)
+    assert st["fallback_queries"] >= 50, st
+    el, ed, ec = c_oracle.flat_search_batch(X, Q[:50], k, metric, live=live, acc64=True, nthreads=16)
+    assert_same(gl[:50], gd[:50], gc[:50], el, ed, ec)
+    assert gc[50] == k
+
+
 @pytest.mark.parametrize("retry", ["1", "0"])
 def test_overflowed_segment_takes_second_pass(hip, mk, retry):
     # the neighbours of three queries sit packed in tile 1 (rows 256..511),
