@@ -1351,7 +1351,7 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const f
 	__shared__ __attribute__((aligned(16))) uint32_t s_keys[SEL_LDS_KEYS];
 	__shared__ unsigned hist[SEL_BINS];
 	__shared__ unsigned sh[SEL_THREADS / 64];
-	__shared__ unsigned s_digit, s_rem, s_nlt, s_neq, s_minex, s_over;
+	__shared__ unsigned s_digit, s_rem, s_nlt, s_neq, s_minex, s_over, s_heq;
 	const int q = blockIdx.x;
 	const int t = threadIdx.x;
 	if (big && !big[q]) return;  // done by select_small_kernel
@@ -1480,6 +1480,7 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const f
 					if (rem <= c + h) {
 						s_digit = (unsigned)(t * BPT + j);
 						s_rem = rem - c;
+						s_heq = h;  // last pass: entries equal to the M-th smallest key
 						break;
 					}
 					c += h;
@@ -1494,6 +1495,32 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const f
 		const uint32_t T = prefix;                // key of the M-th smallest
 		const unsigned n_lt = (unsigned)M - rem;  // entries strictly below T
 		unsigned my_min = 0xFFFFFFFFu;            // smallest key left out
+		if (dense && s_heq > rem) {
+			// Dense source with ties straddling the M-th place: take the equal
+			// keys in entry order = slot order (one block scan per chunk), so
+			// the selection is the M smallest by (key, slot) — the order the
+			// batched exact fallback relies on (slots ascend with labels).
+			unsigned base = 0;
+			for (int64_t i0 = 0; i0 < n; i0 += SEL_THREADS) {
+				const int64_t i = i0 + t;
+				const uint32_t k = i < n ? (in_lds ? s_keys[i] : fkey(row[i])) : KEY_NAN;
+				if (k < T) {
+					unsigned p = atomicAdd(&s_nlt, 1u);
+					cand_slot[(int64_t)q * M + p] = slot_at(i);
+				} else if (k > T && k < KEY_INF) {
+					my_min = min(my_min, k);
+				}
+				unsigned tot;
+				const unsigned ex = block_excl_scan(k == T ? 1u : 0u, sh, tot);
+				if (k == T) {
+					if (base + ex < rem)
+						cand_slot[(int64_t)q * M + n_lt + base + ex] = slot_at(i);
+					else
+						my_min = min(my_min, k);
+				}
+				base += tot;
+			}
+		} else
 		sel_for_each(in_lds, s_keys, row, n, [&](int64_t i, uint32_t k) {
 			if (k < T) {
 				unsigned p = atomicAdd(&s_nlt, 1u);
