@@ -209,6 +209,7 @@ struct Index {
 	int sample_div = 32;  // sample pass covers ~1/sample_div of the tiles (>= 32 tiles)
 	bool small_exact = true;  // one-launch exact search for <= 8 queries over <= 32768 slots
 	bool defer_sync = false;  // caller synchronizes the stream itself (host-buffer search)
+	bool rscan = true;       // append pass by the register-streamed kernel where it fits (option "rscan")
 	bool retry_pass = true;  // rerun uncertified queries with a tighter tau before the exact fallback
 	int cand_extra = 32;  // refined candidates: max(k * refine_factor, k + max(cand_extra, k))
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};

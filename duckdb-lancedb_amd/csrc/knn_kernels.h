@@ -88,6 +88,13 @@ void launch_scan_dense(const StoreView &s, const QueryView &q, int64_t n_tiles, 
 void launch_scan_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
                         int seg_cap, hipStream_t st);
 
+// The same append pass by the register-streamed kernel (rscan_kernels.hip):
+// rows go HBM -> registers (no LDS stage), one wave per SIMD, 16x16x32 bf16
+// MFMA; identical bounds and outputs.  rscan_fits: row bytes a multiple of 512.
+bool rscan_fits(const StoreView &s);
+void launch_rscan_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
+                         int seg_cap, hipStream_t st);
+
 // Sample scan over row tiles t*tile_stride, t < n_tiles (persistent, scan_grid(n_tiles)
 // workgroups): for every tile, each 64-row quarter appends its smallest lower
 // bound per query, (orderedkey(LB), slot), to the workgroup's segment as

@@ -138,7 +138,10 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		ws.seg_pool.need((size_t)n_seg * nq * seg_cap + (size_t)n_seg * (nq_pad / SCAN_BQ));  // + per-workgroup sink
 		ws.seg_cnt.need((size_t)n_seg * nq);
 		tic(2);
-		launch_scan_append(sv, qv, ws.tau.p, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, stream);
+		if (rscan && rscan_fits(sv))
+			launch_rscan_append(sv, qv, ws.tau.p, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, stream);
+		else
+			launch_scan_append(sv, qv, ws.tau.p, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, stream);
 		tic(3);
 		// 3) top-M by LB, exact refine, certificate
 		launch_select_segments(ws.seg_pool.p, ws.seg_cnt.p, seg_cap, n_seg, ws.tau.p, nq, Mfinal, ws.cand_slot.p,
@@ -199,7 +202,10 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 			ws.seg_pool.need((size_t)n_seg * nf * cap2 + (size_t)n_seg * (nf_pad / SCAN_BQ));
 			ws.seg_cnt.need((size_t)n_seg * nf);
 			int *cert2 = ws.rstat.p, *cnt2 = ws.rstat.p + nf, *pool2 = ws.rstat.p + 2 * nf;
-			launch_scan_append(sv, qv2, ws.rtau.p, ws.seg_pool.p, ws.seg_cnt.p, cap2, stream);
+			if (rscan && rscan_fits(sv))
+				launch_rscan_append(sv, qv2, ws.rtau.p, ws.seg_pool.p, ws.seg_cnt.p, cap2, stream);
+			else
+				launch_scan_append(sv, qv2, ws.rtau.p, ws.seg_pool.p, ws.seg_cnt.p, cap2, stream);
 			launch_select_segments(ws.seg_pool.p, ws.seg_cnt.p, cap2, n_seg, ws.rtau.p, nf, Mfinal, ws.cand_slot.p,
 			                       cnt2, ws.cut.p, pool2, ws.selbig.p, stream);
 			launch_refine(sv, qv2, ws.cand_slot.p, cnt2, Mfinal, ws.cand_dist.p, stream);
@@ -220,9 +226,11 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	// N-key radix sort per query.  A query whose selection comes up short of
 	// min(k, live rows) (NaN distances: a zero cosine query) and every query
 	// when k is past the selection's capacity take the per-query sort below.
+	// (a query with no candidate while live rows exist had NaN bounds — a zero
+	// cosine query — which no threshold keeps: exact fallback too)
 	std::vector<int> fbq;
 	for (int q = 0; q < nq; ++q)
-		if (all_fallback || !h_cert[q]) fbq.push_back(q);
+		if (all_fallback || !h_cert[q] || (ws.h_status[nq + q] == 0 && live_rows() > 0)) fbq.push_back(q);
 	last_stats[0] += (int64_t)fbq.size();
 	std::vector<int> slow;
 	if (!fbq.empty() && fast_ok) {
@@ -1022,6 +1030,10 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 		}
 		if (k == "small_exact") {
 			ix->small_exact = (v == "1" || v == "on" || v == "true");
+			return 0;
+		}
+		if (k == "rscan") {
+			ix->rscan = (v == "1" || v == "on" || v == "true");
 			return 0;
 		}
 		if (k == "retry_pass") {
