@@ -92,6 +92,8 @@ def parse():
     ap.add_argument("--nprobe", type=int, default=None, help="IVF configs: nprobes")
     ap.add_argument("--m", type=int, default=None, help="IVF_PQ: num_sub_vectors")
     ap.add_argument("--refine", type=int, default=None, help="IVF configs: refine_factor")
+    ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra index option (lance_hip_set_option), repeatable, e.g. --opt rscan=0")
     a = ap.parse_args()
     for key, v in CONFIGS[a.config].items():
         if getattr(a, key, None) is None:
@@ -488,6 +490,9 @@ def main():
         lance_hip.LanceHipSetOption(h, "sample_div", str(a.sample_div))
     if a.cand_extra:
         lance_hip.LanceHipSetOption(h, "cand_extra", str(a.cand_extra))
+    for kv in a.opt:
+        key, _, val = kv.partition("=")
+        lance_hip.LanceHipSetOption(h, key, val)
     for lo in range(s0, s1, 1 << 18):
         hi = min(s1, lo + (1 << 18))
         X = gen_rows(lo, hi, D, dev, normalize=a.normalize)
@@ -620,7 +625,7 @@ def main():
                 roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic}
             roof.update({
-                    "kernel": f"scan_kernel<{kname},append,{'bf16' if esz == 2 else 'f32'}>",
+                    "kernel": f"{kt['scan_kernel']}<{kname},append,{'bf16' if esz == 2 else 'f32'}>",
                     "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(bytes_launch),
                     "mfma_tflops": round(mfma_tfs, 1), "mfma_frac": round(mfma_tfs / MFMA_BF16_PEAK_TFS, 4)})
         if a.config == "c2":
@@ -646,7 +651,8 @@ def main():
                     + (", rows and queries L2-normalized; base stored as bf16 (RNE)" if a.config == "c3" else ""),
             "config": {"workload": f"{a.config.upper()} flat {a.metric} {N}x{D} {a.storage} k={K} query-batch={BG}",
                        "n": N, "dim": D, "k": K, "global_batch": BG, "batch_per_gpu": B, "metric": a.metric, "storage": a.storage,
-                       "parallelism": f"rowshard{world}", "scan_copy": a.scan_copy},
+                       "parallelism": f"rowshard{world}", "scan_copy": a.scan_copy,
+                       **({"options": a.opt} if a.opt else {})},
             "recall_at_10": recall,
             "recall_queries": None if recall is None else nr,
             "roofline": roof,

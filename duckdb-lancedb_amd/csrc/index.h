@@ -209,13 +209,14 @@ struct Index {
 	int sample_div = 32;  // sample pass covers ~1/sample_div of the tiles (>= 32 tiles)
 	bool small_exact = true;  // one-launch exact search for <= 8 queries over <= 32768 slots
 	bool defer_sync = false;  // caller synchronizes the stream itself (host-buffer search)
-	bool rscan = true;       // append pass by the register-streamed kernel where it fits (option "rscan")
+	bool rscan = false;      // append pass by the register-streamed kernel where it fits (option "rscan"; off: measured 3x slower, profiles/r02_g_*)
 	bool retry_pass = true;  // rerun uncertified queries with a tighter tau before the exact fallback
 	int cand_extra = 32;  // refined candidates: max(k * refine_factor, k + max(cand_extra, k))
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 	double kt_append_ms = 0.0, kt_dense_ms = 0.0;
 	int64_t kt_append_n = 0, kt_dense_n = 0;
 	int64_t kt_append_rows = 0, kt_append_qpad = 0;
+	int kt_append_kernel = 0;  // 1: the last timed append pass ran rscan_kernel, 0: scan_kernel
 	// IVF list scans (ivf_search): launches, ms, and their algorithmic work:
 	// bytes = rows of every probed list once (row data or codes) + per-pair
 	// tables; pair_rows = sum over (query, list) pairs of the list's rows

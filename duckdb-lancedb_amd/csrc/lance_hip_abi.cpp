@@ -160,6 +160,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		kt_append_n += 1;
 		kt_append_rows = n_slots;
 		kt_append_qpad = nq_pad;
+		kt_append_kernel = (rscan && rscan_fits(sv)) ? 1 : 0;
 	}
 	const int *h_cert = ws.h_status;
 	for (int q = 0; q < nq; ++q) {
@@ -1089,16 +1090,18 @@ int32_t lance_hip_last_search_stats(void *handle, int64_t *out, int32_t n) {
 // out[6] = bytes per element the scan streams (2: bf16 store or scan copy),
 // out[7] = total ms of IVF list-scan launches, out[8] = their count,
 // out[9] = their algorithmic bytes (summed), out[10] = (query, row) pairs
-// they scored (summed), out[11] = total ms of the IVF coarse searches.
+// they scored (summed), out[11] = total ms of the IVF coarse searches,
+// out[12] = 1 if the last timed append pass ran rscan_kernel (0: scan_kernel).
 int32_t lance_hip_kernel_times(void *handle, double *out, int32_t n) {
 	if (!handle || !out) return -1;
 	Index *ix = as_index(handle);
 	std::lock_guard<std::mutex> g(ix->mu);
-	double v[12] = {ix->kt_append_ms, (double)ix->kt_append_n, (double)ix->kt_append_rows,
+	double v[13] = {ix->kt_append_ms, (double)ix->kt_append_n, (double)ix->kt_append_rows,
 		               (double)ix->kt_append_qpad, ix->kt_dense_ms, (double)ix->kt_dense_n,
 		               (ix->xbf16 || ix->Xs) ? 2.0 : 4.0, ix->kt_ivf_ms, (double)ix->kt_ivf_n,
-		               ix->kt_ivf_bytes, ix->kt_ivf_pair_rows, ix->kt_ivf_coarse_ms};
-		for (int32_t i = 0; i < n && i < 12; ++i) out[i] = v[i];
+		               ix->kt_ivf_bytes, ix->kt_ivf_pair_rows, ix->kt_ivf_coarse_ms,
+		               (double)ix->kt_append_kernel};
+	for (int32_t i = 0; i < n && i < 13; ++i) out[i] = v[i];
 	return 0;
 }
 

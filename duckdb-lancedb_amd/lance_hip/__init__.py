@@ -412,12 +412,13 @@ def LanceHipLastSearchStats(handle) -> dict:
 
 
 def LanceHipKernelTimes(handle) -> dict:
-    out = np.zeros(12, np.float64)
-    lib().lance_hip_kernel_times(handle, out.ctypes.data, 12)
+    out = np.zeros(13, np.float64)
+    lib().lance_hip_kernel_times(handle, out.ctypes.data, 13)
     return {"scan_ms_total": float(out[0]), "scan_launches": int(out[1]), "scan_rows": int(out[2]),
             "scan_qpad": int(out[3]), "dense_ms_total": float(out[4]), "dense_launches": int(out[5]),
             "scan_elem_bytes": int(out[6]), "ivf_scan_ms_total": float(out[7]), "ivf_scan_launches": int(out[8]),
-            "ivf_scan_bytes": float(out[9]), "ivf_pair_rows": float(out[10]), "ivf_coarse_ms_total": float(out[11])}
+            "ivf_scan_bytes": float(out[9]), "ivf_pair_rows": float(out[10]), "ivf_coarse_ms_total": float(out[11]),
+            "scan_kernel": "rscan_kernel" if out[12] == 1 else "scan_kernel"}
 
 
 IVF_TYPES = {-1: None, 0: "ivf_flat", 1: "ivf_pq"}

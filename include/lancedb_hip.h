@@ -220,7 +220,9 @@ int32_t lance_hip_last_search_stats(void *handle, int64_t *out, int32_t n);
  * (2 with a bf16 store or scan copy, else 4), out[7] total ms of IVF list-scan
  * launches, out[8] their count, out[9] their algorithmic bytes (every probed
  * list's rows or codes once + each query's PQ table, summed), out[10] (query, row)
- * pairs scored (summed), out[11] total ms of the IVF coarse searches.
+ * pairs scored (summed), out[11] total ms of the IVF coarse searches, out[12]
+ * 1 if the last timed threshold scan ran the register-streamed kernel (option
+ * "rscan"), 0 for the LDS-staged one.
  * Returns 0 or -1. */
 int32_t lance_hip_kernel_times(void *handle, double *out, int32_t n);
 
