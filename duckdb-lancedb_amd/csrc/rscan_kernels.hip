@@ -7,46 +7,49 @@
 // the workgroup's segment of the query when LB <= tau[q].  What differs is how
 // the base reaches the matrix cores.  The LDS-staged scan_kernel holds one
 // 32 KiB stage of rows in flight per CU (its ring shares LDS with the query
-// stages), which measured as the limit: a bare DMA skeleton of that ring
-// streams at 4.8 (bf16) / 5.3 (f32) TB/s, below the 70 % target, before any
-// MFMA runs (profiles/r02_f_ablation.log).  Here the rows never touch LDS:
+// stages).  Here the rows never touch LDS:
 //
-//   * a workgroup is 4 waves, one per SIMD (512 registers each); a wave owns
-//     64 rows x 256 queries of the 256 x 256 tile: 4 x 16 blocks of
-//     v_mfma_f32_16x16x32_bf16, 256 accumulator registers;
-//   * each wave loads its own rows straight into a register ring (global
-//     loads, 4 windows of 128 B per row; 3 windows = 96 KiB per CU in flight
-//     ahead of the one being multiplied): lane 16g + r of a 16-row block reads
-//     bytes 16g and 64 + 16g of the row's window, so one instruction covers 16
-//     rows x 64 contiguous bytes;
-//   * f32 rows are rounded to bf16 in registers; the window's 32 k values sit
-//     in the lane in the order {4g..4g+3, 16+4g..16+4g+3}, and the query side
-//     is staged in LDS in that same k order (a permutation of the dot
-//     product's terms, exact either way); bf16 rows (scan copy or bf16 store)
-//     are 64-deep windows in natural order, two k-steps;
-//   * queries (L2-resident, 16 / 32 KiB per window) go through a two-slot LDS
-//     image, loaded one window ahead and written behind each window's MFMAs,
-//     one barrier per window; the tile's row terms likewise (written during
-//     the tile's second window, after every wave has left the previous tile's
-//     epilogue).
-// Every load is an ordinary compiler-visible load: no asm, so the compiler
-// counts and pads everything.  Restricted to stores whose row stride is a
-// multiple of 4 windows (ld % 128 == 0 for f32, % 256 for bf16): the register
-// ring is unrolled by 4 and a tile ends on a ring boundary.
+//   * a workgroup is 4 MFMA waves + 4 loader waves (two waves per SIMD, 256
+//     registers each); an MFMA wave owns 32 rows x 256 queries of the 128 x 256
+//     tile: 2 x 16 blocks of v_mfma_f32_16x16x32_bf16, 128 accumulators;
+//   * each MFMA wave loads its own rows straight into a 4-window register ring
+//     (global loads, windows of 128 B per row; 3 windows = 48 KiB per CU in
+//     flight ahead of the one being multiplied); f32 rows are rounded to bf16
+//     in registers;
+//   * the loader waves stream the queries' windows (L2-resident, 16 / 32 KiB
+//     each) into a 4-slot LDS image by LDS-DMA, three windows ahead, and the
+//     next tile's row terms; one barrier per window.  vmcnt is per wave, so
+//     the MFMA waves' row loads are never drained by a query load (the first
+//     version loaded the queries in the MFMA waves, behind the row loads, and
+//     every window waited for the whole ring: 3x slower, profiles/r02_g_*).
+// Restricted to stores whose row stride is a multiple of 4 windows (ld % 128
+// == 0 for f32, % 256 for bf16): the ring is unrolled by 4 and a tile ends on
+// a ring boundary.
 #include "device_common.h"
 
 #include <stdexcept>
+
+// Development-only timing ablations (results are wrong when set): only an
+// ablation build (tools/rs_ablate.sh, -DLHIP_ABLATION_BUILD) may turn them on.
+#if !defined(LHIP_ABLATION_BUILD) && (defined(LHIP_RS_ABL_NO_QDMA) || defined(LHIP_RS_ABL_NO_MFMA) || \
+                                      defined(LHIP_RS_ABL_NO_EPI) || defined(LHIP_RS_ABL_NO_XLOAD))
+#error "rscan ablation switches are for ablation builds only"
+#endif
 #include <type_traits>
 
 namespace lhip {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int RS_THREADS = 256;  // 4 waves, one per SIMD
-constexpr int RS_BR = 128;       // rows per tile: 32 per wave (2 blocks of 16)
-constexpr int RS_RB = RS_BR / 64;  // 16-row blocks per wave
-constexpr int RS_WIN = 128;      // bytes of each row per window
-constexpr int RS_WLIST = 256;    // survivor list entries per wave
+constexpr int RS_MW = 8;                 // MFMA waves (two per SIMD)
+constexpr int RS_NL = 4;                 // loader waves (one per SIMD)
+constexpr int RS_THREADS = 64 * (RS_MW + RS_NL);
+constexpr int RS_BR = 128;               // rows per tile
+constexpr int RS_WR = RS_BR / RS_MW;     // rows per MFMA wave: 16
+constexpr int RS_RB = RS_WR / 16;        // 16-row blocks per MFMA wave
+constexpr int RS_WIN = 128;              // bytes of each row per window
+constexpr int RS_NQS = 4;                // query image slots: window v+3 streams in while v is multiplied
+constexpr int RS_WLIST = 256;            // survivor list entries per MFMA wave
 constexpr int RS_FLUSH_AT = 192;
 
 template <bool XB>
@@ -55,18 +58,19 @@ struct RsCfg {
 	static constexpr int KW = RS_WIN / XE;       // k per window: 64 / 32
 	static constexpr int KS = KW / 32;           // 16x16x32 k-steps per window: 2 / 1
 	static constexpr int QW = KW * 2;            // bytes of one query per window (bf16): 128 / 64
-	static constexpr int QCH = QW / 16;          // 16-B chunks per query and window: 8 / 4
 	static constexpr int QSLOT = SCAN_BQ * QW;   // 32 / 16 KiB
+	static constexpr int QNI = QSLOT / 1024 / RS_NL;  // 1-KiB DMA pieces per loader wave and window: 8 / 4
 	static constexpr int RA_SLOT = RS_BR * 16;   // 2 KiB of row terms per tile
-	static constexpr int OFF_RA = 2 * QSLOT;
+	static constexpr int OFF_RA = RS_NQS * QSLOT;
 	static constexpr int OFF_QA = OFF_RA + 2 * RA_SLOT;
 	static constexpr int OFF_TAU = OFF_QA + SCAN_BQ * 16;
 	static constexpr int OFF_CNT = OFF_TAU + SCAN_BQ * 4;
 	static constexpr int OFF_LIST = OFF_CNT + SCAN_BQ * 4;
-	static constexpr int LDS = OFF_LIST + 4 * RS_WLIST * 8;
+	static constexpr int LDS = OFF_LIST + RS_MW * RS_WLIST * 8;
 	static_assert(LDS <= 160 * 1024, "LDS budget");
-	// physical 16-B chunk of chunk c of query row q: conflict-free
-	// ds_read_b128 over each 16-lane group (16 queries, one chunk each)
+	static_assert(QSLOT % (1024 * RS_NL) == 0, "query slot in whole DMA pieces");
+	// physical 16-B chunk of chunk c of query row q (an involution): conflict-
+	// free ds_read_b128 over each 16-lane group (16 queries, one chunk each)
 	__device__ static __forceinline__ int qswz(int q, int c) {
 		return QW == 128 ? c ^ ((q >> 1) & 7) : c ^ ((q >> 2) & 3);
 	}
@@ -92,6 +96,24 @@ __device__ __forceinline__ int rs_lane_fresh() {
 	return (int)__builtin_amdgcn_mbcnt_hi(m, __builtin_amdgcn_mbcnt_lo(m, 0u));
 }
 
+// One global_load_lds_dwordx4 (64 lanes x 16 B, lane-linear at the
+// wave-uniform LDS byte address in M0), issued only by the loader waves.
+// Inline asm: the compiler does not see the LDS write in flight, so it puts
+// no vmcnt(0) in front of the MFMA waves' ds_reads or the barriers; ordering is
+// the loader's counted vmcnt + the step barrier.
+__device__ __forceinline__ void rs_dma16(const void *sbase, uint32_t voff, uint32_t lds_addr) {
+	const uint64_t b = (uint64_t)(uintptr_t)sbase;
+	const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+	const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32));
+	const uint64_t ub = ((uint64_t)hi << 32) | (uint64_t)lo;
+	asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds_addr), "v"(voff), "s"(ub) : "memory", "m0");
+}
+
+template <int N>
+__device__ __forceinline__ void rs_wait_vm() {
+	asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 template <int METRIC>
 __device__ __forceinline__ float rs_lower_bound(float s, float4 ra, float4 qa) {
 	// LB = alpha + xn*B + ux*A + (s*sc)*S + C  (scan_kernel's lower_bound)
@@ -102,6 +124,18 @@ __device__ __forceinline__ float rs_lower_bound(float s, float4 ra, float4 qa) {
 	return v + qa.w;
 }
 
+// Workgroup = 4 MFMA waves + 4 loader waves (two waves per SIMD).  Step v of
+// the workgroup = window v of its row stream (window v % S of tile v / S):
+//   MFMA wave: [tile start: accumulators <- row/query bound terms]; issue the
+//              global loads of its 32 rows' window v+R-1 into the register
+//              ring; multiply window v (registers) x the queries' window v
+//              (LDS slot v % NQS); barrier; [tile end: epilogue];
+//   loader wave: LDS-DMA the queries' window v+NQS-1 into slot (v-1) % NQS
+//              (read by the MFMA waves in step v-1, finished at its barrier)
+//              and, at window 1 of a tile, the next tile's row terms; wait
+//              (its own vmcnt) for window v+1's pieces; barrier.
+// vmcnt is per wave, so the MFMA waves' row ring never waits for a query
+// load: the row loads of a window are waited for only where it is multiplied.
 template <int METRIC, bool XB, int R>
 __global__ __launch_bounds__(RS_THREADS, 1) void rscan_kernel(const uint8_t *__restrict__ X,
                                                               const float4 *__restrict__ rowaux, int ld,
@@ -122,22 +156,91 @@ __global__ __launch_bounds__(RS_THREADS, 1) void rscan_kernel(const uint8_t *__r
 	const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
 	const int q0 = blockIdx.y * SCAN_BQ;
 	const int64_t rowb = (int64_t)ld * C::XE;      // bytes per row
-	const int S = (int)(rowb / RS_WIN);            // windows per tile (multiple of R)
+	const int S = (int)(rowb / RS_WIN);            // windows per tile (multiple of R, >= 4)
 	const int my_tiles = (n_tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
 	const int G = my_tiles * S;                    // windows of this workgroup
 	auto tile_row0 = [&](int t) __attribute__((always_inline)) {
 		return ((int64_t)blockIdx.x + (int64_t)t * gridDim.x) * RS_BR;
 	};
+	const uint32_t smem_base = (uint32_t)(uintptr_t)smem;
 
-	QA[tid] = qaux[q0 + tid];
-	TAU[tid] = (q0 + tid < nq) ? tau[q0 + tid] : -F_INF;
-	CNT[tid] = 0u;
+	if (tid < SCAN_BQ) {
+		QA[tid] = qaux[q0 + tid];
+		TAU[tid] = (q0 + tid < nq) ? tau[q0 + tid] : -F_INF;
+		CNT[tid] = 0u;
+	}
 
-	// ---- row stream: window v of this workgroup = window v % S of its tile
-	// v / S.  Lane 16g + r of row block b holds row 32w + 16b + r, bytes
-	// [16g, 16g+16) and [64+16g, 64+16g+16) of the window.
+	if (w >= RS_MW) {
+		// ================= loader waves =================
+		const int lw = w - RS_MW;
+		const uint16_t *qbase = Qb + (int64_t)q0 * ld;
+		// piece i of this wave: bytes [1024 (lw QNI + i), +1024) of the slot
+		// image; lane l's 16 B = physical chunk of query (off / QW)
+		uint32_t qoff[C::QNI];
+#pragma unroll
+		for (int i = 0; i < C::QNI; ++i) {
+			const int off = 1024 * (lw * C::QNI + i) + 16 * lane;
+			const int q = off / C::QW, pc = (off % C::QW) / 16;
+			qoff[i] = (uint32_t)(q * ld * 2) + 16u * (uint32_t)C::qswz(q, pc);  // chunk qswz(q, pc) of row q
+		}
+		auto dma_q = [&](int v) __attribute__((always_inline)) {
+#ifdef LHIP_RS_ABL_NO_QDMA
+			return;
+#endif
+			const int s = v % S, slot = v % RS_NQS;
+#pragma unroll
+			for (int i = 0; i < C::QNI; ++i)
+				rs_dma16(qbase, qoff[i] + (uint32_t)(s * C::QW),
+				         smem_base + (uint32_t)(slot * C::QSLOT + 1024 * (lw * C::QNI + i)));
+		};
+		// row terms of tile t: term 2 lw + (lane >> 5), rows 4 (lane & 31) .. +3
+		// (loader waves 0 and 1, one piece each)
+		auto dma_ra = [&](int t) __attribute__((always_inline)) {
+			const int64_t r0 = tile_row0(t);
+			const uint32_t off = (uint32_t)(raix(r0, 2 * lw + (lane >> 5)) - raix(r0 & ~(int64_t)255, 0)) * 4u +
+			                     16u * (uint32_t)(lane & 31);
+			rs_dma16(reinterpret_cast<const float *>(rowaux) + raix(r0 & ~(int64_t)255, 0), off,
+			         smem_base + (uint32_t)(C::OFF_RA + (t & 1) * C::RA_SLOT + 1024 * lw));
+		};
+		// prologue: windows 0 .. NQS-2 and tile 0's row terms, all landed
+		for (int v = 0; v < RS_NQS - 1 && v < G; ++v) dma_q(v);
+		if (lw < 2) dma_ra(0);
+		rs_wait_vm<0>();
+		__syncthreads();
+		int cur_s = 0, cur_t = 0;
+		for (int v = 0; v < G; ++v) {
+			const bool ra_now = cur_s == 1 && cur_t + 1 < my_tiles && lw < 2;
+			if (ra_now) dma_ra(cur_t + 1);
+			const bool issued = v + RS_NQS - 1 < G;
+			if (issued) dma_q(v + RS_NQS - 1);
+			// window v+1's pieces were issued in step v+2-NQS; younger: the
+			// pieces of steps v+3-NQS .. v (NQS-2 windows) and a row-term
+			// piece issued in one of those steps (cur_s in 1 .. NQS-2)
+			if (!issued || v + 1 >= G) {
+				rs_wait_vm<0>();
+			} else {
+				static_assert(RS_NQS == 4, "vmcnt immediates below assume 4 slots");
+				const bool ra_young = lw < 2 && (cur_s == 1 || cur_s == 2) && cur_t + 1 < my_tiles;
+				if (ra_young) rs_wait_vm<2 * C::QNI + 1>();
+				else rs_wait_vm<2 * C::QNI>();
+			}
+			__syncthreads();
+			if (++cur_s == S) {
+				cur_s = 0;
+				++cur_t;
+			}
+		}
+		__syncthreads();  // the MFMA waves' final counter barrier
+		return;
+	}
+
+	// ================= MFMA waves =================
+	// row stream: lane 16g + r of row block b holds row 32w + 16b + r: bf16
+	// rows bytes [16g, +16) and [64 + 16g, +16) of the window (k 8g.. and
+	// 32 + 8g.., one 16x16x32 k-step each); f32 rows bytes [32g, +32) (k 8g..
+	// 8g+7, one k-step)
 	const int gq = lane >> 4, rr = lane & 15;
-	const uint32_t xlane = (uint32_t)((32 * w + rr) * rowb + 16 * gq);
+	const uint32_t xlane = (uint32_t)((RS_WR * w + rr) * rowb + (XB ? 16 : 32) * gq);
 	const int64_t tile_bytes = (int64_t)RS_BR * rowb;
 	const int64_t tile_step = (int64_t)gridDim.x * tile_bytes;
 	const uint8_t *x_tile = X + (int64_t)blockIdx.x * tile_bytes;  // tile of the next window to load
@@ -151,57 +254,17 @@ __global__ __launch_bounds__(RS_THREADS, 1) void rscan_kernel(const uint8_t *__r
 		for (int rb = 0; rb < RS_RB; ++rb)
 #pragma unroll
 			for (int j = 0; j < 2; ++j)
-				dst[2 * rb + j] = *reinterpret_cast<const float4 *>(p + (int64_t)rb * 16 * rowb + j * 64);
+				dst[2 * rb + j] = *reinterpret_cast<const float4 *>(p + (int64_t)rb * 16 * rowb + j * (XB ? 64 : 16));
 		if (live && ++x_s == S) {
 			x_s = 0;
 			x_tile += tile_step;
 		}
 	};
 
-	// ---- query stream: thread t stages query t of the tile, window s
-	const uint16_t *qrow = Qb + (int64_t)(q0 + tid) * ld;
-	uint4 qst[C::QCH];
-	auto load_q = [&](int s) __attribute__((always_inline)) {
-		const uint4 *src = reinterpret_cast<const uint4 *>(qrow + (int64_t)s * C::KW);
-#pragma unroll
-		for (int c = 0; c < C::QCH; ++c) qst[c] = src[c];
-	};
-	auto store_q = [&](int slot) __attribute__((always_inline)) {
-		uint8_t *dst = smem + slot * C::QSLOT + tid * C::QW;
-		if (XB) {
-#pragma unroll
-			for (int c = 0; c < C::QCH; ++c) *reinterpret_cast<uint4 *>(dst + C::qswz(tid, c) * 16) = qst[c];
-		} else {
-			// f32 rows: lane group g multiplies k {4g..4g+3, 16+4g..16+4g+3}
-			// (see load_x): chunk g of the image holds those 8 values
-			*reinterpret_cast<uint4 *>(dst + C::qswz(tid, 0) * 16) = make_uint4(qst[0].x, qst[0].y, qst[2].x, qst[2].y);
-			*reinterpret_cast<uint4 *>(dst + C::qswz(tid, 1) * 16) = make_uint4(qst[0].z, qst[0].w, qst[2].z, qst[2].w);
-			*reinterpret_cast<uint4 *>(dst + C::qswz(tid, 2) * 16) = make_uint4(qst[1].x, qst[1].y, qst[3].x, qst[3].y);
-			*reinterpret_cast<uint4 *>(dst + C::qswz(tid, 3) * 16) = make_uint4(qst[1].z, qst[1].w, qst[3].z, qst[3].w);
-		}
-	};
-	// ---- row terms of a tile: the 128 rows' four SoA runs of the row aux
-	// block (raix(): 256-row blocks) -> LDS [term][128 rows]; thread t
-	// copies 8 B of term t / 64
-	float2 rast;
-	auto load_ra = [&](int t) __attribute__((always_inline)) {
-		const int64_t r = tile_row0(t) + 2 * (tid & 63);
-		rast = *reinterpret_cast<const float2 *>(reinterpret_cast<const float *>(rowaux) + raix(r, tid >> 6));
-	};
-	auto store_ra = [&](int t) __attribute__((always_inline)) {
-		reinterpret_cast<float2 *>(smem + C::OFF_RA + (t & 1) * C::RA_SLOT)[tid] = rast;
-	};
-
-	// ---- prologue: rows of windows 0 .. R-2 in flight, queries of window 0
-	// and the first tile's row terms in LDS
 	static_for<0, R - 1>([&](auto I) __attribute__((always_inline)) {
 		load_x(xr[decltype(I)::value], decltype(I)::value < G);
 	});
-	load_q(0);
-	load_ra(0);
-	store_q(0);
-	store_ra(0);
-	__syncthreads();
+	__syncthreads();  // prologue: query windows, row terms, QA / TAU / CNT
 
 	f32x4 acc[RS_RB][16];
 	auto init_acc = [&](int t) __attribute__((always_inline)) {
@@ -218,7 +281,7 @@ __global__ __launch_bounds__(RS_THREADS, 1) void rscan_kernel(const uint8_t *__r
 		float av[RS_RB];
 #pragma unroll
 		for (int rb = 0; rb < RS_RB; ++rb) {
-			const int r = 32 * w + 16 * rb + rr;
+			const int r = RS_WR * w + 16 * rb + rr;
 			av[rb] = gq == 0 ? RAs[RS_BR + r] : gq == 1 ? RAs[2 * RS_BR + r] : gq == 2 ? RAs[r] : 1.0f;
 		}
 		const f32x4 z = {0.f, 0.f, 0.f, 0.f};
@@ -256,7 +319,7 @@ __global__ __launch_bounds__(RS_THREADS, 1) void rscan_kernel(const uint8_t *__r
 #pragma unroll
 			for (int qb = 0; qb < 16; ++qb) {
 				const int q = 16 * qb + rr;
-				const int ch = XB ? 4 * ks + gq : gq;
+				const int ch = 4 * ks + gq;
 				const bf16x8 b = *reinterpret_cast<const bf16x8 *>(qs + q * C::QW + C::qswz(q, ch) * 16);
 #pragma unroll
 				for (int rb = 0; rb < RS_RB; ++rb)
@@ -264,7 +327,6 @@ __global__ __launch_bounds__(RS_THREADS, 1) void rscan_kernel(const uint8_t *__r
 			}
 		}
 	};
-
 	// ---- survivors: per-wave LDS list of (raw LB bits, q << 24 | row << 16 | tile)
 	uint2 *wlist = reinterpret_cast<uint2 *>(smem + C::OFF_LIST) + w * RS_WLIST;
 	int n_list = 0;
@@ -306,7 +368,7 @@ __global__ __launch_bounds__(RS_THREADS, 1) void rscan_kernel(const uint8_t *__r
 			}
 			static_for<0, RS_RB>([&](auto RB) __attribute__((always_inline)) {
 				constexpr int rb = decltype(RB)::value;
-				const int r0 = 32 * w + 16 * rb + 4 * gq;  // tile rows r0 .. r0+3 of this lane
+				const int r0 = RS_WR * w + 16 * rb + 4 * gq;  // tile rows r0 .. r0+3 of this lane
 				float l[4][4];                           // [row][query]
 				if (FOLD) {
 #pragma unroll
@@ -392,17 +454,24 @@ __global__ __launch_bounds__(RS_THREADS, 1) void rscan_kernel(const uint8_t *__r
 		constexpr int SL = decltype(SLOT)::value;
 		const int v = cur_t * S + cur_s;
 		if (SL == 0 && cur_s == 0) init_acc(cur_t);
-		load_x(xr[(SL + R - 1) % R], v + R - 1 < G);        // window v+R-1
-		const bool more = v + 1 < G;
-		if (more) load_q(cur_s + 1 == S ? 0 : cur_s + 1);   // window v+1's queries
-		if (SL == 0 && cur_s == 0 && cur_t + 1 < my_tiles) load_ra(cur_t + 1);
-		mma(xr[SL], v & 1);
-		if (more) store_q((v + 1) & 1);
-		if (SL == 1 && cur_s == 1 && cur_t + 1 < my_tiles) store_ra(cur_t + 1);  // every wave is past tile cur_t-1's epilogue
+#ifndef LHIP_RS_ABL_NO_XLOAD
+		load_x(xr[(SL + R - 1) % R], v + R - 1 < G);  // window v+R-1
+#endif
+#ifndef LHIP_RS_ABL_NO_MFMA
+		mma(xr[SL], v % RS_NQS);
+#else
+#pragma unroll
+		for (int j = 0; j < 2 * RS_RB; ++j) asm volatile("" ::"v"(xr[SL][j].x));
+#endif
 		__syncthreads();
 		++cur_s;
 		if (SL == R - 1 && cur_s == S) {
+#ifndef LHIP_RS_ABL_NO_EPI
 			epilogue(cur_t);
+#else
+#pragma unroll
+			for (int j = 0; j < 16; ++j) asm volatile("" ::"v"(acc[0][j][0]));
+#endif
 			cur_s = 0;
 			++cur_t;
 		}
@@ -414,14 +483,15 @@ __global__ __launch_bounds__(RS_THREADS, 1) void rscan_kernel(const uint8_t *__r
 	if (q0 + tid < nq) seg_cnt[(int64_t)blockIdx.x * nq + q0 + tid] = (int)CNT[tid];
 }
 
-// ring depth for a store: the first of 6 / 8 / 4 windows dividing the
-// windows of a row (0: the register-streamed scan does not apply)
+// ring depth for a store (0: the register-streamed scan does not apply)
 static int rscan_ring(const StoreView &s) {
 	const int64_t rowb = (int64_t)s.ld * (s.scan_bf16 ? 2 : 4);
 	if (rowb % RS_WIN != 0) return 0;
 	const int64_t S = rowb / RS_WIN;
-	for (int r : {6, 8, 4})  // 8 measured a few register spills (f32)
-		if (S % r == 0) return r;
+	// cosine keeps per-row scale terms live through the epilogue: deeper rings
+	// spill at the 168-register budget of three waves per SIMD
+	for (int r : {8, 6, 4})
+		if (S % r == 0 && (r == 4 || s.metric != METRIC_COSINE)) return r;
 	return 0;
 }
 
