@@ -58,7 +58,7 @@ CONFIGS = {
     "c4": dict(n=12_500_000, dim=768, k=10, batch=256, metric="l2", storage="f32", normalize=False,
                index_type="ivf_flat", nlist=4096, nprobe=64, m=0, refine=1),
     "c5": dict(n=12_500_000, dim=768, k=10, batch=256, metric="l2", storage="f32", normalize=False,
-               index_type="ivf_pq", nlist=4096, nprobe=64, m=96, refine=10),
+               index_type="ivf_pq", nlist=4096, nprobe=64, m=96, refine=10, pq_query="fp8", pq_scan="fast"),
 }
 # clustered synthetic data of the IVF configs: NCENT Gaussian clusters, centers
 # N(0, 1) per dim (seed CENT_SEED), rows = center + SIGMA * N(0, 1)
@@ -92,14 +92,20 @@ def parse():
     ap.add_argument("--nprobe", type=int, default=None, help="IVF configs: nprobes")
     ap.add_argument("--m", type=int, default=None, help="IVF_PQ: num_sub_vectors")
     ap.add_argument("--refine", type=int, default=None, help="IVF configs: refine_factor")
+    ap.add_argument("--pq-query", dest="pq_query", choices=["fp8", "f32"], default=None,
+                    help="IVF_PQ: ADC tables from fp8 (e4m3) or f32 queries (index option pq_query)")
+    ap.add_argument("--pq-scan", dest="pq_scan", choices=["fast", "exact_lut"], default=None,
+                    help="IVF_PQ: list-major 8-bit-LUT scan or the f32-LUT query-major scan (option pq_scan)")
+    ap.add_argument("--refine-sweep", default="1,10,50", help="IVF_PQ: refine factors of the recall sweep")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="extra index option (lance_hip_set_option), repeatable, e.g. --opt rscan=0")
     a = ap.parse_args()
     for key, v in CONFIGS[a.config].items():
         if getattr(a, key, None) is None:
             setattr(a, key, v)
-    if not hasattr(a, "index_type"):
-        a.index_type = None
+    for key in ("index_type", "pq_query", "pq_scan"):
+        if not hasattr(a, key) or getattr(a, key) is None:
+            setattr(a, key, None)
     return a
 
 
@@ -244,6 +250,12 @@ def main_ivf(a):
     lance_hip.LanceHipSetOption(h, "scan_copy", "off")
     lance_hip.LanceHipSetOption(h, "reserve_rows", str(N))
     lance_hip.LanceHipSetOption(h, "index_type", a.index_type)
+    if a.index_type == "ivf_pq":
+        lance_hip.LanceHipSetOption(h, "pq_query", a.pq_query or "f32")
+        lance_hip.LanceHipSetOption(h, "pq_scan", a.pq_scan or "fast")
+    for kv in a.opt:
+        key, _, val = kv.partition("=")
+        lance_hip.LanceHipSetOption(h, key, val)
     centers = cluster_centers(D, dev)
     t_gen = time.perf_counter()
     for lo in range(s0, s0 + N, 1 << 18):
@@ -312,7 +324,10 @@ def main_ivf(a):
     lance_hip.LanceHipSetOption(h, "time_kernels", "0")
     res_l = res[0].cpu().numpy()
 
+    # the list-major 8-bit-LUT scan runs for m <= 96 and k * refine <= 512 (ivf.h FQ_MAX_M / FQ_MAX_KK)
+    fast_pq = a.index_type == "ivf_pq" and (a.pq_scan or "fast") == "fast" and a.m <= 96 and K * a.refine <= 512
     recall = cpu = None
+    recall_sweep = {}
     if rank == 0 and world == 1 and not a.no_recall:
         from oracle import c_oracle, flat_knn, ivf
 
@@ -325,6 +340,18 @@ def main_ivf(a):
         nthreads = cpu_threads(a)
         el, _, _ = c_oracle.flat_search_batch(Xh, Qh[:nr], K, a.metric, acc64=True, nthreads=nthreads)
         recall = flat_knn.recall_at_k(res_l[:nr], el, min(10, K))
+        if a.index_type == "ivf_pq":
+            # recall@10 against the refine factor (the exact re-rank window), same batch
+            for rf in [int(x) for x in a.refine_sweep.split(",") if x]:
+                sl = torch.empty((BG, K), dtype=torch.int64, device=dev)
+                sd = torch.empty((BG, K), dtype=torch.float32, device=dev)
+                sc = torch.empty((BG,), dtype=torch.int32, device=dev)
+                r = L.lance_hip_search_batch_device(h, Q.data_ptr(), BG, D, K, a.nprobe, rf, sl.data_ptr(),
+                                                    sd.data_ptr(), sc.data_ptr(), e, 2048)
+                if r < 0:
+                    raise RuntimeError(e.value.decode())
+                torch.cuda.synchronize()
+                recall_sweep[str(rf)] = flat_knn.recall_at_k(sl.cpu().numpy()[:nr], el, min(10, K))
         if not a.no_cpu_baseline:
             # the same IVF search on the host (oracle/flat_knn.c's IVF port over the
             # model and lists the GPU built), one query per call, f32 distances
@@ -333,7 +360,8 @@ def main_ivf(a):
             kw = {}
             if a.index_type == "ivf_pq":
                 _, T = ivf.pq_tables(ex["centroids"], ex["codebook"], Qh[:1], a.metric)
-                kw = dict(codes=ex["codes"], codebook=ex["codebook"], T=T, refine_factor=a.refine)
+                kw = dict(codes=ex["codes"], codebook=ex["codebook"], T=T, refine_factor=a.refine,
+                          lut="u8" if fast_pq else "f32", query_fp8=a.pq_query == "fp8")
             done, tc0 = 0, time.perf_counter()
             agree = 0
             while True:
@@ -358,7 +386,8 @@ def main_ivf(a):
             avg_ms = kt["ivf_scan_ms_total"] / kt["ivf_scan_launches"]
             bytes_launch = kt["ivf_scan_bytes"] / kt["ivf_scan_launches"]
             ach = bytes_launch / (avg_ms * 1e-3) / 1e9
-            kname = "flat_list_scan_kernel" if a.index_type == "ivf_flat" else "pq_query_scan_kernel"
+            kname = ("flat_list_scan_kernel" if a.index_type == "ivf_flat" else
+                     "pq_fast_scan_kernel" if fast_pq else "pq_query_scan_kernel")
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": ivf_traffic(a.config, N, D, BG), "kernel": kname,
                     "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(bytes_launch),
@@ -376,8 +405,12 @@ def main_ivf(a):
                                    f"{N}x{D} f32 per GPU k={K} query-batch={BG}",
                        "n_per_gpu": N, "n_total": N * world, "dim": D, "k": K, "global_batch": BG,
                        "metric": a.metric, "index_type": a.index_type, "nlist": a.nlist, "nprobe": a.nprobe,
-                       "m": a.m, "refine_factor": a.refine, "parallelism": f"rowshard{world}"},
+                       "m": a.m, "refine_factor": a.refine, "parallelism": f"rowshard{world}",
+                       **({"pq_query": a.pq_query or "f32", "pq_scan": a.pq_scan or "fast"}
+                          if a.index_type == "ivf_pq" else {}),
+                       **({"options": a.opt} if a.opt else {})},
             "recall_at_10": recall,
+            **({"recall_at_10_by_refine": recall_sweep} if recall_sweep else {}),
             "roofline": roof,
             "cpu_baseline": cpu,
             "build_s": round(build_s, 2), "gen_s": round(gen_s, 2),

@@ -201,6 +201,8 @@ struct Index {
 	int ivf_type_opt = 1;  // 0 IVF_FLAT, 1 IVF_PQ
 	int kmeans_iters = 50;  // lance k-means max_iters default
 	uint64_t ivf_seed = 0x5eedULL;
+	bool pq_fast = true;    // IVF_PQ list-major 8-bit-LUT scan (option "pq_scan" = "fast"; "exact_lut": f32 LUT, query-major)
+	bool pq_fp8 = false;    // IVF_PQ ADC tables from e4m3 (fp8) queries (option "pq_query" = "fp8" | "f32")
 
 	int64_t last_stats[5] = {0, 0, 0, 0, 0};
 

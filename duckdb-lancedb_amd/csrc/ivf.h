@@ -33,6 +33,13 @@ constexpr int IVF_TOPK_CAP = 2048; // LDS top-k buffer of the list scans / merge
 constexpr int IVF_MAX_K = 1024;    // k (and k * refine_factor) bound of the IVF path
 constexpr int FLAT_BLK = 256;      // rows per IVF_FLAT list-scan work item
 constexpr uint32_t SLOT_NONE = 0xFFFFFFFFu;
+// IVF_PQ fast scan (pq_fast_scan_kernel): FQ_G queries share one LUT lookup
+constexpr int FQ_G = 4;             // queries per work item (4 byte lanes of a u32)
+constexpr int FQ_THREADS = 512;
+constexpr int FQ_CAP = 1024;        // LDS candidate buffer per query of an item
+constexpr int FQ_CHUNK = 8192;      // list positions per work item
+constexpr int FQ_MAX_M = 96;        // LUT u32 [m][256] + FQ_G x FQ_CAP keys in LDS
+constexpr int FQ_MAX_KK = 512;      // k * refine_factor bound of the fast scan
 
 struct IvfState {
 	int type = IVF_PQ;
@@ -63,6 +70,12 @@ struct IvfState {
 	DevBuf<int> probe_c, lcnt, pstart, pairs;
 	DevBuf<uint64_t> keys, tkeys, cand_a, cand_b, best;
 	DevBuf<uint8_t> tmpb;
+	// fast PQ scan workspace
+	DevBuf<float> Qq;                        // fp8-rounded queries (option pq_query = fp8)
+	DevBuf<uint8_t> lut8;                    // [nq][m][256]
+	DevBuf<float> qpar;                      // [nq] (D, L0) pairs
+	DevBuf<int> item_off, work, ocnt;
+	DevBuf<uint64_t> thrq, okeys;
 	~IvfState();
 };
 
@@ -142,6 +155,22 @@ void launch_pq_query_scan(const uint8_t *lcodes, int m, int mp, const int64_t *l
                           const float *rowaux_f, int nq, int nprobe, const int64_t *probe_l, const float *probe_d,
                           const float *ltau, const float *P, const int64_t *pref, int S, int kk, uint64_t *out,
                           hipStream_t st);
+// fp8 (OCP e4m3fn) queries for the ADC tables: Qo = e4m3(Q / s) * s, s = absmax / 448 per query
+void launch_pq_query_fp8(const float *Q, int qld, int nq, int dim, float *Qo, hipStream_t st);
+// 8-bit LUTs lut8 [nq][m][256] and qpar [nq] = (D, L0) from P (see pq_lut_u8_kernel)
+void launch_pq_lut_u8(const float *P, int nq, int m, float sP, uint8_t *lut8, float2 *qpar, hipStream_t st);
+// item_off [nlist+1]: work items of the fast scan per list (query groups x row chunks)
+void launch_pq_fast_items(const int *pstart, const int64_t *loff, int nlist, int *item_off, hipStream_t st);
+int pq_fast_lds_bytes(int m);
+// list-major 8-bit-LUT scan: per query its candidate run out [nq][ocap] (count ocnt[q]);
+// work (1 int), thrq [nq] (~0) and ocnt [nq] (0) must be initialised
+void launch_pq_fast_scan(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
+                         const float *rowaux_f, int nlist, int nprobe, const int *pstart, const int *pairs,
+                         const int *item_off, const float *probe_d, const float *ltau, const uint8_t *lut8,
+                         const float2 *qpar, int kk, int *work, uint64_t *thrq, int *ocnt, uint64_t *out, int ocap,
+                         int grid, hipStream_t st);
+void launch_pq_run_merge(const uint64_t *keys, const int *ocnt, int nq, int ocap, int K, uint64_t *out,
+                         hipStream_t st);
 // ltau [npos]: per list position sum_j T[l][j][c_j] (f32, j ascending), 0 for padding
 void launch_pq_tau(const uint8_t *codes, const uint32_t *lslot, const int64_t *loff, int nlist, int64_t npos, int m,
                    int mp, const float *T, float *ltau, hipStream_t st);

@@ -424,13 +424,14 @@ static void layout(Index *ix) {
 // time_kernels: the list-scan launch (events 0/1 on the handle's stream) and
 // its algorithmic work: every probed list's rows once (IVF_FLAT: dim x esz
 // bytes; IVF_PQ: m code bytes + the 4-B row term tau for L2 / cosine) plus, for
-// IVF_PQ, each query's LUT input P[q] (m x 256 f32) once; pair rows = sum over
+// IVF_PQ, each query's LUT (m x 256 entries: f32 P[q], or the fast scan's
+// 8-bit table) once; pair rows = sum over
 // (query, list) pairs of the list's rows.
-static void account_list_scan(Index *ix, int esz, int nq) {
+static void account_list_scan(Index *ix, int esz, int nq, int lut_bytes) {
 	IvfState *s = ix->ivf;
 	std::vector<int> ps((size_t)s->nlist + 1);
 	HIPCHK(hipMemcpy(ps.data(), s->pstart.p, ps.size() * sizeof(int), hipMemcpyDeviceToHost));
-	double bytes = esz ? 0.0 : (double)nq * s->m * PQ_K * 4.0, pair_rows = 0.0;
+	double bytes = esz ? 0.0 : (double)nq * s->m * PQ_K * lut_bytes, pair_rows = 0.0;
 	const double row_pq = (double)s->m + (s->metric == METRIC_DOT ? 0.0 : 4.0);
 	for (int l = 0; l < s->nlist; ++l) {
 		const int np = ps[(size_t)l + 1] - ps[(size_t)l];
@@ -464,6 +465,7 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 	const int64_t per_q = s->type == IVF_FLAT ? (int64_t)nprobe * s->maxb * kk + (int64_t)tail_nb * kk
 	                                          : (int64_t)32 * kp + (int64_t)tail_nb * kk;
 	const int pass = (int)std::max<int64_t>(1, std::min<int64_t>(MAX_PASS_Q, (int64_t)(1 << 27) / std::max<int64_t>(per_q, 1)));
+	const bool fast_pq = s->type == IVF_PQ && ix->pq_fast && s->m <= FQ_MAX_M && kp <= FQ_MAX_KK;
 	for (int q0 = 0; q0 < nq; q0 += pass) {
 		const int n = std::min(pass, nq - q0);
 		s->Qf.need((size_t)n * ld);
@@ -507,9 +509,60 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			launch_ivf_merge(n, nprobe, s->probe_l.p, s->lblk0.p, s->maxb, kk, s->keys.p, tail_nb,
 			                 tail_n > 0 ? s->tkeys.p : nullptr, k, s->cand_a.p, st);
 			launch_keys_to_output(s->cand_a.p, n, k, k, ix->dlabels, oL, oD, oC, st);
-		} else {
+		} else if (ix->pq_fast && s->m <= FQ_MAX_M && kp <= FQ_MAX_KK) {
+			// list-major 8-bit-LUT scan: FQ_G queries per LUT lookup, each probed
+			// list's codes streamed once per query group
+			const float *Qp = cos ? s->Qn.p : s->Qf.p;
+			const int qld = cos ? dim : ld;
+			if (ix->pq_fp8) {
+				s->Qq.need((size_t)n * qld);
+				launch_pq_query_fp8(Qp, qld, n, dim, s->Qq.p, st);
+				Qp = s->Qq.p;
+			}
 			s->P.need((size_t)n * s->m * PQ_K);
-			launch_pq_P(cos ? s->Qn.p : s->Qf.p, cos ? dim : ld, n, s->codebook.p, s->m, s->dsub, s->P.p, st);
+			launch_pq_P(Qp, qld, n, s->codebook.p, s->m, s->dsub, s->P.p, st);
+			s->lut8.need((size_t)n * s->m * PQ_K);
+			s->qpar.need((size_t)2 * n);
+			launch_pq_lut_u8(s->P.p, n, s->m, s->metric == METRIC_DOT ? -1.0f : -2.0f, s->lut8.p,
+			                 reinterpret_cast<float2 *>(s->qpar.p), st);
+			s->item_off.need((size_t)s->nlist + 1);
+			launch_pq_fast_items(s->pstart.p, s->loff.p, s->nlist, s->item_off.p, st);
+			int64_t maxpos = 0;
+			for (int l = 0; l < s->nlist; ++l) maxpos = std::max(maxpos, s->h_loff[(size_t)l + 1] - s->h_loff[(size_t)l]);
+			const int ocap = (int)std::min<int64_t>((int64_t)1 << 30,
+			                                        (int64_t)nprobe * ((maxpos + FQ_CHUNK - 1) / FQ_CHUNK) * FQ_CAP);
+			s->okeys.need((size_t)n * ocap);
+			s->ocnt.need((size_t)n);
+			s->thrq.need((size_t)n);
+			s->work.need(1);
+			HIPCHK(hipMemsetAsync(s->ocnt.p, 0, (size_t)n * sizeof(int), st));
+			HIPCHK(hipMemsetAsync(s->thrq.p, 0xFF, (size_t)n * sizeof(uint64_t), st));
+			HIPCHK(hipMemsetAsync(s->work.p, 0, sizeof(int), st));
+			ix->tic(0);
+			launch_pq_fast_scan(s->lcodes.p, s->m, s->mp, s->loff.p, s->lslot.p,
+			                    reinterpret_cast<const float *>(sv.rowaux), s->nlist, nprobe, s->pstart.p, s->pairs.p,
+			                    s->item_off.p, s->probe_d.p, s->metric == METRIC_DOT ? nullptr : s->ltau.p, s->lut8.p,
+			                    reinterpret_cast<const float2 *>(s->qpar.p), kp, s->work.p, s->thrq.p, s->ocnt.p,
+			                    s->okeys.p, ocap, scan_grid(1 << 20), st);
+			ix->tic(1);
+			s->cand_a.need((size_t)n * kp);
+			launch_pq_run_merge(s->okeys.p, s->ocnt.p, n, ocap, kp, s->cand_a.p, st);
+			if (tail_n > 0) {
+				s->cand_b.need((size_t)n * k);
+				launch_ivf_merge(n, 0, nullptr, nullptr, 1, kk, nullptr, tail_nb, s->tkeys.p, k, s->cand_b.p, st);
+			}
+			launch_ivf_refine_final(sv, s->Qf.p, s->cand_a.p, kp, tail_n > 0 ? s->cand_b.p : nullptr,
+			                        tail_n > 0 ? k : 0, n, k, oL, oD, oC, st);
+		} else {
+			const float *Qp = cos ? s->Qn.p : s->Qf.p;
+			const int qld = cos ? dim : ld;
+			if (ix->pq_fp8) {
+				s->Qq.need((size_t)n * qld);
+				launch_pq_query_fp8(Qp, qld, n, dim, s->Qq.p, st);
+				Qp = s->Qq.p;
+			}
+			s->P.need((size_t)n * s->m * PQ_K);
+			launch_pq_P(Qp, qld, n, s->codebook.p, s->m, s->dsub, s->P.p, st);
 			const int S = pq_segments(n);
 			s->pref.need((size_t)n * (nprobe + 1));
 			launch_probe_prefix(s->probe_l.p, n, nprobe, s->loff.p, s->pref.p, st);
@@ -531,7 +584,7 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 		}
 		HIPCHK(hipGetLastError());
 		spin_sync(st);
-		if (ix->time_kernels) account_list_scan(ix, s->type == IVF_FLAT ? (ix->xbf16 ? 2 : 4) : 0, n);
+		if (ix->time_kernels) account_list_scan(ix, s->type == IVF_FLAT ? (ix->xbf16 ? 2 : 4) : 0, n, fast_pq ? 1 : 4);
 	}
 }
 

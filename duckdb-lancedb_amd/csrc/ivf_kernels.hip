@@ -21,6 +21,13 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 
+// Development-only timing ablations of pq_fast_scan_kernel (results are wrong
+// when set): only an ablation build (tools/pq_ablate.sh) may turn them on.
+#if !defined(LHIP_ABLATION_BUILD) && (defined(LHIP_PQ_ABL_NO_LUT) || defined(LHIP_PQ_ABL_NO_LOOKUP) || \
+                                      defined(LHIP_PQ_ABL_NO_CAND))
+#error "PQ ablation switches are for ablation builds only"
+#endif
+
 namespace lhip {
 
 static constexpr uint64_t KEY64_NONE = ~0ull;
@@ -1231,6 +1238,407 @@ void launch_pq_query_scan(const uint8_t *lcodes, int m, int mp, const int64_t *l
                           hipStream_t st) {
 	pq_query_scan_kernel<<<dim3((unsigned)S, (unsigned)nq), PQ_THREADS, 0, st>>>(
 	    lcodes, m, mp, loff, lslot, rowaux_f, nprobe, probe_l, probe_d, ltau, P, pref, S, kk, out);
+}
+
+// ---------------------------------------------------------------------------
+// IVF_PQ fast scan (list-major, 8-bit LUT, FQ_G queries per lookup)
+// ---------------------------------------------------------------------------
+// OCP e4m3fn round-to-nearest-even of v, |v| <= 448 (3 mantissa bits, minimum
+// normal exponent -6, subnormal step 2^-9); the division by the power-of-two
+// step and the rint are exact, so any IEEE implementation (oracle/ivf.py
+// e4m3_round) gives the same value.
+__device__ __forceinline__ float e4m3_round(float v) {
+	const float a = fabsf(v);
+	if (!(a > 0.0f)) return v;
+	int e;
+	(void)frexpf(a, &e);  // a = f 2^e, f in [0.5, 1): exponent e - 1
+	const int E = e - 1 > -6 ? e - 1 : -6;
+	const float ulp = ldexpf(1.0f, E - 3);
+	const float r = fminf(__fmul_rn(rintf(__fdiv_rn(a, ulp)), ulp), 448.0f);
+	return copysignf(r, v);
+}
+
+// fp8 queries: q' = e4m3(q / s) * s, s = absmax(q) / 448 (per query, f32)
+__global__ __launch_bounds__(256) void pq_query_fp8_kernel(const float *__restrict__ Q, int qld, int dim,
+                                                           float *__restrict__ Qo) {
+	__shared__ float red[4];
+	const int q = blockIdx.x, t = threadIdx.x;
+	const float *x = Q + (int64_t)q * qld;
+	float mx = 0.0f;
+	for (int i = t; i < dim; i += 256) mx = fmaxf(mx, fabsf(x[i]));
+	for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+	if ((t & 63) == 0) red[t >> 6] = mx;
+	__syncthreads();
+	mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+	const float sc = __fdiv_rn(mx, 448.0f);
+	float *y = Qo + (int64_t)q * qld;
+	for (int i = t; i < qld; i += 256)
+		y[i] = (i < dim && sc > 0.0f) ? __fmul_rn(e4m3_round(__fdiv_rn(x[i], sc)), sc) : 0.0f;
+}
+
+void launch_pq_query_fp8(const float *Q, int qld, int nq, int dim, float *Qo, hipStream_t st) {
+	pq_query_fp8_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(Q, qld, dim, Qo);
+}
+
+// 8-bit LUT of query q: L = sP P[q] (exact scaling), lo_j = min_c L[j][c],
+// D = max_j (max_c L[j][c] - lo_j) / 255 (1 if 0), u[j][c] = min(255,
+// rint((L[j][c] - lo_j) * (1 / D))), L0 = sum_j lo_j (j ascending).
+// ADC(row) = ((d0 + tau) + L0) + D * sum_j u[j][c_j]  (oracle/ivf.py pq_lut_u8)
+__global__ __launch_bounds__(256) void pq_lut_u8_kernel(const float *__restrict__ P, int m, float sP,
+                                                        uint8_t *__restrict__ lut8, float2 *__restrict__ qpar) {
+	__shared__ float lo[PQ_MAX_M], sp[PQ_MAX_M];
+	__shared__ float dsh;
+	const int q = blockIdx.x, t = threadIdx.x;
+	const float *Pq = P + (int64_t)q * m * PQ_K;
+	if (t < m) {
+		float a = F_INF, b = -F_INF;
+		for (int c = 0; c < PQ_K; ++c) {
+			const float v = __fmul_rn(sP, Pq[t * PQ_K + c]);
+			a = fminf(a, v);
+			b = fmaxf(b, v);
+		}
+		lo[t] = a;
+		sp[t] = __fsub_rn(b, a);
+	}
+	__syncthreads();
+	if (t == 0) {
+		float mxs = 0.0f, l0 = 0.0f;
+		for (int j = 0; j < m; ++j) {
+			mxs = fmaxf(mxs, sp[j]);
+			l0 = __fadd_rn(l0, lo[j]);
+		}
+		const float D = mxs > 0.0f ? __fdiv_rn(mxs, 255.0f) : 1.0f;
+		dsh = D;
+		qpar[q] = make_float2(D, l0);
+	}
+	__syncthreads();
+	const float inv = __fdiv_rn(1.0f, dsh);
+	uint8_t *o = lut8 + (int64_t)q * m * PQ_K;
+	for (int e = t; e < m * PQ_K; e += 256) {
+		const float v = __fmul_rn(sP, Pq[e]);
+		const float u = fminf(rintf(__fmul_rn(__fsub_rn(v, lo[e >> 8]), inv)), 255.0f);
+		o[e] = (uint8_t)u;
+	}
+}
+
+void launch_pq_lut_u8(const float *P, int nq, int m, float sP, uint8_t *lut8, float2 *qpar, hipStream_t st) {
+	pq_lut_u8_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(P, m, sP, lut8, qpar);
+}
+
+// work items: list l with np_l probing queries -> ceil(np_l / FQ_G) query
+// groups x ceil(positions_l / FQ_CHUNK) row chunks; item_off = exclusive prefix
+__global__ __launch_bounds__(1024) void pq_fast_items_kernel(const int *__restrict__ pstart,
+                                                             const int64_t *__restrict__ loff, int nlist,
+                                                             int *__restrict__ item_off) {
+	__shared__ int sh[1024];
+	const int t = threadIdx.x;
+	const int per = (nlist + 1023) / 1024;
+	const int a = t * per, b = min(nlist, a + per);
+	auto items = [&](int l) {
+		const int np = pstart[l + 1] - pstart[l];
+		const int64_t len = loff[l + 1] - loff[l];
+		return np > 0 && len > 0 ? ((np + FQ_G - 1) / FQ_G) * (int)((len + FQ_CHUNK - 1) / FQ_CHUNK) : 0;
+	};
+	int s = 0;
+	for (int i = a; i < b; ++i) s += items(i);
+	sh[t] = s;
+	__syncthreads();
+	for (int o = 1; o < 1024; o <<= 1) {
+		const int v = t >= o ? sh[t - o] : 0;
+		__syncthreads();
+		sh[t] += v;
+		__syncthreads();
+	}
+	int run = sh[t] - s;
+	for (int i = a; i < b; ++i) {
+		item_off[i] = run;
+		run += items(i);
+	}
+	if (t == 1023) item_off[nlist] = sh[1023];
+}
+
+// Persistent: each workgroup takes work items (one atomic per item).  An item
+// = one 8192-position chunk of list l x up to FQ_G queries probing l: their
+// 8-bit LUTs interleaved in LDS as u32 [j][c] = (u_0, u_1, u_2, u_3)[j][c], so
+// ONE ds_read_b32 per (row, j) serves all FQ_G queries; the four byte lanes
+// are summed two at a time in packed 16-bit halves (max 128 x 255 < 2^16).
+// Per query a threshold-filtered LDS candidate buffer, sorted and cut to kk
+// when it could overflow; its kk-th key is a valid bound for every other item
+// of the query (global atomicMin), and the candidates <= the bound go to the
+// query's output run (atomic cursor; the final order is by key, so the
+// arrival order does not matter).
+template <int MT>  // m at compile time (0: runtime m)
+__global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
+    const uint8_t *__restrict__ lcodes, int m, int mp, const int64_t *__restrict__ loff,
+    const uint32_t *__restrict__ lslot, const float *__restrict__ rowaux_f, int nlist, int nprobe,
+    const int *__restrict__ pstart, const int *__restrict__ pairs, const int *__restrict__ item_off,
+    const float *__restrict__ probe_d, const float *__restrict__ ltau, const uint8_t *__restrict__ lut8,
+    const float2 *__restrict__ qpar, int kk, int *__restrict__ work, unsigned long long *__restrict__ thrq,
+    int *__restrict__ ocnt, uint64_t *__restrict__ out, int ocap) {
+	extern __shared__ __attribute__((aligned(16))) uint8_t fq_smem[];
+	uint32_t *L = reinterpret_cast<uint32_t *>(fq_smem);                  // [m][256]
+	uint64_t *buf = reinterpret_cast<uint64_t *>(fq_smem + (size_t)m * PQ_K * 4);  // [FQ_G][FQ_CAP]
+	__shared__ int cnt[FQ_G], qid[FQ_G], item;
+	__shared__ uint64_t thr[FQ_G];
+	__shared__ float d0s[FQ_G], dls[FQ_G], l0s[FQ_G];
+	const int t = threadIdx.x;
+	const int nch = mp >> 4;
+	const int total = item_off[nlist];
+	for (;;) {
+		if (t == 0) item = atomicAdd(work, 1);
+		__syncthreads();
+		const int it = item;
+		if (it >= total) break;
+		// list of the item: last l with item_off[l] <= it (binary search)
+		int lo = 0, hi = nlist - 1;
+		while (lo < hi) {
+			const int mid = (lo + hi + 1) >> 1;
+			if (item_off[mid] <= it) lo = mid;
+			else hi = mid - 1;
+		}
+		const int l = lo;
+		const int64_t p0 = loff[l], len = loff[l + 1] - p0;
+		const int nc = (int)((len + FQ_CHUNK - 1) / FQ_CHUNK);
+		const int loc = it - item_off[l], g = loc / nc, ch = loc % nc;
+		const int np = pstart[l + 1] - pstart[l];
+		const int ng = min(FQ_G, np - g * FQ_G);
+		if (t < FQ_G) {
+			int q = -1;
+			if (t < ng) {
+				const int id = pairs[pstart[l] + g * FQ_G + t];
+				q = id / nprobe;
+				d0s[t] = probe_d[id];
+				const float2 qp = qpar[q];
+				dls[t] = qp.x;
+				l0s[t] = qp.y;
+				thr[t] = thrq[q];
+			} else {
+				thr[t] = 0;
+			}
+			qid[t] = q;
+			cnt[t] = 0;
+		}
+		__syncthreads();
+		// interleaved LUT: u32 [j][c] = bytes (u_0, u_1, u_2, u_3)
+#ifndef LHIP_PQ_ABL_NO_LUT
+		{
+			const int ne = m * PQ_K / 4;  // 4 codes per step
+			for (int e = t; e < ne; e += FQ_THREADS) {
+				uint32_t w[FQ_G];
+#pragma unroll
+				for (int i = 0; i < FQ_G; ++i)
+					w[i] = qid[i] >= 0 ? reinterpret_cast<const uint32_t *>(lut8 + (int64_t)qid[i] * m * PQ_K)[e] : 0u;
+				// transpose 4 x 4 bytes: out c = byte c of each w[i]
+				const uint32_t a01 = __builtin_amdgcn_perm(w[1], w[0], 0x05010400u);  // w0.b0 w1.b0 w0.b1 w1.b1
+				const uint32_t a23 = __builtin_amdgcn_perm(w[3], w[2], 0x05010400u);
+				const uint32_t b01 = __builtin_amdgcn_perm(w[1], w[0], 0x07030602u);  // w0.b2 w1.b2 w0.b3 w1.b3
+				const uint32_t b23 = __builtin_amdgcn_perm(w[3], w[2], 0x07030602u);
+				uint4 o;
+				o.x = __builtin_amdgcn_perm(a23, a01, 0x05040100u);  // c0: w0 w1 w2 w3
+				o.y = __builtin_amdgcn_perm(a23, a01, 0x07060302u);  // c1
+				o.z = __builtin_amdgcn_perm(b23, b01, 0x05040100u);  // c2
+				o.w = __builtin_amdgcn_perm(b23, b01, 0x07060302u);  // c3
+				reinterpret_cast<uint4 *>(L)[e] = o;
+			}
+		}
+#endif
+		__syncthreads();
+		const int64_t c0 = (int64_t)ch * FQ_CHUNK, c1 = len < c0 + FQ_CHUNK ? len : c0 + FQ_CHUNK;
+		// codes of the next round are loaded while the current round is summed
+		constexpr int NCH = FQ_MAX_M / 16;
+		uint4 cw[NCH];
+		uint32_t cslot = SLOT_NONE;
+		float ctau = 0.0f;
+		auto load_row = [&](int64_t r, uint4 (&w)[NCH], uint32_t &sl, float &ta) __attribute__((always_inline)) {
+			sl = SLOT_NONE;
+			ta = 0.0f;
+			if (r < c1) {
+				const int64_t ps = p0 + r;
+				sl = lslot[ps];
+				if (ltau) ta = ltau[ps];
+				const uint8_t *cp = lcodes + ((ps >> 6) * nch * 64 + (ps & 63)) * 16;
+#pragma unroll
+				for (int c = 0; c < NCH; ++c)
+					if (c < nch) w[c] = *reinterpret_cast<const uint4 *>(cp + (int64_t)c * 64 * 16);
+			}
+		};
+		load_row(c0 + t, cw, cslot, ctau);
+		for (int64_t r0 = c0; r0 < c1; r0 += FQ_THREADS) {
+			uint4 nw[NCH];
+			uint32_t nslot;
+			float ntau;
+			load_row(r0 + FQ_THREADS + t, nw, nslot, ntau);
+			// the query's bound from its other items, consumed at the round's end
+			// (a stale read is only a looser bound)
+			uint64_t gthr = KEY64_NONE;
+			if (t < FQ_G && qid[t] >= 0) gthr = __builtin_nontemporal_load(thrq + qid[t]);
+			uint32_t s02 = 0u, s13 = 0u;
+#ifdef LHIP_PQ_ABL_NO_LOOKUP
+			s02 = cw[0].x ^ cw[1].y ^ cw[2].z ^ cw[3].w ^ cw[4].x ^ cw[5].y;
+			s13 = cw[0].y ^ cw[1].z ^ cw[2].w ^ cw[3].x ^ cw[4].y ^ cw[5].z;
+			if (false) {
+#else
+			{
+#endif
+				// rows past the chunk hold stale codes: summed, never offered
+				if constexpr (MT > 0) {
+					// m known at compile time: 16 independent LDS reads per code
+					// piece, then the sums (no per-j branch, batched lgkm waits)
+#pragma unroll
+					for (int c = 0; c < (MT + 15) / 16; ++c) {
+						const uint32_t wd[4] = {cw[c].x, cw[c].y, cw[c].z, cw[c].w};
+						uint32_t v[16];
+#pragma unroll
+						for (int u = 0; u < 16; ++u) {
+							const int j = c * 16 + u;
+							if (j < MT) v[u] = L[j * PQ_K + ((wd[u >> 2] >> (8 * (u & 3))) & 255u)];
+						}
+#pragma unroll
+						for (int u = 0; u < 16; ++u) {
+							if (c * 16 + u < MT) {
+								s02 += v[u] & 0x00FF00FFu;
+								s13 += __builtin_amdgcn_perm(0u, v[u], 0x0c030c01u);  // bytes 1, 3 -> 0, 2
+							}
+						}
+					}
+				} else {
+#pragma unroll
+					for (int c = 0; c < NCH; ++c) {
+						if (c < nch) {
+							const uint32_t wd[4] = {cw[c].x, cw[c].y, cw[c].z, cw[c].w};
+#pragma unroll
+							for (int u = 0; u < 16; ++u) {
+								const int j = c * 16 + u;
+								if (j < m) {
+									const uint32_t code = (wd[u >> 2] >> (8 * (u & 3))) & 255u;
+									const uint32_t v = L[j * PQ_K + code];
+									s02 += v & 0x00FF00FFu;
+									s13 += (v >> 8) & 0x00FF00FFu;
+								}
+							}
+						}
+					}
+				}
+			}
+			const uint32_t S[FQ_G] = {s02 & 0xFFFFu, s13 & 0xFFFFu, s02 >> 16, s13 >> 16};
+			uint64_t key[FQ_G];
+			bool pass[FQ_G], any = false;
+#pragma unroll
+			for (int i = 0; i < FQ_G; ++i) {
+				float a = ltau ? __fadd_rn(d0s[i], ctau) : d0s[i];
+				a = __fadd_rn(a, l0s[i]);
+				a = __fadd_rn(a, __fmul_rn(dls[i], (float)S[i]));
+				key[i] = key64(a, cslot);
+				pass[i] = cslot != SLOT_NONE && qid[i] >= 0 && key[i] <= thr[i];
+#ifdef LHIP_PQ_ABL_NO_CAND
+				pass[i] = pass[i] && key[i] == 0;
+#endif
+				any |= pass[i];
+			}
+			// row liveness (a random 4-B read) only for rows under some bound
+			if (any && slot_alive(rowaux_f, cslot)) {
+#pragma unroll
+				for (int i = 0; i < FQ_G; ++i)
+					if (pass[i]) {
+						const int p = atomicAdd(&cnt[i], 1);
+						buf[i * FQ_CAP + p] = key[i];
+					}
+			}
+#pragma unroll
+			for (int c = 0; c < NCH; ++c) cw[c] = nw[c];
+			cslot = nslot;
+			ctau = ntau;
+			__syncthreads();
+			for (int i = 0; i < FQ_G; ++i) {
+				if (cnt[i] > FQ_CAP - FQ_THREADS) {  // the next round could overflow: sort, keep kk
+					uint64_t *b = buf + i * FQ_CAP;
+					const int c = cnt[i];
+					const int n2 = pow2_ceil(c);
+					for (int e = c + t; e < n2; e += FQ_THREADS) b[e] = KEY64_NONE;
+					wg_bitonic_sort(b, n2);
+					if (t == 0 && c >= kk) {
+						thr[i] = b[kk - 1];  // inclusive bound: the kk-th key stays
+						cnt[i] = kk;
+						atomicMin(thrq + qid[i], (unsigned long long)b[kk - 1]);
+					}
+					__syncthreads();
+				}
+			}
+			if (t < FQ_G && gthr < thr[t]) thr[t] = gthr;
+			__syncthreads();
+		}
+		// flush: the item's keys within its final bound (entries appended before
+		// the bound tightened may lie above it)
+		for (int i = 0; i < FQ_G; ++i) {
+			const int q = qid[i];
+			if (q < 0) continue;
+			const uint64_t th = thr[i];
+			const uint64_t *b = buf + i * FQ_CAP;
+			for (int e = t; e < cnt[i]; e += FQ_THREADS) {
+				const uint64_t key = b[e];
+				if (key <= th) {
+					const int p = atomicAdd(ocnt + q, 1);
+					if (p < ocap) out[(int64_t)q * ocap + p] = key;
+				}
+			}
+		}
+		__syncthreads();
+	}
+}
+
+int pq_fast_lds_bytes(int m) { return m * PQ_K * 4 + FQ_G * FQ_CAP * 8; }
+
+void launch_pq_fast_items(const int *pstart, const int64_t *loff, int nlist, int *item_off, hipStream_t st) {
+	pq_fast_items_kernel<<<1, 1024, 0, st>>>(pstart, loff, nlist, item_off);
+}
+
+void launch_pq_fast_scan(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
+                         const float *rowaux_f, int nlist, int nprobe, const int *pstart, const int *pairs,
+                         const int *item_off, const float *probe_d, const float *ltau, const uint8_t *lut8,
+                         const float2 *qpar, int kk, int *work, uint64_t *thrq, int *ocnt, uint64_t *out, int ocap,
+                         int grid, hipStream_t st) {
+	const int lds = pq_fast_lds_bytes(m);
+	auto go = [&](auto kern) {
+		HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+		                           160 * 1024 - 256));
+		kern<<<dim3((unsigned)grid), FQ_THREADS, (size_t)lds, st>>>(
+		    lcodes, m, mp, loff, lslot, rowaux_f, nlist, nprobe, pstart, pairs, item_off, probe_d, ltau, lut8, qpar,
+		    kk, work, reinterpret_cast<unsigned long long *>(thrq), ocnt, out, ocap);
+	};
+	switch (m) {
+	case 96: go(pq_fast_scan_kernel<96>); break;
+	case 64: go(pq_fast_scan_kernel<64>); break;
+	case 48: go(pq_fast_scan_kernel<48>); break;
+	case 32: go(pq_fast_scan_kernel<32>); break;
+	case 16: go(pq_fast_scan_kernel<16>); break;
+	case 8: go(pq_fast_scan_kernel<8>); break;
+	default: go(pq_fast_scan_kernel<0>); break;
+	}
+}
+
+// per query: top-K of its output run (count ocnt[q], capped at ocap)
+__global__ __launch_bounds__(256) void pq_run_merge_kernel(const uint64_t *__restrict__ keys, const int *__restrict__ ocnt,
+                                                           int ocap, int K, uint64_t *__restrict__ out) {
+	__shared__ uint64_t buf[IVF_TOPK_CAP];
+	__shared__ int cnt;
+	__shared__ uint64_t thr;
+	const int q = blockIdx.x, t = threadIdx.x;
+	TopK tk{buf, &cnt, &thr, K};
+	tk.reset();
+	const int n = min(ocnt[q], ocap);
+	const uint64_t *src = keys + (int64_t)q * ocap;
+	for (int e0 = 0; e0 < n; e0 += 256) {
+		const int e = e0 + t;
+		const uint64_t k = e < n ? src[e] : KEY64_NONE;
+		tk.offer(k, k != KEY64_NONE);
+	}
+	const int nout = tk.finish();
+	for (int i = t; i < K; i += 256) out[(int64_t)q * K + i] = i < nout ? buf[i] : KEY64_NONE;
+}
+
+void launch_pq_run_merge(const uint64_t *keys, const int *ocnt, int nq, int ocap, int K, uint64_t *out,
+                         hipStream_t st) {
+	pq_run_merge_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(keys, ocnt, ocap, K, out);
 }
 
 // ---------------------------------------------------------------------------

@@ -1062,6 +1062,18 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			ix->kmeans_iters = it;
 			return 0;
 		}
+		if (k == "pq_scan") {
+			if (v == "fast") ix->pq_fast = true;
+			else if (v == "exact_lut") ix->pq_fast = false;
+			else throw Error("pq_scan must be 'fast' or 'exact_lut'");
+			return 0;
+		}
+		if (k == "pq_query") {
+			if (v == "fp8") ix->pq_fp8 = true;
+			else if (v == "f32") ix->pq_fp8 = false;
+			else throw Error("pq_query must be 'fp8' or 'f32'");
+			return 0;
+		}
 		if (k == "ivf_seed") {
 			ix->ivf_seed = std::stoull(v);
 			return 0;

@@ -40,7 +40,7 @@ def lib():
         L.oracle_distances.restype = None
         I32, I64 = ctypes.c_int32, ctypes.c_int64
         L.oracle_ivf_search_batch.argtypes = [P, I32, P, P, P, I32, P, I64, P, P, I32, P, P, P, I32, I32, I32, I32,
-                                              I32, I32, I32, P, P, P]
+                                              I32, I32, I32, I32, P, P, P]
         L.oracle_ivf_search_batch.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -94,9 +94,11 @@ class IvfLayout:
 
 
 def ivf_search_batch(base, labels, layout, centroids, Q, k, nprobe, metric="l2", codes=None, codebook=None, T=None,
-                     refine_factor=1, acc64=True, nthreads=0):
+                     refine_factor=1, acc64=True, nthreads=0, lut="f32", query_fp8=False):
     """IVF_FLAT (codes None) / IVF_PQ search of oracle/flat_knn.c over a given
-    model and layout.  base / labels / codes are per slot.  l2 and dot only."""
+    model and layout.  base / labels / codes are per slot.  l2 and dot only.
+    lut "u8": the fast scan's 8-bit LUT; query_fp8: ADC tables from e4m3 queries
+    (oracle/ivf.py's definitions)."""
     base = np.ascontiguousarray(base, np.float32)
     Q = np.ascontiguousarray(Q, np.float32)
     labels = np.ascontiguousarray(labels, np.int64)
@@ -114,7 +116,8 @@ def ivf_search_batch(base, labels, layout, centroids, Q, k, nprobe, metric="l2",
     rc = lib().oracle_ivf_search_batch(_ptr(base), d, _ptr(labels), _ptr(layout.loff), _ptr(layout.lrows),
                                        layout.nlist, _ptr(layout.tail), len(layout.tail), _ptr(C), _ptr(codes), m,
                                        _ptr(codebook), _ptr(T), _ptr(Q), nq, k, nprobe, refine_factor,
-                                       METRIC_IDS[metric], 1 if acc64 else 0, int(nthreads), _ptr(out_l),
+                                       METRIC_IDS[metric], 1 if acc64 else 0,
+                                       (1 if lut == "u8" else 0) | (2 if query_fp8 else 0), int(nthreads), _ptr(out_l),
                                        _ptr(out_d), _ptr(cnt))
     if rc != 0:
         raise ValueError(f"oracle_ivf_search_batch failed ({rc})")

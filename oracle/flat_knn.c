@@ -228,11 +228,26 @@ void oracle_distances(const float *base, int64_t n, int32_t d, const float *q, i
  *   codebook cb [m][256][d/m], T [nlist][m][256] (NULL for dot).
  *   ADC = (d0 + tau) + sum_j LUT[j][c_j] (f32, j order), tau = sum_j
  *   T[l][j][c_j] (f32 from 0), LUT = -2 P (l2) / -P and tau = 0 (dot).
+ *   pq_flags bit 0: the fast scan's 8-bit LUT (oracle/ivf.py pq_lut_u8: ADC =
+ *   ((d0 + tau) + L0) + D * sum_j u[j][c_j]); bit 1: P from the fp8 (e4m3)
+ *   query (oracle/ivf.py fp8_queries).
  *   metric 0 l2, 1 dot (cosine: -2, not ported).  acc64: f64 exact distances
  *   (the checker) or f32 SIMD (the timed baseline) for the coarse / flat /
  *   re-rank distances; the ADC is f32 in j order in both.
  * Parallel over the probed lists of each query (per-thread heaps).
  */
+/* OCP e4m3fn round-to-nearest-even, |v| <= 448 (oracle/ivf.py e4m3_round) */
+static float e4m3_round(float v) {
+	const float a = fabsf(v);
+	if (!(a > 0.0f)) return v;
+	int e;
+	(void)frexpf(a, &e);
+	const int E = e - 1 > -6 ? e - 1 : -6;
+	const float ulp = ldexpf(1.0f, E - 3);
+	const float r = fminf(rintf(a / ulp) * ulp, 448.0f);
+	return copysignf(r, v);
+}
+
 static void topk_sel(const float *dv, int64_t n, int32_t np, int32_t *ids, float *ds) {
 	hit_t *h = (hit_t *)malloc((size_t)np * sizeof(hit_t));
 	int hn = 0;
@@ -252,8 +267,10 @@ int oracle_ivf_search_batch(const float *base, int32_t d, const int64_t *labels,
                             const int64_t *lrows, int32_t nlist, const int64_t *tail, int64_t ntail, const float *C,
                             const uint8_t *codes, int32_t m, const float *cb, const float *T, const float *Q,
                             int32_t nq, int32_t k, int32_t nprobe, int32_t refine, int32_t metric, int32_t acc64,
-                            int32_t nthreads, int64_t *out_labels, float *out_dist, int32_t *out_counts) {
+                            int32_t pq_flags, int32_t nthreads, int64_t *out_labels, float *out_dist,
+                            int32_t *out_counts) {
 	if (metric != 0 && metric != 1) return -2;
+	const int lut8 = pq_flags & 1, qfp8 = (pq_flags >> 1) & 1;
 	if (nthreads <= 0) nthreads = omp_get_max_threads();
 	if (nprobe > nlist) nprobe = nlist;
 	const int pq = codes != NULL;
@@ -263,6 +280,9 @@ int oracle_ivf_search_batch(const float *base, int32_t d, const int64_t *labels,
 	int32_t *pid = (int32_t *)malloc((size_t)nprobe * sizeof(int32_t));
 	float *pd = (float *)malloc((size_t)nprobe * sizeof(float));
 	float *P = pq ? (float *)malloc((size_t)m * 256 * sizeof(float)) : NULL;
+	uint8_t *U = pq ? (uint8_t *)malloc((size_t)m * 256) : NULL;
+	float *qp = (float *)malloc((size_t)d * sizeof(float));
+	float D8 = 1.0f, L08 = 0.0f;
 	hit_t *heaps = (hit_t *)malloc((size_t)nthreads * kp * sizeof(hit_t));
 	int *hn = (int *)malloc((size_t)nthreads * sizeof(int));
 	hit_t *all = (hit_t *)malloc(((size_t)nthreads * kp + (size_t)k) * sizeof(hit_t));
@@ -277,13 +297,40 @@ int oracle_ivf_search_batch(const float *base, int32_t d, const int64_t *labels,
 			cd[l] = acc64 ? dist64(C + (size_t)l * d, q, d, metric, qn2) : dist32(C + (size_t)l * d, q, d, metric, (float)qn2);
 		topk_sel(cd, nlist, nprobe, pid, pd);
 		if (pq) {
+			/* the ADC tables' query: f32, or e4m3(q / s) * s, s = absmax / 448 */
+			float mx = 0.0f;
+			for (int32_t i = 0; i < d; i++) mx = fmaxf(mx, fabsf(q[i]));
+			const float sc = mx / 448.0f;
+			for (int32_t i = 0; i < d; i++) qp[i] = (qfp8 && sc > 0.0f) ? e4m3_round(q[i] / sc) * sc : (qfp8 ? 0.0f : q[i]);
 #pragma omp parallel for num_threads(nthreads) schedule(static)
 			for (int32_t e = 0; e < m * 256; e++) {
 				const int j = e / 256;
 				const float *y = cb + (size_t)e * dsub;
 				float acc = 0.0f;
-				for (int t = 0; t < dsub; t++) acc = acc + q[j * dsub + t] * y[t];
+				for (int t = 0; t < dsub; t++) acc = acc + qp[j * dsub + t] * y[t];
 				P[e] = acc;
+			}
+			if (lut8) { /* 8-bit LUT, per oracle/ivf.py pq_lut_u8 */
+				const float sP = T ? -2.0f : -1.0f;
+				float mxs = 0.0f;
+				L08 = 0.0f;
+				float *lo = (float *)malloc((size_t)m * sizeof(float));
+				for (int j = 0; j < m; j++) {
+					float a = INFINITY, b = -INFINITY;
+					for (int c = 0; c < 256; c++) {
+						const float v = sP * P[j * 256 + c];
+						a = fminf(a, v);
+						b = fmaxf(b, v);
+					}
+					lo[j] = a;
+					mxs = fmaxf(mxs, b - a);
+				}
+				for (int j = 0; j < m; j++) L08 = L08 + lo[j];
+				D8 = mxs > 0.0f ? mxs / 255.0f : 1.0f;
+				const float inv = 1.0f / D8;
+				for (int e = 0; e < m * 256; e++)
+					U[e] = (uint8_t)fminf(rintf((sP * P[e] - lo[e / 256]) * inv), 255.0f);
+				free(lo);
 			}
 		}
 		for (int t = 0; t < nthreads; t++) hn[t] = 0;
@@ -310,7 +357,14 @@ int oracle_ivf_search_batch(const float *base, int32_t d, const int64_t *labels,
 							for (int j = 0; j < m; j++) tau = tau + Tl[j * 256 + c[j]];
 							acc = acc + tau;
 						}
-						for (int j = 0; j < m; j++) acc = acc + lut[j * 256 + c[j]];
+						if (lut8) {
+							int32_t S = 0;
+							for (int j = 0; j < m; j++) S += U[j * 256 + c[j]];
+							acc = acc + L08;
+							acc = acc + D8 * (float)S;
+						} else {
+							for (int j = 0; j < m; j++) acc = acc + lut[j * 256 + c[j]];
+						}
 						dd = acc;
 					} else {
 						dd = acc64 ? dist64(base + (size_t)s * d, q, d, metric, qn2)
@@ -357,6 +411,8 @@ int oracle_ivf_search_batch(const float *base, int32_t d, const int64_t *labels,
 	free(pid);
 	free(pd);
 	free(P);
+	free(U);
+	free(qp);
 	free(heaps);
 	free(hn);
 	free(all);

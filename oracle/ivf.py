@@ -33,6 +33,16 @@ What it restates (reference paths relative to ``/root/reference``):
             top-(k*r) by (ADC, label), exact re-rank, top-k by (dist, label)
   cosine    q^ = q / f32(sqrt(sum q^2)) (an f32 division) for the coarse
             search and P; the final distances are exact cosine distances.
+  u8 LUT    the fast scan (``pq_scan`` = "fast", the default): per query
+            L = sP P[q] (sP = -2, dot: -1), lo_j = min_c L[j][c], D = max_j
+            (max_c L[j][c] - lo_j) / 255 (1 when 0), u[j][c] = min(255,
+            rint((L[j][c] - lo_j) * f32(1 / D))), L0 = sum_j lo_j (j
+            ascending); ADC = ((d0 + tau) + L0) + D * S with S = sum_j
+            u[j][code_j] (an exact integer); every step one f32 rounding.
+  fp8       ``pq_query`` = "fp8": P is built from q' = e4m3(q / s) * s, s =
+            absmax(q) / 448 per query (OCP e4m3fn, round to nearest even, 3
+            mantissa bits, subnormal step 2^-9); coarse search and re-rank
+            keep the f32 query.
 
 The model (centroids, codebook) and the layout (list and codes of every row)
 come from the library (``lance_hip_ivf_export``): training is checked
@@ -106,6 +116,46 @@ def ivf_flat_search(X, labels, live, lists, C, Q, k, nprobe, metric="l2"):
     return out_l, out_d, cnt
 
 
+def e4m3_round(v):
+    """OCP e4m3fn round-to-nearest-even of f32 values with |v| <= 448 (the
+    HIP path's e4m3_round, ivf_kernels.hip)."""
+    v = np.asarray(v, F32)
+    a = np.abs(v)
+    _, e = np.frexp(a)
+    E = np.maximum(e - 1, -6)
+    ulp = np.ldexp(np.ones_like(a), E - 3).astype(F32)
+    r = np.minimum((np.rint((a / ulp).astype(F32)) * ulp).astype(F32), F32(448.0))
+    r = np.where(a > 0, r, F32(0.0)).astype(F32)
+    return np.copysign(r, v).astype(F32)
+
+
+def fp8_queries(Qp):
+    """q' = e4m3(q / s) * s per row, s = f32(absmax / 448); zero rows stay 0."""
+    Qp = np.asarray(Qp, F32)
+    out = np.zeros_like(Qp)
+    for i, x in enumerate(Qp):
+        mx = F32(np.max(np.abs(x))) if x.size else F32(0.0)
+        sc = F32(mx / F32(448.0))
+        if sc > 0:
+            out[i] = (e4m3_round((x / sc).astype(F32)) * sc).astype(F32)
+    return out
+
+
+def pq_lut_u8(P_i, sP):
+    """8-bit LUT of one query: (u [m, 256] uint8, D, L0) per the module docstring."""
+    L = (F32(sP) * np.asarray(P_i, F32)).astype(F32)
+    lo = L.min(axis=1).astype(F32)
+    sp = (L.max(axis=1) - lo).astype(F32)
+    mxs = max(F32(0.0), F32(sp.max()))
+    D = F32(mxs / F32(255.0)) if mxs > 0 else F32(1.0)
+    inv = F32(F32(1.0) / D)
+    u = np.minimum(np.rint(((L - lo[:, None]).astype(F32) * inv).astype(F32)), F32(255.0)).astype(np.uint8)
+    L0 = F32(0.0)
+    for v in lo:
+        L0 = F32(L0 + v)
+    return u, D, L0
+
+
 def pq_tables(C, codebook, Qp, metric):
     """P [nq, m, 256] and T [nlist, m, 256] (None for dot) per the canonical
     f32 sequential definitions."""
@@ -126,8 +176,11 @@ def pq_tables(C, codebook, Qp, metric):
     return P, T
 
 
-def ivf_pq_search(X, labels, live, lists, codes, C, codebook, Q, k, nprobe, refine_factor=1, metric="l2"):
-    """IVF_PQ search (see the module docstring).  ``codes`` [slots, m] uint8."""
+def ivf_pq_search(X, labels, live, lists, codes, C, codebook, Q, k, nprobe, refine_factor=1, metric="l2",
+                  lut="f32", query_fp8=False):
+    """IVF_PQ search (see the module docstring).  ``codes`` [slots, m] uint8.
+    lut: "f32" (the query-major scan, pq_scan = exact_lut) or "u8" (the fast
+    scan); query_fp8: ADC tables from fp8 queries (pq_query = fp8)."""
     metric = flat_knn.normalize_metric(metric)
     X = np.asarray(X, F32)
     labels = np.asarray(labels, np.int64)
@@ -137,6 +190,8 @@ def ivf_pq_search(X, labels, live, lists, codes, C, codebook, Q, k, nprobe, refi
     Q = np.asarray(Q, F32)
     probes, pd = coarse_probes(C, Q, metric, nprobe)
     Qp = normalize_queries(Q) if metric == "cosine" else Q
+    if query_fp8:
+        Qp = fp8_queries(Qp)
     P, T = pq_tables(C, codebook, Qp, metric)
     m = codes.shape[1]
     kp = k * max(1, refine_factor)
@@ -145,21 +200,30 @@ def ivf_pq_search(X, labels, live, lists, codes, C, codebook, Q, k, nprobe, refi
     out_d = np.full((nq, k), np.nan, F32)
     cnt = np.zeros(nq, np.int32)
     tail = np.nonzero(live & (lists < 0))[0]
+    luts = [pq_lut_u8(P[i], -2.0 if T is not None else -1.0) for i in range(nq)] if lut == "u8" else None
     for i in range(nq):
         cand_adc, cand_slot = [], []
         for p, l in enumerate(probes[i]):
             rows = np.nonzero(live & (lists == l))[0]
             if rows.size == 0:
                 continue
-            lut = (F32(-2.0) * P[i]).astype(F32) if T is not None else (-P[i]).astype(F32)
             acc = np.full(rows.size, pd[i, p], F32)
             if T is not None:
                 tau = np.zeros(rows.size, F32)
                 for j in range(m):
                     tau = (tau + T[l][j, codes[rows, j]]).astype(F32)
                 acc = (acc + tau).astype(F32)
-            for j in range(m):
-                acc = (acc + lut[j, codes[rows, j]]).astype(F32)
+            if lut == "u8":
+                u, D, L0 = luts[i]
+                S = np.zeros(rows.size, np.int64)
+                for j in range(m):
+                    S += u[j, codes[rows, j]]
+                acc = (acc + L0).astype(F32)
+                acc = (acc + (D * S.astype(F32)).astype(F32)).astype(F32)
+            else:
+                lt = (F32(-2.0) * P[i]).astype(F32) if T is not None else (-P[i]).astype(F32)
+                for j in range(m):
+                    acc = (acc + lt[j, codes[rows, j]]).astype(F32)
             cand_adc.append(acc)
             cand_slot.append(rows)
         sel = np.zeros(0, np.int64)

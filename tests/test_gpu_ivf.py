@@ -44,13 +44,15 @@ def clustered(rng, n, d, centers=48, spread=0.35):
     return (C[lab] + spread * rng.standard_normal((n, d))).astype(np.float32)
 
 
-def oracle_search(hip, h, X_by_label, Q, k, nprobe, rf, metric):
+def oracle_search(hip, h, X_by_label, Q, k, nprobe, rf, metric, lut="u8", query_fp8=False):
+    """lut: "u8" for the default fast scan (pq_scan = fast), "f32" for
+    pq_scan = exact_lut; query_fp8 mirrors pq_query = fp8."""
     ex = hip.LanceHipIvfExport(h)
     X = X_by_label[ex["labels"]]
     if ex["type"] == "ivf_flat":
         return ivf.ivf_flat_search(X, ex["labels"], ex["live"], ex["lists"], ex["centroids"], Q, k, nprobe, metric)
     return ivf.ivf_pq_search(X, ex["labels"], ex["live"], ex["lists"], ex["codes"], ex["centroids"], ex["codebook"],
-                             Q, k, nprobe, rf, metric)
+                             Q, k, nprobe, rf, metric, lut=lut, query_fp8=query_fp8)
 
 
 @pytest.mark.parametrize("index_type", ["ivf_flat", "ivf_pq"])
@@ -69,10 +71,18 @@ def test_ivf_parity(hip, mk, index_type, metric):
     # rows added after the build are searched exactly (the unindexed tail)
     hip.LanceDetachedAddBatch(h, X[10_000:], n - 10_000, d)
     hip.LanceDetachedDeleteBatch(h, rng.choice(n, 200, replace=False))
-    for nprobe, rf, k in [(6, 2, 10), (1, 1, 5), (20, 3, 40)]:
-        gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, k, nprobes=nprobe, refine_factor=rf)
-        el, ed, ec = oracle_search(hip, h, X, Q, k, nprobe, rf, metric)
-        assert_same(gl, gd, gc, el, ed, ec)
+    modes = [("fast", "f32")]
+    if index_type == "ivf_pq":  # both PQ scans, f32 and fp8 (e4m3) ADC queries
+        modes = [("fast", "f32"), ("fast", "fp8"), ("exact_lut", "f32"), ("exact_lut", "fp8")]
+    for scan, qm in modes:
+        if index_type == "ivf_pq":
+            hip.LanceHipSetOption(h, "pq_scan", scan)
+            hip.LanceHipSetOption(h, "pq_query", qm)
+        for nprobe, rf, k in [(6, 2, 10), (1, 1, 5), (20, 3, 40)]:
+            gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, k, nprobes=nprobe, refine_factor=rf)
+            el, ed, ec = oracle_search(hip, h, X, Q, k, nprobe, rf, metric, "u8" if scan == "fast" else "f32",
+                                       qm == "fp8")
+            assert_same(gl, gd, gc, el, ed, ec)
 
 
 @pytest.mark.parametrize("metric", ["l2", "dot"])

@@ -64,14 +64,14 @@ def build(hip, X, index_type):
     return h
 
 
-def port_search(hip, h, X, Q, nprobe, refine):
+def port_search(hip, h, X, Q, nprobe, refine, lut="u8", query_fp8=False):
     ex = hip.LanceHipIvfExport(h)
     Xs = X[ex["labels"]]
     lay = c_oracle.IvfLayout(ex["lists"], ex["live"], NLIST)
     kw = {}
     if ex["type"] == "ivf_pq":
         _, T = ivf.pq_tables(ex["centroids"], ex["codebook"], Q[:1], "l2")
-        kw = dict(codes=ex["codes"], codebook=ex["codebook"], T=T, refine_factor=refine)
+        kw = dict(codes=ex["codes"], codebook=ex["codebook"], T=T, refine_factor=refine, lut=lut, query_fp8=query_fp8)
     return c_oracle.ivf_search_batch(Xs, ex["labels"], lay, ex["centroids"], Q, K, nprobe, "l2", acc64=True,
                                      nthreads=16, **kw)
 
@@ -99,6 +99,9 @@ def test_c4_ivf_flat_nlist4096_nprobe64(hip, data, exact):
 
 
 def test_c5_ivf_pq_m96_refine_sweep(hip, data, exact):
+    """The default fast scan (8-bit LUT, list-major) over a refine sweep, the
+    fp8-query variant the C5 config names, and the f32-LUT query-major scan,
+    each against the C port in the same mode."""
     X, Q = data
     h = build(hip, X, "ivf_pq")
     try:
@@ -107,12 +110,25 @@ def test_c5_ivf_pq_m96_refine_sweep(hip, data, exact):
             gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, K, nprobes=NPROBE, refine_factor=rf)
             check(gl, gd, gc, *port_search(hip, h, X, Q, NPROBE, rf))
             recalls[rf] = flat_knn.recall_at_k(gl, exact[0], K)
-        print("C5 params: recall@10 by refine_factor", recalls)
+        print("C5 params, fast scan: recall@10 by refine_factor", recalls)
         # a wider exact re-rank window can only help (the ADC candidates of
         # refine r are a prefix of those of r' > r)
         assert recalls[1] <= recalls[10] + 1e-9 <= recalls[50] + 2e-9
-        # measured on MI355X: 0.294 / 0.818 / 0.996 (profiles/r02_c_ivf_params.log)
+        # f32-LUT scan measured on MI355X: 0.294 / 0.818 / 0.996 (profiles/r02_c_ivf_params.log)
         assert recalls[10] >= 0.75
         assert recalls[50] >= 0.98
+        hip.LanceHipSetOption(h, "pq_query", "fp8")
+        gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, K, nprobes=NPROBE, refine_factor=10)
+        check(gl, gd, gc, *port_search(hip, h, X, Q, NPROBE, 10, query_fp8=True))
+        r8 = flat_knn.recall_at_k(gl, exact[0], K)
+        print(f"C5 params, fast scan, fp8 queries: recall@10 = {r8:.4f} (refine 10)")
+        assert r8 >= recalls[10] - 0.05
+        hip.LanceHipSetOption(h, "pq_query", "f32")
+        hip.LanceHipSetOption(h, "pq_scan", "exact_lut")
+        gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, K, nprobes=NPROBE, refine_factor=10)
+        check(gl, gd, gc, *port_search(hip, h, X, Q, NPROBE, 10, lut="f32"))
+        r32 = flat_knn.recall_at_k(gl, exact[0], K)
+        print(f"C5 params, f32-LUT scan: recall@10 = {r32:.4f} (refine 10)")
+        assert r32 >= 0.75
     finally:
         hip.LanceFreeDetached(h)

@@ -93,10 +93,38 @@ def test_c_ivf_port_matches_numpy_oracle():
             np.testing.assert_array_equal(gl, el)
             np.testing.assert_array_equal(gd, ed)
             for rf in (1, 3):
-                el, ed, ec = ivf.ivf_pq_search(X, lab, live, lists, codes, C, cb, Q, k, nprobe, rf, metric)
-                _, T = ivf.pq_tables(C, cb, Q[:1], metric)
-                gl, gd, gc = c_oracle.ivf_search_batch(X, lab, lay, C, Q, k, nprobe, metric, codes=codes, codebook=cb,
-                                                       T=T, refine_factor=rf)
-                np.testing.assert_array_equal(gc, ec)
-                np.testing.assert_array_equal(gl, el)
-                np.testing.assert_array_equal(gd, ed)
+                for lut, fp8 in (("f32", False), ("u8", False), ("u8", True), ("f32", True)):
+                    el, ed, ec = ivf.ivf_pq_search(X, lab, live, lists, codes, C, cb, Q, k, nprobe, rf, metric,
+                                                   lut=lut, query_fp8=fp8)
+                    _, T = ivf.pq_tables(C, cb, Q[:1], metric)
+                    gl, gd, gc = c_oracle.ivf_search_batch(X, lab, lay, C, Q, k, nprobe, metric, codes=codes,
+                                                           codebook=cb, T=T, refine_factor=rf, lut=lut,
+                                                           query_fp8=fp8)
+                    np.testing.assert_array_equal(gc, ec)
+                    np.testing.assert_array_equal(gl, el)
+                    np.testing.assert_array_equal(gd, ed)
+
+
+def test_e4m3_round_matches_torch_float8():
+    """The fp8 query restatement (OCP e4m3fn, round to nearest even) equals
+    torch's float8_e4m3fn cast on 1M values spanning subnormals to 448."""
+    import torch
+
+    rng = np.random.default_rng(0)
+    v = (rng.standard_normal(1_000_000) * np.exp(rng.uniform(-12, 6, 1_000_000))).astype(np.float32)
+    v = np.clip(v, -448, 448)
+    want = torch.from_numpy(v).to(torch.float8_e4m3fn).float().numpy()
+    np.testing.assert_array_equal(ivf.e4m3_round(v), want)
+
+
+def test_u8_lut_bounds_the_f32_lut():
+    """Each 8-bit entry reconstructs its f32 LUT entry within D / 2 (+ f32
+    rounding), so the quantised ADC is within m * D / 2 of the f32 ADC."""
+    rng = np.random.default_rng(4)
+    P = rng.standard_normal((16, 256)).astype(np.float32) * 3
+    u, D, L0 = ivf.pq_lut_u8(P, -2.0)
+    L = (np.float32(-2.0) * P).astype(np.float32)
+    lo = L.min(axis=1)
+    rec = lo[:, None] + D * u.astype(np.float32)
+    assert np.all(np.abs(rec - L) <= D * 0.5 * (1 + 1e-5) + 1e-5)
+    assert u.max() <= 255 and abs(L0 - lo.astype(np.float64).sum()) < 1e-3
