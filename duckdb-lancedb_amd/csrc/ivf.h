@@ -40,6 +40,7 @@ constexpr int FQ_CAP = 1024;        // LDS candidate buffer per query of an item
 constexpr int FQ_CHUNK = 8192;      // list positions per work item
 constexpr int FQ_MAX_M = 96;        // LUT u32 [m][256] + FQ_G x FQ_CAP keys in LDS
 constexpr int FQ_MAX_KK = 512;      // k * refine_factor bound of the fast scan
+constexpr int FL_KEYS = 16;         // IVF_FLAT bound scan: (LB, slot) keys per (query, item); k <= FL_KEYS - 1
 
 struct IvfState {
 	int type = IVF_PQ;
@@ -76,6 +77,12 @@ struct IvfState {
 	DevBuf<float> qpar;                      // [nq] (D, L0) pairs
 	DevBuf<int> item_off, work, ocnt;
 	DevBuf<uint64_t> thrq, okeys;
+	// IVF_FLAT bound scan workspace
+	DevBuf<float> lbQf, cut;
+	DevBuf<uint16_t> lbQb;
+	DevBuf<float4> lbqaux;
+	DevBuf<int> cert;
+	std::vector<int> h_cert;
 	~IvfState();
 };
 
@@ -142,6 +149,17 @@ void launch_flat_list_scan(const StoreView &s, const int *blk_list, const int64_
                            const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart, const int *pairs,
                            int nprobe, int maxb, int64_t tail_s0, int64_t tail_n, int nq, const double *Qd,
                            const double *qn2, int kk, uint64_t *out, hipStream_t st);
+// IVF_FLAT bound scan (MFMA bf16 lower bounds): out [pair][maxb][16] (LB, slot) keys per (query, item)
+void launch_flat_list_lb(const StoreView &s, const int *blk_list, const int64_t *blk_pos0, const int *lblk0,
+                         const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart, const int *pairs,
+                         int nprobe, int maxb, const uint16_t *Qb, const float4 *qaux, uint64_t *out, hipStream_t st);
+// per query: top-M bound candidates of its probed lists and the cut (every other row has LB >= cut)
+void launch_flat_lb_merge(int nq, int nprobe, const int64_t *probe_l, const int *lblk0, int maxb, const uint64_t *keys,
+                          int M, uint64_t *cand, float *cut, hipStream_t st);
+// exact re-rank + tail merge + certificate (cert[q] = 1 when no left-out row can enter the top k)
+void launch_flat_lb_refine(const StoreView &s, const float *Qf, const uint64_t *ca, int M, const uint64_t *cb, int kb,
+                           const float *cut, int nq, int k, int64_t *outL, float *outD, int *outC, int *cert,
+                           hipStream_t st);
 // Qd [nq][ld] f64 copy of the padded f32 queries Qf, qn2 [nq] = sum of q^2 in element order
 void launch_ivf_qd(const float *Qf, int nq, int ld, int dim, double *Qd, double *qn2, hipStream_t st);
 void launch_pq_P(const float *Q, int qld, int nq, const float *cb, int m, int dsub, float *P, hipStream_t st);

@@ -466,6 +466,8 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 	                                          : (int64_t)32 * kp + (int64_t)tail_nb * kk;
 	const int pass = (int)std::max<int64_t>(1, std::min<int64_t>(MAX_PASS_Q, (int64_t)(1 << 27) / std::max<int64_t>(per_q, 1)));
 	const bool fast_pq = s->type == IVF_PQ && ix->pq_fast && s->m <= FQ_MAX_M && kp <= FQ_MAX_KK;
+	// IVF_FLAT bound scan: bf16 scan rows, k within an item's leaders
+	const bool lb_flat = s->type == IVF_FLAT && ix->ivf_flat_bound && sv.scan_bf16 && ld % 64 == 0 && k <= FL_KEYS - 1;
 	for (int q0 = 0; q0 < nq; q0 += pass) {
 		const int n = std::min(pass, nq - q0);
 		s->Qf.need((size_t)n * ld);
@@ -499,7 +501,43 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			launch_flat_list_scan(sv, nullptr, nullptr, nullptr, nullptr, nullptr, tail_nb, nullptr, nullptr, 1, 1,
 			                      s->n_indexed, tail_n, n, s->Qd.p, s->qn2.p, kk, s->tkeys.p, st);
 		}
-		if (s->type == IVF_FLAT) {
+		bool exact_flat = s->type == IVF_FLAT;
+		if (s->type == IVF_FLAT && lb_flat) {
+			// MFMA lower bounds per (query, item) -> top-M by bound -> exact
+			// re-rank with a certificate; an uncertified pass reruns exactly
+			const int nq_pad = (int)round_up(n, SCAN_BQ);
+			s->lbQf.need((size_t)nq_pad * ld);
+			s->lbQb.need((size_t)nq_pad * ld);
+			s->lbqaux.need((size_t)nq_pad);
+			launch_prep_queries(dQ + (int64_t)q0 * dim, n, dim, ld, nq_pad, s->metric, ix->max_alpha, ix->max_ux,
+			                    s->lbQf.p, s->lbQb.p, s->lbqaux.p, nullptr, st);
+			s->keys.need((size_t)n * nprobe * s->maxb * FL_KEYS);
+			ix->tic(0);
+			launch_flat_list_lb(sv, s->blk_list.p, s->blk_pos0.p, s->lblk0.p, s->loff.p, s->lslot.p, s->nblk,
+			                    s->pstart.p, s->pairs.p, nprobe, s->maxb, s->lbQb.p, s->lbqaux.p, s->keys.p, st);
+			ix->tic(1);
+			const int M = std::min(IVF_TOPK_CAP - 1, k + 32);
+			s->cand_a.need((size_t)n * M);
+			s->cut.need((size_t)n);
+			launch_flat_lb_merge(n, nprobe, s->probe_l.p, s->lblk0.p, s->maxb, s->keys.p, M, s->cand_a.p, s->cut.p, st);
+			if (tail_n > 0) {
+				s->cand_b.need((size_t)n * k);
+				launch_ivf_merge(n, 0, nullptr, nullptr, 1, kk, nullptr, tail_nb, s->tkeys.p, k, s->cand_b.p, st);
+			}
+			s->cert.need((size_t)n);
+			launch_flat_lb_refine(sv, s->Qf.p, s->cand_a.p, M, tail_n > 0 ? s->cand_b.p : nullptr, tail_n > 0 ? k : 0,
+			                      s->cut.p, n, k, oL, oD, oC, s->cert.p, st);
+			HIPCHK(hipGetLastError());
+			s->h_cert.resize((size_t)n);
+			HIPCHK(hipMemcpyAsync(s->h_cert.data(), s->cert.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, st));
+			spin_sync(st);
+			exact_flat = false;
+			for (int i = 0; i < n; ++i)
+				if (!s->h_cert[(size_t)i]) exact_flat = true;
+			if (exact_flat) ix->ivf_flat_fallbacks += 1;
+			if (ix->time_kernels) account_list_scan(ix, 2, n, 0);
+		}
+		if (exact_flat) {
 			s->keys.need((size_t)n * nprobe * s->maxb * kk);
 			ix->tic(0);
 			launch_flat_list_scan(sv, s->blk_list.p, s->blk_pos0.p, s->lblk0.p, s->loff.p, s->lslot.p, s->nblk,
@@ -509,6 +547,8 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			launch_ivf_merge(n, nprobe, s->probe_l.p, s->lblk0.p, s->maxb, kk, s->keys.p, tail_nb,
 			                 tail_n > 0 ? s->tkeys.p : nullptr, k, s->cand_a.p, st);
 			launch_keys_to_output(s->cand_a.p, n, k, k, ix->dlabels, oL, oD, oC, st);
+		} else if (s->type == IVF_FLAT) {
+			// bound scan certified every query of the pass
 		} else if (ix->pq_fast && s->m <= FQ_MAX_M && kp <= FQ_MAX_KK) {
 			// list-major 8-bit-LUT scan: FQ_G queries per LUT lookup, each probed
 			// list's codes streamed once per query group
@@ -584,7 +624,8 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 		}
 		HIPCHK(hipGetLastError());
 		spin_sync(st);
-		if (ix->time_kernels) account_list_scan(ix, s->type == IVF_FLAT ? (ix->xbf16 ? 2 : 4) : 0, n, fast_pq ? 1 : 4);
+		if (ix->time_kernels && !(s->type == IVF_FLAT && lb_flat && !exact_flat))
+			account_list_scan(ix, s->type == IVF_FLAT ? (ix->xbf16 ? 2 : 4) : 0, n, fast_pq ? 1 : 4);
 	}
 }
 

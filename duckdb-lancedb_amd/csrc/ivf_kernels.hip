@@ -1036,6 +1036,320 @@ __global__ __launch_bounds__(256) void flat_list_scan_kernel(
 	}
 }
 
+// ---------------------------------------------------------------------------
+// IVF_FLAT bound scan (MFMA): the same work items, but each (query, row) pair
+// gets the flat scan's rigorous bf16 lower bound LB <= exact distance
+// (knn_kernels.hip prep_queries / scan_kernel numerics: bf16 rows of the scan
+// copy or bf16 store, v_mfma_f32_16x16x32_bf16, the row / query bound terms)
+// instead of an f64 distance; per (query, item) the FL_T smallest (LB, slot)
+// keys go out.  The per-query merge keeps the FL_T - 1 leaders of every item
+// and takes the top M by LB; cut = min(the (M+1)-th merged LB, every item's
+// FL_T-th LB): every row left out has LB >= cut.  The exact f64 re-rank of the
+// M then returns the top k, certified when cut > the k-th exact distance;
+// an uncertified batch reruns on the exact list scan.
+// Block: 4 waves x 64 rows (4 blocks of 16), one 16-query MFMA column block.
+// ---------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int FL_G = 16;   // queries per MFMA column block
+constexpr int FL_T = FL_KEYS;  // keys per (query, item)
+
+template <int METRIC>
+__global__ __launch_bounds__(256) void flat_list_lb_kernel(
+    const uint16_t *__restrict__ Xb, int ld, const float *__restrict__ rowaux_f, const int *__restrict__ blk_list,
+    const int64_t *__restrict__ blk_pos0, const int *__restrict__ lblk0, const int64_t *__restrict__ loff,
+    const uint32_t *__restrict__ lslot, const int *__restrict__ pstart, const int *__restrict__ pairs, int nprobe,
+    int maxb, const uint16_t *__restrict__ Qb, const float4 *__restrict__ qaux, uint64_t *__restrict__ out) {
+	extern __shared__ __attribute__((aligned(16))) uint8_t fl_smem[];
+	const int qrow = ld * 2 + 16;  // padded query row (bytes): 16 lanes reading 16 rows hit distinct banks
+	uint8_t *qs = fl_smem;                                                          // [FL_G][qrow]
+	uint64_t *sk = reinterpret_cast<uint64_t *>(fl_smem + FL_G * qrow);            // [FL_G][256] keys
+	__shared__ uint32_t sslot[FLAT_BLK];
+	__shared__ float4 ras[FLAT_BLK];
+	__shared__ float4 qas[FL_G];
+	__shared__ int sq[FL_G], spair[FL_G];
+	constexpr bool FOLD = METRIC != METRIC_COSINE;
+	const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+	const int gq = lane >> 4, rr = lane & 15;
+	const int b = blockIdx.x;
+	const int l = blk_list[b];
+	const int64_t p0 = blk_pos0[b];
+	const int64_t p1 = min<int64_t>(loff[l + 1], p0 + FLAT_BLK);
+	const int pa = pstart[l], pb = pstart[l + 1];
+	const int bi = b - lblk0[l];
+	if (pa >= pb) return;
+	{
+		uint32_t s = SLOT_NONE;
+		if (p0 + t < p1) s = lslot[p0 + t];
+		sslot[t] = s;
+		// row terms (alpha, xn, ux, sc); padding: alpha = +inf (LB = +inf)
+		float4 r = make_float4(F_INF, 0.f, 0.f, 0.f);
+		if (s != SLOT_NONE)
+			r = make_float4(rowaux_f[raix(s, 0)], rowaux_f[raix(s, 1)], rowaux_f[raix(s, 2)], rowaux_f[raix(s, 3)]);
+		ras[t] = r;
+	}
+	const int nw = ld / 64;  // 64-deep k windows (ld is a multiple of 64)
+	for (int g0 = pa; g0 < pb; g0 += FL_G) {
+		const int ng = min(FL_G, pb - g0);
+		__syncthreads();
+		if (t < FL_G) {
+			const int pid = t < ng ? pairs[g0 + t] : -1;
+			spair[t] = pid;
+			sq[t] = pid < 0 ? -1 : pid / nprobe;
+			qas[t] = pid < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : qaux[pid / nprobe];
+		}
+		__syncthreads();
+		// the group's bf16 query rows into LDS (zero rows for unused columns)
+		for (int e = t; e < FL_G * (ld / 8); e += 256) {
+			const int c = e / (ld / 8), k8 = e % (ld / 8);
+			uint4 v = make_uint4(0u, 0u, 0u, 0u);
+			if (sq[c] >= 0) v = *reinterpret_cast<const uint4 *>(Qb + (int64_t)sq[c] * ld + 8 * k8);
+			*reinterpret_cast<uint4 *>(qs + c * qrow + 16 * k8) = v;
+		}
+		__syncthreads();
+		// accumulators: rows 64w + 16rb + (4 gq .. 4 gq + 3), query rr
+		f32x4 acc[4];
+		if (FOLD) {
+			// alpha + C + xn*B + ux*A by one exact-f32 16x16x4 MFMA per block:
+			// A[row][k] = (xn, ux, alpha, 1), B[k][query] = (B, A, 1, C)
+			const float4 qa = qas[rr];
+			const float bv = gq == 0 ? qa.z : gq == 1 ? qa.y : gq == 2 ? 1.0f : qa.w;
+			const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+			for (int rb = 0; rb < 4; ++rb) {
+				const float4 ra = ras[64 * w + 16 * rb + rr];
+				const float av = gq == 0 ? ra.y : gq == 1 ? ra.z : gq == 2 ? ra.x : 1.0f;
+				acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, z, 0, 0, 0);
+			}
+		} else {
+#pragma unroll
+			for (int rb = 0; rb < 4; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+		}
+		// row pointers of this lane's 4 rows (padding rows read slot 0: finite
+		// bf16, their LB is +inf through alpha)
+		const uint16_t *xp[4];
+#pragma unroll
+		for (int rb = 0; rb < 4; ++rb) {
+			const uint32_t s = sslot[64 * w + 16 * rb + rr];
+			xp[rb] = Xb + (int64_t)(s == SLOT_NONE ? 0u : s) * ld + 8 * gq;
+		}
+		const uint8_t *qb = qs + rr * qrow + 16 * gq;
+		// two windows of rows in flight
+		uint4 xa[2][4][2];
+		auto ldx = [&](uint4 (&d)[4][2], int kw) __attribute__((always_inline)) {
+#pragma unroll
+			for (int rb = 0; rb < 4; ++rb) {
+				d[rb][0] = *reinterpret_cast<const uint4 *>(xp[rb] + 64 * kw);
+				d[rb][1] = *reinterpret_cast<const uint4 *>(xp[rb] + 64 * kw + 32);
+			}
+		};
+		ldx(xa[0], 0);
+		if (nw > 1) ldx(xa[1], 1);
+		for (int kw = 0; kw < nw; kw += 2) {
+#pragma unroll
+			for (int h = 0; h < 2; ++h) {
+				const int k = kw + h;
+				if (k < nw) {
+					const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(qb + 128 * k);
+					const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(qb + 128 * k + 64);
+					uint4 cur[4][2];
+#pragma unroll
+					for (int rb = 0; rb < 4; ++rb) {
+						cur[rb][0] = xa[h][rb][0];
+						cur[rb][1] = xa[h][rb][1];
+					}
+					if (k + 2 < nw) ldx(xa[h], k + 2);
+#pragma unroll
+					for (int rb = 0; rb < 4; ++rb) {
+						acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, cur[rb][0]), b0,
+						                                                  acc[rb], 0, 0, 0);
+						acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, cur[rb][1]), b1,
+						                                                  acc[rb], 0, 0, 0);
+					}
+				}
+			}
+		}
+		// keys -> LDS [query][row]
+		{
+			const float4 qa = qas[rr];
+#pragma unroll
+			for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+				for (int i = 0; i < 4; ++i) {
+					const int r = 64 * w + 16 * rb + 4 * gq + i;
+					const uint32_t s = sslot[r];
+					float lb;
+					if (FOLD) {
+						lb = acc[rb][i];
+					} else {
+						const float4 ra = ras[r];
+						float v = fmaf(ra.y, qa.z, ra.x);
+						v = fmaf(ra.z, qa.y, v);
+						v = fmaf(acc[rb][i] * ra.w, qa.x, v);
+						lb = v + qa.w;
+					}
+					const bool ok = s != SLOT_NONE && ras[r].x != F_INF && !__builtin_isnan(lb);
+					sk[rr * FLAT_BLK + r] = ok ? key64(lb, s) : KEY64_NONE;
+				}
+		}
+		__syncthreads();
+		// per query: each wave sorts its 64 rows' keys, the 4 x 16 leaders are
+		// sorted again; wave w handles queries w, w + 4, ...
+		for (int c = w; c < ng; c += 4) {
+			uint64_t best = KEY64_NONE;
+#pragma unroll
+			for (int ww = 0; ww < 4; ++ww) {
+				const uint64_t ks = wave_sort64(sk[c * FLAT_BLK + 64 * ww + lane]);
+				// leader lanes 16 ww .. 16 ww + 15 of the final sort take ks[0..15]
+				const uint64_t moved = __shfl(ks, lane & 15, 64);
+				if ((lane >> 4) == ww) best = moved;
+			}
+			best = wave_sort64(best);
+			if (lane < FL_T) out[((int64_t)spair[c] * maxb + bi) * FL_T + lane] = best;
+		}
+	}
+}
+
+// per query: merge the items' leaders of its probed lists (FL_T - 1 per item
+// into a top-M), cut = min(the item boundaries, the merged (M+1)-th LB)
+__global__ __launch_bounds__(256) void flat_lb_merge_kernel(int nprobe, const int64_t *__restrict__ probe_l,
+                                                            const int *__restrict__ lblk0, int maxb,
+                                                            const uint64_t *__restrict__ keys, int M,
+                                                            uint64_t *__restrict__ cand, float *__restrict__ cut) {
+	__shared__ uint64_t buf[IVF_TOPK_CAP];
+	__shared__ int cnt;
+	__shared__ uint64_t thr;
+	__shared__ uint32_t bmin;
+	const int q = blockIdx.x, t = threadIdx.x;
+	TopK tk{buf, &cnt, &thr, M + 1};
+	if (t == 0) bmin = 0xFFFFFFFFu;
+	tk.reset();
+	uint32_t mymin = 0xFFFFFFFFu;
+	for (int p = 0; p < nprobe; ++p) {
+		const int64_t l = probe_l[(int64_t)q * nprobe + p];
+		if (l < 0) continue;
+		const int nb = lblk0[l + 1] - lblk0[l];
+		const uint64_t *src = keys + ((int64_t)q * nprobe + p) * maxb * FL_T;
+		const int tot = nb * FL_T;
+		for (int e0 = 0; e0 < tot; e0 += 256) {
+			const int e = e0 + t;
+			uint64_t k = e < tot ? src[e] : KEY64_NONE;
+			if (e < tot && (e % FL_T) == FL_T - 1) {  // an item's boundary
+				if (k != KEY64_NONE) mymin = min(mymin, (uint32_t)(k >> 32));
+				k = KEY64_NONE;
+			}
+			tk.offer(k, k != KEY64_NONE);
+		}
+	}
+	atomicMin(&bmin, mymin);
+	const int n = tk.finish();
+	__syncthreads();
+	uint32_t cm = bmin;
+	if (n > M) cm = min(cm, (uint32_t)(buf[M] >> 32));
+	for (int i = t; i < M; i += 256) cand[(int64_t)q * M + i] = i < n ? buf[i] : KEY64_NONE;
+	if (t == 0) cut[q] = cm == 0xFFFFFFFFu ? F_INF : fkey_inv(cm);
+}
+
+// exact f64 re-rank of the M bound candidates (+ the tail's exact keys), top k,
+// certificate: cut > the k-th exact distance of the result (or fewer than k
+// rows exist and nothing was cut)
+template <int METRIC, typename T>
+__global__ __launch_bounds__(256) void flat_lb_refine_kernel(const T *__restrict__ X, int ld, int dim,
+                                                             const float *__restrict__ Qf,
+                                                             const uint64_t *__restrict__ ca, int M,
+                                                             const uint64_t *__restrict__ cbk, int kb,
+                                                             const float *__restrict__ cut, int k,
+                                                             const int64_t *__restrict__ labels,
+                                                             int64_t *__restrict__ outL, float *__restrict__ outD,
+                                                             int *__restrict__ outC, int *__restrict__ cert) {
+	__shared__ uint64_t sk[IVF_TOPK_CAP];
+	__shared__ uint32_t ss[IVF_TOPK_CAP];
+	__shared__ int n;
+	const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+	if (t == 0) n = 0;
+	__syncthreads();
+	for (int i = t; i < M + kb; i += 256) {
+		const uint64_t key = i < M ? ca[(int64_t)q * M + i] : cbk[(int64_t)q * kb + (i - M)];
+		if (key != KEY64_NONE) ss[atomicAdd(&n, 1)] = (uint32_t)key;
+	}
+	__syncthreads();
+	const int nc = n;
+	for (int i = w; i < nc; i += 4) {
+		const uint32_t slot = ss[i];
+		const float d = exact_distance<METRIC, T>(X + (int64_t)slot * ld, Qf + (int64_t)q * ld, dim, lane);
+		if (lane == 0) sk[i] = key64(d, slot);
+	}
+	const int np = pow2_ceil(nc);
+	__syncthreads();
+	for (int i = nc + t; i < np; i += 256) sk[i] = KEY64_NONE;
+	wg_bitonic_sort(sk, np);
+	const int nout = nc < k ? nc : k;
+	for (int i = t; i < k; i += 256) {
+		if (i < nout) {
+			outL[(int64_t)q * k + i] = labels[(uint32_t)sk[i]];
+			outD[(int64_t)q * k + i] = key64_dist(sk[i]);
+		} else {
+			outL[(int64_t)q * k + i] = -1;
+			outD[(int64_t)q * k + i] = __builtin_nanf("");
+		}
+	}
+	if (t == 0) {
+		outC[q] = nout;
+		const float cq = cut[q];
+		bool ok;
+		if (nout < k) ok = cq == F_INF;  // every row of the probed lists is a candidate
+		else ok = cq > key64_dist(sk[k - 1]);  // NaN cut or distance: false
+		cert[q] = ok ? 1 : 0;
+	}
+}
+
+size_t flat_lb_lds_bytes(int ld) { return (size_t)FL_G * (ld * 2 + 16) + (size_t)FL_G * FLAT_BLK * 8; }
+
+void launch_flat_list_lb(const StoreView &s, const int *blk_list, const int64_t *blk_pos0, const int *lblk0,
+                         const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart, const int *pairs,
+                         int nprobe, int maxb, const uint16_t *Qb, const float4 *qaux, uint64_t *out, hipStream_t st) {
+	if (nblk <= 0) return;
+	if (!s.scan_bf16 || s.ld % 64) throw std::runtime_error("IVF_FLAT bound scan needs bf16 scan rows");
+	const uint16_t *Xb = static_cast<const uint16_t *>(s.Xscan);
+	const float *ra = reinterpret_cast<const float *>(s.rowaux);
+	const size_t lds = flat_lb_lds_bytes(s.ld);
+	auto go = [&](auto kern) {
+		HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+		                           (int)lds));
+		kern<<<dim3((unsigned)nblk), 256, lds, st>>>(Xb, s.ld, ra, blk_list, blk_pos0, lblk0, loff, lslot, pstart,
+		                                              pairs, nprobe, maxb, Qb, qaux, out);
+	};
+	switch (s.metric) {
+	case METRIC_L2: go(flat_list_lb_kernel<METRIC_L2>); break;
+	case METRIC_DOT: go(flat_list_lb_kernel<METRIC_DOT>); break;
+	default: go(flat_list_lb_kernel<METRIC_COSINE>); break;
+	}
+}
+
+void launch_flat_lb_merge(int nq, int nprobe, const int64_t *probe_l, const int *lblk0, int maxb, const uint64_t *keys,
+                          int M, uint64_t *cand, float *cut, hipStream_t st) {
+	flat_lb_merge_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(nprobe, probe_l, lblk0, maxb, keys, M, cand, cut);
+}
+
+void launch_flat_lb_refine(const StoreView &s, const float *Qf, const uint64_t *ca, int M, const uint64_t *cb, int kb,
+                           const float *cut, int nq, int k, int64_t *outL, float *outD, int *outC, int *cert,
+                           hipStream_t st) {
+	dim3 grid((unsigned)nq);
+	auto go = [&](auto kern, auto X) {
+		kern<<<grid, 256, 0, st>>>(X, s.ld, s.dim, Qf, ca, M, cb, kb, cut, k, s.labels, outL, outD, outC, cert);
+	};
+	if (s.xbf16) {
+		const uint16_t *X = static_cast<const uint16_t *>(s.X);
+		if (s.metric == METRIC_L2) go(flat_lb_refine_kernel<METRIC_L2, uint16_t>, X);
+		else if (s.metric == METRIC_DOT) go(flat_lb_refine_kernel<METRIC_DOT, uint16_t>, X);
+		else go(flat_lb_refine_kernel<METRIC_COSINE, uint16_t>, X);
+	} else {
+		const float *X = static_cast<const float *>(s.X);
+		if (s.metric == METRIC_L2) go(flat_lb_refine_kernel<METRIC_L2, float>, X);
+		else if (s.metric == METRIC_DOT) go(flat_lb_refine_kernel<METRIC_DOT, float>, X);
+		else go(flat_lb_refine_kernel<METRIC_COSINE, float>, X);
+	}
+}
+
 template <typename T>
 static void flat_scan_dispatch(const StoreView &s, const int *blk_list, const int64_t *blk_pos0, const int *lblk0,
                                const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart,

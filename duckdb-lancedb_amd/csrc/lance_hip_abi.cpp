@@ -1062,6 +1062,12 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			ix->kmeans_iters = it;
 			return 0;
 		}
+		if (k == "ivf_flat_scan") {
+			if (v == "bound") ix->ivf_flat_bound = true;
+			else if (v == "exact") ix->ivf_flat_bound = false;
+			else throw Error("ivf_flat_scan must be 'bound' or 'exact'");
+			return 0;
+		}
 		if (k == "pq_scan") {
 			if (v == "fast") ix->pq_fast = true;
 			else if (v == "exact_lut") ix->pq_fast = false;

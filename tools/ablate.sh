@@ -7,7 +7,7 @@ D=duckdb-lancedb_amd
 F="-DLHIP_ABLATION_BUILD -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-inline-asm -Wno-unused-result"
 mkdir -p abl
 make -s -C $D  # the other objects of the library (lib/*.o)
-OTHERS="$D/lib/ivf_kernels.o $D/lib/lance_hip_abi.o $D/lib/ivf_index.o $D/lib/meta.o"
+OTHERS="$D/lib/rscan_kernels.o $D/lib/ivf_kernels.o $D/lib/lance_hip_abi.o $D/lib/ivf_index.o $D/lib/meta.o"
 build() { # name defines...
 	local n=$1; shift
 	hipcc $F "$@" -c $D/csrc/knn_kernels.hip -o abl/k_$n.o

@@ -3,9 +3,12 @@
 with the derived figures bench.py's roofline cites:
   HBM traffic   = 2 x FETCH_SIZE (gfx950 counts half of a wide streaming read,
                   MI355X_MICROARCH.md 'HBM') + WRITE_SIZE, KiB -> bytes
-  MFMA busy     = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x SIMDs): the
+  MFMA busy     = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x SIMDs): the
                   counter counts 32 cycles per v_mfma_f32_32x32x16_bf16 (same
-                  guide, cycle-constants table), summed over the chip's SIMDs
+                  guide, cycle-constants table), summed over the chip's SIMDs;
+                  GRBM_GUI_ACTIVE is the sum over the 8 XCDs (guide, 'DVFS
+                  give-back'), so / 8 is the kernel's cycles at the live clock
+  clock         = GRBM_GUI_ACTIVE / 8 / kernel time (with --kernel-ms)
 usage: tools/pmc_summary.py TAG KERNEL_SUBSTRING OUT.json [--simds 1024] [--meta k=v ...]
 """
 import argparse
@@ -23,6 +26,8 @@ def main():
     ap.add_argument("--simds", type=int, default=1024)
     ap.add_argument("--dir", default="gpurun_out")
     ap.add_argument("--meta", nargs="*", default=[])
+    ap.add_argument("--kernel-ms", type=float, default=None, help="average launch time (bench HIP events)")
+    ap.add_argument("--xcds", type=int, default=8)
     a = ap.parse_args()
     vals = {}
     names = set()
@@ -39,7 +44,10 @@ def main():
         d["hbm_write_bytes"] = avg["WRITE_SIZE"] * 1024.0
         d["traffic_bytes_per_launch"] = d["hbm_read_bytes"] + d["hbm_write_bytes"]
     if "SQ_VALU_MFMA_BUSY_CYCLES" in avg and "GRBM_GUI_ACTIVE" in avg:
-        d["mfma_busy_frac"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (avg["GRBM_GUI_ACTIVE"] * a.simds)
+        d["kernel_cycles"] = avg["GRBM_GUI_ACTIVE"] / a.xcds
+        d["mfma_busy_frac"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (d["kernel_cycles"] * a.simds)
+        if a.kernel_ms:
+            d["effective_clock_ghz"] = d["kernel_cycles"] / (a.kernel_ms * 1e-3) / 1e9
         d["mfma_count_from_busy"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / 32.0
     if "SQ_WAIT_INST_ANY" in avg and "SQ_WAVE_CYCLES" in avg:
         d["wait_inst_any_frac_of_wave_cycles"] = avg["SQ_WAIT_INST_ANY"] / avg["SQ_WAVE_CYCLES"]
