@@ -247,7 +247,9 @@ def main_ivf(a):
     if not h:
         raise RuntimeError(e.value.decode())
     lance_hip.LanceHipSetOption(h, "storage", a.storage)
-    lance_hip.LanceHipSetOption(h, "scan_copy", "off")
+    # IVF_FLAT's bound scan streams the bf16 scan copy (the exact re-rank reads
+    # the f32 rows); IVF_PQ scans codes only
+    lance_hip.LanceHipSetOption(h, "scan_copy", a.scan_copy if a.index_type == "ivf_flat" else "off")
     lance_hip.LanceHipSetOption(h, "reserve_rows", str(N))
     lance_hip.LanceHipSetOption(h, "index_type", a.index_type)
     if a.index_type == "ivf_pq":
@@ -386,7 +388,9 @@ def main_ivf(a):
             avg_ms = kt["ivf_scan_ms_total"] / kt["ivf_scan_launches"]
             bytes_launch = kt["ivf_scan_bytes"] / kt["ivf_scan_launches"]
             ach = bytes_launch / (avg_ms * 1e-3) / 1e9
-            kname = ("flat_list_scan_kernel" if a.index_type == "ivf_flat" else
+            bound_flat = a.index_type == "ivf_flat" and a.scan_copy == "on" and K <= 15 and \
+                "ivf_flat_scan=exact" not in a.opt
+            kname = (("flat_list_lb_kernel" if bound_flat else "flat_list_scan_kernel") if a.index_type == "ivf_flat" else
                      "pq_fast_scan_kernel" if fast_pq else "pq_query_scan_kernel")
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": ivf_traffic(a.config, N, D, BG), "kernel": kname,
