@@ -151,7 +151,7 @@ def test_filtered_ivf_search(hip, index_type):
                 el, ed, ec = ivf.ivf_flat_search(X, ex["labels"], m, ex["lists"], ex["centroids"], Q, 10, 6, "l2")
             else:
                 el, ed, ec = ivf.ivf_pq_search(X, ex["labels"], m, ex["lists"], ex["codes"], ex["centroids"],
-                                               ex["codebook"], Q, 10, 6, 3, "l2")
+                                               ex["codebook"], Q, 10, 6, 3, "l2", lut="u8")
             assert_same(gl, gd, gc, el, ed, ec)
     finally:
         hip.LanceFreeDetached(h)

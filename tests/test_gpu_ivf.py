@@ -205,3 +205,49 @@ def test_ivf_errors(hip, mk):
     # a failed build leaves the flat path serving exact results
     gl, gd, gc = hip.LanceDetachedSearchBatch(h, X[:3], 5)
     assert list(gl[:, 0]) == [0, 1, 2]
+
+
+@pytest.mark.parametrize("storage", ["f32", "bf16"])
+@pytest.mark.parametrize("metric", ["l2", "dot", "cosine"])
+def test_ivf_flat_bound_scan_matches_exact_scan(hip, mk, storage, metric):
+    """The MFMA bound scan (ivf_flat_scan = bound, the default with bf16 scan
+    rows) returns the exact list scan's results: same labels and distances as
+    the oracle, for f32 rows (bf16 scan copy) and a bf16 store."""
+    rng = np.random.default_rng(21)
+    n, d, nlist = 20_000, 128, 40
+    X = clustered(rng, n, d, centers=60)
+    if storage == "bf16":
+        import torch
+
+        X = torch.from_numpy(X).to(torch.bfloat16).float().numpy()
+    Q = (X[rng.choice(n, 90, replace=False)] + 0.3 * rng.standard_normal((90, d))).astype(np.float32)
+    h = mk(d, metric, "ivf_flat")
+    hip.LanceHipSetOption(h, "storage", storage)
+    hip.LanceDetachedAddBatch(h, X, n, d)
+    hip.LanceDetachedDeleteBatch(h, rng.choice(n, 500, replace=False))
+    hip.LanceDetachedCreateIndex(h, nlist, 0)
+    for nprobe, k in [(8, 10), (3, 1), (40, 15)]:
+        hip.LanceHipSetOption(h, "ivf_flat_scan", "bound")
+        gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, k, nprobes=nprobe)
+        el, ed, ec = oracle_search(hip, h, X, Q, k, nprobe, 1, metric)
+        assert_same(gl, gd, gc, el, ed, ec)
+        hip.LanceHipSetOption(h, "ivf_flat_scan", "exact")
+        xl, xd, xc = hip.LanceDetachedSearchBatch(h, Q, k, nprobes=nprobe)
+        assert_same(xl, xd, xc, el, ed, ec)
+
+
+def test_ivf_flat_bound_scan_ties_fall_back_exactly(hip, mk):
+    """Hundreds of identical rows in one list tie every bound at the k-th
+    distance: the certificate fails and the pass reruns on the exact scan,
+    which orders the ties by label."""
+    rng = np.random.default_rng(8)
+    n, d, nlist = 6_000, 64, 12
+    X = clustered(rng, n, d, centers=12)
+    X[100:900] = X[100]  # 800 copies
+    Q = np.stack([X[100] + 0.01, X[5], X[2000]]).astype(np.float32)
+    h = mk(d, "l2", "ivf_flat")
+    hip.LanceDetachedAddBatch(h, X, n, d)
+    hip.LanceDetachedCreateIndex(h, nlist, 0)
+    gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 10, nprobes=4)
+    el, ed, ec = oracle_search(hip, h, X, Q, 10, 4, 1, "l2")
+    assert_same(gl, gd, gc, el, ed, ec)
