@@ -148,7 +148,7 @@ def gen_clustered(start, stop, dim, device, centers, seed=1234):
     return out
 
 
-def measured_traffic(n, dim, batch, elem_bytes):
+def measured_traffic(n, dim, batch, elem_bytes, kernel=None):
     """Per-launch HBM bytes of the scan kernel from the committed rocprofv3 PMC
     passes (profiles/*_scan_traffic.json, made by tools/pmc_traffic.py from
     separate FETCH_SIZE / WRITE_SIZE runs of this bench) for the same shape."""
@@ -161,12 +161,13 @@ def measured_traffic(n, dim, batch, elem_bytes):
                 t = json.load(fh)
         except (OSError, ValueError):
             continue
-        if (t.get("n"), t.get("dim"), t.get("batch"), t.get("scan_elem_bytes", 4)) == (n, dim, batch, elem_bytes):
+        if (t.get("n"), t.get("dim"), t.get("batch"), t.get("scan_elem_bytes", 4)) == (n, dim, batch, elem_bytes) and \
+                (kernel is None or t.get("bench_kernel") == kernel):
             best = t
     return None if best is None else int(best["traffic_bytes_per_launch"])
 
 
-def ivf_traffic(config, n, dim, batch):
+def ivf_traffic(config, n, dim, batch, kernel=None):
     """Per-launch HBM bytes of the IVF list scan from the committed rocprofv3
     PMC passes of the same config (profiles/*_<config>_ivf_traffic.json, made by
     tools/pmc_passes.sh + tools/pmc_traffic.py)."""
@@ -179,7 +180,8 @@ def ivf_traffic(config, n, dim, batch):
                 t = json.load(fh)
         except (OSError, ValueError):
             continue
-        if (t.get("n"), t.get("dim"), t.get("batch")) == (n, dim, batch):
+        if (t.get("n"), t.get("dim"), t.get("batch")) == (n, dim, batch) and \
+                (kernel is None or t.get("bench_kernel") == kernel):
             best = t
     return None if best is None else int(best["traffic_bytes_per_launch"])
 
@@ -393,7 +395,7 @@ def main_ivf(a):
             kname = (("flat_list_lb_kernel" if bound_flat else "flat_list_scan_kernel") if a.index_type == "ivf_flat" else
                      "pq_fast_scan_kernel" if fast_pq else "pq_query_scan_kernel")
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": ivf_traffic(a.config, N, D, BG), "kernel": kname,
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": ivf_traffic(a.config, N, D, BG, kname), "kernel": kname,
                     "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(bytes_launch),
                     "pair_rows_per_launch": int(kt["ivf_pair_rows"] / kt["ivf_scan_launches"]),
                     "coarse_ms_per_batch": round(kt["ivf_coarse_ms_total"] / kt["ivf_scan_launches"], 4)}
@@ -648,7 +650,8 @@ def main():
             # algorithmic bytes per launch: every base row (ld elements + 16 B row aux) + the bf16 query tile
             bytes_launch = kt["scan_rows"] * (ld * esz + 16) + kt["scan_qpad"] * ld * 2
             ach = bytes_launch / (avg_ms * 1e-3) / 1e9
-            traffic = measured_traffic(N // world, D, BG, esz)
+            kstr = f"{kt['scan_kernel']}<{ {'l2': 'L2', 'dot': 'DOT', 'cosine': 'COSINE'}[a.metric]},append,{'bf16' if esz == 2 else 'f32'}>"
+            traffic = measured_traffic(N // world, D, BG, esz, kstr)
             mfma_tfs = 2.0 * kt["scan_rows"] * D * BG / (avg_ms * 1e-3) / 1e12
             kname = {"l2": "L2", "dot": "DOT", "cosine": "COSINE"}[a.metric]
             # the bounding roof: HBM time of the bytes vs dense-bf16 MFMA time of the flops
