@@ -16,6 +16,24 @@ static constexpr uint32_t KEY_INF = 0xFF800000u;  // ordered key of +inf
 static constexpr uint32_t KEY_NAN = 0xFFFFFFFFu;  // every NaN is canonicalised to this
 
 // ---------------------------------------------------------------------------
+// MFMA operand guard (gfx950, ROCm 7.2).  hipcc lets a VALU instruction right
+// after the last MFMAs of a tile overwrite one of their A / B operand VGPRs
+// (the epilogue's first v_mbcnt was allocated onto the A register of the
+// still-executing last MFMA, ~9 issue slots after it): the MFMA then read the
+// new value and one accumulator column came out wrong (wrong cosine bounds in
+// ~1 of 40 repeated searches; which kernel build shows it depends only on
+// register allocation).  A scheduling fence with 64 wait states between the
+// last MFMA and the first instruction after it closes the window: once per
+// tile, not per k-step (within the k-loop the next writes of the operand
+// registers are ds_reads, whose data lands much later than the MFMA reads).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void mfma_operand_guard() {
+	__builtin_amdgcn_sched_barrier(0);
+	asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+	__builtin_amdgcn_sched_barrier(0);
+}
+
+// ---------------------------------------------------------------------------
 // small helpers
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t fkey(float f) {

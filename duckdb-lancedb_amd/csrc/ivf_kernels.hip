@@ -322,6 +322,7 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(const T *__restrict_
 		}
 		__syncthreads();
 	}
+	mfma_operand_guard();
 	// epilogue: this lane's data row = rw + ni*32 + fr; centroids in registers
 #pragma unroll
 	for (int ni = 0; ni < 2; ++ni) {
@@ -425,6 +426,7 @@ __global__ __launch_bounds__(256) void kmeans_assign_f32_kernel(const T *__restr
 		if (s + 1 < nst) store(As[cur ^ 1], Bs[cur ^ 1]);
 		__syncthreads();
 	}
+	mfma_operand_guard();
 #pragma unroll
 	for (int ni = 0; ni < 2; ++ni) {
 		const int64_t row = rt0 + rw + ni * 32 + fr;
@@ -1168,6 +1170,7 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
 				}
 			}
 		}
+		mfma_operand_guard();
 		// keys -> LDS [query][row]
 		{
 			const float4 qa = qas[rr];

@@ -332,6 +332,9 @@ extern "C" int lhip_prof_read(unsigned long long *out, int reset) {
 #ifndef LHIP_SK_BF16
 #define LHIP_SK_BF16 64  // k per stage with a bf16 base: 64 (2 slots) or 32 (3 slots)
 #endif
+#ifndef LHIP_PF
+#define LHIP_PF 0  // bf16 base: each stage issue also touches the rows of the stage this many ahead into L2 (0 = off)
+#endif
 
 constexpr int SCAN_THREADS = 512;
 constexpr int SCAN_WAVES = SCAN_THREADS / 64;          // 8: 2 per SIMD, 256 registers each
@@ -361,14 +364,19 @@ struct ScanCfg {
 	static constexpr int QDMA = QST / 1024 / SCAN_WAVES;       // Q DMA instructions per wave and stage
 	static constexpr int ROWS_PER_DMA = 1024 / XROW;
 	static constexpr int QROWS_PER_DMA = 1024 / QROW;
-	static constexpr int DMA = XDMA + (LHIP_ABL_NO_QDMA ? 0 : QDMA);  // + 1 row aux on waves 0..3 at a tile's stage 0
+	// L2 prefetch distance in stages (bf16 rows only): one touch instruction per
+	// wave and stage issue, the youngest instruction of its issue group
+	static constexpr int PF = XB ? LHIP_PF : 0;
+	static constexpr int TCH = PF > 0 ? 1 : 0;
+	static constexpr int PF_BYTES = TCH * 1024;  // the touches' scratch (16 B per lane, shared by the waves)
+	static constexpr int DMA = XDMA + (LHIP_ABL_NO_QDMA ? 0 : QDMA) + TCH;  // + 1 row aux on waves 0..3 at a tile's stage 0
 	// survivor list per wave (8 B entries): f32 32, flushed after every tile by
 	// one counted store; bf16 256, kept across tiles and flushed (drained)
 	// only past FLUSH_AT entries, or at the end
 	static constexpr int WLIST = XB ? 256 : 32;
 	static constexpr int FLUSH_AT = XB ? WLIST - 64 : 0;
 	static constexpr int LIST_BYTES = SCAN_WAVES * WLIST * 8;
-	static constexpr int LDS = RING + RA_BYTES + CNT_BYTES + QA_BYTES + LIST_BYTES;
+	static constexpr int LDS = RING + RA_BYTES + CNT_BYTES + QA_BYTES + LIST_BYTES + PF_BYTES;
 	static_assert(LDS <= 160 * 1024, "LDS budget");
 	static_assert(XDMA * SCAN_WAVES * 1024 == XST && QDMA * SCAN_WAVES * 1024 == QST, "stages = whole DMA instructions");
 	static_assert((XROW == 128 || XROW == 64) && (QROW == 128 || QROW == 64), "swizzles below");
@@ -408,11 +416,29 @@ __device__ __forceinline__ void dma16s(const void *sbase, uint32_t voff, uint32_
 	const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32));
 	const uint64_t ub = ((uint64_t)hi << 32) | (uint64_t)lo;
 	if (NT)
-		asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2 nt" ::"s"(lds_addr), "v"(voff), "s"(ub)
+		asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt" ::"s"(lds_addr), "v"(voff), "s"(ub)
 		             : "memory", "m0");
 	else
-		asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds_addr), "v"(voff), "s"(ub)
+		asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds_addr), "v"(voff), "s"(ub)
 		             : "memory", "m0");
+}
+
+// L2 prefetch touch: one global_load_lds_dwordx4 (16 B per lane into scratch
+// LDS nobody reads) pulls the 64 B sector of each lane's address into L2
+// (and L1) without holding a VGPR: a dead VGPR destination would be written
+// back whenever the load returned, after the compiler had reused the register.
+// s_nop 4: the base may be fresh from v_readfirstlane (VALU SGPR write -> VMEM
+// read); s_nop 0: the M0 write -> LDS-DMA hazard (else the load may take the
+// previous M0, the last ring DMA's slot, and overwrite 1 KiB of it).  The same
+// dwordx4 form as the ring DMA: a global_load_lds_dword touch in the same vmcnt
+// stream gave wrong bounds (measured: counted waits no longer covered the ring).
+__device__ __forceinline__ void touch4s(const void *sbase, uint32_t voff, uint32_t lds_addr) {
+	const uint64_t b = (uint64_t)(uintptr_t)sbase;
+	const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+	const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32));
+	const uint64_t ub = ((uint64_t)hi << 32) | (uint64_t)lo;
+	asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds_addr), "v"(voff), "s"(ub)
+	             : "memory", "m0");
 }
 
 #define LHIP_WAIT_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
@@ -527,6 +553,25 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 	const uint16_t *iss_q = qbase;
 	uint32_t iss_lds = lds0;  // LDS slot of the next stage to issue
 	int iss_g = 0, iss_s = 0, iss_t = 0;
+	// Prefetch cursor: stage iss_g + PF (held at the last stage near the end,
+	// so every issue group has the same instruction count).  Lane -> row
+	// w*32 + lane%32, 64 B half lane/32 of the row's 128 B stage piece.
+	const uint8_t *pf_xtile = iss_xtile, *pf_xt = iss_xt;
+	int pf_g = 0, pf_s = 0;
+	auto pf_adv = [&]() {
+		if (pf_g + 1 >= G) return;
+		++pf_g;
+		if (++pf_s == S) {
+			pf_s = 0;
+			pf_xtile += tile_rows_step * ld * C::XE;
+			pf_xt = pf_xtile;
+		} else {
+			pf_xt += C::SK * C::XE;
+		}
+	};
+	for (int i = 0; i < C::PF; ++i) pf_adv();
+	const uint32_t pfoff = (uint32_t)((w * 32 + (lane & 31)) * ld * C::XE + (lane >> 5) * 64);
+	const uint32_t pf_lds = lds0 + (uint32_t)(C::LDS - C::PF_BYTES);
 	auto issue_one = [&]() {
 		if (iss_s == 0 && w < 4)
 			dma16s(iss_ra + w * 64, raoff, lds0 + C::RING + (uint32_t)(iss_t & 1) * RA_SLOT + (uint32_t)w * 1024u);
@@ -536,6 +581,10 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 #pragma unroll
 		for (int j = 0; j < (LHIP_ABL_NO_QDMA ? 0 : C::QDMA); ++j)
 			dma16s(iss_q, qoff[j], iss_lds + (uint32_t)C::XST + (uint32_t)(C::QDMA * w + j) * 1024u);
+		if (C::TCH) {
+			touch4s(pf_xt, pfoff, pf_lds);
+			pf_adv();
+		}
 		++iss_g;
 		iss_lds = iss_lds + C::STAGE == lds0 + C::RING ? lds0 : iss_lds + C::STAGE;
 		if (++iss_s == S) {
@@ -612,14 +661,15 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 	int fpos1 = -1, fpos2 = -1;
 	auto fl_younger = [&](int h) { return (fpos1 > h ? 1 : 0) + (fpos2 > h ? 1 : 0); };
 	auto wait_stage = [&](int h, int sh) {
+		// (+ TCH: stage h's own prefetch touch is issued after its DMA)
 		const int m = iss_g - 1 - h;
 		if (m <= 0) {
-			wait_vm(fl_younger(h));
+			wait_vm(C::TCH + fl_younger(h));
 			return;
 		}
 		const int d0 = S - 1 - sh;  // stages after h up to the next tile start, exclusive
 		const int n0 = ra_wave ? (d0 < m) + (d0 + S < m) : 0;
-		wait_vm(m * C::DMA + n0 + fl_younger(h));
+		wait_vm(m * C::DMA + C::TCH + n0 + fl_younger(h));
 	};
 
 	// This wave's survivor list: n_list entries (wave-uniform), possibly of
@@ -805,10 +855,10 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 			static_assert(C::NST >= 2 && C::NST <= 4, "steady-state wait counts below");
 			const bool st0 = C::NST >= 3 && (cur_s + 2 == S || (C::NST == 4 && (cur_s + 3 == S || (S == 2 && cur_s == 1))));
 			switch ((ra_wave && st0 ? 1 : 0) + fl_younger(g + 1)) {
-			case 0: wait_vm_c<(C::NST - 2) * C::DMA>(); break;
-			case 1: wait_vm_c<(C::NST - 2) * C::DMA + 1>(); break;
-			case 2: wait_vm_c<(C::NST - 2) * C::DMA + 2>(); break;
-			default: wait_vm_c<(C::NST - 2) * C::DMA + 3>(); break;
+			case 0: wait_vm_c<(C::NST - 2) * C::DMA + C::TCH>(); break;
+			case 1: wait_vm_c<(C::NST - 2) * C::DMA + C::TCH + 1>(); break;
+			case 2: wait_vm_c<(C::NST - 2) * C::DMA + C::TCH + 2>(); break;
+			default: wait_vm_c<(C::NST - 2) * C::DMA + C::TCH + 3>(); break;
 			}
 		} else if (g + 1 < G) {
 			wait_stage(g + 1, tile_end ? 0 : cur_s + 1);  // the last stages, or a held-back issue
@@ -839,6 +889,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 		read_k(F[0], rd_next, 0);
 		mfma_k(F[1]);
 		rd = rd_next;
+		if (tile_end) mfma_operand_guard();  // the epilogue follows the tile's last MFMAs
 		asm volatile("" ::: "memory");
 		PROF_T(t3);
 #if LHIP_PROF
@@ -1189,6 +1240,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 		atomicAdd(&lhip_prof[20 + (MODE == 1) * 2 + 1], (unsigned long long)prof_slown);
 	}
 #endif
+	// the last prefetch touches write the workgroup's LDS: land them before it can be reallocated
+	if (C::TCH) LHIP_WAIT_VM(0);
 	if (MODE >= 1) {
 		if (DEFER && pend) write_pending();
 		if (n_list > 0) write_list_all();  // what is left in the list

@@ -347,6 +347,7 @@ __global__ __launch_bounds__(RS_THREADS, 1) void rscan_kernel(const uint8_t *__r
 	};
 
 	auto epilogue = [&](int ti) __attribute__((always_inline)) {
+		mfma_operand_guard();
 		const float *RAs = reinterpret_cast<const float *>(smem + C::OFF_RA + (ti & 1) * C::RA_SLOT);
 		auto ra4 = [&](int r0, int c) __attribute__((always_inline)) {
 			return *reinterpret_cast<const float4 *>(RAs + c * RS_BR + r0);

@@ -52,6 +52,11 @@ for v in "$@"; do
 	
 	
 	
+	PF0) build PF0 -DLHIP_PF=0 ;;
+	PF1) build PF1 -DLHIP_PF=1 ;;
+	PF2) build PF2 -DLHIP_PF=2 ;;
+	PF4) build PF4 -DLHIP_PF=4 ;;
+	PF6) build PF6 -DLHIP_PF=6 ;;
 	PREV) # the committed (HEAD) kernel file, for same-box A/B timing
 		git show HEAD:$D/csrc/knn_kernels.hip > abl/prev_kernels.hip
 		hipcc $F -I$D/csrc -c abl/prev_kernels.hip -o abl/k_PREV.o
