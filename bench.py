@@ -647,27 +647,31 @@ def main():
             ld = ((D + 63) // 64) * 64
             esz = kt.get("scan_elem_bytes") or (2 if a.storage == "bf16" else 4)
             avg_ms = kt["scan_ms_total"] / kt["scan_launches"]
-            # algorithmic bytes per launch: every base row (ld elements + 16 B row aux) + the bf16 query tile
-            bytes_launch = kt["scan_rows"] * (ld * esz + 16) + kt["scan_qpad"] * ld * 2
+            # algorithmic bytes per launch: every base row (ld elements + 16 B row aux) + the query tile
+            # (bf16; int8 with the int8 scan copy)
+            bytes_launch = kt["scan_rows"] * (ld * esz + 16) + kt["scan_qpad"] * ld * (1 if esz == 1 else 2)
+            xname = {1: "i8", 2: "bf16"}.get(esz, "f32")
+            # dense MFMA peak of the scan's operand type (int8: 2x bf16)
+            mfma_peak = MFMA_BF16_PEAK_TFS * (2 if esz == 1 else 1)
             ach = bytes_launch / (avg_ms * 1e-3) / 1e9
-            kstr = f"{kt['scan_kernel']}<{ {'l2': 'L2', 'dot': 'DOT', 'cosine': 'COSINE'}[a.metric]},append,{'bf16' if esz == 2 else 'f32'}>"
+            kstr = f"{kt['scan_kernel']}<{ {'l2': 'L2', 'dot': 'DOT', 'cosine': 'COSINE'}[a.metric]},append,{xname}>"
             traffic = measured_traffic(N // world, D, BG, esz, kstr)
             mfma_tfs = 2.0 * kt["scan_rows"] * D * BG / (avg_ms * 1e-3) / 1e12
             kname = {"l2": "L2", "dot": "DOT", "cosine": "COSINE"}[a.metric]
             # the bounding roof: HBM time of the bytes vs dense-bf16 MFMA time of the flops
             # (N = 1: HBM; at N > 1 a 1/N shard meets N x the queries and MFMA can bind)
-            mfma_bound = (2.0 * kt["scan_rows"] * D * BG) / (MFMA_BF16_PEAK_TFS * 1e12) > bytes_launch / (HBM_PEAK_GBS * 1e9)
+            mfma_bound = (2.0 * kt["scan_rows"] * D * BG) / (mfma_peak * 1e12) > bytes_launch / (HBM_PEAK_GBS * 1e9)
             if mfma_bound:
-                roof = {"bound": "mfma", "achieved": round(mfma_tfs, 1), "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
-                        "frac": round(mfma_tfs / MFMA_BF16_PEAK_TFS, 4), "traffic": traffic,
+                roof = {"bound": "mfma", "achieved": round(mfma_tfs, 1), "peak": mfma_peak, "unit": "TFLOP/s",
+                        "frac": round(mfma_tfs / mfma_peak, 4), "traffic": traffic,
                         "hbm_gbs": round(ach, 1), "hbm_frac": round(ach / HBM_PEAK_GBS, 4)}
             else:
                 roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic}
             roof.update({
-                    "kernel": f"{kt['scan_kernel']}<{kname},append,{'bf16' if esz == 2 else 'f32'}>",
+                    "kernel": f"{kt['scan_kernel']}<{kname},append,{xname}>",
                     "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(bytes_launch),
-                    "mfma_tflops": round(mfma_tfs, 1), "mfma_frac": round(mfma_tfs / MFMA_BF16_PEAK_TFS, 4)})
+                    "mfma_tflops": round(mfma_tfs, 1), "mfma_frac": round(mfma_tfs / mfma_peak, 4)})
         if a.config == "c2":
             metric_name = "kNN queries/sec + recall@10, 1Mx768 f32 flat; GB/s vs HBM roofline"
         elif a.config == "nstar":

@@ -9,6 +9,8 @@ namespace lhip {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+typedef __attribute__((ext_vector_type(16))) int i32x16;
 
 static constexpr float F_INF = __builtin_huge_valf();
 static constexpr float F_MAX = 3.40282347e+38f;

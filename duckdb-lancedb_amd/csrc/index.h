@@ -163,6 +163,18 @@ struct Index {
 	bool scan_copy = true;
 	bool has_scan_copy() const { return !xbf16 && scan_copy; }
 	float4 *rowaux = nullptr;  // aux for `metric`
+	// int8 scan copy (option scan_i8): derived from X on demand (ensure_i8) and
+	// rebuilt after any change of the rows or tombstones (mut_ver); the flat
+	// scans stream it with rowaux8 as their row terms, everything else uses X
+	bool scan_i8 = true;
+	int last_scan_esz = 0;  // bytes per element the last flat search's scan streamed (1 int8, 2 bf16, 4 f32)
+	int8_t *Xq = nullptr;
+	float4 *rowaux8 = nullptr;
+	int64_t q8_cap = 0;
+	uint64_t mut_ver = 1, q8_ver = 0;
+	DevBuf<unsigned> stats8;
+	float max_alpha8 = 0.f, max_x8 = 0.f;
+	int cand_extra_i8 = 192;  // refined candidates with the int8 scan: k + max(cand_extra_i8, k) (looser bounds: at 10M x 768 up to ~110 rows lie below the 10th distance)
 	float4 *rowaux_l2 = nullptr;  // aux for L2 when metric_quirk is on and metric != l2
 	int64_t *dlabels = nullptr;
 	int64_t cap = 0, n_slots = 0;
@@ -233,6 +245,8 @@ struct Index {
 		(void)hipSetDevice(device);
 		if (X) (void)hipFree(X);
 		if (Xs) (void)hipFree(Xs);
+		if (Xq) (void)hipFree(Xq);
+		if (rowaux8) (void)hipFree(rowaux8);
 		if (rowaux) (void)hipFree(rowaux);
 		if (rowaux_l2) (void)hipFree(rowaux_l2);
 		if (dlabels) (void)hipFree(dlabels);
@@ -269,6 +283,7 @@ struct Index {
 	// grow the device store to hold at least `want` slots (contents preserved)
 	void reserve(int64_t want) {
 		if (want <= cap) return;
+		++mut_ver;
 		// capacity is a multiple of the scan tile and the tail past n_slots is
 		// zero: the scan kernel streams whole tiles without clamping rows
 		int64_t c = round_up(std::max<int64_t>(want, std::max<int64_t>(4096, cap * 2)), SCAN_BR);
@@ -345,8 +360,50 @@ struct Index {
 		HIPCHK(hipStreamSynchronize(stream));
 	}
 
+	// the int8 scan applies: an f32 store whose rows fit the int8 stages (ld a
+	// multiple of 128, exact integer dot products up to ld = 1024), no filter,
+	// ranking by the index metric
+	bool i8_usable() const {
+		return scan_i8 && !xbf16 && X && n_slots > 0 && ld % 128 == 0 && ld <= 1024 && !filter_on &&
+		       !(metric_quirk && metric != METRIC_L2);
+	}
+	// (re)build the int8 scan copy and its row terms from X when stale
+	void ensure_i8() {
+		if (Xq && q8_ver == mut_ver && q8_cap == cap) return;
+		if (!Xq || q8_cap != cap) {
+			if (Xq) HIPCHK(hipFree(Xq));
+			if (rowaux8) HIPCHK(hipFree(rowaux8));
+			Xq = nullptr;
+			rowaux8 = nullptr;
+			HIPCHK(hipMalloc(&Xq, (size_t)cap * ld));
+			HIPCHK(hipMalloc(&rowaux8, (size_t)cap * sizeof(float4)));
+			q8_cap = cap;
+		}
+		stats8.need(2);
+		HIPCHK(hipMemsetAsync(stats8.p, 0, 2 * sizeof(unsigned), stream));
+		HIPCHK(hipMemsetAsync(Xq + (size_t)n_slots * ld, 0, (size_t)(cap - n_slots) * ld, stream));
+		launch_rows_to_i8(static_cast<const float *>(X), ld, dim, metric, n_slots, rowaux, Xq, rowaux8, stats8.p,
+		                  stream);
+		launch_fill_rowaux(rowaux8, n_slots, cap, stream);
+		HIPCHK(hipGetLastError());
+		unsigned h[2];
+		HIPCHK(hipMemcpyAsync(h, stats8.p, sizeof(h), hipMemcpyDeviceToHost, stream));
+		HIPCHK(hipStreamSynchronize(stream));
+		memcpy(&max_alpha8, &h[0], 4);
+		memcpy(&max_x8, &h[1], 4);
+		q8_ver = mut_ver;
+	}
+	void drop_i8() {
+		if (Xq) HIPCHK(hipFree(Xq));
+		if (rowaux8) HIPCHK(hipFree(rowaux8));
+		Xq = nullptr;
+		rowaux8 = nullptr;
+		q8_cap = 0;
+	}
+
 	// append rows already resident on the device at X[n_slots .. n_slots+num)
 	int64_t commit_rows(int64_t num) {
+		++mut_ver;
 		const int64_t first = next_label;
 		std::vector<int64_t> labs((size_t)num);
 		for (int64_t i = 0; i < num; ++i) labs[(size_t)i] = first + i;
@@ -425,6 +482,7 @@ struct Index {
 	void set_storage(bool bf16) {
 		if (n_slots > 0) throw Error("storage can only be changed on an empty table");
 		if (bf16 == xbf16) return;
+		++mut_ver;
 		if (X) {
 			HIPCHK(hipFree(X));
 			if (Xs) HIPCHK(hipFree(Xs));
@@ -458,6 +516,7 @@ struct Index {
 			done.push_back(labels[i]);
 		}
 		if (!slots.empty()) {
+			++mut_ver;
 			ws.idx.need(slots.size());
 			HIPCHK(hipMemcpyAsync(ws.idx.p, slots.data(), slots.size() * sizeof(int64_t), hipMemcpyHostToDevice,
 			                      stream));
@@ -471,6 +530,7 @@ struct Index {
 
 	void compact() {
 		if (n_live == n_slots) return;
+		++mut_ver;
 		std::vector<int64_t> keep;
 		keep.reserve((size_t)n_live);
 		for (int64_t s = 0; s < n_slots; ++s)

@@ -37,13 +37,18 @@ struct StoreView {
 	// hold for either: ux covers |x - bf16(x)| with the same RNE rounding.
 	const void *Xscan;
 	int scan_bf16;
+	// int8 scan copy (option scan_i8): Xscan = int8 rows (stride ld bytes) and the
+	// scan kernels read scan_aux, its own row terms (alpha, |e_x|, |x~|, scale),
+	// instead of rowaux; null / 0 = rowaux and the bf16 / f32 rows above
+	const float4 *scan_aux = nullptr;
+	int scan_i8 = 0;
 };
 
 // Per-query constants for the lower-bound epilogue:
 //   LB = alpha + xn*B + ux*A + (s*sc)*S + C      (s = bf16 MFMA dot)
 struct QueryView {
 	const float *Qf;         // [nq_pad][ld] f32 queries, zero padded
-	const uint16_t *Qb;      // [nq_pad][ld] bf16 queries
+	const uint16_t *Qb;      // [nq_pad][ld] bf16 queries (int8 scan: int8 in the first ld bytes of each row)
 	const float4 *qaux;      // [nq_pad] (S, A, B, C)
 	int nq;
 	int nq_pad;              // multiple of SCAN_BQ
@@ -60,6 +65,12 @@ void launch_rowaux(const void *X, int xbf16, int ld, int dim, int metric, int64_
 // dst rows of stride ld, zero-filling columns [dim, ld).
 void launch_rows_to_bf16(const float *src, int64_t src_ld, int64_t n, int dim, int ld, uint16_t *dst, hipStream_t st);
 
+// int8 scan copy of slots [0, n) of an f32 store: int8 rows Xq (stride ld
+// bytes, zero padded) and their row terms aux8 (tombstones copied from
+// rowaux); stats[0] = max |alpha|, stats[1] = max(xn, ux) as float bits.
+void launch_rows_to_i8(const float *X, int ld, int dim, int metric, int64_t n, const float4 *rowaux, int8_t *Xq,
+                       float4 *aux8, unsigned *stats, hipStream_t st);
+
 // rowaux[from, to) = (+inf, 0, 0, 0): padding rows past the last slot.
 void launch_fill_rowaux(float4 *rowaux, int64_t from, int64_t to, hipStream_t st);
 
@@ -71,6 +82,10 @@ void launch_filter_rowaux(const float4 *src, const uint8_t *mask, int64_t n_slot
                           hipStream_t st);
 
 // ---- search ------------------------------------------------------------------
+// int8 scan (scan_i8): int8 queries into Qb's rows (first ld bytes of each
+// 2*ld-byte row) and the int8 bound's constants; Qf and zero3 as below.
+void launch_prep_queries_i8(const float *Q, int nq, int dim, int ld, int nq_pad, int metric, float max_alpha,
+                            float max_x, float *Qf, uint16_t *Qb, float4 *qaux, int *zero3, hipStream_t st);
 // Also zeroes zero3[0 .. 3*nq) when non-null (the search's status words).
 void launch_prep_queries(const float *Q, int nq, int dim, int ld, int nq_pad, int metric, float max_alpha,
                          float max_ux, float *Qf, uint16_t *Qb, float4 *qaux, int *zero3, hipStream_t st);
@@ -160,10 +175,11 @@ void launch_small_exact(const StoreView &s, const float *Q, int nq, int k, void 
 
 // Second threshold pass of failed queries fq[0..nf): packs their prepared
 // query rows into Qf2/Qb2/qaux2 (nf_pad rows, pads zero), tau2[i] = min(tau,
-// first-pass k-th exact distance), zeroes status2 = [cert | cnt | pool] x nf.
+// first-pass k-th exact distance) (keep_tau: tau itself — a rerun that only
+// widens the selection), zeroes status2 = [cert | cnt | pool] x nf.
 void launch_retry_gather(const int *fq, int nf, int nf_pad, int ld, int k, const QueryView &q, const float *tau,
                          const float *dists, float *Qf2, uint16_t *Qb2, float4 *qaux2, float *tau2, int *status2,
-                         hipStream_t st);
+                         hipStream_t st, int keep_tau = 0);
 // Writes back the rerun results of the queries the rerun certified; for the
 // others tau[q] = min(tau2, rerun k-th exact distance) for a further rerun.
 void launch_retry_scatter(const int *fq, int nf, int k, const int64_t *L2, const float *D2, const int *C2,

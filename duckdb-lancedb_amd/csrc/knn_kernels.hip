@@ -104,6 +104,81 @@ void launch_rows_to_bf16(const float *src, int64_t src_ld, int64_t n, int dim, i
 	rows_to_bf16_kernel<<<dim3((unsigned)n), dim3(256), 0, st>>>(src, src_ld, n, dim, ld, dst);
 }
 
+// ---------------------------------------------------------------------------
+// int8 scan copy (option scan_i8, an f32 store): per row x^ = rint(x * 127 /
+// max|x_i|) in [-127, 127], scale s = max|x_i| / 127 (an f32 value), x~ = s*x^.
+// The int8 scan's rigorous bound (scan_kernel XT = 2):
+//   |x.q - s_x s_q (x^.q^)| <= |e_x||q| + |x~||e_q|,   e_x = x - x~  (f64, exact)
+// and x^.q^ is an exact integer (|x^.q^| <= ld * 127^2 < 2^24 for ld <= 1024:
+// exact in f32 too).  Row terms (tile-blocked SoA like rowaux):
+//   l2: (|x|^2, |e_x|, |x~|, s)   dot: (0, |e_x|, |x~|, s)
+//   cosine: (0, |e_x|/|x|, |x~|/|x|, s/|x|)   (norms rounded up)
+// alpha copies the store's tombstones (+inf); a zero cosine row is NaN (exact
+// fallback), as in rowaux.  stats[0] = max |alpha|, stats[1] = max(xn, ux).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rows_to_i8_kernel(const float *__restrict__ X, int ld, int dim, int metric,
+                                                         int64_t n, const float4 *__restrict__ rowaux,
+                                                         int8_t *__restrict__ Xq, float4 *__restrict__ aux8,
+                                                         unsigned *__restrict__ stats) {
+	const int lane = threadIdx.x & 63;
+	const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+	if (r >= n) return;
+	const float *x = X + r * (int64_t)ld;
+	float m = 0.f;
+	for (int i = lane; i < dim; i += 64) m = fmaxf(m, fabsf(x[i]));
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+	const float sx = m / 127.0f;
+	const float inv = m > 0.f ? 127.0f / m : 0.f;
+	double s2 = 0.0, e2 = 0.0, t2 = 0.0;
+	int8_t *xq = Xq + r * (int64_t)ld;
+	for (int i = lane; i < ld; i += 64) {
+		int qv = 0;
+		if (i < dim) {
+			const float v = x[i];
+			qv = min(127, max(-127, (int)rintf(v * inv)));
+			const double xt = (double)sx * (double)qv;
+			const double e = (double)v - xt;
+			s2 += (double)v * v;
+			e2 += e * e;
+			t2 += xt * xt;
+		}
+		xq[i] = (int8_t)qv;
+	}
+	s2 = wave_sum_f64(s2);
+	e2 = wave_sum_f64(e2);
+	t2 = wave_sum_f64(t2);
+	if (lane != 0) return;
+	const double up = 1.0 + 4.0 * U_BOUND;
+	const double xn = sqrt(s2), ex = sqrt(e2) * up, xt = sqrt(t2) * up;
+	float4 a;
+	if (metric == METRIC_L2) {
+		a = make_float4((float)s2, (float)ex, (float)xt, sx);
+	} else if (metric == METRIC_DOT) {
+		a = make_float4(0.0f, (float)ex, (float)xt, sx);
+	} else if (xn > 0.0) {
+		a = make_float4(0.0f, (float)(ex / xn * up), (float)(xt / xn * up), (float)(sx / xn));
+	} else {
+		a = make_float4(__builtin_nanf(""), 0.0f, 0.0f, 0.0f);
+	}
+	const float *ra = reinterpret_cast<const float *>(rowaux);
+	if (__builtin_isinf(ra[raix(r, 0)])) a.x = F_INF;  // tombstone
+	float *o = reinterpret_cast<float *>(aux8);
+	o[raix(r, 0)] = a.x;
+	o[raix(r, 1)] = a.y;
+	o[raix(r, 2)] = a.z;
+	o[raix(r, 3)] = a.w;
+	if (a.x == a.x && a.x != F_INF) atomicMax(&stats[0], __float_as_uint(fabsf(a.x)));
+	if (a.y == a.y) atomicMax(&stats[1], __float_as_uint(fmaxf(a.y, a.z)));
+}
+
+void launch_rows_to_i8(const float *X, int ld, int dim, int metric, int64_t n, const float4 *rowaux, int8_t *Xq,
+                       float4 *aux8, unsigned *stats, hipStream_t st) {
+	if (n <= 0) return;
+	rows_to_i8_kernel<<<dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st>>>(X, ld, dim, metric, n, rowaux, Xq, aux8,
+	                                                                       stats);
+}
+
 __global__ void fill_rowaux_kernel(float4 *rowaux, int64_t from, int64_t to) {
 	const int64_t i = from + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if (i < to) {
@@ -217,6 +292,84 @@ void launch_prep_queries(const float *Q, int nq, int dim, int ld, int nq_pad, in
                          float max_ux, float *Qf, uint16_t *Qb, float4 *qaux, int *zero3, hipStream_t st) {
 	prep_queries_kernel<<<dim3(nq_pad), dim3(256), 0, st>>>(Q, nq, dim, ld, metric, max_alpha, max_ux, Qf, Qb,
 	                                                           qaux, zero3);
+}
+
+// int8 scan queries: Qf as prep_queries; Qi = int8 q^ = rint(q * 127 / max|q_i|)
+// in the first ld bytes of each 2*ld-byte row of the Qb buffer (so the retry
+// gather copies it like a bf16 row); per-query constants of the int8 bound
+// (rows_to_i8_kernel): LB = alpha + xn*B + ux*A + (s*sc)*S + C with
+//   l2: S = -2 s_q, A = -2|e_q|, B = -2|q|, C = |q|^2 - slack
+//   dot: S = -s_q, A = -|e_q|, B = -|q|, C = 1 - slack
+//   cosine: S = -s_q/|q|, A = -|e_q|/|q|, B = -1, C = 1 - slack
+// slack: f32 evaluation of the five-term sum, every intermediate bounded by
+// max_alpha + |q|^2 + 4 max_x (|q| + |e_q|) (max_x = max over rows of xn, ux).
+__global__ __launch_bounds__(256) void prep_queries_i8_kernel(const float *__restrict__ Q, int nq, int dim, int ld,
+                                                              int metric, float max_alpha, float max_x,
+                                                              float *__restrict__ Qf, int8_t *__restrict__ Qi,
+                                                              float4 *__restrict__ qaux, int *__restrict__ zero3) {
+	__shared__ double red[2][4];
+	__shared__ float redm[4];
+	const int q = blockIdx.x;
+	const int t = threadIdx.x;
+	if (zero3 && t < 3 && q < nq) zero3[t * nq + q] = 0;
+	float m = 0.f;
+	for (int i = t; i < ld; i += 256) {
+		const float v = (q < nq && i < dim) ? Q[(int64_t)q * dim + i] : 0.0f;
+		Qf[(int64_t)q * ld + i] = v;
+		m = fmaxf(m, fabsf(v));
+	}
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+	if ((t & 63) == 0) redm[t >> 6] = m;
+	__syncthreads();
+	m = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
+	const float sq = m / 127.0f;
+	const float inv = m > 0.f ? 127.0f / m : 0.f;
+	double s2 = 0.0, e2 = 0.0;
+	for (int i = t; i < ld; i += 256) {
+		const float v = (q < nq && i < dim) ? Q[(int64_t)q * dim + i] : 0.0f;
+		const int qv = min(127, max(-127, (int)rintf(v * inv)));
+		Qi[(int64_t)q * ld * 2 + i] = (int8_t)qv;
+		const double e = (double)v - (double)sq * (double)qv;
+		s2 += (double)v * v;
+		e2 += e * e;
+	}
+	s2 = wave_sum_f64(s2);
+	e2 = wave_sum_f64(e2);
+	if ((t & 63) == 0) {
+		red[0][t >> 6] = s2;
+		red[1][t >> 6] = e2;
+	}
+	__syncthreads();
+	if (t != 0) return;
+	s2 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+	e2 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+	if (q >= nq) {
+		qaux[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+		return;
+	}
+	const double u = U_BOUND, up = 1.0 + 4.0 * u;
+	const double qn = sqrt(s2), qnu = qn * up, equ = sqrt(e2) * up;
+	float4 a;
+	if (metric == METRIC_L2) {
+		const double slack = 16.0 * u * ((double)max_alpha + s2 + 4.0 * (double)max_x * (qnu + equ)) + 1e-30;
+		a = make_float4(-2.0f * sq, (float)(-2.0 * equ), (float)(-2.0 * qnu), (float)(s2 - slack));
+	} else if (metric == METRIC_DOT) {
+		const double slack = 16.0 * u * (1.0 + 4.0 * (double)max_x * (qnu + equ)) + 1e-30;
+		a = make_float4(-sq, (float)(-equ), (float)(-qnu), (float)(1.0 - slack));
+	} else if (qn > 0.0) {
+		const double slack = 16.0 * u * (2.0 + 4.0 * (double)max_x * (1.0 + equ / qn) * up) + 1e-30;
+		a = make_float4((float)(-(double)sq / qn), (float)(-(equ / qn) * up), -1.0f, (float)(1.0 - slack));
+	} else {
+		a = make_float4(0.f, 0.f, 0.f, __builtin_nanf(""));  // undefined: exact fallback
+	}
+	qaux[q] = a;
+}
+
+void launch_prep_queries_i8(const float *Q, int nq, int dim, int ld, int nq_pad, int metric, float max_alpha,
+                            float max_x, float *Qf, uint16_t *Qb, float4 *qaux, int *zero3, hipStream_t st) {
+	prep_queries_i8_kernel<<<dim3(nq_pad), dim3(256), 0, st>>>(Q, nq, dim, ld, metric, max_alpha, max_x, Qf,
+	                                                              reinterpret_cast<int8_t *>(Qb), qaux, zero3);
 }
 
 constexpr int BR = SCAN_BR, BQ = SCAN_BQ;
@@ -345,19 +498,23 @@ constexpr int QA_BYTES = BQ * 16 + BQ * 4;             // per-query bound consta
 static_assert(RA_SLOT / 1024 == 4 && SCAN_WAVES >= 4, "row aux: one DMA instruction on waves 0..3");
 static_assert(SCAN_WAVES == 8, "8 waves: 4 row quarters x 2 query halves");
 
-// per base element type: f32 store (XB = false) or bf16 store / scan copy (XB = true)
-template <bool XB>
+// per scanned element type XT: 0 = f32 store, 1 = bf16 store / scan copy,
+// 2 = int8 scan copy (per-row scale; int8 queries, v_mfma_i32_32x32x32_i8)
+template <int XT>
 struct ScanCfg {
-	static constexpr int SK = XB ? LHIP_SK_BF16 : 32;          // k per stage
-	static constexpr int KQ = SK / 16;                         // MFMA k-steps per stage: 4 / 2
-	static constexpr int XE = XB ? 2 : 4;                      // bytes per base element
+	static constexpr bool XB = XT != 0;                        // 16 B operand chunks straight from LDS
+	static constexpr bool I8 = XT == 2;
+	static constexpr int SK = I8 ? 128 : XB ? LHIP_SK_BF16 : 32;  // k per stage
+	static constexpr int KQ = SK / (I8 ? 32 : 16);             // MFMA k-steps per stage: 4 / 4 / 2
+	static constexpr int XE = I8 ? 1 : XB ? 2 : 4;             // bytes per base element
 	static constexpr int XROW = SK * XE;                       // bytes per row and stage: 128
 	static constexpr int XCH = XROW / 16;                      // 16 B chunks per row
 	static constexpr int XST = BR * XROW;                      // 32 KiB
-	static constexpr int QROW = SK * 2;                        // bytes per query and stage: 128 / 64
+	static constexpr int QE = I8 ? 1 : 2;                      // bytes per query element
+	static constexpr int QROW = SK * QE;                       // bytes per query and stage: 128 / 64
 	static constexpr int QCH = QROW / 16;
 	static constexpr int QST = BQ * QROW;                      // 32 / 16 KiB
-	static constexpr int NST = XB ? (SK == 64 ? 2 : LHIP_NST_BF16_32) : 3;  // ring slots
+	static constexpr int NST = XB ? (SK == 64 || I8 ? 2 : LHIP_NST_BF16_32) : 3;  // ring slots
 	static constexpr int STAGE = XST + QST;
 	static constexpr int RING = NST * STAGE;                   // 128 / 144 KiB
 	static constexpr int XDMA = XST / 1024 / SCAN_WAVES;       // X DMA instructions per wave and stage
@@ -390,12 +547,12 @@ struct ScanCfg {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-template <int METRIC>
+template <int METRIC, bool SC = false>
 __device__ __forceinline__ float lower_bound(float s, float4 ra, float4 qa) {
-	// LB = alpha + xn*B + ux*A + (s*sc)*S + C
+	// LB = alpha + xn*B + ux*A + (s*sc)*S + C   (sc: cosine 1/|x|, int8 scan the row scale)
 	float v = fmaf(ra.y, qa.z, ra.x);
 	v = fmaf(ra.z, qa.y, v);
-	float ss = (METRIC == METRIC_COSINE) ? s * ra.w : s;
+	float ss = (METRIC == METRIC_COSINE || SC) ? s * ra.w : s;
 	v = fmaf(ss, qa.x, v);
 	return v + qa.w;
 }
@@ -487,7 +644,7 @@ __device__ __forceinline__ int lane_id_fresh() {
 	return (int)__builtin_amdgcn_mbcnt_hi(m, __builtin_amdgcn_mbcnt_lo(m, 0u));
 }
 
-template <int METRIC, int MODE, bool XB>
+template <int METRIC, int MODE, int XT>
 __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__restrict__ Xv,
                                                                const float4 *__restrict__ rowaux, int ld,
                                                                const uint16_t *__restrict__ Qb,
@@ -497,7 +654,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
                                                                const float *__restrict__ tau,
                                                                uint2 *__restrict__ seg_pool,
                                                                int *__restrict__ seg_cnt, int seg_cap) {
-	using C = ScanCfg<XB>;
+	using C = ScanCfg<XT>;
+	constexpr bool XB = C::XB, I8 = C::I8;
 	__shared__ __attribute__((aligned(16))) uint8_t smem[C::LDS];
 	unsigned *CNT = reinterpret_cast<unsigned *>(smem + C::RING + RA_BYTES);
 	float4 *QA = reinterpret_cast<float4 *>(smem + C::RING + RA_BYTES + CNT_BYTES);
@@ -542,15 +700,15 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 #pragma unroll
 	for (int j = 0; j < C::QDMA; ++j) {
 		const int qr = (C::QDMA * w + j) * C::QROWS_PER_DMA + lane / C::QCH;
-		qoff[j] = (uint32_t)(qr * ld + (C::qswz(qr, lane % C::QCH) << 3)) * 2u;
+		qoff[j] = (uint32_t)(qr * ld * 2 + (C::qswz(qr, lane % C::QCH) << 4));  // query rows: 2*ld bytes apart
 	}
 	const uint32_t raoff = (uint32_t)lane * 16u;
 	const int64_t tile_rows_step = (int64_t)gridDim.x * tile_stride * BR;  // rows between this workgroup's tiles
-	const uint16_t *qbase = Qb + (int64_t)q0 * ld;
+	const uint8_t *qbase = reinterpret_cast<const uint8_t *>(Qb + (int64_t)q0 * ld);
 	const uint8_t *iss_xtile = X + (int64_t)blockIdx.x * tile_stride * BR * ld * C::XE;
 	const uint8_t *iss_xt = iss_xtile;
 	const float4 *iss_ra = rowaux + (int64_t)blockIdx.x * tile_stride * BR;
-	const uint16_t *iss_q = qbase;
+	const uint8_t *iss_q = qbase;
 	uint32_t iss_lds = lds0;  // LDS slot of the next stage to issue
 	int iss_g = 0, iss_s = 0, iss_t = 0;
 	// Prefetch cursor: stage iss_g + PF (held at the last stage near the end,
@@ -596,7 +754,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 			iss_q = qbase;
 		} else {
 			iss_xt += C::SK * C::XE;
-			iss_q += C::SK;
+			iss_q += C::SK * C::QE;
 		}
 	};
 
@@ -605,8 +763,13 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 	// terms (FOLD: alpha + C + xn*B + ux*A by two exact f32 MFMAs) and the
 	// bf16 MFMAs add S*s (queries pre-scaled by S), so at the tile end the
 	// accumulator IS the lower bound; cosine (per-row scale) starts at 0.
-	constexpr bool FOLD = METRIC != METRIC_COSINE;
+	// (int8: integer accumulators, scaled per row in the epilogue; kept as f32x16 bits)
+	constexpr bool FOLD = METRIC != METRIC_COSINE && !I8;
+	constexpr bool SCL = METRIC == METRIC_COSINE || I8;  // epilogue multiplies the dot product by the row's sc
 	f32x16 acc[2][4];
+	auto accf = [&](int t, int u, int r) -> float {
+		return I8 ? (float)__float_as_int(acc[t][u][r]) : acc[t][u][r];
+	};
 	auto init_acc = [&](int ti) {
 		if (!FOLD) {
 #pragma unroll
@@ -796,6 +959,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 			for (int u = 0; u < 4; ++u) {
 				if (LHIP_ABL_NO_MFMA)
 					asm volatile("" ::"v"(av), "v"(f.b[u]));
+				else if (I8)
+					acc[t][u] = __builtin_bit_cast(
+					    f32x16, __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, av),
+					                                                  __builtin_bit_cast(i32x4, f.b[u]),
+					                                                  __builtin_bit_cast(i32x16, acc[t][u]), 0, 0, 0));
 				else
 					acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, f.b[u], acc[t][u], 0, 0, 0);
 			}
@@ -935,10 +1103,10 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 						}
 						const float4 al = ra4(r0, 0), xn = ra4(r0, 1), ux = ra4(r0, 2), sc = ra4(r0, 3);
 						*reinterpret_cast<float4 *>(dst + r0) = make_float4(
-						    lower_bound<METRIC>(acc[t][u][4 * gq + 0], make_float4(al.x, xn.x, ux.x, sc.x), qa),
-						    lower_bound<METRIC>(acc[t][u][4 * gq + 1], make_float4(al.y, xn.y, ux.y, sc.y), qa),
-						    lower_bound<METRIC>(acc[t][u][4 * gq + 2], make_float4(al.z, xn.z, ux.z, sc.z), qa),
-						    lower_bound<METRIC>(acc[t][u][4 * gq + 3], make_float4(al.w, xn.w, ux.w, sc.w), qa));
+						    lower_bound<METRIC, I8>(accf(t, u, 4 * gq + 0), make_float4(al.x, xn.x, ux.x, sc.x), qa),
+						    lower_bound<METRIC, I8>(accf(t, u, 4 * gq + 1), make_float4(al.y, xn.y, ux.y, sc.y), qa),
+						    lower_bound<METRIC, I8>(accf(t, u, 4 * gq + 2), make_float4(al.z, xn.z, ux.z, sc.z), qa),
+						    lower_bound<METRIC, I8>(accf(t, u, 4 * gq + 3), make_float4(al.w, xn.w, ux.w, sc.w), qa));
 					}
 			}
 		} else if (MODE == 2) {
@@ -958,10 +1126,10 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 						if (!FOLD) al = ra4(r0, 0), xn = ra4(r0, 1), ux = ra4(r0, 2), sc = ra4(r0, 3);
 #pragma unroll
 						for (int j = 0; j < 4; ++j) {
-							const float a = acc[t][u][4 * gq + j];
+							const float a = accf(t, u, 4 * gq + j);
 							const float lb =
 							    FOLD ? a
-							         : lower_bound<METRIC>(a,
+							         : lower_bound<METRIC, I8>(a,
 							                               j == 0   ? make_float4(al.x, xn.x, ux.x, sc.x)
 							                               : j == 1 ? make_float4(al.y, xn.y, ux.y, sc.y)
 							                               : j == 2 ? make_float4(al.z, xn.z, ux.z, sc.z)
@@ -1017,7 +1185,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 					}
 					const float4 al = FOLD ? make_float4(0.f, 0.f, 0.f, 0.f) : ra4(r0, 0);
 					const float4 xn = FOLD ? al : ra4(r0, 1), ux = FOLD ? al : ra4(r0, 2);
-					const float4 sc = (METRIC == METRIC_COSINE) ? ra4(r0, 3) : make_float4(1.f, 1.f, 1.f, 1.f);
+					const float4 sc = SCL ? ra4(r0, 3) : make_float4(1.f, 1.f, 1.f, 1.f);
 #pragma unroll
 					for (int u = 0; u < 4 && !FOLD; ++u) {
 						const f32x2 Bq = {qa[u].z, qa[u].z}, Aq = {qa[u].y, qa[u].y}, Sq = {qa[u].x, qa[u].x};
@@ -1027,8 +1195,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 							const f32x2 a2 = p ? f32x2{al.z, al.w} : f32x2{al.x, al.y};
 							const f32x2 x2 = p ? f32x2{xn.z, xn.w} : f32x2{xn.x, xn.y};
 							const f32x2 u2 = p ? f32x2{ux.z, ux.w} : f32x2{ux.x, ux.y};
-							f32x2 s2 = {acc[t][u][4 * gq + 2 * p], acc[t][u][4 * gq + 2 * p + 1]};
-							if (METRIC == METRIC_COSINE) s2 = s2 * (p ? f32x2{sc.z, sc.w} : f32x2{sc.x, sc.y});
+							f32x2 s2 = {accf(t, u, 4 * gq + 2 * p), accf(t, u, 4 * gq + 2 * p + 1)};
+							if (SCL) s2 = s2 * (p ? f32x2{sc.z, sc.w} : f32x2{sc.x, sc.y});
 							// = lower_bound(): alpha + xn*B + ux*A + (s*sc)*S + C
 							f32x2 y = __builtin_elementwise_fma(x2, Bq, a2);
 							y = __builtin_elementwise_fma(u2, Aq, y);
@@ -1265,25 +1433,26 @@ static int num_cus() {
 
 int scan_grid(int64_t n_tiles) { return (int)std::min<int64_t>(n_tiles, (int64_t)num_cus()); }
 
-template <int MODE, bool XB>
+template <int MODE, int XT>
 static void scan_dispatch_x(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, float *dense,
                             int64_t ld_out, const float *tau, uint2 *seg_pool, int *seg_cnt, int seg_cap,
                             hipStream_t st) {
 	dim3 grid((unsigned)scan_grid(n_tiles), (unsigned)(q.nq_pad / BQ));
 	dim3 block(SCAN_THREADS);
+	const float4 *saux = s.scan_aux ? s.scan_aux : s.rowaux;
 	switch (s.metric) {
 	case METRIC_L2:
-		scan_kernel<METRIC_L2, MODE, XB><<<grid, block, 0, st>>>(s.Xscan, s.rowaux, s.ld, q.Qb, q.qaux, q.nq, (int)n_tiles,
+		scan_kernel<METRIC_L2, MODE, XT><<<grid, block, 0, st>>>(s.Xscan, saux, s.ld, q.Qb, q.qaux, q.nq, (int)n_tiles,
 		                                                          (int)tile_stride, dense, ld_out, tau, seg_pool,
 		                                                          seg_cnt, seg_cap);
 		break;
 	case METRIC_DOT:
-		scan_kernel<METRIC_DOT, MODE, XB><<<grid, block, 0, st>>>(s.Xscan, s.rowaux, s.ld, q.Qb, q.qaux, q.nq, (int)n_tiles,
+		scan_kernel<METRIC_DOT, MODE, XT><<<grid, block, 0, st>>>(s.Xscan, saux, s.ld, q.Qb, q.qaux, q.nq, (int)n_tiles,
 		                                                           (int)tile_stride, dense, ld_out, tau, seg_pool,
 		                                                           seg_cnt, seg_cap);
 		break;
 	default:
-		scan_kernel<METRIC_COSINE, MODE, XB><<<grid, block, 0, st>>>(s.Xscan, s.rowaux, s.ld, q.Qb, q.qaux, q.nq,
+		scan_kernel<METRIC_COSINE, MODE, XT><<<grid, block, 0, st>>>(s.Xscan, saux, s.ld, q.Qb, q.qaux, q.nq,
 		                                                              (int)n_tiles, (int)tile_stride, dense, ld_out,
 		                                                              tau, seg_pool, seg_cnt, seg_cap);
 		break;
@@ -1294,10 +1463,14 @@ template <int MODE>
 static void scan_dispatch(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, float *dense,
                           int64_t ld_out, const float *tau, uint2 *seg_pool, int *seg_cnt, int seg_cap,
                           hipStream_t st) {
-	if (s.scan_bf16)
-		scan_dispatch_x<MODE, true>(s, q, n_tiles, tile_stride, dense, ld_out, tau, seg_pool, seg_cnt, seg_cap, st);
-	else
-		scan_dispatch_x<MODE, false>(s, q, n_tiles, tile_stride, dense, ld_out, tau, seg_pool, seg_cnt, seg_cap, st);
+	if (s.scan_i8) {
+		if (s.ld % 128) throw std::runtime_error("int8 scan: row stride must be a multiple of 128");
+		scan_dispatch_x<MODE, 2>(s, q, n_tiles, tile_stride, dense, ld_out, tau, seg_pool, seg_cnt, seg_cap, st);
+	} else if (s.scan_bf16) {
+		scan_dispatch_x<MODE, 1>(s, q, n_tiles, tile_stride, dense, ld_out, tau, seg_pool, seg_cnt, seg_cap, st);
+	} else {
+		scan_dispatch_x<MODE, 0>(s, q, n_tiles, tile_stride, dense, ld_out, tau, seg_pool, seg_cnt, seg_cap, st);
+	}
 }
 
 void launch_scan_dense(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, float *out,
@@ -2162,7 +2335,8 @@ __global__ __launch_bounds__(256) void retry_gather_kernel(const int *__restrict
                                                            const float *__restrict__ tau,
                                                            const float *__restrict__ dists, float *__restrict__ Qf2,
                                                            uint16_t *__restrict__ Qb2, float4 *__restrict__ qaux2,
-                                                           float *__restrict__ tau2, int *__restrict__ status2) {
+                                                           float *__restrict__ tau2, int *__restrict__ status2,
+                                                           int keep_tau) {
 	const int i = blockIdx.x;
 	const int t = threadIdx.x;
 	const int src = i < nf ? fq[i] : -1;
@@ -2175,15 +2349,15 @@ __global__ __launch_bounds__(256) void retry_gather_kernel(const int *__restrict
 	if (src < 0) return;
 	const float t0 = tau[src];
 	const float dk = dists[(int64_t)src * k + k - 1];  // NaN when fewer than k were found
-	tau2[i] = (dk < t0) ? dk : t0;
+	tau2[i] = (!keep_tau && dk < t0) ? dk : t0;
 	status2[i] = status2[nf + i] = status2[2 * nf + i] = 0;
 }
 
 void launch_retry_gather(const int *fq, int nf, int nf_pad, int ld, int k, const QueryView &q, const float *tau,
                          const float *dists, float *Qf2, uint16_t *Qb2, float4 *qaux2, float *tau2, int *status2,
-                         hipStream_t st) {
+                         hipStream_t st, int keep_tau) {
 	retry_gather_kernel<<<dim3(nf_pad), dim3(256), 0, st>>>(fq, nf, ld, k, q.Qf, q.Qb, q.qaux, tau, dists, Qf2, Qb2,
-	                                                         qaux2, tau2, status2);
+	                                                         qaux2, tau2, status2, keep_tau);
 }
 
 __global__ __launch_bounds__(64) void retry_scatter_kernel(const int *__restrict__ fq, int k,

@@ -50,6 +50,18 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	const float mu = (metric_quirk && metric != METRIC_L2) ? max_ux_l2 : max_ux;
 	StoreView sv{X, aux, dlabels, n_slots, ld, dim, eff_metric, xbf16 ? 1 : 0,
 	             Xs ? static_cast<const void *>(Xs) : X, (xbf16 || Xs) ? 1 : 0};
+	// int8 scan copy (option scan_i8): the scans stream int8 rows with their own
+	// row terms; refine, fallback and the outputs read X and rowaux as always
+	// (k <= 32: past that the looser bounds leave more rows below the k-th
+	// distance than the selection's capacity holds)
+	const bool use8 = i8_usable() && k <= 32;
+	last_scan_esz = use8 ? 1 : (xbf16 || Xs) ? 2 : 4;
+	if (use8) {
+		ensure_i8();
+		sv.Xscan = Xq;
+		sv.scan_aux = rowaux8;
+		sv.scan_i8 = 1;
+	}
 	if (small_exact && small_exact_fits(n_slots, dim, nq, k)) {
 		// a few queries over a small store (one query per lance_search call):
 		// one launch of exact distances + merge, no bounds, no status readback
@@ -82,12 +94,18 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	ws.status.need((size_t)3 * nq);
 	ws.need_host_status((size_t)3 * nq);
 	int *d_cert = ws.status.p, *d_cand_cnt = ws.status.p + nq, *d_pool_cnt = ws.status.p + 2 * nq;
-	launch_prep_queries(dQ, nq, dim, ld, nq_pad, eff_metric, ma, mu, ws.Qf.p, ws.Qb.p, ws.qaux.p, ws.status.p, stream);
+	if (use8)
+		launch_prep_queries_i8(dQ, nq, dim, ld, nq_pad, eff_metric, max_alpha8, max_x8, ws.Qf.p, ws.Qb.p, ws.qaux.p,
+		                       ws.status.p, stream);
+	else
+		launch_prep_queries(dQ, nq, dim, ld, nq_pad, eff_metric, ma, mu, ws.Qf.p, ws.Qb.p, ws.qaux.p, ws.status.p,
+		                    stream);
 	QueryView qv{ws.Qf.p, ws.Qb.p, ws.qaux.p, nq, nq_pad};
 
 	// refined candidates: k + max(32, k) — past k the bound slack (bf16 query
 	// rounding) spans more ranks as the neighbour distances crowd (C3: k = 100)
-	const int Mfinal = std::min(MAX_CAND, std::max(k * std::max(refine, 1), k + std::max(cand_extra, k)));
+	// (int8 scan: looser bounds, more rows below the k-th distance, cand_extra_i8)
+	const int Mfinal = std::min(MAX_CAND, std::max(k * std::max(refine, 1), k + std::max(use8 ? cand_extra_i8 : cand_extra, k)));
 	const int64_t n_tiles = (n_slots + SCAN_BR - 1) / SCAN_BR;
 	const bool fast_ok = (k + 8 <= MAX_CAND) && live_rows() > 0;
 	bool all_fallback = !fast_ok;
@@ -194,10 +212,18 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 			ws.rD.need((size_t)nf * k);
 			ws.rC.need(nf);
 			HIPCHK(hipMemcpyAsync(ws.rfq.p, fq.data(), (size_t)nf * sizeof(int), hipMemcpyHostToDevice, stream));
+			// int8 scan, first rerun: the first pass usually found the true top-k
+			// but more rows than Mfinal lay below its k-th distance; a tau
+			// tightened to that distance could never certify (cut = d_k), so
+			// the rerun keeps tau and only widens the selection (Mr)
 			launch_retry_gather(ws.rfq.p, nf, nf_pad, ld, k, qv, ws.tau.p, dD, ws.rQf.p, ws.rQb.p, ws.rqaux.p,
-			                    ws.rtau.p, ws.rstat.p, stream);
+			                    ws.rtau.p, ws.rstat.p, stream, use8 && attempt == 0);
 			const QueryView qv2{ws.rQf.p, ws.rQb.p, ws.rqaux.p, nf, nf_pad};
 			const int n_seg = scan_grid(n_tiles);
+			// int8 scan: the rerun selects to the full capacity (a failed first
+			// certificate usually means more rows lay below the k-th distance
+			// than Mfinal)
+			const int Mr = use8 ? MAX_CAND : Mfinal;
 			int cap2 = 1024;  // the scan's maximum, bounded to a 1 GiB pool
 			while (cap2 > 64 && (size_t)n_seg * nf * cap2 * sizeof(uint2) > ((size_t)1 << 30)) cap2 /= 2;
 			ws.seg_pool.need((size_t)n_seg * nf * cap2 + (size_t)n_seg * (nf_pad / SCAN_BQ));
@@ -207,10 +233,10 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 				launch_rscan_append(sv, qv2, ws.rtau.p, ws.seg_pool.p, ws.seg_cnt.p, cap2, stream);
 			else
 				launch_scan_append(sv, qv2, ws.rtau.p, ws.seg_pool.p, ws.seg_cnt.p, cap2, stream);
-			launch_select_segments(ws.seg_pool.p, ws.seg_cnt.p, cap2, n_seg, ws.rtau.p, nf, Mfinal, ws.cand_slot.p,
+			launch_select_segments(ws.seg_pool.p, ws.seg_cnt.p, cap2, n_seg, ws.rtau.p, nf, Mr, ws.cand_slot.p,
 			                       cnt2, ws.cut.p, pool2, ws.selbig.p, stream);
-			launch_refine(sv, qv2, ws.cand_slot.p, cnt2, Mfinal, ws.cand_dist.p, stream);
-			launch_finalize(sv, ws.cand_slot.p, cnt2, ws.cand_dist.p, ws.cut.p, nf, Mfinal, k, 1, 0, nullptr, ws.rL.p,
+			launch_refine(sv, qv2, ws.cand_slot.p, cnt2, Mr, ws.cand_dist.p, stream);
+			launch_finalize(sv, ws.cand_slot.p, cnt2, ws.cand_dist.p, ws.cut.p, nf, Mr, k, 1, 0, nullptr, ws.rL.p,
 			                ws.rD.p, ws.rC.p, cert2, stream);
 			launch_retry_scatter(ws.rfq.p, nf, k, ws.rL.p, ws.rD.p, ws.rC.p, cert2, ws.rtau.p, dL, dD, dC, d_cert, ws.tau.p,
 			                     stream);
@@ -1023,6 +1049,19 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			ix->set_scan_copy(v == "on");
 			return 0;
 		}
+		if (k == "scan_i8") {
+			if (v != "on" && v != "off") throw Error("scan_i8 must be 'on' or 'off'");
+			ix->bind();
+			ix->scan_i8 = v == "on";
+			if (!ix->scan_i8) ix->drop_i8();
+			return 0;
+		}
+		if (k == "cand_extra_i8") {
+			const int d = std::stoi(v);
+			if (d < 8 || d > 256) throw Error("cand_extra_i8 must be in [8, 256]");
+			ix->cand_extra_i8 = d;
+			return 0;
+		}
 		if (k == "cand_extra") {
 			const int d = std::stoi(v);
 			if (d < 8 || d > 256) throw Error("cand_extra must be in [8, 256]");
@@ -1116,7 +1155,8 @@ int32_t lance_hip_kernel_times(void *handle, double *out, int32_t n) {
 	std::lock_guard<std::mutex> g(ix->mu);
 	double v[13] = {ix->kt_append_ms, (double)ix->kt_append_n, (double)ix->kt_append_rows,
 		               (double)ix->kt_append_qpad, ix->kt_dense_ms, (double)ix->kt_dense_n,
-		               (ix->xbf16 || ix->Xs) ? 2.0 : 4.0, ix->kt_ivf_ms, (double)ix->kt_ivf_n,
+		               ix->last_scan_esz ? (double)ix->last_scan_esz : (ix->xbf16 || ix->Xs) ? 2.0 : 4.0, ix->kt_ivf_ms,
+		               (double)ix->kt_ivf_n,
 		               ix->kt_ivf_bytes, ix->kt_ivf_pair_rows, ix->kt_ivf_coarse_ms,
 		               (double)ix->kt_append_kernel};
 	for (int32_t i = 0; i < n && i < 13; ++i) out[i] = v[i];

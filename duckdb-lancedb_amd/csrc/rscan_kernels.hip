@@ -496,7 +496,7 @@ static int rscan_ring(const StoreView &s) {
 	return 0;
 }
 
-bool rscan_fits(const StoreView &s) { return rscan_ring(s) != 0; }
+bool rscan_fits(const StoreView &s) { return !s.scan_i8 && rscan_ring(s) != 0; }
 
 template <int METRIC, bool XB>
 static void rscan_launch_r(int R, dim3 grid, hipStream_t st, const uint8_t *X, const StoreView &s, const QueryView &q,
