@@ -174,7 +174,10 @@ struct Index {
 	uint64_t mut_ver = 1, q8_ver = 0;
 	DevBuf<unsigned> stats8;
 	float max_alpha8 = 0.f, max_x8 = 0.f;
-	int cand_extra_i8 = 192;  // refined candidates with the int8 scan: k + max(cand_extra_i8, k) (looser bounds: at 10M x 768 up to ~110 rows lie below the 10th distance)
+	// refined candidates with the int8 scan: k + max(cand_extra_i8, k) (looser bounds put more rows below the
+	// k-th distance: 1M x 768 up to ~80, 10M x 768 up to ~110); 0 = auto: 96 up to 4M slots, 192 past that
+	int cand_extra_i8 = 0;
+	int cand_extra_i8_eff() const { return cand_extra_i8 ? cand_extra_i8 : (n_slots > (4 << 20) ? 192 : 96); }
 	float4 *rowaux_l2 = nullptr;  // aux for L2 when metric_quirk is on and metric != l2
 	int64_t *dlabels = nullptr;
 	int64_t cap = 0, n_slots = 0;

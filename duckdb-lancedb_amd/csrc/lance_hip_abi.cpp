@@ -105,7 +105,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	// refined candidates: k + max(32, k) — past k the bound slack (bf16 query
 	// rounding) spans more ranks as the neighbour distances crowd (C3: k = 100)
 	// (int8 scan: looser bounds, more rows below the k-th distance, cand_extra_i8)
-	const int Mfinal = std::min(MAX_CAND, std::max(k * std::max(refine, 1), k + std::max(use8 ? cand_extra_i8 : cand_extra, k)));
+	const int Mfinal = std::min(MAX_CAND, std::max(k * std::max(refine, 1), k + std::max(use8 ? cand_extra_i8_eff() : cand_extra, k)));
 	const int64_t n_tiles = (n_slots + SCAN_BR - 1) / SCAN_BR;
 	const bool fast_ok = (k + 8 <= MAX_CAND) && live_rows() > 0;
 	bool all_fallback = !fast_ok;
@@ -1058,7 +1058,7 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 		}
 		if (k == "cand_extra_i8") {
 			const int d = std::stoi(v);
-			if (d < 8 || d > 256) throw Error("cand_extra_i8 must be in [8, 256]");
+			if (d != 0 && (d < 8 || d > 256)) throw Error("cand_extra_i8 must be 0 (auto) or in [8, 256]");
 			ix->cand_extra_i8 = d;
 			return 0;
 		}

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--scan-copy", choices=["on", "off"], default="on")
+    ap.add_argument("--scan-i8", choices=["on", "off"], default="on")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     L = lance_hip.lib()
@@ -40,6 +41,7 @@ def main():
     h = L.lance_create_detached(b"", a.dim, b"l2", b"prof", e, 2048)
     lance_hip.LanceHipSetOption(h, "reserve_rows", str(a.n))
     lance_hip.LanceHipSetOption(h, "scan_copy", a.scan_copy)
+    lance_hip.LanceHipSetOption(h, "scan_i8", a.scan_i8)
     for lo in range(0, a.n, 1 << 18):
         hi = min(a.n, lo + (1 << 18))
         X = gen_rows(lo, hi, a.dim, dev)
