@@ -668,6 +668,8 @@ def main():
             else:
                 roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic}
+            # context only (never `achieved`): the rate at which the scan covers the f32 base's own bytes
+            roof["f32_equivalent_gbs"] = round(kt["scan_rows"] * ld * 4 / (avg_ms * 1e-3) / 1e9, 1)
             roof.update({
                     "kernel": f"{kt['scan_kernel']}<{kname},append,{xname}>",
                     "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(bytes_launch),
