@@ -485,6 +485,9 @@ extern "C" int lhip_prof_read(unsigned long long *out, int reset) {
 #ifndef LHIP_SK_BF16
 #define LHIP_SK_BF16 64  // k per stage with a bf16 base: 64 (2 slots) or 32 (3 slots)
 #endif
+#ifndef LHIP_I8_TFOLD
+#define LHIP_I8_TFOLD 1  // int8 append pass: fold the bound into the accumulators (convert + scale + two f32 MFMAs) before the screen
+#endif
 #ifndef LHIP_PF
 #define LHIP_PF 0  // bf16 base: each stage issue also touches the rows of the stage this many ahead into L2 (0 = off)
 #endif
@@ -1150,6 +1153,47 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 				}
 			}
 		} else {
+			// int8 (TFOLD): turn each integer accumulator block into the finished
+			// lower bound in place, as the bf16 path's fold does at the tile start:
+			// acc = f32(s) * sc * S (row scale, query scale), then + alpha + C +
+			// xn*B + ux*A by the same two exact-f32 MFMAs (row terms from the
+			// tile's RA slot, query terms from QA); the screen below then reads
+			// the bounds straight from the accumulators
+			constexpr bool FOLDE = FOLD || (I8 && LHIP_I8_TFOLD);
+			if (I8 && LHIP_I8_TFOLD) {
+				const int ln = lane_id_fresh();
+				const int li = ln & 31, hk = ln >> 5;
+				float bq[4], cq[4], sq[4];
+#pragma unroll
+				for (int u = 0; u < 4; ++u) {
+					const float4 qf = QA[wq * 128 + 32 * u + li];
+					bq[u] = hk ? qf.y : qf.z;  // k0: B, k1: A
+					cq[u] = hk ? qf.w : 1.0f;  // k0: 1, k1: C
+					sq[u] = QA[qlb + 32 * u].x;  // S of this lane's accumulator column
+				}
+#pragma unroll
+				for (int t = 0; t < 2; ++t) {
+					const int r = wr * 64 + 32 * t + li;
+					const float axu = RAs[(1 + hk) * BR + r];  // k0: xn, k1: ux
+					const float aal = hk ? 1.0f : RAs[r];     // k0: alpha, k1: 1
+					float4 scv[4];
+#pragma unroll
+					for (int gq = 0; gq < 4; ++gq) scv[gq] = ra4(rb + 32 * t + 8 * gq, 3);
+#pragma unroll
+					for (int u = 0; u < 4; ++u) {
+#pragma unroll
+						for (int gq = 0; gq < 4; ++gq) {
+							acc[t][u][4 * gq + 0] = (float)__float_as_int(acc[t][u][4 * gq + 0]) * scv[gq].x * sq[u];
+							acc[t][u][4 * gq + 1] = (float)__float_as_int(acc[t][u][4 * gq + 1]) * scv[gq].y * sq[u];
+							acc[t][u][4 * gq + 2] = (float)__float_as_int(acc[t][u][4 * gq + 2]) * scv[gq].z * sq[u];
+							acc[t][u][4 * gq + 3] = (float)__float_as_int(acc[t][u][4 * gq + 3]) * scv[gq].w * sq[u];
+						}
+						acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(axu, bq[u], acc[t][u], 0, 0, 0);
+						acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(aal, cq[u], acc[t][u], 0, 0, 0);
+					}
+				}
+				mfma_operand_guard();
+			}
 			// tau = +inf (fewer live sample rows than needed) must still drop
 			// dead rows (LB = +inf): compare against min(tau, FLT_MAX)
 			float4 qa[4];
@@ -1177,17 +1221,17 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 				for (int gq = 0; gq < 4; ++gq) {
 					const int r0 = rb + 32 * t + 8 * gq;
 					float l[4][4];
-					if (FOLD) {
+					if (FOLDE) {
 #pragma unroll
 						for (int j = 0; j < 4; ++j)
 #pragma unroll
 							for (int u = 0; u < 4; ++u) l[j][u] = acc[t][u][4 * gq + j];
 					}
-					const float4 al = FOLD ? make_float4(0.f, 0.f, 0.f, 0.f) : ra4(r0, 0);
-					const float4 xn = FOLD ? al : ra4(r0, 1), ux = FOLD ? al : ra4(r0, 2);
-					const float4 sc = SCL ? ra4(r0, 3) : make_float4(1.f, 1.f, 1.f, 1.f);
+					const float4 al = FOLDE ? make_float4(0.f, 0.f, 0.f, 0.f) : ra4(r0, 0);
+					const float4 xn = FOLDE ? al : ra4(r0, 1), ux = FOLDE ? al : ra4(r0, 2);
+					const float4 sc = (SCL && !FOLDE) ? ra4(r0, 3) : make_float4(1.f, 1.f, 1.f, 1.f);
 #pragma unroll
-					for (int u = 0; u < 4 && !FOLD; ++u) {
+					for (int u = 0; u < 4 && !FOLDE; ++u) {
 						const f32x2 Bq = {qa[u].z, qa[u].z}, Aq = {qa[u].y, qa[u].y}, Sq = {qa[u].x, qa[u].x};
 						const f32x2 Cq = {qa[u].w, qa[u].w};
 #pragma unroll

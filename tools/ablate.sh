@@ -52,6 +52,7 @@ for v in "$@"; do
 	
 	
 	
+	TFOLD0) build TFOLD0 -DLHIP_I8_TFOLD=0 ;;
 	PF0) build PF0 -DLHIP_PF=0 ;;
 	PF1) build PF1 -DLHIP_PF=1 ;;
 	PF2) build PF2 -DLHIP_PF=2 ;;
