@@ -116,13 +116,9 @@ void launch_rows_to_bf16(const float *src, int64_t src_ld, int64_t n, int dim, i
 // alpha copies the store's tombstones (+inf); a zero cosine row is NaN (exact
 // fallback), as in rowaux.  stats[0] = max |alpha|, stats[1] = max(xn, ux).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void rows_to_i8_kernel(const float *__restrict__ X, int ld, int dim, int metric,
-                                                         int64_t n, const float4 *__restrict__ rowaux,
-                                                         int8_t *__restrict__ Xq, float4 *__restrict__ aux8,
-                                                         unsigned *__restrict__ stats) {
-	const int lane = threadIdx.x & 63;
-	const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-	if (r >= n) return;
+__device__ __forceinline__ void rows_to_i8_row(const float *__restrict__ X, int ld, int dim, int metric, int64_t r,
+                                               const float4 *__restrict__ rowaux, int8_t *__restrict__ Xq,
+                                               float4 *__restrict__ aux8, unsigned *__restrict__ stats, int lane) {
 	const float *x = X + r * (int64_t)ld;
 	float m = 0.f;
 	for (int i = lane; i < dim; i += 64) m = fmaxf(m, fabsf(x[i]));
@@ -131,19 +127,26 @@ __global__ __launch_bounds__(256) void rows_to_i8_kernel(const float *__restrict
 	const float sx = m / 127.0f;
 	const float inv = m > 0.f ? 127.0f / m : 0.f;
 	double s2 = 0.0, e2 = 0.0, t2 = 0.0;
-	int8_t *xq = Xq + r * (int64_t)ld;
-	for (int i = lane; i < ld; i += 64) {
-		int qv = 0;
-		if (i < dim) {
-			const float v = x[i];
-			qv = min(127, max(-127, (int)rintf(v * inv)));
-			const double xt = (double)sx * (double)qv;
-			const double e = (double)v - xt;
-			s2 += (double)v * v;
-			e2 += e * e;
-			t2 += xt * xt;
+	// four elements per lane and step: one packed 4-byte store (ld is a multiple of 128)
+	uint32_t *xq = reinterpret_cast<uint32_t *>(Xq + r * (int64_t)ld);
+	for (int i0 = 4 * lane; i0 < ld; i0 += 256) {
+		uint32_t packed = 0u;
+#pragma unroll
+		for (int j = 0; j < 4; ++j) {
+			const int i = i0 + j;
+			int qv = 0;
+			if (i < dim) {
+				const float v = x[i];
+				qv = min(127, max(-127, (int)rintf(v * inv)));
+				const double xt = (double)sx * (double)qv;
+				const double e = (double)v - xt;
+				s2 += (double)v * v;
+				e2 += e * e;
+				t2 += xt * xt;
+			}
+			packed |= ((uint32_t)qv & 0xFFu) << (8 * j);
 		}
-		xq[i] = (int8_t)qv;
+		xq[i0 >> 2] = packed;
 	}
 	s2 = wave_sum_f64(s2);
 	e2 = wave_sum_f64(e2);
@@ -172,11 +175,22 @@ __global__ __launch_bounds__(256) void rows_to_i8_kernel(const float *__restrict
 	if (a.y == a.y) atomicMax(&stats[1], __float_as_uint(fmaxf(a.y, a.z)));
 }
 
+__global__ __launch_bounds__(256) void rows_to_i8_kernel(const float *__restrict__ X, int ld, int dim, int metric,
+                                                         int64_t n, const float4 *__restrict__ rowaux,
+                                                         int8_t *__restrict__ Xq, float4 *__restrict__ aux8,
+                                                         unsigned *__restrict__ stats) {
+	const int lane = threadIdx.x & 63;
+	// grid-stride over rows (one wave per row at a time): a grid of one block
+	// per 4 rows spent its time in workgroup dispatch (22.7 ms for 1M rows)
+	for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += (int64_t)gridDim.x * 4)
+		rows_to_i8_row(X, ld, dim, metric, r, rowaux, Xq, aux8, stats, lane);
+}
+
 void launch_rows_to_i8(const float *X, int ld, int dim, int metric, int64_t n, const float4 *rowaux, int8_t *Xq,
                        float4 *aux8, unsigned *stats, hipStream_t st) {
 	if (n <= 0) return;
-	rows_to_i8_kernel<<<dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st>>>(X, ld, dim, metric, n, rowaux, Xq, aux8,
-	                                                                       stats);
+	const int64_t blocks = std::min<int64_t>((n + 3) / 4, 4096);
+	rows_to_i8_kernel<<<dim3((unsigned)blocks), dim3(256), 0, st>>>(X, ld, dim, metric, n, rowaux, Xq, aux8, stats);
 }
 
 __global__ void fill_rowaux_kernel(float4 *rowaux, int64_t from, int64_t to) {
