@@ -38,12 +38,8 @@ namespace lhip {
 // ingest: per-row auxiliary data
 // ---------------------------------------------------------------------------
 template <typename T>
-__global__ __launch_bounds__(256) void rowaux_kernel(const T *__restrict__ X, int ld, int dim, int metric,
-                                                     int64_t s0, int64_t n, float4 *__restrict__ rowaux,
-                                                     unsigned *__restrict__ stats) {
-	const int lane = threadIdx.x & 63;
-	const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-	if (r >= n) return;
+__device__ __forceinline__ void rowaux_row(const T *__restrict__ X, int ld, int dim, int metric, int64_t s0, int64_t r,
+                                           float4 *__restrict__ rowaux, unsigned *__restrict__ stats, int lane) {
 	const T *x = X + (s0 + r) * (int64_t)ld;
 	double s2 = 0.0, e2 = 0.0;
 	for (int i = lane; i < dim; i += 64) {
@@ -79,10 +75,20 @@ __global__ __launch_bounds__(256) void rowaux_kernel(const T *__restrict__ X, in
 	}
 }
 
+template <typename T>
+__global__ __launch_bounds__(256) void rowaux_kernel(const T *__restrict__ X, int ld, int dim, int metric,
+                                                     int64_t s0, int64_t n, float4 *__restrict__ rowaux,
+                                                     unsigned *__restrict__ stats) {
+	// grid-stride, one wave per row at a time (one block per 4 rows was dispatch-bound)
+	const int lane = threadIdx.x & 63;
+	for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += (int64_t)gridDim.x * 4)
+		rowaux_row(X, ld, dim, metric, s0, r, rowaux, stats, lane);
+}
+
 void launch_rowaux(const void *X, int xbf16, int ld, int dim, int metric, int64_t s0, int64_t n, float4 *rowaux,
                    unsigned *stats, hipStream_t st) {
 	if (n <= 0) return;
-	int64_t blocks = (n + 3) / 4;
+	const int64_t blocks = std::min<int64_t>((n + 3) / 4, 4096);
 	if (xbf16)
 		rowaux_kernel<<<dim3((unsigned)blocks), dim3(256), 0, st>>>((const uint16_t *)X, ld, dim, metric, s0, n, rowaux,
 		                                                            stats);
