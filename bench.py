@@ -540,6 +540,8 @@ def main():
         if r < 0:
             raise RuntimeError(e.value.decode())
         del X
+    # index preparation (outside any timing): the int8 scan copy is derived from the rows
+    lance_hip.LanceHipSetOption(h, "prepare", "1")
     g = torch.Generator(device=dev)
     g.manual_seed(5678)
     # global batch: weak = B per rank (per-GPU flops fixed), strong = B in all

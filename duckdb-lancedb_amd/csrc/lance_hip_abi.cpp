@@ -1056,6 +1056,13 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			if (!ix->scan_i8) ix->drop_i8();
 			return 0;
 		}
+		if (k == "prepare") {
+			// build the derived scan structures now (the int8 scan copy) instead
+			// of on the first search after a change
+			ix->bind();
+			if (ix->i8_usable()) ix->ensure_i8();
+			return 0;
+		}
 		if (k == "cand_extra_i8") {
 			const int d = std::stoi(v);
 			if (d != 0 && (d < 8 || d > 256)) throw Error("cand_extra_i8 must be 0 (auto) or in [8, 256]");

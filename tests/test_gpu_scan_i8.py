@@ -168,3 +168,34 @@ def test_i8_zero_cosine_query(hip, tmp_path):
             np.testing.assert_array_equal(gl[i], el[i])
     finally:
         hip.LanceFreeDetached(h)
+
+
+def test_i8_prepare_option(hip, tmp_path):
+    # "prepare" builds the int8 copy eagerly; searches after it (and after a
+    # later change, which rebuilds lazily) stay exact; a no-op where int8 does not apply
+    rng = np.random.default_rng(12)
+    d = 256
+    X = rng.standard_normal((90_000, d)).astype(np.float32)
+    Q = rng.standard_normal((20, d)).astype(np.float32)
+    h = _mk(hip, tmp_path, d, "dot")
+    try:
+        hip.LanceDetachedAddBatch(h, X[:60_000], 60_000, d)
+        hip.LanceHipSetOption(h, "prepare", "1")
+        live = np.zeros(90_000, bool)
+        live[:60_000] = True
+        gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 7)
+        el, ed, ec = c_oracle.flat_search_batch(X, Q, 7, "dot", live=live, acc64=True, nthreads=16)
+        assert_same(gl, gd, gc, el, ed, ec)
+        hip.LanceDetachedAddBatch(h, X[60_000:], 30_000, d)
+        live[:] = True
+        gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 7)
+        el, ed, ec = c_oracle.flat_search_batch(X, Q, 7, "dot", live=live, acc64=True, nthreads=16)
+        assert_same(gl, gd, gc, el, ed, ec)
+    finally:
+        hip.LanceFreeDetached(h)
+    h2 = _mk(hip, tmp_path, 40, "l2")  # ld 64: int8 does not apply
+    try:
+        hip.LanceDetachedAddBatch(h2, X[:1000, :40].copy(), 1000, 40)
+        hip.LanceHipSetOption(h2, "prepare", "1")
+    finally:
+        hip.LanceFreeDetached(h2)
