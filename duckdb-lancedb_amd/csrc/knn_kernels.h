@@ -136,6 +136,11 @@ void launch_select_segments(const uint2 *seg_pool, const int *seg_cnt, int seg_c
 void launch_refine(const StoreView &s, const QueryView &q, const uint32_t *cand_slot, const int *cand_cnt, int M,
                    float *cand_dist, hipStream_t st);
 
+// refine + finalize mode 0 in one launch: tau[q] = the need-th smallest exact
+// distance of the candidates (+inf when fewer, NaN when any is NaN).
+void launch_refine_tau(const StoreView &s, const QueryView &q, const uint32_t *cand_slot, const int *cand_cnt, int M,
+                       int need, float *tau, hipStream_t st);
+
 // Sort candidates by (distance, label).  mode 0 (TAU): tau[q] = largest exact
 // distance among the candidates when at least need_for_tau of them exist, else
 // +inf.  mode 1 (FINAL): writes top-k, counts and the certificate ok[q].

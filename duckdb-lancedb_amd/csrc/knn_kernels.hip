@@ -1999,6 +1999,71 @@ void launch_refine(const StoreView &s, const QueryView &q, const uint32_t *cand_
 }
 
 // ---------------------------------------------------------------------------
+// refine + tau in one launch (the sample pass's candidates): one 8-wave
+// workgroup per query computes the exact distances of its m candidates (the
+// value refine_kernel computes) into LDS and writes tau = the need-th smallest
+// of them (+inf when fewer, NaN when any is NaN): finalize_kernel's mode 0
+// without the refine launch and the cand_dist round trip
+// ---------------------------------------------------------------------------
+template <int METRIC, typename T>
+__global__ __launch_bounds__(512) void refine_tau_kernel(const T *__restrict__ X, int ld, int dim,
+                                                         const float *__restrict__ Qf,
+                                                         const uint32_t *__restrict__ cand_slot,
+                                                         const int *__restrict__ cand_cnt, int M, int need,
+                                                         float *__restrict__ tau) {
+	__shared__ float sd[MAX_CAND];
+	const int q = blockIdx.x;
+	const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+	const int m = min(cand_cnt[q], M);
+	for (int i = w; i < m; i += 8) {
+		const uint32_t slot = cand_slot[(int64_t)q * M + i];
+		const float d = exact_distance<METRIC, T>(X + (int64_t)slot * ld, Qf + (int64_t)q * ld, dim, lane);
+		if (lane == 0) sd[i] = d;
+	}
+	__syncthreads();
+	bool nan = false;
+	for (int i = 0; i < m; ++i) nan |= __builtin_isnan(sd[i]);
+	if (m < need || m == 0 || nan) {
+		if (t == 0) tau[q] = nan ? __builtin_nanf("") : F_INF;
+		return;
+	}
+	for (int i = t; i < m; i += 512) {
+		int rank = 0;
+		const float d = sd[i];
+		for (int j = 0; j < m; ++j) rank += (sd[j] < d || (sd[j] == d && j < i)) ? 1 : 0;
+		if (rank == need - 1) tau[q] = d;
+	}
+}
+
+template <typename T>
+static void refine_tau_dispatch(const StoreView &s, const QueryView &q, const uint32_t *cand_slot, const int *cand_cnt,
+                                int M, int need, float *tau, hipStream_t st) {
+	const T *X = static_cast<const T *>(s.X);
+	const dim3 grid((unsigned)q.nq);
+	switch (s.metric) {
+	case METRIC_L2:
+		refine_tau_kernel<METRIC_L2, T><<<grid, 512, 0, st>>>(X, s.ld, s.dim, q.Qf, cand_slot, cand_cnt, M, need, tau);
+		break;
+	case METRIC_DOT:
+		refine_tau_kernel<METRIC_DOT, T><<<grid, 512, 0, st>>>(X, s.ld, s.dim, q.Qf, cand_slot, cand_cnt, M, need, tau);
+		break;
+	default:
+		refine_tau_kernel<METRIC_COSINE, T><<<grid, 512, 0, st>>>(X, s.ld, s.dim, q.Qf, cand_slot, cand_cnt, M, need,
+		                                                          tau);
+		break;
+	}
+}
+
+void launch_refine_tau(const StoreView &s, const QueryView &q, const uint32_t *cand_slot, const int *cand_cnt, int M,
+                       int need, float *tau, hipStream_t st) {
+	if (M > MAX_CAND) throw std::runtime_error("refine_tau: M past MAX_CAND");
+	if (s.xbf16)
+		refine_tau_dispatch<uint16_t>(s, q, cand_slot, cand_cnt, M, need, tau, st);
+	else
+		refine_tau_dispatch<float>(s, q, cand_slot, cand_cnt, M, need, tau, st);
+}
+
+// ---------------------------------------------------------------------------
 // finalize: rank candidates by (distance, label); top-k + certificate, or tau
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void finalize_kernel(const int64_t *__restrict__ labels,

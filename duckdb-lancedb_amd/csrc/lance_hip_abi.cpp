@@ -145,9 +145,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		ws.selbig.need((size_t)nq);
 		launch_select_segments(ws.seg_pool.p, ws.seg_cnt.p, cap_s, n_seg_s, nullptr, nq, Ms, ws.cand_slot.p,
 		                       d_cand_cnt, ws.cut.p, nullptr, ws.selbig.p, stream);
-		launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Ms, ws.cand_dist.p, stream);
-		launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Ms, k, 0, k, ws.tau.p,
-		                nullptr, nullptr, nullptr, nullptr, stream);
+		launch_refine_tau(sv, qv, ws.cand_slot.p, d_cand_cnt, Ms, k, ws.tau.p, stream);
 		// 2) threshold scan over every row into per-(workgroup, query) segments;
 		//    a segment holds ~4x its expected share of the (k+8)*N/sample pool
 		const int n_seg = scan_grid(n_tiles);
