@@ -141,6 +141,11 @@ void launch_refine(const StoreView &s, const QueryView &q, const uint32_t *cand_
 void launch_refine_tau(const StoreView &s, const QueryView &q, const uint32_t *cand_slot, const int *cand_cnt, int M,
                        int need, float *tau, hipStream_t st);
 
+// refine + finalize mode 1 in one launch (the same outputs and certificate;
+// cand_dist not written).
+void launch_refine_final(const StoreView &s, const QueryView &q, const uint32_t *cand_slot, const int *cand_cnt,
+                         const float *cut, int M, int k, int64_t *L, float *D, int *C, int *cert, hipStream_t st);
+
 // Sort candidates by (distance, label).  mode 0 (TAU): tau[q] = largest exact
 // distance among the candidates when at least need_for_tau of them exist, else
 // +inf.  mode 1 (FINAL): writes top-k, counts and the certificate ok[q].

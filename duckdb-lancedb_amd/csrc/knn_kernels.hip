@@ -2146,6 +2146,92 @@ void launch_finalize(const StoreView &s, const uint32_t *cand_slot, const int *c
 }
 
 // ---------------------------------------------------------------------------
+// refine + finalize (mode 1) in one launch: one 16-wave workgroup per query
+// computes the exact distances of its candidates into LDS (refine_kernel's
+// value), then ranks them by (distance, label) exactly as finalize_kernel does:
+// top-k, counts, certificate against cut.  cand_dist is not written.
+// ---------------------------------------------------------------------------
+constexpr int RF_THREADS = 1024;
+template <int METRIC, typename T>
+__global__ __launch_bounds__(RF_THREADS) void refine_final_kernel(
+    const T *__restrict__ X, int ld, int dim, const float *__restrict__ Qf, const int64_t *__restrict__ labels,
+    const uint32_t *__restrict__ cand_slot, const int *__restrict__ cand_cnt, const float *__restrict__ cut, int M,
+    int k, int64_t *__restrict__ out_labels, float *__restrict__ out_dists, int *__restrict__ out_counts,
+    int *__restrict__ cert_ok) {
+	__shared__ float sd[MAX_CAND];
+	__shared__ int64_t sl[MAX_CAND];
+	__shared__ float s_dk;
+	const int q = blockIdx.x;
+	const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+	const int m = min(cand_cnt[q], M);
+	for (int i = w; i < m; i += RF_THREADS / 64) {
+		const uint32_t slot = cand_slot[(int64_t)q * M + i];
+		const float d = exact_distance<METRIC, T>(X + (int64_t)slot * ld, Qf + (int64_t)q * ld, dim, lane);
+		if (lane == 0) {
+			sd[i] = d;
+			sl[i] = labels[slot];
+		}
+	}
+	if (t == 0) s_dk = F_INF;
+	__syncthreads();
+	const int nout = m < k ? m : k;
+	for (int i = t; i < m; i += RF_THREADS) {
+		int rank = 0;
+		const float d = sd[i];
+		const int64_t l = sl[i];
+		for (int j = 0; j < m; ++j) rank += hit_less(sd[j], sl[j], d, l) ? 1 : 0;
+		if (rank < k) {
+			out_labels[(int64_t)q * k + rank] = l;
+			out_dists[(int64_t)q * k + rank] = d;
+		}
+		if (rank == k - 1) s_dk = d;
+	}
+	for (int i = nout + t; i < k; i += RF_THREADS) {
+		out_labels[(int64_t)q * k + i] = -1;
+		out_dists[(int64_t)q * k + i] = __builtin_nanf("");
+	}
+	__syncthreads();
+	if (t == 0) {
+		out_counts[q] = nout;
+		const float c = cut[q];
+		bool ok;
+		if (c == F_INF) {
+			ok = true;  // nothing live was left out
+		} else {
+			const float dk = s_dk;  // +inf when fewer than k candidates
+			ok = !__builtin_isnan(dk) && dk < F_INF && c > nextafterf(dk, F_INF);
+		}
+		cert_ok[q] = ok ? 1 : 0;
+	}
+}
+
+template <typename T>
+static void refine_final_dispatch(const StoreView &s, const QueryView &q, const uint32_t *cand_slot,
+                                  const int *cand_cnt, const float *cut, int M, int k, int64_t *L, float *D, int *C,
+                                  int *cert, hipStream_t st) {
+	const T *X = static_cast<const T *>(s.X);
+	const dim3 grid((unsigned)q.nq);
+#define LHIP_RF(MET) \
+	refine_final_kernel<MET, T><<<grid, RF_THREADS, 0, st>>>(X, s.ld, s.dim, q.Qf, s.labels, cand_slot, cand_cnt, cut, M, \
+	                                                        k, L, D, C, cert)
+	switch (s.metric) {
+	case METRIC_L2: LHIP_RF(METRIC_L2); break;
+	case METRIC_DOT: LHIP_RF(METRIC_DOT); break;
+	default: LHIP_RF(METRIC_COSINE); break;
+	}
+#undef LHIP_RF
+}
+
+void launch_refine_final(const StoreView &s, const QueryView &q, const uint32_t *cand_slot, const int *cand_cnt,
+                         const float *cut, int M, int k, int64_t *L, float *D, int *C, int *cert, hipStream_t st) {
+	if (M > MAX_CAND) throw std::runtime_error("refine_final: M past MAX_CAND");
+	if (s.xbf16)
+		refine_final_dispatch<uint16_t>(s, q, cand_slot, cand_cnt, cut, M, k, L, D, C, cert, st);
+	else
+		refine_final_dispatch<float>(s, q, cand_slot, cand_cnt, cut, M, k, L, D, C, cert, st);
+}
+
+// ---------------------------------------------------------------------------
 // exact fallback
 // ---------------------------------------------------------------------------
 template <int METRIC, typename T>

@@ -162,9 +162,13 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		// 3) top-M by LB, exact refine, certificate
 		launch_select_segments(ws.seg_pool.p, ws.seg_cnt.p, seg_cap, n_seg, ws.tau.p, nq, Mfinal, ws.cand_slot.p,
 		                       d_cand_cnt, ws.cut.p, d_pool_cnt, ws.selbig.p, stream);
-		launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Mfinal, ws.cand_dist.p, stream);
-		launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Mfinal, k, 1, 0, nullptr, dL,
-		                dD, dC, d_cert, stream);
+		if (fused_refine)
+			launch_refine_final(sv, qv, ws.cand_slot.p, d_cand_cnt, ws.cut.p, Mfinal, k, dL, dD, dC, d_cert, stream);
+		else {
+			launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Mfinal, ws.cand_dist.p, stream);
+			launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Mfinal, k, 1, 0, nullptr, dL,
+			                dD, dC, d_cert, stream);
+		}
 	}
 	HIPCHK(hipGetLastError());
 
@@ -1052,6 +1056,10 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			ix->bind();
 			ix->scan_i8 = v == "on";
 			if (!ix->scan_i8) ix->drop_i8();
+			return 0;
+		}
+		if (k == "fused_refine") {
+			ix->fused_refine = (v == "1" || v == "on" || v == "true");
 			return 0;
 		}
 		if (k == "prepare") {
