@@ -167,8 +167,10 @@ struct Index {
 	// rebuilt after any change of the rows or tombstones (mut_ver); the flat
 	// scans stream it with rowaux8 as their row terms, everything else uses X
 	bool scan_i8 = true;
-	int last_scan_esz = 0;
-	bool fused_refine = false;  // append path: refine + finalize in one launch (option "fused_refine"; measured ~10 us slower: 7 sequential exact distances per wave vs one wave per candidate)  // bytes per element the last flat search's scan streamed (1 int8, 2 bf16, 4 f32)
+	int last_scan_esz = 0;  // bytes per element the last flat search's scan streamed (1 int8, 2 bf16, 4 f32)
+	// append path: refine + finalize in one launch (option "fused_refine"; measured ~10 us slower: a
+	// per-wave sequence of exact distances against one wave per candidate)
+	bool fused_refine = false;
 	int8_t *Xq = nullptr;
 	float4 *rowaux8 = nullptr;
 	int64_t q8_cap = 0;
