@@ -1105,6 +1105,47 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 		const int eln = lane_id_fresh();
 		const int qlb = wq * 128 + (eln & 31);  // tile-local query of acc[.][u]: qlb + 32u
 		const int rb = wr * 64 + 4 * (eln >> 5); // tile-local row of acc[t][.] reg r: rb + 32t + (r&3) + 8(r>>2)
+		// int8 (TFOLD): turn each integer accumulator block into the finished
+		// lower bound in place, as the bf16 path's fold does at the tile start:
+		// acc = f32(s) * sc * S (row scale, query scale), then + alpha + C +
+		// xn*B + ux*A by the same two exact-f32 MFMAs (row terms from the
+		// tile's RA slot, query terms from QA); the screen below then reads
+		// the bounds straight from the accumulators
+		constexpr bool FOLDE = FOLD || (I8 && LHIP_I8_TFOLD && MODE != 0);
+		if (I8 && LHIP_I8_TFOLD && MODE != 0) {
+			const int ln = lane_id_fresh();
+			const int li = ln & 31, hk = ln >> 5;
+			float bq[4], cq[4], sq[4];
+#pragma unroll
+			for (int u = 0; u < 4; ++u) {
+				const float4 qf = QA[wq * 128 + 32 * u + li];
+				bq[u] = hk ? qf.y : qf.z;  // k0: B, k1: A
+				cq[u] = hk ? qf.w : 1.0f;  // k0: 1, k1: C
+				sq[u] = QA[qlb + 32 * u].x;  // S of this lane's accumulator column
+			}
+#pragma unroll
+			for (int t = 0; t < 2; ++t) {
+				const int r = wr * 64 + 32 * t + li;
+				const float axu = RAs[(1 + hk) * BR + r];  // k0: xn, k1: ux
+				const float aal = hk ? 1.0f : RAs[r];     // k0: alpha, k1: 1
+				float4 scv[4];
+#pragma unroll
+				for (int gq = 0; gq < 4; ++gq) scv[gq] = ra4(rb + 32 * t + 8 * gq, 3);
+#pragma unroll
+				for (int u = 0; u < 4; ++u) {
+#pragma unroll
+					for (int gq = 0; gq < 4; ++gq) {
+						acc[t][u][4 * gq + 0] = (float)__float_as_int(acc[t][u][4 * gq + 0]) * scv[gq].x * sq[u];
+						acc[t][u][4 * gq + 1] = (float)__float_as_int(acc[t][u][4 * gq + 1]) * scv[gq].y * sq[u];
+						acc[t][u][4 * gq + 2] = (float)__float_as_int(acc[t][u][4 * gq + 2]) * scv[gq].z * sq[u];
+						acc[t][u][4 * gq + 3] = (float)__float_as_int(acc[t][u][4 * gq + 3]) * scv[gq].w * sq[u];
+					}
+					acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(axu, bq[u], acc[t][u], 0, 0, 0);
+					acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(aal, cq[u], acc[t][u], 0, 0, 0);
+				}
+			}
+			mfma_operand_guard();
+		}
 		if (LHIP_ABL_NO_EPILOGUE) {
 			if (acc[0][0][0] == 12345.f && acc[1][3][3] == 54321.f && acc[0][1][1] == acc[1][2][2]) seg_cnt[0] = 1;
 		} else if (MODE == 0) {
@@ -1146,12 +1187,12 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 					for (int gq = 0; gq < 4; ++gq) {
 						const int r0 = rb + 32 * t + 8 * gq;
 						float4 al, xn, ux, sc;
-						if (!FOLD) al = ra4(r0, 0), xn = ra4(r0, 1), ux = ra4(r0, 2), sc = ra4(r0, 3);
+						if (!FOLDE) al = ra4(r0, 0), xn = ra4(r0, 1), ux = ra4(r0, 2), sc = ra4(r0, 3);
 #pragma unroll
 						for (int j = 0; j < 4; ++j) {
-							const float a = accf(t, u, 4 * gq + j);
+							const float a = FOLDE ? acc[t][u][4 * gq + j] : accf(t, u, 4 * gq + j);
 							const float lb =
-							    FOLD ? a
+							    FOLDE ? a
 							         : lower_bound<METRIC, I8>(a,
 							                               j == 0   ? make_float4(al.x, xn.x, ux.x, sc.x)
 							                               : j == 1 ? make_float4(al.y, xn.y, ux.y, sc.y)
@@ -1173,47 +1214,6 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 				}
 			}
 		} else {
-			// int8 (TFOLD): turn each integer accumulator block into the finished
-			// lower bound in place, as the bf16 path's fold does at the tile start:
-			// acc = f32(s) * sc * S (row scale, query scale), then + alpha + C +
-			// xn*B + ux*A by the same two exact-f32 MFMAs (row terms from the
-			// tile's RA slot, query terms from QA); the screen below then reads
-			// the bounds straight from the accumulators
-			constexpr bool FOLDE = FOLD || (I8 && LHIP_I8_TFOLD);
-			if (I8 && LHIP_I8_TFOLD) {
-				const int ln = lane_id_fresh();
-				const int li = ln & 31, hk = ln >> 5;
-				float bq[4], cq[4], sq[4];
-#pragma unroll
-				for (int u = 0; u < 4; ++u) {
-					const float4 qf = QA[wq * 128 + 32 * u + li];
-					bq[u] = hk ? qf.y : qf.z;  // k0: B, k1: A
-					cq[u] = hk ? qf.w : 1.0f;  // k0: 1, k1: C
-					sq[u] = QA[qlb + 32 * u].x;  // S of this lane's accumulator column
-				}
-#pragma unroll
-				for (int t = 0; t < 2; ++t) {
-					const int r = wr * 64 + 32 * t + li;
-					const float axu = RAs[(1 + hk) * BR + r];  // k0: xn, k1: ux
-					const float aal = hk ? 1.0f : RAs[r];     // k0: alpha, k1: 1
-					float4 scv[4];
-#pragma unroll
-					for (int gq = 0; gq < 4; ++gq) scv[gq] = ra4(rb + 32 * t + 8 * gq, 3);
-#pragma unroll
-					for (int u = 0; u < 4; ++u) {
-#pragma unroll
-						for (int gq = 0; gq < 4; ++gq) {
-							acc[t][u][4 * gq + 0] = (float)__float_as_int(acc[t][u][4 * gq + 0]) * scv[gq].x * sq[u];
-							acc[t][u][4 * gq + 1] = (float)__float_as_int(acc[t][u][4 * gq + 1]) * scv[gq].y * sq[u];
-							acc[t][u][4 * gq + 2] = (float)__float_as_int(acc[t][u][4 * gq + 2]) * scv[gq].z * sq[u];
-							acc[t][u][4 * gq + 3] = (float)__float_as_int(acc[t][u][4 * gq + 3]) * scv[gq].w * sq[u];
-						}
-						acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(axu, bq[u], acc[t][u], 0, 0, 0);
-						acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(aal, cq[u], acc[t][u], 0, 0, 0);
-					}
-				}
-				mfma_operand_guard();
-			}
 			// tau = +inf (fewer live sample rows than needed) must still drop
 			// dead rows (LB = +inf): compare against min(tau, FLT_MAX)
 			float4 qa[4];
