@@ -522,11 +522,17 @@ struct Index {
 			done.push_back(labels[i]);
 		}
 		if (!slots.empty()) {
+			// a current int8 scan copy takes the tombstones in place (no rebuild)
+			const bool i8_cur = Xq && q8_ver == mut_ver && q8_cap == cap;
 			++mut_ver;
 			ws.idx.need(slots.size());
 			HIPCHK(hipMemcpyAsync(ws.idx.p, slots.data(), slots.size() * sizeof(int64_t), hipMemcpyHostToDevice,
 			                      stream));
 			launch_tombstone(rowaux, ws.idx.p, (int)slots.size(), stream);
+			if (i8_cur) {
+				launch_tombstone(rowaux8, ws.idx.p, (int)slots.size(), stream);
+				q8_ver = mut_ver;
+			}
 			if (rowaux_l2) launch_tombstone(rowaux_l2, ws.idx.p, (int)slots.size(), stream);
 			HIPCHK(hipGetLastError());
 			HIPCHK(hipStreamSynchronize(stream));
