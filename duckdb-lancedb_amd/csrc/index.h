@@ -388,7 +388,7 @@ struct Index {
 		stats8.need(2);
 		HIPCHK(hipMemsetAsync(stats8.p, 0, 2 * sizeof(unsigned), stream));
 		HIPCHK(hipMemsetAsync(Xq + (size_t)n_slots * ld, 0, (size_t)(cap - n_slots) * ld, stream));
-		launch_rows_to_i8(static_cast<const float *>(X), ld, dim, metric, n_slots, rowaux, Xq, rowaux8, stats8.p,
+		launch_rows_to_i8(static_cast<const float *>(X), ld, dim, metric, 0, n_slots, rowaux, Xq, rowaux8, stats8.p,
 		                  stream);
 		launch_fill_rowaux(rowaux8, n_slots, cap, stream);
 		HIPCHK(hipGetLastError());
@@ -409,6 +409,8 @@ struct Index {
 
 	// append rows already resident on the device at X[n_slots .. n_slots+num)
 	int64_t commit_rows(int64_t num) {
+		// a current int8 scan copy (same capacity) takes the new rows in place
+		const bool i8_cur = Xq && q8_ver == mut_ver && q8_cap == cap;
 		++mut_ver;
 		const int64_t first = next_label;
 		std::vector<int64_t> labs((size_t)num);
@@ -418,9 +420,19 @@ struct Index {
 		if (Xs) fill_scan_copy(n_slots, num, Xs);
 		launch_rowaux(X, xbf16, ld, dim, metric, n_slots, num, rowaux, stats.p, stream);
 		if (rowaux_l2) launch_rowaux(X, xbf16, ld, dim, METRIC_L2, n_slots, num, rowaux_l2, stats.p + 2, stream);
+		if (i8_cur)
+			launch_rows_to_i8(static_cast<const float *>(X), ld, dim, metric, n_slots, num, rowaux, Xq, rowaux8,
+			                  stats8.p, stream);
 		HIPCHK(hipGetLastError());
 		HIPCHK(hipStreamSynchronize(stream));
 		refresh_stats();
+		if (i8_cur) {
+			unsigned h8[2];
+			HIPCHK(hipMemcpy(h8, stats8.p, sizeof(h8), hipMemcpyDeviceToHost));
+			memcpy(&max_alpha8, &h8[0], 4);
+			memcpy(&max_x8, &h8[1], 4);
+			q8_ver = mut_ver;
+		}
 		slot_label.insert(slot_label.end(), labs.begin(), labs.end());
 		live.insert(live.end(), (size_t)num, 1);
 		if (meta && meta->cols.size() && meta->cols[0].size() < (size_t)(n_slots + num))

@@ -65,11 +65,11 @@ void launch_rowaux(const void *X, int xbf16, int ld, int dim, int metric, int64_
 // dst rows of stride ld, zero-filling columns [dim, ld).
 void launch_rows_to_bf16(const float *src, int64_t src_ld, int64_t n, int dim, int ld, uint16_t *dst, hipStream_t st);
 
-// int8 scan copy of slots [0, n) of an f32 store: int8 rows Xq (stride ld
+// int8 scan copy of slots [s0, s0+n) of an f32 store: int8 rows Xq (stride ld
 // bytes, zero padded) and their row terms aux8 (tombstones copied from
-// rowaux); stats[0] = max |alpha|, stats[1] = max(xn, ux) as float bits.
-void launch_rows_to_i8(const float *X, int ld, int dim, int metric, int64_t n, const float4 *rowaux, int8_t *Xq,
-                       float4 *aux8, unsigned *stats, hipStream_t st);
+// rowaux); folds max |alpha| and max(xn, ux) into stats[0], stats[1] (float bits).
+void launch_rows_to_i8(const float *X, int ld, int dim, int metric, int64_t s0, int64_t n, const float4 *rowaux,
+                       int8_t *Xq, float4 *aux8, unsigned *stats, hipStream_t st);
 
 // rowaux[from, to) = (+inf, 0, 0, 0): padding rows past the last slot.
 void launch_fill_rowaux(float4 *rowaux, int64_t from, int64_t to, hipStream_t st);

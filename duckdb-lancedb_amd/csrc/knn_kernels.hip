@@ -128,7 +128,7 @@ void launch_rows_to_bf16(const float *src, int64_t src_ld, int64_t n, int dim, i
 // alpha copies the store's tombstones (+inf); a zero cosine row is NaN (exact
 // fallback), as in rowaux.  stats[0] = max |alpha|, stats[1] = max(xn, ux).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void rows_to_i8_row(const float *__restrict__ X, int ld, int dim, int metric, int64_t r,
+__device__ __forceinline__ void rows_to_i8_row(const float *__restrict__ X, int ld, int dim, int metric, int64_t r,  // r: absolute slot
                                                const float4 *__restrict__ rowaux, int8_t *__restrict__ Xq,
                                                float4 *__restrict__ aux8, unsigned &m0, unsigned &m1, int lane) {
 	const float *x = X + r * (int64_t)ld;
@@ -188,7 +188,7 @@ __device__ __forceinline__ void rows_to_i8_row(const float *__restrict__ X, int 
 }
 
 __global__ __launch_bounds__(256) void rows_to_i8_kernel(const float *__restrict__ X, int ld, int dim, int metric,
-                                                         int64_t n, const float4 *__restrict__ rowaux,
+                                                         int64_t s0, int64_t n, const float4 *__restrict__ rowaux,
                                                          int8_t *__restrict__ Xq, float4 *__restrict__ aux8,
                                                          unsigned *__restrict__ stats) {
 	const int lane = threadIdx.x & 63;
@@ -197,18 +197,18 @@ __global__ __launch_bounds__(256) void rows_to_i8_kernel(const float *__restrict
 	// the whole build (22.7 ms for 1M rows)
 	unsigned m0 = 0u, m1 = 0u;
 	for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += (int64_t)gridDim.x * 4)
-		rows_to_i8_row(X, ld, dim, metric, r, rowaux, Xq, aux8, m0, m1, lane);
+		rows_to_i8_row(X, ld, dim, metric, s0 + r, rowaux, Xq, aux8, m0, m1, lane);
 	if (lane == 0) {
 		atomicMax(&stats[0], m0);
 		atomicMax(&stats[1], m1);
 	}
 }
 
-void launch_rows_to_i8(const float *X, int ld, int dim, int metric, int64_t n, const float4 *rowaux, int8_t *Xq,
-                       float4 *aux8, unsigned *stats, hipStream_t st) {
+void launch_rows_to_i8(const float *X, int ld, int dim, int metric, int64_t s0, int64_t n, const float4 *rowaux,
+                       int8_t *Xq, float4 *aux8, unsigned *stats, hipStream_t st) {
 	if (n <= 0) return;
 	const int64_t blocks = std::min<int64_t>((n + 3) / 4, 4096);
-	rows_to_i8_kernel<<<dim3((unsigned)blocks), dim3(256), 0, st>>>(X, ld, dim, metric, n, rowaux, Xq, aux8, stats);
+	rows_to_i8_kernel<<<dim3((unsigned)blocks), dim3(256), 0, st>>>(X, ld, dim, metric, s0, n, rowaux, Xq, aux8, stats);
 }
 
 __global__ void fill_rowaux_kernel(float4 *rowaux, int64_t from, int64_t to) {

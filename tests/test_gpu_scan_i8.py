@@ -199,3 +199,31 @@ def test_i8_prepare_option(hip, tmp_path):
         hip.LanceHipSetOption(h2, "prepare", "1")
     finally:
         hip.LanceFreeDetached(h2)
+
+
+def test_i8_incremental_append_and_delete(hip, tmp_path):
+    # appends that fit the reserved capacity and deletes update a current int8
+    # copy in place (no rebuild); results stay exact after each change
+    rng = np.random.default_rng(321)
+    d = 128
+    X = rng.standard_normal((120_000, d)).astype(np.float32)
+    X[100_000:] *= 3.0  # later rows with larger norms: the int8 maxima must grow
+    Q = rng.standard_normal((24, d)).astype(np.float32) * 2.0
+    h = _mk(hip, tmp_path, d, "l2")
+    try:
+        hip.LanceHipSetOption(h, "reserve_rows", "131072")
+        live = np.zeros(len(X), bool)
+        for lo, hi in ((0, 70_000), (70_000, 100_000), (100_000, 120_000)):
+            hip.LanceDetachedAddBatch(h, X[lo:hi], hi - lo, d)
+            live[lo:hi] = True
+            gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 10)
+            el, ed, ec = c_oracle.flat_search_batch(X, Q, 10, "l2", live=live, acc64=True, nthreads=16)
+            assert_same(gl, gd, gc, el, ed, ec)
+            dead = np.unique(el[:, :3])
+            hip.LanceDetachedDeleteBatch(h, dead)
+            live[dead] = False
+            gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 10)
+            el, ed, ec = c_oracle.flat_search_batch(X, Q, 10, "l2", live=live, acc64=True, nthreads=16)
+            assert_same(gl, gd, gc, el, ed, ec)
+    finally:
+        hip.LanceFreeDetached(h)
