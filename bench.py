@@ -98,7 +98,7 @@ def parse():
                     help="IVF_PQ: list-major 8-bit-LUT scan or the f32-LUT query-major scan (option pq_scan)")
     ap.add_argument("--refine-sweep", default="1,10,50", help="IVF_PQ: refine factors of the recall sweep")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
-                    help="extra index option (lance_hip_set_option), repeatable, e.g. --opt rscan=0")
+                    help="extra index option (lance_hip_set_option), repeatable, e.g. --opt scan_i8=off")
     a = ap.parse_args()
     for key, v in CONFIGS[a.config].items():
         if getattr(a, key, None) is None:

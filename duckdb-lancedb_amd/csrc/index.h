@@ -90,6 +90,7 @@ struct Workspace {
 	DevBuf<float> Qin, Qf, tau, cut, dense, cand_dist, out_d, fb_keys, fb_keys2, stage;
 	DevBuf<uint16_t> Qb;
 	DevBuf<float4> qaux;
+	DevBuf<float2> qm;  // int8 queries: per-query maxima (the batch scale)
 	DevBuf<uint2> seg_pool;
 	DevBuf<int> seg_cnt;
 	DevBuf<int> status, out_c;  // status = [cert | cand_cnt | pool_cnt] x nq
@@ -168,11 +169,9 @@ struct Index {
 	// scans stream it with rowaux8 as their row terms, everything else uses X
 	bool scan_i8 = true;
 	int last_scan_esz = 0;  // bytes per element the last flat search's scan streamed (1 int8, 2 bf16, 4 f32)
-	// append path: refine + finalize in one launch (option "fused_refine"; measured ~10 us slower: a
-	// per-wave sequence of exact distances against one wave per candidate)
-	bool fused_refine = false;
 	int8_t *Xq = nullptr;
 	float4 *rowaux8 = nullptr;
+	float4 *tstat8 = nullptr;  // per row tile: (s_T, max |e_x|, max |x~|, 0) of the int8 copy
 	int64_t q8_cap = 0;
 	uint64_t mut_ver = 1, q8_ver = 0;
 	DevBuf<unsigned> stats8;
@@ -231,14 +230,13 @@ struct Index {
 	int sample_div = 32;  // sample pass covers ~1/sample_div of the tiles (>= 32 tiles)
 	bool small_exact = true;  // one-launch exact search for <= 8 queries over <= 32768 slots
 	bool defer_sync = false;  // caller synchronizes the stream itself (host-buffer search)
-	bool rscan = false;      // append pass by the register-streamed kernel where it fits (option "rscan"; off: measured 3x slower, profiles/r02_g_*)
 	bool retry_pass = true;  // rerun uncertified queries with a tighter tau before the exact fallback
 	int cand_extra = 32;  // refined candidates: max(k * refine_factor, k + max(cand_extra, k))
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 	double kt_append_ms = 0.0, kt_dense_ms = 0.0;
 	int64_t kt_append_n = 0, kt_dense_n = 0;
 	int64_t kt_append_rows = 0, kt_append_qpad = 0;
-	int kt_append_kernel = 0;  // 1: the last timed append pass ran rscan_kernel, 0: scan_kernel
+	int kt_append_kernel = 0;  // 2: the last timed append pass ran scan8_kernel, 0: scan_kernel
 	// IVF list scans (ivf_search): launches, ms, and their algorithmic work:
 	// bytes = rows of every probed list once (row data or codes) + per-pair
 	// tables; pair_rows = sum over (query, list) pairs of the list's rows
@@ -253,6 +251,7 @@ struct Index {
 		if (Xs) (void)hipFree(Xs);
 		if (Xq) (void)hipFree(Xq);
 		if (rowaux8) (void)hipFree(rowaux8);
+		if (tstat8) (void)hipFree(tstat8);
 		if (rowaux) (void)hipFree(rowaux);
 		if (rowaux_l2) (void)hipFree(rowaux_l2);
 		if (dlabels) (void)hipFree(dlabels);
@@ -377,20 +376,20 @@ struct Index {
 	void ensure_i8() {
 		if (Xq && q8_ver == mut_ver && q8_cap == cap) return;
 		if (!Xq || q8_cap != cap) {
-			if (Xq) HIPCHK(hipFree(Xq));
-			if (rowaux8) HIPCHK(hipFree(rowaux8));
-			Xq = nullptr;
-			rowaux8 = nullptr;
+			drop_i8();
 			HIPCHK(hipMalloc(&Xq, (size_t)cap * ld));
 			HIPCHK(hipMalloc(&rowaux8, (size_t)cap * sizeof(float4)));
+			HIPCHK(hipMalloc(&tstat8, (size_t)(cap / SCAN_BR) * sizeof(float4)));
 			q8_cap = cap;
 		}
 		stats8.need(2);
 		HIPCHK(hipMemsetAsync(stats8.p, 0, 2 * sizeof(unsigned), stream));
-		HIPCHK(hipMemsetAsync(Xq + (size_t)n_slots * ld, 0, (size_t)(cap - n_slots) * ld, stream));
-		launch_rows_to_i8(static_cast<const float *>(X), ld, dim, metric, 0, n_slots, rowaux, Xq, rowaux8, stats8.p,
-		                  stream);
-		launch_fill_rowaux(rowaux8, n_slots, cap, stream);
+		// whole tiles up to the last row; past them: zero rows, +inf row terms
+		const int64_t t1 = (n_slots + SCAN_BR - 1) / SCAN_BR, r1 = t1 * SCAN_BR;
+		HIPCHK(hipMemsetAsync(Xq + (size_t)r1 * ld, 0, (size_t)(cap - r1) * ld, stream));
+		launch_tiles_to_i8(static_cast<const float *>(X), ld, dim, metric, n_slots, 0, t1, rowaux, Xq, rowaux8, tstat8,
+		                   stats8.p, stream);
+		launch_fill_rowaux(rowaux8, r1, cap, stream);
 		HIPCHK(hipGetLastError());
 		unsigned h[2];
 		HIPCHK(hipMemcpyAsync(h, stats8.p, sizeof(h), hipMemcpyDeviceToHost, stream));
@@ -402,8 +401,10 @@ struct Index {
 	void drop_i8() {
 		if (Xq) HIPCHK(hipFree(Xq));
 		if (rowaux8) HIPCHK(hipFree(rowaux8));
+		if (tstat8) HIPCHK(hipFree(tstat8));
 		Xq = nullptr;
 		rowaux8 = nullptr;
+		tstat8 = nullptr;
 		q8_cap = 0;
 	}
 
@@ -420,9 +421,10 @@ struct Index {
 		if (Xs) fill_scan_copy(n_slots, num, Xs);
 		launch_rowaux(X, xbf16, ld, dim, metric, n_slots, num, rowaux, stats.p, stream);
 		if (rowaux_l2) launch_rowaux(X, xbf16, ld, dim, METRIC_L2, n_slots, num, rowaux_l2, stats.p + 2, stream);
+		// (the tile the new rows start in is re-quantised whole: its scale may grow)
 		if (i8_cur)
-			launch_rows_to_i8(static_cast<const float *>(X), ld, dim, metric, n_slots, num, rowaux, Xq, rowaux8,
-			                  stats8.p, stream);
+			launch_tiles_to_i8(static_cast<const float *>(X), ld, dim, metric, n_slots + num, n_slots / SCAN_BR,
+			                   (n_slots + num + SCAN_BR - 1) / SCAN_BR, rowaux, Xq, rowaux8, tstat8, stats8.p, stream);
 		HIPCHK(hipGetLastError());
 		HIPCHK(hipStreamSynchronize(stream));
 		refresh_stats();

@@ -1069,6 +1069,7 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
 	__shared__ float4 ras[FLAT_BLK];
 	__shared__ float4 qas[FL_G];
 	__shared__ int sq[FL_G], spair[FL_G];
+	__shared__ int snan[FL_G];  // a live row of this item has a NaN bound for the query (zero cosine row / query)
 	constexpr bool FOLD = METRIC != METRIC_COSINE;
 	const int t = threadIdx.x, lane = t & 63, w = t >> 6;
 	const int gq = lane >> 4, rr = lane & 15;
@@ -1098,6 +1099,7 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
 			spair[t] = pid;
 			sq[t] = pid < 0 ? -1 : pid / nprobe;
 			qas[t] = pid < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : qaux[pid / nprobe];
+			snan[t] = 0;
 		}
 		__syncthreads();
 		// the group's bf16 query rows into LDS (zero rows for unused columns)
@@ -1122,6 +1124,7 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
 				const float av = gq == 0 ? ra.y : gq == 1 ? ra.z : gq == 2 ? ra.x : 1.0f;
 				acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, z, 0, 0, 0);
 			}
+			mfma_operand_guard();  // VALU (row pointers) follows the fold MFMAs
 		} else {
 #pragma unroll
 			for (int rb = 0; rb < 4; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1153,20 +1156,16 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
 				if (k < nw) {
 					const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(qb + 128 * k);
 					const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(qb + 128 * k + 64);
-					uint4 cur[4][2];
 #pragma unroll
 					for (int rb = 0; rb < 4; ++rb) {
-						cur[rb][0] = xa[h][rb][0];
-						cur[rb][1] = xa[h][rb][1];
+						acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xa[h][rb][0]), b0,
+						                                                  acc[rb], 0, 0, 0);
+						acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xa[h][rb][1]), b1,
+						                                                  acc[rb], 0, 0, 0);
 					}
+					// refill the window's registers after the MFMAs that read them (no
+					// register copy between the load and the MFMAs; the load lands late)
 					if (k + 2 < nw) ldx(xa[h], k + 2);
-#pragma unroll
-					for (int rb = 0; rb < 4; ++rb) {
-						acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, cur[rb][0]), b0,
-						                                                  acc[rb], 0, 0, 0);
-						acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, cur[rb][1]), b1,
-						                                                  acc[rb], 0, 0, 0);
-					}
 				}
 			}
 		}
@@ -1190,7 +1189,11 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
 						v = fmaf(acc[rb][i] * ra.w, qa.x, v);
 						lb = v + qa.w;
 					}
-					const bool ok = s != SLOT_NONE && ras[r].x != F_INF && !__builtin_isnan(lb);
+					const bool live = s != SLOT_NONE && ras[r].x != F_INF;
+					const bool ok = live && !__builtin_isnan(lb);
+					// a live row without a bound cannot be certified away: the
+					// item's boundary becomes -inf (the query reruns exactly)
+					if (live && __builtin_isnan(lb)) snan[rr] = 1;
 					sk[rr * FLAT_BLK + r] = ok ? key64(lb, s) : KEY64_NONE;
 				}
 		}
@@ -1207,6 +1210,7 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
 				if ((lane >> 4) == ww) best = moved;
 			}
 			best = wave_sort64(best);
+			if (lane == FL_T - 1 && snan[c]) best = key64(-F_INF, 0u);  // boundary -inf: never certified
 			if (lane < FL_T) out[((int64_t)spair[c] * maxb + bi) * FL_T + lane] = best;
 		}
 	}

@@ -42,6 +42,8 @@ struct StoreView {
 	// instead of rowaux; null / 0 = rowaux and the bf16 / f32 rows above
 	const float4 *scan_aux = nullptr;
 	int scan_i8 = 0;
+	// int8 scan copy: per row tile (s_T, max |e_x|, max |x~|, 0)
+	const float4 *tstat = nullptr;
 };
 
 // Per-query constants for the lower-bound epilogue:
@@ -65,11 +67,14 @@ void launch_rowaux(const void *X, int xbf16, int ld, int dim, int metric, int64_
 // dst rows of stride ld, zero-filling columns [dim, ld).
 void launch_rows_to_bf16(const float *src, int64_t src_ld, int64_t n, int dim, int ld, uint16_t *dst, hipStream_t st);
 
-// int8 scan copy of slots [s0, s0+n) of an f32 store: int8 rows Xq (stride ld
-// bytes, zero padded) and their row terms aux8 (tombstones copied from
-// rowaux); folds max |alpha| and max(xn, ux) into stats[0], stats[1] (float bits).
-void launch_rows_to_i8(const float *X, int ld, int dim, int metric, int64_t s0, int64_t n, const float4 *rowaux,
-                       int8_t *Xq, float4 *aux8, unsigned *stats, hipStream_t st);
+// int8 scan copy of the row tiles [t0, t1) (SCAN_BR rows each) of an f32 store
+// holding n_slots rows: one scale per tile, int8 rows Xq (stride ld bytes, zero
+// padded; rows past n_slots zero), their row terms aux8 (tombstones copied from
+// rowaux, rows past n_slots +inf) and per-tile terms tstat[t] = (s_T, max |e_x|,
+// max |x~|, 0); folds max |alpha| and max(xn, ux) into stats[0], stats[1] (float bits).
+void launch_tiles_to_i8(const float *X, int ld, int dim, int metric, int64_t n_slots, int64_t t0, int64_t t1,
+                        const float4 *rowaux, int8_t *Xq, float4 *aux8, float4 *tstat, unsigned *stats,
+                        hipStream_t st);
 
 // rowaux[from, to) = (+inf, 0, 0, 0): padding rows past the last slot.
 void launch_fill_rowaux(float4 *rowaux, int64_t from, int64_t to, hipStream_t st);
@@ -82,10 +87,12 @@ void launch_filter_rowaux(const float4 *src, const uint8_t *mask, int64_t n_slot
                           hipStream_t st);
 
 // ---- search ------------------------------------------------------------------
-// int8 scan (scan_i8): int8 queries into Qb's rows (first ld bytes of each
-// 2*ld-byte row) and the int8 bound's constants; Qf and zero3 as below.
+// int8 scan (scan_i8): int8 queries (one scale for the batch) into Qb's rows
+// (first ld bytes of each 2*ld-byte row) and the int8 bound's constants; Qf and
+// zero3 as below; qm = nq scratch float2 (per-query maxima).
 void launch_prep_queries_i8(const float *Q, int nq, int dim, int ld, int nq_pad, int metric, float max_alpha,
-                            float max_x, float *Qf, uint16_t *Qb, float4 *qaux, int *zero3, hipStream_t st);
+                            float max_x, float2 *qm, float *Qf, uint16_t *Qb, float4 *qaux, int *zero3,
+                            hipStream_t st);
 // Also zeroes zero3[0 .. 3*nq) when non-null (the search's status words).
 void launch_prep_queries(const float *Q, int nq, int dim, int ld, int nq_pad, int metric, float max_alpha,
                          float max_ux, float *Qf, uint16_t *Qb, float4 *qaux, int *zero3, hipStream_t st);
@@ -103,13 +110,6 @@ void launch_scan_dense(const StoreView &s, const QueryView &q, int64_t n_tiles, 
 void launch_scan_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
                         int seg_cap, hipStream_t st);
 
-// The same append pass by the register-streamed kernel (rscan_kernels.hip):
-// rows go HBM -> registers (no LDS stage), one wave per SIMD, 16x16x32 bf16
-// MFMA; identical bounds and outputs.  rscan_fits: row bytes a multiple of 512.
-bool rscan_fits(const StoreView &s);
-void launch_rscan_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
-                         int seg_cap, hipStream_t st);
-
 // Sample scan over row tiles t*tile_stride, t < n_tiles (persistent, scan_grid(n_tiles)
 // workgroups): for every tile, each 64-row quarter appends its smallest lower
 // bound per query, (orderedkey(LB), slot), to the workgroup's segment as
@@ -119,6 +119,19 @@ void launch_scan_tilemin(const StoreView &s, const QueryView &q, int64_t n_tiles
 
 // Workgroups a scan over n_tiles tiles launches (= min(n_tiles, CUs)).
 int scan_grid(int64_t n_tiles);
+
+// The int8 append pass by scan8_kernel (scan8_kernels.hip): workgroup PAIRS,
+// each half of a 256-query tile resident in LDS, rows HBM -> registers, bounds
+// screened in exact integers (tile / batch common scales).  Applies to an int8
+// scan copy with ld in [512, 1024]; writes scan8_segments(n_tiles) segments per
+// query (one per pair) in launch_scan_append's format.
+bool scan8_fits(const StoreView &s);
+int scan8_segments(int64_t n_tiles);
+void scan8_set_variant(int v);  // development knob: geometry of the ld = 768 kernel (0 = default)
+void launch_scan8_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
+                         int seg_cap, hipStream_t st);
+// Segments per query launch_scan_append writes for this store.
+int scan_append_segments(const StoreView &s, int64_t n_tiles);
 
 // Per-query top-M selection by LB.  Writes cand_slot[q][0..M), cand_cnt[q] and
 // the cut cut[q] = a lower bound on the true distance of every live row not
@@ -132,6 +145,19 @@ void launch_select_segments(const uint2 *seg_pool, const int *seg_cnt, int seg_c
                             int nq, int M, uint32_t *cand_slot, int *cand_cnt, float *cut, int *pool_total,
                             int *big, hipStream_t st);
 
+// Select + refine + finalize of a threshold pass in one launch: per query the
+// segments (every row with LB <= tau) sorted by (LB, slot) and refined in that
+// order.  mode 1 (final): until the next bound exceeds the k-th exact distance;
+// writes top-k L / D / C and the certificate (as finalize, incl. the live-count
+// check; tau may be null = +inf).  mode 0 (sample): refines the m_tau smallest
+// bounds, tau_out[q] = their k-th smallest exact distance (+inf when fewer,
+// NaN when any is NaN).  refined[q] = rows refined, pool_total[q] = pool size
+// (-1 on overflow); both may be null.  n_seg <= 512, k <= MAX_CAND.
+void launch_pool_refine(const StoreView &s, const QueryView &q, const uint2 *seg_pool, const int *seg_cnt,
+                        int seg_cap, int n_seg, const float *tau, int k, int mode, int m_tau, int64_t live,
+                        float *tau_out, int64_t *L, float *D, int *C, int *cert, int *refined, int *pool_total,
+                        hipStream_t st);
+
 // Exact distances (f64 accumulation, rounded to f32) of the candidates.
 void launch_refine(const StoreView &s, const QueryView &q, const uint32_t *cand_slot, const int *cand_cnt, int M,
                    float *cand_dist, hipStream_t st);
@@ -141,17 +167,14 @@ void launch_refine(const StoreView &s, const QueryView &q, const uint32_t *cand_
 void launch_refine_tau(const StoreView &s, const QueryView &q, const uint32_t *cand_slot, const int *cand_cnt, int M,
                        int need, float *tau, hipStream_t st);
 
-// refine + finalize mode 1 in one launch (the same outputs and certificate;
-// cand_dist not written).
-void launch_refine_final(const StoreView &s, const QueryView &q, const uint32_t *cand_slot, const int *cand_cnt,
-                         const float *cut, int M, int k, int64_t *L, float *D, int *C, int *cert, hipStream_t st);
-
 // Sort candidates by (distance, label).  mode 0 (TAU): tau[q] = largest exact
 // distance among the candidates when at least need_for_tau of them exist, else
-// +inf.  mode 1 (FINAL): writes top-k, counts and the certificate ok[q].
+// +inf.  mode 1 (FINAL): writes top-k, counts and the certificate ok[q] (false when
+// live >= 0 and fewer than min(k, live) hits came out).
 void launch_finalize(const StoreView &s, const uint32_t *cand_slot, const int *cand_cnt, const float *cand_dist,
                      const float *cut, int nq, int M, int k, int mode, int need_for_tau, float *tau,
-                     int64_t *out_labels, float *out_dists, int *out_counts, int *cert_ok, hipStream_t st);
+                     int64_t *out_labels, float *out_dists, int *out_counts, int *cert_ok, hipStream_t st,
+                    int64_t live = -1);
 
 // Exact fallback for one query: exact distance of every slot into keys[n_slots]
 // (dead slots -> NaN with all-ones payload so they sort last), labels into vals.

@@ -55,7 +55,10 @@ __device__ __forceinline__ void rowaux_row(const T *__restrict__ X, int ld, int 
 		double ux = (xn + ex) * (1.0 + 4.0 * U_BOUND);
 		float4 a;
 		if (metric == METRIC_L2) {
-			a = make_float4((float)s2, (float)xn, (float)ux, 1.0f);
+			// alpha = +inf is the tombstone code: a live row whose |x|^2 overflows f32
+			// keeps the largest finite alpha (below |x|^2: the bound stays a lower
+			// bound; finalize's count check catches a bound that still overflows)
+			a = make_float4(fminf((float)s2, F_MAX), (float)xn, (float)ux, 1.0f);
 		} else if (metric == METRIC_DOT) {
 			a = make_float4(0.0f, (float)xn, (float)ux, 1.0f);
 		} else {
@@ -117,98 +120,156 @@ void launch_rows_to_bf16(const float *src, int64_t src_ld, int64_t n, int dim, i
 }
 
 // ---------------------------------------------------------------------------
-// int8 scan copy (option scan_i8, an f32 store): per row x^ = rint(x * 127 /
-// max|x_i|) in [-127, 127], scale s = max|x_i| / 127 (an f32 value), x~ = s*x^.
-// The int8 scan's rigorous bound (scan_kernel XT = 2):
-//   |x.q - s_x s_q (x^.q^)| <= |e_x||q| + |x~||e_q|,   e_x = x - x~  (f64, exact)
+// int8 scan copy (option scan_i8, an f32 store), one scale per 256-row tile:
+//   v = x (l2, dot) or x/|x| (cosine), s_T = max over the tile's rows of
+//   max|v_i| / 127 (an f32 value), x^ = rint(v / s_T) in [-127, 127], x~ = s_T x^.
+// The int8 scans' rigorous bound:
+//   |v.q - s_T s_Q (x^.q^)| <= |e_x||q| + |x~||e_q|,   e_x = v - x~  (f64)
 // and x^.q^ is an exact integer (|x^.q^| <= ld * 127^2 < 2^24 for ld <= 1024:
 // exact in f32 too).  Row terms (tile-blocked SoA like rowaux):
-//   l2: (|x|^2, |e_x|, |x~|, s)   dot: (0, |e_x|, |x~|, s)
-//   cosine: (0, |e_x|/|x|, |x~|/|x|, s/|x|)   (norms rounded up)
-// alpha copies the store's tombstones (+inf); a zero cosine row is NaN (exact
-// fallback), as in rowaux.  stats[0] = max |alpha|, stats[1] = max(xn, ux).
+//   l2: (|x|^2, |e_x|, |x~|, s_T)   dot: (0, |e_x|, |x~|, s_T)
+//   cosine: (0, |e_x|, |x~|, s_T) of the normalised row   (norms rounded up)
+// Per tile: tstat = (s_T, max |e_x|, max |x~|, 0) over its rows.  A scale common
+// to the tile (and one common to the query batch, prep_queries_i8) makes the
+// product scale of a bound s_T s_Q the same for every (row, query) of a tile:
+// scan8_kernel screens bounds in exact integers with it.  alpha copies the
+// store's tombstones (+inf); a zero cosine row is NaN (exact fallback), as in
+// rowaux.  stats[0] = max |alpha|, stats[1] = max(xn, ux).
+// One 256-thread workgroup per tile: row maxima into LDS, the tile scale, then
+// each wave quantises rows (rows past n_slots: zero, alpha = +inf).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void rows_to_i8_row(const float *__restrict__ X, int ld, int dim, int metric, int64_t r,  // r: absolute slot
-                                               const float4 *__restrict__ rowaux, int8_t *__restrict__ Xq,
-                                               float4 *__restrict__ aux8, unsigned &m0, unsigned &m1, int lane) {
-	const float *x = X + r * (int64_t)ld;
-	float m = 0.f;
-	for (int i = lane; i < dim; i += 64) m = fmaxf(m, fabsf(x[i]));
-#pragma unroll
-	for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-	const float sx = m / 127.0f;
-	const float inv = m > 0.f ? 127.0f / m : 0.f;
-	double s2 = 0.0, e2 = 0.0, t2 = 0.0;
-	// four elements per lane and step: one packed 4-byte store (ld is a multiple of 128)
-	uint32_t *xq = reinterpret_cast<uint32_t *>(Xq + r * (int64_t)ld);
-	for (int i0 = 4 * lane; i0 < ld; i0 += 256) {
-		uint32_t packed = 0u;
-#pragma unroll
-		for (int j = 0; j < 4; ++j) {
-			const int i = i0 + j;
-			int qv = 0;
-			if (i < dim) {
+__global__ __launch_bounds__(256) void tiles_to_i8_kernel(const float *__restrict__ X, int ld, int dim, int metric,
+                                                          int64_t n_slots, int64_t t0,
+                                                          const float4 *__restrict__ rowaux, int8_t *__restrict__ Xq,
+                                                          float4 *__restrict__ aux8, float4 *__restrict__ tstat,
+                                                          unsigned *__restrict__ stats) {
+	__shared__ float rmax[SCAN_BR];
+	__shared__ double rnorm[SCAN_BR];
+	__shared__ float red[3][4];
+	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+	const int64_t tile = t0 + blockIdx.x;
+	const bool cosine = metric == METRIC_COSINE;
+	// pass 1: per row max|v_i| and |x|
+	for (int rr = wv; rr < SCAN_BR; rr += 4) {
+		const int64_t r = tile * SCAN_BR + rr;
+		float m = 0.f;
+		double s2 = 0.0;
+		if (r < n_slots) {
+			const float *x = X + r * (int64_t)ld;
+			for (int i = lane; i < dim; i += 64) {
 				const float v = x[i];
-				qv = min(127, max(-127, (int)rintf(v * inv)));
-				const double xt = (double)sx * (double)qv;
-				const double e = (double)v - xt;
+				m = fmaxf(m, fabsf(v));
 				s2 += (double)v * v;
-				e2 += e * e;
-				t2 += xt * xt;
 			}
-			packed |= ((uint32_t)qv & 0xFFu) << (8 * j);
 		}
-		xq[i0 >> 2] = packed;
+#pragma unroll
+		for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+		s2 = wave_sum_f64(s2);
+		if (lane == 0) {
+			const double xn = sqrt(s2);
+			rnorm[rr] = xn;
+			rmax[rr] = cosine ? (xn > 0.0 ? (float)((double)m / xn) : 0.f) : m;
+		}
 	}
-	s2 = wave_sum_f64(s2);
-	e2 = wave_sum_f64(e2);
-	t2 = wave_sum_f64(t2);
-	if (lane != 0) return;
+	__syncthreads();
+	float M = 0.f;
+	for (int i = threadIdx.x; i < SCAN_BR; i += 256) M = fmaxf(M, rmax[i]);
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
+	if (lane == 0) red[0][wv] = M;
+	__syncthreads();
+	M = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+	// (cosine: the rounded row maxima may sit a hair under the f64 quotients;
+	// the clamp to +-127 keeps x^ in range and e_x stays exact either way)
+	const float sT = M / 127.0f;
+	const double inv = M > 0.f ? 127.0 / (double)M : 0.0;
 	const double up = 1.0 + 4.0 * U_BOUND;
-	const double xn = sqrt(s2), ex = sqrt(e2) * up, xt = sqrt(t2) * up;
-	float4 a;
-	if (metric == METRIC_L2) {
-		a = make_float4((float)s2, (float)ex, (float)xt, sx);
-	} else if (metric == METRIC_DOT) {
-		a = make_float4(0.0f, (float)ex, (float)xt, sx);
-	} else if (xn > 0.0) {
-		a = make_float4(0.0f, (float)(ex / xn * up), (float)(xt / xn * up), (float)(sx / xn));
-	} else {
-		a = make_float4(__builtin_nanf(""), 0.0f, 0.0f, 0.0f);
-	}
-	const float *ra = reinterpret_cast<const float *>(rowaux);
-	if (__builtin_isinf(ra[raix(r, 0)])) a.x = F_INF;  // tombstone
-	float *o = reinterpret_cast<float *>(aux8);
-	o[raix(r, 0)] = a.x;
-	o[raix(r, 1)] = a.y;
-	o[raix(r, 2)] = a.z;
-	o[raix(r, 3)] = a.w;
-	if (a.x == a.x && a.x != F_INF) m0 = max(m0, __float_as_uint(fabsf(a.x)));
-	if (a.y == a.y) m1 = max(m1, __float_as_uint(fmaxf(a.y, a.z)));
-}
-
-__global__ __launch_bounds__(256) void rows_to_i8_kernel(const float *__restrict__ X, int ld, int dim, int metric,
-                                                         int64_t s0, int64_t n, const float4 *__restrict__ rowaux,
-                                                         int8_t *__restrict__ Xq, float4 *__restrict__ aux8,
-                                                         unsigned *__restrict__ stats) {
-	const int lane = threadIdx.x & 63;
-	// grid-stride over rows (one wave per row at a time); the maxima go out
-	// once per wave: an atomicMax per row on the same two words serialised
-	// the whole build (22.7 ms for 1M rows)
 	unsigned m0 = 0u, m1 = 0u;
-	for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += (int64_t)gridDim.x * 4)
-		rows_to_i8_row(X, ld, dim, metric, s0 + r, rowaux, Xq, aux8, m0, m1, lane);
+	float wxn = 0.f, wux = 0.f;  // this wave's row maxima of |e_x|, |x~|
+	__syncthreads();             // red[0] read by every wave before it is reused
+	// pass 2: quantise
+	for (int rr = wv; rr < SCAN_BR; rr += 4) {
+		const int64_t r = tile * SCAN_BR + rr;
+		uint32_t *xq = reinterpret_cast<uint32_t *>(Xq + r * (int64_t)ld);
+		float *o = reinterpret_cast<float *>(aux8);
+		if (r >= n_slots) {
+			for (int i0 = 4 * lane; i0 < ld; i0 += 256) xq[i0 >> 2] = 0u;
+			if (lane == 0) {
+				o[raix(r, 0)] = F_INF;
+				o[raix(r, 1)] = 0.f;
+				o[raix(r, 2)] = 0.f;
+				o[raix(r, 3)] = sT;
+			}
+			continue;
+		}
+		const float *x = X + r * (int64_t)ld;
+		const double xn = rnorm[rr];
+		const double rs = (cosine && xn > 0.0) ? 1.0 / xn : 1.0;
+		double e2 = 0.0, t2 = 0.0;
+		// four elements per lane and step: one packed 4-byte store (ld is a multiple of 128)
+		for (int i0 = 4 * lane; i0 < ld; i0 += 256) {
+			uint32_t packed = 0u;
+#pragma unroll
+			for (int j = 0; j < 4; ++j) {
+				const int i = i0 + j;
+				int qv = 0;
+				if (i < dim) {
+					const double v = cosine ? (double)x[i] * rs : (double)x[i];
+					qv = (int)fmin(127.0, fmax(-127.0, rint(v * inv)));
+					const double xt = (double)sT * (double)qv;
+					const double e = v - xt;
+					e2 += e * e;
+					t2 += xt * xt;
+				}
+				packed |= ((uint32_t)qv & 0xFFu) << (8 * j);
+			}
+			xq[i0 >> 2] = packed;
+		}
+		e2 = wave_sum_f64(e2);
+		t2 = wave_sum_f64(t2);
+		// cosine: v = x/|x| carries the f64 rounding of the quotient; 2^-40
+		// covers it in |e_x| (the bound needs |v_true - x~|)
+		const double ex = sqrt(e2) * up + (cosine ? 0x1p-40 : 0.0), xt = sqrt(t2) * up;
+		float4 a;
+		if (metric == METRIC_L2)
+			a = make_float4((float)(xn * xn), (float)ex, (float)xt, sT);
+		else if (!cosine || xn > 0.0)
+			a = make_float4(0.0f, (float)ex, (float)xt, sT);
+		else
+			a = make_float4(__builtin_nanf(""), 0.0f, 0.0f, sT);  // cosine undefined: exact fallback
+		const float *ra = reinterpret_cast<const float *>(rowaux);
+		if (__builtin_isinf(ra[raix(r, 0)])) a.x = F_INF;  // tombstone
+		// (|x|^2 as rowaux computes it: the f64 sum rounded once)
+		if (metric == METRIC_L2 && a.x != F_INF) a.x = ra[raix(r, 0)];
+		if (lane == 0) {
+			o[raix(r, 0)] = a.x;
+			o[raix(r, 1)] = a.y;
+			o[raix(r, 2)] = a.z;
+			o[raix(r, 3)] = a.w;
+		}
+		wxn = fmaxf(wxn, a.y);
+		wux = fmaxf(wux, a.z);
+		if (a.x == a.x && a.x != F_INF) m0 = max(m0, __float_as_uint(fabsf(a.x)));
+		m1 = max(m1, __float_as_uint(fmaxf(a.y, a.z)));
+	}
 	if (lane == 0) {
+		red[1][wv] = wxn;
+		red[2][wv] = wux;
 		atomicMax(&stats[0], m0);
 		atomicMax(&stats[1], m1);
 	}
+	__syncthreads();
+	if (threadIdx.x == 0)
+		tstat[tile] = make_float4(sT, fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3])),
+		                          fmaxf(fmaxf(red[2][0], red[2][1]), fmaxf(red[2][2], red[2][3])), 0.f);
 }
 
-void launch_rows_to_i8(const float *X, int ld, int dim, int metric, int64_t s0, int64_t n, const float4 *rowaux,
-                       int8_t *Xq, float4 *aux8, unsigned *stats, hipStream_t st) {
-	if (n <= 0) return;
-	const int64_t blocks = std::min<int64_t>((n + 3) / 4, 4096);
-	rows_to_i8_kernel<<<dim3((unsigned)blocks), dim3(256), 0, st>>>(X, ld, dim, metric, s0, n, rowaux, Xq, aux8, stats);
+void launch_tiles_to_i8(const float *X, int ld, int dim, int metric, int64_t n_slots, int64_t t0, int64_t t1,
+                        const float4 *rowaux, int8_t *Xq, float4 *aux8, float4 *tstat, unsigned *stats,
+                        hipStream_t st) {
+	if (t1 <= t0) return;
+	tiles_to_i8_kernel<<<dim3((unsigned)(t1 - t0)), dim3(256), 0, st>>>(X, ld, dim, metric, n_slots, t0, rowaux, Xq,
+	                                                                    aux8, tstat, stats);
 }
 
 __global__ void fill_rowaux_kernel(float4 *rowaux, int64_t from, int64_t to) {
@@ -326,17 +387,49 @@ void launch_prep_queries(const float *Q, int nq, int dim, int ld, int nq_pad, in
 	                                                           qaux, zero3);
 }
 
-// int8 scan queries: Qf as prep_queries; Qi = int8 q^ = rint(q * 127 / max|q_i|)
-// in the first ld bytes of each 2*ld-byte row of the Qb buffer (so the retry
-// gather copies it like a bf16 row); per-query constants of the int8 bound
-// (rows_to_i8_kernel): LB = alpha + xn*B + ux*A + (s*sc)*S + C with
-//   l2: S = -2 s_q, A = -2|e_q|, B = -2|q|, C = |q|^2 - slack
-//   dot: S = -s_q, A = -|e_q|, B = -|q|, C = 1 - slack
-//   cosine: S = -s_q/|q|, A = -|e_q|/|q|, B = -1, C = 1 - slack
+// int8 scan queries, one scale for the whole batch (tiles_to_i8_kernel keeps one
+// per row tile): v = q (l2, dot) or q/|q| (cosine), s_Q = max over the batch of
+// max|v_i| / 127, q^ = rint(v / s_Q).  Pass 1 (query_absmax_kernel): per query
+// (max|v_i|, |q|); pass 2: Qf as prep_queries; Qi = q^ in the first ld bytes of
+// each 2*ld-byte row of the Qb buffer (so the retry gather copies it like a bf16
+// row); per-query constants of the int8 bound:
+//   LB = alpha + xn*B + ux*A + (s*sc)*S + C      (sc = s_T of the row's tile)
+//   l2: S = -2 s_Q, A = -2|e_q|, B = -2|q|, C = |q|^2 - slack
+//   dot: S = -s_Q, A = -|e_q|, B = -|q|, C = 1 - slack
+//   cosine: S = -s_Q, A = -|e_q|, B = -1, C = 1 - slack   (normalised rows and query)
+// S is the same for every query of the batch (scan8_kernel relies on it).
 // slack: f32 evaluation of the five-term sum, every intermediate bounded by
 // max_alpha + |q|^2 + 4 max_x (|q| + |e_q|) (max_x = max over rows of xn, ux).
+__global__ __launch_bounds__(256) void query_absmax_kernel(const float *__restrict__ Q, int nq, int dim, int metric,
+                                                           float2 *__restrict__ qm) {
+	__shared__ float redm[4];
+	__shared__ double reds[4];
+	const int q = blockIdx.x, t = threadIdx.x;
+	float m = 0.f;
+	double s2 = 0.0;
+	for (int i = t; i < dim; i += 256) {
+		const float v = Q[(int64_t)q * dim + i];
+		m = fmaxf(m, fabsf(v));
+		s2 += (double)v * v;
+	}
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+	s2 = wave_sum_f64(s2);
+	if ((t & 63) == 0) {
+		redm[t >> 6] = m;
+		reds[t >> 6] = s2;
+	}
+	__syncthreads();
+	if (t != 0) return;
+	m = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
+	const double qn = sqrt(reds[0] + reds[1] + reds[2] + reds[3]);
+	const float mv = metric == METRIC_COSINE ? (qn > 0.0 ? (float)((double)m / qn) : 0.f) : m;
+	qm[q] = make_float2(mv, (float)qn);
+}
+
 __global__ __launch_bounds__(256) void prep_queries_i8_kernel(const float *__restrict__ Q, int nq, int dim, int ld,
                                                               int metric, float max_alpha, float max_x,
+                                                              const float2 *__restrict__ qm,
                                                               float *__restrict__ Qf, int8_t *__restrict__ Qi,
                                                               float4 *__restrict__ qaux, int *__restrict__ zero3) {
 	__shared__ double red[2][4];
@@ -344,26 +437,27 @@ __global__ __launch_bounds__(256) void prep_queries_i8_kernel(const float *__res
 	const int q = blockIdx.x;
 	const int t = threadIdx.x;
 	if (zero3 && t < 3 && q < nq) zero3[t * nq + q] = 0;
+	// the batch scale: max over every query's max|v_i|
 	float m = 0.f;
-	for (int i = t; i < ld; i += 256) {
-		const float v = (q < nq && i < dim) ? Q[(int64_t)q * dim + i] : 0.0f;
-		Qf[(int64_t)q * ld + i] = v;
-		m = fmaxf(m, fabsf(v));
-	}
+	for (int i = t; i < nq; i += 256) m = fmaxf(m, qm[i].x);
 #pragma unroll
 	for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
 	if ((t & 63) == 0) redm[t >> 6] = m;
 	__syncthreads();
 	m = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
+	const bool cosine = metric == METRIC_COSINE;
+	const double qn0 = q < nq ? (double)qm[q].y : 0.0;  // (|q| rounded to f32: only scales v below)
 	const float sq = m / 127.0f;
-	const float inv = m > 0.f ? 127.0f / m : 0.f;
+	const double inv = m > 0.f ? 127.0 / (double)m : 0.0;
 	double s2 = 0.0, e2 = 0.0;
 	for (int i = t; i < ld; i += 256) {
-		const float v = (q < nq && i < dim) ? Q[(int64_t)q * dim + i] : 0.0f;
-		const int qv = min(127, max(-127, (int)rintf(v * inv)));
+		const float x = (q < nq && i < dim) ? Q[(int64_t)q * dim + i] : 0.0f;
+		Qf[(int64_t)q * ld + i] = x;
+		const double v = (cosine && qn0 > 0.0) ? (double)x / qn0 : (double)x;
+		const int qv = (int)fmin(127.0, fmax(-127.0, rint(v * inv)));
 		Qi[(int64_t)q * ld * 2 + i] = (int8_t)qv;
-		const double e = (double)v - (double)sq * (double)qv;
-		s2 += (double)v * v;
+		const double e = v - (double)sq * (double)qv;
+		s2 += (double)x * x;
 		e2 += e * e;
 	}
 	s2 = wave_sum_f64(s2);
@@ -381,7 +475,10 @@ __global__ __launch_bounds__(256) void prep_queries_i8_kernel(const float *__res
 		return;
 	}
 	const double u = U_BOUND, up = 1.0 + 4.0 * u;
-	const double qn = sqrt(s2), qnu = qn * up, equ = sqrt(e2) * up;
+	const double qn = sqrt(s2), qnu = qn * up;
+	// cosine: v = q/|q| in f64 from an f32-rounded |q|; |e_q| (taken against the
+	// true q/|q|) and |v| <= 1 + 2^-20 cover both roundings
+	const double equ = sqrt(e2) * up + (cosine ? 0x1p-20 * (1.0 + sqrt(e2)) : 0.0);
 	float4 a;
 	if (metric == METRIC_L2) {
 		const double slack = 16.0 * u * ((double)max_alpha + s2 + 4.0 * (double)max_x * (qnu + equ)) + 1e-30;
@@ -390,8 +487,9 @@ __global__ __launch_bounds__(256) void prep_queries_i8_kernel(const float *__res
 		const double slack = 16.0 * u * (1.0 + 4.0 * (double)max_x * (qnu + equ)) + 1e-30;
 		a = make_float4(-sq, (float)(-equ), (float)(-qnu), (float)(1.0 - slack));
 	} else if (qn > 0.0) {
-		const double slack = 16.0 * u * (2.0 + 4.0 * (double)max_x * (1.0 + equ / qn) * up) + 1e-30;
-		a = make_float4((float)(-(double)sq / qn), (float)(-(equ / qn) * up), -1.0f, (float)(1.0 - slack));
+		const double vn = 1.0 + 0x1p-20;  // |q/|q|| with the quotient's rounding
+		const double slack = 16.0 * u * (2.0 + 4.0 * (double)max_x * (vn + equ)) + 1e-30;
+		a = make_float4(-sq, (float)(-equ), (float)(-vn * up), (float)(1.0 - slack));
 	} else {
 		a = make_float4(0.f, 0.f, 0.f, __builtin_nanf(""));  // undefined: exact fallback
 	}
@@ -399,8 +497,10 @@ __global__ __launch_bounds__(256) void prep_queries_i8_kernel(const float *__res
 }
 
 void launch_prep_queries_i8(const float *Q, int nq, int dim, int ld, int nq_pad, int metric, float max_alpha,
-                            float max_x, float *Qf, uint16_t *Qb, float4 *qaux, int *zero3, hipStream_t st) {
-	prep_queries_i8_kernel<<<dim3(nq_pad), dim3(256), 0, st>>>(Q, nq, dim, ld, metric, max_alpha, max_x, Qf,
+                            float max_x, float2 *qm, float *Qf, uint16_t *Qb, float4 *qaux, int *zero3,
+                            hipStream_t st) {
+	if (nq > 0) query_absmax_kernel<<<dim3(nq), dim3(256), 0, st>>>(Q, nq, dim, metric, qm);
+	prep_queries_i8_kernel<<<dim3(nq_pad), dim3(256), 0, st>>>(Q, nq, dim, ld, metric, max_alpha, max_x, qm, Qf,
 	                                                              reinterpret_cast<int8_t *>(Qb), qaux, zero3);
 }
 
@@ -607,11 +707,16 @@ __device__ __forceinline__ void dma16s(const void *sbase, uint32_t voff, uint32_
 	const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
 	const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32));
 	const uint64_t ub = ((uint64_t)hi << 32) | (uint64_t)lo;
+	// s_nop 4: the base may come straight from v_readfirstlane (a VALU write of
+	// an SGPR that the VMEM below reads: the compiler cannot see through the asm);
+	// s_nop 0: the M0 write -> LDS-DMA hazard
 	if (NT)
-		asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt" ::"s"(lds_addr), "v"(voff), "s"(ub)
+		asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt" ::"s"(lds_addr),
+		             "v"(voff), "s"(ub)
 		             : "memory", "m0");
 	else
-		asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds_addr), "v"(voff), "s"(ub)
+		asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds_addr),
+		             "v"(voff), "s"(ub)
 		             : "memory", "m0");
 }
 
@@ -1562,11 +1667,19 @@ void launch_scan_tilemin(const StoreView &s, const QueryView &q, int64_t n_tiles
 	scan_dispatch<2>(s, q, n_tiles, tile_stride, nullptr, 0, nullptr, seg_pool, seg_cnt, seg_cap, st);
 }
 
+int scan_append_segments(const StoreView &s, int64_t n_tiles) {
+	return scan8_fits(s) ? scan8_segments(n_tiles) : scan_grid(n_tiles);
+}
+
 void launch_scan_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
                         int seg_cap, hipStream_t st) {
 	int64_t n_tiles = (s.n_slots + BR - 1) / BR;
 	if (n_tiles <= 0) return;
 	if (seg_cap <= 0 || seg_cap > 1024) throw std::runtime_error("scan: segment capacity must be in [1, 1024]");
+	if (scan8_fits(s)) {
+		launch_scan8_append(s, q, tau, seg_pool, seg_cnt, seg_cap, st);
+		return;
+	}
 	if ((n_tiles + scan_grid(n_tiles) - 1) / scan_grid(n_tiles) >= 65536)
 		throw std::runtime_error("scan: more than 65535 tiles per workgroup");  // 16-bit tile index in list entries
 	scan_dispatch<1>(s, q, n_tiles, 1, nullptr, 0, tau, seg_pool, seg_cnt, seg_cap, st);
@@ -2086,7 +2199,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(const int64_t *__restrict
                                                        int need_for_tau, float *__restrict__ tau,
                                                        int64_t *__restrict__ out_labels,
                                                        float *__restrict__ out_dists, int *__restrict__ out_counts,
-                                                       int *__restrict__ cert_ok) {
+                                                       int *__restrict__ cert_ok, int64_t live) {
 	__shared__ float sd[MAX_CAND];
 	__shared__ int64_t sl[MAX_CAND];
 	__shared__ float s_dk;
@@ -2146,101 +2259,288 @@ __global__ __launch_bounds__(256) void finalize_kernel(const int64_t *__restrict
 			const float dk = s_dk;  // +inf when fewer than k candidates
 			ok = !__builtin_isnan(dk) && dk < F_INF && c > nextafterf(dk, F_INF);
 		}
+		// fewer hits than min(k, live rows): a live row is missing (one whose
+		// bound overflowed to +inf, as a tombstone's does): never certified
+		if (live >= 0 && (int64_t)nout < (live < (int64_t)k ? live : (int64_t)k)) ok = false;
 		cert_ok[q] = ok ? 1 : 0;
 	}
 }
 
 void launch_finalize(const StoreView &s, const uint32_t *cand_slot, const int *cand_cnt, const float *cand_dist,
                      const float *cut, int nq, int M, int k, int mode, int need_for_tau, float *tau,
-                     int64_t *out_labels, float *out_dists, int *out_counts, int *cert_ok, hipStream_t st) {
+                     int64_t *out_labels, float *out_dists, int *out_counts, int *cert_ok, hipStream_t st,
+                     int64_t live) {
 	finalize_kernel<<<dim3(nq), dim3(256), 0, st>>>(s.labels, cand_slot, cand_cnt, cand_dist, cut, M, k, mode,
-	                                                 need_for_tau, tau, out_labels, out_dists, out_counts, cert_ok);
+	                                                 need_for_tau, tau, out_labels, out_dists, out_counts, cert_ok,
+	                                                 live);
 }
 
 // ---------------------------------------------------------------------------
-// refine + finalize (mode 1) in one launch: one 16-wave workgroup per query
-// computes the exact distances of its candidates into LDS (refine_kernel's
-// value), then ranks them by (distance, label) exactly as finalize_kernel does:
-// top-k, counts, certificate against cut.  cand_dist is not written.
+// pool_refine: select + refine + finalize of a threshold pass in ONE launch,
+// refining only as far as the certificate needs.  One 512-thread workgroup
+// per query gathers the query's segments (every row with LB <= tau, from the
+// append or sample scan) into LDS as (orderedkey(LB), slot), sorts them by
+// (LB, slot), then refines them IN BOUND ORDER, 64 per round (8 per wave,
+// exact f64 distances as refine_kernel computes them), merging each round into
+// the running top-k by (distance, label):
+//   final mode: stop as soon as the next bound exceeds nextafter(d_k) (every
+//   row left, in the pool or not, then has LB > d_k: certified as finalize
+//   does, cut = min(next bound, tau)); the refined count adapts to how many
+//   bounds lie below d_k instead of a fixed top-M (the int8 bounds put ~60-250
+//   rows there at 1M-10M rows x 768);
+//   tau mode (the sample pass): refine the m_tau smallest bounds, tau = their
+//   k-th smallest exact distance (+inf when fewer, NaN when any is NaN), the
+//   value refine_tau_kernel computes.
+// A segment that overflowed, a pool past PR_CAP or a NaN bound fails the
+// certificate (cut = -inf), as select_kernel's does; the rows refined still
+// give the rerun a tau.  Returns the refined count and the pool size.
 // ---------------------------------------------------------------------------
-constexpr int RF_THREADS = 1024;
-template <int METRIC, typename T>
-__global__ __launch_bounds__(RF_THREADS) void refine_final_kernel(
-    const T *__restrict__ X, int ld, int dim, const float *__restrict__ Qf, const int64_t *__restrict__ labels,
-    const uint32_t *__restrict__ cand_slot, const int *__restrict__ cand_cnt, const float *__restrict__ cut, int M,
-    int k, int64_t *__restrict__ out_labels, float *__restrict__ out_dists, int *__restrict__ out_counts,
-    int *__restrict__ cert_ok) {
-	__shared__ float sd[MAX_CAND];
-	__shared__ int64_t sl[MAX_CAND];
-	__shared__ float s_dk;
-	const int q = blockIdx.x;
-	const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-	const int m = min(cand_cnt[q], M);
-	for (int i = w; i < m; i += RF_THREADS / 64) {
-		const uint32_t slot = cand_slot[(int64_t)q * M + i];
-		const float d = exact_distance<METRIC, T>(X + (int64_t)slot * ld, Qf + (int64_t)q * ld, dim, lane);
-		if (lane == 0) {
-			sd[i] = d;
-			sl[i] = labels[slot];
+constexpr int PR_THREADS = 512;
+constexpr int PR_WAVES = PR_THREADS / 64;
+constexpr int PR_CAP = 16384;       // pool entries held in LDS
+constexpr int PR_PER_WAVE = 8;      // candidates per wave and round
+constexpr int PR_CHUNK = PR_WAVES * PR_PER_WAVE;
+constexpr int PR_MAXK = MAX_CAND;   // k of the fast path (k + 8 <= MAX_CAND)
+
+// exact distances of NC rows to one query by one wave (each the value
+// exact_distance returns), every row's loads issued before any accumulates
+template <int METRIC, typename T, int NC>
+__device__ __forceinline__ void exact_distance_multi(const T *__restrict__ X, int ld, const uint32_t *slots,
+                                                     int nvalid, const float *__restrict__ q, int dim, int lane,
+                                                     float *out) {
+	double a[NC], b[NC], c[NC];
+#pragma unroll
+	for (int r = 0; r < NC; ++r) a[r] = b[r] = c[r] = 0.0;
+	const int d4 = dim >> 2;
+	for (int i4 = lane; i4 < d4; i4 += 64) {
+		const float4 qv = *reinterpret_cast<const float4 *>(q + 4 * i4);
+		float4 xv[NC];
+#pragma unroll
+		for (int r = 0; r < NC; ++r)
+			xv[r] = r < nvalid ? xval4(X + (int64_t)slots[r] * ld, 4 * i4) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+		for (int r = 0; r < NC; ++r) {
+			exact_acc<METRIC>(xv[r].x, qv.x, a[r], b[r], c[r]);
+			exact_acc<METRIC>(xv[r].y, qv.y, a[r], b[r], c[r]);
+			exact_acc<METRIC>(xv[r].z, qv.z, a[r], b[r], c[r]);
+			exact_acc<METRIC>(xv[r].w, qv.w, a[r], b[r], c[r]);
 		}
 	}
-	if (t == 0) s_dk = F_INF;
-	__syncthreads();
-	const int nout = m < k ? m : k;
-	for (int i = t; i < m; i += RF_THREADS) {
-		int rank = 0;
-		const float d = sd[i];
-		const int64_t l = sl[i];
-		for (int j = 0; j < m; ++j) rank += hit_less(sd[j], sl[j], d, l) ? 1 : 0;
-		if (rank < k) {
-			out_labels[(int64_t)q * k + rank] = l;
-			out_dists[(int64_t)q * k + rank] = d;
-		}
-		if (rank == k - 1) s_dk = d;
-	}
-	for (int i = nout + t; i < k; i += RF_THREADS) {
-		out_labels[(int64_t)q * k + i] = -1;
-		out_dists[(int64_t)q * k + i] = __builtin_nanf("");
-	}
-	__syncthreads();
-	if (t == 0) {
-		out_counts[q] = nout;
-		const float c = cut[q];
-		bool ok;
-		if (c == F_INF) {
-			ok = true;  // nothing live was left out
+	for (int i = 4 * d4 + lane; i < dim; i += 64)
+#pragma unroll
+		for (int r = 0; r < NC; ++r)
+			if (r < nvalid) exact_acc<METRIC>(xval(X + (int64_t)slots[r] * ld, i), q[i], a[r], b[r], c[r]);
+#pragma unroll
+	for (int r = 0; r < NC; ++r) {
+		const double sa = wave_sum_f64(a[r]);
+		double res;
+		if (METRIC == METRIC_L2) {
+			res = sa;
+		} else if (METRIC == METRIC_DOT) {
+			res = 1.0 - sa;
 		} else {
-			const float dk = s_dk;  // +inf when fewer than k candidates
-			ok = !__builtin_isnan(dk) && dk < F_INF && c > nextafterf(dk, F_INF);
+			const double sb = wave_sum_f64(b[r]), sc = wave_sum_f64(c[r]);
+			res = 1.0 - sa / (sqrt(sb) * sqrt(sc));
 		}
-		cert_ok[q] = ok ? 1 : 0;
+		float f = (float)res + 0.0f;  // canonical +0
+		if (__builtin_isnan(f)) f = __builtin_nanf("");
+		out[r] = f;
+	}
+}
+
+template <int METRIC, typename T>
+__global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
+    const uint2 *__restrict__ seg_pool, const int *__restrict__ seg_cnt, int seg_cap, int n_seg, int nq,
+    const float *__restrict__ tau, const T *__restrict__ X, int ld, int dim, const float *__restrict__ Qf,
+    const int64_t *__restrict__ labels, int k, int mode, int m_tau, int64_t live, float *__restrict__ tau_out,
+    int64_t *__restrict__ outL, float *__restrict__ outD, int *__restrict__ outC, int *__restrict__ cert,
+    int *__restrict__ refined, int *__restrict__ pool_total) {
+	__shared__ uint64_t keys[PR_CAP];
+	__shared__ float cd[2][PR_MAXK + PR_CHUNK];  // running top-k (double-buffered) + the round's distances
+	__shared__ int64_t cl[2][PR_MAXK + PR_CHUNK];
+	__shared__ unsigned sh[PR_WAVES];
+	__shared__ int s_over, s_nfin, s_nnan, s_dnan;
+	const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+	if (t == 0) {
+		s_over = 0;
+		s_nfin = 0;
+		s_nnan = 0;
+		s_dnan = 0;
+	}
+	__syncthreads();
+	// ---- gather the pool (thread s < n_seg: segment s) ----------------------
+	unsigned c = 0;
+	if (t < n_seg) {
+		const int cs = seg_cnt[(int64_t)t * nq + q];
+		if (cs > seg_cap) s_over = 1;
+		c = (unsigned)min(cs, seg_cap);
+	}
+	unsigned total;
+	static_assert(PR_THREADS == SEL_THREADS, "block_excl_scan's geometry");
+	const unsigned off = block_excl_scan(c, sh, total);
+	const int n = (int)min(total, (unsigned)PR_CAP);
+	if (t < n_seg && c) {
+		const uint2 *seg = seg_pool + ((int64_t)t * nq + q) * seg_cap;
+		for (unsigned i = 0; i < c && off + i < (unsigned)PR_CAP; ++i) {
+			const uint2 e = seg[i];
+			keys[off + i] = ((uint64_t)e.x << 32) | e.y;
+		}
+	}
+	int P = 64;
+	while (P < n) P <<= 1;
+	for (int i = n + t; i < P; i += PR_THREADS) keys[i] = ~0ull;
+	__syncthreads();
+	if (t == 0 && total > (unsigned)PR_CAP) s_over = 1;
+	// ---- sort by (LB, slot) --------------------------------------------------
+	for (int size = 2; size <= P; size <<= 1) {
+		for (int stride = size >> 1; stride > 0; stride >>= 1) {
+			for (int i = t; i < (P >> 1); i += PR_THREADS) {
+				const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
+				const bool asc = (lo & size) == 0;
+				const uint64_t a = keys[lo], b = keys[hi];
+				if ((a > b) == asc) {
+					keys[lo] = b;
+					keys[hi] = a;
+				}
+			}
+			__syncthreads();
+		}
+	}
+	// finite bounds first, then +inf, then NaN (KEY_INF < KEY_NAN), then padding
+	{
+		unsigned nf = 0, nn = 0;
+		for (int i = t; i < n; i += PR_THREADS) {
+			const uint32_t kk = (uint32_t)(keys[i] >> 32);
+			nf += kk < KEY_INF ? 1u : 0u;
+			nn += kk == KEY_NAN ? 1u : 0u;
+		}
+#pragma unroll
+		for (int o = 32; o > 0; o >>= 1) {
+			nf += __shfl_xor(nf, o, 64);
+			nn += __shfl_xor(nn, o, 64);
+		}
+		if (lane == 0) {
+			atomicAdd(&s_nfin, (int)nf);
+			atomicAdd(&s_nnan, (int)nn);
+		}
+	}
+	__syncthreads();
+	const int nfin = s_nfin;
+	const float ftau = tau ? tau[q] : F_INF;
+	const float *qrow = Qf + (int64_t)q * ld;
+	// ---- refine in bound order ------------------------------------------------
+	const int limit = mode == 0 ? min(nfin, m_tau) : nfin;
+	int cnt = 0, cur = 0, pos = 0;  // top entries held, buffer holding them, candidates refined
+	float dk = F_INF;               // k-th distance of the top (+inf while fewer than k)
+	while (pos < limit) {
+		if (mode == 1 && cnt >= k) {
+			const float lbn = fkey_inv((uint32_t)(keys[pos] >> 32));
+			if (lbn > nextafterf(dk, F_INF)) break;  // NaN dk: never (uncertified below)
+		}
+		const int nr = min(PR_CHUNK, limit - pos);
+		// wave w refines candidates pos + w*8 .. (all its loads in flight together)
+		{
+			uint32_t sl[PR_PER_WAVE];
+			const int b0 = w * PR_PER_WAVE, nv = max(0, min(PR_PER_WAVE, nr - b0));
+#pragma unroll
+			for (int r = 0; r < PR_PER_WAVE; ++r) sl[r] = r < nv ? (uint32_t)keys[pos + b0 + r] : 0u;
+			float d[PR_PER_WAVE];
+			if (nv > 0) exact_distance_multi<METRIC, T, PR_PER_WAVE>(X, ld, sl, nv, qrow, dim, lane, d);
+			if (lane < nv) {
+				float dv = d[0];
+				uint32_t sv = sl[0];
+#pragma unroll
+				for (int r = 1; r < PR_PER_WAVE; ++r)
+					if (lane == r) dv = d[r], sv = sl[r];
+				cd[cur][cnt + b0 + lane] = dv;
+				cl[cur][cnt + b0 + lane] = labels[sv];
+				if (__builtin_isnan(dv)) s_dnan = 1;
+			}
+		}
+		__syncthreads();
+		// merge: rank of every entry (top so far + this round) by (distance, label)
+		const int m = cnt + nr;
+		for (int i = t; i < m; i += PR_THREADS) {
+			const float di = cd[cur][i];
+			const int64_t li = cl[cur][i];
+			int rank = 0;
+			for (int j = 0; j < m; ++j) rank += hit_less(cd[cur][j], cl[cur][j], di, li) ? 1 : 0;
+			if (rank < k) {
+				cd[cur ^ 1][rank] = di;
+				cl[cur ^ 1][rank] = li;
+			}
+		}
+		__syncthreads();
+		cur ^= 1;
+		cnt = min(m, k);
+		dk = cnt >= k ? cd[cur][k - 1] : F_INF;
+		pos += nr;
+	}
+	if (mode == 0) {
+		if (t == 0) {
+			tau_out[q] = s_dnan ? __builtin_nanf("") : (cnt >= k ? cd[cur][k - 1] : F_INF);
+			if (refined) refined[q] = pos;
+			if (pool_total) pool_total[q] = s_over ? -1 : (int)total;
+		}
+		return;
+	}
+	// ---- outputs and the certificate -----------------------------------------
+	for (int i = t; i < k; i += PR_THREADS) {
+		outL[(int64_t)q * k + i] = i < cnt ? cl[cur][i] : -1;
+		outD[(int64_t)q * k + i] = i < cnt ? cd[cur][i] : __builtin_nanf("");
+	}
+	if (t == 0) {
+		// every row not refined has LB >= cut: the pool's next bound, tau for the rest
+		float cutv = pos < n ? fkey_inv((uint32_t)(keys[pos] >> 32)) : F_INF;
+		if (pos >= n && s_nnan == 0 && total <= (unsigned)PR_CAP) cutv = F_INF;
+		if (ftau < cutv) cutv = ftau;
+		if (s_over || s_nnan > 0) cutv = -F_INF;
+		bool ok;
+		if (cutv == F_INF)
+			ok = true;  // nothing live was left out
+		else
+			ok = !__builtin_isnan(dk) && dk < F_INF && cutv > nextafterf(dk, F_INF);
+		if (live >= 0 && (int64_t)cnt < (live < (int64_t)k ? live : (int64_t)k)) ok = false;
+		outC[q] = cnt;
+		cert[q] = ok ? 1 : 0;
+		if (refined) refined[q] = pos;
+		if (pool_total) pool_total[q] = s_over ? -1 : (int)total;
 	}
 }
 
 template <typename T>
-static void refine_final_dispatch(const StoreView &s, const QueryView &q, const uint32_t *cand_slot,
-                                  const int *cand_cnt, const float *cut, int M, int k, int64_t *L, float *D, int *C,
-                                  int *cert, hipStream_t st) {
+static void pool_refine_dispatch(const StoreView &s, const QueryView &q, const uint2 *seg_pool, const int *seg_cnt,
+                                 int seg_cap, int n_seg, const float *tau, int k, int mode, int m_tau,
+                                 int64_t live, float *tau_out, int64_t *L, float *D, int *C, int *cert, int *refined,
+                                 int *pool_total, hipStream_t st) {
 	const T *X = static_cast<const T *>(s.X);
 	const dim3 grid((unsigned)q.nq);
-#define LHIP_RF(MET) \
-	refine_final_kernel<MET, T><<<grid, RF_THREADS, 0, st>>>(X, s.ld, s.dim, q.Qf, s.labels, cand_slot, cand_cnt, cut, M, \
-	                                                        k, L, D, C, cert)
+#define LHIP_PR(MET)                                                                                                  \
+	pool_refine_kernel<MET, T><<<grid, PR_THREADS, 0, st>>>(seg_pool, seg_cnt, seg_cap, n_seg, q.nq, tau, X, s.ld,   \
+	                                                        s.dim, q.Qf, s.labels, k, mode, m_tau, live, tau_out, L, \
+	                                                        D, C, cert, refined, pool_total)
 	switch (s.metric) {
-	case METRIC_L2: LHIP_RF(METRIC_L2); break;
-	case METRIC_DOT: LHIP_RF(METRIC_DOT); break;
-	default: LHIP_RF(METRIC_COSINE); break;
+	case METRIC_L2: LHIP_PR(METRIC_L2); break;
+	case METRIC_DOT: LHIP_PR(METRIC_DOT); break;
+	default: LHIP_PR(METRIC_COSINE); break;
 	}
-#undef LHIP_RF
+#undef LHIP_PR
 }
 
-void launch_refine_final(const StoreView &s, const QueryView &q, const uint32_t *cand_slot, const int *cand_cnt,
-                         const float *cut, int M, int k, int64_t *L, float *D, int *C, int *cert, hipStream_t st) {
-	if (M > MAX_CAND) throw std::runtime_error("refine_final: M past MAX_CAND");
+void launch_pool_refine(const StoreView &s, const QueryView &q, const uint2 *seg_pool, const int *seg_cnt,
+                        int seg_cap, int n_seg, const float *tau, int k, int mode, int m_tau, int64_t live,
+                        float *tau_out, int64_t *L, float *D, int *C, int *cert, int *refined, int *pool_total,
+                        hipStream_t st) {
+	if (q.nq <= 0) return;
+	if (n_seg > PR_THREADS) throw std::runtime_error("pool_refine: more segments than threads");
+	if (k <= 0 || k > PR_MAXK) throw std::runtime_error("pool_refine: k past the selection capacity");
+	if (mode == 0 && m_tau > PR_MAXK) throw std::runtime_error("pool_refine: m_tau past the selection capacity");
 	if (s.xbf16)
-		refine_final_dispatch<uint16_t>(s, q, cand_slot, cand_cnt, cut, M, k, L, D, C, cert, st);
+		pool_refine_dispatch<uint16_t>(s, q, seg_pool, seg_cnt, seg_cap, n_seg, tau, k, mode, m_tau, live, tau_out, L,
+		                               D, C, cert, refined, pool_total, st);
 	else
-		refine_final_dispatch<float>(s, q, cand_slot, cand_cnt, cut, M, k, L, D, C, cert, st);
+		pool_refine_dispatch<float>(s, q, seg_pool, seg_cnt, seg_cap, n_seg, tau, k, mode, m_tau, live, tau_out, L, D,
+		                            C, cert, refined, pool_total, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -2576,7 +2876,10 @@ __global__ __launch_bounds__(256) void retry_gather_kernel(const int *__restrict
 	if (src < 0) return;
 	const float t0 = tau[src];
 	const float dk = dists[(int64_t)src * k + k - 1];  // NaN when fewer than k were found
-	tau2[i] = (!keep_tau && dk < t0) ? dk : t0;
+	// two steps above d_k: a rerun's cut (<= tau2) can then still exceed
+	// nextafter(d_k), which the certificate needs
+	const float dk2 = nextafterf(nextafterf(dk, F_INF), F_INF);
+	tau2[i] = (!keep_tau && dk2 < t0) ? dk2 : t0;
 	status2[i] = status2[nf + i] = status2[2 * nf + i] = 0;
 }
 

@@ -61,6 +61,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		sv.Xscan = Xq;
 		sv.scan_aux = rowaux8;
 		sv.scan_i8 = 1;
+		sv.tstat = tstat8;
 	}
 	if (small_exact && small_exact_fits(n_slots, dim, nq, k)) {
 		// a few queries over a small store (one query per lance_search call):
@@ -94,9 +95,11 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	ws.status.need((size_t)3 * nq);
 	ws.need_host_status((size_t)3 * nq);
 	int *d_cert = ws.status.p, *d_cand_cnt = ws.status.p + nq, *d_pool_cnt = ws.status.p + 2 * nq;
-	if (use8)
-		launch_prep_queries_i8(dQ, nq, dim, ld, nq_pad, eff_metric, max_alpha8, max_x8, ws.Qf.p, ws.Qb.p, ws.qaux.p,
-		                       ws.status.p, stream);
+	if (use8) {
+		ws.qm.need(nq);
+		launch_prep_queries_i8(dQ, nq, dim, ld, nq_pad, eff_metric, max_alpha8, max_x8, ws.qm.p, ws.Qf.p, ws.Qb.p,
+		                       ws.qaux.p, ws.status.p, stream);
+	}
 	else
 		launch_prep_queries(dQ, nq, dim, ld, nq_pad, eff_metric, ma, mu, ws.Qf.p, ws.Qb.p, ws.qaux.p, ws.status.p,
 		                    stream);
@@ -122,7 +125,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		launch_select_dense(ws.dense.p, cols, cols, 1, nq, Mfinal, ws.cand_slot.p, d_cand_cnt, ws.cut.p, stream);
 		launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Mfinal, ws.cand_dist.p, stream);
 		launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Mfinal, k, 1, 0, nullptr, dL,
-		                dD, dC, d_cert, stream);
+		                dD, dC, d_cert, stream, live_rows());
 		if (time_kernels) {
 			kt_dense_ms += toc_ms(0, 1);
 			kt_dense_n += 1;
@@ -142,33 +145,21 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		ws.seg_pool.need((size_t)n_seg_s * nq * cap_s + (size_t)n_seg_s * (nq_pad / SCAN_BQ));
 		ws.seg_cnt.need((size_t)n_seg_s * nq);
 		launch_scan_tilemin(sv, qv, n_sample, stride, ws.seg_pool.p, ws.seg_cnt.p, cap_s, stream);
-		ws.selbig.need((size_t)nq);
-		launch_select_segments(ws.seg_pool.p, ws.seg_cnt.p, cap_s, n_seg_s, nullptr, nq, Ms, ws.cand_slot.p,
-		                       d_cand_cnt, ws.cut.p, nullptr, ws.selbig.p, stream);
-		launch_refine_tau(sv, qv, ws.cand_slot.p, d_cand_cnt, Ms, k, ws.tau.p, stream);
+		launch_pool_refine(sv, qv, ws.seg_pool.p, ws.seg_cnt.p, cap_s, n_seg_s, nullptr, k, 0, Ms, -1, ws.tau.p,
+		                   nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
 		// 2) threshold scan over every row into per-(workgroup, query) segments;
 		//    a segment holds ~4x its expected share of the (k+8)*N/sample pool
-		const int n_seg = scan_grid(n_tiles);
+		const int n_seg = scan_append_segments(sv, n_tiles);
 		const int64_t expect = (int64_t)(k + 4) * ((n_tiles + n_sample - 1) / n_sample);
 		const int seg_cap = (int)std::min<int64_t>(1024, round_up(std::max<int64_t>(64, 4 * expect / n_seg), 32));
 		ws.seg_pool.need((size_t)n_seg * nq * seg_cap + (size_t)n_seg * (nq_pad / SCAN_BQ));  // + per-workgroup sink
 		ws.seg_cnt.need((size_t)n_seg * nq);
 		tic(2);
-		if (rscan && rscan_fits(sv))
-			launch_rscan_append(sv, qv, ws.tau.p, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, stream);
-		else
-			launch_scan_append(sv, qv, ws.tau.p, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, stream);
+		launch_scan_append(sv, qv, ws.tau.p, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, stream);
 		tic(3);
-		// 3) top-M by LB, exact refine, certificate
-		launch_select_segments(ws.seg_pool.p, ws.seg_cnt.p, seg_cap, n_seg, ws.tau.p, nq, Mfinal, ws.cand_slot.p,
-		                       d_cand_cnt, ws.cut.p, d_pool_cnt, ws.selbig.p, stream);
-		if (fused_refine)
-			launch_refine_final(sv, qv, ws.cand_slot.p, d_cand_cnt, ws.cut.p, Mfinal, k, dL, dD, dC, d_cert, stream);
-		else {
-			launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Mfinal, ws.cand_dist.p, stream);
-			launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Mfinal, k, 1, 0, nullptr, dL,
-			                dD, dC, d_cert, stream);
-		}
+		// 3) the pool in bound order, exact refine until certified
+		launch_pool_refine(sv, qv, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, n_seg, ws.tau.p, k, 1, 0, live_rows(),
+		                   nullptr, dL, dD, dC, d_cert, d_cand_cnt, d_pool_cnt, stream);
 	}
 	HIPCHK(hipGetLastError());
 
@@ -180,7 +171,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		kt_append_n += 1;
 		kt_append_rows = n_slots;
 		kt_append_qpad = nq_pad;
-		kt_append_kernel = (rscan && rscan_fits(sv)) ? 1 : 0;
+		kt_append_kernel = scan8_fits(sv) ? 2 : 0;
 	}
 	const int *h_cert = ws.h_status;
 	for (int q = 0; q < nq; ++q) {
@@ -214,32 +205,20 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 			ws.rD.need((size_t)nf * k);
 			ws.rC.need(nf);
 			HIPCHK(hipMemcpyAsync(ws.rfq.p, fq.data(), (size_t)nf * sizeof(int), hipMemcpyHostToDevice, stream));
-			// int8 scan, first rerun: the first pass usually found the true top-k
-			// but more rows than Mfinal lay below its k-th distance; a tau
-			// tightened to that distance could never certify (cut = d_k), so
-			// the rerun keeps tau and only widens the selection (Mr)
+			// tau tightened to just above the first pass's k-th distance (a pool
+			// that overflowed shrinks; pool_refine refines as far as it needs)
 			launch_retry_gather(ws.rfq.p, nf, nf_pad, ld, k, qv, ws.tau.p, dD, ws.rQf.p, ws.rQb.p, ws.rqaux.p,
-			                    ws.rtau.p, ws.rstat.p, stream, use8 && attempt == 0);
+			                    ws.rtau.p, ws.rstat.p, stream);
 			const QueryView qv2{ws.rQf.p, ws.rQb.p, ws.rqaux.p, nf, nf_pad};
-			const int n_seg = scan_grid(n_tiles);
-			// int8 scan: the rerun selects to the full capacity (a failed first
-			// certificate usually means more rows lay below the k-th distance
-			// than Mfinal)
-			const int Mr = use8 ? MAX_CAND : Mfinal;
+			const int n_seg = scan_append_segments(sv, n_tiles);
 			int cap2 = 1024;  // the scan's maximum, bounded to a 1 GiB pool
 			while (cap2 > 64 && (size_t)n_seg * nf * cap2 * sizeof(uint2) > ((size_t)1 << 30)) cap2 /= 2;
 			ws.seg_pool.need((size_t)n_seg * nf * cap2 + (size_t)n_seg * (nf_pad / SCAN_BQ));
 			ws.seg_cnt.need((size_t)n_seg * nf);
 			int *cert2 = ws.rstat.p, *cnt2 = ws.rstat.p + nf, *pool2 = ws.rstat.p + 2 * nf;
-			if (rscan && rscan_fits(sv))
-				launch_rscan_append(sv, qv2, ws.rtau.p, ws.seg_pool.p, ws.seg_cnt.p, cap2, stream);
-			else
-				launch_scan_append(sv, qv2, ws.rtau.p, ws.seg_pool.p, ws.seg_cnt.p, cap2, stream);
-			launch_select_segments(ws.seg_pool.p, ws.seg_cnt.p, cap2, n_seg, ws.rtau.p, nf, Mr, ws.cand_slot.p,
-			                       cnt2, ws.cut.p, pool2, ws.selbig.p, stream);
-			launch_refine(sv, qv2, ws.cand_slot.p, cnt2, Mr, ws.cand_dist.p, stream);
-			launch_finalize(sv, ws.cand_slot.p, cnt2, ws.cand_dist.p, ws.cut.p, nf, Mr, k, 1, 0, nullptr, ws.rL.p,
-			                ws.rD.p, ws.rC.p, cert2, stream);
+			launch_scan_append(sv, qv2, ws.rtau.p, ws.seg_pool.p, ws.seg_cnt.p, cap2, stream);
+			launch_pool_refine(sv, qv2, ws.seg_pool.p, ws.seg_cnt.p, cap2, n_seg, ws.rtau.p, k, 1, 0, live_rows(),
+			                   nullptr, ws.rL.p, ws.rD.p, ws.rC.p, cert2, cnt2, pool2, stream);
 			launch_retry_scatter(ws.rfq.p, nf, k, ws.rL.p, ws.rD.p, ws.rC.p, cert2, ws.rtau.p, dL, dD, dC, d_cert, ws.tau.p,
 			                     stream);
 			HIPCHK(hipGetLastError());
@@ -1058,15 +1037,16 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			if (!ix->scan_i8) ix->drop_i8();
 			return 0;
 		}
-		if (k == "fused_refine") {
-			ix->fused_refine = (v == "1" || v == "on" || v == "true");
-			return 0;
-		}
+
 		if (k == "prepare") {
 			// build the derived scan structures now (the int8 scan copy) instead
 			// of on the first search after a change
 			ix->bind();
 			if (ix->i8_usable()) ix->ensure_i8();
+			return 0;
+		}
+		if (k == "scan8_variant") {  // development knob (all ld = 768 scans of the process)
+			lhip::scan8_set_variant(std::stoi(v));
 			return 0;
 		}
 		if (k == "cand_extra_i8") {
@@ -1085,10 +1065,7 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			ix->small_exact = (v == "1" || v == "on" || v == "true");
 			return 0;
 		}
-		if (k == "rscan") {
-			ix->rscan = (v == "1" || v == "on" || v == "true");
-			return 0;
-		}
+
 		if (k == "retry_pass") {
 			ix->retry_pass = (v == "1" || v == "on" || v == "true");
 			return 0;
@@ -1161,7 +1138,7 @@ int32_t lance_hip_last_search_stats(void *handle, int64_t *out, int32_t n) {
 // out[7] = total ms of IVF list-scan launches, out[8] = their count,
 // out[9] = their algorithmic bytes (summed), out[10] = (query, row) pairs
 // they scored (summed), out[11] = total ms of the IVF coarse searches,
-// out[12] = 1 if the last timed append pass ran rscan_kernel (0: scan_kernel).
+// out[12] = which kernel ran the last timed append pass: 0 scan_kernel, 2 scan8_kernel.
 int32_t lance_hip_kernel_times(void *handle, double *out, int32_t n) {
 	if (!handle || !out) return -1;
 	Index *ix = as_index(handle);

@@ -1,0 +1,382 @@
+// gfx950 (MI355X / CDNA4): the int8 append pass of the flat scan ("scan8").
+//
+// Replaces, for the int8 scan copy, the threshold pass of knn_kernels.hip's
+// scan_kernel (MODE 1): every row's rigorous lower bound LB(row, query) is
+// screened against tau[query] and the rows with LB <= tau go to the query's
+// segment as (orderedkey(LB), slot).  The search it serves is the reference's
+// flat KNN (rust_lib/src/lance_manager.rs:393-451 -> lance 0.22 flat scan);
+// DESIGN.md §3 "scan8" has the derivation.
+//
+// Layout (one workgroup per CU, two per pair of CUs):
+//   * a PAIR of workgroups walks the same row tiles (pair p: tiles p, p + NP, ...),
+//     each with one half of a 256-query tile: its 128 int8 queries stay RESIDENT
+//     in LDS for the whole launch (128 x ld bytes; ld = 768: 96 KiB), so nothing
+//     but rows streams.  The partner's copy of a row comes from L2 / the
+//     Infinity Cache (workgroups b and b + 8 share an XCD under round-robin
+//     placement: speed only, never correctness).
+//   * 8 waves, two per SIMD, no barrier after the prologue: wave w owns rows
+//     32w .. 32w + 31 of every tile of its pair and all 128 queries,
+//     2 x 8 v_mfma_i32_16x16x64_i8 accumulators (64 VGPRs).  Its rows stream
+//     HBM -> VGPRs (global_load_dwordx4, 16 rows x 64 B per instruction) through
+//     a D-deep register ring of 64-deep k-steps; query fragments come from LDS
+//     (XOR-swizzled 16 B chunks: conflict-free ds_read_b128).
+//   * the bound is screened in EXACT INTEGERS.  With one scale s_T per row tile
+//     and one s_Q per query batch (tiles_to_i8_kernel, prep_queries_i8_kernel),
+//       LB = alpha + C + xn B + ux A + s s_T S      (s = x^.q^ exact, S < 0)
+//     and LB <= tau  <=>  s >= (alpha + C + xn B + ux A - tau) W,  W = 1/(-S s_T);
+//     with xn, ux replaced by the tile's maxima (B, A <= 0: the threshold only
+//     drops) it splits into a row part Bi <= alpha W and a query part
+//     Gi <= (C + max xn B + max ux A - tau) W, both rounded DOWN to integers.
+//     The accumulators start at -Bi (the first MFMA's C operand) and a bound
+//     passes iff acc >= Gi: per lane and query block one v_max3 chain and one
+//     compare.  Every (row, query) with LB <= tau passes (a superset; the
+//     passes that exceed tau only cost a segment entry).
+//   * a passing bound is kept in the wave's LDS list as (s, slot, query); the
+//     list becomes (orderedkey(LB), slot) segment entries at the end (or when it
+//     fills): LB is evaluated there exactly as scan_kernel's lower_bound does,
+//     from the row terms in global memory.
+// ---------------------------------------------------------------------------
+#include "knn_kernels.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "device_common.h"
+
+namespace lhip {
+
+namespace {
+constexpr int QH = 128;               // queries per workgroup (half a SCAN_BQ tile)
+constexpr int LDS8 = 160 * 1024;      // one workgroup per CU
+constexpr int BIG = 1 << 30;          // row part of a dead row / query part that passes nothing
+constexpr int LIVE_MAX = 1 << 29;     // largest row part of a live row
+constexpr int GLO = -(1 << 29) - (1 << 25);  // query part that passes every live row
+static_assert(BIG - (1 << 24) > -GLO, "a dead row (acc <= 2^24 - BIG) never reaches GLO");
+static_assert(-(1 << 24) - LIVE_MAX > GLO, "a live row (acc >= -2^24 - LIVE_MAX) always reaches GLO");
+}  // namespace
+
+
+
+// row part: an integer Bi <= alpha * W (exact), in [0, LIVE_MAX]; BIG for a dead
+// row (+inf) or a NaN bound (never passes, as in scan_kernel)
+__device__ __forceinline__ int s8_row_part(float alpha, float W) {
+	if (!(alpha < F_INF)) return BIG;
+	float b = alpha * W;                          // alpha >= 0, W >= 0 (NaN: 0 * inf -> 0 below)
+	b = fmaf(-fabsf(b), 0x1p-20f, b) - 1.0f;      // below alpha W despite the two roundings
+	b = fminf(fmaxf(b, 0.0f), (float)LIVE_MAX);   // (fmaxf drops a NaN)
+	return (int)b;
+}
+
+// query part: an integer Gi <= (C - tau + xnmax B + uxmax A) W (exact), in
+// [GLO, BIG]; BIG (nothing passes) for a NaN query term or tau (a zero cosine
+// query, a NaN distance in the sample: exact fallback) and for padding queries
+// (tau = -inf); GLO (every live row passes) when it overflows or tau = +inf
+__device__ __forceinline__ int s8_query_part(float4 qa, float tq, float4 ts, float W) {
+	const float cmt = qa.w - tq;
+	if (!(cmt < F_INF)) return BIG;
+	float g = fmaf(ts.y, qa.z, fmaf(ts.z, qa.y, cmt)) * W;
+	// f32 evaluation error of the four terms (a few units of 2^-24 of their magnitudes)
+	const float E = (fabsf(qa.w) + fabsf(tq) + ts.y * fabsf(qa.z) + ts.z * fabsf(qa.y)) * W * 0x1p-20f + 1.0f;
+	g = g - E;
+	if (!(fabsf(g) < F_INF)) return GLO;
+	return (int)floorf(fminf(fmaxf(g, (float)GLO), (float)BIG));
+}
+
+template <int KS, int D, int RB>
+__global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *__restrict__ Xq, const float4 *__restrict__ aux8,
+                                                      const float4 *__restrict__ tstat, int ld,
+                                                      const int8_t *__restrict__ Qi, const float4 *__restrict__ qaux,
+                                                      int nq, int n_tiles, const float *__restrict__ tau,
+                                                      uint2 *__restrict__ seg_pool, int *__restrict__ seg_cnt,
+                                                      int seg_cap, int list_cap) {
+	static_assert(KS % D == 0 && KS % 2 == 0, "ring slot and fragment buffer of a k-step must be static");
+	constexpr int NW = 16 / RB, T8 = 64 * NW;  // waves: each owns 16 RB rows of every tile
+	constexpr int WR = 16 * RB;                // rows per wave and tile
+	constexpr int P = (KS * 64 + 255) / 256 * 256;  // LDS bytes per query row (XOR groups of 16 chunks)
+	__shared__ __attribute__((aligned(16))) uint8_t smem[LDS8];
+	uint8_t *QL = smem;
+	float4 *QA = reinterpret_cast<float4 *>(smem + QH * P);
+	float *TAU = reinterpret_cast<float *>(QA + QH);
+	unsigned *CNT = reinterpret_cast<unsigned *>(TAU + QH);
+	uint2 *LIST = reinterpret_cast<uint2 *>(CNT + QH);                 // [NW][list_cap] (s, slot)
+	uint8_t *LISTQ = reinterpret_cast<uint8_t *>(LIST + NW * list_cap);  // [NW][list_cap] local query
+
+	// Row group and query half of this workgroup.  A query tile with more than
+	// QH queries: pairs (workgroups b, b + 8 share an XCD under round-robin
+	// placement), each pair one row group, each workgroup one half; otherwise
+	// (a small batch, a rerun) every workgroup its own row group, all queries.
+	const int nb = (int)gridDim.x, b_id = (int)blockIdx.x;
+	const int q_tile = (int)blockIdx.y * SCAN_BQ;
+	const bool halves = nq - q_tile > QH;
+	int h = 0, pr = b_id, NP = nb;
+	if (halves) {
+		NP = nb >> 1;
+		if ((nb & 15) == 0) {
+			h = (b_id >> 3) & 1;
+			pr = (b_id & 7) | ((b_id >> 4) << 3);
+		} else {
+			h = b_id & 1;
+			pr = b_id >> 1;
+		}
+	}
+	const int qb = q_tile + h * QH;  // first query of this workgroup
+	const int tid = threadIdx.x, lane = tid & 63;
+	const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+	const int lr = lane & 15, lg = lane >> 4;
+
+	// ---- prologue: the 128 queries into LDS (chunk c of query n at c ^ (n & 15)) --
+	{
+		constexpr int NCH = KS * 4;  // 16 B chunks per query row
+		for (int i = tid; i < QH * NCH; i += T8) {
+			const int n = i / NCH, c = i - n * NCH;
+			const i32x4 v = *reinterpret_cast<const i32x4 *>(Qi + (int64_t)(qb + n) * 2 * ld + 16 * c);
+			*reinterpret_cast<i32x4 *>(QL + n * P + ((c ^ (n & 15)) << 4)) = v;
+		}
+	}
+	if (tid < QH) {
+		const int q = qb + tid;
+		QA[tid] = qaux[q];
+		TAU[tid] = q < nq ? tau[q] : -F_INF;
+		CNT[tid] = 0u;
+	}
+	__syncthreads();
+	// -S: the same for every query with a usable bound (0 for padding / zero cosine queries)
+	float Sabs = fmaxf(-QA[lane].x, -QA[lane + 64].x);
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) Sabs = fmaxf(Sabs, __shfl_xor(Sabs, o, 64));
+
+	const int my_tiles = pr < n_tiles ? (n_tiles - 1 - pr) / NP + 1 : 0;
+	int n_list = 0;
+	uint2 *wl = LIST + w * list_cap;
+	uint8_t *wq = LISTQ + w * list_cap;
+	// list -> segment entries: LB as scan_kernel's lower_bound<., SC> evaluates it
+	auto flush = [&]() {
+		const float *ra = reinterpret_cast<const float *>(aux8);
+		for (int e = lane; e < n_list; e += 64) {
+			const uint2 en = wl[e];
+			const int ql = wq[e];
+			const int64_t r = (int64_t)en.y;
+			const float al = ra[raix(r, 0)], xn = ra[raix(r, 1)], ux = ra[raix(r, 2)], sc = ra[raix(r, 3)];
+			const float4 qa = QA[ql];
+			float v = fmaf(xn, qa.z, al);
+			v = fmaf(ux, qa.y, v);
+			v = fmaf((float)(int)en.x * sc, qa.x, v);
+			v = v + qa.w;
+			const unsigned p = atomicAdd(&CNT[ql], 1u);
+			if (p < (unsigned)seg_cap) seg_pool[((int64_t)b_id * nq + qb + ql) * seg_cap + p] = make_uint2(fkey(v), en.y);
+		}
+		n_list = 0;
+	};
+
+	if (my_tiles > 0) {
+		// this lane's A rows: WR w + 16 rb + lr of each tile, k bytes 64 j + 16 lg.
+		// Address = uniform tile base (SGPRs) + per-lane offset + immediate: no
+		// VALU in the k-loop (a VALU write right after an MFMA may land on one of
+		// its A / B registers while it still reads them: device_common.h)
+		uint32_t xo[RB];
+#pragma unroll
+		for (int rb = 0; rb < RB; ++rb) xo[rb] = (uint32_t)((WR * w + 16 * rb + lr) * ld + 16 * lg);
+		auto xtile = [&](int b) -> const int8_t * {
+			const int bb = b < my_tiles ? b : my_tiles - 1;  // past the end: the last block again (unused)
+			return Xq + (pr + (int64_t)bb * NP) * SCAN_BR * (int64_t)ld;
+		};
+		auto xload = [&](const int8_t *tb, int j, int rb) -> i32x4 {
+			return *reinterpret_cast<const i32x4 *>(tb + xo[rb] + 64 * j);
+		};
+		// row terms of block b: alpha of this lane's accumulator rows (16 rb + 4 lg + i) and the tile's terms
+		auto aload = [&](int b, float4 (&a)[RB], float4 &ts) {
+			const int bb = b < my_tiles ? b : my_tiles - 1;
+			const int64_t tile = pr + (int64_t)bb * NP;
+			const float *A = reinterpret_cast<const float *>(aux8) + (tile << 10) + WR * w + 4 * lg;
+#pragma unroll
+			for (int rb = 0; rb < RB; ++rb) a[rb] = *reinterpret_cast<const float4 *>(A + 16 * rb);
+			ts = tstat[tile];
+		};
+		// B fragment of query block u, k-step j: query 16u + lr, logical chunk 4j + lg
+		// (two base registers per j & 3 keep every offset an immediate below 64 KiB)
+		uint32_t qo[2][4];
+#pragma unroll
+		for (int m = 0; m < 4; ++m) {
+			qo[0][m] = (uint32_t)(lr * P + ((((4 * m + lg) ^ lr)) << 4));
+			qo[1][m] = qo[0][m] + 64u * P;
+			asm volatile("" : "+v"(qo[1][m]));  // a register of its own (not re-folded into an add per read)
+		}
+		auto bload = [&](int j, int u) -> i32x4 {
+			return *reinterpret_cast<const i32x4 *>(QL + qo[u >> 2][j & 3] + 16 * (u & 3) * P + 256 * (j >> 2));
+		};
+
+		float4 an[RB], tn;
+		aload(0, an, tn);
+		i32x4 xa[D][RB];
+		{
+			const int8_t *tb = xtile(0);
+#pragma unroll
+			for (int j = 0; j < D; ++j)
+#pragma unroll
+				for (int rb = 0; rb < RB; ++rb) xa[j][rb] = xload(tb, j, rb);
+		}
+		// query fragments, double-buffered: k-step j + 1's are read while k-step j multiplies
+		i32x4 bq[2][8];
+#pragma unroll
+		for (int u = 0; u < 8; ++u) bq[0][u] = bload(0, u);
+
+		for (int b = 0; b < my_tiles; ++b) {
+			float4 al[RB];
+#pragma unroll
+			for (int rb = 0; rb < RB; ++rb) al[rb] = an[rb];
+			const float4 ts = tn;
+			aload(b + 1, an, tn);
+			const float W = (Sabs > 0.f && ts.x > 0.f) ? 1.0f / (Sabs * ts.x) : 0.f;
+			i32x4 bias[RB];
+#pragma unroll
+			for (int rb = 0; rb < RB; ++rb) {
+				bias[rb][0] = -s8_row_part(al[rb].x, W);
+				bias[rb][1] = -s8_row_part(al[rb].y, W);
+				bias[rb][2] = -s8_row_part(al[rb].z, W);
+				bias[rb][3] = -s8_row_part(al[rb].w, W);
+			}
+			int gi[8];
+#pragma unroll
+			for (int u = 0; u < 8; ++u) gi[u] = s8_query_part(QA[16 * u + lr], TAU[16 * u + lr], ts, W);
+
+			i32x4 acc[RB][8];
+			const int8_t *tb_cur = xtile(b), *tb_next = xtile(b + 1);
+			__builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+			for (int j = 0; j < KS; ++j) {
+				const int sl = j % D, cur = j & 1;  // (KS even: k-step 0 of the next block reads buffer 0)
+#pragma unroll
+				for (int u = 0; u < 8; ++u) bq[cur ^ 1][u] = bload((j + 1) % KS, u);
+#pragma unroll
+				for (int u = 0; u < 8; ++u) {
+#pragma unroll
+					for (int rb = 0; rb < RB; ++rb)
+						acc[rb][u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xa[sl][rb], bq[cur][u],
+						                                                   j == 0 ? bias[rb] : acc[rb][u], 0, 0, 0);
+				}
+				// refill the slot with k-step j + D of this wave's stream
+				const int jn = j + D;
+#pragma unroll
+				for (int rb = 0; rb < RB; ++rb) xa[sl][rb] = xload(jn < KS ? tb_cur : tb_next, jn % KS, rb);
+				__builtin_amdgcn_sched_barrier(0);
+			}
+			mfma_operand_guard();  // the screen's VALU follows the block's last MFMAs
+
+			// ---- screen: lane bit u = some bound of query 16u + lr passes ----
+			int hitm = 0;
+#pragma unroll
+			for (int u = 0; u < 8; ++u) {
+				int m = max(max(acc[0][u][0], acc[0][u][1]), max(acc[0][u][2], acc[0][u][3]));
+#pragma unroll
+				for (int rb = 1; rb < RB; ++rb)
+					m = max(m, max(max(acc[rb][u][0], acc[rb][u][1]), max(acc[rb][u][2], acc[rb][u][3])));
+				hitm |= (m >= gi[u] ? 1 : 0) << u;
+			}
+			if (__builtin_amdgcn_ballot_w64(hitm != 0)) {
+				// rare: append every passing (s, slot, query) to the wave's list
+				const uint32_t row0 = (uint32_t)((pr + (int64_t)b * NP) * SCAN_BR) + (uint32_t)(WR * w) + 4u * lg;
+#pragma unroll
+				for (int u = 0; u < 8; ++u) {
+					if (!__builtin_amdgcn_ballot_w64((hitm >> u) & 1)) continue;
+#pragma unroll
+					for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+						for (int i = 0; i < 4; ++i) {
+							const bool pass = acc[rb][u][i] >= gi[u];
+							const uint64_t mk = __builtin_amdgcn_ballot_w64(pass);
+							if (!mk) continue;
+							const int c = __builtin_popcountll(mk);
+							if (n_list + c > list_cap) flush();
+							if (pass) {
+								const int pos = n_list + (int)__builtin_amdgcn_mbcnt_hi(
+								                             (uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+								wl[pos] = make_uint2((uint32_t)(acc[rb][u][i] - bias[rb][i]), row0 + 16u * rb + (uint32_t)i);
+								wq[pos] = (uint8_t)(16 * u + lr);
+							}
+							n_list += c;
+						}
+				}
+			}
+		}
+	}
+	if (n_list > 0) flush();
+	__syncthreads();  // every wave's counter updates
+	// segment b_id of every query of the tile: this workgroup's counts for its
+	// half, zero for the other half (its partner fills its own segment)
+	for (int i = tid; i < SCAN_BQ; i += T8) {
+		const int q = q_tile + i;
+		if (q >= nq) break;
+		const int ql = q - qb;
+		seg_cnt[(int64_t)b_id * nq + q] = (ql >= 0 && ql < QH) ? (int)CNT[ql] : 0;
+	}
+}
+
+// workgroups of a launch over n_tiles row tiles: one per CU, an even count
+// (pairs), at most two per tile
+static int s8_groups(int64_t n_tiles) {
+	static int cus = 0;
+	if (cus == 0) {
+		int dev = 0, v = 0;
+		cus = (hipGetDevice(&dev) == hipSuccess &&
+		       hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v >= 2)
+		          ? v
+		          : 256;
+	}
+	return (int)(2 * std::max<int64_t>(1, std::min<int64_t>(cus / 2, n_tiles)));
+}
+
+bool scan8_fits(const StoreView &s) {
+	return s.scan_i8 && s.tstat && s.ld >= 512 && s.ld <= 1024 && s.ld % 128 == 0;
+}
+
+int scan8_segments(int64_t n_tiles) { return s8_groups(n_tiles); }
+
+static int s8_list_cap(int ld, int nw) {
+	const int P = (ld + 255) / 256 * 256;
+	const int room = LDS8 - QH * P - QH * 24;
+	return std::min(1024, room / (nw * 9) / 64 * 64);
+}
+
+template <int KS, int D, int RB>
+static void s8_launch(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
+                      int seg_cap, int64_t n_tiles, hipStream_t st) {
+	const dim3 grid((unsigned)s8_groups(n_tiles), (unsigned)(q.nq_pad / SCAN_BQ));
+	constexpr int NW = 16 / RB;
+	scan8_kernel<KS, D, RB><<<grid, dim3(64 * NW), 0, st>>>(
+	    static_cast<const int8_t *>(s.Xscan), s.scan_aux, s.tstat, s.ld, reinterpret_cast<const int8_t *>(q.Qb), q.qaux,
+	    q.nq, (int)n_tiles, tau, seg_pool, seg_cnt, seg_cap, s8_list_cap(s.ld, NW));
+}
+
+// geometry of the ld = 768 kernel (development knob, option "scan8_variant"):
+// 16-row blocks per wave (4: four waves, one per SIMD; 2: eight waves) and the
+// register ring depth in 64-deep k-steps
+static int g_s8_variant = 0;
+void scan8_set_variant(int v) { g_s8_variant = v; }
+
+void launch_scan8_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
+                         int seg_cap, hipStream_t st) {
+	const int64_t n_tiles = (s.n_slots + SCAN_BR - 1) / SCAN_BR;
+	if (n_tiles <= 0) return;
+	if (!scan8_fits(s)) throw std::runtime_error("scan8: int8 scan copy with ld in [512, 1024] required");
+	if (n_tiles * (int64_t)SCAN_BR > ((int64_t)1 << 32)) throw std::runtime_error("scan8: slots past 2^32");
+	if (q.nq_pad % SCAN_BQ) throw std::runtime_error("scan8: query tile padding");
+	switch (s.ld / 64) {
+	case 8: s8_launch<8, 4, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+	case 10: s8_launch<10, 5, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+	case 12:
+		switch (g_s8_variant) {
+		case 1: s8_launch<12, 4, 4>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		case 2: s8_launch<12, 6, 4>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		case 3: s8_launch<12, 12, 4>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		case 4: s8_launch<12, 3, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		case 5: s8_launch<12, 6, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		case 6: s8_launch<12, 12, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		default: s8_launch<12, 4, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		}
+		break;
+	case 14: s8_launch<14, 7, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+	default: s8_launch<16, 4, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+	}
+}
+
+}  // namespace lhip

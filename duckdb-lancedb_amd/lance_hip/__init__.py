@@ -418,7 +418,7 @@ def LanceHipKernelTimes(handle) -> dict:
             "scan_qpad": int(out[3]), "dense_ms_total": float(out[4]), "dense_launches": int(out[5]),
             "scan_elem_bytes": int(out[6]), "ivf_scan_ms_total": float(out[7]), "ivf_scan_launches": int(out[8]),
             "ivf_scan_bytes": float(out[9]), "ivf_pair_rows": float(out[10]), "ivf_coarse_ms_total": float(out[11]),
-            "scan_kernel": "rscan_kernel" if out[12] == 1 else "scan_kernel"}
+            "scan_kernel": {2: "scan8_kernel"}.get(int(out[12]), "scan_kernel")}
 
 
 IVF_TYPES = {-1: None, 0: "ivf_flat", 1: "ivf_pq"}
