@@ -158,7 +158,10 @@ struct Index {
 	bool xbf16 = false;
 	size_t xes() const { return xbf16 ? 2 : 4; }
 	uint8_t *xrow(int64_t s) const { return static_cast<uint8_t *>(X) + (size_t)s * ld * xes(); }
-	// bf16 scan copy of an f32 store (option scan_copy, default on): the scan
+	// bf16 scan copy of an f32 store (option scan_copy, default on): built on the
+	// first search that streams bf16 rows (ensure_xs: the flat scans when the int8
+	// copy does not apply, the IVF_FLAT bound scan), never when the int8 copy
+	// serves every search (10M x 768: 15 GB not held); then the scan
 	// streams 2 B per element; refine, get_vector and compact use the f32 rows
 	uint16_t *Xs = nullptr;
 	bool scan_copy = true;
@@ -297,7 +300,7 @@ struct Index {
 		float4 *na = nullptr, *na2 = nullptr;
 		int64_t *nl = nullptr;
 		HIPCHK(hipMalloc(&nX, (size_t)c * ld * xes()));
-		if (has_scan_copy()) HIPCHK(hipMalloc(&nXs, (size_t)c * ld * 2));
+		if (Xs) HIPCHK(hipMalloc(&nXs, (size_t)c * ld * 2));
 		HIPCHK(hipMalloc(&na, (size_t)c * sizeof(float4)));
 		HIPCHK(hipMalloc(&nl, (size_t)c * sizeof(int64_t)));
 		if (rowaux_l2 || (metric_quirk && metric != METRIC_L2)) HIPCHK(hipMalloc(&na2, (size_t)c * sizeof(float4)));
@@ -355,9 +358,11 @@ struct Index {
 		if (!on) {
 			if (Xs) HIPCHK(hipFree(Xs));
 			Xs = nullptr;
-			return;
 		}
-		if (xbf16 || !X) return;  // allocated with the store
+	}
+	// the bf16 scan copy, built now if the store keeps one and it is not there yet
+	void ensure_xs() {
+		if (!has_scan_copy() || Xs || !X || cap == 0) return;
 		HIPCHK(hipMalloc(&Xs, (size_t)cap * ld * 2));
 		HIPCHK(hipMemsetAsync(Xs, 0, (size_t)cap * ld * 2, stream));
 		fill_scan_copy(0, n_slots, Xs);

@@ -28,6 +28,7 @@ IvfState::~IvfState() { delete coarse; }
 void ivf_free(IvfState *s) { delete s; }
 
 static StoreView store_view(Index *ix) {
+	ix->ensure_xs();  // the IVF_FLAT bound scan and the coarse search stream bf16 rows
 	return StoreView{ix->X,  ix->rowaux, ix->dlabels, ix->n_slots, ix->ld, ix->dim, ix->metric, ix->xbf16 ? 1 : 0,
 	                 ix->Xs ? static_cast<const void *>(ix->Xs) : ix->X, (ix->xbf16 || ix->Xs) ? 1 : 0};
 }

@@ -47,14 +47,15 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	const int eff_metric = metric_quirk ? METRIC_L2 : metric;
 	const float4 *aux = search_aux((metric_quirk && metric != METRIC_L2) ? rowaux_l2 : rowaux);
 	const float ma = (metric_quirk && metric != METRIC_L2) ? max_alpha_l2 : max_alpha;
-	const float mu = (metric_quirk && metric != METRIC_L2) ? max_ux_l2 : max_ux;
-	StoreView sv{X, aux, dlabels, n_slots, ld, dim, eff_metric, xbf16 ? 1 : 0,
-	             Xs ? static_cast<const void *>(Xs) : X, (xbf16 || Xs) ? 1 : 0};
 	// int8 scan copy (option scan_i8): the scans stream int8 rows with their own
 	// row terms; refine, fallback and the outputs read X and rowaux as always
 	// (k <= 32: past that the looser bounds leave more rows below the k-th
-	// distance than the selection's capacity holds)
+	// distance than the selection's capacity holds); otherwise bf16 rows
 	const bool use8 = i8_usable() && k <= 32;
+	if (!use8) ensure_xs();
+	const float mu = (metric_quirk && metric != METRIC_L2) ? max_ux_l2 : max_ux;
+	StoreView sv{X, aux, dlabels, n_slots, ld, dim, eff_metric, xbf16 ? 1 : 0,
+	             Xs ? static_cast<const void *>(Xs) : X, (xbf16 || Xs) ? 1 : 0};
 	last_scan_esz = use8 ? 1 : (xbf16 || Xs) ? 2 : 4;
 	if (use8) {
 		ensure_i8();

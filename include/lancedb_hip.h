@@ -179,14 +179,25 @@ int32_t lance_hip_device_count(void);
  *                  bf16 keeps the nearest-even bf16 of each added row and every
  *                  result is exact with respect to those stored rows.  Only
  *                  while the table holds no rows.
- *   "scan_copy"    "on" (default) | "off": an f32 store also keeps a bf16 copy
- *                  of its rows that the scan streams (2 B per element instead
- *                  of 4; +50% device memory); refine and get_vector read the
- *                  f32 rows, results are unchanged
+ *   "scan_i8"      "on" (default) | "off": an f32 store with dim padded to a
+ *                  multiple of 128 (<= 1024) also keeps an int8 copy of its rows
+ *                  (one scale per 256-row tile, 1 B per element + 16 B of row
+ *                  terms) that the flat scans stream when k <= 32, no predicate
+ *                  and no metric_quirk; results are unchanged (exact re-rank +
+ *                  certificate).  Built on the first search or by "prepare".
+ *   "prepare"      "1": build the int8 scan copy now (outside any timing)
+ *   "scan_copy"    "on" (default) | "off": an f32 store may keep a bf16 copy of
+ *                  its rows for the scans the int8 copy does not serve (k > 32,
+ *                  a predicate, metric_quirk) and the IVF_FLAT bound scan; built
+ *                  on the first search that needs it; refine and get_vector read
+ *                  the f32 rows, results are unchanged
  *   "sample_div"   the threshold sample pass covers ~1/sample_div of the row
  *                  tiles (at least 32 tiles); default "32"
- *   "cand_extra"   exact candidates re-ranked per query beyond k: max(k *
- *                  refine_factor, k + max(cand_extra, k)), default "32"
+ *   "cand_extra"   small stores (dense path, <= 65536 rows): exact candidates
+ *                  re-ranked per query beyond k: max(k * refine_factor, k +
+ *                  max(cand_extra, k)), default "32"; the threshold path re-ranks
+ *                  in bound order until its certificate holds (no fixed count)
+ *   "cand_extra_i8" the same for the dense path on the int8 copy; "0" = auto (96)
  *   "small_exact"  "1" (default) | "0": <= 8 queries over <= 32768 slots
  *                  (k <= 64, dim <= 4096) take one launch of exact f64
  *                  distances + merge instead of the bound/refine pipeline
@@ -195,15 +206,25 @@ int32_t lance_hip_device_count(void);
  *   "index_type"   "ivf_pq" (default) | "ivf_flat": what create_index builds
  *   "kmeans_iters" k-means iterations (coarse and PQ), default "50"
  *   "ivf_seed"     seed of the k-means training sample, default 24301
+ *   "ivf_flat_scan" "bound" (default) | "exact": IVF_FLAT list scan by MFMA bf16
+ *                  lower bounds + certified exact re-rank, or exact f64 distances
+ *   "pq_scan"      "fast" (default) | "exact_lut": IVF_PQ list-major 8-bit-LUT
+ *                  scan, or the query-major f32-LUT scan
+ *   "pq_query"     "f32" (default) | "fp8": IVF_PQ distance tables from e4m3
+ *                  (fp8) queries (BASELINE.json configs[4]); coarse search and
+ *                  re-rank keep the f32 query
  *   "time_kernels" "1" = record HIP events around scan launches
  *                  (lance_hip_kernel_times); default "0"
+ *   "scan8_variant" development knob: geometry of the int8 append kernel at
+ *                  dim 768 (rows per wave, register ring depth); "0" = default
  * The handle is bound to the HIP device current when it was created.
  * Returns 0 or -1. */
 int32_t lance_hip_set_option(void *handle, const char *key, const char *value, char *err_buf, int err_buf_len);
 
 /* Statistics of the last search on this handle (for benches/tests):
  * out[0] = queries whose exactness certificate failed and took the exact
- * fallback, out[1] = total candidates refined, out[2] = max pool size,
+ * fallback, out[1] = total candidates refined (first pass), out[2] = max pool
+ * size,
  * out[3] = 1 if the dense (small-N) path ran, 2 if the one-launch small exact
  * search ran (option "small_exact", default on: <= 8 queries, <= 32768 slots,
  * k <= 64, dim <= 4096), out[4] = queries rerun by the
@@ -217,12 +238,12 @@ int32_t lance_hip_last_search_stats(void *handle, int64_t *out, int32_t n);
  * out[0] total ms of threshold-scan launches, out[1] their count, out[2] rows
  * per launch, out[3] padded queries per launch, out[4] total ms of small-store
  * dense scans, out[5] their count, out[6] bytes per element the scan streams
- * (2 with a bf16 store or scan copy, else 4), out[7] total ms of IVF list-scan
- * launches, out[8] their count, out[9] their algorithmic bytes (every probed
- * list's rows or codes once + each query's PQ table, summed), out[10] (query, row)
- * pairs scored (summed), out[11] total ms of the IVF coarse searches, out[12]
- * 1 if the last timed threshold scan ran the register-streamed kernel (option
- * "rscan"), 0 for the LDS-staged one.
+ * (1 with the int8 scan copy, 2 with a bf16 store or scan copy, else 4),
+ * out[7] total ms of IVF list-scan launches, out[8] their count, out[9] their
+ * algorithmic bytes (every probed list's rows or codes once + each query's PQ
+ * table, summed), out[10] (query, row) pairs scored (summed), out[11] total ms
+ * of the IVF coarse searches, out[12] which kernel ran the last timed threshold
+ * scan: 2 the int8 scan8_kernel, 0 the LDS-staged scan_kernel.
  * Returns 0 or -1. */
 int32_t lance_hip_kernel_times(void *handle, double *out, int32_t n);
 

@@ -251,3 +251,27 @@ def test_ivf_flat_bound_scan_ties_fall_back_exactly(hip, mk):
     gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 10, nprobes=4)
     el, ed, ec = oracle_search(hip, h, X, Q, 10, 4, 1, "l2")
     assert_same(gl, gd, gc, el, ed, ec)
+
+
+def test_ivf_flat_bound_scan_zero_cosine_rows_and_query(hip, mk):
+    """Cosine with zero rows and a zero query: the rows' / query's bounds are
+    NaN (cosine undefined).  The bound scan must not certify a result that left
+    such a live row out; it reruns on the exact scan and returns what the exact
+    scan returns (NaN-distance rows after every other row)."""
+    rng = np.random.default_rng(17)
+    n, d, nlist = 8_000, 128, 16
+    X = clustered(rng, n, d, centers=16)
+    X[10:14] = 0.0  # zero rows
+    Q = np.concatenate([X[rng.choice(n, 6, replace=False)] + 0.2, np.zeros((1, d), np.float32)]).astype(np.float32)
+    h = mk(d, "cosine", "ivf_flat")
+    hip.LanceDetachedAddBatch(h, X, n, d)
+    hip.LanceDetachedCreateIndex(h, nlist, 0)
+    for nprobe, k in [(16, 10), (4, 15), (1, 15)]:  # k <= 15: the bound scan applies
+        hip.LanceHipSetOption(h, "ivf_flat_scan", "bound")
+        bl, bd, bc = hip.LanceDetachedSearchBatch(h, Q, k, nprobes=nprobe)
+        hip.LanceHipSetOption(h, "ivf_flat_scan", "exact")
+        xl, xd, xc = hip.LanceDetachedSearchBatch(h, Q, k, nprobes=nprobe)
+        assert bc[-1] == min(k, n)  # the zero query: every probed row, NaN distances, label order
+        np.testing.assert_array_equal(bc, xc)
+        np.testing.assert_array_equal(bl, xl)
+        np.testing.assert_allclose(bd, xd, rtol=1e-6, equal_nan=True)

@@ -1,0 +1,178 @@
+"""GPU parity of scan8_kernel, the int8 append pass (scan8_kernels.hip,
+DESIGN.md §3): query halves resident in LDS, rows streamed into registers, the
+bound screened in exact integers against per-tile / per-batch scales, then the
+pool refined in bound order until certified (pool_refine_kernel).  Results must
+equal the f64 oracle exactly (labels bit-exact, distances within 1e-4 relative;
+reference semantics lance_manager.rs:393-451, squared L2 / 1 - x.q / cosine).
+
+Covers every ld the kernel is instantiated for, the three metrics, the
+distributions where common scales are worst (the CPU restatement
+tests/test_i8_bound_cpu.py checks the same algebra in f64), in-place appends
+into partly filled tiles (the tile scale grows), zero rows, deletes, every
+query-batch geometry (one tile split into halves, a small batch on every
+workgroup, several tiles) and the C2 configuration at full size."""
+import numpy as np
+import pytest
+
+from oracle import c_oracle, flat_knn
+from tests.test_gpu_parity import assert_same
+
+pytestmark = pytest.mark.gpu
+
+
+def _mk(hip, tmp_path, d, metric):
+    h = hip.LanceCreateDetached(str(tmp_path), d, metric, "t")
+    hip.LanceHipSetOption(h, "scan_i8", "on")
+    hip.LanceHipSetOption(h, "time_kernels", "1")
+    return h
+
+
+def _ran_scan8(hip, h):
+    kt = hip.LanceHipKernelTimes(h)
+    return kt["scan_elem_bytes"] == 1 and kt["scan_kernel"] == "scan8_kernel"
+
+
+@pytest.mark.parametrize("metric", ["l2", "dot", "cosine"])
+@pytest.mark.parametrize("d", [512, 600, 768, 896, 1000])  # ld 512, 640, 768, 896, 1024
+def test_scan8_every_ld(hip, tmp_path, d, metric):
+    rng = np.random.default_rng(d)
+    n = 80_000
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Q = rng.standard_normal((300, d)).astype(np.float32)  # a split tile + a small one
+    h = _mk(hip, tmp_path, d, metric)
+    try:
+        hip.LanceDetachedAddBatch(h, X, n, d)
+        dead = rng.choice(n, 4_000, replace=False)
+        hip.LanceDetachedDeleteBatch(h, dead)
+        live = np.ones(n, bool)
+        live[dead] = False
+        gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 10)
+        assert _ran_scan8(hip, h)
+        el, ed, ec = c_oracle.flat_search_batch(X, Q, 10, metric, live=live, acc64=True, nthreads=16)
+        assert_same(gl, gd, gc, el, ed, ec)
+        assert hip.LanceHipLastSearchStats(h)["fallback_queries"] <= 3
+    finally:
+        hip.LanceFreeDetached(h)
+
+
+def _datasets(rng, n, d):
+    yield "heavy", rng.standard_cauchy((n, d)).clip(-1e4, 1e4).astype(np.float32)
+    spike = rng.standard_normal((n, d)).astype(np.float32) * 1e-3
+    spike[np.arange(n), rng.integers(0, d, n)] = 50.0
+    yield "spike", spike
+    yield "near_const", (3.0 + 1e-4 * rng.standard_normal((n, d))).astype(np.float32)
+    yield "tiny", (1e-15 * rng.standard_normal((n, d))).astype(np.float32)
+    yield "huge", (1e15 * rng.standard_normal((n, d))).astype(np.float32)
+    yield "sparse_int", rng.integers(-3, 4, (n, d)).astype(np.float32)
+    mixed = rng.standard_normal((n, d)).astype(np.float32)
+    mixed[rng.random(n) < 0.5] *= 100.0  # two norm scales inside every tile
+    yield "mixed_norms", mixed
+
+
+@pytest.mark.parametrize("metric", ["l2", "dot", "cosine"])
+def test_scan8_adversarial_distributions(hip, tmp_path, metric):
+    # the distributions tests/test_i8_bound_cpu.py pins in f64, end to end at d = 768
+    rng = np.random.default_rng(99)
+    n, d = 70_000, 768
+    for name, X in _datasets(rng, n, d):
+        Q = np.concatenate([X[:32] + np.float32(0.01) * np.abs(X[:32]).max() * rng.standard_normal((32, d)).astype(np.float32),
+                            rng.standard_normal((32, d)).astype(np.float32) * np.abs(X).max()])
+        h = _mk(hip, tmp_path, d, metric)
+        try:
+            hip.LanceDetachedAddBatch(h, X, n, d)
+            gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 10)
+            assert _ran_scan8(hip, h), name
+            el, ed, ec = c_oracle.flat_search_batch(X, Q, 10, metric, acc64=True, nthreads=16)
+            assert_same(gl, gd, gc, el, ed, ec)
+        finally:
+            hip.LanceFreeDetached(h)
+
+
+@pytest.mark.parametrize("metric", ["l2", "dot", "cosine"])
+def test_scan8_incremental_append_and_delete(hip, tmp_path, metric):
+    # appends into a partly filled tile re-quantise it (its scale grows with
+    # larger rows); rows of smaller norm keep it; zero rows (cosine: undefined,
+    # exact fallback) and deletes update the copy in place
+    rng = np.random.default_rng(4321)
+    d = 768
+    X = rng.standard_normal((110_000, d)).astype(np.float32)
+    X[90_000:100_000] *= 4.0    # larger norms: tile scales grow
+    X[100_000:] *= 0.25         # smaller norms: scales unchanged
+    X[100_500:100_510] = 0.0    # zero rows
+    Q = rng.standard_normal((40, d)).astype(np.float32)
+    h = _mk(hip, tmp_path, d, metric)
+    try:
+        hip.LanceHipSetOption(h, "reserve_rows", "131072")
+        live = np.zeros(len(X), bool)
+        for lo, hi in ((0, 70_100), (70_100, 90_000), (90_000, 100_000), (100_000, 110_000)):
+            hip.LanceDetachedAddBatch(h, X[lo:hi], hi - lo, d)
+            live[lo:hi] = True
+            gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 10)
+            el, ed, ec = c_oracle.flat_search_batch(X, Q, 10, metric, live=live, acc64=True, nthreads=16)
+            assert_same(gl, gd, gc, el, ed, ec)
+            dead = np.unique(el[:, :3])
+            hip.LanceDetachedDeleteBatch(h, dead)
+            live[dead] = False
+            gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 10)
+            el, ed, ec = c_oracle.flat_search_batch(X, Q, 10, metric, live=live, acc64=True, nthreads=16)
+            assert_same(gl, gd, gc, el, ed, ec)
+    finally:
+        hip.LanceFreeDetached(h)
+
+
+@pytest.mark.parametrize("nq", [1, 7, 128, 129, 256, 257, 700])
+def test_scan8_query_batches(hip, tmp_path, nq):
+    # one workgroup per half of a tile (> 128 queries in it) or all workgroups on
+    # one half (<= 128), several tiles per launch
+    rng = np.random.default_rng(nq)
+    n, d = 90_000, 768
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Q = rng.standard_normal((nq, d)).astype(np.float32)
+    h = _mk(hip, tmp_path, d, "l2")
+    try:
+        hip.LanceDetachedAddBatch(h, X, n, d)
+        gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 10)
+        el, ed, ec = c_oracle.flat_search_batch(X, Q, 10, "l2", acc64=True, nthreads=16)
+        assert_same(gl, gd, gc, el, ed, ec)
+    finally:
+        hip.LanceFreeDetached(h)
+
+
+def test_scan8_zero_cosine_query_and_k_edges(hip, tmp_path):
+    rng = np.random.default_rng(3)
+    n, d = 70_000, 768
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Q = rng.standard_normal((6, d)).astype(np.float32)
+    Q[2] = 0.0
+    h = _mk(hip, tmp_path, d, "cosine")
+    try:
+        hip.LanceDetachedAddBatch(h, X, n, d)
+        for k in (1, 32):
+            gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, k)
+            el, ed, ec = flat_knn.flat_search_batch(X, np.arange(n), np.ones(n, bool), Q, k, metric="cosine")
+            for i in (0, 1, 3, 4, 5):
+                assert gc[i] == ec[i]
+                np.testing.assert_array_equal(gl[i], el[i])
+    finally:
+        hip.LanceFreeDetached(h)
+
+
+def test_c2_full_size(hip, tmp_path):
+    # BASELINE.json configs[1] at its own size: 1M x 768 f32, k = 10, 256 queries,
+    # every query against the f64 oracle
+    rng = np.random.default_rng(20260)
+    n, d = 1_000_000, 768
+    X = rng.standard_normal((n, d), dtype=np.float32)
+    Q = rng.standard_normal((256, d), dtype=np.float32)
+    h = _mk(hip, tmp_path, d, "l2")
+    try:
+        for lo in range(0, n, 250_000):
+            hip.LanceDetachedAddBatch(h, X[lo:lo + 250_000], 250_000, d)
+        gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 10)
+        assert _ran_scan8(hip, h)
+        st = hip.LanceHipLastSearchStats(h)
+        el, ed, ec = c_oracle.flat_search_batch(X, Q, 10, "l2", acc64=True, nthreads=16)
+        assert_same(gl, gd, gc, el, ed, ec)
+        assert st["fallback_queries"] == 0, st
+    finally:
+        hip.LanceFreeDetached(h)
