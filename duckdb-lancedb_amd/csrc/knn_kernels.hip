@@ -2734,34 +2734,58 @@ __global__ __launch_bounds__(SMALL_THREADS) void small_exact_kernel(const T *__r
 	const int q = blockIdx.y, G = gridDim.x, t = threadIdx.x;
 	for (int i = t; i < dim; i += SMALL_THREADS) sq[i] = Q[(int64_t)q * dim + i];
 	__syncthreads();
-	const int64_t r = (int64_t)blockIdx.x * SMALL_THREADS + t;
-	SHit h{F_INF, 0, INT64_MAX};
-	if (r < n && reinterpret_cast<const float *>(rowaux)[raix(r, 0)] != F_INF) {
-		const T *x = X + r * ld;
-		double a = 0.0, b = 0.0, c = 0.0;
+	// distances: each wave takes 64 of the workgroup's rows in 8 groups of 8;
+	// a row is split over 8 lanes (float4 chunks sub, sub + 8, ...: coalesced
+	// row reads, every group's loads in flight together), partial f64 sums
+	// reduced over the 8 lanes (the sum of the same products as exact_distance)
+	{
+		const int lane = t & 63, w = t >> 6, sub = lane & 7;
 		const int d4 = dim >> 2;  // rows are padded to a multiple of 4 elements: aligned 16-B (8-B bf16) loads
-#pragma unroll 4
-		for (int i4 = 0; i4 < d4; ++i4) {
-			const float4 xv = xval4(x, 4 * i4);
-			const float4 qv = *reinterpret_cast<const float4 *>(sq + 4 * i4);
-			exact_acc<METRIC>(xv.x, qv.x, a, b, c);
-			exact_acc<METRIC>(xv.y, qv.y, a, b, c);
-			exact_acc<METRIC>(xv.z, qv.z, a, b, c);
-			exact_acc<METRIC>(xv.w, qv.w, a, b, c);
+#pragma unroll
+		for (int g = 0; g < 8; ++g) {
+			const int rl = w * 64 + g * 8 + (lane >> 3);  // row within the workgroup
+			const int64_t r = (int64_t)blockIdx.x * SMALL_THREADS + rl;
+			const bool ok = r < n && reinterpret_cast<const float *>(rowaux)[raix(r < n ? r : 0, 0)] != F_INF;
+			double a = 0.0, b = 0.0, c = 0.0;
+			if (ok) {
+				const T *x = X + r * ld;
+#pragma unroll 2
+				for (int i4 = sub; i4 < d4; i4 += 8) {
+					const float4 xv = xval4(x, 4 * i4);
+					const float4 qv = *reinterpret_cast<const float4 *>(sq + 4 * i4);
+					exact_acc<METRIC>(xv.x, qv.x, a, b, c);
+					exact_acc<METRIC>(xv.y, qv.y, a, b, c);
+					exact_acc<METRIC>(xv.z, qv.z, a, b, c);
+					exact_acc<METRIC>(xv.w, qv.w, a, b, c);
+				}
+				for (int i = 4 * d4 + sub; i < dim; i += 8) exact_acc<METRIC>(xval(x, i), sq[i], a, b, c);
+			}
+#pragma unroll
+			for (int o = 1; o < 8; o <<= 1) {
+				a += __shfl_xor(a, o, 64);
+				if (METRIC == METRIC_COSINE) {
+					b += __shfl_xor(b, o, 64);
+					c += __shfl_xor(c, o, 64);
+				}
+			}
+			if (sub == 0) {
+				SHit h{F_INF, 0, INT64_MAX};
+				if (ok) {
+					double v;
+					if (METRIC == METRIC_L2)
+						v = a;
+					else if (METRIC == METRIC_DOT)
+						v = 1.0 - a;
+					else
+						v = 1.0 - a / (sqrt(b) * sqrt(c));
+					float f = (float)v + 0.0f;
+					if (__builtin_isnan(f)) f = __builtin_nanf("");
+					h = SHit{f, 1, labels[r]};
+				}
+				s[rl] = h;
+			}
 		}
-		for (int i = 4 * d4; i < dim; ++i) exact_acc<METRIC>(xval(x, i), sq[i], a, b, c);
-		double v;
-		if (METRIC == METRIC_L2)
-			v = a;
-		else if (METRIC == METRIC_DOT)
-			v = 1.0 - a;
-		else
-			v = 1.0 - a / (sqrt(b) * sqrt(c));
-		float f = (float)v + 0.0f;
-		if (__builtin_isnan(f)) f = __builtin_nanf("");
-		h = SHit{f, 1, labels[r]};
 	}
-	s[t] = h;
 	__syncthreads();
 	// this workgroup's top-k: sorted by (distance, label)
 	if (!LHIP_ABL_SMALL_NOWGSORT) shit_sort(s, SMALL_THREADS);

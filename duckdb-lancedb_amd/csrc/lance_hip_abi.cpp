@@ -776,12 +776,36 @@ int32_t lance_detached_search_batch(void *handle, const float *queries, int32_t 
 		}
 		ix->bind();
 		auto &ws = ix->ws;
+		const size_t qb = (size_t)nq * dim * sizeof(float), lb = (size_t)nq * k * sizeof(int64_t);
+		const size_t db = (size_t)nq * k * sizeof(float), cb = (size_t)nq * sizeof(int32_t);
+		struct DeferSync {
+			decltype(ix) p;
+			~DeferSync() { p->defer_sync = false; }
+		} defer{ix};
+		if (nq <= 8) {
+			// the lance_search() pattern (one query per call, lance_search.cpp:73-74):
+			// no copies at all — the kernels read the query from, and write the
+			// results into, pinned host memory (device-visible), one stream wait
+			const size_t qb16 = (qb + 15) / 16 * 16;
+			uint8_t *io = ws.need_host_io(qb16 + lb + db + cb);
+			void *dio = nullptr;
+			HIPCHK(hipHostGetDevicePointer(&dio, io, 0));
+			uint8_t *d8 = static_cast<uint8_t *>(dio);
+			memcpy(io, queries, qb);
+			ix->defer_sync = true;
+			ix->search_any(reinterpret_cast<const float *>(d8), nq, k, nprobes, refine_factor,
+			               reinterpret_cast<int64_t *>(d8 + qb16), reinterpret_cast<float *>(d8 + qb16 + lb),
+			               reinterpret_cast<int32_t *>(d8 + qb16 + lb + db));
+			lhip::spin_sync(ix->stream);
+			memcpy(out_labels, io + qb16, lb);
+			memcpy(out_distances, io + qb16 + lb, db);
+			memcpy(out_counts, io + qb16 + lb + db, cb);
+			return nq;
+		}
 		ws.Qin.need((size_t)nq * dim);
 		// pinned staging: true async copies on the handle's stream, one wait at
 		// the end; the results [labels | distances | counts] are one device
 		// block, read back by one copy
-		const size_t qb = (size_t)nq * dim * sizeof(float), lb = (size_t)nq * k * sizeof(int64_t);
-		const size_t db = (size_t)nq * k * sizeof(float), cb = (size_t)nq * sizeof(int32_t);
 		ws.out_blk.need(lb + db + cb);
 		int64_t *dL = reinterpret_cast<int64_t *>(ws.out_blk.p);
 		float *dD = reinterpret_cast<float *>(ws.out_blk.p + lb);
@@ -789,10 +813,6 @@ int32_t lance_detached_search_batch(void *handle, const float *queries, int32_t 
 		uint8_t *io = ws.need_host_io(std::max(qb, lb + db + cb));
 		memcpy(io, queries, qb);
 		HIPCHK(hipMemcpyAsync(ws.Qin.p, io, qb, hipMemcpyHostToDevice, ix->stream));
-		struct DeferSync {
-			decltype(ix) p;
-			~DeferSync() { p->defer_sync = false; }
-		} defer{ix};
 		ix->defer_sync = true;  // the readback below waits for the search
 		ix->search_any(ws.Qin.p, nq, k, nprobes, refine_factor, dL, dD, dC);
 		HIPCHK(hipMemcpyAsync(io, ws.out_blk.p, lb + db + cb, hipMemcpyDeviceToHost, ix->stream));

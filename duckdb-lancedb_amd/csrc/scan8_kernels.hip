@@ -239,7 +239,13 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 #pragma unroll
 			for (int u = 0; u < 8; ++u) gi[u] = s8_query_part(QA[16 * u + lr], TAU[16 * u + lr], ts, W);
 
+			// accumulators start at -Bi (copies, then every MFMA accumulates in place:
+			// a bias operand shared by 8 MFMAs made the compiler rename them per k-step)
 			i32x4 acc[RB][8];
+#pragma unroll
+			for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+				for (int u = 0; u < 8; ++u) acc[rb][u] = bias[rb];
 			const int8_t *tb_cur = xtile(b), *tb_next = xtile(b + 1);
 			__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -251,8 +257,7 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 				for (int u = 0; u < 8; ++u) {
 #pragma unroll
 					for (int rb = 0; rb < RB; ++rb)
-						acc[rb][u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xa[sl][rb], bq[cur][u],
-						                                                   j == 0 ? bias[rb] : acc[rb][u], 0, 0, 0);
+						acc[rb][u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xa[sl][rb], bq[cur][u], acc[rb][u], 0, 0, 0);
 				}
 				// refill the slot with k-step j + D of this wave's stream
 				const int jn = j + D;
