@@ -10,6 +10,7 @@ enum Metric : int { METRIC_L2 = 0, METRIC_DOT = 1, METRIC_COSINE = 2 };
 
 // Scan tile geometry (see DESIGN.md "Scan kernel").
 constexpr int SCAN_BR = 256;  // base rows per workgroup tile (MFMA M)
+constexpr int I8_CHUNK_STRIDE = SCAN_BR * 64;  // int8 copy (k-major tiles): bytes between a tile's 64-B k-chunks
 constexpr int SCAN_BQ = 256;  // queries per workgroup tile   (MFMA N)
 constexpr int SCAN_BK = 64;   // k-step
 constexpr int DPAD = 64;      // row stride of the device store is a multiple of this

@@ -129,6 +129,12 @@ void launch_rows_to_bf16(const float *src, int64_t src_ld, int64_t n, int dim, i
 // exact in f32 too).  Row terms (tile-blocked SoA like rowaux):
 //   l2: (|x|^2, |e_x|, |x~|, s_T)   dot: (0, |e_x|, |x~|, s_T)
 //   cosine: (0, |e_x|, |x~|, s_T) of the normalised row   (norms rounded up)
+// Layout (k-major tiles): tile t is one block of 256 * ld bytes holding its rows'
+// 64-byte k-chunks chunk-major, byte c of row r at
+//   t * 256 * ld + (c / 64) * 16384 + (r % 256) * 64 + c % 64,
+// so one k-step of 16 rows (an MFMA operand load) is 1 KiB contiguous.  The
+// two workgroups that read a tile (scan8's query halves) then share it in L2;
+// row-major rows (16 half-used lines per load) ran 1.5x longer at 10M x 768.
 // Per tile: tstat = (s_T, max |e_x|, max |x~|, 0) over its rows.  A scale common
 // to the tile (and one common to the query batch, prep_queries_i8) makes the
 // product scale of a bound s_T s_Q the same for every (row, query) of a tile:
@@ -190,10 +196,13 @@ __global__ __launch_bounds__(256) void tiles_to_i8_kernel(const float *__restric
 	// pass 2: quantise
 	for (int rr = wv; rr < SCAN_BR; rr += 4) {
 		const int64_t r = tile * SCAN_BR + rr;
-		uint32_t *xq = reinterpret_cast<uint32_t *>(Xq + r * (int64_t)ld);
+		int8_t *xrow = Xq + tile * SCAN_BR * (int64_t)ld + rr * 64;  // k-chunk c at xrow + c * I8_CHUNK_STRIDE
+		auto xq_at = [&](int i0) -> uint32_t * {
+			return reinterpret_cast<uint32_t *>(xrow + (int64_t)(i0 >> 6) * I8_CHUNK_STRIDE + (i0 & 63));
+		};
 		float *o = reinterpret_cast<float *>(aux8);
 		if (r >= n_slots) {
-			for (int i0 = 4 * lane; i0 < ld; i0 += 256) xq[i0 >> 2] = 0u;
+			for (int i0 = 4 * lane; i0 < ld; i0 += 256) *xq_at(i0) = 0u;
 			if (lane == 0) {
 				o[raix(r, 0)] = F_INF;
 				o[raix(r, 1)] = 0.f;
@@ -223,7 +232,7 @@ __global__ __launch_bounds__(256) void tiles_to_i8_kernel(const float *__restric
 				}
 				packed |= ((uint32_t)qv & 0xFFu) << (8 * j);
 			}
-			xq[i0 >> 2] = packed;
+			*xq_at(i0) = packed;
 		}
 		e2 = wave_sum_f64(e2);
 		t2 = wave_sum_f64(t2);
@@ -835,7 +844,10 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 #pragma unroll
 	for (int j = 0; j < C::XDMA; ++j) {
 		const int xr = (C::XDMA * w + j) * C::ROWS_PER_DMA + lane / C::XCH;
-		xoff[j] = (uint32_t)(xr * ld * C::XE + (C::xswz(xr, lane % C::XCH) << 4));
+		const int c = C::xswz(xr, lane % C::XCH);  // 16 B source chunk of the stage's SK bytes
+		// int8: k-major tiles (tiles_to_i8_kernel): 64-B chunk c / 4 of the stage
+		xoff[j] = I8 ? (uint32_t)((c >> 2) * I8_CHUNK_STRIDE + xr * 64 + ((c & 3) << 4))
+		             : (uint32_t)(xr * ld * C::XE + (c << 4));
 	}
 #pragma unroll
 	for (int j = 0; j < C::QDMA; ++j) {
@@ -893,7 +905,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 			iss_ra += tile_rows_step;
 			iss_q = qbase;
 		} else {
-			iss_xt += C::SK * C::XE;
+			iss_xt += I8 ? (C::SK / 64) * I8_CHUNK_STRIDE : C::SK * C::XE;
 			iss_q += C::SK * C::QE;
 		}
 	};
@@ -2348,6 +2360,29 @@ __device__ __forceinline__ void exact_distance_multi(const T *__restrict__ X, in
 	}
 }
 
+// ascending bitonic sort of a[0, P) (P a power of two >= 64) by the block
+__device__ __forceinline__ void pr_bitonic(uint64_t *a, int P) {
+	const int t = threadIdx.x;
+	for (int size = 2; size <= P; size <<= 1) {
+		for (int stride = size >> 1; stride > 0; stride >>= 1) {
+			for (int i = t; i < (P >> 1); i += PR_THREADS) {
+				const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
+				const bool asc = (lo & size) == 0;
+				const uint64_t x = a[lo], y = a[hi];
+				if ((x > y) == asc) {
+					a[lo] = y;
+					a[hi] = x;
+				}
+			}
+			__syncthreads();
+		}
+	}
+}
+
+constexpr int PR_SEL = 1024;  // chunk capacity: the smallest bounds, sorted
+constexpr int PR_HB = 1024;   // histogram bins of a chunk selection
+constexpr int PR_R = 256;     // chunk target of the final pass
+
 template <int METRIC, typename T>
 __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
     const uint2 *__restrict__ seg_pool, const int *__restrict__ seg_cnt, int seg_cap, int n_seg, int nq,
@@ -2356,16 +2391,20 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
     int64_t *__restrict__ outL, float *__restrict__ outD, int *__restrict__ outC, int *__restrict__ cert,
     int *__restrict__ refined, int *__restrict__ pool_total) {
 	__shared__ uint64_t keys[PR_CAP];
+	__shared__ uint64_t sel[PR_SEL];
+	__shared__ unsigned hist[PR_HB];
 	__shared__ float cd[2][PR_MAXK + PR_CHUNK];  // running top-k (double-buffered) + the round's distances
 	__shared__ int64_t cl[2][PR_MAXK + PR_CHUNK];
 	__shared__ unsigned sh[PR_WAVES];
-	__shared__ int s_over, s_nfin, s_nnan, s_dnan;
+	__shared__ int s_over, s_nnan, s_dnan;
+	__shared__ unsigned s_nfin, s_knf, s_kmin, s_kmax, s_bstar, s_cum, s_below, s_ns;
 	const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
 	if (t == 0) {
 		s_over = 0;
-		s_nfin = 0;
 		s_nnan = 0;
 		s_dnan = 0;
+		s_nfin = 0;
+		s_knf = 0xFFFFFFFFu;
 	}
 	__syncthreads();
 	// ---- gather the pool (thread s < n_seg: segment s) ----------------------
@@ -2379,71 +2418,180 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 	static_assert(PR_THREADS == SEL_THREADS, "block_excl_scan's geometry");
 	const unsigned off = block_excl_scan(c, sh, total);
 	const int n = (int)min(total, (unsigned)PR_CAP);
-	if (t < n_seg && c) {
+	if (t < n_seg && c && off < (unsigned)PR_CAP) {
 		const uint2 *seg = seg_pool + ((int64_t)t * nq + q) * seg_cap;
-		for (unsigned i = 0; i < c && off + i < (unsigned)PR_CAP; ++i) {
-			const uint2 e = seg[i];
-			keys[off + i] = ((uint64_t)e.x << 32) | e.y;
+		const unsigned cm = min(c, (unsigned)PR_CAP - off);
+		for (unsigned i = 0; i < cm; i += 8) {  // 8 loads in flight per thread
+			uint2 e[8];
+#pragma unroll
+			for (int u = 0; u < 8; ++u)
+				if (i + u < cm) e[u] = seg[i + u];
+#pragma unroll
+			for (int u = 0; u < 8; ++u)
+				if (i + u < cm) keys[off + i + u] = ((uint64_t)e[u].x << 32) | e[u].y;
 		}
 	}
-	int P = 64;
-	while (P < n) P <<= 1;
-	for (int i = n + t; i < P; i += PR_THREADS) keys[i] = ~0ull;
 	__syncthreads();
 	if (t == 0 && total > (unsigned)PR_CAP) s_over = 1;
-	// ---- sort by (LB, slot) --------------------------------------------------
-	for (int size = 2; size <= P; size <<= 1) {
-		for (int stride = size >> 1; stride > 0; stride >>= 1) {
-			for (int i = t; i < (P >> 1); i += PR_THREADS) {
-				const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
-				const bool asc = (lo & size) == 0;
-				const uint64_t a = keys[lo], b = keys[hi];
-				if ((a > b) == asc) {
-					keys[lo] = b;
-					keys[hi] = a;
-				}
-			}
-			__syncthreads();
-		}
-	}
-	// finite bounds first, then +inf, then NaN (KEY_INF < KEY_NAN), then padding
+	// finite bounds (key < KEY_INF), NaN bounds, the smallest non-finite key
 	{
-		unsigned nf = 0, nn = 0;
+		unsigned nf = 0, nn = 0, knf = 0xFFFFFFFFu;
 		for (int i = t; i < n; i += PR_THREADS) {
 			const uint32_t kk = (uint32_t)(keys[i] >> 32);
 			nf += kk < KEY_INF ? 1u : 0u;
 			nn += kk == KEY_NAN ? 1u : 0u;
+			if (kk >= KEY_INF) knf = min(knf, kk);
 		}
 #pragma unroll
 		for (int o = 32; o > 0; o >>= 1) {
 			nf += __shfl_xor(nf, o, 64);
 			nn += __shfl_xor(nn, o, 64);
+			knf = min(knf, (unsigned)__shfl_xor(knf, o, 64));
 		}
 		if (lane == 0) {
-			atomicAdd(&s_nfin, (int)nf);
+			atomicAdd(&s_nfin, nf);
 			atomicAdd(&s_nnan, (int)nn);
+			atomicMin(&s_knf, knf);
 		}
 	}
 	__syncthreads();
-	const int nfin = s_nfin;
+	const int nfin = (int)s_nfin;
 	const float ftau = tau ? tau[q] : F_INF;
 	const float *qrow = Qf + (int64_t)q * ld;
+
+	// next chunk: the finite keys >= lo up to a histogram bin holding the R-th
+	// smallest (all keys equal to the chunk's last are in it), sorted into sel.
+	// Returns its size (0: none left), -1 when > PR_SEL keys share one value.
+	auto next_chunk = [&](unsigned lo, int R) -> int {
+		if (t == 0) {
+			s_kmin = 0xFFFFFFFFu;
+			s_kmax = 0;
+		}
+		__syncthreads();
+		{
+			unsigned kmn = 0xFFFFFFFFu, kmx = 0;
+			for (int i = t; i < n; i += PR_THREADS) {
+				const uint32_t kk = (uint32_t)(keys[i] >> 32);
+				if (kk >= lo && kk < KEY_INF) {
+					kmn = min(kmn, kk);
+					kmx = max(kmx, kk);
+				}
+			}
+#pragma unroll
+			for (int o = 32; o > 0; o >>= 1) {
+				kmn = min(kmn, (unsigned)__shfl_xor(kmn, o, 64));
+				kmx = max(kmx, (unsigned)__shfl_xor(kmx, o, 64));
+			}
+			if (lane == 0) {
+				atomicMin(&s_kmin, kmn);
+				atomicMax(&s_kmax, kmx);
+			}
+		}
+		__syncthreads();
+		unsigned kmin = s_kmin, kmax = s_kmax;
+		if (kmin == 0xFFFFFFFFu) return 0;
+		int shift;
+		unsigned bstar;
+		for (;;) {  // narrow until the chunk fits
+			const unsigned span = kmax - kmin;
+			shift = span >= (unsigned)PR_HB ? (32 - __builtin_clz(span)) - 10 : 0;  // (span >> shift) < PR_HB
+			for (int i = t; i < PR_HB; i += PR_THREADS) hist[i] = 0;
+			if (t == 0) {
+				s_bstar = PR_HB - 1;
+				s_cum = 0xFFFFFFFFu;
+				s_below = 0;
+			}
+			__syncthreads();
+			for (int i = t; i < n; i += PR_THREADS) {
+				const uint32_t kk = (uint32_t)(keys[i] >> 32);
+				if (kk >= kmin && kk <= kmax) atomicAdd(&hist[(kk - kmin) >> shift], 1u);
+			}
+			__syncthreads();
+			const unsigned h0 = hist[2 * t], h1 = hist[2 * t + 1];
+			static_assert(PR_HB == 2 * PR_THREADS, "two bins per thread");
+			unsigned tot;
+			const unsigned ex = block_excl_scan(h0 + h1, sh, tot);
+			if (ex < (unsigned)R && ex + h0 + h1 >= (unsigned)R) {
+				const bool first = ex + h0 >= (unsigned)R;
+				s_bstar = first ? 2 * t : 2 * t + 1;
+				s_cum = first ? ex + h0 : ex + h0 + h1;
+				s_below = first ? ex : ex + h0;
+			}
+			__syncthreads();
+			bstar = s_bstar;
+			const unsigned cum = s_cum == 0xFFFFFFFFu ? tot : s_cum, below = s_cum == 0xFFFFFFFFu ? tot : s_below;
+			if (cum <= (unsigned)PR_SEL) break;
+			if (below > 0) {  // the bins before b* alone
+				unsigned b = bstar;
+				while (b > 0 && hist[b - 1] == 0) --b;  // uniform: every thread reads the same bins
+				bstar = b - 1;
+				break;
+			}
+			if (shift == 0) return -1;  // > PR_SEL keys of one value
+			// everything up to b* is inside b*: histogram that bin alone
+			const unsigned nlo = kmin + (bstar << shift);
+			const unsigned nhi = nlo + ((1u << shift) - 1u);
+			kmin = nlo;
+			kmax = min(kmax, nhi);
+			__syncthreads();
+		}
+		if (t == 0) s_ns = 0;
+		__syncthreads();
+		for (int i = t; i < n; i += PR_THREADS) {
+			const uint64_t e = keys[i];
+			const uint32_t kk = (uint32_t)(e >> 32);
+			if (kk >= kmin && kk <= kmax && ((kk - kmin) >> shift) <= bstar) sel[atomicAdd(&s_ns, 1u)] = e;
+		}
+		__syncthreads();
+		const int ns = (int)s_ns;
+		int P = 64;
+		while (P < ns) P <<= 1;
+		for (int i = ns + t; i < P; i += PR_THREADS) sel[i] = ~0ull;
+		__syncthreads();
+		pr_bitonic(sel, P);
+		return ns;
+	};
+
 	// ---- refine in bound order ------------------------------------------------
 	const int limit = mode == 0 ? min(nfin, m_tau) : nfin;
 	int cnt = 0, cur = 0, pos = 0;  // top entries held, buffer holding them, candidates refined
 	float dk = F_INF;               // k-th distance of the top (+inf while fewer than k)
+	const uint64_t *arr = sel;      // the chunk being refined: arr[sp, ns)
+	int ns = 0, sp = 0;
+	unsigned lo = 0;                // keys < lo are refined
+	bool whole = false;             // the whole pool sorted (keys of one value past PR_SEL)
 	while (pos < limit) {
+		if (sp == ns) {
+			if (whole) break;
+			const int r = next_chunk(lo, mode == 0 ? limit - pos : PR_R);
+			if (r < 0) {
+				int P = 64;
+				while (P < n) P <<= 1;
+				for (int i = n + t; i < P; i += PR_THREADS) keys[i] = ~0ull;
+				__syncthreads();
+				pr_bitonic(keys, P);
+				arr = keys;  // the first pos entries are the keys < lo, refined already
+				ns = nfin;
+				sp = pos;
+				whole = true;
+			} else {
+				if (r == 0) break;
+				ns = r;
+				sp = 0;
+				lo = (uint32_t)(sel[r - 1] >> 32) + 1u;  // finite keys < KEY_INF: no wrap
+			}
+		}
 		if (mode == 1 && cnt >= k) {
-			const float lbn = fkey_inv((uint32_t)(keys[pos] >> 32));
+			const float lbn = fkey_inv((uint32_t)(arr[sp] >> 32));
 			if (lbn > nextafterf(dk, F_INF)) break;  // NaN dk: never (uncertified below)
 		}
-		const int nr = min(PR_CHUNK, limit - pos);
-		// wave w refines candidates pos + w*8 .. (all its loads in flight together)
+		const int nr = min(min(PR_CHUNK, limit - pos), ns - sp);
+		// wave w refines candidates sp + w*8 .. (all its loads in flight together)
 		{
 			uint32_t sl[PR_PER_WAVE];
 			const int b0 = w * PR_PER_WAVE, nv = max(0, min(PR_PER_WAVE, nr - b0));
 #pragma unroll
-			for (int r = 0; r < PR_PER_WAVE; ++r) sl[r] = r < nv ? (uint32_t)keys[pos + b0 + r] : 0u;
+			for (int r = 0; r < PR_PER_WAVE; ++r) sl[r] = r < nv ? (uint32_t)arr[sp + b0 + r] : 0u;
 			float d[PR_PER_WAVE];
 			if (nv > 0) exact_distance_multi<METRIC, T, PR_PER_WAVE>(X, ld, sl, nv, qrow, dim, lane, d);
 			if (lane < nv) {
@@ -2464,6 +2612,7 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 			const float di = cd[cur][i];
 			const int64_t li = cl[cur][i];
 			int rank = 0;
+#pragma unroll 8
 			for (int j = 0; j < m; ++j) rank += hit_less(cd[cur][j], cl[cur][j], di, li) ? 1 : 0;
 			if (rank < k) {
 				cd[cur ^ 1][rank] = di;
@@ -2475,6 +2624,7 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 		cnt = min(m, k);
 		dk = cnt >= k ? cd[cur][k - 1] : F_INF;
 		pos += nr;
+		sp += nr;
 	}
 	if (mode == 0) {
 		if (t == 0) {
@@ -2490,9 +2640,16 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 		outD[(int64_t)q * k + i] = i < cnt ? cd[cur][i] : __builtin_nanf("");
 	}
 	if (t == 0) {
-		// every row not refined has LB >= cut: the pool's next bound, tau for the rest
-		float cutv = pos < n ? fkey_inv((uint32_t)(keys[pos] >> 32)) : F_INF;
-		if (pos >= n && s_nnan == 0 && total <= (unsigned)PR_CAP) cutv = F_INF;
+		// every row not refined has LB >= cut: the next bound in order (a finite
+		// one, else the smallest non-finite), +inf when the pool is exhausted;
+		// tau for the rows outside the pool
+		float cutv;
+		if (sp < ns)
+			cutv = fkey_inv((uint32_t)(arr[sp] >> 32));
+		else if (n > nfin)
+			cutv = fkey_inv(s_knf);
+		else
+			cutv = F_INF;
 		if (ftau < cutv) cutv = ftau;
 		if (s_over || s_nnan > 0) cutv = -F_INF;
 		bool ok;

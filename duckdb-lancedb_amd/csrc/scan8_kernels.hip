@@ -58,28 +58,32 @@ static_assert(-(1 << 24) - LIVE_MAX > GLO, "a live row (acc >= -2^24 - LIVE_MAX)
 
 
 // row part: an integer Bi <= alpha * W (exact), in [0, LIVE_MAX]; BIG for a dead
-// row (+inf) or a NaN bound (never passes, as in scan_kernel)
+// row (+inf) or a NaN bound (never passes, as in scan_kernel).  Branch-free: the
+// per-block terms are selects, not exec-masked blocks.
 __device__ __forceinline__ int s8_row_part(float alpha, float W) {
-	if (!(alpha < F_INF)) return BIG;
 	float b = alpha * W;                          // alpha >= 0, W >= 0 (NaN: 0 * inf -> 0 below)
 	b = fmaf(-fabsf(b), 0x1p-20f, b) - 1.0f;      // below alpha W despite the two roundings
 	b = fminf(fmaxf(b, 0.0f), (float)LIVE_MAX);   // (fmaxf drops a NaN)
-	return (int)b;
+	return alpha < F_INF ? (int)b : BIG;
+}
+
+// query terms, once per query: qp = (C - tau, A, B, |C| + |tau|) from the
+// query's (S, A, B, C) and tau
+__device__ __forceinline__ float4 s8_query_terms(float4 qa, float tq) {
+	return make_float4(qa.w - tq, qa.y, qa.z, fabsf(qa.w) + fabsf(tq));
 }
 
 // query part: an integer Gi <= (C - tau + xnmax B + uxmax A) W (exact), in
 // [GLO, BIG]; BIG (nothing passes) for a NaN query term or tau (a zero cosine
 // query, a NaN distance in the sample: exact fallback) and for padding queries
 // (tau = -inf); GLO (every live row passes) when it overflows or tau = +inf
-__device__ __forceinline__ int s8_query_part(float4 qa, float tq, float4 ts, float W) {
-	const float cmt = qa.w - tq;
-	if (!(cmt < F_INF)) return BIG;
-	float g = fmaf(ts.y, qa.z, fmaf(ts.z, qa.y, cmt)) * W;
+__device__ __forceinline__ int s8_query_part(float4 qp, float4 ts, float W) {
+	float g = fmaf(ts.y, qp.z, fmaf(ts.z, qp.y, qp.x)) * W;
 	// f32 evaluation error of the four terms (a few units of 2^-24 of their magnitudes)
-	const float E = (fabsf(qa.w) + fabsf(tq) + ts.y * fabsf(qa.z) + ts.z * fabsf(qa.y)) * W * 0x1p-20f + 1.0f;
+	const float E = (qp.w + ts.y * fabsf(qp.z) + ts.z * fabsf(qp.y)) * W * 0x1p-20f + 1.0f;
 	g = g - E;
-	if (!(fabsf(g) < F_INF)) return GLO;
-	return (int)floorf(fminf(fmaxf(g, (float)GLO), (float)BIG));
+	const int r = fabsf(g) < F_INF ? (int)floorf(fminf(fmaxf(g, (float)GLO), (float)BIG)) : GLO;
+	return qp.x < F_INF ? r : BIG;
 }
 
 template <int KS, int D, int RB>
@@ -96,8 +100,8 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 	__shared__ __attribute__((aligned(16))) uint8_t smem[LDS8];
 	uint8_t *QL = smem;
 	float4 *QA = reinterpret_cast<float4 *>(smem + QH * P);
-	float *TAU = reinterpret_cast<float *>(QA + QH);
-	unsigned *CNT = reinterpret_cast<unsigned *>(TAU + QH);
+	float4 *QP = QA + QH;  // s8_query_terms of each query
+	unsigned *CNT = reinterpret_cast<unsigned *>(QP + QH);
 	uint2 *LIST = reinterpret_cast<uint2 *>(CNT + QH);                 // [NW][list_cap] (s, slot)
 	uint8_t *LISTQ = reinterpret_cast<uint8_t *>(LIST + NW * list_cap);  // [NW][list_cap] local query
 
@@ -135,8 +139,9 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 	}
 	if (tid < QH) {
 		const int q = qb + tid;
-		QA[tid] = qaux[q];
-		TAU[tid] = q < nq ? tau[q] : -F_INF;
+		const float4 qa = qaux[q];
+		QA[tid] = qa;
+		QP[tid] = s8_query_terms(qa, q < nq ? tau[q] : -F_INF);
 		CNT[tid] = 0u;
 	}
 	__syncthreads();
@@ -169,28 +174,33 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 	};
 
 	if (my_tiles > 0) {
-		// this lane's A rows: WR w + 16 rb + lr of each tile, k bytes 64 j + 16 lg.
-		// Address = uniform tile base (SGPRs) + per-lane offset + immediate: no
-		// VALU in the k-loop (a VALU write right after an MFMA may land on one of
-		// its A / B registers while it still reads them: device_common.h)
+		// this lane's A rows: WR w + 16 rb + lr of each tile, k bytes 64 j + 16 lg,
+		// in the k-major tile layout (tiles_to_i8_kernel): a k-step of 16 rows is
+		// 1 KiB contiguous.  Address = uniform tile base + 16 KiB j (SGPRs) + per-lane
+		// offset: no VALU in the k-loop (a VALU write right after an MFMA may land
+		// on one of its A / B registers while it still reads them: device_common.h)
 		uint32_t xo[RB];
 #pragma unroll
-		for (int rb = 0; rb < RB; ++rb) xo[rb] = (uint32_t)((WR * w + 16 * rb + lr) * ld + 16 * lg);
+		for (int rb = 0; rb < RB; ++rb) xo[rb] = (uint32_t)((WR * w + 16 * rb + lr) * 64 + 16 * lg);
 		auto xtile = [&](int b) -> const int8_t * {
 			const int bb = b < my_tiles ? b : my_tiles - 1;  // past the end: the last block again (unused)
 			return Xq + (pr + (int64_t)bb * NP) * SCAN_BR * (int64_t)ld;
 		};
 		auto xload = [&](const int8_t *tb, int j, int rb) -> i32x4 {
-			return *reinterpret_cast<const i32x4 *>(tb + xo[rb] + 64 * j);
+			return *reinterpret_cast<const i32x4 *>(tb + (int64_t)j * I8_CHUNK_STRIDE + xo[rb]);
 		};
 		// row terms of block b: alpha of this lane's accumulator rows (16 rb + 4 lg + i) and the tile's terms
+		// (the tile terms by a vector load: a scalar load in flight forces
+		// lgkmcnt(0) (SMEM returns out of order) at the block's first LDS wait)
+		uint32_t vz;
+		asm volatile("v_mov_b32 %0, 0" : "=v"(vz));  // a zero the compiler cannot see is uniform
 		auto aload = [&](int b, float4 (&a)[RB], float4 &ts) {
 			const int bb = b < my_tiles ? b : my_tiles - 1;
 			const int64_t tile = pr + (int64_t)bb * NP;
 			const float *A = reinterpret_cast<const float *>(aux8) + (tile << 10) + WR * w + 4 * lg;
 #pragma unroll
 			for (int rb = 0; rb < RB; ++rb) a[rb] = *reinterpret_cast<const float4 *>(A + 16 * rb);
-			ts = tstat[tile];
+			ts = tstat[tile + vz];
 		};
 		// B fragment of query block u, k-step j: query 16u + lr, logical chunk 4j + lg
 		// (two base registers per j & 3 keep every offset an immediate below 64 KiB)
@@ -205,15 +215,27 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 			return *reinterpret_cast<const i32x4 *>(QL + qo[u >> 2][j & 3] + 16 * (u & 3) * P + 256 * (j >> 2));
 		};
 
+		// the query terms of queries lane and lane + 64 (this lane's query parts,
+		// handed to the accumulator lanes of column 16 u + lr by ds_bpermute)
+		const float4 qp0 = QP[lane], qp1 = QP[lane + 64];
 		float4 an[RB], tn;
 		aload(0, an, tn);
+		// complete on the entry path: the block loop carries an[] as plain copies,
+		// and a pending load merged into its header made the waitcnt pass drain
+		// every in-flight ring load at each block start
+		__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (gfx9 encoding: expcnt 7, lgkmcnt 15 = no wait)
 		i32x4 xa[D][RB];
 		{
+			// issued in ring order, as the block loop refills it: the waitcnt pass
+			// merges this path into the loop header, and a reordered entry (slot 0
+			// youngest) made it wait for every ring load at each block's first MFMA
 			const int8_t *tb = xtile(0);
 #pragma unroll
-			for (int j = 0; j < D; ++j)
+			for (int j = 0; j < D; ++j) {
 #pragma unroll
 				for (int rb = 0; rb < RB; ++rb) xa[j][rb] = xload(tb, j, rb);
+				__builtin_amdgcn_sched_barrier(0);
+			}
 		}
 		// query fragments, double-buffered: k-step j + 1's are read while k-step j multiplies
 		i32x4 bq[2][8];
@@ -236,8 +258,11 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 				bias[rb][3] = -s8_row_part(al[rb].w, W);
 			}
 			int gi[8];
+			{
+				const int g0 = s8_query_part(qp0, ts, W), g1 = s8_query_part(qp1, ts, W);
 #pragma unroll
-			for (int u = 0; u < 8; ++u) gi[u] = s8_query_part(QA[16 * u + lr], TAU[16 * u + lr], ts, W);
+				for (int u = 0; u < 8; ++u) gi[u] = __builtin_amdgcn_ds_bpermute(4 * ((16 * u + lr) & 63), u < 4 ? g0 : g1);
+			}
 
 			// accumulators start at -Bi (copies, then every MFMA accumulates in place:
 			// a bias operand shared by 8 MFMAs made the compiler rename them per k-step)
@@ -338,7 +363,7 @@ int scan8_segments(int64_t n_tiles) { return s8_groups(n_tiles); }
 
 static int s8_list_cap(int ld, int nw) {
 	const int P = (ld + 255) / 256 * 256;
-	const int room = LDS8 - QH * P - QH * 24;
+	const int room = LDS8 - QH * P - QH * 36;  // QA, QP, CNT
 	return std::min(1024, room / (nw * 9) / 64 * 64);
 }
 
