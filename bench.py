@@ -97,6 +97,11 @@ def parse():
     ap.add_argument("--pq-scan", dest="pq_scan", choices=["fast", "exact_lut"], default=None,
                     help="IVF_PQ: list-major 8-bit-LUT scan or the f32-LUT query-major scan (option pq_scan)")
     ap.add_argument("--refine-sweep", default="1,10,50", help="IVF_PQ: refine factors of the recall sweep")
+    ap.add_argument("--api", choices=["device", "host_batch", "per_call"], default="device",
+                    help="flat configs, one GPU: device = lance_hip_search_device on resident queries (a step = the "
+                         "batch); host_batch = lance_detached_search_batch on host buffers (H2D queries + D2H results "
+                         "inside the step); per_call = one lance_detached_search per query, the DuckDB call pattern "
+                         "(lance_search.cpp:73-74; a step = one query)")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="extra index option (lance_hip_set_option), repeatable, e.g. --opt scan_i8=off")
     a = ap.parse_args()
@@ -301,7 +306,18 @@ def main_ivf(a):
                              hip_device_merge(L), label_offset=s0, dist=dist, world=world)
     torch.cuda.synchronize()
 
+    if a.api != "device" and world > 1:
+        raise SystemExit("--api host_batch / per_call: one GPU (the host C-ABI is unsharded)")
+    Qh_api = Q.cpu().numpy() if a.api != "device" else None
+    call_i = [0]
+
     def step():
+        if a.api == "host_batch":
+            return lance_hip.LanceDetachedSearchBatch(h, Qh_api, K)
+        if a.api == "per_call":
+            i = call_i[0] % BG
+            call_i[0] += 1
+            return lance_hip.LanceDetachedSearch(h, Qh_api[i], D, K)
         return searcher.search(Q, K, reuse_outputs=True)
 
     for _ in range(a.warmup):
@@ -555,7 +571,18 @@ def main():
                              world=world)
     torch.cuda.synchronize()
 
+    if a.api != "device" and world > 1:
+        raise SystemExit("--api host_batch / per_call: one GPU (the host C-ABI is unsharded)")
+    Qh_api = Q.cpu().numpy() if a.api != "device" else None
+    call_i = [0]
+
     def step():
+        if a.api == "host_batch":
+            return lance_hip.LanceDetachedSearchBatch(h, Qh_api, K)
+        if a.api == "per_call":
+            i = call_i[0] % BG
+            call_i[0] += 1
+            return lance_hip.LanceDetachedSearch(h, Qh_api[i], D, K)
         return searcher.search(Q, K, reuse_outputs=True)
 
     for _ in range(a.warmup):
@@ -563,11 +590,15 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
+    call_i[0] = 0  # per_call: the timed calls start at query 0 (the recall subset below)
     t0 = time.perf_counter()
     marks = []
+    per_call_l = []
     for _ in range(a.steps):
         res = step()
         marks.append(time.perf_counter())
+        if a.api == "per_call" and len(per_call_l) < BG:
+            per_call_l.append(res[0])
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -587,8 +618,14 @@ def main():
     torch.cuda.synchronize()
     kt = lance_hip.LanceHipKernelTimes(h)
     lance_hip.LanceHipSetOption(h, "time_kernels", "0")
-    res_l = res[0].cpu().numpy()
-    res_d = res[1].cpu().numpy()
+    if a.api == "device":
+        res_l = res[0].cpu().numpy()
+        res_d = res[1].cpu().numpy()
+    elif a.api == "host_batch":
+        res_l, res_d = res[0], res[1]
+    else:  # per call: the results of the first calls, one query each
+        res_l = np.stack(per_call_l)
+        res_d = None
 
     # ---- recall@10 vs exact (CPU oracle, float64) on a query subset ----------
     recall = None
@@ -606,13 +643,14 @@ def main():
             Xh[lo:hi] = Xr.cpu().numpy()
             del Xr
         Qh = Q.cpu().numpy()
-        nr = min(a.recall_queries or BG, BG)
+        nr = min(a.recall_queries or BG, BG, len(res_l))
         nthreads = cpu_threads(a)
         el, ed, _ = c_oracle.flat_search_batch(Xh, Qh[:nr], K, a.metric, acc64=True, nthreads=nthreads)
         recall = flat_knn.recall_at_k(res_l[:nr], el, min(10, K))
         recall_k = flat_knn.recall_at_k(res_l[:nr], el, K)
         exact_ids = bool((res_l[:nr] == el).all())
-        max_rel = float(np.max(np.abs(res_d[:nr] - ed) / np.maximum(np.abs(ed), 1e-30)))
+        max_rel = (float(np.max(np.abs(res_d[:nr] - ed) / np.maximum(np.abs(ed), 1e-30)))
+                   if res_d is not None else None)
         if world == 1 and not a.no_cpu_baseline:
             # bounded sample: one query per call (the reference API, lance_search.cpp:73-74)
             done, t_cpu0 = 0, time.perf_counter()
@@ -643,7 +681,7 @@ def main():
 
     if rank == 0:
         ms_step = 1000.0 * t / a.steps
-        value = BG * a.steps / t
+        value = (1 if a.api == "per_call" else BG) * a.steps / t
         roof = None
         if kt["scan_launches"] > 0:
             ld = ((D + 63) // 64) * 64
@@ -676,6 +714,8 @@ def main():
                     "kernel": f"{kt['scan_kernel']}<{kname},append,{xname}>",
                     "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(bytes_launch),
                     "mfma_tflops": round(mfma_tfs, 1), "mfma_frac": round(mfma_tfs / mfma_peak, 4)})
+        api_note = {"device": "", "host_batch": ", lance_detached_search_batch on host buffers (H2D + D2H timed)",
+                    "per_call": ", one lance_detached_search per query (host buffers; the DuckDB call pattern)"}[a.api]
         if a.config == "c2":
             metric_name = "kNN queries/sec + recall@10, 1Mx768 f32 flat; GB/s vs HBM roofline"
         elif a.config == "nstar":
@@ -697,7 +737,9 @@ def main():
             "dtype": a.storage,
             "data": "synthetic N(0,1) base (seeded torch Philox), independent N(0,1) queries"
                     + (", rows and queries L2-normalized; base stored as bf16 (RNE)" if a.config == "c3" else ""),
-            "config": {"workload": f"{a.config.upper()} flat {a.metric} {N}x{D} {a.storage} k={K} query-batch={BG}",
+            "config": {"workload": f"{a.config.upper()} flat {a.metric} {N}x{D} {a.storage} k={K} "
+                                   f"query-batch={1 if a.api == 'per_call' else BG}{api_note}",
+                       "api": a.api,
                        "n": N, "dim": D, "k": K, "global_batch": BG, "batch_per_gpu": B, "metric": a.metric, "storage": a.storage,
                        "parallelism": f"rowshard{world}", "scan_copy": a.scan_copy,
                        **({"options": a.opt} if a.opt else {})},

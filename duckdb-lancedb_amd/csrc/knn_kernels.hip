@@ -2291,18 +2291,21 @@ void launch_finalize(const StoreView &s, const uint32_t *cand_slot, const int *c
 // pool_refine: select + refine + finalize of a threshold pass in ONE launch,
 // refining only as far as the certificate needs.  One 512-thread workgroup
 // per query gathers the query's segments (every row with LB <= tau, from the
-// append or sample scan) into LDS as (orderedkey(LB), slot), sorts them by
-// (LB, slot), then refines them IN BOUND ORDER, 64 per round (8 per wave,
-// exact f64 distances as refine_kernel computes them), merging each round into
-// the running top-k by (distance, label):
-//   final mode: stop as soon as the next bound exceeds nextafter(d_k) (every
-//   row left, in the pool or not, then has LB > d_k: certified as finalize
-//   does, cut = min(next bound, tau)); the refined count adapts to how many
-//   bounds lie below d_k instead of a fixed top-M (the int8 bounds put ~60-250
-//   rows there at 1M-10M rows x 768);
-//   tau mode (the sample pass): refine the m_tau smallest bounds, tau = their
-//   k-th smallest exact distance (+inf when fewer, NaN when any is NaN), the
-//   value refine_tau_kernel computes.
+// append or sample scan) into LDS as (orderedkey(LB), slot) and refines it in
+// threshold chunks, no sort: a chunk is every unrefined bound up to a key
+// picked from a histogram of the pool's keys, refined 128 per round (16 per
+// wave, exact f64 distances as refine_kernel computes them) and merged into the
+// running top-k by (distance, label):
+//   final mode: the first chunk holds the ~PR_R smallest bounds; each later one
+//   every unrefined bound <= nextafter(d_k) (d_k of the top so far: it only
+//   falls, so each row a bound-order refine would take is taken), until none
+//   is left; then every unrefined row, in the pool or not, has LB > d_k:
+//   certified as finalize does, cut = min(smallest unrefined bound, tau) (the
+//   int8 bounds put ~60-250 rows below d_k at 1M-10M rows x 768);
+//   tau mode (the sample pass): refine at least the m_tau smallest bounds (a
+//   whole chunk), tau = the k-th smallest exact distance among them (+inf when
+//   fewer than k, NaN when any is NaN): an upper bound on the k-th nearest
+//   distance, never above refine_tau_kernel's from the m_tau smallest alone.
 // A segment that overflowed, a pool past PR_CAP or a NaN bound fails the
 // certificate (cut = -inf), as select_kernel's does; the rows refined still
 // give the rerun a tau.  Returns the refined count and the pool size.
@@ -2310,7 +2313,7 @@ void launch_finalize(const StoreView &s, const uint32_t *cand_slot, const int *c
 constexpr int PR_THREADS = 512;
 constexpr int PR_WAVES = PR_THREADS / 64;
 constexpr int PR_CAP = 16384;       // pool entries held in LDS
-constexpr int PR_PER_WAVE = 8;      // candidates per wave and round
+constexpr int PR_PER_WAVE = 16;     // candidates per wave and round
 constexpr int PR_CHUNK = PR_WAVES * PR_PER_WAVE;
 constexpr int PR_MAXK = MAX_CAND;   // k of the fast path (k + 8 <= MAX_CAND)
 
@@ -2379,9 +2382,9 @@ __device__ __forceinline__ void pr_bitonic(uint64_t *a, int P) {
 	}
 }
 
-constexpr int PR_SEL = 1024;  // chunk capacity: the smallest bounds, sorted
+constexpr int PR_SEL = 1024;  // chunk capacity
 constexpr int PR_HB = 1024;   // histogram bins of a chunk selection
-constexpr int PR_R = 256;     // chunk target of the final pass
+constexpr int PR_R = 128;     // first chunk of the final pass (one round)
 
 template <int METRIC, typename T>
 __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
@@ -2389,16 +2392,30 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
     const float *__restrict__ tau, const T *__restrict__ X, int ld, int dim, const float *__restrict__ Qf,
     const int64_t *__restrict__ labels, int k, int mode, int m_tau, int64_t live, float *__restrict__ tau_out,
     int64_t *__restrict__ outL, float *__restrict__ outD, int *__restrict__ outC, int *__restrict__ cert,
-    int *__restrict__ refined, int *__restrict__ pool_total) {
+    int *__restrict__ refined, int *__restrict__ pool_total, int prof_on) {
 	__shared__ uint64_t keys[PR_CAP];
-	__shared__ uint64_t sel[PR_SEL];
+	__shared__ uint32_t sel[PR_SEL];  // slots of the chunk being refined
 	__shared__ unsigned hist[PR_HB];
 	__shared__ float cd[2][PR_MAXK + PR_CHUNK];  // running top-k (double-buffered) + the round's distances
 	__shared__ int64_t cl[2][PR_MAXK + PR_CHUNK];
 	__shared__ unsigned sh[PR_WAVES];
 	__shared__ int s_over, s_nnan, s_dnan;
-	__shared__ unsigned s_nfin, s_knf, s_kmin, s_kmax, s_bstar, s_cum, s_below, s_ns;
+	__shared__ unsigned s_nfin, s_knf, s_kmin, s_kmax, s_bstar, s_cum, s_below, s_ns, s_hi;
 	const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+#ifdef LHIP_PR_PROF
+	// phase stamps (diagnostic build, one designated launch): thread 0 prints
+	// the cycles of each phase for the first queries and any slow workgroup
+	uint64_t stamp[24];
+	int nst = 0;
+	auto mark = [&]() {
+		if (nst < 24) stamp[nst++] = __builtin_amdgcn_s_memtime();
+	};
+	mark();
+#else
+	auto mark = [&]() {};
+#endif
+	// candidates per wave and round (cosine: three f64 sums per row, half as many)
+	constexpr int PW = METRIC == METRIC_COSINE ? PR_PER_WAVE / 2 : PR_PER_WAVE, CH = PR_WAVES * PW;
 	if (t == 0) {
 		s_over = 0;
 		s_nnan = 0;
@@ -2432,6 +2449,7 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 		}
 	}
 	__syncthreads();
+	mark();
 	if (t == 0 && total > (unsigned)PR_CAP) s_over = 1;
 	// finite bounds (key < KEY_INF), NaN bounds, the smallest non-finite key
 	{
@@ -2455,24 +2473,29 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 		}
 	}
 	__syncthreads();
+	mark();
 	const int nfin = (int)s_nfin;
 	const float ftau = tau ? tau[q] : F_INF;
 	const float *qrow = Qf + (int64_t)q * ld;
 
-	// next chunk: the finite keys >= lo up to a histogram bin holding the R-th
-	// smallest (all keys equal to the chunk's last are in it), sorted into sel.
-	// Returns its size (0: none left), -1 when > PR_SEL keys share one value.
-	auto next_chunk = [&](unsigned lo, int R) -> int {
+	// next chunk: the finite keys in [lo, hi_goal] up to a histogram bin holding
+	// the R-th smallest of them (all of them when fewer), at most PR_SEL, slots
+	// into sel.  Returns its size (0: none in the range) and its largest key in
+	// s_hi (every key in [lo, s_hi] is in it); -1 when more than PR_SEL keys share
+	// one value.
+	auto next_chunk = [&](unsigned lo, unsigned hi_goal, int R) -> int {
 		if (t == 0) {
 			s_kmin = 0xFFFFFFFFu;
 			s_kmax = 0;
+			s_ns = 0;
+			s_hi = 0;
 		}
 		__syncthreads();
 		{
 			unsigned kmn = 0xFFFFFFFFu, kmx = 0;
 			for (int i = t; i < n; i += PR_THREADS) {
 				const uint32_t kk = (uint32_t)(keys[i] >> 32);
-				if (kk >= lo && kk < KEY_INF) {
+				if (kk >= lo && kk <= hi_goal && kk < KEY_INF) {
 					kmn = min(kmn, kk);
 					kmx = max(kmx, kk);
 				}
@@ -2530,101 +2553,147 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 			if (shift == 0) return -1;  // > PR_SEL keys of one value
 			// everything up to b* is inside b*: histogram that bin alone
 			const unsigned nlo = kmin + (bstar << shift);
-			const unsigned nhi = nlo + ((1u << shift) - 1u);
 			kmin = nlo;
-			kmax = min(kmax, nhi);
+			kmax = min(kmax, nlo + ((1u << shift) - 1u));
 			__syncthreads();
 		}
-		if (t == 0) s_ns = 0;
-		__syncthreads();
 		for (int i = t; i < n; i += PR_THREADS) {
 			const uint64_t e = keys[i];
 			const uint32_t kk = (uint32_t)(e >> 32);
-			if (kk >= kmin && kk <= kmax && ((kk - kmin) >> shift) <= bstar) sel[atomicAdd(&s_ns, 1u)] = e;
+			if (kk >= kmin && kk <= kmax && ((kk - kmin) >> shift) <= bstar) {
+				sel[atomicAdd(&s_ns, 1u)] = (uint32_t)e;
+				atomicMax(&s_hi, kk);
+			}
 		}
 		__syncthreads();
-		const int ns = (int)s_ns;
-		int P = 64;
-		while (P < ns) P <<= 1;
-		for (int i = ns + t; i < P; i += PR_THREADS) sel[i] = ~0ull;
-		__syncthreads();
-		pr_bitonic(sel, P);
-		return ns;
+		return (int)s_ns;
 	};
 
-	// ---- refine in bound order ------------------------------------------------
-	const int limit = mode == 0 ? min(nfin, m_tau) : nfin;
+	// ---- refine in threshold chunks -------------------------------------------
 	int cnt = 0, cur = 0, pos = 0;  // top entries held, buffer holding them, candidates refined
 	float dk = F_INF;               // k-th distance of the top (+inf while fewer than k)
-	const uint64_t *arr = sel;      // the chunk being refined: arr[sp, ns)
-	int ns = 0, sp = 0;
-	unsigned lo = 0;                // keys < lo are refined
-	bool whole = false;             // the whole pool sorted (keys of one value past PR_SEL)
-	while (pos < limit) {
-		if (sp == ns) {
-			if (whole) break;
-			const int r = next_chunk(lo, mode == 0 ? limit - pos : PR_R);
-			if (r < 0) {
-				int P = 64;
-				while (P < n) P <<= 1;
-				for (int i = n + t; i < P; i += PR_THREADS) keys[i] = ~0ull;
-				__syncthreads();
-				pr_bitonic(keys, P);
-				arr = keys;  // the first pos entries are the keys < lo, refined already
-				ns = nfin;
-				sp = pos;
-				whole = true;
-			} else {
-				if (r == 0) break;
-				ns = r;
-				sp = 0;
-				lo = (uint32_t)(sel[r - 1] >> 32) + 1u;  // finite keys < KEY_INF: no wrap
+	unsigned lo = 0;                // the finite keys < lo are refined, those >= lo are not
+	bool whole = false;             // > PR_SEL bounds of one value: the rest by the whole-pool sort
+	const uint64_t *order = nullptr;  // (whole) the sorted pool
+	for (;;) {
+		int ns;
+		const uint32_t *slots = sel;
+		if (mode == 0) {
+			if (pos >= min(nfin, m_tau)) break;
+			ns = next_chunk(lo, KEY_INF - 1u, m_tau - pos);
+		} else {
+			// the bounds a bound-order refine could still take: <= nextafter(d_k)
+			unsigned hi_goal = KEY_INF - 1u;
+			if (cnt >= k && !__builtin_isnan(dk)) {
+				const uint32_t kt = fkey(nextafterf(dk, F_INF));
+				if (kt < lo) break;
+				hi_goal = min(kt, KEY_INF - 1u);
 			}
+			ns = next_chunk(lo, hi_goal, cnt >= k ? PR_SEL : PR_R);
 		}
-		if (mode == 1 && cnt >= k) {
-			const float lbn = fkey_inv((uint32_t)(arr[sp] >> 32));
-			if (lbn > nextafterf(dk, F_INF)) break;  // NaN dk: never (uncertified below)
+		mark();
+		if (ns == 0) break;
+		if (ns < 0) {
+			whole = true;
+			break;
 		}
-		const int nr = min(min(PR_CHUNK, limit - pos), ns - sp);
-		// wave w refines candidates sp + w*8 .. (all its loads in flight together)
-		{
-			uint32_t sl[PR_PER_WAVE];
-			const int b0 = w * PR_PER_WAVE, nv = max(0, min(PR_PER_WAVE, nr - b0));
+		lo = s_hi + 1u;  // (finite keys < KEY_INF: no wrap)
+		for (int sp = 0; sp < ns; sp += CH) {
+			const int nr = min(CH, ns - sp);
+			// wave w refines candidates sp + w*PW .. (all its loads in flight together)
+			{
+				uint32_t sl[PW];
+				const int b0 = w * PW, nv = max(0, min(PW, nr - b0));
 #pragma unroll
-			for (int r = 0; r < PR_PER_WAVE; ++r) sl[r] = r < nv ? (uint32_t)arr[sp + b0 + r] : 0u;
-			float d[PR_PER_WAVE];
-			if (nv > 0) exact_distance_multi<METRIC, T, PR_PER_WAVE>(X, ld, sl, nv, qrow, dim, lane, d);
-			if (lane < nv) {
-				float dv = d[0];
-				uint32_t sv = sl[0];
+				for (int r = 0; r < PW; ++r) sl[r] = r < nv ? slots[sp + b0 + r] : 0u;
+				float d[PW];
+				if (nv > 0) exact_distance_multi<METRIC, T, PW>(X, ld, sl, nv, qrow, dim, lane, d);
+				if (lane < nv) {
+					float dv = d[0];
+					uint32_t sv = sl[0];
 #pragma unroll
-				for (int r = 1; r < PR_PER_WAVE; ++r)
-					if (lane == r) dv = d[r], sv = sl[r];
-				cd[cur][cnt + b0 + lane] = dv;
-				cl[cur][cnt + b0 + lane] = labels[sv];
-				if (__builtin_isnan(dv)) s_dnan = 1;
+					for (int r = 1; r < PW; ++r)
+						if (lane == r) dv = d[r], sv = sl[r];
+					cd[cur][cnt + b0 + lane] = dv;
+					cl[cur][cnt + b0 + lane] = labels[sv];
+					if (__builtin_isnan(dv)) s_dnan = 1;
+				}
 			}
-		}
-		__syncthreads();
-		// merge: rank of every entry (top so far + this round) by (distance, label)
-		const int m = cnt + nr;
-		for (int i = t; i < m; i += PR_THREADS) {
-			const float di = cd[cur][i];
-			const int64_t li = cl[cur][i];
-			int rank = 0;
+			__syncthreads();
+			// merge: rank of every entry (top so far + this round) by (distance, label)
+			const int m = cnt + nr;
+			for (int i = t; i < m; i += PR_THREADS) {
+				const float di = cd[cur][i];
+				const int64_t li = cl[cur][i];
+				int rank = 0;
 #pragma unroll 8
-			for (int j = 0; j < m; ++j) rank += hit_less(cd[cur][j], cl[cur][j], di, li) ? 1 : 0;
-			if (rank < k) {
-				cd[cur ^ 1][rank] = di;
-				cl[cur ^ 1][rank] = li;
+				for (int j = 0; j < m; ++j) rank += hit_less(cd[cur][j], cl[cur][j], di, li) ? 1 : 0;
+				if (rank < k) {
+					cd[cur ^ 1][rank] = di;
+					cl[cur ^ 1][rank] = li;
+				}
 			}
+			__syncthreads();
+			cur ^= 1;
+			cnt = min(m, k);
+			dk = cnt >= k ? cd[cur][k - 1] : F_INF;
+			pos += nr;
+			mark();
 		}
+	}
+	if (whole) {
+		// > PR_SEL bounds of one value (duplicate rows): the rest in bound order
+		// from the sorted pool, as a bound-order refine takes them
+		int P = 64;
+		while (P < n) P <<= 1;
+		for (int i = n + t; i < P; i += PR_THREADS) keys[i] = ~0ull;
 		__syncthreads();
-		cur ^= 1;
-		cnt = min(m, k);
-		dk = cnt >= k ? cd[cur][k - 1] : F_INF;
-		pos += nr;
-		sp += nr;
+		pr_bitonic(keys, P);
+		order = keys;
+		int sp = pos;  // the first pos entries of the sorted pool are the keys < lo
+		const int limit = mode == 0 ? min(nfin, m_tau) : nfin;
+		while (sp < limit) {
+			if (mode == 1 && cnt >= k && fkey_inv((uint32_t)(order[sp] >> 32)) > nextafterf(dk, F_INF)) break;
+			const int nr = min(CH, limit - sp);
+			{
+				uint32_t sl[PW];
+				const int b0 = w * PW, nv = max(0, min(PW, nr - b0));
+#pragma unroll
+				for (int r = 0; r < PW; ++r) sl[r] = r < nv ? (uint32_t)order[sp + b0 + r] : 0u;
+				float d[PW];
+				if (nv > 0) exact_distance_multi<METRIC, T, PW>(X, ld, sl, nv, qrow, dim, lane, d);
+				if (lane < nv) {
+					float dv = d[0];
+					uint32_t sv = sl[0];
+#pragma unroll
+					for (int r = 1; r < PW; ++r)
+						if (lane == r) dv = d[r], sv = sl[r];
+					cd[cur][cnt + b0 + lane] = dv;
+					cl[cur][cnt + b0 + lane] = labels[sv];
+					if (__builtin_isnan(dv)) s_dnan = 1;
+				}
+			}
+			__syncthreads();
+			const int m = cnt + nr;
+			for (int i = t; i < m; i += PR_THREADS) {
+				const float di = cd[cur][i];
+				const int64_t li = cl[cur][i];
+				int rank = 0;
+#pragma unroll 8
+				for (int j = 0; j < m; ++j) rank += hit_less(cd[cur][j], cl[cur][j], di, li) ? 1 : 0;
+				if (rank < k) {
+					cd[cur ^ 1][rank] = di;
+					cl[cur ^ 1][rank] = li;
+				}
+			}
+			__syncthreads();
+			cur ^= 1;
+			cnt = min(m, k);
+			dk = cnt >= k ? cd[cur][k - 1] : F_INF;
+			sp += nr;
+			pos += nr;
+		}
+		lo = sp < nfin ? (uint32_t)(order[sp] >> 32) : KEY_INF;  // the next bound, as the smallest unrefined key
 	}
 	if (mode == 0) {
 		if (t == 0) {
@@ -2635,17 +2704,33 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 		return;
 	}
 	// ---- outputs and the certificate -----------------------------------------
+	// the smallest unrefined finite bound (every finite key < lo is refined)
+	if (t == 0) s_kmin = 0xFFFFFFFFu;
+	__syncthreads();
+	if (!whole) {
+		unsigned kmn = 0xFFFFFFFFu;
+		for (int i = t; i < n; i += PR_THREADS) {
+			const uint32_t kk = (uint32_t)(keys[i] >> 32);
+			if (kk >= lo && kk < KEY_INF) kmn = min(kmn, kk);
+		}
+#pragma unroll
+		for (int o = 32; o > 0; o >>= 1) kmn = min(kmn, (unsigned)__shfl_xor(kmn, o, 64));
+		if (lane == 0) atomicMin(&s_kmin, kmn);
+	} else if (t == 0 && lo < KEY_INF) {
+		s_kmin = lo;
+	}
 	for (int i = t; i < k; i += PR_THREADS) {
 		outL[(int64_t)q * k + i] = i < cnt ? cl[cur][i] : -1;
 		outD[(int64_t)q * k + i] = i < cnt ? cd[cur][i] : __builtin_nanf("");
 	}
+	__syncthreads();
 	if (t == 0) {
-		// every row not refined has LB >= cut: the next bound in order (a finite
-		// one, else the smallest non-finite), +inf when the pool is exhausted;
-		// tau for the rows outside the pool
+		// every row not refined has LB >= cut: the smallest unrefined bound (a
+		// finite one, else the smallest non-finite), +inf when the pool is
+		// exhausted; tau for the rows outside the pool
 		float cutv;
-		if (sp < ns)
-			cutv = fkey_inv((uint32_t)(arr[sp] >> 32));
+		if (s_kmin != 0xFFFFFFFFu)
+			cutv = fkey_inv(s_kmin);
 		else if (n > nfin)
 			cutv = fkey_inv(s_knf);
 		else
@@ -2660,6 +2745,16 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 		if (live >= 0 && (int64_t)cnt < (live < (int64_t)k ? live : (int64_t)k)) ok = false;
 		outC[q] = cnt;
 		cert[q] = ok ? 1 : 0;
+#ifdef LHIP_PR_PROF
+		mark();
+		if (prof_on && (q < 6 || stamp[nst - 1] - stamp[0] > 60000)) {
+			int d[12];
+			for (int i = 0; i < 12; ++i) d[i] = i + 1 < nst ? (int)(stamp[i + 1] - stamp[i]) : -1;
+			printf("PR q=%d pool=%d refined=%d nst=%d total=%d | %d %d %d %d %d %d %d %d %d %d %d %d\n", q, n, pos, nst,
+			       (int)(stamp[nst - 1] - stamp[0]), d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9], d[10],
+			       d[11]);
+		}
+#endif
 		if (refined) refined[q] = pos;
 		if (pool_total) pool_total[q] = s_over ? -1 : (int)total;
 	}
@@ -2672,10 +2767,12 @@ static void pool_refine_dispatch(const StoreView &s, const QueryView &q, const u
                                  int *pool_total, hipStream_t st) {
 	const T *X = static_cast<const T *>(s.X);
 	const dim3 grid((unsigned)q.nq);
+	static int calls = 0;  // (LHIP_PR_PROF: the 12th final-mode launch of the process prints its phases)
+	const int prof_on = mode == 1 && ++calls == 12;
 #define LHIP_PR(MET)                                                                                                  \
 	pool_refine_kernel<MET, T><<<grid, PR_THREADS, 0, st>>>(seg_pool, seg_cnt, seg_cap, n_seg, q.nq, tau, X, s.ld,   \
 	                                                        s.dim, q.Qf, s.labels, k, mode, m_tau, live, tau_out, L, \
-	                                                        D, C, cert, refined, pool_total)
+	                                                        D, C, cert, refined, pool_total, prof_on)
 	switch (s.metric) {
 	case METRIC_L2: LHIP_PR(METRIC_L2); break;
 	case METRIC_DOT: LHIP_PR(METRIC_DOT); break;

@@ -86,13 +86,17 @@ __device__ __forceinline__ int s8_query_part(float4 qp, float4 ts, float W) {
 	return qp.x < F_INF ? r : BIG;
 }
 
-template <int KS, int D, int RB>
+// ABL (timing ablations, wrong results): bit 0 skips the screen, bit 1 the
+// per-block bound terms (constants instead), bit 2 the appends; bit 3 (a speed
+// option, results exact): s_setprio 2 over the k-loop, 0 over the rest; bit 4:
+// a workgroup barrier per block; bit 5: s_setprio alternating by block parity
+template <int KS, int D, int RB, int ABL = 0>
 __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *__restrict__ Xq, const float4 *__restrict__ aux8,
                                                       const float4 *__restrict__ tstat, int ld,
                                                       const int8_t *__restrict__ Qi, const float4 *__restrict__ qaux,
                                                       int nq, int n_tiles, const float *__restrict__ tau,
                                                       uint2 *__restrict__ seg_pool, int *__restrict__ seg_cnt,
-                                                      int seg_cap, int list_cap) {
+                                                      int seg_cap, int list_cap, int stagger) {
 	static_assert(KS % D == 0 && KS % 2 == 0, "ring slot and fragment buffer of a k-step must be static");
 	constexpr int NW = 16 / RB, T8 = 64 * NW;  // waves: each owns 16 RB rows of every tile
 	constexpr int WR = 16 * RB;                // rows per wave and tile
@@ -152,6 +156,19 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 
 	const int my_tiles = pr < n_tiles ? (n_tiles - 1 - pr) / NP + 1 : 0;
 	int n_list = 0;
+#ifdef LHIP_S8_PROF
+	// diagnostic build: per-wave cycles in each phase of the block loop
+	uint64_t pf_pro = 0, pf_k = 0, pf_scr = 0, pf_app = 0, pf_t = 0;
+	int pf_hitb = 0;
+#define S8_T(acc)                                            \
+	{                                                        \
+		const uint64_t now_ = __builtin_amdgcn_s_memtime(); \
+		acc += now_ - pf_t;                                  \
+		pf_t = now_;                                         \
+	}
+#else
+#define S8_T(acc)
+#endif
 	uint2 *wl = LIST + w * list_cap;
 	uint8_t *wq = LISTQ + w * list_cap;
 	// list -> segment entries: LB as scan_kernel's lower_bound<., SC> evaluates it
@@ -174,6 +191,11 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 	};
 
 	if (my_tiles > 0) {
+		// stagger: the upper half of the waves (the second wave of each SIMD)
+		// starts stagger x 64 cycles late, so one wave's per-block VALU (terms,
+		// screen) runs while the other one multiplies
+		if (w >= NW / 2)
+			for (int z = 0; z < stagger; z += 64) __builtin_amdgcn_s_sleep(64);
 		// this lane's A rows: WR w + 16 rb + lr of each tile, k bytes 64 j + 16 lg,
 		// in the k-major tile layout (tiles_to_i8_kernel): a k-step of 16 rows is
 		// 1 KiB contiguous.  Address = uniform tile base + 16 KiB j (SGPRs) + per-lane
@@ -189,17 +211,17 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 		auto xload = [&](const int8_t *tb, int j, int rb) -> i32x4 {
 			return *reinterpret_cast<const i32x4 *>(tb + (int64_t)j * I8_CHUNK_STRIDE + xo[rb]);
 		};
-		// row terms of block b: alpha of this lane's accumulator rows (16 rb + 4 lg + i) and the tile's terms
+		// row terms of block b: the alpha of ONE of the wave's WR rows per lane (row
+		// lane % WR; its row part is handed to the accumulator lanes of that row by
+		// ds_bpermute: 16 lanes share each accumulator row) and the tile's terms.
 		// (the tile terms by a vector load: a scalar load in flight forces
 		// lgkmcnt(0) (SMEM returns out of order) at the block's first LDS wait)
 		uint32_t vz;
 		asm volatile("v_mov_b32 %0, 0" : "=v"(vz));  // a zero the compiler cannot see is uniform
-		auto aload = [&](int b, float4 (&a)[RB], float4 &ts) {
+		auto aload = [&](int b, float &a, float4 &ts) {
 			const int bb = b < my_tiles ? b : my_tiles - 1;
 			const int64_t tile = pr + (int64_t)bb * NP;
-			const float *A = reinterpret_cast<const float *>(aux8) + (tile << 10) + WR * w + 4 * lg;
-#pragma unroll
-			for (int rb = 0; rb < RB; ++rb) a[rb] = *reinterpret_cast<const float4 *>(A + 16 * rb);
+			a = reinterpret_cast<const float *>(aux8)[(tile << 10) + WR * w + (lane & (WR - 1))];
 			ts = tstat[tile + vz];
 		};
 		// B fragment of query block u, k-step j: query 16u + lr, logical chunk 4j + lg
@@ -218,7 +240,8 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 		// the query terms of queries lane and lane + 64 (this lane's query parts,
 		// handed to the accumulator lanes of column 16 u + lr by ds_bpermute)
 		const float4 qp0 = QP[lane], qp1 = QP[lane + 64];
-		float4 an[RB], tn;
+		float an;
+		float4 tn;
 		aload(0, an, tn);
 		// complete on the entry path: the block loop carries an[] as plain copies,
 		// and a pending load merged into its header made the waitcnt pass drain
@@ -242,23 +265,37 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 #pragma unroll
 		for (int u = 0; u < 8; ++u) bq[0][u] = bload(0, u);
 
+#ifdef LHIP_S8_PROF
+		pf_t = __builtin_amdgcn_s_memtime();
+#endif
 		for (int b = 0; b < my_tiles; ++b) {
-			float4 al[RB];
-#pragma unroll
-			for (int rb = 0; rb < RB; ++rb) al[rb] = an[rb];
+			// the two waves of a SIMD (w, w + NW/2) in step: oldest-first issue
+			// arbitration otherwise lets the lower half run ~40% ahead, and the
+			// upper half ends the launch alone, one wave per SIMD
+			if (ABL & 16) __syncthreads();
+			if (ABL & 32) {
+				if (((b + (w >= NW / 2 ? 1 : 0)) & 1) != 0)
+					__builtin_amdgcn_s_setprio(1);
+				else
+					__builtin_amdgcn_s_setprio(0);
+			}
+			const float al = an;
 			const float4 ts = tn;
 			aload(b + 1, an, tn);
 			const float W = (Sabs > 0.f && ts.x > 0.f) ? 1.0f / (Sabs * ts.x) : 0.f;
 			i32x4 bias[RB];
-#pragma unroll
-			for (int rb = 0; rb < RB; ++rb) {
-				bias[rb][0] = -s8_row_part(al[rb].x, W);
-				bias[rb][1] = -s8_row_part(al[rb].y, W);
-				bias[rb][2] = -s8_row_part(al[rb].z, W);
-				bias[rb][3] = -s8_row_part(al[rb].w, W);
-			}
 			int gi[8];
-			{
+			if (ABL & 2) {
+#pragma unroll
+				for (int rb = 0; rb < RB; ++rb) bias[rb] = i32x4{rb, 1, 2, 3};
+#pragma unroll
+				for (int u = 0; u < 8; ++u) gi[u] = BIG - u;
+			} else {
+				const int bl = -s8_row_part(al, W);  // row lane % WR
+#pragma unroll
+				for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+					for (int i = 0; i < 4; ++i) bias[rb][i] = __builtin_amdgcn_ds_bpermute(4 * (16 * rb + 4 * lg + i), bl);
 				const int g0 = s8_query_part(qp0, ts, W), g1 = s8_query_part(qp1, ts, W);
 #pragma unroll
 				for (int u = 0; u < 8; ++u) gi[u] = __builtin_amdgcn_ds_bpermute(4 * ((16 * u + lr) & 63), u < 4 ? g0 : g1);
@@ -272,6 +309,8 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 #pragma unroll
 				for (int u = 0; u < 8; ++u) acc[rb][u] = bias[rb];
 			const int8_t *tb_cur = xtile(b), *tb_next = xtile(b + 1);
+			S8_T(pf_pro);
+			if (ABL & 8) __builtin_amdgcn_s_setprio(2);  // the k-loop: MFMA issue first on the SIMD
 			__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 			for (int j = 0; j < KS; ++j) {
@@ -291,9 +330,17 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 				__builtin_amdgcn_sched_barrier(0);
 			}
 			mfma_operand_guard();  // the screen's VALU follows the block's last MFMAs
+			S8_T(pf_k);
+			if (ABL & 8) __builtin_amdgcn_s_setprio(0);  // screen, appends, next terms: behind the partner's MFMAs
 
 			// ---- screen: lane bit u = some bound of query 16u + lr passes ----
 			int hitm = 0;
+			if (ABL & 1) {
+				int m = 0;
+#pragma unroll
+				for (int u = 0; u < 8; ++u) m ^= acc[0][u][0];
+				hitm = m == 0x7fffffff ? 1 : 0;  // (keeps the MFMAs alive)
+			} else
 #pragma unroll
 			for (int u = 0; u < 8; ++u) {
 				int m = max(max(acc[0][u][0], acc[0][u][1]), max(acc[0][u][2], acc[0][u][3]));
@@ -302,33 +349,63 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 					m = max(m, max(max(acc[rb][u][0], acc[rb][u][1]), max(acc[rb][u][2], acc[rb][u][3])));
 				hitm |= (m >= gi[u] ? 1 : 0) << u;
 			}
-			if (__builtin_amdgcn_ballot_w64(hitm != 0)) {
+			S8_T(pf_scr);
+#ifdef LHIP_S8_PROF
+			pf_hitb += __builtin_amdgcn_ballot_w64(hitm != 0) ? 1 : 0;
+#endif
+			if (ABL & 4) {
+				if (__builtin_amdgcn_ballot_w64(hitm != 0) == 0x123456789ull) n_list += 1;  // (keeps the screen)
+			} else if (__builtin_amdgcn_ballot_w64(hitm != 0)) {
 				// rare: append every passing (s, slot, query) to the wave's list
 				const uint32_t row0 = (uint32_t)((pr + (int64_t)b * NP) * SCAN_BR) + (uint32_t)(WR * w) + 4u * lg;
 #pragma unroll
 				for (int u = 0; u < 8; ++u) {
 					if (!__builtin_amdgcn_ballot_w64((hitm >> u) & 1)) continue;
+					// this query block's passing bounds (one ballot per accumulator
+					// register), then ONE list-room check: a flush site per u, not per
+					// (rb, i) (64 inlined flushes made the kernel ~4x larger than its
+					// loop).  (A per-lane mask + wave prefix scan instead of the ballots
+					// measured slower: six dependent ds_bpermute per hit block.)
+					uint64_t mk[RB][4];
+					unsigned cu = 0;
 #pragma unroll
 					for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
 						for (int i = 0; i < 4; ++i) {
-							const bool pass = acc[rb][u][i] >= gi[u];
-							const uint64_t mk = __builtin_amdgcn_ballot_w64(pass);
-							if (!mk) continue;
-							const int c = __builtin_popcountll(mk);
-							if (n_list + c > list_cap) flush();
-							if (pass) {
+							mk[rb][i] = __builtin_amdgcn_ballot_w64(acc[rb][u][i] >= gi[u]);
+							cu += (unsigned)__builtin_popcountll(mk[rb][i]);
+						}
+					if (n_list + (int)cu > list_cap) flush();
+					if ((int)cu > list_cap) {
+						// more than the whole list: these queries fail their certificate
+						// (a segment count past seg_cap), never a silent drop
+						if ((hitm >> u) & 1) atomicOr(&CNT[16 * u + lr], 1u << 30);  // sticky: > any seg_cap
+						continue;
+					}
+#pragma unroll
+					for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+						for (int i = 0; i < 4; ++i) {
+							const uint64_t m = mk[rb][i];
+							if (!m) continue;
+							if ((m >> lane) & 1) {
 								const int pos = n_list + (int)__builtin_amdgcn_mbcnt_hi(
-								                             (uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+								                             (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 								wl[pos] = make_uint2((uint32_t)(acc[rb][u][i] - bias[rb][i]), row0 + 16u * rb + (uint32_t)i);
 								wq[pos] = (uint8_t)(16 * u + lr);
 							}
-							n_list += c;
+							n_list += __builtin_popcountll(m);
 						}
 				}
 			}
+			S8_T(pf_app);
 		}
 	}
+#ifdef LHIP_S8_PROF
+	if (b_id < 3 && lane == 0)
+		printf("S8 wg=%d w=%d blocks=%d pro=%d k=%d scr=%d app=%d hitblocks=%d\n", b_id, w, my_tiles, (int)pf_pro,
+		       (int)pf_k, (int)pf_scr, (int)pf_app, pf_hitb);
+#endif
 	if (n_list > 0) flush();
 	__syncthreads();  // every wave's counter updates
 	// segment b_id of every query of the tile: this workgroup's counts for its
@@ -367,21 +444,28 @@ static int s8_list_cap(int ld, int nw) {
 	return std::min(1024, room / (nw * 9) / 64 * 64);
 }
 
-template <int KS, int D, int RB>
+static int g_s8_variant = 0, g_s8_stagger = 0;
+
+template <int KS, int D, int RB, int ABL = 0>
 static void s8_launch(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
                       int seg_cap, int64_t n_tiles, hipStream_t st) {
 	const dim3 grid((unsigned)s8_groups(n_tiles), (unsigned)(q.nq_pad / SCAN_BQ));
 	constexpr int NW = 16 / RB;
-	scan8_kernel<KS, D, RB><<<grid, dim3(64 * NW), 0, st>>>(
+	scan8_kernel<KS, D, RB, ABL><<<grid, dim3(64 * NW), 0, st>>>(
 	    static_cast<const int8_t *>(s.Xscan), s.scan_aux, s.tstat, s.ld, reinterpret_cast<const int8_t *>(q.Qb), q.qaux,
-	    q.nq, (int)n_tiles, tau, seg_pool, seg_cnt, seg_cap, s8_list_cap(s.ld, NW));
+	    q.nq, (int)n_tiles, tau, seg_pool, seg_cnt, seg_cap, s8_list_cap(s.ld, NW), g_s8_stagger);
 }
 
 // geometry of the ld = 768 kernel (development knob, option "scan8_variant"):
 // 16-row blocks per wave (4: four waves, one per SIMD; 2: eight waves) and the
 // register ring depth in 64-deep k-steps
-static int g_s8_variant = 0;
-void scan8_set_variant(int v) { g_s8_variant = v; }
+// (>= 1000: v - 1000 = the wave stagger in sleep units of 64 cycles, see scan8_kernel)
+void scan8_set_variant(int v) {
+	if (v >= 1000)
+		g_s8_stagger = v - 1000;
+	else
+		g_s8_variant = v;
+}
 
 void launch_scan8_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
                          int seg_cap, hipStream_t st) {
@@ -401,6 +485,16 @@ void launch_scan8_append(const StoreView &s, const QueryView &q, const float *ta
 		case 4: s8_launch<12, 3, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
 		case 5: s8_launch<12, 6, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
 		case 6: s8_launch<12, 12, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		case 21: s8_launch<12, 4, 2, 1>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		case 22: s8_launch<12, 4, 2, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		case 23: s8_launch<12, 4, 2, 3>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		case 24: s8_launch<12, 4, 2, 4>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		case 28: s8_launch<12, 4, 2, 8>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		case 30: s8_launch<12, 4, 2, 16>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		case 31: s8_launch<12, 4, 2, 32>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		case 32: s8_launch<12, 4, 2, 48>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		case 33: s8_launch<12, 6, 2, 16>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		case 29: s8_launch<12, 6, 2, 8>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
 		default: s8_launch<12, 4, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
 		}
 		break;

@@ -25,10 +25,13 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 		}                                                                               \
 	} while (0)
 
-constexpr int KS = 12, D = 4, RB = 2, LD = 768, TR = 256;
+constexpr int KS = 12, D = 4, LD = 768, TR = 256, P = 768;
 
-template <int LAYOUT, int MFMA>
-__global__ __launch_bounds__(512, 1) void probe(const int8_t *__restrict__ X, int n_tiles, int pairs, int *out) {
+// LDSB: B fragments read from a 128-query LDS image (scan8's swizzle, double
+// buffered one k-step ahead) instead of constant registers
+template <int LAYOUT, int MFMA, int LDSB, int RB>
+__global__ __launch_bounds__(64 * (16 / RB), 1) void probe(const int8_t *__restrict__ X, int n_tiles, int pairs, int *out) {
+	__shared__ __attribute__((aligned(16))) uint8_t QL[128 * P];
 	const int nb = gridDim.x, b_id = blockIdx.x;
 	int pr = b_id, NP = nb;
 	if (pairs) {
@@ -36,12 +39,28 @@ __global__ __launch_bounds__(512, 1) void probe(const int8_t *__restrict__ X, in
 		pr = (b_id & 7) | ((b_id >> 4) << 3);
 	}
 	const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lr = lane & 15, lg = lane >> 4;
+	constexpr int WR = 16 * RB;
+	for (int i = tid; i < 128 * P / 16; i += 64 * (16 / RB)) {
+		const unsigned hsh = (unsigned)i * 2654435761u;
+		reinterpret_cast<i32x4 *>(QL)[i] = i32x4{(int)hsh, (int)(hsh * 747796405u), (int)(hsh ^ 0x9E3779B9u), (int)(hsh * 277803737u)};
+	}
+	__syncthreads();
+	uint32_t qo[2][4];
+#pragma unroll
+	for (int m = 0; m < 4; ++m) {
+		qo[0][m] = (uint32_t)(lr * P + ((((4 * m + lg) ^ lr)) << 4));
+		qo[1][m] = qo[0][m] + 64u * P;
+		asm volatile("" : "+v"(qo[1][m]));
+	}
+	auto bload = [&](int j, int u) -> i32x4 {
+		return *reinterpret_cast<const i32x4 *>(QL + qo[u >> 2][j & 3] + 16 * (u & 3) * P + 256 * (j >> 2));
+	};
 	const int my_tiles = pr < n_tiles ? (n_tiles - 1 - pr) / NP + 1 : 0;
 	uint32_t xo[RB];
 #pragma unroll
 	for (int rb = 0; rb < RB; ++rb)
-		xo[rb] = LAYOUT == 0 ? (uint32_t)((32 * w + 16 * rb + lr) * LD + 16 * lg)
-		                     : (uint32_t)((2 * w + rb) * 1024 + 16 * lane);
+		xo[rb] = LAYOUT == 0 ? (uint32_t)((WR * w + 16 * rb + lr) * LD + 16 * lg)
+		                     : (uint32_t)((WR * w + 16 * rb + lr) * 64 + 16 * lg);
 	auto xtile = [&](int b) -> const int8_t * {
 		const int bb = b < my_tiles ? b : my_tiles - 1;
 		return X + (pr + (int64_t)bb * NP) * TR * (int64_t)LD;
@@ -61,9 +80,15 @@ __global__ __launch_bounds__(512, 1) void probe(const int8_t *__restrict__ X, in
 			__builtin_amdgcn_sched_barrier(0);
 		}
 	}
-	i32x4 bq[8];
+	i32x4 bq[2][8];
 #pragma unroll
-	for (int u = 0; u < 8; ++u) bq[u] = i32x4{lane + u, lane ^ u, u, lane};
+	for (int u = 0; u < 8; ++u) {
+		const unsigned hsh = (unsigned)(lane * 8 + u + 1) * 2654435761u;
+		bq[0][u] = bq[1][u] = i32x4{(int)hsh, (int)(hsh * 747796405u), (int)(hsh ^ 0x9E3779B9u), (int)(hsh * 277803737u)};
+	}
+	if (LDSB)
+#pragma unroll
+		for (int u = 0; u < 8; ++u) bq[0][u] = bload(0, u);
 	i32x4 sum = {0, 0, 0, 0};
 	for (int b = 0; b < my_tiles; ++b) {
 		i32x4 acc[RB][8];
@@ -75,13 +100,16 @@ __global__ __launch_bounds__(512, 1) void probe(const int8_t *__restrict__ X, in
 		__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 		for (int j = 0; j < KS; ++j) {
-			const int sl = j % D;
+			const int sl = j % D, cur = LDSB ? (j & 1) : 0;
+			if (LDSB)
+#pragma unroll
+				for (int u = 0; u < 8; ++u) bq[cur ^ 1][u] = bload((j + 1) % KS, u);
 			if (MFMA) {
 #pragma unroll
 				for (int u = 0; u < 8; ++u)
 #pragma unroll
 					for (int rb = 0; rb < RB; ++rb)
-						acc[rb][u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xa[sl][rb], bq[u], acc[rb][u], 0, 0, 0);
+						acc[rb][u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xa[sl][rb], bq[cur][u], acc[rb][u], 0, 0, 0);
 			} else {
 #pragma unroll
 				for (int rb = 0; rb < RB; ++rb) acc[rb][0] ^= xa[sl][rb];
@@ -103,6 +131,16 @@ __global__ __launch_bounds__(512, 1) void probe(const int8_t *__restrict__ X, in
 	if (s == 0x7fffffff) out[b_id] = s;  // keeps the work alive
 }
 
+__global__ void fill_random(uint32_t *p, size_t n) {
+	for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+		uint32_t h = (uint32_t)i * 2654435761u ^ (uint32_t)(i >> 32);
+		h ^= h >> 15;
+		h *= 2246822519u;
+		h ^= h >> 13;
+		p[i] = h;
+	}
+}
+
 int main(int argc, char **argv) {
 	const int64_t n = argc > 1 ? atoll(argv[1]) : 10000000;
 	const int n_tiles = (int)((n + TR - 1) / TR);
@@ -111,17 +149,21 @@ int main(int argc, char **argv) {
 	int *out;
 	CHK(hipMalloc(&X, bytes));
 	CHK(hipMalloc(&out, 1024 * sizeof(int)));
-	CHK(hipMemset(X, 1, bytes));
+	fill_random<<<4096, 256>>>(reinterpret_cast<uint32_t *>(X), bytes / 4);  // random operands: the clock MFMA work really runs at
+	CHK(hipDeviceSynchronize());
 	hipEvent_t e0, e1;
 	CHK(hipEventCreate(&e0));
 	CHK(hipEventCreate(&e1));
-	auto run = [&](int layout, int mfma, int pairs) {
+	auto run = [&](int layout, int mfma, int pairs, int ldsb, int rb) {
 		auto launch = [&]() {
-			const dim3 g(256), t(512);
-			if (layout == 0 && mfma == 0) probe<0, 0><<<g, t>>>(X, n_tiles, pairs, out);
-			if (layout == 0 && mfma == 1) probe<0, 1><<<g, t>>>(X, n_tiles, pairs, out);
-			if (layout == 1 && mfma == 0) probe<1, 0><<<g, t>>>(X, n_tiles, pairs, out);
-			if (layout == 1 && mfma == 1) probe<1, 1><<<g, t>>>(X, n_tiles, pairs, out);
+			const dim3 g(256), t2(512), t4(256);
+			if (layout == 0 && mfma == 1 && ldsb == 0 && rb == 2) probe<0, 1, 0, 2><<<g, t2>>>(X, n_tiles, pairs, out);
+			if (layout == 1 && mfma == 0 && ldsb == 0 && rb == 2) probe<1, 0, 0, 2><<<g, t2>>>(X, n_tiles, pairs, out);
+			if (layout == 1 && mfma == 1 && ldsb == 0 && rb == 2) probe<1, 1, 0, 2><<<g, t2>>>(X, n_tiles, pairs, out);
+			if (layout == 1 && mfma == 1 && ldsb == 1 && rb == 2) probe<1, 1, 1, 2><<<g, t2>>>(X, n_tiles, pairs, out);
+			if (layout == 1 && mfma == 1 && ldsb == 0 && rb == 4) probe<1, 1, 0, 4><<<g, t4>>>(X, n_tiles, pairs, out);
+			if (layout == 1 && mfma == 1 && ldsb == 1 && rb == 4) probe<1, 1, 1, 4><<<g, t4>>>(X, n_tiles, pairs, out);
+			if (layout == 1 && mfma == 0 && ldsb == 1 && rb == 2) probe<1, 0, 1, 2><<<g, t2>>>(X, n_tiles, pairs, out);
 		};
 		for (int i = 0; i < 3; ++i) launch();
 		CHK(hipDeviceSynchronize());
@@ -134,13 +176,18 @@ int main(int argc, char **argv) {
 		CHK(hipEventElapsedTime(&ms, e0, e1));
 		ms /= reps;
 		const double unique = (double)bytes / 1e9;
-		printf("layout=%d mfma=%d pairs=%d  %.3f ms  unique %.2f GB -> %.0f GB/s  (CU ingest %.0f GB/s)\n", layout, mfma,
-		       pairs, ms, unique, unique / ms * 1e3, unique * (pairs ? 2 : 1) / ms * 1e3);
+		printf("layout=%d mfma=%d pairs=%d ldsb=%d rb=%d  %.3f ms  unique %.2f GB -> %.0f GB/s  (CU ingest %.0f GB/s)\n", layout, mfma,
+		       pairs, ldsb, rb, ms, unique, unique / ms * 1e3, unique * (pairs ? 2 : 1) / ms * 1e3);
 		fflush(stdout);
 	};
-	for (int pairs = 0; pairs < 2; ++pairs)
-		for (int layout = 0; layout < 2; ++layout)
-			for (int mfma = 0; mfma < 2; ++mfma) run(layout, mfma, pairs);
+	run(0, 1, 1, 0, 2);
+	run(1, 0, 1, 0, 2);
+	run(1, 1, 1, 0, 2);
+	run(1, 1, 1, 1, 2);
+	run(1, 0, 1, 1, 2);
+	run(1, 1, 1, 0, 4);
+	run(1, 1, 1, 1, 4);
+	run(1, 1, 0, 1, 2);
 	CHK(hipFree(X));
 	CHK(hipFree(out));
 	return 0;
