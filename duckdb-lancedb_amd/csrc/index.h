@@ -235,7 +235,10 @@ struct Index {
 	bool defer_sync = false;  // caller synchronizes the stream itself (host-buffer search)
 	bool retry_pass = true;  // rerun uncertified queries with a tighter tau before the exact fallback
 	int cand_extra = 32;  // refined candidates: max(k * refine_factor, k + max(cand_extra, k))
-	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+	hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+	// progressive threshold (int8 append pass): the first 1/split_div of the tiles
+	// with the sample's tau, then the rest with the tau their pool gives (0: one pass)
+	int split_div = 0;
 	double kt_append_ms = 0.0, kt_dense_ms = 0.0;
 	int64_t kt_append_n = 0, kt_dense_n = 0;
 	int64_t kt_append_rows = 0, kt_append_qpad = 0;

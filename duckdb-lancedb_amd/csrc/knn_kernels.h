@@ -125,12 +125,14 @@ int scan_grid(int64_t n_tiles);
 // each half of a 256-query tile resident in LDS, rows HBM -> registers, bounds
 // screened in exact integers (tile / batch common scales).  Applies to an int8
 // scan copy with ld in [512, 1024]; writes scan8_segments(n_tiles) segments per
-// query (one per pair) in launch_scan_append's format.
+// query (one per pair) in launch_scan_append's format.  A tile range [t0, t1)
+// (t1 < 0: to the end) writes its segments from segment seg_base on, so two
+// launches over disjoint ranges fill disjoint segment sets of one pool.
 bool scan8_fits(const StoreView &s);
 int scan8_segments(int64_t n_tiles);
 void scan8_set_variant(int v);  // development knob: geometry of the ld = 768 kernel (0 = default)
 void launch_scan8_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
-                         int seg_cap, hipStream_t st);
+                         int seg_cap, hipStream_t st, int64_t t0 = 0, int64_t t1 = -1, int seg_base = 0);
 // Segments per query launch_scan_append writes for this store.
 int scan_append_segments(const StoreView &s, int64_t n_tiles);
 

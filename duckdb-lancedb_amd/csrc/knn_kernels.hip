@@ -2305,7 +2305,9 @@ void launch_finalize(const StoreView &s, const uint32_t *cand_slot, const int *c
 //   tau mode (the sample pass): refine at least the m_tau smallest bounds (a
 //   whole chunk), tau = the k-th smallest exact distance among them (+inf when
 //   fewer than k, NaN when any is NaN): an upper bound on the k-th nearest
-//   distance, never above refine_tau_kernel's from the m_tau smallest alone.
+//   distance, never above refine_tau_kernel's from the m_tau smallest alone;
+//   given an input tau (the pool of a first threshold pass over part of the
+//   tiles), tau = min(input, that) (the input when that is NaN).
 // A segment that overflowed, a pool past PR_CAP or a NaN bound fails the
 // certificate (cut = -inf), as select_kernel's does; the rows refined still
 // give the rerun a tau.  Returns the refined count and the pool size.
@@ -2697,7 +2699,10 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 	}
 	if (mode == 0) {
 		if (t == 0) {
-			tau_out[q] = s_dnan ? __builtin_nanf("") : (cnt >= k ? cd[cur][k - 1] : F_INF);
+			const float tk = s_dnan ? __builtin_nanf("") : (cnt >= k ? cd[cur][k - 1] : F_INF);
+			// with an input tau (a later threshold pass): the smaller of the two,
+			// the input when this one is NaN
+			tau_out[q] = !tau ? tk : (tk < ftau ? tk : ftau);
 			if (refined) refined[q] = pos;
 			if (pool_total) pool_total[q] = s_over ? -1 : (int)total;
 		}

@@ -87,16 +87,17 @@ __device__ __forceinline__ int s8_query_part(float4 qp, float4 ts, float W) {
 }
 
 // ABL (timing ablations, wrong results): bit 0 skips the screen, bit 1 the
-// per-block bound terms (constants instead), bit 2 the appends; bit 3 (a speed
-// option, results exact): s_setprio 2 over the k-loop, 0 over the rest; bit 4:
-// a workgroup barrier per block; bit 5: s_setprio alternating by block parity
+// per-block bound terms (constants instead), bit 2 the appends, bit 6 the appends
+// kept in the code but never taken; bit 3 (a speed option, results exact):
+// s_setprio 2 over the k-loop, 0 over the rest
 template <int KS, int D, int RB, int ABL = 0>
 __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *__restrict__ Xq, const float4 *__restrict__ aux8,
                                                       const float4 *__restrict__ tstat, int ld,
                                                       const int8_t *__restrict__ Qi, const float4 *__restrict__ qaux,
-                                                      int nq, int n_tiles, const float *__restrict__ tau,
+                                                      int nq, int n_tiles, int tile0, int seg_base,
+                                                      const float *__restrict__ tau,
                                                       uint2 *__restrict__ seg_pool, int *__restrict__ seg_cnt,
-                                                      int seg_cap, int list_cap, int stagger) {
+                                                      int seg_cap, int list_cap) {
 	static_assert(KS % D == 0 && KS % 2 == 0, "ring slot and fragment buffer of a k-step must be static");
 	constexpr int NW = 16 / RB, T8 = 64 * NW;  // waves: each owns 16 RB rows of every tile
 	constexpr int WR = 16 * RB;                // rows per wave and tile
@@ -106,7 +107,8 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 	float4 *QA = reinterpret_cast<float4 *>(smem + QH * P);
 	float4 *QP = QA + QH;  // s8_query_terms of each query
 	unsigned *CNT = reinterpret_cast<unsigned *>(QP + QH);
-	uint2 *LIST = reinterpret_cast<uint2 *>(CNT + QH);                 // [NW][list_cap] (s, slot)
+	unsigned *UCNT = CNT + QH;                                          // next unclaimed unit (+3 pad words)
+	uint2 *LIST = reinterpret_cast<uint2 *>(CNT + QH + 4);             // [NW][list_cap] (s, slot)
 	uint8_t *LISTQ = reinterpret_cast<uint8_t *>(LIST + NW * list_cap);  // [NW][list_cap] local query
 
 	// Row group and query half of this workgroup.  A query tile with more than
@@ -148,6 +150,7 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 		QP[tid] = s8_query_terms(qa, q < nq ? tau[q] : -F_INF);
 		CNT[tid] = 0u;
 	}
+	if (tid == 0) *UCNT = (unsigned)NW;  // units 0 .. NW-1: one per wave, the rest claimed
 	__syncthreads();
 	// -S: the same for every query with a usable bound (0 for padding / zero cosine queries)
 	float Sabs = fmaxf(-QA[lane].x, -QA[lane + 64].x);
@@ -155,6 +158,14 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 	for (int o = 32; o > 0; o >>= 1) Sabs = fmaxf(Sabs, __shfl_xor(Sabs, o, 64));
 
 	const int my_tiles = pr < n_tiles ? (n_tiles - 1 - pr) / NP + 1 : 0;
+	// Work units: a unit = WR rows of one of this workgroup's tiles (unit u: tile
+	// u / NW, rows WR (u % NW) ..) against its QH queries.  Wave w starts on unit
+	// w and claims later ones from an LDS counter, two ahead (the claim's result
+	// is read a block later: no wait): the waves of a SIMD share its issue and
+	// the older one wins arbitration, so a fixed split (wave w: rows WR w of every
+	// tile) left the younger half ~40 % behind, running the end of every launch
+	// alone, one wave per SIMD.
+	const int NU = my_tiles * NW;
 	int n_list = 0;
 #ifdef LHIP_S8_PROF
 	// diagnostic build: per-wave cycles in each phase of the block loop
@@ -185,44 +196,45 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 			v = fmaf((float)(int)en.x * sc, qa.x, v);
 			v = v + qa.w;
 			const unsigned p = atomicAdd(&CNT[ql], 1u);
-			if (p < (unsigned)seg_cap) seg_pool[((int64_t)b_id * nq + qb + ql) * seg_cap + p] = make_uint2(fkey(v), en.y);
+			if (p < (unsigned)seg_cap)
+				seg_pool[((int64_t)(seg_base + b_id) * nq + qb + ql) * seg_cap + p] = make_uint2(fkey(v), en.y);
 		}
 		n_list = 0;
 	};
 
-	if (my_tiles > 0) {
-		// stagger: the upper half of the waves (the second wave of each SIMD)
-		// starts stagger x 64 cycles late, so one wave's per-block VALU (terms,
-		// screen) runs while the other one multiplies
-		if (w >= NW / 2)
-			for (int z = 0; z < stagger; z += 64) __builtin_amdgcn_s_sleep(64);
-		// this lane's A rows: WR w + 16 rb + lr of each tile, k bytes 64 j + 16 lg,
-		// in the k-major tile layout (tiles_to_i8_kernel): a k-step of 16 rows is
-		// 1 KiB contiguous.  Address = uniform tile base + 16 KiB j (SGPRs) + per-lane
-		// offset: no VALU in the k-loop (a VALU write right after an MFMA may land
-		// on one of its A / B registers while it still reads them: device_common.h)
+	if (w < NU) {
+		// this lane's A rows: WR (u % NW) + 16 rb + lr of the unit's tile, k bytes
+		// 64 j + 16 lg, in the k-major tile layout (tiles_to_i8_kernel): a k-step of
+		// 16 rows is 1 KiB contiguous.  Address = uniform unit base + 16 KiB j
+		// (SGPRs) + per-lane offset: no VALU in the k-loop (a VALU write right after
+		// an MFMA may land on one of its A / B registers while it still reads them:
+		// device_common.h)
 		uint32_t xo[RB];
 #pragma unroll
-		for (int rb = 0; rb < RB; ++rb) xo[rb] = (uint32_t)((WR * w + 16 * rb + lr) * 64 + 16 * lg);
-		auto xtile = [&](int b) -> const int8_t * {
-			const int bb = b < my_tiles ? b : my_tiles - 1;  // past the end: the last block again (unused)
-			return Xq + (pr + (int64_t)bb * NP) * SCAN_BR * (int64_t)ld;
+		for (int rb = 0; rb < RB; ++rb) xo[rb] = (uint32_t)((16 * rb + lr) * 64 + 16 * lg);
+		auto utile = [&](int u) -> int64_t { return tile0 + pr + (int64_t)(u / NW) * NP; };
+		auto xunit = [&](int u) -> const int8_t * {
+			return Xq + utile(u) * SCAN_BR * (int64_t)ld + (int64_t)(WR * (u % NW)) * 64;
 		};
 		auto xload = [&](const int8_t *tb, int j, int rb) -> i32x4 {
 			return *reinterpret_cast<const i32x4 *>(tb + (int64_t)j * I8_CHUNK_STRIDE + xo[rb]);
 		};
-		// row terms of block b: the alpha of ONE of the wave's WR rows per lane (row
-		// lane % WR; its row part is handed to the accumulator lanes of that row by
+		// row terms of a unit: the alpha of ONE of its WR rows per lane (row lane %
+		// WR; its row part is handed to the accumulator lanes of that row by
 		// ds_bpermute: 16 lanes share each accumulator row) and the tile's terms.
 		// (the tile terms by a vector load: a scalar load in flight forces
 		// lgkmcnt(0) (SMEM returns out of order) at the block's first LDS wait)
 		uint32_t vz;
 		asm volatile("v_mov_b32 %0, 0" : "=v"(vz));  // a zero the compiler cannot see is uniform
-		auto aload = [&](int b, float &a, float4 &ts) {
-			const int bb = b < my_tiles ? b : my_tiles - 1;
-			const int64_t tile = pr + (int64_t)bb * NP;
-			a = reinterpret_cast<const float *>(aux8)[(tile << 10) + WR * w + (lane & (WR - 1))];
+		auto aload = [&](int u, float &a, float4 &ts) {
+			const int64_t tile = utile(u);
+			a = reinterpret_cast<const float *>(aux8)[(tile << 10) + WR * (u % NW) + (lane & (WR - 1))];
 			ts = tstat[tile + vz];
+		};
+		auto claim = [&]() -> int {  // (lane 0's LDS atomic; read by readfirstlane where used)
+			unsigned v = 0;
+			if (lane == 0) v = atomicAdd(UCNT, 1u);
+			return (int)v;
 		};
 		// B fragment of query block u, k-step j: query 16u + lr, logical chunk 4j + lg
 		// (two base registers per j & 3 keep every offset an immediate below 64 KiB)
@@ -240,9 +252,11 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 		// the query terms of queries lane and lane + 64 (this lane's query parts,
 		// handed to the accumulator lanes of column 16 u + lr by ds_bpermute)
 		const float4 qp0 = QP[lane], qp1 = QP[lane + 64];
+		int unit = w;                                        // this block's unit
+		int unext = __builtin_amdgcn_readfirstlane(claim()); // the next one (>= NU: none)
 		float an;
 		float4 tn;
-		aload(0, an, tn);
+		aload(unit, an, tn);
 		// complete on the entry path: the block loop carries an[] as plain copies,
 		// and a pending load merged into its header made the waitcnt pass drain
 		// every in-flight ring load at each block start
@@ -252,7 +266,7 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 			// issued in ring order, as the block loop refills it: the waitcnt pass
 			// merges this path into the loop header, and a reordered entry (slot 0
 			// youngest) made it wait for every ring load at each block's first MFMA
-			const int8_t *tb = xtile(0);
+			const int8_t *tb = xunit(unit);
 #pragma unroll
 			for (int j = 0; j < D; ++j) {
 #pragma unroll
@@ -263,25 +277,17 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 		// query fragments, double-buffered: k-step j + 1's are read while k-step j multiplies
 		i32x4 bq[2][8];
 #pragma unroll
-		for (int u = 0; u < 8; ++u) bq[0][u] = bload(0, u);
+		for (int q8 = 0; q8 < 8; ++q8) bq[0][q8] = bload(0, q8);
 
 #ifdef LHIP_S8_PROF
 		pf_t = __builtin_amdgcn_s_memtime();
 #endif
-		for (int b = 0; b < my_tiles; ++b) {
-			// the two waves of a SIMD (w, w + NW/2) in step: oldest-first issue
-			// arbitration otherwise lets the lower half run ~40% ahead, and the
-			// upper half ends the launch alone, one wave per SIMD
-			if (ABL & 16) __syncthreads();
-			if (ABL & 32) {
-				if (((b + (w >= NW / 2 ? 1 : 0)) & 1) != 0)
-					__builtin_amdgcn_s_setprio(1);
-				else
-					__builtin_amdgcn_s_setprio(0);
-			}
+		for (;;) {
+			const int unn_raw = claim();        // the unit after next (read at this block's end)
+			const int ux = unext < NU ? unext : unit;  // past the end: this unit's rows again (unused)
 			const float al = an;
 			const float4 ts = tn;
-			aload(b + 1, an, tn);
+			aload(ux, an, tn);
 			const float W = (Sabs > 0.f && ts.x > 0.f) ? 1.0f / (Sabs * ts.x) : 0.f;
 			i32x4 bias[RB];
 			int gi[8];
@@ -308,7 +314,7 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 			for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
 				for (int u = 0; u < 8; ++u) acc[rb][u] = bias[rb];
-			const int8_t *tb_cur = xtile(b), *tb_next = xtile(b + 1);
+			const int8_t *tb_cur = xunit(unit), *tb_next = xunit(ux);
 			S8_T(pf_pro);
 			if (ABL & 8) __builtin_amdgcn_s_setprio(2);  // the k-loop: MFMA issue first on the SIMD
 			__builtin_amdgcn_sched_barrier(0);
@@ -349,6 +355,11 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 					m = max(m, max(max(acc[rb][u][0], acc[rb][u][1]), max(acc[rb][u][2], acc[rb][u][3])));
 				hitm |= (m >= gi[u] ? 1 : 0) << u;
 			}
+			if (ABL & 64) {  // append code kept, never taken (hit mask through an opaque zero)
+				int z = 0;
+				asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+				hitm &= z;
+			}
 			S8_T(pf_scr);
 #ifdef LHIP_S8_PROF
 			pf_hitb += __builtin_amdgcn_ballot_w64(hitm != 0) ? 1 : 0;
@@ -357,7 +368,7 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 				if (__builtin_amdgcn_ballot_w64(hitm != 0) == 0x123456789ull) n_list += 1;  // (keeps the screen)
 			} else if (__builtin_amdgcn_ballot_w64(hitm != 0)) {
 				// rare: append every passing (s, slot, query) to the wave's list
-				const uint32_t row0 = (uint32_t)((pr + (int64_t)b * NP) * SCAN_BR) + (uint32_t)(WR * w) + 4u * lg;
+				const uint32_t row0 = (uint32_t)(utile(unit) * SCAN_BR) + (uint32_t)(WR * (unit % NW)) + 4u * lg;
 #pragma unroll
 				for (int u = 0; u < 8; ++u) {
 					if (!__builtin_amdgcn_ballot_w64((hitm >> u) & 1)) continue;
@@ -399,14 +410,20 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 				}
 			}
 			S8_T(pf_app);
+			if (unext >= NU) break;
+			unit = unext;
+			unext = __builtin_amdgcn_readfirstlane(unn_raw);
 		}
 	}
-#ifdef LHIP_S8_PROF
-	if (b_id < 3 && lane == 0)
-		printf("S8 wg=%d w=%d blocks=%d pro=%d k=%d scr=%d app=%d hitblocks=%d\n", b_id, w, my_tiles, (int)pf_pro,
-		       (int)pf_k, (int)pf_scr, (int)pf_app, pf_hitb);
-#endif
+	const int nl_end = n_list;
 	if (n_list > 0) flush();
+#ifdef LHIP_S8_PROF
+	uint64_t pf_fl = 0;
+	S8_T(pf_fl);
+	if (b_id < 3 && lane == 0)
+		printf("S8 wg=%d w=%d blocks=%d pro=%d k=%d scr=%d app=%d flush=%d list_end=%d hitblocks=%d\n", b_id, w,
+		       my_tiles, (int)pf_pro, (int)pf_k, (int)pf_scr, (int)pf_app, (int)pf_fl, nl_end, pf_hitb);
+#endif
 	__syncthreads();  // every wave's counter updates
 	// segment b_id of every query of the tile: this workgroup's counts for its
 	// half, zero for the other half (its partner fills its own segment)
@@ -414,7 +431,7 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 		const int q = q_tile + i;
 		if (q >= nq) break;
 		const int ql = q - qb;
-		seg_cnt[(int64_t)b_id * nq + q] = (ql >= 0 && ql < QH) ? (int)CNT[ql] : 0;
+		seg_cnt[(int64_t)(seg_base + b_id) * nq + q] = (ql >= 0 && ql < QH) ? (int)CNT[ql] : 0;
 	}
 }
 
@@ -440,66 +457,60 @@ int scan8_segments(int64_t n_tiles) { return s8_groups(n_tiles); }
 
 static int s8_list_cap(int ld, int nw) {
 	const int P = (ld + 255) / 256 * 256;
-	const int room = LDS8 - QH * P - QH * 36;  // QA, QP, CNT
+	const int room = LDS8 - QH * P - QH * 36 - 16;  // QA, QP, CNT, the unit counter
 	return std::min(1024, room / (nw * 9) / 64 * 64);
 }
 
-static int g_s8_variant = 0, g_s8_stagger = 0;
+static int g_s8_variant = 0;
 
 template <int KS, int D, int RB, int ABL = 0>
 static void s8_launch(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
-                      int seg_cap, int64_t n_tiles, hipStream_t st) {
+                      int seg_cap, int64_t t0, int64_t n_tiles, int seg_base, hipStream_t st) {
 	const dim3 grid((unsigned)s8_groups(n_tiles), (unsigned)(q.nq_pad / SCAN_BQ));
 	constexpr int NW = 16 / RB;
 	scan8_kernel<KS, D, RB, ABL><<<grid, dim3(64 * NW), 0, st>>>(
 	    static_cast<const int8_t *>(s.Xscan), s.scan_aux, s.tstat, s.ld, reinterpret_cast<const int8_t *>(q.Qb), q.qaux,
-	    q.nq, (int)n_tiles, tau, seg_pool, seg_cnt, seg_cap, s8_list_cap(s.ld, NW), g_s8_stagger);
+	    q.nq, (int)n_tiles, (int)t0, seg_base, tau, seg_pool, seg_cnt, seg_cap, s8_list_cap(s.ld, NW));
 }
 
 // geometry of the ld = 768 kernel (development knob, option "scan8_variant"):
 // 16-row blocks per wave (4: four waves, one per SIMD; 2: eight waves) and the
 // register ring depth in 64-deep k-steps
-// (>= 1000: v - 1000 = the wave stagger in sleep units of 64 cycles, see scan8_kernel)
-void scan8_set_variant(int v) {
-	if (v >= 1000)
-		g_s8_stagger = v - 1000;
-	else
-		g_s8_variant = v;
-}
+void scan8_set_variant(int v) { g_s8_variant = v; }
 
 void launch_scan8_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
-                         int seg_cap, hipStream_t st) {
-	const int64_t n_tiles = (s.n_slots + SCAN_BR - 1) / SCAN_BR;
+                         int seg_cap, hipStream_t st, int64_t t0, int64_t t1, int seg_base) {
+	const int64_t all_tiles = (s.n_slots + SCAN_BR - 1) / SCAN_BR;
+	if (t1 < 0 || t1 > all_tiles) t1 = all_tiles;
+	if (t0 < 0 || t0 > t1) throw std::runtime_error("scan8: tile range");
+	const int64_t n_tiles = t1 - t0;
 	if (n_tiles <= 0) return;
 	if (!scan8_fits(s)) throw std::runtime_error("scan8: int8 scan copy with ld in [512, 1024] required");
-	if (n_tiles * (int64_t)SCAN_BR > ((int64_t)1 << 32)) throw std::runtime_error("scan8: slots past 2^32");
+	if (all_tiles * (int64_t)SCAN_BR > ((int64_t)1 << 32)) throw std::runtime_error("scan8: slots past 2^32");
 	if (q.nq_pad % SCAN_BQ) throw std::runtime_error("scan8: query tile padding");
 	switch (s.ld / 64) {
-	case 8: s8_launch<8, 4, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-	case 10: s8_launch<10, 5, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+	case 8: s8_launch<8, 4, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+	case 10: s8_launch<10, 5, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
 	case 12:
 		switch (g_s8_variant) {
-		case 1: s8_launch<12, 4, 4>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-		case 2: s8_launch<12, 6, 4>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-		case 3: s8_launch<12, 12, 4>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-		case 4: s8_launch<12, 3, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-		case 5: s8_launch<12, 6, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-		case 6: s8_launch<12, 12, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-		case 21: s8_launch<12, 4, 2, 1>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-		case 22: s8_launch<12, 4, 2, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-		case 23: s8_launch<12, 4, 2, 3>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-		case 24: s8_launch<12, 4, 2, 4>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-		case 28: s8_launch<12, 4, 2, 8>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-		case 30: s8_launch<12, 4, 2, 16>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-		case 31: s8_launch<12, 4, 2, 32>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-		case 32: s8_launch<12, 4, 2, 48>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-		case 33: s8_launch<12, 6, 2, 16>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-		case 29: s8_launch<12, 6, 2, 8>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-		default: s8_launch<12, 4, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+		case 1: s8_launch<12, 4, 4>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		case 2: s8_launch<12, 6, 4>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		case 3: s8_launch<12, 12, 4>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		case 4: s8_launch<12, 3, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		case 5: s8_launch<12, 6, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		case 6: s8_launch<12, 12, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		case 21: s8_launch<12, 4, 2, 1>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		case 22: s8_launch<12, 4, 2, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		case 23: s8_launch<12, 4, 2, 3>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		case 24: s8_launch<12, 4, 2, 4>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		case 28: s8_launch<12, 4, 2, 8>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		case 34: s8_launch<12, 4, 2, 64>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		case 29: s8_launch<12, 6, 2, 8>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		default: s8_launch<12, 4, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
 		}
 		break;
-	case 14: s8_launch<14, 7, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
-	default: s8_launch<16, 4, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, n_tiles, st); break;
+	case 14: s8_launch<14, 7, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+	default: s8_launch<16, 4, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
 	}
 }
 

@@ -193,6 +193,10 @@ int32_t lance_hip_device_count(void);
  *                  the f32 rows, results are unchanged
  *   "sample_div"   the threshold sample pass covers ~1/sample_div of the row
  *                  tiles (at least 32 tiles); default "32"
+ *   "split_div"    int8 append pass over >= 128 * split_div tiles: the first
+ *                  1/split_div of the tiles with the sample's threshold, the rest
+ *                  with the tighter one their candidates give (e.g. "8"); "0"
+ *                  or "1" = one pass, the default (results unchanged either way)
  *   "cand_extra"   small stores (dense path, <= 65536 rows): exact candidates
  *                  re-ranked per query beyond k: max(k * refine_factor, k +
  *                  max(cand_extra, k)), default "32"; the threshold path re-ranks
