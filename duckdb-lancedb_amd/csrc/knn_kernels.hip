@@ -2976,6 +2976,32 @@ __device__ __forceinline__ void shit_sort(SHit *s, int n) {
 	}
 }
 
+// ascending bitonic sort of one 64-bit key per lane across the wave (registers
+// and cross-lane shuffles only: no LDS round trips, no barriers)
+__device__ __forceinline__ uint64_t wave_sort_u64(uint64_t key, int lane) {
+#pragma unroll
+	for (int size = 2; size <= 64; size <<= 1)
+#pragma unroll
+		for (int stride = size >> 1; stride > 0; stride >>= 1) {
+			const uint64_t other = __shfl_xor(key, stride, 64);
+			const bool keep_min = ((lane & stride) == 0) == ((lane & size) == 0 || size == 64);
+			key = keep_min ? (key < other ? key : other) : (key < other ? other : key);
+		}
+	return key;
+}
+// a and b ascending in lanes 0..31 (~0 past their valid entries): the 64
+// smallest of both, ascending (a bitonic merge of a with b reversed)
+__device__ __forceinline__ uint64_t wave_merge_u64(uint64_t a, uint64_t b, int lane) {
+	const uint64_t br = __shfl(b, 63 - lane, 64);
+	uint64_t key = lane < 32 ? a : br;
+#pragma unroll
+	for (int stride = 32; stride > 0; stride >>= 1) {
+		const uint64_t other = __shfl_xor(key, stride, 64);
+		key = (lane & stride) == 0 ? (key < other ? key : other) : (key < other ? other : key);
+	}
+	return key;
+}
+
 template <int METRIC, typename T>
 __global__ __launch_bounds__(SMALL_THREADS) void small_exact_kernel(const T *__restrict__ X,
                                                                     const float4 *__restrict__ rowaux,
@@ -2984,76 +3010,213 @@ __global__ __launch_bounds__(SMALL_THREADS) void small_exact_kernel(const T *__r
                                                                     SHit *__restrict__ part,
                                                                     unsigned *__restrict__ counter,
                                                                     int64_t *__restrict__ out_l,
-                                                                    float *__restrict__ out_d, int *__restrict__ out_c) {
+                                                                    float *__restrict__ out_d, int *__restrict__ out_c,
+                                                                    int se_prof) {
 	__shared__ __attribute__((aligned(16))) float sq[SMALL_MAX_DIM];
 	__shared__ SHit s_rows[SMALL_MAX_PART], s2[SMALL_MAX_PART], red[SMALL_THREADS];
 	__shared__ unsigned s_ns;
 	__shared__ int s_last;
 	SHit *s = s_rows;
 	const int q = blockIdx.y, G = gridDim.x, t = threadIdx.x;
+	uint64_t mykey;  // (k <= 32 path) this lane's row key
+	__shared__ uint64_t wkeys[SMALL_THREADS];
+#ifdef LHIP_SE_PROF
+	uint64_t st_[12];
+	int nst_ = 0;
+#define SE_T() \
+	if (nst_ < 12) st_[nst_++] = __builtin_amdgcn_s_memtime()
+	SE_T();
+#else
+#define SE_T()
+#endif
 	for (int i = t; i < dim; i += SMALL_THREADS) sq[i] = Q[(int64_t)q * dim + i];
 	__syncthreads();
 	// distances: each wave takes 64 of the workgroup's rows in 8 groups of 8;
 	// a row is split over 8 lanes (float4 chunks sub, sub + 8, ...: coalesced
-	// row reads, every group's loads in flight together), partial f64 sums
-	// reduced over the 8 lanes (the sum of the same products as exact_distance)
+	// row reads), partial f64 sums reduced over the 8 lanes (the sum of the
+	// same products as exact_distance).  Per chunk of SE_CH float4 per lane
+	// the loads of all 8 groups are issued before any product (one memory
+	// latency per chunk instead of one per group and chunk; each lane's
+	// summation order is unchanged: chunk, then its float4 in order).
 	{
+		constexpr int SE_CH = 4;
 		const int lane = t & 63, w = t >> 6, sub = lane & 7;
 		const int d4 = dim >> 2;  // rows are padded to a multiple of 4 elements: aligned 16-B (8-B bf16) loads
+		int64_t r[8];
+		bool ok[8];
+		double a[8], b[8], c[8];
+		mykey = ~0ull;
 #pragma unroll
 		for (int g = 0; g < 8; ++g) {
-			const int rl = w * 64 + g * 8 + (lane >> 3);  // row within the workgroup
-			const int64_t r = (int64_t)blockIdx.x * SMALL_THREADS + rl;
-			const bool ok = r < n && reinterpret_cast<const float *>(rowaux)[raix(r < n ? r : 0, 0)] != F_INF;
-			double a = 0.0, b = 0.0, c = 0.0;
-			if (ok) {
-				const T *x = X + r * ld;
-#pragma unroll 2
-				for (int i4 = sub; i4 < d4; i4 += 8) {
-					const float4 xv = xval4(x, 4 * i4);
-					const float4 qv = *reinterpret_cast<const float4 *>(sq + 4 * i4);
-					exact_acc<METRIC>(xv.x, qv.x, a, b, c);
-					exact_acc<METRIC>(xv.y, qv.y, a, b, c);
-					exact_acc<METRIC>(xv.z, qv.z, a, b, c);
-					exact_acc<METRIC>(xv.w, qv.w, a, b, c);
-				}
-				for (int i = 4 * d4 + sub; i < dim; i += 8) exact_acc<METRIC>(xval(x, i), sq[i], a, b, c);
+			r[g] = (int64_t)blockIdx.x * SMALL_THREADS + w * 64 + g * 8 + (lane >> 3);
+			ok[g] = r[g] < n && reinterpret_cast<const float *>(rowaux)[raix(r[g] < n ? r[g] : 0, 0)] != F_INF;
+			a[g] = b[g] = c[g] = 0.0;
+		}
+		for (int c0 = sub; c0 < d4; c0 += 8 * SE_CH) {
+			float4 qv[SE_CH], xv[8][SE_CH];
+#pragma unroll
+			for (int u = 0; u < SE_CH; ++u) {
+				const int i4 = c0 + 8 * u;
+				qv[u] = i4 < d4 ? *reinterpret_cast<const float4 *>(sq + 4 * i4) : make_float4(0.f, 0.f, 0.f, 0.f);
 			}
 #pragma unroll
+			for (int g = 0; g < 8; ++g)
+#pragma unroll
+				for (int u = 0; u < SE_CH; ++u) {
+					const int i4 = c0 + 8 * u;
+					xv[g][u] = (ok[g] && i4 < d4) ? xval4(X + r[g] * ld, 4 * i4) : make_float4(0.f, 0.f, 0.f, 0.f);
+				}
+#pragma unroll
+			for (int g = 0; g < 8; ++g)
+#pragma unroll
+				for (int u = 0; u < SE_CH; ++u)
+					if (c0 + 8 * u < d4) {  // (only real chunks: a padded product would change cosine's sums)
+						exact_acc<METRIC>(xv[g][u].x, qv[u].x, a[g], b[g], c[g]);
+						exact_acc<METRIC>(xv[g][u].y, qv[u].y, a[g], b[g], c[g]);
+						exact_acc<METRIC>(xv[g][u].z, qv[u].z, a[g], b[g], c[g]);
+						exact_acc<METRIC>(xv[g][u].w, qv[u].w, a[g], b[g], c[g]);
+					}
+		}
+#pragma unroll
+		for (int g = 0; g < 8; ++g) {
+			if (ok[g])
+				for (int i = 4 * d4 + sub; i < dim; i += 8)
+					exact_acc<METRIC>(xval(X + r[g] * ld, i), sq[i], a[g], b[g], c[g]);
+#pragma unroll
 			for (int o = 1; o < 8; o <<= 1) {
-				a += __shfl_xor(a, o, 64);
+				a[g] += __shfl_xor(a[g], o, 64);
 				if (METRIC == METRIC_COSINE) {
-					b += __shfl_xor(b, o, 64);
-					c += __shfl_xor(c, o, 64);
+					b[g] += __shfl_xor(b[g], o, 64);
+					c[g] += __shfl_xor(c[g], o, 64);
 				}
 			}
 			if (sub == 0) {
 				SHit h{F_INF, 0, INT64_MAX};
-				if (ok) {
+				if (ok[g]) {
 					double v;
 					if (METRIC == METRIC_L2)
-						v = a;
+						v = a[g];
 					else if (METRIC == METRIC_DOT)
-						v = 1.0 - a;
+						v = 1.0 - a[g];
 					else
-						v = 1.0 - a / (sqrt(b) * sqrt(c));
+						v = 1.0 - a[g] / (sqrt(b[g]) * sqrt(c[g]));
 					float f = (float)v + 0.0f;
 					if (__builtin_isnan(f)) f = __builtin_nanf("");
-					h = SHit{f, 1, labels[r]};
+					h = SHit{f, 1, labels[r[g]]};
 				}
-				s[rl] = h;
+				s[w * 64 + g * 8 + (lane >> 3)] = h;
+			}
+			// (every lane of the 8 holds the sums: lane sub keeps group sub's row,
+			// one row per lane; key = (ordered distance, slot): slots ascend with
+			// labels, so key order is (distance, label) order, NaN last, none last)
+			if (sub == g && ok[g]) {
+				double v;
+				if (METRIC == METRIC_L2)
+					v = a[g];
+				else if (METRIC == METRIC_DOT)
+					v = 1.0 - a[g];
+				else
+					v = 1.0 - a[g] / (sqrt(b[g]) * sqrt(c[g]));
+				float f = (float)v + 0.0f;
+				if (__builtin_isnan(f)) f = __builtin_nanf("");
+				mykey = ((uint64_t)fkey(f) << 32) | (uint32_t)r[g];
 			}
 		}
 	}
 	__syncthreads();
+	SE_T();
+	const int lane = t & 63, wv = t >> 6;
+	constexpr int NWV = SMALL_THREADS / 64;
+	if (k <= 32) {
+		// ---- k <= 32: register sorts of 64-bit keys, no workgroup sort --------
+		uint64_t key = wave_sort_u64(mykey, lane);
+		wkeys[t] = lane < k ? key : ~0ull;
+		__syncthreads();
+		if (wv == 0) {
+			uint64_t acc = wkeys[lane];
+#pragma unroll
+			for (int v = 1; v < NWV; ++v) {
+				acc = wave_merge_u64(acc, wkeys[v * 64 + lane], lane);
+				if (lane >= k) acc = ~0ull;
+			}
+			uint64_t *mine = reinterpret_cast<uint64_t *>(part) + ((int64_t)q * G + blockIdx.x) * k;
+			if (lane < k) mine[lane] = acc;
+			__threadfence();
+		}
+		__syncthreads();
+		if (t == 0) s_last = atomicAdd(&counter[q], 1u) == (unsigned)(G - 1);
+		__syncthreads();
+		if (!s_last) return;
+		__threadfence();
+		// merge: only keys <= thr = the smallest of the lists' k-th keys can
+		// place; each wave takes 64-key chunks of those, keeps a running top-k,
+		// and wave 0 merges the waves' lists
+		const uint64_t *all = reinterpret_cast<const uint64_t *>(part) + (int64_t)q * G * k;
+		const int P = G * k;
+		uint64_t tk = ~0ull;
+		for (int g = t; g < G; g += SMALL_THREADS) tk = min(tk, all[(int64_t)g * k + k - 1]);
+#pragma unroll
+		for (int o = 32; o > 0; o >>= 1) tk = min(tk, (uint64_t)__shfl_xor(tk, o, 64));
+		if (lane == 0) wkeys[wv] = tk;
+		if (t == 0) s_ns = 0;
+		__syncthreads();
+		uint64_t thr = wkeys[0];
+#pragma unroll
+		for (int v = 1; v < NWV; ++v) thr = min(thr, wkeys[v]);
+		uint64_t *cand = reinterpret_cast<uint64_t *>(s2);
+		for (int i = t; i < P; i += SMALL_THREADS) {
+			const uint64_t e = all[i];
+			if (e <= thr) cand[atomicAdd(&s_ns, 1u)] = e;
+		}
+		__syncthreads();
+		const int ns = (int)s_ns;
+		uint64_t best = ~0ull;
+		for (int c0 = wv * 64; c0 < ns; c0 += NWV * 64) {
+			uint64_t ck = c0 + lane < ns ? cand[c0 + lane] : ~0ull;
+			ck = wave_sort_u64(ck, lane);
+			if (lane >= k) ck = ~0ull;
+			best = wave_merge_u64(best, ck, lane);
+			if (lane >= k) best = ~0ull;
+		}
+		__syncthreads();  // (wkeys reused)
+		wkeys[t] = best;
+		__syncthreads();
+		if (wv == 0) {
+			uint64_t acc = wkeys[lane];
+#pragma unroll
+			for (int v = 1; v < NWV; ++v) {
+				acc = wave_merge_u64(acc, wkeys[v * 64 + lane], lane);
+				if (lane >= k) acc = ~0ull;
+			}
+			if (lane < k) {
+				const bool valid = acc != ~0ull;
+				out_l[(int64_t)q * k + lane] = valid ? labels[(uint32_t)acc] : -1;
+				out_d[(int64_t)q * k + lane] = valid ? fkey_inv((uint32_t)(acc >> 32)) : __builtin_nanf("");
+			}
+			const uint64_t vm = __builtin_amdgcn_ballot_w64(lane < k && acc != ~0ull);
+			if (lane == 0) {
+				out_c[q] = __builtin_popcountll(vm);
+				counter[q] = 0u;  // ready for the next launch on this stream
+			}
+		}
+		return;
+	}
+	// ---- k > 32: bitonic sorts of the workgroup's rows ------------------------
 	// this workgroup's top-k: sorted by (distance, label)
 	if (!LHIP_ABL_SMALL_NOWGSORT) shit_sort(s, SMALL_THREADS);
+	SE_T();
 	SHit *mine = part + ((int64_t)q * G + blockIdx.x) * k;
 	for (int i = t; i < k; i += SMALL_THREADS) mine[i] = s[i];
 	if (!LHIP_ABL_SMALL_NOFENCE) __threadfence();
 	__syncthreads();
 	if (t == 0) s_last = atomicAdd(&counter[q], 1u) == (unsigned)(G - 1);
 	__syncthreads();
+	SE_T();
+#ifdef LHIP_SE_PROF
+	if (!s_last && t == 0 && blockIdx.x < 2 && se_prof)
+		printf("SE wg=%d dist=%d sort=%d publish=%d\n", blockIdx.x, (int)(st_[1] - st_[0]), (int)(st_[2] - st_[1]),
+		       (int)(st_[3] - st_[2]));
+#endif
 	if (!s_last) return;
 	if (!LHIP_ABL_SMALL_NOFENCE) __threadfence();
 	// merge: every list is sorted, so the k-th smallest overall is <= each
@@ -3071,6 +3234,7 @@ __global__ __launch_bounds__(SMALL_THREADS) void small_exact_kernel(const T *__r
 		__syncthreads();
 	}
 	const SHit thr = red[0];
+	SE_T();
 	for (int i = t; i < P; i += SMALL_THREADS)
 		if (!shit_less(thr, s[i])) s2[atomicAdd(&s_ns, 1u)] = s[i];
 	__syncthreads();
@@ -3079,7 +3243,9 @@ __global__ __launch_bounds__(SMALL_THREADS) void small_exact_kernel(const T *__r
 	while (n2 < ns) n2 <<= 1;
 	for (int i = ns + t; i < n2; i += SMALL_THREADS) s2[i] = SHit{F_INF, 0, INT64_MAX};
 	__syncthreads();
+	SE_T();
 	if (!LHIP_ABL_SMALL_NOMERGE) shit_sort(s2, n2);
+	SE_T();
 	s = s2;
 	for (int i = t; i < k; i += SMALL_THREADS) {
 		out_l[(int64_t)q * k + i] = s[i].v ? s[i].l : -1;
@@ -3091,6 +3257,13 @@ __global__ __launch_bounds__(SMALL_THREADS) void small_exact_kernel(const T *__r
 		out_c[q] = cnt;
 		counter[q] = 0u;  // ready for the next launch on this stream
 	}
+#ifdef LHIP_SE_PROF
+	SE_T();
+	if (t == 0 && se_prof)
+		printf("SE last wg=%d dist=%d sort=%d publish=%d load+thr=%d compact=%d sort2=%d out=%d ns=%d\n", blockIdx.x,
+		       (int)(st_[1] - st_[0]), (int)(st_[2] - st_[1]), (int)(st_[3] - st_[2]), (int)(st_[4] - st_[3]),
+		       (int)(st_[5] - st_[4]), (int)(st_[6] - st_[5]), (int)(st_[7] - st_[6]), ns);
+#endif
 }
 
 int small_exact_grid(int64_t n_slots) { return (int)((n_slots + SMALL_THREADS - 1) / SMALL_THREADS); }
@@ -3107,18 +3280,20 @@ static void small_exact_dispatch(const StoreView &s, const float *Q, int nq, int
 	const dim3 grid((unsigned)small_exact_grid(s.n_slots), (unsigned)nq);
 	const T *X = static_cast<const T *>(s.X);
 	SHit *p = static_cast<SHit *>(part);
+	static int calls = 0;  // (LHIP_SE_PROF: the 200th launch of the process prints its phases)
+	const int se_prof = ++calls == 200;
 	switch (s.metric) {
 	case METRIC_L2:
 		small_exact_kernel<METRIC_L2, T><<<grid, SMALL_THREADS, 0, st>>>(X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim, Q,
-		                                                                 k, p, counter, L, D, C);
+		                                                                 k, p, counter, L, D, C, se_prof);
 		break;
 	case METRIC_DOT:
 		small_exact_kernel<METRIC_DOT, T><<<grid, SMALL_THREADS, 0, st>>>(X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim,
-		                                                                  Q, k, p, counter, L, D, C);
+		                                                                  Q, k, p, counter, L, D, C, se_prof);
 		break;
 	default:
 		small_exact_kernel<METRIC_COSINE, T><<<grid, SMALL_THREADS, 0, st>>>(X, s.rowaux, s.labels, s.n_slots, s.ld,
-		                                                                     s.dim, Q, k, p, counter, L, D, C);
+		                                                                     s.dim, Q, k, p, counter, L, D, C, se_prof);
 		break;
 	}
 }

@@ -415,7 +415,9 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 			unext = __builtin_amdgcn_readfirstlane(unn_raw);
 		}
 	}
+#ifdef LHIP_S8_PROF
 	const int nl_end = n_list;
+#endif
 	if (n_list > 0) flush();
 #ifdef LHIP_S8_PROF
 	uint64_t pf_fl = 0;

@@ -7,7 +7,7 @@ D=duckdb-lancedb_amd
 F="-DLHIP_ABLATION_BUILD -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-inline-asm -Wno-unused-result"
 mkdir -p abl
 make -s -C $D  # the other objects of the library (lib/*.o)
-OTHERS="$D/lib/rscan_kernels.o $D/lib/ivf_kernels.o $D/lib/lance_hip_abi.o $D/lib/ivf_index.o $D/lib/meta.o"
+OTHERS="$D/lib/scan8_kernels.o $D/lib/ivf_kernels.o $D/lib/lance_hip_abi.o $D/lib/ivf_index.o $D/lib/meta.o"
 build() { # name defines...
 	local n=$1; shift
 	hipcc $F "$@" -c $D/csrc/knn_kernels.hip -o abl/k_$n.o
@@ -29,8 +29,6 @@ for v in "$@"; do
 	NOMFMA_NOREADS_NOEPI) build NOMFMA_NOREADS_NOEPI -DLHIP_ABL_NO_MFMA=1 -DLHIP_ABL_NO_READS=1 -DLHIP_ABL_NO_EPILOGUE=1 ;;
 	NOFLUSH) build NOFLUSH -DLHIP_ABL_NO_FLUSH=1 ;;
 	SNOFENCE) build SNOFENCE -DLHIP_ABL_SMALL_NOFENCE=1 ;;
-	SNOWGSORT) build SNOWGSORT -DLHIP_ABL_SMALL_NOWGSORT=1 ;;
-	SNOMERGE) build SNOMERGE -DLHIP_ABL_SMALL_NOMERGE=1 ;;
 	SLOW_NEVER) build SLOW_NEVER -DLHIP_ABL_SLOW_NEVER=1 ;;
 	SLOW_UNROLL) build SLOW_UNROLL -DLHIP_SLOW_VALU=0 -DLHIP_SLOW_UNROLL=1 ;;
 	SLOW_SWITCH) build SLOW_SWITCH -DLHIP_SLOW_VALU=0 ;;
