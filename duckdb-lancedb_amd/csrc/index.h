@@ -373,11 +373,11 @@ struct Index {
 		HIPCHK(hipStreamSynchronize(stream));
 	}
 
-	// the int8 scan applies: an f32 store whose rows fit the int8 stages (ld a
-	// multiple of 128, exact integer dot products up to ld = 1024), no filter,
-	// ranking by the index metric
+	// the int8 scan applies: an f32 or bf16 store whose rows fit the int8 stages
+	// (ld a multiple of 128, exact integer dot products up to ld = 1024), no
+	// filter, ranking by the index metric
 	bool i8_usable() const {
-		return scan_i8 && !xbf16 && X && n_slots > 0 && ld % 128 == 0 && ld <= 1024 && !filter_on &&
+		return scan_i8 && X && n_slots > 0 && ld % 128 == 0 && ld <= 1024 && !filter_on &&
 		       !(metric_quirk && metric != METRIC_L2);
 	}
 	// (re)build the int8 scan copy and its row terms from X when stale
@@ -395,7 +395,7 @@ struct Index {
 		// whole tiles up to the last row; past them: zero rows, +inf row terms
 		const int64_t t1 = (n_slots + SCAN_BR - 1) / SCAN_BR, r1 = t1 * SCAN_BR;
 		HIPCHK(hipMemsetAsync(Xq + (size_t)r1 * ld, 0, (size_t)(cap - r1) * ld, stream));
-		launch_tiles_to_i8(static_cast<const float *>(X), ld, dim, metric, n_slots, 0, t1, rowaux, Xq, rowaux8, tstat8,
+		launch_tiles_to_i8(X, xbf16 ? 1 : 0, ld, dim, metric, n_slots, 0, t1, rowaux, Xq, rowaux8, tstat8,
 		                   stats8.p, stream);
 		launch_fill_rowaux(rowaux8, r1, cap, stream);
 		HIPCHK(hipGetLastError());
@@ -431,7 +431,7 @@ struct Index {
 		if (rowaux_l2) launch_rowaux(X, xbf16, ld, dim, METRIC_L2, n_slots, num, rowaux_l2, stats.p + 2, stream);
 		// (the tile the new rows start in is re-quantised whole: its scale may grow)
 		if (i8_cur)
-			launch_tiles_to_i8(static_cast<const float *>(X), ld, dim, metric, n_slots + num, n_slots / SCAN_BR,
+			launch_tiles_to_i8(X, xbf16 ? 1 : 0, ld, dim, metric, n_slots + num, n_slots / SCAN_BR,
 			                   (n_slots + num + SCAN_BR - 1) / SCAN_BR, rowaux, Xq, rowaux8, tstat8, stats8.p, stream);
 		HIPCHK(hipGetLastError());
 		HIPCHK(hipStreamSynchronize(stream));

@@ -73,8 +73,8 @@ void launch_rows_to_bf16(const float *src, int64_t src_ld, int64_t n, int dim, i
 // padded; rows past n_slots zero), their row terms aux8 (tombstones copied from
 // rowaux, rows past n_slots +inf) and per-tile terms tstat[t] = (s_T, max |e_x|,
 // max |x~|, 0); folds max |alpha| and max(xn, ux) into stats[0], stats[1] (float bits).
-void launch_tiles_to_i8(const float *X, int ld, int dim, int metric, int64_t n_slots, int64_t t0, int64_t t1,
-                        const float4 *rowaux, int8_t *Xq, float4 *aux8, float4 *tstat, unsigned *stats,
+void launch_tiles_to_i8(const void *X, int xbf16, int ld, int dim, int metric, int64_t n_slots, int64_t t0,
+                        int64_t t1, const float4 *rowaux, int8_t *Xq, float4 *aux8, float4 *tstat, unsigned *stats,
                         hipStream_t st);
 
 // rowaux[from, to) = (+inf, 0, 0, 0): padding rows past the last slot.

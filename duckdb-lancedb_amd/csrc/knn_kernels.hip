@@ -144,7 +144,8 @@ void launch_rows_to_bf16(const float *src, int64_t src_ld, int64_t n, int dim, i
 // One 256-thread workgroup per tile: row maxima into LDS, the tile scale, then
 // each wave quantises rows (rows past n_slots: zero, alpha = +inf).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void tiles_to_i8_kernel(const float *__restrict__ X, int ld, int dim, int metric,
+template <typename T>
+__global__ __launch_bounds__(256) void tiles_to_i8_kernel(const T *__restrict__ X, int ld, int dim, int metric,
                                                           int64_t n_slots, int64_t t0,
                                                           const float4 *__restrict__ rowaux, int8_t *__restrict__ Xq,
                                                           float4 *__restrict__ aux8, float4 *__restrict__ tstat,
@@ -161,9 +162,9 @@ __global__ __launch_bounds__(256) void tiles_to_i8_kernel(const float *__restric
 		float m = 0.f;
 		double s2 = 0.0;
 		if (r < n_slots) {
-			const float *x = X + r * (int64_t)ld;
+			const T *x = X + r * (int64_t)ld;
 			for (int i = lane; i < dim; i += 64) {
-				const float v = x[i];
+				const float v = xval(x, i);
 				m = fmaxf(m, fabsf(v));
 				s2 += (double)v * v;
 			}
@@ -211,7 +212,7 @@ __global__ __launch_bounds__(256) void tiles_to_i8_kernel(const float *__restric
 			}
 			continue;
 		}
-		const float *x = X + r * (int64_t)ld;
+		const T *x = X + r * (int64_t)ld;
 		const double xn = rnorm[rr];
 		const double rs = (cosine && xn > 0.0) ? 1.0 / xn : 1.0;
 		double e2 = 0.0, t2 = 0.0;
@@ -223,7 +224,7 @@ __global__ __launch_bounds__(256) void tiles_to_i8_kernel(const float *__restric
 				const int i = i0 + j;
 				int qv = 0;
 				if (i < dim) {
-					const double v = cosine ? (double)x[i] * rs : (double)x[i];
+					const double v = cosine ? (double)xval(x, i) * rs : (double)xval(x, i);
 					qv = (int)fmin(127.0, fmax(-127.0, rint(v * inv)));
 					const double xt = (double)sT * (double)qv;
 					const double e = v - xt;
@@ -273,12 +274,17 @@ __global__ __launch_bounds__(256) void tiles_to_i8_kernel(const float *__restric
 		                          fmaxf(fmaxf(red[2][0], red[2][1]), fmaxf(red[2][2], red[2][3])), 0.f);
 }
 
-void launch_tiles_to_i8(const float *X, int ld, int dim, int metric, int64_t n_slots, int64_t t0, int64_t t1,
-                        const float4 *rowaux, int8_t *Xq, float4 *aux8, float4 *tstat, unsigned *stats,
+void launch_tiles_to_i8(const void *X, int xbf16, int ld, int dim, int metric, int64_t n_slots, int64_t t0,
+                        int64_t t1, const float4 *rowaux, int8_t *Xq, float4 *aux8, float4 *tstat, unsigned *stats,
                         hipStream_t st) {
 	if (t1 <= t0) return;
-	tiles_to_i8_kernel<<<dim3((unsigned)(t1 - t0)), dim3(256), 0, st>>>(X, ld, dim, metric, n_slots, t0, rowaux, Xq,
-	                                                                    aux8, tstat, stats);
+	const dim3 grid((unsigned)(t1 - t0)), blk(256);
+	if (xbf16)
+		tiles_to_i8_kernel<uint16_t><<<grid, blk, 0, st>>>(static_cast<const uint16_t *>(X), ld, dim, metric, n_slots,
+		                                                   t0, rowaux, Xq, aux8, tstat, stats);
+	else
+		tiles_to_i8_kernel<float><<<grid, blk, 0, st>>>(static_cast<const float *>(X), ld, dim, metric, n_slots, t0,
+		                                                rowaux, Xq, aux8, tstat, stats);
 }
 
 __global__ void fill_rowaux_kernel(float4 *rowaux, int64_t from, int64_t to) {
@@ -2403,6 +2409,7 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 	__shared__ unsigned sh[PR_WAVES];
 	__shared__ int s_over, s_nnan, s_dnan;
 	__shared__ unsigned s_nfin, s_knf, s_kmin, s_kmax, s_bstar, s_cum, s_below, s_ns, s_hi;
+	__shared__ unsigned segc[PR_THREADS];  // (big pools) segment counts
 	const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
 #ifdef LHIP_PR_PROF
 	// phase stamps (diagnostic build, one designated launch): thread 0 prints
@@ -2436,8 +2443,102 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 	unsigned total;
 	static_assert(PR_THREADS == SEL_THREADS, "block_excl_scan's geometry");
 	const unsigned off = block_excl_scan(c, sh, total);
-	const int n = (int)min(total, (unsigned)PR_CAP);
-	if (t < n_seg && c && off < (unsigned)PR_CAP) {
+	// a pool past PR_CAP: keep its smallest bounds (whole histogram bins, at most
+	// PR_CAP) and treat the rest like rows outside the pool: cut <= the smallest
+	// bound left out (excl_min), an exact certificate without a rerun.  Only when
+	// one bin alone overflows do the first PR_CAP entries stay (uncertified).
+	unsigned excl_min = 0xFFFFFFFFu;
+	bool big = false;
+	if (total > (unsigned)PR_CAP) {
+		if (t < n_seg) segc[t] = c;
+		if (t == 0) {
+			s_kmin = 0xFFFFFFFFu;
+			s_kmax = 0;
+			s_bstar = 0xFFFFFFFFu;
+			s_ns = 0;
+			s_hi = 0xFFFFFFFFu;
+		}
+		for (int i = t; i < PR_HB; i += PR_THREADS) hist[i] = 0;
+		__syncthreads();
+		const int m = max(1, PR_THREADS / max(n_seg, 1));  // threads per segment
+		const int sg = t / m, sub = t - sg * m;
+		// every entry of this thread's segment share, 4 loads in flight
+		auto each = [&](auto &&f) {
+			if (sg >= n_seg) return;
+			const uint2 *seg = seg_pool + ((int64_t)sg * nq + q) * seg_cap;
+			const unsigned cs = segc[sg];
+			for (unsigned i = sub; i < cs; i += 4u * m) {
+				uint2 e[4];
+#pragma unroll
+				for (int u = 0; u < 4; ++u)
+					if (i + u * m < cs) e[u] = seg[i + u * m];
+#pragma unroll
+				for (int u = 0; u < 4; ++u)
+					if (i + u * m < cs) f(e[u]);
+			}
+		};
+		unsigned kmn = 0xFFFFFFFFu, kmx = 0, nn = 0;
+		each([&](uint2 e) {
+			if (e.x < KEY_INF) {
+				kmn = min(kmn, e.x);
+				kmx = max(kmx, e.x);
+			}
+			nn += e.x == KEY_NAN ? 1u : 0u;
+		});
+#pragma unroll
+		for (int o = 32; o > 0; o >>= 1) {
+			kmn = min(kmn, (unsigned)__shfl_xor(kmn, o, 64));
+			kmx = max(kmx, (unsigned)__shfl_xor(kmx, o, 64));
+			nn += __shfl_xor(nn, o, 64);
+		}
+		if (lane == 0) {
+			atomicMin(&s_kmin, kmn);
+			atomicMax(&s_kmax, kmx);
+			if (nn) atomicAdd(&s_nnan, (int)nn);
+		}
+		__syncthreads();
+		const unsigned kmin = s_kmin, kmax = s_kmax;
+		const unsigned span = kmax - kmin;
+		const int shift = kmin == 0xFFFFFFFFu ? 0 : (span >= (unsigned)PR_HB ? (32 - __builtin_clz(span)) - 10 : 0);
+		if (kmin != 0xFFFFFFFFu) {
+			each([&](uint2 e) {
+				if (e.x < KEY_INF) atomicAdd(&hist[(e.x - kmin) >> shift], 1u);
+			});
+		}
+		__syncthreads();
+		{
+			static_assert(PR_HB == 2 * PR_THREADS, "two bins per thread");
+			const unsigned h0 = hist[2 * t], h1 = hist[2 * t + 1];
+			unsigned tot;
+			const unsigned ex = block_excl_scan(h0 + h1, sh, tot);
+			int cand = -1;  // the last bin whose inclusive count fits
+			if (ex + h0 + h1 <= (unsigned)PR_CAP)
+				cand = 2 * t + 1;
+			else if (ex + h0 <= (unsigned)PR_CAP)
+				cand = 2 * t;
+			if (cand >= 0) atomicMax(reinterpret_cast<int *>(&s_bstar) + 0, cand);  // (s_bstar starts at -1)
+		}
+		__syncthreads();
+		const int bstar = (int)s_bstar;
+		if (kmin != 0xFFFFFFFFu && bstar >= 0) {
+			big = true;
+			unsigned xm = 0xFFFFFFFFu;
+			each([&](uint2 e) {
+				const bool keep = e.x < KEY_INF && (int)((e.x - kmin) >> shift) <= bstar;
+				if (keep)
+					keys[atomicAdd(&s_ns, 1u)] = ((uint64_t)e.x << 32) | e.y;
+				else
+					xm = min(xm, e.x);
+			});
+#pragma unroll
+			for (int o = 32; o > 0; o >>= 1) xm = min(xm, (unsigned)__shfl_xor(xm, o, 64));
+			if (lane == 0) atomicMin(&s_hi, xm);
+		}
+		__syncthreads();
+		excl_min = s_hi;
+	}
+	const int n = big ? (int)s_ns : (int)min(total, (unsigned)PR_CAP);
+	if (!big && t < n_seg && c && off < (unsigned)PR_CAP) {
 		const uint2 *seg = seg_pool + ((int64_t)t * nq + q) * seg_cap;
 		const unsigned cm = min(c, (unsigned)PR_CAP - off);
 		for (unsigned i = 0; i < cm; i += 8) {  // 8 loads in flight per thread
@@ -2452,8 +2553,9 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 	}
 	__syncthreads();
 	mark();
-	if (t == 0 && total > (unsigned)PR_CAP) s_over = 1;
+	if (t == 0 && total > (unsigned)PR_CAP && !big) s_over = 1;
 	// finite bounds (key < KEY_INF), NaN bounds, the smallest non-finite key
+	// (big: NaN bounds were counted over the whole pool above)
 	{
 		unsigned nf = 0, nn = 0, knf = 0xFFFFFFFFu;
 		for (int i = t; i < n; i += PR_THREADS) {
@@ -2740,6 +2842,8 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 			cutv = fkey_inv(s_knf);
 		else
 			cutv = F_INF;
+		// (big pool: the bounds left out of it)
+		if (excl_min != 0xFFFFFFFFu && excl_min != KEY_NAN && fkey_inv(excl_min) < cutv) cutv = fkey_inv(excl_min);
 		if (ftau < cutv) cutv = ftau;
 		if (s_over || s_nnan > 0) cutv = -F_INF;
 		bool ok;

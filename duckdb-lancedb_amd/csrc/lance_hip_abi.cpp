@@ -48,10 +48,12 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	const float4 *aux = search_aux((metric_quirk && metric != METRIC_L2) ? rowaux_l2 : rowaux);
 	const float ma = (metric_quirk && metric != METRIC_L2) ? max_alpha_l2 : max_alpha;
 	// int8 scan copy (option scan_i8): the scans stream int8 rows with their own
-	// row terms; refine, fallback and the outputs read X and rowaux as always
-	// (k <= 32: past that the looser bounds leave more rows below the k-th
-	// distance than the selection's capacity holds); otherwise bf16 rows
-	const bool use8 = i8_usable() && k <= 32;
+	// row terms; refine, fallback and the outputs read X and rowaux as always.
+	// Any k on the threshold path (pool_refine refines as far as its certificate
+	// needs); k <= 32 on the dense path of small stores (a fixed candidate count:
+	// past that the looser bounds leave more rows below the k-th distance than
+	// it holds); otherwise bf16 rows
+	const bool use8 = i8_usable() && (k <= 32 || (n_slots > 65536 && k + 8 <= MAX_CAND));
 	if (!use8) ensure_xs();
 	const float mu = (metric_quirk && metric != METRIC_L2) ? max_ux_l2 : max_ux;
 	StoreView sv{X, aux, dlabels, n_slots, ld, dim, eff_metric, xbf16 ? 1 : 0,
@@ -163,8 +165,11 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		const int nA = tA ? scan8_segments(tA) : 0;
 		const int n_seg = tA ? nA + scan8_segments(n_tiles - tA) : scan_append_segments(sv, n_tiles);
 		const int n_seg1 = tA ? n_seg : scan_append_segments(sv, n_tiles);  // (segments one pass would write)
+		// (32x headroom: the int8 bounds put several times more rows under tau
+		// than (k+4)*N/sample, and pool_refine keeps the smallest of a pool past
+		// its LDS capacity, but a segment past seg_cap fails the certificate)
 		const int64_t expect = (int64_t)(k + 4) * ((n_tiles + n_sample - 1) / n_sample);
-		const int seg_cap = (int)std::min<int64_t>(1024, round_up(std::max<int64_t>(64, 4 * expect / n_seg1), 32));
+		const int seg_cap = (int)std::min<int64_t>(1024, round_up(std::max<int64_t>(64, 32 * expect / n_seg1), 32));
 		ws.seg_pool.need((size_t)n_seg * nq * seg_cap + (size_t)n_seg * (nq_pad / SCAN_BQ));  // + per-workgroup sink
 		ws.seg_cnt.need((size_t)n_seg * nq);
 		tic(2);

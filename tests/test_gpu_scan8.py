@@ -176,3 +176,36 @@ def test_c2_full_size(hip, tmp_path):
         assert st["fallback_queries"] == 0, st
     finally:
         hip.LanceFreeDetached(h)
+
+
+@pytest.mark.parametrize("metric", ["dot", "l2"])
+def test_bf16_store_k100_int8(hip, tmp_path, metric):
+    # C3's shape at reduced size (configs[2]: a bf16 store, L2-normalised rows,
+    # inner product, k = 100): the int8 copy is built from the bf16 rows, the
+    # pools of the first pass exceed pool_refine's LDS capacity (the smallest
+    # bounds are kept, the rest bounds the certificate) and every query must
+    # still certify without a rerun; ids exact against the f64 oracle on the
+    # stored (bf16-rounded) rows
+    import torch
+    rng = np.random.default_rng(100)
+    n, d = 400_000, 768
+    X = rng.standard_normal((n, d), dtype=np.float32)
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    Q = rng.standard_normal((96, d), dtype=np.float32)
+    Q /= np.linalg.norm(Q, axis=1, keepdims=True)
+    Xs = torch.from_numpy(X).to(torch.bfloat16).float().numpy()  # what a bf16 store holds
+    h = hip.LanceCreateDetached(str(tmp_path), d, metric, "t")
+    try:
+        hip.LanceHipSetOption(h, "storage", "bf16")
+        hip.LanceHipSetOption(h, "time_kernels", "1")
+        for lo in range(0, n, 100_000):
+            hip.LanceDetachedAddBatch(h, X[lo:lo + 100_000], 100_000, d)
+        gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 100)
+        assert _ran_scan8(hip, h)
+        st = hip.LanceHipLastSearchStats(h)
+        el, ed, ec = c_oracle.flat_search_batch(Xs, Q, 100, metric, acc64=True, nthreads=16)
+        assert_same(gl, gd, gc, el, ed, ec)
+        assert st["fallback_queries"] == 0, st
+        assert st["retried_queries"] == 0, st
+    finally:
+        hip.LanceFreeDetached(h)
