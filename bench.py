@@ -689,7 +689,13 @@ def main():
             avg_ms = kt["scan_ms_total"] / kt["scan_launches"]
             # algorithmic bytes per launch: every base row (ld elements + 16 B row aux) + the query tile
             # (bf16; int8 with the int8 scan copy)
-            bytes_launch = kt["scan_rows"] * (ld * esz + 16) + kt["scan_qpad"] * ld * (1 if esz == 1 else 2)
+            if kt["scan_kernel"] == "scan8_kernel":
+                # scan8 reads, per row, its int8 k-chunks and its alpha (the other row
+                # terms are per 256-row tile: 16 B), and the int8 query tile once
+                tiles = (kt["scan_rows"] + 255) // 256
+                bytes_launch = kt["scan_rows"] * (ld + 4) + tiles * 16 + kt["scan_qpad"] * ld
+            else:
+                bytes_launch = kt["scan_rows"] * (ld * esz + 16) + kt["scan_qpad"] * ld * (1 if esz == 1 else 2)
             xname = {1: "i8", 2: "bf16"}.get(esz, "f32")
             # dense MFMA peak of the scan's operand type (int8: 2x bf16)
             mfma_peak = MFMA_BF16_PEAK_TFS * (2 if esz == 1 else 1)
