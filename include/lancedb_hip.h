@@ -179,12 +179,14 @@ int32_t lance_hip_device_count(void);
  *                  bf16 keeps the nearest-even bf16 of each added row and every
  *                  result is exact with respect to those stored rows.  Only
  *                  while the table holds no rows.
- *   "scan_i8"      "on" (default) | "off": an f32 store with dim padded to a
- *                  multiple of 128 (<= 1024) also keeps an int8 copy of its rows
- *                  (one scale per 256-row tile, 1 B per element + 16 B of row
- *                  terms) that the flat scans stream when k <= 32, no predicate
- *                  and no metric_quirk; results are unchanged (exact re-rank +
- *                  certificate).  Built on the first search or by "prepare".
+ *   "scan_i8"      "on" (default) | "off": a store (f32 or bf16) with dim padded
+ *                  to a multiple of 128 (<= 1024) also keeps an int8 copy of its
+ *                  rows (one scale per 256-row tile, 1 B per element + 16 B of
+ *                  row terms) that the flat scans stream when there is no
+ *                  predicate and no metric_quirk (any k on the threshold path of
+ *                  > 65536 slots, k <= 32 on the dense path of smaller stores);
+ *                  results are unchanged (exact re-rank + certificate).  Built on
+ *                  the first search or by "prepare".
  *   "prepare"      "1": build the int8 scan copy now (outside any timing)
  *   "scan_copy"    "on" (default) | "off": an f32 store may keep a bf16 copy of
  *                  its rows for the scans the int8 copy does not serve (k > 32,

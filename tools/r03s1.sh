@@ -1,0 +1,10 @@
+# session-2 check of round-3 HEAD on one MI355X: GPU suite, smoke, C2 + nstar lines
+source tools/gpu_step.sh
+T=${1:-r03s1}
+step ${T}_pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+step ${T}_smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+step ${T}_bench_c2 300 python -u bench.py --steps 20
+step ${T}_bench_nstar 600 python -u bench.py --config nstar --steps 10 --recall-queries 64 --cpu-seconds 10
+step ${T}_trace_c2 300 rocprofv3 --kernel-trace -d gpurun_out/${T}_trace_c2 -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-recall
+step ${T}_trace_c2s8 300 rocprofv3 --kernel-trace -d gpurun_out/${T}_trace_c2s8 -o run -- python3 bench.py --n 125000 --steps 5 --warmup 2 --no-cpu-baseline --no-recall
+LANCE_HIP_LIB=abl/lib_PRPROF.so step ${T}_prprof_c2 300 python3 -u bench.py --steps 5 --warmup 8 --no-cpu-baseline --no-recall
