@@ -61,7 +61,8 @@ def main():
         if os.path.isdir(fd) and os.path.isdir(wd):
             subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), fd, wd,
                             os.path.join(P, f"{out}_{cfg}_scan_traffic.json"), "--n", str(n), "--dim", str(dim),
-                            "--batch", str(batch), "--elem-bytes", "1", "--kernel", "scan8_kernel"], check=True)
+                            "--batch", str(batch), "--elem-bytes", "1", "--kernel", "scan8_kernel",
+                            "--bench-kernel", "scan8_kernel<L2,append,i8>"], check=True)
         summ = {"kernel": "scan8_kernel", "config": cfg}
         for grp in ("tcc", "sq", "lds"):
             d = os.path.join(G, f"{tag}_pmc_{cfg}_{grp}")

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--batch", type=int, required=True)
     ap.add_argument("--elem-bytes", type=int, default=4, help="bytes per element the scan streams")
     ap.add_argument("--kernel", default="scan_kernel<0, 1>")
+    ap.add_argument("--bench-kernel", default=None, help="bench.py's roofline.kernel name the passes belong to")
     a = ap.parse_args()
     fk, nf = per_launch(a.fetch_dir, "FETCH_SIZE", a.kernel)
     wk, nw = per_launch(a.write_dir, "WRITE_SIZE", a.kernel)
@@ -45,6 +46,8 @@ def main():
            "hbm_read_bytes_corrected": read_b, "hbm_write_bytes": write_b,
            "traffic_bytes_per_launch": read_b + write_b,
            "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE as is; KiB -> bytes"}
+    if a.bench_kernel:
+        out["bench_kernel"] = a.bench_kernel
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
