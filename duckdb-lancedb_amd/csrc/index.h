@@ -106,6 +106,7 @@ struct Workspace {
 	DevBuf<int> rfq, rstat, rC;
 	DevBuf<int64_t> rL;
 	int *h_status = nullptr;    // pinned mirror of status
+	int *d_status_map = nullptr;  // its device-visible address (the threshold path writes it in place)
 	size_t h_status_n = 0;
 	DevBuf<uint32_t> cand_slot;
 	DevBuf<int64_t> out_l, fb_vals, fb_vals2, idx;
@@ -131,6 +132,9 @@ struct Workspace {
 		h_status = nullptr;
 		HIPCHK(hipHostMalloc(&h_status, n * sizeof(int)));
 		h_status_n = n;
+		void *dv = nullptr;
+		HIPCHK(hipHostGetDevicePointer(&dv, h_status, 0));
+		d_status_map = static_cast<int *>(dv);
 	}
 };
 

@@ -156,6 +156,8 @@ void launch_select_segments(const uint2 *seg_pool, const int *seg_cnt, int seg_c
 // bounds, tau_out[q] = their k-th smallest exact distance (+inf when fewer,
 // NaN when any is NaN).  refined[q] = rows refined, pool_total[q] = pool size
 // (-1 on overflow); both may be null.  n_seg <= 512, k <= MAX_CAND.
+// first chunk of pool_refine's final mode (development knob, option "pr_first"; process-wide)
+void pool_refine_set_first(int r);
 void launch_pool_refine(const StoreView &s, const QueryView &q, const uint2 *seg_pool, const int *seg_cnt,
                         int seg_cap, int n_seg, const float *tau, int k, int mode, int m_tau, int64_t live,
                         float *tau_out, int64_t *L, float *D, int *C, int *cert, int *refined, int *pool_total,

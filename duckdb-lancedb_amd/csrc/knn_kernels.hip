@@ -2392,7 +2392,9 @@ __device__ __forceinline__ void pr_bitonic(uint64_t *a, int P) {
 
 constexpr int PR_SEL = 1024;  // chunk capacity
 constexpr int PR_HB = 1024;   // histogram bins of a chunk selection
-constexpr int PR_R = 128;     // first chunk of the final pass (one round)
+constexpr int PR_R = 96;      // first chunk of the final pass (C2: ~80 rows lie below d_k; refined rows
+                              // are the kernel's HBM traffic: 96 refined 18 % fewer than 128 at equal
+                              // step time or better, r03s2)
 
 template <int METRIC, typename T>
 __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
@@ -2400,7 +2402,7 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
     const float *__restrict__ tau, const T *__restrict__ X, int ld, int dim, const float *__restrict__ Qf,
     const int64_t *__restrict__ labels, int k, int mode, int m_tau, int64_t live, float *__restrict__ tau_out,
     int64_t *__restrict__ outL, float *__restrict__ outD, int *__restrict__ outC, int *__restrict__ cert,
-    int *__restrict__ refined, int *__restrict__ pool_total, int prof_on) {
+    int *__restrict__ refined, int *__restrict__ pool_total, int prof_on, int r_first) {
 	__shared__ uint64_t keys[PR_CAP];
 	__shared__ uint32_t sel[PR_SEL];  // slots of the chunk being refined
 	__shared__ unsigned hist[PR_HB];
@@ -2408,7 +2410,7 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 	__shared__ int64_t cl[2][PR_MAXK + PR_CHUNK];
 	__shared__ unsigned sh[PR_WAVES];
 	__shared__ int s_over, s_nnan, s_dnan;
-	__shared__ unsigned s_nfin, s_knf, s_kmin, s_kmax, s_bstar, s_cum, s_below, s_ns, s_hi;
+	__shared__ unsigned s_nfin, s_knf, s_kmin, s_kmax, s_bstar, s_cum, s_below, s_ns, s_hi, s_pmin, s_pmax;
 	__shared__ unsigned segc[PR_THREADS];  // (big pools) segment counts
 	const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
 #ifdef LHIP_PR_PROF
@@ -2431,8 +2433,24 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 		s_dnan = 0;
 		s_nfin = 0;
 		s_knf = 0xFFFFFFFFu;
+		s_pmin = 0xFFFFFFFFu;
+		s_pmax = 0;
 	}
 	__syncthreads();
+	// statistics of the keys as they are gathered (one reduction below, no pass
+	// over the pool): finite count, NaN count, smallest non-finite key, the
+	// finite keys' range (the first chunk's histogram range)
+	unsigned g_nf = 0, g_nn = 0, g_knf = 0xFFFFFFFFu, g_kmn = 0xFFFFFFFFu, g_kmx = 0;
+	auto gstat = [&](uint32_t kk) {
+		if (kk < KEY_INF) {
+			++g_nf;
+			g_kmn = min(g_kmn, kk);
+			g_kmx = max(g_kmx, kk);
+		} else {
+			g_knf = min(g_knf, kk);
+		}
+		g_nn += kk == KEY_NAN ? 1u : 0u;
+	};
 	// ---- gather the pool (thread s < n_seg: segment s) ----------------------
 	unsigned c = 0;
 	if (t < n_seg) {
@@ -2525,9 +2543,10 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 			unsigned xm = 0xFFFFFFFFu;
 			each([&](uint2 e) {
 				const bool keep = e.x < KEY_INF && (int)((e.x - kmin) >> shift) <= bstar;
-				if (keep)
+				if (keep) {
 					keys[atomicAdd(&s_ns, 1u)] = ((uint64_t)e.x << 32) | e.y;
-				else
+					gstat(e.x);  // (finite: NaN bounds were counted over the whole pool above)
+				} else
 					xm = min(xm, e.x);
 			});
 #pragma unroll
@@ -2548,36 +2567,35 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 				if (i + u < cm) e[u] = seg[i + u];
 #pragma unroll
 			for (int u = 0; u < 8; ++u)
-				if (i + u < cm) keys[off + i + u] = ((uint64_t)e[u].x << 32) | e[u].y;
+				if (i + u < cm) {
+					keys[off + i + u] = ((uint64_t)e[u].x << 32) | e[u].y;
+					gstat(e[u].x);
+				}
 		}
+	}
+	// finite bounds (key < KEY_INF), NaN bounds, the smallest non-finite key and
+	// the finite range, from the gather (big: NaN bounds were counted over the
+	// whole pool above)
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) {
+		g_nf += __shfl_xor(g_nf, o, 64);
+		g_nn += __shfl_xor(g_nn, o, 64);
+		g_knf = min(g_knf, (unsigned)__shfl_xor(g_knf, o, 64));
+		g_kmn = min(g_kmn, (unsigned)__shfl_xor(g_kmn, o, 64));
+		g_kmx = max(g_kmx, (unsigned)__shfl_xor(g_kmx, o, 64));
+	}
+	if (lane == 0) {
+		if (g_nf) {
+			atomicAdd(&s_nfin, g_nf);
+			atomicMin(&s_pmin, g_kmn);
+			atomicMax(&s_pmax, g_kmx);
+		}
+		if (g_nn) atomicAdd(&s_nnan, (int)g_nn);
+		if (g_knf != 0xFFFFFFFFu) atomicMin(&s_knf, g_knf);
 	}
 	__syncthreads();
 	mark();
 	if (t == 0 && total > (unsigned)PR_CAP && !big) s_over = 1;
-	// finite bounds (key < KEY_INF), NaN bounds, the smallest non-finite key
-	// (big: NaN bounds were counted over the whole pool above)
-	{
-		unsigned nf = 0, nn = 0, knf = 0xFFFFFFFFu;
-		for (int i = t; i < n; i += PR_THREADS) {
-			const uint32_t kk = (uint32_t)(keys[i] >> 32);
-			nf += kk < KEY_INF ? 1u : 0u;
-			nn += kk == KEY_NAN ? 1u : 0u;
-			if (kk >= KEY_INF) knf = min(knf, kk);
-		}
-#pragma unroll
-		for (int o = 32; o > 0; o >>= 1) {
-			nf += __shfl_xor(nf, o, 64);
-			nn += __shfl_xor(nn, o, 64);
-			knf = min(knf, (unsigned)__shfl_xor(knf, o, 64));
-		}
-		if (lane == 0) {
-			atomicAdd(&s_nfin, nf);
-			atomicAdd(&s_nnan, (int)nn);
-			atomicMin(&s_knf, knf);
-		}
-	}
-	__syncthreads();
-	mark();
 	const int nfin = (int)s_nfin;
 	const float ftau = tau ? tau[q] : F_INF;
 	const float *qrow = Qf + (int64_t)q * ld;
@@ -2588,14 +2606,16 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 	// s_hi (every key in [lo, s_hi] is in it); -1 when more than PR_SEL keys share
 	// one value.
 	auto next_chunk = [&](unsigned lo, unsigned hi_goal, int R) -> int {
+		// every finite key (the first chunk): the range from the gather
+		const bool whole_range = lo == 0u && hi_goal == KEY_INF - 1u;
 		if (t == 0) {
-			s_kmin = 0xFFFFFFFFu;
-			s_kmax = 0;
+			s_kmin = whole_range ? s_pmin : 0xFFFFFFFFu;
+			s_kmax = whole_range ? s_pmax : 0u;
 			s_ns = 0;
 			s_hi = 0;
 		}
 		__syncthreads();
-		{
+		if (!whole_range) {
 			unsigned kmn = 0xFFFFFFFFu, kmx = 0;
 			for (int i = t; i < n; i += PR_THREADS) {
 				const uint32_t kk = (uint32_t)(keys[i] >> 32);
@@ -2693,7 +2713,7 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 				if (kt < lo) break;
 				hi_goal = min(kt, KEY_INF - 1u);
 			}
-			ns = next_chunk(lo, hi_goal, cnt >= k ? PR_SEL : PR_R);
+			ns = next_chunk(lo, hi_goal, cnt >= k ? PR_SEL : r_first);
 		}
 		mark();
 		if (ns == 0) break;
@@ -2710,16 +2730,17 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 				const int b0 = w * PW, nv = max(0, min(PW, nr - b0));
 #pragma unroll
 				for (int r = 0; r < PW; ++r) sl[r] = r < nv ? slots[sp + b0 + r] : 0u;
+				// this lane's label load in flight with the row loads
+				const int64_t lab = lane < nv ? labels[slots[sp + b0 + lane]] : 0;
 				float d[PW];
 				if (nv > 0) exact_distance_multi<METRIC, T, PW>(X, ld, sl, nv, qrow, dim, lane, d);
 				if (lane < nv) {
 					float dv = d[0];
-					uint32_t sv = sl[0];
 #pragma unroll
 					for (int r = 1; r < PW; ++r)
-						if (lane == r) dv = d[r], sv = sl[r];
+						if (lane == r) dv = d[r];
 					cd[cur][cnt + b0 + lane] = dv;
-					cl[cur][cnt + b0 + lane] = labels[sv];
+					cl[cur][cnt + b0 + lane] = lab;
 					if (__builtin_isnan(dv)) s_dnan = 1;
 				}
 			}
@@ -2869,6 +2890,9 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 	}
 }
 
+static int g_pr_first = PR_R;
+void pool_refine_set_first(int r) { g_pr_first = std::max(8, std::min(PR_SEL, r)); }
+
 template <typename T>
 static void pool_refine_dispatch(const StoreView &s, const QueryView &q, const uint2 *seg_pool, const int *seg_cnt,
                                  int seg_cap, int n_seg, const float *tau, int k, int mode, int m_tau,
@@ -2878,10 +2902,11 @@ static void pool_refine_dispatch(const StoreView &s, const QueryView &q, const u
 	const dim3 grid((unsigned)q.nq);
 	static int calls = 0;  // (LHIP_PR_PROF: the 12th final-mode launch of the process prints its phases)
 	const int prof_on = mode == 1 && ++calls == 12;
+	const int r_first = g_pr_first;
 #define LHIP_PR(MET)                                                                                                  \
 	pool_refine_kernel<MET, T><<<grid, PR_THREADS, 0, st>>>(seg_pool, seg_cnt, seg_cap, n_seg, q.nq, tau, X, s.ld,   \
 	                                                        s.dim, q.Qf, s.labels, k, mode, m_tau, live, tau_out, L, \
-	                                                        D, C, cert, refined, pool_total, prof_on)
+	                                                        D, C, cert, refined, pool_total, prof_on, r_first)
 	switch (s.metric) {
 	case METRIC_L2: LHIP_PR(METRIC_L2); break;
 	case METRIC_DOT: LHIP_PR(METRIC_DOT); break;

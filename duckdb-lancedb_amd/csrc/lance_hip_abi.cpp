@@ -95,16 +95,28 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	ws.cut.need(nq);
 	ws.cand_slot.need((size_t)nq * MAX_CAND);
 	ws.cand_dist.need((size_t)nq * MAX_CAND);
-	ws.status.need((size_t)3 * nq);
 	ws.need_host_status((size_t)3 * nq);
-	int *d_cert = ws.status.p, *d_cand_cnt = ws.status.p + nq, *d_pool_cnt = ws.status.p + 2 * nq;
+	// [cert | cand_cnt | pool_cnt]: on the threshold path the kernels write it
+	// straight into pinned host memory (only pool_refine / retry_scatter store
+	// into it, no kernel reads it back), so the step ends with one stream wait
+	// and no readback copy; the dense path keeps it in HBM (its refine and
+	// finalize read the candidate counts) and copies it back once
+	const bool hmap = n_slots > 65536;
+	int *dstat;
+	if (hmap) {
+		dstat = ws.d_status_map;
+	} else {
+		ws.status.need((size_t)3 * nq);
+		dstat = ws.status.p;
+	}
+	int *d_cert = dstat, *d_cand_cnt = dstat + nq, *d_pool_cnt = dstat + 2 * nq;
 	if (use8) {
 		ws.qm.need(nq);
 		launch_prep_queries_i8(dQ, nq, dim, ld, nq_pad, eff_metric, max_alpha8, max_x8, ws.qm.p, ws.Qf.p, ws.Qb.p,
-		                       ws.qaux.p, ws.status.p, stream);
+		                       ws.qaux.p, dstat, stream);
 	}
 	else
-		launch_prep_queries(dQ, nq, dim, ld, nq_pad, eff_metric, ma, mu, ws.Qf.p, ws.Qb.p, ws.qaux.p, ws.status.p,
+		launch_prep_queries(dQ, nq, dim, ld, nq_pad, eff_metric, ma, mu, ws.Qf.p, ws.Qb.p, ws.qaux.p, dstat,
 		                    stream);
 	QueryView qv{ws.Qf.p, ws.Qb.p, ws.qaux.p, nq, nq_pad};
 
@@ -191,8 +203,10 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	}
 	HIPCHK(hipGetLastError());
 
-	// one pinned readback of [cert | cand_cnt | pool_cnt]
-	HIPCHK(hipMemcpyAsync(ws.h_status, ws.status.p, (size_t)3 * nq * sizeof(int), hipMemcpyDeviceToHost, stream));
+	// [cert | cand_cnt | pool_cnt] on the host: written in place (threshold
+	// path) or one pinned readback (dense path)
+	if (!hmap)
+		HIPCHK(hipMemcpyAsync(ws.h_status, ws.status.p, (size_t)3 * nq * sizeof(int), hipMemcpyDeviceToHost, stream));
 	spin_sync(stream);
 	if (time_kernels && !all_fallback && last_stats[3] == 0) {
 		// the append scan's own time (both launches of a progressive pass)
@@ -252,7 +266,8 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 			launch_retry_scatter(ws.rfq.p, nf, k, ws.rL.p, ws.rD.p, ws.rC.p, cert2, ws.rtau.p, dL, dD, dC, d_cert, ws.tau.p,
 			                     stream);
 			HIPCHK(hipGetLastError());
-			HIPCHK(hipMemcpyAsync(ws.h_status, d_cert, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, stream));
+			if (!hmap)
+				HIPCHK(hipMemcpyAsync(ws.h_status, d_cert, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, stream));
 			spin_sync(stream);
 		}
 	}
@@ -1093,6 +1108,10 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			// of on the first search after a change
 			ix->bind();
 			if (ix->i8_usable()) ix->ensure_i8();
+			return 0;
+		}
+		if (k == "pr_first") {  // development knob (all pool_refine launches of the process)
+			lhip::pool_refine_set_first(std::stoi(v));
 			return 0;
 		}
 		if (k == "scan8_variant") {  // development knob (all ld = 768 scans of the process)

@@ -109,7 +109,11 @@ def hip_device_search(lib, handle, dim: int, nprobes: int = 20, refine_factor: i
             if reuse_outputs:
                 cache[key] = outs
         ol, od, oc = outs
-        torch.cuda.current_stream().synchronize()  # Q written on torch's stream
+        # Q written on torch's stream: wait for it only when that stream still has
+        # work (a query of an idle stream costs ~1 us, a synchronize ~15 us)
+        cs = torch.cuda.current_stream()
+        if not cs.query():
+            cs.synchronize()
         r = fn(handle, Q.data_ptr(), nq, dim, k, nprobes, refine_factor, ol.data_ptr(), od.data_ptr(), oc.data_ptr(),
                e, err_len)
         if r < 0:

@@ -223,6 +223,8 @@ int32_t lance_hip_device_count(void);
  *                  (lance_hip_kernel_times); default "0"
  *   "scan8_variant" development knob: geometry of the int8 append kernel at
  *                  dim 768 (rows per wave, register ring depth); "0" = default
+ *   "pr_first"     development knob: bounds refined in the first chunk of the
+ *                  final threshold-path refine (process-wide), default "128"
  * The handle is bound to the HIP device current when it was created.
  * Returns 0 or -1. */
 int32_t lance_hip_set_option(void *handle, const char *key, const char *value, char *err_buf, int err_buf_len);
