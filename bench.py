@@ -37,7 +37,16 @@ for _p in (ROOT, PKG):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-import lance_hip  # noqa: E402
+lance_hip = None  # loaded by _load_lib() in the ranks (the --gpus N parent never touches the GPU)
+
+
+def _load_lib():
+    global lance_hip
+    if lance_hip is None:
+        import lance_hip as _lh
+
+        lance_hip = _lh
+    return lance_hip
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 MFMA_BF16_PEAK_TFS = 2500.0  # dense bf16 MFMA (no sparsity), same table
@@ -79,8 +88,16 @@ def parse():
     ap.add_argument("--metric", default=None)
     ap.add_argument("--storage", choices=["f32", "bf16"], default=None, help="index option storage")
     ap.add_argument("--scan-copy", choices=["on", "off"], default="on", help="index option scan_copy")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                    help="multi-GPU: weak = global batch B x world, strong = global batch B")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+                    help="multi-GPU (flat configs): strong (default, SURVEY.md §8e) = the global batch B over N/world "
+                         "rows per rank; weak = global batch B x world. With --gpus > 1 the other mode is timed too "
+                         "and reported under its own key")
+    ap.add_argument("--no-other-scaling", action="store_true", help="multi-GPU: skip the extra weak/strong leg")
+    ap.add_argument("--no-host-batch", action="store_true",
+                    help="N = 1 flat configs: skip the extra host-buffer leg (H2D + D2H timed, SURVEY.md §8d QPS)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: ranks join a gloo group and time a CPU stand-in step "
+                         "through the same barrier / max-over-ranks code (tests/test_bench_launcher_cpu.py)")
     ap.add_argument("--recall-queries", type=int, default=None, help="default: the whole batch")
     ap.add_argument("--cpu-threads", type=int, default=None, help="default: every core this job may use")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -112,6 +129,105 @@ def parse():
         if not hasattr(a, key) or getattr(a, key) is None:
             setattr(a, key, None)
     return a
+
+
+def _free_port():
+    import socket
+
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    port = so.getsockname()[1]
+    so.close()
+    return port
+
+
+def launch_ranks(a):
+    """`bench.py --gpus N` with no WORLD_SIZE in the environment: start N fresh
+    rank processes (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set,
+    RCCL backend), BEFORE this process makes any GPU call; only rank 0's JSON
+    line reaches stdout.  Returns the exit status (the first failing rank's)."""
+    import subprocess
+
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for o in live:  # a rank failed: the others would wait in a collective
+                    o.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def timed_steps(step, steps, warmup, dist, device, sync):
+    """W untimed steps, then EXACTLY K steps bracketed by a barrier + device sync
+    on both sides; returns (max over ranks of the elapsed seconds, the last
+    step's result, per-step host marks)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    marks = []
+    res = None
+    for _ in range(steps):
+        res = step()
+        marks.append(time.perf_counter())
+    sync()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
+    if dist:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    return float(elapsed.item()), res, np.diff(np.array([t0] + marks)) * 1e3
+
+
+def main_dry_run(a):
+    """--dry-run: the rank launch, process group, barrier and max-over-ranks
+    timing of a real run, with a CPU stand-in step on gloo (no GPU, no library)."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    x = torch.randn(64, 64)
+
+    def step():
+        return x @ x
+
+    t, _, _ = timed_steps(step, a.steps, a.warmup, dist, "cpu", lambda: None)
+    ranks = torch.tensor([rank], dtype=torch.int64)
+    if dist:
+        allr = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(allr, ranks)
+        seen = sorted(int(v.item()) for v in allr)
+    else:
+        seen = [rank]
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (launcher check, no GPU)", "value": a.steps / t, "unit": "steps/s",
+                          "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                          "ms_per_step": round(1000.0 * t / a.steps, 4), "higher_is_better": True,
+                          "scaling": a.scaling, "dry_run": True, "ranks_seen": seen,
+                          "pids_differ": bool(dist) and world > 1}), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def gen_rows(start, stop, dim, device, seed=1234, normalize=False):
@@ -513,6 +629,18 @@ def main_c1(a):
 
 def main():
     a = parse()
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        # one process per GPU, started here (the driver may also start them with
+        # torch.distributed.run, which sets WORLD_SIZE)
+        return launch_ranks(a)
+    if env_world is not None and int(env_world) != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={env_world}: launch one rank per GPU")
+    if a.dry_run:
+        return main_dry_run(a)
+    _load_lib()
     if a.config == "c1":
         return main_c1(a)
     if a.index_type:
@@ -560,7 +688,7 @@ def main():
     lance_hip.LanceHipSetOption(h, "prepare", "1")
     g = torch.Generator(device=dev)
     g.manual_seed(5678)
-    # global batch: weak = B per rank (per-GPU flops fixed), strong = B in all
+    # global batch: strong (default) = B in all, weak = B per rank (per-GPU flops fixed)
     BG = B * world if a.scaling == "weak" else B
     Q = torch.randn((BG, D), generator=g, device=dev, dtype=torch.float32)
     if a.normalize:
@@ -573,7 +701,7 @@ def main():
 
     if a.api != "device" and world > 1:
         raise SystemExit("--api host_batch / per_call: one GPU (the host C-ABI is unsharded)")
-    Qh_api = Q.cpu().numpy() if a.api != "device" else None
+    Qh_api = Q.cpu().numpy() if (a.api != "device" or (world == 1 and not a.no_host_batch)) else None
     call_i = [0]
 
     def step():
@@ -585,31 +713,43 @@ def main():
             return lance_hip.LanceDetachedSearch(h, Qh_api[i], D, K)
         return searcher.search(Q, K, reuse_outputs=True)
 
+    # warmup for per_call: the timed calls then start at query 0 (the recall subset below)
     for _ in range(a.warmup):
         step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    call_i[0] = 0  # per_call: the timed calls start at query 0 (the recall subset below)
-    t0 = time.perf_counter()
-    marks = []
+    call_i[0] = 0
     per_call_l = []
-    for _ in range(a.steps):
-        res = step()
-        marks.append(time.perf_counter())
+
+    def step_rec():
+        r = step()
         if a.api == "per_call" and len(per_call_l) < BG:
-            per_call_l.append(res[0])
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if dist:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    t = float(elapsed.item())
+            per_call_l.append(r[0])
+        return r
+
+    t, res, per = timed_steps(step_rec, a.steps, 0, dist, dev, torch.cuda.synchronize)
     st = lance_hip.LanceHipLastSearchStats(h)
-    per = np.diff(np.array([t0] + marks)) * 1e3
     print(f"[bench] per-step ms: min {per.min():.4f} median {np.median(per):.4f} max {per.max():.4f}", file=sys.stderr)
+    # extra legs (never `value`): the other multi-GPU scaling mode, and at N = 1
+    # the host-buffer C-ABI (H2D queries + D2H results inside the step: SURVEY.md
+    # §8(d)'s QPS definition) beside the device-resident figure
+    other = None
+    if world > 1 and a.api == "device" and not a.no_other_scaling:
+        om = "weak" if a.scaling == "strong" else "strong"
+        BO = B * world if om == "weak" else B
+        Qo = torch.randn((BO, D), generator=g, device=dev, dtype=torch.float32)
+        if a.normalize:
+            Qo /= torch.linalg.vector_norm(Qo, dim=1, keepdim=True)
+        to, _, _ = timed_steps(lambda: searcher.search(Qo, K), a.steps, a.warmup, dist, dev, torch.cuda.synchronize)
+        other = {"scaling": om, "value": round(BO * a.steps / to, 1), "unit": "queries/s",
+                 "ms_per_step": round(1000.0 * to / a.steps, 4), "global_batch": BO,
+                 "rows_per_gpu": n_local}
+        del Qo
+    hostb = None
+    if world == 1 and a.api == "device" and not a.no_host_batch:
+        th, rh, _ = timed_steps(lambda: lance_hip.LanceDetachedSearchBatch(h, Qh_api, K), a.steps, a.warmup, None,
+                                dev, torch.cuda.synchronize)
+        hostb = {"value": round(BG * a.steps / th, 1), "unit": "queries/s", "ms_per_step": round(1000.0 * th / a.steps, 4),
+                 "api": "lance_detached_search_batch (host query / result buffers, H2D + D2H timed)",
+                 "ids_equal_device": bool((rh[0] == res[0].cpu().numpy()).all())}
     # the scan kernel's own duration (HIP events on the stream it runs on),
     # from separate steps so the event calls stay out of the timed loop above
     lance_hip.LanceHipSetOption(h, "time_kernels", "1")
@@ -755,6 +895,10 @@ def main():
             "cpu_baseline": cpu,
             "search_stats": st,
         }
+        if other:
+            line[f"{other['scaling']}_scaling"] = other
+        if hostb:
+            line["host_batch"] = hostb
         if recall is not None:
             line[f"recall_at_{K}"] = recall_k
             line["exact_ids_on_recall_subset"] = exact_ids
@@ -767,4 +911,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -230,7 +230,7 @@ struct Index {
 	bool ivf_flat_bound = true;  // IVF_FLAT list scan by MFMA bf16 lower bounds + certified exact re-rank (option "ivf_flat_scan" = "bound" | "exact")
 	int64_t ivf_flat_fallbacks = 0;  // batches the bound scan could not certify (rerun exactly)    // IVF_PQ ADC tables from e4m3 (fp8) queries (option "pq_query" = "fp8" | "f32")
 
-	int64_t last_stats[5] = {0, 0, 0, 0, 0};
+	int64_t last_stats[6] = {0, 0, 0, 0, 0, 0};
 
 	// optional HIP-event timing of the scan kernels, on the stream they run on
 	bool time_kernels = false;
@@ -243,6 +243,8 @@ struct Index {
 	// progressive threshold (int8 append pass): the first 1/split_div of the tiles
 	// with the sample's tau, then the rest with the tau their pool gives (0: one pass)
 	int split_div = 0;
+	int pr_first = 0;    // option "pr_first": pool_refine's first final-mode chunk (0 = the kernel's default)
+	int s8_variant = 0;  // option "scan8_variant": scan8 geometry (release builds: 0 only)
 	double kt_append_ms = 0.0, kt_dense_ms = 0.0;
 	int64_t kt_append_n = 0, kt_dense_n = 0;
 	int64_t kt_append_rows = 0, kt_append_qpad = 0;

@@ -45,6 +45,11 @@ struct StoreView {
 	int scan_i8 = 0;
 	// int8 scan copy: per row tile (s_T, max |e_x|, max |x~|, 0)
 	const float4 *tstat = nullptr;
+	// per-handle tuning (results exact for every accepted value): pool_refine's
+	// first final-mode chunk (0 = default), the ld = 768 scan8 geometry (0 =
+	// default; other values only in LHIP_ABLATION_BUILD builds)
+	int pr_first = 0;
+	int s8_variant = 0;
 };
 
 // Per-query constants for the lower-bound epilogue:
@@ -130,7 +135,7 @@ int scan_grid(int64_t n_tiles);
 // launches over disjoint ranges fill disjoint segment sets of one pool.
 bool scan8_fits(const StoreView &s);
 int scan8_segments(int64_t n_tiles);
-void scan8_set_variant(int v);  // development knob: geometry of the ld = 768 kernel (0 = default)
+bool scan8_variant_ok(int v);  // a geometry this build carries (release: 0 only)
 void launch_scan8_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
                          int seg_cap, hipStream_t st, int64_t t0 = 0, int64_t t1 = -1, int seg_base = 0);
 // Segments per query launch_scan_append writes for this store.
@@ -156,8 +161,9 @@ void launch_select_segments(const uint2 *seg_pool, const int *seg_cnt, int seg_c
 // bounds, tau_out[q] = their k-th smallest exact distance (+inf when fewer,
 // NaN when any is NaN).  refined[q] = rows refined, pool_total[q] = pool size
 // (-1 on overflow); both may be null.  n_seg <= 512, k <= MAX_CAND.
-// first chunk of pool_refine's final mode (development knob, option "pr_first"; process-wide)
-void pool_refine_set_first(int r);
+// first chunk of pool_refine's final mode: StoreView::pr_first (handle option
+// "pr_first"), clamped to [8, pool_refine_max_first()]
+int pool_refine_max_first();
 void launch_pool_refine(const StoreView &s, const QueryView &q, const uint2 *seg_pool, const int *seg_cnt,
                         int seg_cap, int n_seg, const float *tau, int k, int mode, int m_tau, int64_t live,
                         float *tau_out, int64_t *L, float *D, int *C, int *cert, int *refined, int *pool_total,

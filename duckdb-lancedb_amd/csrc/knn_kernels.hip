@@ -18,6 +18,7 @@
 //   exact_all/sort fallback for a query whose certificate failed
 //
 // No hipify, no CUDA shims: wave64, MFMA and LDS idioms written for CDNA4.
+#include <atomic>
 #include "knn_kernels.h"
 
 #include <cstring>
@@ -1618,15 +1619,14 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void scan_kernel(const void *__res
 }
 
 static int num_cus() {
-	static int n = 0;
-	if (n == 0) {
+	// (a function-local static: initialised once, thread-safe, C++11)
+	static const int n = [] {
 		int dev = 0, v = 0;
-		if (hipGetDevice(&dev) == hipSuccess &&
-		    hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-			n = v;
-		else
-			n = 256;
-	}
+		return (hipGetDevice(&dev) == hipSuccess &&
+		        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+		           ? v
+		           : 256;
+	}();
 	return n;
 }
 
@@ -2890,8 +2890,7 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 	}
 }
 
-static int g_pr_first = PR_R;
-void pool_refine_set_first(int r) { g_pr_first = std::max(8, std::min(PR_SEL, r)); }
+int pool_refine_max_first() { return PR_SEL; }
 
 template <typename T>
 static void pool_refine_dispatch(const StoreView &s, const QueryView &q, const uint2 *seg_pool, const int *seg_cnt,
@@ -2900,9 +2899,13 @@ static void pool_refine_dispatch(const StoreView &s, const QueryView &q, const u
                                  int *pool_total, hipStream_t st) {
 	const T *X = static_cast<const T *>(s.X);
 	const dim3 grid((unsigned)q.nq);
-	static int calls = 0;  // (LHIP_PR_PROF: the 12th final-mode launch of the process prints its phases)
+#ifdef LHIP_PR_PROF
+	static std::atomic<int> calls{0};  // (diagnostic build: the 12th final-mode launch of the process prints its phases)
 	const int prof_on = mode == 1 && ++calls == 12;
-	const int r_first = g_pr_first;
+#else
+	const int prof_on = 0;
+#endif
+	const int r_first = s.pr_first > 0 ? std::max(8, std::min(PR_SEL, s.pr_first)) : PR_R;
 #define LHIP_PR(MET)                                                                                                  \
 	pool_refine_kernel<MET, T><<<grid, PR_THREADS, 0, st>>>(seg_pool, seg_cnt, seg_cap, n_seg, q.nq, tau, X, s.ld,   \
 	                                                        s.dim, q.Qf, s.labels, k, mode, m_tau, live, tau_out, L, \
@@ -3409,8 +3412,12 @@ static void small_exact_dispatch(const StoreView &s, const float *Q, int nq, int
 	const dim3 grid((unsigned)small_exact_grid(s.n_slots), (unsigned)nq);
 	const T *X = static_cast<const T *>(s.X);
 	SHit *p = static_cast<SHit *>(part);
-	static int calls = 0;  // (LHIP_SE_PROF: the 200th launch of the process prints its phases)
+#ifdef LHIP_SE_PROF
+	static std::atomic<int> calls{0};  // (diagnostic build: the 200th launch of the process prints its phases)
 	const int se_prof = ++calls == 200;
+#else
+	const int se_prof = 0;
+#endif
 	switch (s.metric) {
 	case METRIC_L2:
 		small_exact_kernel<METRIC_L2, T><<<grid, SMALL_THREADS, 0, st>>>(X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim, Q,

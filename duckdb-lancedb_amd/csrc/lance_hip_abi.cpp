@@ -34,7 +34,7 @@
 namespace lhip {
 
 void Index::search_device(const float *dQ, int nq, int k, int refine, int64_t *dL, float *dD, int *dC) {
-	last_stats[0] = last_stats[1] = last_stats[2] = last_stats[3] = last_stats[4] = 0;
+	for (auto &v : last_stats) v = 0;
 	// one pipeline pass covers up to MAX_PASS_Q queries (several query tiles
 	// per scan launch): the per-pass fixed cost is paid once per pass
 	for (int s = 0; s < nq; s += MAX_PASS_Q) {
@@ -58,6 +58,8 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	const float mu = (metric_quirk && metric != METRIC_L2) ? max_ux_l2 : max_ux;
 	StoreView sv{X, aux, dlabels, n_slots, ld, dim, eff_metric, xbf16 ? 1 : 0,
 	             Xs ? static_cast<const void *>(Xs) : X, (xbf16 || Xs) ? 1 : 0};
+	sv.pr_first = pr_first;
+	sv.s8_variant = s8_variant;
 	last_scan_esz = use8 ? 1 : (xbf16 || Xs) ? 2 : 4;
 	if (use8) {
 		ensure_i8();
@@ -185,6 +187,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		ws.seg_pool.need((size_t)n_seg * nq * seg_cap + (size_t)n_seg * (nq_pad / SCAN_BQ));  // + per-workgroup sink
 		ws.seg_cnt.need((size_t)n_seg * nq);
 		tic(2);
+		last_stats[5] += tA ? 2 : 1;  // threshold append launches of the first pass
 		if (tA) {
 			launch_scan8_append(sv, qv, ws.tau.p, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, stream, 0, tA, 0);
 			tic(3);
@@ -1110,12 +1113,18 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			if (ix->i8_usable()) ix->ensure_i8();
 			return 0;
 		}
-		if (k == "pr_first") {  // development knob (all pool_refine launches of the process)
-			lhip::pool_refine_set_first(std::stoi(v));
+		if (k == "pr_first") {  // this handle's first final-mode pool_refine chunk (results exact for any value)
+			const int r = std::stoi(v);
+			if (r != 0 && (r < 8 || r > lhip::pool_refine_max_first()))
+				throw Error("pr_first must be 0 (default) or in [8, " + std::to_string(lhip::pool_refine_max_first()) + "]");
+			ix->pr_first = r;
 			return 0;
 		}
-		if (k == "scan8_variant") {  // development knob (all ld = 768 scans of the process)
-			lhip::scan8_set_variant(std::stoi(v));
+		if (k == "scan8_variant") {  // this handle's ld = 768 scan8 geometry; release builds: 0 only
+			const int r = std::stoi(v);
+			if (!lhip::scan8_variant_ok(r))
+				throw Error("scan8_variant " + v + " exists only in development (LHIP_ABLATION_BUILD) builds");
+			ix->s8_variant = r;
 			return 0;
 		}
 		if (k == "cand_extra_i8") {
@@ -1202,7 +1211,7 @@ int32_t lance_hip_last_search_stats(void *handle, int64_t *out, int32_t n) {
 	if (!handle || !out) return -1;
 	Index *ix = as_index(handle);
 	std::lock_guard<std::mutex> g(ix->mu);
-	for (int32_t i = 0; i < n && i < 5; ++i) out[i] = ix->last_stats[i];
+	for (int32_t i = 0; i < n && i < 6; ++i) out[i] = ix->last_stats[i];
 	return 0;
 }
 

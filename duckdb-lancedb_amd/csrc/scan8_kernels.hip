@@ -440,14 +440,14 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 // workgroups of a launch over n_tiles row tiles: one per CU, an even count
 // (pairs), at most two per tile
 static int s8_groups(int64_t n_tiles) {
-	static int cus = 0;
-	if (cus == 0) {
+	// (a function-local static: initialised once, thread-safe, C++11)
+	static const int cus = [] {
 		int dev = 0, v = 0;
-		cus = (hipGetDevice(&dev) == hipSuccess &&
-		       hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v >= 2)
-		          ? v
-		          : 256;
-	}
+		return (hipGetDevice(&dev) == hipSuccess &&
+		        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v >= 2)
+		           ? v
+		           : 256;
+	}();
 	return (int)(2 * std::max<int64_t>(1, std::min<int64_t>(cus / 2, n_tiles)));
 }
 
@@ -463,11 +463,12 @@ static int s8_list_cap(int ld, int nw) {
 	return std::min(1024, room / (nw * 9) / 64 * 64);
 }
 
-static int g_s8_variant = 0;
-
 template <int KS, int D, int RB, int ABL = 0>
 static void s8_launch(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
                       int seg_cap, int64_t t0, int64_t n_tiles, int seg_base, hipStream_t st) {
+#ifndef LHIP_ABLATION_BUILD
+	static_assert(ABL == 0, "scan8 ablations (wrong results) exist only in LHIP_ABLATION_BUILD builds");
+#endif
 	const dim3 grid((unsigned)s8_groups(n_tiles), (unsigned)(q.nq_pad / SCAN_BQ));
 	constexpr int NW = 16 / RB;
 	scan8_kernel<KS, D, RB, ABL><<<grid, dim3(64 * NW), 0, st>>>(
@@ -475,10 +476,13 @@ static void s8_launch(const StoreView &s, const QueryView &q, const float *tau, 
 	    q.nq, (int)n_tiles, (int)t0, seg_base, tau, seg_pool, seg_cnt, seg_cap, s8_list_cap(s.ld, NW));
 }
 
-// geometry of the ld = 768 kernel (development knob, option "scan8_variant"):
-// 16-row blocks per wave (4: four waves, one per SIMD; 2: eight waves) and the
-// register ring depth in 64-deep k-steps
-void scan8_set_variant(int v) { g_s8_variant = v; }
+bool scan8_variant_ok(int v) {
+#ifdef LHIP_ABLATION_BUILD
+	return v >= 0;
+#else
+	return v == 0;  // release builds carry the default geometry only
+#endif
+}
 
 void launch_scan8_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
                          int seg_cap, hipStream_t st, int64_t t0, int64_t t1, int seg_base) {
@@ -490,11 +494,16 @@ void launch_scan8_append(const StoreView &s, const QueryView &q, const float *ta
 	if (!scan8_fits(s)) throw std::runtime_error("scan8: int8 scan copy with ld in [512, 1024] required");
 	if (all_tiles * (int64_t)SCAN_BR > ((int64_t)1 << 32)) throw std::runtime_error("scan8: slots past 2^32");
 	if (q.nq_pad % SCAN_BQ) throw std::runtime_error("scan8: query tile padding");
+	if (!scan8_variant_ok(s.s8_variant)) throw std::runtime_error("scan8: geometry variant of a development build");
 	switch (s.ld / 64) {
 	case 8: s8_launch<8, 4, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
 	case 10: s8_launch<10, 5, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
 	case 12:
-		switch (g_s8_variant) {
+		switch (s.s8_variant) {
+#ifdef LHIP_ABLATION_BUILD
+		// development geometries (handle option "scan8_variant"): 16-row blocks per
+		// wave (4: four waves, one per SIMD; 2: eight waves), register ring depth in
+		// 64-deep k-steps; ABL != 0: timing ablations (wrong results, 8: setprio)
 		case 1: s8_launch<12, 4, 4>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
 		case 2: s8_launch<12, 6, 4>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
 		case 3: s8_launch<12, 12, 4>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
@@ -508,6 +517,7 @@ void launch_scan8_append(const StoreView &s, const QueryView &q, const float *ta
 		case 28: s8_launch<12, 4, 2, 8>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
 		case 34: s8_launch<12, 4, 2, 64>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
 		case 29: s8_launch<12, 6, 2, 8>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+#endif
 		default: s8_launch<12, 4, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
 		}
 		break;

@@ -405,10 +405,11 @@ def LanceHipSetOption(handle, key: str, value: str) -> None:
 
 
 def LanceHipLastSearchStats(handle) -> dict:
-    out = np.zeros(5, np.int64)
-    lib().lance_hip_last_search_stats(handle, out.ctypes.data, 5)
+    out = np.zeros(6, np.int64)
+    lib().lance_hip_last_search_stats(handle, out.ctypes.data, 6)
     return {"fallback_queries": int(out[0]), "refined": int(out[1]), "max_pool": int(out[2]),
-            "dense_path": bool(out[3]), "small_exact": int(out[3]) == 2, "retried_queries": int(out[4])}
+            "dense_path": bool(out[3]), "small_exact": int(out[3]) == 2, "retried_queries": int(out[4]),
+            "append_launches": int(out[5])}
 
 
 def LanceHipKernelTimes(handle) -> dict:

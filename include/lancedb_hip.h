@@ -221,10 +221,13 @@ int32_t lance_hip_device_count(void);
  *                  re-rank keep the f32 query
  *   "time_kernels" "1" = record HIP events around scan launches
  *                  (lance_hip_kernel_times); default "0"
- *   "scan8_variant" development knob: geometry of the int8 append kernel at
- *                  dim 768 (rows per wave, register ring depth); "0" = default
- *   "pr_first"     development knob: bounds refined in the first chunk of the
- *                  final threshold-path refine (process-wide), default "128"
+ *   "scan8_variant" geometry of the int8 append kernel at dim 768: "0" (the
+ *                  default) is the only value a release build accepts; other
+ *                  geometries and timing ablations exist only in development
+ *                  builds (LHIP_ABLATION_BUILD) and are rejected here (-1)
+ *   "pr_first"     bounds refined in the first chunk of the final
+ *                  threshold-path refine, this handle only: "0" = the default
+ *                  (96), else 8..1024; results are exact for every value
  * The handle is bound to the HIP device current when it was created.
  * Returns 0 or -1. */
 int32_t lance_hip_set_option(void *handle, const char *key, const char *value, char *err_buf, int err_buf_len);
@@ -238,7 +241,9 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
  * k <= 64, dim <= 4096), out[4] = queries rerun by the
  * second threshold pass (option "retry_pass", default on: an uncertified
  * query is rescanned with tau = its first-pass k-th exact distance and
- * full-size segments before it may take the exact fallback).  Returns 0 or -1. */
+ * full-size segments before it may take the exact fallback), out[5] = launches
+ * of the threshold append scan in the first pass (2 with option "split_div").
+ * Returns 0 or -1. */
 int32_t lance_hip_last_search_stats(void *handle, int64_t *out, int32_t n);
 
 /* Per-handle HIP-event timings of the scan kernels (enable with option

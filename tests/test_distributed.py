@@ -151,6 +151,74 @@ def test_sharded_hip_search_two_ranks_one_gpu():
         np.testing.assert_allclose(dd, ed, rtol=1e-4, atol=1e-5)
 
 
+def _gpu_scan8_worker(rank, world, port, n, d, k, q, out):
+    # the bench's flat multi-GPU flow on the DEFAULT large-store path: each shard
+    # > 65536 rows at d = 768 takes the threshold pipeline (sample pass, int8
+    # scan8_kernel append pass, pool_refine), per-shard lists gathered and merged
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    import lance_hip
+    from lance_hip.sharded import hip_device_merge, hip_device_search
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    L = lance_hip.lib()
+    rng = np.random.default_rng(21)
+    X = rng.standard_normal((n, d), dtype=np.float32)
+    Q = rng.standard_normal((q, d), dtype=np.float32)
+    s0, s1 = shard_range(n, world, rank)
+    h = lance_hip.LanceCreateDetached("", d, "l2", f"s8shard{rank}")
+    for lo in range(s0, s1, 1 << 16):
+        hi = min(s1, lo + (1 << 16))
+        lance_hip.LanceDetachedAddBatch(h, X[lo:hi], hi - lo, d)
+    del X
+    lance_hip.LanceHipSetOption(h, "time_kernels", "1")
+    dev_search = hip_device_search(L, h, d)
+    dev_merge = hip_device_merge(L)
+
+    def local_search(Qt, kk):
+        l, dd, c = dev_search(Qt.cuda(), kk)
+        return l.cpu(), dd.cpu(), c.cpu()
+
+    def merge(gl, gd, gc):
+        l, dd, c = dev_merge(gl.cuda(), gd.cuda(), gc.cuda())
+        return l.cpu(), dd.cpu(), c.cpu()
+
+    s = ShardedSearch(local_search, merge, label_offset=s0, dist=dist, world=world)
+    l, dd, c = s.search(torch.from_numpy(Q), k)
+    st = lance_hip.LanceHipLastSearchStats(h)
+    kt = lance_hip.LanceHipKernelTimes(h)
+    out[rank] = (l.numpy(), dd.numpy(), c.numpy(), st, kt["scan_kernel"], kt["scan_launches"])
+    lance_hip.LanceFreeDetached(h)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_scan8_two_ranks_one_gpu():
+    """2 ranks x 80k rows x 768, 256 queries: every rank's shard search is the
+    int8 threshold path (scan8_kernel + pool_refine, certified, no fallback);
+    the merged top-10 equals the unsharded exact search (f64 C oracle)."""
+    from oracle import c_oracle
+
+    world, n, d, k, q = 2, 160_000, 768, 10, 256
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_gpu_scan8_worker, args=(world, _free_port(), n, d, k, q, out), nprocs=world, join=True)
+    rng = np.random.default_rng(21)
+    X = rng.standard_normal((n, d), dtype=np.float32)
+    Q = rng.standard_normal((q, d), dtype=np.float32)
+    el, ed, _ = c_oracle.flat_search_batch(X, Q, k, "l2", acc64=True, nthreads=16)
+    for r in range(world):
+        l, dd, c, st, kern, launches = out[r]
+        assert kern == "scan8_kernel" and launches == 1, (kern, launches)
+        assert not st["dense_path"] and st["append_launches"] == 1 and st["fallback_queries"] == 0, st
+        assert (c == k).all()
+        np.testing.assert_array_equal(l, el)
+        np.testing.assert_allclose(dd, ed, rtol=1e-4, atol=1e-5)
+
+
 def _gpu_ivf_worker(rank, world, port, n, d, k, q, nlist, nprobe, out):
     # the bench's IVF multi-GPU flow (bench.py main_ivf): rank 0 trains, the model
     # is broadcast, every other rank installs it and indexes its own shard

@@ -50,7 +50,10 @@ def exact(data):
 
 def build(hip, X, index_type):
     h = hip.LanceCreateDetached("", D, "l2", "c45")
-    hip.LanceHipSetOption(h, "scan_copy", "off")
+    # IVF_FLAT keeps the default bf16 scan copy (its bound scan streams it, as
+    # bench.py --config c4 runs); IVF_PQ scans codes only
+    if index_type == "ivf_pq":
+        hip.LanceHipSetOption(h, "scan_copy", "off")
     hip.LanceHipSetOption(h, "reserve_rows", str(len(X)))
     hip.LanceHipSetOption(h, "index_type", index_type)
     for lo in range(0, len(X), 1 << 18):
@@ -85,15 +88,35 @@ def check(gl, gd, gc, el, ed, ec):
 
 
 def test_c4_ivf_flat_nlist4096_nprobe64(hip, data, exact):
+    """The shipped default IVF_FLAT path at C4's parameters — the bf16 MFMA bound
+    scan of every probed list (flat_list_lb_kernel) + certified exact re-rank,
+    what bench.py --config c4 times — then the exact f64 list scan
+    (ivf_flat_scan=exact) on the same index; both against the C port."""
     X, Q = data
     h = build(hip, X, "ivf_flat")
     try:
+        ref = port_search(hip, h, X, Q, NPROBE, 1)
+        hip.LanceHipSetOption(h, "time_kernels", "1")
         gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, K, nprobes=NPROBE, refine_factor=1)
-        check(gl, gd, gc, *port_search(hip, h, X, Q, NPROBE, 1))
+        kt = hip.LanceHipKernelTimes(h)
+        hip.LanceHipSetOption(h, "time_kernels", "0")
+        check(gl, gd, gc, *ref)
         # IVF_FLAT distances are exact: recall is the probe coverage alone
         rec = flat_knn.recall_at_k(gl, exact[0], K)
-        print(f"C4 params: recall@10 = {rec:.4f} (nprobe {NPROBE})")
+        print(f"C4 params, bound scan: recall@10 = {rec:.4f} (nprobe {NPROBE})")
         assert rec >= 0.99
+        hip.LanceHipSetOption(h, "ivf_flat_scan", "exact")
+        hip.LanceHipSetOption(h, "time_kernels", "1")
+        gl2, gd2, gc2 = hip.LanceDetachedSearchBatch(h, Q, K, nprobes=NPROBE, refine_factor=1)
+        kt2 = hip.LanceHipKernelTimes(h)
+        hip.LanceHipSetOption(h, "time_kernels", "0")
+        check(gl2, gd2, gc2, *ref)
+        np.testing.assert_array_equal(gl2, gl)
+        # the default run was ONE certified bound-scan launch over bf16 rows (2 B per
+        # element: half the exact scan's f32 bytes for the same probed lists; an
+        # uncertified batch would have added an exact launch)
+        assert kt["ivf_scan_launches"] == 1 and kt2["ivf_scan_launches"] == 1, (kt, kt2)
+        assert kt2["ivf_scan_bytes"] == 2 * kt["ivf_scan_bytes"], (kt, kt2)
     finally:
         hip.LanceFreeDetached(h)
 

@@ -209,3 +209,68 @@ def test_bf16_store_k100_int8(hip, tmp_path, metric):
         assert st["retried_queries"] == 0, st
     finally:
         hip.LanceFreeDetached(h)
+
+
+@pytest.mark.parametrize("metric", ["l2", "dot", "cosine"])
+def test_split_div_progressive_threshold(hip, metric):
+    """Option split_div (progressive threshold, lance_hip_abi.cpp search_chunk):
+    the first 1/8 of the tiles with the sample's tau, their pool refined in tau
+    mode (tau' = min(tau, k-th exact distance)), the other 7/8 with tau' into a
+    disjoint segment range, the final certificate against tau'.  Two scan8
+    launches must run, and the results must equal the one-pass search and the
+    f64 oracle for k = 10 and k = 100."""
+    rng = np.random.default_rng(77)
+    n, d = 262_144, 768  # 1024 tiles = 128 * split_div
+    X = rng.standard_normal((n, d), dtype=np.float32)
+    Q = rng.standard_normal((256, d), dtype=np.float32)
+    h = hip.LanceCreateDetached("", d, metric, "t")
+    try:
+        hip.LanceHipSetOption(h, "time_kernels", "1")
+        for lo in range(0, n, 131_072):
+            hip.LanceDetachedAddBatch(h, X[lo:lo + 131_072], 131_072, d)
+        for k in (10, 100):
+            el, ed, ec = c_oracle.flat_search_batch(X, Q, k, metric, acc64=True, nthreads=16)
+            hip.LanceHipSetOption(h, "split_div", "0")
+            g1 = hip.LanceDetachedSearchBatch(h, Q, k)
+            assert hip.LanceHipLastSearchStats(h)["append_launches"] == 1
+            hip.LanceHipSetOption(h, "split_div", "8")
+            g8 = hip.LanceDetachedSearchBatch(h, Q, k)
+            st = hip.LanceHipLastSearchStats(h)
+            assert _ran_scan8(hip, h)
+            assert st["append_launches"] == 2, st
+            assert st["fallback_queries"] == 0, st
+            assert_same(*g8, el, ed, ec)
+            assert_same(*g1, el, ed, ec)
+            np.testing.assert_array_equal(g8[0], g1[0])
+            np.testing.assert_array_equal(g8[1], g1[1])
+    finally:
+        hip.LanceFreeDetached(h)
+
+
+def test_release_build_rejects_development_knobs(hip):
+    """The wrong-result scan8 timing ablations are not in a release build:
+    option scan8_variant accepts only the default geometry; pr_first is a
+    per-handle value, range-checked, and leaves the results unchanged."""
+    rng = np.random.default_rng(5)
+    n, d = 70_000, 768
+    X = rng.standard_normal((n, d), dtype=np.float32)
+    Q = rng.standard_normal((64, d), dtype=np.float32)
+    h = hip.LanceCreateDetached("", d, "l2", "t")
+    h2 = hip.LanceCreateDetached("", d, "l2", "t2")
+    try:
+        for v in ("1", "6", "21", "22", "24", "28", "34", "-1"):
+            with pytest.raises(hip.IOException):
+                hip.LanceHipSetOption(h, "scan8_variant", v)
+        hip.LanceHipSetOption(h, "scan8_variant", "0")
+        for v in ("4", "2000", "-3"):
+            with pytest.raises(hip.IOException):
+                hip.LanceHipSetOption(h, "pr_first", v)
+        hip.LanceDetachedAddBatch(h, X, n, d)
+        hip.LanceDetachedAddBatch(h2, X, n, d)
+        hip.LanceHipSetOption(h, "pr_first", "8")  # this handle only
+        el, ed, ec = c_oracle.flat_search_batch(X, Q, 10, "l2", acc64=True, nthreads=16)
+        assert_same(*hip.LanceDetachedSearchBatch(h, Q, 10), el, ed, ec)
+        assert_same(*hip.LanceDetachedSearchBatch(h2, Q, 10), el, ed, ec)
+    finally:
+        hip.LanceFreeDetached(h)
+        hip.LanceFreeDetached(h2)

@@ -7,7 +7,14 @@ searches).  tools/check_mfma_war.py walks every kernel of every gfx950 code
 object in duckdb-lancedb_amd/lib/*.o and reports a VALU write into a live A / B
 register after the MFMAs that end a run (the tile-final MFMAs, where
 mfma_operand_guard() sits in scan8_kernel, scan_kernel and the IVF kernels).
-A new register allocation that reintroduces the hazard fails this test."""
+Loads (VMEM / DS) writing a live A / B register are modelled at their minimum
+return latency (tools/check_mfma_war.py LOAD_MIN_LATENCY).  A new register
+allocation that reintroduces the hazard fails this test.
+
+The release build carries no scan8 timing ablation: every scan8_kernel
+instantiation in the code object has ABL = 0 and the ld = 768 default geometry
+<12, 4, 2> (the wrong-result variants exist only in LHIP_ABLATION_BUILD builds)."""
+import re
 import glob
 import os
 import subprocess
@@ -23,10 +30,16 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 @pytest.mark.skipif(not OBJS or not os.path.exists(os.path.join(LLVM, "llvm-objdump")),
                     reason="needs the built objects (make) and the ROCm LLVM tools")
 def test_no_valu_write_into_a_live_mfma_operand():
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_mfma_war.py"), *OBJS],
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_mfma_war.py"), "--list", *OBJS],
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     # every object with MFMAs was really disassembled
     kernels_with_mfma = [ln for ln in r.stdout.splitlines() if "MFMAs," in ln]
     assert any(ln.startswith("scan8_kernels.o") for ln in kernels_with_mfma), r.stdout
     assert any(ln.startswith("knn_kernels.o") for ln in kernels_with_mfma), r.stdout
+    assert any(ln.startswith("ivf_kernels.o") for ln in kernels_with_mfma), r.stdout
+    # release scan8 instantiations: ABL = 0 only, ld = 768 only the default geometry
+    s8 = set(re.findall(r"scan8_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", r.stdout))
+    assert s8, r.stdout[-2000:]
+    assert all(abl == "0" for (_, _, _, abl) in s8), sorted(s8)
+    assert {(d, rb) for (ks, d, rb, _) in s8 if ks == "12"} == {("4", "2")}, sorted(s8)

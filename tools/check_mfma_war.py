@@ -13,6 +13,16 @@ MFMA as the end of the window since the matrix pipe runs them in order); any
 VALU instruction inside that window writing one of its A / B registers is
 reported.  Exit status 1 when something is found.
 
+Loads that write a register (VMEM global_/buffer_/flat_ and DS ds_read*) are
+checked too: such a write lands when the data returns, at the earliest the
+load's minimum return latency after its issue (LOAD_MIN_LATENCY: an LDS read
+returns in >= ~50 cycles on an idle CU, a vector-memory load in >= ~120 even on
+an L1 hit, MI355X_MICROARCH.md constants; the model takes 32 and 64); a load
+whose return could land inside the MFMA's operand window is reported like a
+VALU write.  (A load refilling an A / B register right after the MFMAs that
+read it, as scan8_kernel's register ring and the IVF bound scan do, returns
+long after the operands were read: not a hazard under this model.)
+
 Default mode checks the MFMAs that END a run (no further MFMA in the next RUN_GAP
 instructions: the tile-final MFMAs before an epilogue, where round 2 saw the
 failure and where mfma_operand_guard() sits).  --strict checks every MFMA: that
@@ -21,7 +31,7 @@ k-loops (e.g. scan_kernel<.,.,i8>'s address updates into a just-used B
 register) in kernels whose outputs are bit-exact across the whole GPU suite, so
 A / B are read at issue there; the strict count is reported for reference.
 
-usage: tools/check_mfma_war.py [--strict] [objects...]   (default: duckdb-lancedb_amd/lib/*.o)
+usage: tools/check_mfma_war.py [--strict] [--list] [objects...]   (default: duckdb-lancedb_amd/lib/*.o)
 """
 import glob
 import os
@@ -34,6 +44,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LLVM = "/opt/rocm/lib/llvm/bin"
 MARGIN = 16
 RUN_GAP = 24
+# earliest return of a register-writing load after its issue (cycles; conservative)
+LOAD_MIN_LATENCY = {"ds_": 32, "global_": 64, "buffer_": 64, "flat_": 32, "scratch_": 64}
+
+
+def load_latency(mn):
+    """Minimum return latency of a load that writes its first operand, else None."""
+    for pre, lat in LOAD_MIN_LATENCY.items():
+        if mn.startswith(pre) and ("load" in mn or "read" in mn or ("atomic" in mn and "rtn" in mn)):
+            return lat
+    return None
 
 
 def mfma_cycles(op):
@@ -122,6 +142,9 @@ def check(funcs, strict=False):
                     hit = regs(ops2[0]) & src
                     if hit:
                         bad.append((name, i, mn, j, mn2, ops2[0], t))
+                lat = load_latency(mn2)
+                if lat is not None and ops2 and t + lat < window and regs(ops2[0]) & src:
+                    bad.append((name, i, mn, j, mn2, ops2[0], t + lat))
                 t += issue_cost(mn2, ops2)
                 if t >= window:
                     break
@@ -131,7 +154,7 @@ def check(funcs, strict=False):
 def main():
     args = sys.argv[1:]
     strict = "--strict" in args
-    args = [a for a in args if a != "--strict"]
+    args = [a for a in args if a not in ("--strict", "--list")]
     objs = args or sorted(glob.glob(os.path.join(ROOT, "duckdb-lancedb_amd", "lib", "*.o")))
     total_bad, total = 0, 0
     with tempfile.TemporaryDirectory() as tmp:
@@ -140,8 +163,12 @@ def main():
                 dis = code_object(obj, tmp)
             except subprocess.CalledProcessError:
                 continue  # host-only object
-            bad, n = check(parse(dis), strict)
+            funcs = parse(dis)
+            bad, n = check(funcs, strict)
             total += n
+            if "--list" in sys.argv:
+                for name in sorted(funcs):
+                    print(f"kernel {os.path.basename(obj)} {name}")
             if n == 0:
                 continue
             print(f"{os.path.basename(obj)}: {n} MFMAs, {len(bad)} VALU writes into a live MFMA operand")
