@@ -93,6 +93,9 @@ def parse():
                          "rows per rank; weak = global batch B x world. With --gpus > 1 the other mode is timed too "
                          "and reported under its own key")
     ap.add_argument("--no-other-scaling", action="store_true", help="multi-GPU: skip the extra weak/strong leg")
+    ap.add_argument("--sync", action="store_true",
+                    help="one GPU, device API: one synchronous search call per batch instead of two batches in "
+                         "flight (the synchronous figure is reported beside the pipelined one either way)")
     ap.add_argument("--no-host-batch", action="store_true",
                     help="N = 1 flat configs: skip the extra host-buffer leg (H2D + D2H timed, SURVEY.md §8d QPS)")
     ap.add_argument("--dry-run", action="store_true",
@@ -693,7 +696,7 @@ def main():
     Q = torch.randn((BG, D), generator=g, device=dev, dtype=torch.float32)
     if a.normalize:
         Q /= torch.linalg.vector_norm(Q, dim=1, keepdim=True)
-    from lance_hip.sharded import ShardedSearch, hip_device_merge, hip_device_search
+    from lance_hip.sharded import AsyncPipeline, ShardedSearch, hip_device_merge, hip_device_search
 
     searcher = ShardedSearch(hip_device_search(L, h, D), hip_device_merge(L), label_offset=s0, dist=dist,
                              world=world)
@@ -704,6 +707,13 @@ def main():
     Qh_api = Q.cpu().numpy() if (a.api != "device" or (world == 1 and not a.no_host_batch)) else None
     call_i = [0]
 
+    # one GPU, device API: two batches in flight (lance_hip_search_batch_device_async;
+    # every batch completes — certified, reruns / fallbacks done — at its wait
+    # inside the timed region); --sync: one synchronous call per batch
+    pipelined = world == 1 and a.api == "device" and not a.sync
+    pipe = AsyncPipeline(L, h, D) if pipelined else None
+    last_out = [None]
+
     def step():
         if a.api == "host_batch":
             return lance_hip.LanceDetachedSearchBatch(h, Qh_api, K)
@@ -711,11 +721,22 @@ def main():
             i = call_i[0] % BG
             call_i[0] += 1
             return lance_hip.LanceDetachedSearch(h, Qh_api[i], D, K)
+        if pipelined:
+            r = pipe.step(Q, K)
+            last_out[0] = r if r is not None else last_out[0]
+            return r
         return searcher.search(Q, K, reuse_outputs=True)
+
+    def sync():
+        if pipelined:
+            r = pipe.drain()
+            last_out[0] = r if r is not None else last_out[0]
+        torch.cuda.synchronize()
 
     # warmup for per_call: the timed calls then start at query 0 (the recall subset below)
     for _ in range(a.warmup):
         step()
+    sync()
     call_i[0] = 0
     per_call_l = []
 
@@ -725,7 +746,11 @@ def main():
             per_call_l.append(r[0])
         return r
 
-    t, res, per = timed_steps(step_rec, a.steps, 0, dist, dev, torch.cuda.synchronize)
+    t, res, per = timed_steps(step_rec, a.steps, 0, dist, dev, sync)
+    if pipelined:
+        res = last_out[0]
+    if a.api == "device":  # (the output buffers are reused by the legs below)
+        res = tuple(x.clone() for x in res)
     st = lance_hip.LanceHipLastSearchStats(h)
     print(f"[bench] per-step ms: min {per.min():.4f} median {np.median(per):.4f} max {per.max():.4f}", file=sys.stderr)
     # extra legs (never `value`): the other multi-GPU scaling mode, and at N = 1
@@ -743,6 +768,13 @@ def main():
                  "ms_per_step": round(1000.0 * to / a.steps, 4), "global_batch": BO,
                  "rows_per_gpu": n_local}
         del Qo
+    syncleg = None
+    if pipelined:
+        ts, rs, _ = timed_steps(lambda: searcher.search(Q, K, reuse_outputs=True), a.steps, a.warmup, None, dev,
+                                torch.cuda.synchronize)
+        syncleg = {"value": round(BG * a.steps / ts, 1), "unit": "queries/s", "ms_per_step": round(1000.0 * ts / a.steps, 4),
+                   "api": "lance_hip_search_batch_device, one synchronous call per batch",
+                   "ids_equal_pipelined": bool((rs[0].cpu() == res[0].cpu()).all())}
     hostb = None
     if world == 1 and a.api == "device" and not a.no_host_batch:
         th, rh, _ = timed_steps(lambda: lance_hip.LanceDetachedSearchBatch(h, Qh_api, K), a.steps, a.warmup, None,
@@ -755,7 +787,7 @@ def main():
     lance_hip.LanceHipSetOption(h, "time_kernels", "1")
     for _ in range(max(3, min(a.steps, 10))):
         step()
-    torch.cuda.synchronize()
+    sync()
     kt = lance_hip.LanceHipKernelTimes(h)
     lance_hip.LanceHipSetOption(h, "time_kernels", "0")
     if a.api == "device":
@@ -897,6 +929,10 @@ def main():
         }
         if other:
             line[f"{other['scaling']}_scaling"] = other
+        if pipelined:
+            line["config"]["pipeline"] = ("async: 2 batches in flight on the handle's stream "
+                                          "(lance_hip_search_batch_device_async / lance_hip_search_wait)")
+            line["sync"] = syncleg
         if hostb:
             line["host_batch"] = hostb
         if recall is not None:

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -86,14 +87,58 @@ struct DevBuf {
 	}
 };
 
-struct Workspace {
-	DevBuf<float> Qin, Qf, tau, cut, dense, cand_dist, out_d, fb_keys, fb_keys2, stage;
+// Per-pass buffers of the flat pipeline: the prepared queries, tau and the
+// status words [cert | cand_cnt | pool_cnt] x nq (pinned host memory the
+// threshold path's kernels write in place; the dense path's copy in HBM).
+// Two sets: an asynchronous pass still in flight keeps its own while the next
+// pass is enqueued (Index::search_async).
+struct PassBufs {
+	DevBuf<float> Qf, tau;
 	DevBuf<uint16_t> Qb;
 	DevBuf<float4> qaux;
 	DevBuf<float2> qm;  // int8 queries: per-query maxima (the batch scale)
+	DevBuf<int> status;
+	int *h_status = nullptr;      // pinned
+	int *d_status_map = nullptr;  // its device-visible address
+	size_t h_status_n = 0;
+	hipEvent_t done = nullptr;    // end of an asynchronous pass
+	PassBufs() = default;
+	PassBufs(const PassBufs &) = delete;
+	PassBufs &operator=(const PassBufs &) = delete;
+	~PassBufs() {
+		if (h_status) (void)hipHostFree(h_status);
+		if (done) (void)hipEventDestroy(done);
+	}
+	void need_host_status(size_t n) {
+		if (n <= h_status_n) return;
+		if (h_status) HIPCHK(hipHostFree(h_status));
+		h_status = nullptr;
+		HIPCHK(hipHostMalloc(&h_status, n * sizeof(int)));
+		h_status_n = n;
+		void *dv = nullptr;
+		HIPCHK(hipHostGetDevicePointer(&dv, h_status, 0));
+		d_status_map = static_cast<int *>(dv);
+	}
+};
+
+// An enqueued pass whose completion check (certificates, reruns, fallback)
+// is still to run (Index::finish_chunk).
+struct PendingPass {
+	int slot = 0, nq = 0, k = 0;
+	int64_t *dL = nullptr;
+	float *dD = nullptr;
+	int *dC = nullptr;
+	StoreView sv{};
+	QueryView qv{};
+	bool hmap = false, fast_ok = false, dense = false, two_append = false, async = false;
+	int64_t n_tiles = 0, ticket = 0, st3 = 0, st5 = 0;
+};
+
+struct Workspace {
+	DevBuf<float> Qin, cut, dense, cand_dist, out_d, fb_keys, fb_keys2, stage;
 	DevBuf<uint2> seg_pool;
 	DevBuf<int> seg_cnt;
-	DevBuf<int> status, out_c;  // status = [cert | cand_cnt | pool_cnt] x nq
+	DevBuf<int> out_c;
 	DevBuf<int> selbig;         // per query: pool too large for the small select
 	// small exact search (search_chunk): per-workgroup partial top-k lists and
 	// the per-query completion counters (zeroed at allocation, left zeroed)
@@ -105,16 +150,12 @@ struct Workspace {
 	DevBuf<float4> rqaux;
 	DevBuf<int> rfq, rstat, rC;
 	DevBuf<int64_t> rL;
-	int *h_status = nullptr;    // pinned mirror of status
-	int *d_status_map = nullptr;  // its device-visible address (the threshold path writes it in place)
-	size_t h_status_n = 0;
 	DevBuf<uint32_t> cand_slot;
 	DevBuf<int64_t> out_l, fb_vals, fb_vals2, idx;
 	DevBuf<uint8_t> sort_tmp, out_blk;
 	uint8_t *h_io = nullptr;    // pinned staging of the host-buffer API (queries in, results out)
 	size_t h_io_n = 0;
 	~Workspace() {
-		if (h_status) (void)hipHostFree(h_status);
 		if (h_io) (void)hipHostFree(h_io);
 	}
 	uint8_t *need_host_io(size_t bytes) {
@@ -125,16 +166,6 @@ struct Workspace {
 			h_io_n = bytes;
 		}
 		return h_io;
-	}
-	void need_host_status(size_t n) {
-		if (n <= h_status_n) return;
-		if (h_status) HIPCHK(hipHostFree(h_status));
-		h_status = nullptr;
-		HIPCHK(hipHostMalloc(&h_status, n * sizeof(int)));
-		h_status_n = n;
-		void *dv = nullptr;
-		HIPCHK(hipHostGetDevicePointer(&dv, h_status, 0));
-		d_status_map = static_cast<int *>(dv);
 	}
 };
 
@@ -194,6 +225,9 @@ struct Index {
 	float max_alpha = 0.f, max_ux = 0.f, max_alpha_l2 = 0.f, max_ux_l2 = 0.f;
 	hipStream_t stream = nullptr;
 	Workspace ws;
+	PassBufs pb[2];
+	std::deque<PendingPass> pending;  // asynchronous passes not finished yet (<= 2)
+	int64_t next_ticket = 1;
 
 	// persistence
 	FILE *log = nullptr;
@@ -256,6 +290,7 @@ struct Index {
 	int64_t kt_ivf_n = 0;
 
 	~Index() {
+		if (stream) (void)hipStreamSynchronize(stream);  // (pending passes: their kernels end first)
 		if (log) fclose(log);
 		ivf_free(ivf);
 		(void)hipSetDevice(device);
@@ -295,7 +330,14 @@ struct Index {
 		HIPCHK(hipStreamSynchronize(stream));
 	}
 
-	void bind() { HIPCHK(hipSetDevice(device)); }
+	// every entry point that touches the device: the handle's device current,
+	// and no asynchronous search pending (finished first: a mutation or another
+	// search never runs under one)
+	void bind() {
+		HIPCHK(hipSetDevice(device));
+		drain();
+	}
+	void bind_nodrain() { HIPCHK(hipSetDevice(device)); }
 
 	// grow the device store to hold at least `want` slots (contents preserved)
 	void reserve(int64_t want) {
@@ -720,6 +762,15 @@ struct Index {
 	// Device-side batched search; dQ [nq][dim] (device), outputs device.
 	void search_device(const float *dQ, int nq, int k, int refine, int64_t *dL, float *dD, int *dC);
 	void search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL, float *dD, int *dC);
+	bool enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL, float *dD, int *dC, int slot,
+	                   bool async, PendingPass &p);
+	void finish_chunk(PendingPass &p);
+	int pb_free_slot() const;
+	// asynchronous search: enqueue (returns a ticket), complete at wait_ticket
+	int64_t search_async(const float *dQ, int nq, int k, int nprobes, int refine, int64_t *dL, float *dD, int *dC);
+	void wait_ticket(int64_t ticket);  // <= 0: every pending search
+	void finish_oldest();
+	void drain();
 };
 
 // A search with a predicate: evaluates it over the slots (host, vectorised),

@@ -562,11 +562,21 @@ constexpr int BR = SCAN_BR, BQ = SCAN_BQ;
      defined(LHIP_ABL_NO_QDMA) || defined(LHIP_ABL_NO_SLOW) || defined(LHIP_ABL_SLOW_NEVER) ||               \
      defined(LHIP_ABL_DRAIN_EPI) || defined(LHIP_ABL_NO_LISTWRITE) || defined(LHIP_ABL_NO_FLUSH) ||          \
      defined(LHIP_ABL_SMALL_NOWGSORT) || defined(LHIP_ABL_SMALL_NOMERGE) || defined(LHIP_ABL_SMALL_NOFENCE) || \
+     defined(LHIP_ABL_PR_NOMERGE) || defined(LHIP_ABL_PR_NOLOAD) || defined(LHIP_ABL_PR_F32MATH) ||             \
      defined(LHIP_PROF))
 #error "LHIP_ABL_* / LHIP_PROF are timing ablations that break results: build them through tools/ablate.sh"
 #endif
 #ifndef LHIP_ABL_NO_EPILOGUE
 #define LHIP_ABL_NO_EPILOGUE 0
+#endif
+#ifndef LHIP_ABL_PR_NOMERGE
+#define LHIP_ABL_PR_NOMERGE 0  // pool_refine: no top-k merge after a round (timing only)
+#endif
+#ifndef LHIP_ABL_PR_NOLOAD
+#define LHIP_ABL_PR_NOLOAD 0  // pool_refine (one-column-step path): rows not loaded (timing only)
+#endif
+#ifndef LHIP_ABL_PR_F32MATH
+#define LHIP_ABL_PR_F32MATH 0  // pool_refine (one-column-step path): f32 partial sums (timing only)
 #endif
 #ifndef LHIP_ABL_NO_MFMA
 #define LHIP_ABL_NO_MFMA 0  // fragments read, no MFMA
@@ -2326,27 +2336,66 @@ constexpr int PR_CHUNK = PR_WAVES * PR_PER_WAVE;
 constexpr int PR_MAXK = MAX_CAND;   // k of the fast path (k + 8 <= MAX_CAND)
 
 // exact distances of NC rows to one query by one wave (each the value
-// exact_distance returns), every row's loads issued before any accumulates
-template <int METRIC, typename T, int NC>
+// exact_distance returns), every row's loads issued before any accumulates.
+// NI > 0: rows of at most 256 NI elements (d4 <= 64 NI); a lane's NI x NC
+// 16-B loads are ALL in flight together (one memory latency per round, not
+// NI of them) and the query comes from LDS (qs: 256 NI floats, zero past
+// dim).  NI = 0: any dimension, one 16-B column step at a time.
+template <int METRIC, typename T, int NC, int NI>
 __device__ __forceinline__ void exact_distance_multi(const T *__restrict__ X, int ld, const uint32_t *slots,
-                                                     int nvalid, const float *__restrict__ q, int dim, int lane,
-                                                     float *out) {
+                                                     int nvalid, const float *__restrict__ q, const float *qs,
+                                                     int dim, int lane, float *out) {
 	double a[NC], b[NC], c[NC];
 #pragma unroll
 	for (int r = 0; r < NC; ++r) a[r] = b[r] = c[r] = 0.0;
 	const int d4 = dim >> 2;
-	for (int i4 = lane; i4 < d4; i4 += 64) {
-		const float4 qv = *reinterpret_cast<const float4 *>(q + 4 * i4);
-		float4 xv[NC];
+	if constexpr (NI > 0) {
+		float4 xv[NI][NC];
 #pragma unroll
-		for (int r = 0; r < NC; ++r)
-			xv[r] = r < nvalid ? xval4(X + (int64_t)slots[r] * ld, 4 * i4) : make_float4(0.f, 0.f, 0.f, 0.f);
+		for (int it = 0; it < NI; ++it) {
+			const int i4 = lane + 64 * it;
 #pragma unroll
-		for (int r = 0; r < NC; ++r) {
-			exact_acc<METRIC>(xv[r].x, qv.x, a[r], b[r], c[r]);
-			exact_acc<METRIC>(xv[r].y, qv.y, a[r], b[r], c[r]);
-			exact_acc<METRIC>(xv[r].z, qv.z, a[r], b[r], c[r]);
-			exact_acc<METRIC>(xv[r].w, qv.w, a[r], b[r], c[r]);
+			for (int r = 0; r < NC; ++r)
+				xv[it][r] = (r < nvalid && i4 < d4) ? xval4(X + (int64_t)slots[r] * ld, 4 * i4)
+				                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+		}
+#pragma unroll
+		for (int it = 0; it < NI; ++it) {
+			const float4 qv = *reinterpret_cast<const float4 *>(qs + 4 * (lane + 64 * it));  // zero past dim
+#pragma unroll
+			for (int r = 0; r < NC; ++r) {
+				exact_acc<METRIC>(xv[it][r].x, qv.x, a[r], b[r], c[r]);
+				exact_acc<METRIC>(xv[it][r].y, qv.y, a[r], b[r], c[r]);
+				exact_acc<METRIC>(xv[it][r].z, qv.z, a[r], b[r], c[r]);
+				exact_acc<METRIC>(xv[it][r].w, qv.w, a[r], b[r], c[r]);
+			}
+		}
+	} else {
+		for (int i4 = lane; i4 < d4; i4 += 64) {
+			const float4 qv = *reinterpret_cast<const float4 *>(q + 4 * i4);
+			float4 xv[NC];
+#pragma unroll
+			for (int r = 0; r < NC; ++r)
+				xv[r] = (r < nvalid && !LHIP_ABL_PR_NOLOAD) ? xval4(X + (int64_t)slots[r] * ld, 4 * i4)
+				                                          : make_float4(0.f, (float)r, 0.f, (float)i4);
+			if (LHIP_ABL_PR_F32MATH) {
+				float fa[NC];
+#pragma unroll
+				for (int r = 0; r < NC; ++r) {
+					const float dx = xv[r].x - qv.x, dy = xv[r].y - qv.y, dz = xv[r].z - qv.z, dw = xv[r].w - qv.w;
+					fa[r] = fmaf(dx, dx, fmaf(dy, dy, fmaf(dz, dz, dw * dw)));
+				}
+#pragma unroll
+				for (int r = 0; r < NC; ++r) a[r] += (double)fa[r];
+			} else {
+#pragma unroll
+				for (int r = 0; r < NC; ++r) {
+					exact_acc<METRIC>(xv[r].x, qv.x, a[r], b[r], c[r]);
+					exact_acc<METRIC>(xv[r].y, qv.y, a[r], b[r], c[r]);
+					exact_acc<METRIC>(xv[r].z, qv.z, a[r], b[r], c[r]);
+					exact_acc<METRIC>(xv[r].w, qv.w, a[r], b[r], c[r]);
+				}
+			}
 		}
 	}
 	for (int i = 4 * d4 + lane; i < dim; i += 64)
@@ -2370,6 +2419,19 @@ __device__ __forceinline__ void exact_distance_multi(const T *__restrict__ X, in
 		out[r] = f;
 	}
 }
+
+// rows per wave and refine round of pool_refine: every load of a round in
+// flight at once (NI x NC 16-B loads per lane) within the register budget of
+// two waves per SIMD; cosine keeps three f64 sums per row (half the rows)
+template <int METRIC, int NI>
+struct PrGeom {
+#ifdef LHIP_PR_PW3  // (development builds: rows per wave of the ld <= 768 path)
+	static constexpr int base = NI == 0 ? 16 : NI == 1 ? 16 : NI == 2 ? 12 : NI == 3 ? LHIP_PR_PW3 : 8;
+#else
+	static constexpr int base = NI == 0 ? 16 : NI == 1 ? 16 : NI == 2 ? 12 : 8;
+#endif
+	static constexpr int PW = METRIC == METRIC_COSINE ? base / 2 : base;
+};
 
 // ascending bitonic sort of a[0, P) (P a power of two >= 64) by the block
 __device__ __forceinline__ void pr_bitonic(uint64_t *a, int P) {
@@ -2396,7 +2458,7 @@ constexpr int PR_R = 96;      // first chunk of the final pass (C2: ~80 rows lie
                               // are the kernel's HBM traffic: 96 refined 18 % fewer than 128 at equal
                               // step time or better, r03s2)
 
-template <int METRIC, typename T>
+template <int METRIC, typename T, int NI>
 __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
     const uint2 *__restrict__ seg_pool, const int *__restrict__ seg_cnt, int seg_cap, int n_seg, int nq,
     const float *__restrict__ tau, const T *__restrict__ X, int ld, int dim, const float *__restrict__ Qf,
@@ -2412,6 +2474,7 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 	__shared__ int s_over, s_nnan, s_dnan;
 	__shared__ unsigned s_nfin, s_knf, s_kmin, s_kmax, s_bstar, s_cum, s_below, s_ns, s_hi, s_pmin, s_pmax;
 	__shared__ unsigned segc[PR_THREADS];  // (big pools) segment counts
+	__shared__ __attribute__((aligned(16))) float qs[NI > 0 ? 256 * NI : 4];  // the query row (NI > 0)
 	const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
 #ifdef LHIP_PR_PROF
 	// phase stamps (diagnostic build, one designated launch): thread 0 prints
@@ -2426,7 +2489,8 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 	auto mark = [&]() {};
 #endif
 	// candidates per wave and round (cosine: three f64 sums per row, half as many)
-	constexpr int PW = METRIC == METRIC_COSINE ? PR_PER_WAVE / 2 : PR_PER_WAVE, CH = PR_WAVES * PW;
+	constexpr int PW = PrGeom<METRIC, NI>::PW, CH = PR_WAVES * PW;
+	static_assert(CH <= PR_CHUNK, "round buffer");
 	if (t == 0) {
 		s_over = 0;
 		s_nnan = 0;
@@ -2599,6 +2663,9 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 	const int nfin = (int)s_nfin;
 	const float ftau = tau ? tau[q] : F_INF;
 	const float *qrow = Qf + (int64_t)q * ld;
+	// the query row in LDS (NI > 0: every refine round reads it there, zero past dim)
+	if (NI > 0)
+		for (int i = t; i < 64 * 4 * (NI > 0 ? NI : 1); i += PR_THREADS) qs[i] = i < dim ? qrow[i] : 0.f;
 
 	// next chunk: the finite keys in [lo, hi_goal] up to a histogram bin holding
 	// the R-th smallest of them (all of them when fewer), at most PR_SEL, slots
@@ -2733,7 +2800,7 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 				// this lane's label load in flight with the row loads
 				const int64_t lab = lane < nv ? labels[slots[sp + b0 + lane]] : 0;
 				float d[PW];
-				if (nv > 0) exact_distance_multi<METRIC, T, PW>(X, ld, sl, nv, qrow, dim, lane, d);
+				if (nv > 0) exact_distance_multi<METRIC, T, PW, NI>(X, ld, sl, nv, qrow, qs, dim, lane, d);
 				if (lane < nv) {
 					float dv = d[0];
 #pragma unroll
@@ -2747,7 +2814,7 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 			__syncthreads();
 			// merge: rank of every entry (top so far + this round) by (distance, label)
 			const int m = cnt + nr;
-			for (int i = t; i < m; i += PR_THREADS) {
+			for (int i = t; i < (LHIP_ABL_PR_NOMERGE ? 0 : m); i += PR_THREADS) {
 				const float di = cd[cur][i];
 				const int64_t li = cl[cur][i];
 				int rank = 0;
@@ -2786,7 +2853,7 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 #pragma unroll
 				for (int r = 0; r < PW; ++r) sl[r] = r < nv ? (uint32_t)order[sp + b0 + r] : 0u;
 				float d[PW];
-				if (nv > 0) exact_distance_multi<METRIC, T, PW>(X, ld, sl, nv, qrow, dim, lane, d);
+				if (nv > 0) exact_distance_multi<METRIC, T, PW, NI>(X, ld, sl, nv, qrow, qs, dim, lane, d);
 				if (lane < nv) {
 					float dv = d[0];
 					uint32_t sv = sl[0];
@@ -2906,15 +2973,35 @@ static void pool_refine_dispatch(const StoreView &s, const QueryView &q, const u
 	const int prof_on = 0;
 #endif
 	const int r_first = s.pr_first > 0 ? std::max(8, std::min(PR_SEL, s.pr_first)) : PR_R;
-#define LHIP_PR(MET)                                                                                                  \
-	pool_refine_kernel<MET, T><<<grid, PR_THREADS, 0, st>>>(seg_pool, seg_cnt, seg_cap, n_seg, q.nq, tau, X, s.ld,   \
-	                                                        s.dim, q.Qf, s.labels, k, mode, m_tau, live, tau_out, L, \
-	                                                        D, C, cert, refined, pool_total, prof_on, r_first)
-	switch (s.metric) {
-	case METRIC_L2: LHIP_PR(METRIC_L2); break;
-	case METRIC_DOT: LHIP_PR(METRIC_DOT); break;
-	default: LHIP_PR(METRIC_COSINE); break;
+#define LHIP_PR(MET, NI)                                                                                              \
+	pool_refine_kernel<MET, T, NI><<<grid, PR_THREADS, 0, st>>>(seg_pool, seg_cnt, seg_cap, n_seg, q.nq, tau, X, s.ld,\
+	                                                            s.dim, q.Qf, s.labels, k, mode, m_tau, live, tau_out,  \
+	                                                            L, D, C, cert, refined, pool_total, prof_on, r_first)
+#define LHIP_PR_NI(MET)                                                                                               \
+	switch (ni) {                                                                                                      \
+	case 1: LHIP_PR(MET, 1); break;                                                                                    \
+	case 2: LHIP_PR(MET, 2); break;                                                                                    \
+	case 3: LHIP_PR(MET, 3); break;                                                                                    \
+	case 4: LHIP_PR(MET, 4); break;                                                                                    \
+	default: LHIP_PR(MET, 0); break;                                                                                   \
 	}
+	// row length in 256-element steps (one 16-B load per lane each): <= 4 -> all in flight per round
+	// tau mode (at most m_tau <= MAX_CAND rows, typically k + 8: one round) takes every
+	// load of the round at once (NI path, measured 15.4 vs 17.0 us at C2); the final
+	// mode's rounds are larger and keep 16 rows per wave one column step at a time
+	// (66 vs 75 us at C2: twice the rows per round, half the rounds and merges;
+	// r04d kernel traces)
+#ifdef LHIP_PR_FORCE_NI0  // (development builds: the one-column-step path everywhere)
+	const int ni = 0;
+#else
+	const int ni = mode == 1 ? 0 : s.dim <= 256 ? 1 : s.dim <= 512 ? 2 : s.dim <= 768 ? 3 : s.dim <= 1024 ? 4 : 0;
+#endif
+	switch (s.metric) {
+	case METRIC_L2: LHIP_PR_NI(METRIC_L2); break;
+	case METRIC_DOT: LHIP_PR_NI(METRIC_DOT); break;
+	default: LHIP_PR_NI(METRIC_COSINE); break;
+	}
+#undef LHIP_PR_NI
 #undef LHIP_PR
 }
 

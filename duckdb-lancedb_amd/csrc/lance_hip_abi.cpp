@@ -44,6 +44,31 @@ void Index::search_device(const float *dQ, int nq, int k, int refine, int64_t *d
 }
 
 void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL, float *dD, int *dC) {
+	PendingPass p;
+	if (enqueue_chunk(dQ, nq, k, refine, dL, dD, dC, pb_free_slot(), false, p)) finish_chunk(p);
+}
+
+// the pass-buffer set no pending pass holds (at most one pass is pending when
+// a new one is enqueued)
+int Index::pb_free_slot() const {
+	for (int i = 0; i < 2; ++i) {
+		bool used = false;
+		for (const auto &q : pending) used |= q.slot == i;
+		if (!used) return i;
+	}
+	throw Error("internal: no free pass buffers");
+}
+
+// Everything of a search pass up to its completion wait: prep, sample pass,
+// threshold scan, final refine (or the dense path of small stores), enqueued
+// on the handle's stream.  Returns false when the pass already completed (the
+// one-launch small exact search); otherwise `p` describes what finish_chunk
+// checks once the stream reaches its end.  async: other passes may still be
+// pending on the stream; any workspace the pending kernels read is kept
+// (growth drains them first).
+bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL, float *dD, int *dC, int slot,
+                          bool async, PendingPass &p) {
+	PassBufs &P = pb[slot];
 	const int eff_metric = metric_quirk ? METRIC_L2 : metric;
 	const float4 *aux = search_aux((metric_quirk && metric != METRIC_L2) ? rowaux_l2 : rowaux);
 	const float ma = (metric_quirk && metric != METRIC_L2) ? max_alpha_l2 : max_alpha;
@@ -87,17 +112,17 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 			kt_dense_n += 1;
 		}
 		if (!defer_sync) HIPCHK(hipStreamSynchronize(stream));
-		return;
+		return false;
 	}
 	const int nq_pad = (int)round_up(nq, SCAN_BQ);
-	ws.Qf.need((size_t)nq_pad * ld);
-	ws.Qb.need((size_t)nq_pad * ld);
-	ws.qaux.need(nq_pad);
-	ws.tau.need(nq);
+	P.Qf.need((size_t)nq_pad * ld);
+	P.Qb.need((size_t)nq_pad * ld);
+	P.qaux.need(nq_pad);
+	P.tau.need(nq);
 	ws.cut.need(nq);
 	ws.cand_slot.need((size_t)nq * MAX_CAND);
 	ws.cand_dist.need((size_t)nq * MAX_CAND);
-	ws.need_host_status((size_t)3 * nq);
+	P.need_host_status((size_t)3 * nq);
 	// [cert | cand_cnt | pool_cnt]: on the threshold path the kernels write it
 	// straight into pinned host memory (only pool_refine / retry_scatter store
 	// into it, no kernel reads it back), so the step ends with one stream wait
@@ -106,21 +131,21 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	const bool hmap = n_slots > 65536;
 	int *dstat;
 	if (hmap) {
-		dstat = ws.d_status_map;
+		dstat = P.d_status_map;
 	} else {
-		ws.status.need((size_t)3 * nq);
-		dstat = ws.status.p;
+		P.status.need((size_t)3 * nq);
+		dstat = P.status.p;
 	}
 	int *d_cert = dstat, *d_cand_cnt = dstat + nq, *d_pool_cnt = dstat + 2 * nq;
 	if (use8) {
-		ws.qm.need(nq);
-		launch_prep_queries_i8(dQ, nq, dim, ld, nq_pad, eff_metric, max_alpha8, max_x8, ws.qm.p, ws.Qf.p, ws.Qb.p,
-		                       ws.qaux.p, dstat, stream);
+		P.qm.need(nq);
+		launch_prep_queries_i8(dQ, nq, dim, ld, nq_pad, eff_metric, max_alpha8, max_x8, P.qm.p, P.Qf.p, P.Qb.p,
+		                       P.qaux.p, dstat, stream);
 	}
 	else
-		launch_prep_queries(dQ, nq, dim, ld, nq_pad, eff_metric, ma, mu, ws.Qf.p, ws.Qb.p, ws.qaux.p, dstat,
+		launch_prep_queries(dQ, nq, dim, ld, nq_pad, eff_metric, ma, mu, P.Qf.p, P.Qb.p, P.qaux.p, dstat,
 		                    stream);
-	QueryView qv{ws.Qf.p, ws.Qb.p, ws.qaux.p, nq, nq_pad};
+	QueryView qv{P.Qf.p, P.Qb.p, P.qaux.p, nq, nq_pad};
 
 	// refined candidates: k + max(32, k) — past k the bound slack (bf16 query
 	// rounding) spans more ranks as the neighbour distances crowd (C3: k = 100)
@@ -128,7 +153,6 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	const int Mfinal = std::min(MAX_CAND, std::max(k * std::max(refine, 1), k + std::max(use8 ? cand_extra_i8_eff() : cand_extra, k)));
 	const int64_t n_tiles = (n_slots + SCAN_BR - 1) / SCAN_BR;
 	const bool fast_ok = (k + 8 <= MAX_CAND) && live_rows() > 0;
-	bool all_fallback = !fast_ok;
 	constexpr int64_t DENSE_MAX_ROWS = 65536;
 
 	if (fast_ok && n_slots <= DENSE_MAX_ROWS) {
@@ -159,11 +183,6 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		const int Ms = k + 8;
 		const int n_seg_s = scan_grid(n_sample);
 		const int cap_s = (int)round_up(4 * ((n_sample + n_seg_s - 1) / n_seg_s), 4);
-		ws.seg_pool.need((size_t)n_seg_s * nq * cap_s + (size_t)n_seg_s * (nq_pad / SCAN_BQ));
-		ws.seg_cnt.need((size_t)n_seg_s * nq);
-		launch_scan_tilemin(sv, qv, n_sample, stride, ws.seg_pool.p, ws.seg_cnt.p, cap_s, stream);
-		launch_pool_refine(sv, qv, ws.seg_pool.p, ws.seg_cnt.p, cap_s, n_seg_s, nullptr, k, 0, Ms, -1, ws.tau.p,
-		                   nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
 		// 2) threshold scan over every row into per-(workgroup, query) segments;
 		//    a segment holds ~4x its expected share of the (k+8)*N/sample pool.
 		//    int8 scan8 path, large stores: progressive threshold.  The first
@@ -184,47 +203,108 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		// its LDS capacity, but a segment past seg_cap fails the certificate)
 		const int64_t expect = (int64_t)(k + 4) * ((n_tiles + n_sample - 1) / n_sample);
 		const int seg_cap = (int)std::min<int64_t>(1024, round_up(std::max<int64_t>(64, 32 * expect / n_seg1), 32));
-		ws.seg_pool.need((size_t)n_seg * nq * seg_cap + (size_t)n_seg * (nq_pad / SCAN_BQ));  // + per-workgroup sink
-		ws.seg_cnt.need((size_t)n_seg * nq);
+		const size_t pool_s = (size_t)n_seg_s * nq * cap_s + (size_t)n_seg_s * (nq_pad / SCAN_BQ);
+		const size_t pool_a = (size_t)n_seg * nq * seg_cap + (size_t)n_seg * (nq_pad / SCAN_BQ);  // + per-workgroup sink
+		const size_t cnt_n = (size_t)std::max(n_seg_s, n_seg) * nq;
+		// kernels of a pending pass read seg_pool / seg_cnt: grow them only once it is done
+		if (async && !pending.empty() && (ws.seg_pool.n < std::max(pool_s, pool_a) || ws.seg_cnt.n < cnt_n))
+			drain();
+		ws.seg_pool.need(std::max(pool_s, pool_a));
+		ws.seg_cnt.need(cnt_n);
+		launch_scan_tilemin(sv, qv, n_sample, stride, ws.seg_pool.p, ws.seg_cnt.p, cap_s, stream);
+		launch_pool_refine(sv, qv, ws.seg_pool.p, ws.seg_cnt.p, cap_s, n_seg_s, nullptr, k, 0, Ms, -1, P.tau.p,
+		                   nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
 		tic(2);
 		last_stats[5] += tA ? 2 : 1;  // threshold append launches of the first pass
 		if (tA) {
-			launch_scan8_append(sv, qv, ws.tau.p, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, stream, 0, tA, 0);
+			launch_scan8_append(sv, qv, P.tau.p, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, stream, 0, tA, 0);
 			tic(3);
-			launch_pool_refine(sv, qv, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, nA, ws.tau.p, k, 0, Ms, -1, ws.tau.p,
+			launch_pool_refine(sv, qv, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, nA, P.tau.p, k, 0, Ms, -1, P.tau.p,
 			                   nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
 			tic(4);
-			launch_scan8_append(sv, qv, ws.tau.p, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, stream, tA, n_tiles, nA);
+			launch_scan8_append(sv, qv, P.tau.p, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, stream, tA, n_tiles, nA);
 			tic(5);
 		} else {
-			launch_scan_append(sv, qv, ws.tau.p, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, stream);
+			launch_scan_append(sv, qv, P.tau.p, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, stream);
 			tic(3);
 		}
 		// 3) the pool in bound order, exact refine until certified
-		launch_pool_refine(sv, qv, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, n_seg, ws.tau.p, k, 1, 0, live_rows(),
+		launch_pool_refine(sv, qv, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, n_seg, P.tau.p, k, 1, 0, live_rows(),
 		                   nullptr, dL, dD, dC, d_cert, d_cand_cnt, d_pool_cnt, stream);
+		p.two_append = tA > 0;
 	}
 	HIPCHK(hipGetLastError());
-
 	// [cert | cand_cnt | pool_cnt] on the host: written in place (threshold
 	// path) or one pinned readback (dense path)
 	if (!hmap)
-		HIPCHK(hipMemcpyAsync(ws.h_status, ws.status.p, (size_t)3 * nq * sizeof(int), hipMemcpyDeviceToHost, stream));
-	spin_sync(stream);
-	if (time_kernels && !all_fallback && last_stats[3] == 0) {
+		HIPCHK(hipMemcpyAsync(P.h_status, P.status.p, (size_t)3 * nq * sizeof(int), hipMemcpyDeviceToHost, stream));
+	p.slot = slot;
+	p.nq = nq;
+	p.k = k;
+	p.dL = dL;
+	p.dD = dD;
+	p.dC = dC;
+	p.sv = sv;
+	p.qv = qv;
+	p.hmap = hmap;
+	p.fast_ok = fast_ok;
+	p.dense = last_stats[3] == 1;
+	p.n_tiles = n_tiles;
+	if (async) {
+		if (!P.done) HIPCHK(hipEventCreateWithFlags(&P.done, hipEventDisableTiming));
+		HIPCHK(hipEventRecord(P.done, stream));
+	}
+	return true;
+}
+
+// The rest of a pass once its kernels completed: the certificate check, the
+// reruns of uncertified queries and the exact fallback (synchronous).
+void Index::finish_chunk(PendingPass &p) {
+	PassBufs &P = pb[p.slot];
+	const int nq = p.nq, k = p.k;
+	int64_t *dL = p.dL;
+	float *dD = p.dD;
+	int *dC = p.dC;
+	const StoreView &sv = p.sv;
+	const QueryView &qv = p.qv;
+	const bool hmap = p.hmap, fast_ok = p.fast_ok, all_fallback = !p.fast_ok;
+	const int64_t n_tiles = p.n_tiles;
+	constexpr int64_t DENSE_MAX_ROWS = 65536;
+	int *dstat = hmap ? P.d_status_map : P.status.p;
+	int *d_cert = dstat;
+	// a pass enqueued asynchronously completes at its event (later passes may be
+	// queued behind it); a synchronous one at the end of the stream
+	if (p.async) {
+		for (auto &v : last_stats) v = 0;  // this pass's statistics alone
+		last_stats[3] = p.st3;
+		last_stats[5] = p.st5;
+		hipError_t e;
+		while ((e = hipEventQuery(P.done)) == hipErrorNotReady) {
+		}
+		if (e != hipSuccess) throw Error(std::string("HIP error: ") + hipGetErrorString(e) + " at pass completion");
+	} else {
+		spin_sync(stream);
+	}
+	if (time_kernels && !all_fallback && !p.dense) {
 		// the append scan's own time (both launches of a progressive pass)
-		const bool two = split_div > 1 && scan8_fits(sv) && n_tiles >= (int64_t)128 * split_div;
-		kt_append_ms += toc_ms(2, 3) + (two ? toc_ms(4, 5) : 0.f);
+		kt_append_ms += toc_ms(2, 3) + (p.two_append ? toc_ms(4, 5) : 0.f);
 		kt_append_n += 1;
 		kt_append_rows = n_slots;
-		kt_append_qpad = nq_pad;
+		kt_append_qpad = qv.nq_pad;
 		kt_append_kernel = scan8_fits(sv) ? 2 : 0;
 	}
-	const int *h_cert = ws.h_status;
+	const int *h_cert = P.h_status;
 	for (int q = 0; q < nq; ++q) {
-		last_stats[1] += ws.h_status[nq + q];
-		last_stats[2] = std::max<int64_t>(last_stats[2], ws.h_status[2 * nq + q]);
+		last_stats[1] += P.h_status[nq + q];
+		last_stats[2] = std::max<int64_t>(last_stats[2], P.h_status[2 * nq + q]);
 	}
+	// any rerun / fallback below: first let every later pass queued behind this
+	// one finish (their kernels read the shared workspace these launches reuse)
+	bool synced = !p.async;
+	auto sync_later = [&]() {
+		if (!synced) spin_sync(stream);
+		synced = true;
+	};
 	// threshold path: rerun the uncertified queries as a batch of their own,
 	// tau = their previous pass's k-th exact distance, full-size segments (up
 	// to two reruns: a pool over the selection's capacity still yields real
@@ -232,13 +312,16 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	// A query that found no candidate at all (NaN bound: a zero cosine query)
 	// goes straight to the exact fallback.
 	std::vector<char> rerun(nq, 0);
-	for (int q = 0; q < nq; ++q) rerun[q] = !h_cert[q] && ws.h_status[nq + q] > 0;
+	for (int q = 0; q < nq; ++q) rerun[q] = !h_cert[q] && P.h_status[nq + q] > 0;
+	bool enqueued = false;
 	for (int attempt = 0; attempt < 2 && fast_ok && n_slots > DENSE_MAX_ROWS && retry_pass; ++attempt) {
 		std::vector<int> fq;
 		for (int q = 0; q < nq; ++q)
 			if (rerun[q] && !h_cert[q]) fq.push_back(q);
 		const int nf = (int)fq.size();
 		if (nf == 0) break;
+		sync_later();
+		enqueued = true;
 		{
 			if (attempt == 0) last_stats[4] += nf;
 			const int nf_pad = (int)round_up(nf, SCAN_BQ);
@@ -254,7 +337,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 			HIPCHK(hipMemcpyAsync(ws.rfq.p, fq.data(), (size_t)nf * sizeof(int), hipMemcpyHostToDevice, stream));
 			// tau tightened to just above the first pass's k-th distance (a pool
 			// that overflowed shrinks; pool_refine refines as far as it needs)
-			launch_retry_gather(ws.rfq.p, nf, nf_pad, ld, k, qv, ws.tau.p, dD, ws.rQf.p, ws.rQb.p, ws.rqaux.p,
+			launch_retry_gather(ws.rfq.p, nf, nf_pad, ld, k, qv, P.tau.p, dD, ws.rQf.p, ws.rQb.p, ws.rqaux.p,
 			                    ws.rtau.p, ws.rstat.p, stream);
 			const QueryView qv2{ws.rQf.p, ws.rQb.p, ws.rqaux.p, nf, nf_pad};
 			const int n_seg = scan_append_segments(sv, n_tiles);
@@ -266,11 +349,11 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 			launch_scan_append(sv, qv2, ws.rtau.p, ws.seg_pool.p, ws.seg_cnt.p, cap2, stream);
 			launch_pool_refine(sv, qv2, ws.seg_pool.p, ws.seg_cnt.p, cap2, n_seg, ws.rtau.p, k, 1, 0, live_rows(),
 			                   nullptr, ws.rL.p, ws.rD.p, ws.rC.p, cert2, cnt2, pool2, stream);
-			launch_retry_scatter(ws.rfq.p, nf, k, ws.rL.p, ws.rD.p, ws.rC.p, cert2, ws.rtau.p, dL, dD, dC, d_cert, ws.tau.p,
+			launch_retry_scatter(ws.rfq.p, nf, k, ws.rL.p, ws.rD.p, ws.rC.p, cert2, ws.rtau.p, dL, dD, dC, d_cert, P.tau.p,
 			                     stream);
 			HIPCHK(hipGetLastError());
 			if (!hmap)
-				HIPCHK(hipMemcpyAsync(ws.h_status, d_cert, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, stream));
+				HIPCHK(hipMemcpyAsync(P.h_status, d_cert, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, stream));
 			spin_sync(stream);
 		}
 	}
@@ -286,10 +369,12 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 	// cosine query — which no threshold keeps: exact fallback too)
 	std::vector<int> fbq;
 	for (int q = 0; q < nq; ++q)
-		if (all_fallback || !h_cert[q] || (ws.h_status[nq + q] == 0 && live_rows() > 0)) fbq.push_back(q);
+		if (all_fallback || !h_cert[q] || (P.h_status[nq + q] == 0 && live_rows() > 0)) fbq.push_back(q);
 	last_stats[0] += (int64_t)fbq.size();
 	std::vector<int> slow;
+	if (!fbq.empty()) sync_later();
 	if (!fbq.empty() && fast_ok) {
+		enqueued = true;
 		const int nf = (int)fbq.size();
 		const int nf_pad = (int)round_up(nf, SCAN_BQ);
 		ws.rfq.need(nf);
@@ -302,7 +387,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		ws.rD.need((size_t)nf * k);
 		ws.rC.need(nf);
 		HIPCHK(hipMemcpyAsync(ws.rfq.p, fbq.data(), (size_t)nf * sizeof(int), hipMemcpyHostToDevice, stream));
-		launch_retry_gather(ws.rfq.p, nf, nf_pad, ld, k, qv, ws.tau.p, dD, ws.rQf.p, ws.rQb.p, ws.rqaux.p, ws.rtau.p,
+		launch_retry_gather(ws.rfq.p, nf, nf_pad, ld, k, qv, P.tau.p, dD, ws.rQf.p, ws.rQb.p, ws.rqaux.p, ws.rtau.p,
 		                    ws.rstat.p, stream);
 		// keys of up to FB_GROUP queries at a time, within 1 GiB
 		constexpr int FB_GROUP = 16;
@@ -325,7 +410,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		// says about ties at the cut
 		HIPCHK(hipMemsetAsync(cert2, 0x01, (size_t)nf * sizeof(int), stream));
 		launch_retry_scatter(ws.rfq.p, nf, k, ws.rL.p, ws.rD.p, ws.rC.p, cert2, ws.rtau.p, dL, dD, dC, d_cert,
-		                     ws.tau.p, stream);
+		                     P.tau.p, stream);
 		HIPCHK(hipGetLastError());
 		std::vector<int> hc((size_t)nf);
 		HIPCHK(hipMemcpyAsync(hc.data(), ws.rC.p, (size_t)nf * sizeof(int), hipMemcpyDeviceToHost, stream));
@@ -337,6 +422,7 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		slow = fbq;
 	}
 	for (int q : slow) {
+		enqueued = true;
 		ws.fb_keys.need((size_t)n_slots);
 		ws.fb_keys2.need((size_t)n_slots);
 		ws.fb_vals.need((size_t)n_slots);
@@ -351,7 +437,53 @@ void Index::search_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL
 		launch_copy_fallback(ws.fb_keys2.p, ws.fb_vals2.p, live_rows(), k, q, dL, dD, dC, stream);
 		HIPCHK(hipGetLastError());
 	}
-	HIPCHK(hipStreamSynchronize(stream));
+	if (enqueued) HIPCHK(hipStreamSynchronize(stream));
+}
+
+// ---- asynchronous searches (lance_hip_search_batch_device_async) ----------
+// A threshold-path pass (one pipeline pass, no filter / IVF / timing) is only
+// enqueued; its certificate check and any reruns run at wait (or when a third
+// search arrives, or before anything else touches the handle).  Two pass-buffer
+// sets let pass i+1 be enqueued while pass i is still on the device.
+int64_t Index::search_async(const float *dQ, int nq, int k, int nprobes, int refine, int64_t *dL, float *dD,
+                            int *dC) {
+	const int64_t ticket = next_ticket++;
+	const bool asyncable = !ivf && !filter_on && !time_kernels && nq <= MAX_PASS_Q && n_slots > 65536 &&
+	                       !(small_exact && small_exact_fits(n_slots, dim, nq, k));
+	if (!asyncable) {
+		drain();
+		search_any(dQ, nq, k, nprobes, refine, dL, dD, dC);
+		return ticket;
+	}
+	while (pending.size() >= 2) finish_oldest();
+	// a stale int8 copy / missing scan copy is rebuilt in place: not under pending passes
+	if (!pending.empty() && ((i8_usable() && !(Xq && q8_ver == mut_ver && q8_cap == cap)) ||
+	                         (has_scan_copy() && !Xs)))
+		drain();
+	for (auto &v : last_stats) v = 0;
+	PendingPass p;
+	const int slot = pb_free_slot();
+	if (!enqueue_chunk(dQ, nq, k, refine, dL, dD, dC, slot, true, p)) return ticket;  // (completed)
+	p.async = true;
+	p.st3 = last_stats[3];
+	p.st5 = last_stats[5];
+	p.ticket = ticket;
+	pending.push_back(p);
+	return ticket;
+}
+
+void Index::finish_oldest() {
+	PendingPass p = pending.front();
+	pending.pop_front();
+	finish_chunk(p);
+}
+
+void Index::wait_ticket(int64_t ticket) {
+	while (!pending.empty() && (ticket <= 0 || pending.front().ticket <= ticket)) finish_oldest();
+}
+
+void Index::drain() {
+	while (!pending.empty()) finish_oldest();
 }
 
 // ---------------------------------------------------------------------------
@@ -1286,6 +1418,50 @@ int32_t lance_hip_search_batch_device(void *handle, const float *d_queries, int3
 		}
 		ix->search_any(d_queries, nq, k, nprobes, refine_factor, d_out_labels, d_out_distances, d_out_counts);
 		return nq;
+	}
+	API_GUARD("search failed: ", -1)
+}
+
+int64_t lance_hip_search_batch_device_async(void *handle, const float *d_queries, int32_t nq, int32_t dim, int32_t k,
+                                            int32_t nprobes, int32_t refine_factor, int64_t *d_out_labels,
+                                            float *d_out_distances, int32_t *d_out_counts, char *err_buf,
+                                            int err_buf_len) {
+	if (!handle) {
+		lhip::write_err(err_buf, err_buf_len, "null handle");
+		return -1;
+	}
+	try {
+		Index *ix = as_index(handle);
+		if (dim != ix->dim)
+			throw Error("expected query dimension " + std::to_string(ix->dim) + ", got " + std::to_string(dim));
+		if (k <= 0) throw Error("k must be positive");
+		if (nq < 0) throw Error("negative query count");
+		if (nq > 0 && (!d_queries || !d_out_labels || !d_out_distances || !d_out_counts)) throw Error("null buffer");
+		std::lock_guard<std::mutex> g(ix->mu);
+		ix->bind_nodrain();
+		if (nq == 0) return ix->next_ticket++;
+		if (ix->n_live == 0) {
+			ix->drain();
+			HIPCHK(hipMemsetAsync(d_out_counts, 0, (size_t)nq * sizeof(int32_t), ix->stream));
+			HIPCHK(hipStreamSynchronize(ix->stream));
+			return ix->next_ticket++;
+		}
+		return ix->search_async(d_queries, nq, k, nprobes, refine_factor, d_out_labels, d_out_distances, d_out_counts);
+	}
+	API_GUARD("search failed: ", -1)
+}
+
+int32_t lance_hip_search_wait(void *handle, int64_t ticket, char *err_buf, int err_buf_len) {
+	if (!handle) {
+		lhip::write_err(err_buf, err_buf_len, "null handle");
+		return -1;
+	}
+	try {
+		Index *ix = as_index(handle);
+		std::lock_guard<std::mutex> g(ix->mu);
+		ix->bind_nodrain();
+		ix->wait_ticket(ticket);
+		return 0;
 	}
 	API_GUARD("search failed: ", -1)
 }

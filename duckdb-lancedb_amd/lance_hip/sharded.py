@@ -121,3 +121,64 @@ def hip_device_search(lib, handle, dim: int, nprobes: int = 20, refine_factor: i
         return ol, od, oc
 
     return search
+
+
+class AsyncPipeline:
+    """Two batches in flight on one handle (lance_hip_search_batch_device_async):
+    ``step(Q, k)`` enqueues a batch and completes the previous one (certificate
+    check, reruns, fallbacks at its wait), so the host's per-batch work overlaps
+    the device's; ``drain()`` completes the last.  Returns the outputs of the
+    batch completed by the call (None on the first)."""
+
+    def __init__(self, lib, handle, dim: int, nprobes: int = 20, refine_factor: int = 1, err_len: int = 2048):
+        import ctypes
+
+        self.lib, self.h, self.dim = lib, handle, dim
+        self.nprobes, self.refine = nprobes, refine_factor
+        self.e = ctypes.create_string_buffer(err_len)
+        self.err_len = err_len
+        self.outs = {}
+        self.pending = []  # (ticket, outputs)
+        self.i = 0
+
+    def _out(self, nq, k, dev, j):
+        import torch
+
+        key = (nq, k, dev, j)
+        if key not in self.outs:
+            self.outs[key] = (torch.empty((nq, k), dtype=torch.int64, device=dev),
+                              torch.empty((nq, k), dtype=torch.float32, device=dev),
+                              torch.empty((nq,), dtype=torch.int32, device=dev))
+        return self.outs[key]
+
+    def submit(self, Q, k):
+        import torch
+
+        nq = Q.shape[0]
+        ol, od, oc = o = self._out(nq, k, Q.device, self.i & 1)
+        self.i += 1
+        cs = torch.cuda.current_stream()
+        if not cs.query():
+            cs.synchronize()
+        t = self.lib.lance_hip_search_batch_device_async(self.h, Q.data_ptr(), nq, self.dim, k, self.nprobes,
+                                                         self.refine, ol.data_ptr(), od.data_ptr(), oc.data_ptr(),
+                                                         self.e, self.err_len)
+        if t < 0:
+            raise RuntimeError(self.e.value.decode())
+        self.pending.append((t, o))
+        return t
+
+    def wait(self, ticket=0):
+        if self.lib.lance_hip_search_wait(self.h, ticket, self.e, self.err_len) != 0:
+            raise RuntimeError(self.e.value.decode())
+        done = [p for p in self.pending if ticket <= 0 or p[0] <= ticket]
+        self.pending = [p for p in self.pending if not (ticket <= 0 or p[0] <= ticket)]
+        return done[-1][1] if done else None
+
+    def step(self, Q, k):
+        prev = self.pending[-1][0] if self.pending else None
+        self.submit(Q, k)
+        return self.wait(prev) if prev is not None else None
+
+    def drain(self):
+        return self.wait(0)

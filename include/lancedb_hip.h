@@ -272,6 +272,27 @@ int32_t lance_hip_search_batch_device(void *handle, const float *d_queries, int3
                                       int32_t nprobes, int32_t refine_factor, int64_t *d_out_labels,
                                       float *d_out_distances, int32_t *d_out_counts, char *err_buf, int err_buf_len);
 
+/* NEW — asynchronous device-pointer search (a serving loop that keeps the GPU
+ * busy while the host prepares the next batch).  Same arguments and results as
+ * lance_hip_search_batch_device, but the call only enqueues the search on the
+ * handle's stream and returns a ticket (>= 1) or -1; the results are final —
+ * certified, reruns and exact fallbacks done — once lance_hip_search_wait
+ * returns for that ticket.  d_queries must be ready on entry (stream-ordered
+ * before the call); it and the outputs must stay valid until the wait.  At
+ * most two searches are in flight per handle (a third call first completes
+ * the oldest); any other call on the handle (search, add, delete, options,
+ * ...) first completes every pending one.  Searches that are not a single
+ * threshold-path pass (IVF, predicate, small stores, > 2048 queries, option
+ * time_kernels) run synchronously inside the call. */
+int64_t lance_hip_search_batch_device_async(void *handle, const float *d_queries, int32_t nq, int32_t dim, int32_t k,
+                                            int32_t nprobes, int32_t refine_factor, int64_t *d_out_labels,
+                                            float *d_out_distances, int32_t *d_out_counts, char *err_buf,
+                                            int err_buf_len);
+
+/* NEW — completes every asynchronous search of the handle up to `ticket`
+ * (<= 0: all of them).  0 or -1. */
+int32_t lance_hip_search_wait(void *handle, int64_t ticket, char *err_buf, int err_buf_len);
+
 /* Device-pointer variant of lance_hip_merge_topk (current device, null stream). */
 int32_t lance_hip_merge_topk_device(int32_t nshard, int32_t nq, int32_t k, const int64_t *d_part_labels,
                                     const float *d_part_dists, const int32_t *d_part_counts, int64_t *d_out_labels,

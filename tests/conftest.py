@@ -20,6 +20,15 @@ def hip():
     """The product library; GPU tests fail loudly (no fallback) if it is missing."""
     import lance_hip
 
+    # torch's bundled HIP runtime first (tests move queries and outputs through
+    # torch tensors): initialised after the library's runtime it finds no device
+    try:
+        import torch
+
+        if torch.cuda.device_count() > 0:
+            torch.cuda.init()
+    except ImportError:
+        pass
     lance_hip.lib()
     assert lance_hip.device_count() > 0, "no HIP device visible to liblancedb_hip.so"
     return lance_hip

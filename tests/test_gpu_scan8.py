@@ -274,3 +274,51 @@ def test_release_build_rejects_development_knobs(hip):
     finally:
         hip.LanceFreeDetached(h)
         hip.LanceFreeDetached(h2)
+
+
+def test_async_pipeline_matches_sync(hip):
+    """lance_hip_search_batch_device_async / lance_hip_search_wait: two batches
+    in flight per handle (the second pass enqueued while the first is on the
+    device, each with its own query / status buffers), a third submit completes
+    the oldest, a mutation completes every pending search before it changes the
+    store; every batch's results equal the synchronous search and the oracle."""
+    import torch
+    from lance_hip.sharded import AsyncPipeline, hip_device_search
+
+    rng = np.random.default_rng(42)
+    n, d, k = 120_000, 768, 10
+    X = rng.standard_normal((n, d), dtype=np.float32)
+    Qs = [rng.standard_normal((nq, d), dtype=np.float32) for nq in (256, 300, 17, 256)]
+    h = hip.LanceCreateDetached("", d, "l2", "t")
+    try:
+        hip.LanceDetachedAddBatch(h, X[:100_000], 100_000, d)
+        L = hip.lib()
+        pipe = AsyncPipeline(L, h, d)
+        sync = hip_device_search(L, h, d)
+        Qd = [torch.from_numpy(q).cuda() for q in Qs]
+        exp = [c_oracle.flat_search_batch(X[:100_000], q, k, "l2", acc64=True, nthreads=16) for q in Qs]
+        t = [pipe.submit(Qd[i], k) for i in range(3)]  # the third submit completes the first
+        assert t[0] < t[1] < t[2]
+        outs = {}
+        for i in (1, 2):
+            o = pipe.wait(t[i])
+            outs[i] = tuple(x.cpu().numpy() for x in o)
+        for i in (1, 2):
+            assert_same(*outs[i], *exp[i])
+        # a pending search, then an append: the append first completes it
+        t3 = pipe.submit(Qd[3], k)
+        o3 = pipe.pending[-1][1]
+        hip.LanceDetachedAddBatch(h, X[100_000:], n - 100_000, d)
+        pipe.wait(t3)
+        assert_same(*(x.cpu().numpy() for x in o3), *exp[3])
+        # after the append: pipelined steps over the whole store == synchronous search
+        e0 = c_oracle.flat_search_batch(X, Qs[0], k, "l2", acc64=True, nthreads=16)
+        res = [pipe.step(Qd[0], k) for _ in range(4)]
+        last = pipe.drain()
+        for r in [x for x in res if x is not None] + [last]:
+            assert_same(*(x.cpu().numpy() for x in r), *e0)
+        assert_same(*(x.cpu().numpy() for x in sync(Qd[0], k)), *e0)
+        st = hip.LanceHipLastSearchStats(h)
+        assert st["fallback_queries"] == 0 and st["append_launches"] == 1, st
+    finally:
+        hip.LanceFreeDetached(h)
