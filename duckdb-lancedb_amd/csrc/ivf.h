@@ -62,6 +62,10 @@ struct IvfState {
 	DevBuf<uint8_t> lcodes;                  // [npos/64][mp/16][64][16] blocked codes
 	DevBuf<float> ltau;                      // [npos] row term of the L2 / cosine ADC (list order)
 	DevBuf<int> blk_list, lblk0;             // IVF_FLAT work items (256 positions each)
+	// IVF_FLAT bound scan: the bf16 (RNE) rows in list position order, [npos + 256][ld]
+	// (zero rows for padding): an item's 256 rows are one contiguous 256 x ld block
+	DevBuf<uint16_t> lrows;
+	bool lrows_ok = false;
 	DevBuf<int64_t> blk_pos0;
 	int nblk = 0, maxb = 1;
 	// search workspace
@@ -149,10 +153,15 @@ void launch_flat_list_scan(const StoreView &s, const int *blk_list, const int64_
                            const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart, const int *pairs,
                            int nprobe, int maxb, int64_t tail_s0, int64_t tail_n, int nq, const double *Qd,
                            const double *qn2, int kk, uint64_t *out, hipStream_t st);
-// IVF_FLAT bound scan (MFMA bf16 lower bounds): out [pair][maxb][16] (LB, slot) keys per (query, item)
+// IVF_FLAT bound scan (MFMA bf16 lower bounds): out [pair][maxb][16] (LB, slot) keys per (query, item);
+// rows from lrows (list order, launch_list_rows_bf16) or, when null, from the store's bf16 scan rows by slot
 void launch_flat_list_lb(const StoreView &s, const int *blk_list, const int64_t *blk_pos0, const int *lblk0,
                          const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart, const int *pairs,
-                         int nprobe, int maxb, const uint16_t *Qb, const float4 *qaux, uint64_t *out, hipStream_t st);
+                         int nprobe, int maxb, const uint16_t *Qb, const float4 *qaux, uint64_t *out, hipStream_t st,
+                         const uint16_t *lrows = nullptr);
+// out [npos][ld] = bf16 (RNE) of the row at each list position (f32 or bf16 store X), zero for padding
+void launch_list_rows_bf16(const void *X, int xbf16, int ld, int dim, const uint32_t *lslot, int64_t npos,
+                           uint16_t *out, hipStream_t st);
 // per query: top-M bound candidates of its probed lists and the cut (every other row has LB >= cut)
 void launch_flat_lb_merge(int nq, int nprobe, const int64_t *probe_l, const int *lblk0, int maxb, const uint64_t *keys,
                           int M, uint64_t *cand, float *cut, hipStream_t st);

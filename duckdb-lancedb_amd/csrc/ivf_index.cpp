@@ -28,7 +28,8 @@ IvfState::~IvfState() { delete coarse; }
 void ivf_free(IvfState *s) { delete s; }
 
 static StoreView store_view(Index *ix) {
-	ix->ensure_xs();  // the IVF_FLAT bound scan and the coarse search stream bf16 rows
+	// (the IVF_FLAT bound scan streams its own list-order bf16 rows, IvfState::lrows;
+	// the exact list scans, re-ranks and PQ read X)
 	return StoreView{ix->X,  ix->rowaux, ix->dlabels, ix->n_slots, ix->ld, ix->dim, ix->metric, ix->xbf16 ? 1 : 0,
 	                 ix->Xs ? static_cast<const void *>(ix->Xs) : ix->X, (ix->xbf16 || ix->Xs) ? 1 : 0};
 }
@@ -409,6 +410,19 @@ static void layout(Index *ix) {
 			HIPCHK(hipMemcpyAsync(s->blk_pos0.p, bp.data(), bp.size() * sizeof(int64_t), hipMemcpyHostToDevice, st));
 		}
 		HIPCHK(hipMemcpyAsync(s->lblk0.p, l0.data(), l0.size() * sizeof(int), hipMemcpyHostToDevice, st));
+		// the bound scan's rows in list order (+ one item of zero rows past the
+		// end: the last item reads 256 positions); rebuilt with the layout
+		s->lrows_ok = false;
+		if (ix->ivf_flat_bound && ix->ld % 64 == 0) {
+			const size_t rows = (size_t)npos + FLAT_BLK;
+			s->lrows.need(rows * ix->ld);
+			HIPCHK(hipMemsetAsync(s->lrows.p + (size_t)npos * ix->ld, 0, (size_t)FLAT_BLK * ix->ld * sizeof(uint16_t), st));
+			launch_list_rows_bf16(ix->X, ix->xbf16 ? 1 : 0, ix->ld, ix->dim, s->lslot.p, npos, s->lrows.p, st);
+			HIPCHK(hipGetLastError());
+			s->lrows_ok = true;
+		} else {
+			s->lrows.release();
+		}
 	} else {
 		s->lcodes.need((size_t)std::max<int64_t>(npos, 64) * s->mp);
 		launch_pq_layout(s->codes.p, s->lslot.p, npos, s->mp, s->lcodes.p, st);
@@ -468,7 +482,8 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 	const int pass = (int)std::max<int64_t>(1, std::min<int64_t>(MAX_PASS_Q, (int64_t)(1 << 27) / std::max<int64_t>(per_q, 1)));
 	const bool fast_pq = s->type == IVF_PQ && ix->pq_fast && s->m <= FQ_MAX_M && kp <= FQ_MAX_KK;
 	// IVF_FLAT bound scan: bf16 scan rows, k within an item's leaders
-	const bool lb_flat = s->type == IVF_FLAT && ix->ivf_flat_bound && sv.scan_bf16 && ld % 64 == 0 && k <= FL_KEYS - 1;
+	const bool lb_flat = s->type == IVF_FLAT && ix->ivf_flat_bound && (s->lrows_ok || sv.scan_bf16) && ld % 64 == 0 &&
+	                     k <= FL_KEYS - 1;
 	for (int q0 = 0; q0 < nq; q0 += pass) {
 		const int n = std::min(pass, nq - q0);
 		s->Qf.need((size_t)n * ld);
@@ -515,7 +530,8 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			s->keys.need((size_t)n * nprobe * s->maxb * FL_KEYS);
 			ix->tic(0);
 			launch_flat_list_lb(sv, s->blk_list.p, s->blk_pos0.p, s->lblk0.p, s->loff.p, s->lslot.p, s->nblk,
-			                    s->pstart.p, s->pairs.p, nprobe, s->maxb, s->lbQb.p, s->lbqaux.p, s->keys.p, st);
+			                    s->pstart.p, s->pairs.p, nprobe, s->maxb, s->lbQb.p, s->lbqaux.p, s->keys.p, st,
+			                    s->lrows_ok ? s->lrows.p : nullptr);
 			ix->tic(1);
 			const int M = std::min(IVF_TOPK_CAP - 1, k + 32);
 			s->cand_a.need((size_t)n * M);

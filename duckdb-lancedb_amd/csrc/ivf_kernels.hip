@@ -1060,7 +1060,8 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
     const uint16_t *__restrict__ Xb, int ld, const float *__restrict__ rowaux_f, const int *__restrict__ blk_list,
     const int64_t *__restrict__ blk_pos0, const int *__restrict__ lblk0, const int64_t *__restrict__ loff,
     const uint32_t *__restrict__ lslot, const int *__restrict__ pstart, const int *__restrict__ pairs, int nprobe,
-    int maxb, const uint16_t *__restrict__ Qb, const float4 *__restrict__ qaux, uint64_t *__restrict__ out) {
+    int maxb, const uint16_t *__restrict__ Qb, const float4 *__restrict__ qaux, uint64_t *__restrict__ out,
+    const uint16_t *__restrict__ Lrows) {
 	extern __shared__ __attribute__((aligned(16))) uint8_t fl_smem[];
 	const int qrow = ld * 2 + 16;  // padded query row (bytes): 16 lanes reading 16 rows hit distinct banks
 	uint8_t *qs = fl_smem;                                                          // [FL_G][qrow]
@@ -1129,13 +1130,16 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
 #pragma unroll
 			for (int rb = 0; rb < 4; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
 		}
-		// row pointers of this lane's 4 rows (padding rows read slot 0: finite
-		// bf16, their LB is +inf through alpha)
+		// row pointers of this lane's 4 rows: list-order rows (the item is one
+		// contiguous 256 x ld block; positions past the list end read the next
+		// list's or zero padding rows), else by slot (padding rows read slot 0);
+		// either way a padding row's LB is +inf through alpha
 		const uint16_t *xp[4];
 #pragma unroll
 		for (int rb = 0; rb < 4; ++rb) {
-			const uint32_t s = sslot[64 * w + 16 * rb + rr];
-			xp[rb] = Xb + (int64_t)(s == SLOT_NONE ? 0u : s) * ld + 8 * gq;
+			const int r = 64 * w + 16 * rb + rr;
+			const uint32_t s = sslot[r];
+			xp[rb] = Lrows ? Lrows + (p0 + r) * (int64_t)ld + 8 * gq : Xb + (int64_t)(s == SLOT_NONE ? 0u : s) * ld + 8 * gq;
 		}
 		const uint8_t *qb = qs + rr * qrow + 16 * gq;
 		// two windows of rows in flight
@@ -1313,9 +1317,10 @@ size_t flat_lb_lds_bytes(int ld) { return (size_t)FL_G * (ld * 2 + 16) + (size_t
 
 void launch_flat_list_lb(const StoreView &s, const int *blk_list, const int64_t *blk_pos0, const int *lblk0,
                          const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart, const int *pairs,
-                         int nprobe, int maxb, const uint16_t *Qb, const float4 *qaux, uint64_t *out, hipStream_t st) {
+                         int nprobe, int maxb, const uint16_t *Qb, const float4 *qaux, uint64_t *out, hipStream_t st,
+                         const uint16_t *lrows) {
 	if (nblk <= 0) return;
-	if (!s.scan_bf16 || s.ld % 64) throw std::runtime_error("IVF_FLAT bound scan needs bf16 scan rows");
+	if ((!lrows && !s.scan_bf16) || s.ld % 64) throw std::runtime_error("IVF_FLAT bound scan needs bf16 scan rows");
 	const uint16_t *Xb = static_cast<const uint16_t *>(s.Xscan);
 	const float *ra = reinterpret_cast<const float *>(s.rowaux);
 	const size_t lds = flat_lb_lds_bytes(s.ld);
@@ -1323,13 +1328,45 @@ void launch_flat_list_lb(const StoreView &s, const int *blk_list, const int64_t 
 		HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
 		                           (int)lds));
 		kern<<<dim3((unsigned)nblk), 256, lds, st>>>(Xb, s.ld, ra, blk_list, blk_pos0, lblk0, loff, lslot, pstart,
-		                                              pairs, nprobe, maxb, Qb, qaux, out);
+		                                              pairs, nprobe, maxb, Qb, qaux, out, lrows);
 	};
 	switch (s.metric) {
 	case METRIC_L2: go(flat_list_lb_kernel<METRIC_L2>); break;
 	case METRIC_DOT: go(flat_list_lb_kernel<METRIC_DOT>); break;
 	default: go(flat_list_lb_kernel<METRIC_COSINE>); break;
 	}
+}
+
+// one wave per list position: 8 elements per lane and step (two 16-B f32 loads
+// or one 16-B bf16 load -> one 16-B store)
+__global__ __launch_bounds__(256) void list_rows_bf16_kernel(const void *__restrict__ X, int xbf16, int ld, int dim,
+                                                             const uint32_t *__restrict__ lslot, int64_t npos,
+                                                             uint16_t *__restrict__ out) {
+	const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+	const int lane = threadIdx.x & 63;
+	if (p >= npos) return;
+	const uint32_t s = lslot[p];
+	for (int c = 8 * lane; c < ld; c += 512) {
+		uint4 o = make_uint4(0u, 0u, 0u, 0u);
+		if (s != SLOT_NONE) {
+			if (xbf16) {
+				o = *reinterpret_cast<const uint4 *>(static_cast<const uint16_t *>(X) + (int64_t)s * ld + c);
+			} else {
+				const float *x = static_cast<const float *>(X) + (int64_t)s * ld + c;
+				const float4 a = *reinterpret_cast<const float4 *>(x), b = *reinterpret_cast<const float4 *>(x + 4);
+				// (padding columns of the store are zero: bf16 zero)
+				o = make_uint4(pk_bf16(a.x, a.y), pk_bf16(a.z, a.w), pk_bf16(b.x, b.y), pk_bf16(b.z, b.w));
+			}
+		}
+		*reinterpret_cast<uint4 *>(out + p * ld + c) = o;
+	}
+}
+
+void launch_list_rows_bf16(const void *X, int xbf16, int ld, int dim, const uint32_t *lslot, int64_t npos,
+                           uint16_t *out, hipStream_t st) {
+	if (npos <= 0) return;
+	if (ld % 8) throw std::runtime_error("list rows: row stride must be a multiple of 8");
+	list_rows_bf16_kernel<<<dim3((unsigned)((npos + 3) / 4)), 256, 0, st>>>(X, xbf16, ld, dim, lslot, npos, out);
 }
 
 void launch_flat_lb_merge(int nq, int nprobe, const int64_t *probe_l, const int *lblk0, int maxb, const uint64_t *keys,
@@ -1742,7 +1779,40 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 		__syncthreads();
 		// interleaved LUT: u32 [j][c] = bytes (u_0, u_1, u_2, u_3)
 #ifndef LHIP_PQ_ABL_NO_LUT
-		{
+		if constexpr (MT > 0 && (MT * PQ_K / 16) % FQ_THREADS == 0) {
+			// 16 codes per lane and query per step, every step's loads in flight at
+			// once (the four tables are L2 / MALL reads: one latency per item, not
+			// one per step), then 4 x 4 byte transposes into four 16-B LDS stores
+			constexpr int NS = MT * PQ_K / 16 / FQ_THREADS;  // steps per thread (m = 96: 3)
+			uint4 w[NS][FQ_G];
+#pragma unroll
+			for (int sI = 0; sI < NS; ++sI)
+#pragma unroll
+				for (int i = 0; i < FQ_G; ++i)
+					w[sI][i] = qid[i] >= 0 ? reinterpret_cast<const uint4 *>(lut8 + (int64_t)qid[i] * MT * PQ_K)[t + sI * FQ_THREADS]
+					                       : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+			for (int sI = 0; sI < NS; ++sI) {
+				const int e16 = t + sI * FQ_THREADS;
+#pragma unroll
+				for (int sub = 0; sub < 4; ++sub) {
+					const uint32_t w0 = sub == 0 ? w[sI][0].x : sub == 1 ? w[sI][0].y : sub == 2 ? w[sI][0].z : w[sI][0].w;
+					const uint32_t w1 = sub == 0 ? w[sI][1].x : sub == 1 ? w[sI][1].y : sub == 2 ? w[sI][1].z : w[sI][1].w;
+					const uint32_t w2 = sub == 0 ? w[sI][2].x : sub == 1 ? w[sI][2].y : sub == 2 ? w[sI][2].z : w[sI][2].w;
+					const uint32_t w3 = sub == 0 ? w[sI][3].x : sub == 1 ? w[sI][3].y : sub == 2 ? w[sI][3].z : w[sI][3].w;
+					const uint32_t a01 = __builtin_amdgcn_perm(w1, w0, 0x05010400u);
+					const uint32_t a23 = __builtin_amdgcn_perm(w3, w2, 0x05010400u);
+					const uint32_t b01 = __builtin_amdgcn_perm(w1, w0, 0x07030602u);
+					const uint32_t b23 = __builtin_amdgcn_perm(w3, w2, 0x07030602u);
+					uint4 o;
+					o.x = __builtin_amdgcn_perm(a23, a01, 0x05040100u);
+					o.y = __builtin_amdgcn_perm(a23, a01, 0x07060302u);
+					o.z = __builtin_amdgcn_perm(b23, b01, 0x05040100u);
+					o.w = __builtin_amdgcn_perm(b23, b01, 0x07060302u);
+					reinterpret_cast<uint4 *>(L)[4 * e16 + sub] = o;
+				}
+			}
+		} else {
 			const int ne = m * PQ_K / 4;  // 4 codes per step
 			for (int e = t; e < ne; e += FQ_THREADS) {
 				uint32_t w[FQ_G];

@@ -138,6 +138,14 @@ int scan8_segments(int64_t n_tiles);
 bool scan8_variant_ok(int v);  // a geometry this build carries (release: 0 only)
 void launch_scan8_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
                          int seg_cap, hipStream_t st, int64_t t0 = 0, int64_t t1 = -1, int seg_base = 0);
+// The sample pass on the int8 copy (scan8_kernel, tilemin mode): row tiles
+// t * tile_stride, t < n_tiles; per tile, query and 32-row unit the row of
+// smallest bound -> (orderedkey(LB), slot) into scan8_segments(n_tiles)
+// segments per query of capacity >= scan8_tilemin_cap(n_tiles) (+inf / NaN
+// bounds skipped), launch_scan_tilemin's format.
+int scan8_tilemin_cap(int64_t n_tiles);
+void launch_scan8_tilemin(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, uint2 *seg_pool,
+                          int *seg_cnt, int seg_cap, hipStream_t st);
 // Segments per query launch_scan_append writes for this store.
 int scan_append_segments(const StoreView &s, int64_t n_tiles);
 

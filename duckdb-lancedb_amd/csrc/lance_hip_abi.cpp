@@ -27,6 +27,7 @@
 #include <stdexcept>
 #include <string>
 #include <sys/stat.h>
+#include <unistd.h>
 #include <vector>
 #include "index.h"
 #include "ivf.h"
@@ -181,8 +182,11 @@ bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *d
 		    n_tiles, std::max<int64_t>({(n_tiles + sample_div - 1) / sample_div, 32, (k + 9) / 2}));
 		const int64_t stride = std::max<int64_t>(1, n_tiles / n_sample);
 		const int Ms = k + 8;
-		const int n_seg_s = scan_grid(n_sample);
-		const int cap_s = (int)round_up(4 * ((n_sample + n_seg_s - 1) / n_seg_s), 4);
+		// (int8 copy: scan8_kernel's tilemin mode, one entry per 32-row unit; else
+		// scan_kernel's, one per 64-row quarter)
+		const bool s8s = scan8_fits(sv);
+		const int n_seg_s = s8s ? scan8_segments(n_sample) : scan_grid(n_sample);
+		const int cap_s = s8s ? scan8_tilemin_cap(n_sample) : (int)round_up(4 * ((n_sample + n_seg_s - 1) / n_seg_s), 4);
 		// 2) threshold scan over every row into per-(workgroup, query) segments;
 		//    a segment holds ~4x its expected share of the (k+8)*N/sample pool.
 		//    int8 scan8 path, large stores: progressive threshold.  The first
@@ -211,7 +215,10 @@ bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *d
 			drain();
 		ws.seg_pool.need(std::max(pool_s, pool_a));
 		ws.seg_cnt.need(cnt_n);
-		launch_scan_tilemin(sv, qv, n_sample, stride, ws.seg_pool.p, ws.seg_cnt.p, cap_s, stream);
+		if (s8s)
+			launch_scan8_tilemin(sv, qv, n_sample, stride, ws.seg_pool.p, ws.seg_cnt.p, cap_s, stream);
+		else
+			launch_scan_tilemin(sv, qv, n_sample, stride, ws.seg_pool.p, ws.seg_cnt.p, cap_s, stream);
 		launch_pool_refine(sv, qv, ws.seg_pool.p, ws.seg_cnt.p, cap_s, n_seg_s, nullptr, k, 0, Ms, -1, P.tau.p,
 		                   nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
 		tic(2);
@@ -229,6 +236,10 @@ bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *d
 			tic(3);
 		}
 		// 3) the pool in bound order, exact refine until certified
+#ifdef LHIP_DEV_PR_IDLE  // (development build: the final refine starts on an idle GPU, DVFS probe)
+		HIPCHK(hipStreamSynchronize(stream));
+		usleep(LHIP_DEV_PR_IDLE);
+#endif
 		launch_pool_refine(sv, qv, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, n_seg, P.tau.p, k, 1, 0, live_rows(),
 		                   nullptr, dL, dD, dC, d_cert, d_cand_cnt, d_pool_cnt, stream);
 		p.two_append = tA > 0;
@@ -1308,9 +1319,14 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			return 0;
 		}
 		if (k == "ivf_flat_scan") {
-			if (v == "bound") ix->ivf_flat_bound = true;
-			else if (v == "exact") ix->ivf_flat_bound = false;
+			bool b;
+			if (v == "bound") b = true;
+			else if (v == "exact") b = false;
 			else throw Error("ivf_flat_scan must be 'bound' or 'exact'");
+			ix->bind();
+			// the bound scan's list-order rows are built with the layout
+			if (b && !ix->ivf_flat_bound && ix->ivf) ix->ivf->dirty = true;
+			ix->ivf_flat_bound = b;
 			return 0;
 		}
 		if (k == "pq_scan") {

@@ -90,14 +90,20 @@ __device__ __forceinline__ int s8_query_part(float4 qp, float4 ts, float W) {
 // per-block bound terms (constants instead), bit 2 the appends, bit 6 the appends
 // kept in the code but never taken; bit 3 (a speed option, results exact):
 // s_setprio 2 over the k-loop, 0 over the rest
-template <int KS, int D, int RB, int ABL = 0>
+//
+// TM = 1: the SAMPLE pass instead (tilemin: row tile t of the launch is tile
+// tile0 + t * tstride): no threshold, the accumulators hold s; per work unit
+// (32 rows) and query the row of smallest bound, (orderedkey(LB), slot), goes
+// to the workgroup's segment (+inf / NaN bounds skipped): 8 entries per tile
+// and query for pool_refine's tau mode.
+template <int KS, int D, int RB, int ABL = 0, int TM = 0>
 __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *__restrict__ Xq, const float4 *__restrict__ aux8,
                                                       const float4 *__restrict__ tstat, int ld,
                                                       const int8_t *__restrict__ Qi, const float4 *__restrict__ qaux,
                                                       int nq, int n_tiles, int tile0, int seg_base,
                                                       const float *__restrict__ tau,
                                                       uint2 *__restrict__ seg_pool, int *__restrict__ seg_cnt,
-                                                      int seg_cap, int list_cap) {
+                                                      int seg_cap, int list_cap, int tstride) {
 	static_assert(KS % D == 0 && KS % 2 == 0, "ring slot and fragment buffer of a k-step must be static");
 	constexpr int NW = 16 / RB, T8 = 64 * NW;  // waves: each owns 16 RB rows of every tile
 	constexpr int WR = 16 * RB;                // rows per wave and tile
@@ -130,6 +136,9 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 		}
 	}
 	const int qb = q_tile + h * QH;  // first query of this workgroup
+#ifdef LHIP_S8_PROF
+	const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();  // (100 MHz: comparable across workgroups)
+#endif
 	const int tid = threadIdx.x, lane = tid & 63;
 	const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
 	const int lr = lane & 15, lg = lane >> 4;
@@ -147,7 +156,7 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 		const int q = qb + tid;
 		const float4 qa = qaux[q];
 		QA[tid] = qa;
-		QP[tid] = s8_query_terms(qa, q < nq ? tau[q] : -F_INF);
+		QP[tid] = s8_query_terms(qa, (TM == 0 && q < nq) ? tau[q] : -F_INF);
 		CNT[tid] = 0u;
 	}
 	if (tid == 0) *UCNT = (unsigned)NW;  // units 0 .. NW-1: one per wave, the rest claimed
@@ -212,7 +221,7 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 		uint32_t xo[RB];
 #pragma unroll
 		for (int rb = 0; rb < RB; ++rb) xo[rb] = (uint32_t)((16 * rb + lr) * 64 + 16 * lg);
-		auto utile = [&](int u) -> int64_t { return tile0 + pr + (int64_t)(u / NW) * NP; };
+		auto utile = [&](int u) -> int64_t { return tile0 + (pr + (int64_t)(u / NW) * NP) * (TM ? tstride : 1); };
 		auto xunit = [&](int u) -> const int8_t * {
 			return Xq + utile(u) * SCAN_BR * (int64_t)ld + (int64_t)(WR * (u % NW)) * 64;
 		};
@@ -281,6 +290,9 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 
 #ifdef LHIP_S8_PROF
 		pf_t = __builtin_amdgcn_s_memtime();
+		const uint64_t rt_loop = __builtin_amdgcn_s_memrealtime();
+		if (w == 0 && lane == 0 && TM == 0 && tile0 == 0)
+			printf("S8T wg=%d phase=loop t=%llu tiles=%d\n", b_id, (unsigned long long)rt_loop, my_tiles);
 #endif
 		for (;;) {
 			const int unn_raw = claim();        // the unit after next (read at this block's end)
@@ -291,7 +303,12 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 			const float W = (Sabs > 0.f && ts.x > 0.f) ? 1.0f / (Sabs * ts.x) : 0.f;
 			i32x4 bias[RB];
 			int gi[8];
-			if (ABL & 2) {
+			if (TM) {  // the sample pass: plain s in the accumulators
+#pragma unroll
+				for (int rb = 0; rb < RB; ++rb) bias[rb] = i32x4{0, 0, 0, 0};
+#pragma unroll
+				for (int u = 0; u < 8; ++u) gi[u] = BIG;
+			} else if (ABL & 2) {
 #pragma unroll
 				for (int rb = 0; rb < RB; ++rb) bias[rb] = i32x4{rb, 1, 2, 3};
 #pragma unroll
@@ -339,6 +356,55 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 			S8_T(pf_k);
 			if (ABL & 8) __builtin_amdgcn_s_setprio(0);  // screen, appends, next terms: behind the partner's MFMAs
 
+			if (TM) {
+				// per query: the smallest bound of this unit's WR rows (this lane: rows
+				// 16 rb + 4 lg + i, query 16 u + lr; then across the four lane groups)
+				const float *ra = reinterpret_cast<const float *>(aux8);
+				const int64_t rbase = utile(unit) * SCAN_BR + (int64_t)(WR * (unit % NW));
+				float4 t4[RB][4];
+#pragma unroll
+				for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+					for (int c = 0; c < 4; ++c)
+						t4[rb][c] = *reinterpret_cast<const float4 *>(ra + raix(rbase + 16 * rb + 4 * lg, c));
+#pragma unroll
+				for (int u = 0; u < 8; ++u) {
+					const float4 qa = QA[16 * u + lr];
+					uint64_t best = ~0ull;
+#pragma unroll
+					for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+						for (int i = 0; i < 4; ++i) {
+							const float al = i == 0 ? t4[rb][0].x : i == 1 ? t4[rb][0].y : i == 2 ? t4[rb][0].z : t4[rb][0].w;
+							const float xn = i == 0 ? t4[rb][1].x : i == 1 ? t4[rb][1].y : i == 2 ? t4[rb][1].z : t4[rb][1].w;
+							const float uxv = i == 0 ? t4[rb][2].x : i == 1 ? t4[rb][2].y : i == 2 ? t4[rb][2].z : t4[rb][2].w;
+							const float sc = i == 0 ? t4[rb][3].x : i == 1 ? t4[rb][3].y : i == 2 ? t4[rb][3].z : t4[rb][3].w;
+							// LB as the append pass's flush evaluates it
+							float v = fmaf(xn, qa.z, al);
+							v = fmaf(uxv, qa.y, v);
+							v = fmaf((float)acc[rb][u][i] * sc, qa.x, v);
+							v = v + qa.w;
+							const uint64_t key = ((uint64_t)fkey(v) << 32) | (uint32_t)(rbase + 16 * rb + 4 * lg + i);
+							best = key < best ? key : best;
+						}
+#pragma unroll
+					for (int o = 16; o < 64; o <<= 1) {
+						const uint64_t ob = ((uint64_t)(uint32_t)__shfl_xor((int)(best >> 32), o, 64) << 32) |
+						                    (uint32_t)__shfl_xor((int)(uint32_t)best, o, 64);
+						best = ob < best ? ob : best;
+					}
+					if (lg == 0 && (uint32_t)(best >> 32) < KEY_INF && qb + 16 * u + lr < nq) {
+						const unsigned p = atomicAdd(&CNT[16 * u + lr], 1u);
+						if (p < (unsigned)seg_cap)
+							seg_pool[((int64_t)(seg_base + b_id) * nq + qb + 16 * u + lr) * seg_cap + p] =
+							    make_uint2((uint32_t)(best >> 32), (uint32_t)best);
+					}
+				}
+				if (unext >= NU) break;
+				unit = unext;
+				unext = __builtin_amdgcn_readfirstlane(unn_raw);
+				continue;
+			}
 			// ---- screen: lane bit u = some bound of query 16u + lr passes ----
 			int hitm = 0;
 			if (ABL & 1) {
@@ -422,6 +488,9 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 #ifdef LHIP_S8_PROF
 	uint64_t pf_fl = 0;
 	S8_T(pf_fl);
+	if (lane == 0 && TM == 0 && tile0 == 0)
+		printf("S8T wg=%d w=%d phase=end t=%llu start=%llu\n", b_id, w, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+		       (unsigned long long)rt_start);
 	if (b_id < 3 && lane == 0)
 		printf("S8 wg=%d w=%d blocks=%d pro=%d k=%d scr=%d app=%d flush=%d list_end=%d hitblocks=%d\n", b_id, w,
 		       my_tiles, (int)pf_pro, (int)pf_k, (int)pf_scr, (int)pf_app, (int)pf_fl, nl_end, pf_hitb);
@@ -463,17 +532,42 @@ static int s8_list_cap(int ld, int nw) {
 	return std::min(1024, room / (nw * 9) / 64 * 64);
 }
 
-template <int KS, int D, int RB, int ABL = 0>
+template <int KS, int D, int RB, int ABL = 0, int TM = 0>
 static void s8_launch(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
-                      int seg_cap, int64_t t0, int64_t n_tiles, int seg_base, hipStream_t st) {
+                      int seg_cap, int64_t t0, int64_t n_tiles, int seg_base, hipStream_t st, int tstride = 1) {
 #ifndef LHIP_ABLATION_BUILD
 	static_assert(ABL == 0, "scan8 ablations (wrong results) exist only in LHIP_ABLATION_BUILD builds");
 #endif
 	const dim3 grid((unsigned)s8_groups(n_tiles), (unsigned)(q.nq_pad / SCAN_BQ));
 	constexpr int NW = 16 / RB;
-	scan8_kernel<KS, D, RB, ABL><<<grid, dim3(64 * NW), 0, st>>>(
+	scan8_kernel<KS, D, RB, ABL, TM><<<grid, dim3(64 * NW), 0, st>>>(
 	    static_cast<const int8_t *>(s.Xscan), s.scan_aux, s.tstat, s.ld, reinterpret_cast<const int8_t *>(q.Qb), q.qaux,
-	    q.nq, (int)n_tiles, (int)t0, seg_base, tau, seg_pool, seg_cnt, seg_cap, s8_list_cap(s.ld, NW));
+	    q.nq, (int)n_tiles, (int)t0, seg_base, tau, seg_pool, seg_cnt, seg_cap, s8_list_cap(s.ld, NW), tstride);
+}
+
+int scan8_tilemin_cap(int64_t n_tiles) {
+	const int groups = s8_groups(n_tiles);
+	const int64_t per = (n_tiles + groups / 2 - 1) / (groups / 2);  // tiles per pair (or per workgroup)
+	return (int)round_up(8 * per, 4);  // 8 units of 32 rows per tile, one entry per unit and query
+}
+
+void launch_scan8_tilemin(const StoreView &s, const QueryView &q, int64_t n_tiles, int64_t tile_stride, uint2 *seg_pool,
+                          int *seg_cnt, int seg_cap, hipStream_t st) {
+	if (n_tiles <= 0) return;
+	if (!scan8_fits(s)) throw std::runtime_error("scan8: int8 scan copy with ld in [512, 1024] required");
+	const int64_t all_tiles = (s.n_slots + SCAN_BR - 1) / SCAN_BR;
+	if ((n_tiles - 1) * tile_stride >= all_tiles) throw std::runtime_error("scan8 tilemin: tile range");
+	if (all_tiles * (int64_t)SCAN_BR > ((int64_t)1 << 32)) throw std::runtime_error("scan8: slots past 2^32");
+	if (q.nq_pad % SCAN_BQ) throw std::runtime_error("scan8: query tile padding");
+	if (seg_cap < scan8_tilemin_cap(n_tiles)) throw std::runtime_error("scan8 tilemin: segment capacity");
+	const int ts = (int)tile_stride;
+	switch (s.ld / 64) {
+	case 8: s8_launch<8, 4, 2, 0, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
+	case 10: s8_launch<10, 5, 2, 0, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
+	case 12: s8_launch<12, 4, 2, 0, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
+	case 14: s8_launch<14, 7, 2, 0, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
+	default: s8_launch<16, 4, 2, 0, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
+	}
 }
 
 bool scan8_variant_ok(int v) {
