@@ -268,7 +268,11 @@ struct Index {
 
 	// optional HIP-event timing of the scan kernels, on the stream they run on
 	bool time_kernels = false;
-	int sample_div = 32;  // sample pass covers ~1/sample_div of the tiles (>= 32 tiles)
+	// sample pass covers ~1/sample_div of the tiles (>= 32 tiles); 0 = auto: 16 up to
+	// 8192 tiles (2M rows: a tighter tau, fewer appended bounds; C2 790k vs 762k q/s,
+	// r04h), 32 past that (10M rows: the larger sample costs more than it saves, r03x)
+	int sample_div = 0;
+	int sample_div_eff(int64_t n_tiles) const { return sample_div > 0 ? sample_div : (n_tiles <= 8192 ? 16 : 32); }
 	bool small_exact = true;  // one-launch exact search for <= 8 queries over <= 32768 slots
 	bool defer_sync = false;  // caller synchronizes the stream itself (host-buffer search)
 	bool retry_pass = true;  // rerun uncertified queries with a tighter tau before the exact fallback

@@ -562,8 +562,7 @@ constexpr int BR = SCAN_BR, BQ = SCAN_BQ;
      defined(LHIP_ABL_NO_QDMA) || defined(LHIP_ABL_NO_SLOW) || defined(LHIP_ABL_SLOW_NEVER) ||               \
      defined(LHIP_ABL_DRAIN_EPI) || defined(LHIP_ABL_NO_LISTWRITE) || defined(LHIP_ABL_NO_FLUSH) ||          \
      defined(LHIP_ABL_SMALL_NOWGSORT) || defined(LHIP_ABL_SMALL_NOMERGE) || defined(LHIP_ABL_SMALL_NOFENCE) || \
-     defined(LHIP_ABL_PR_NOMERGE) || defined(LHIP_ABL_PR_NOLOAD) || defined(LHIP_ABL_PR_F32MATH) ||             \
-     defined(LHIP_PROF))
+     defined(LHIP_ABL_PR_NOMERGE) || defined(LHIP_PROF))
 #error "LHIP_ABL_* / LHIP_PROF are timing ablations that break results: build them through tools/ablate.sh"
 #endif
 #ifndef LHIP_ABL_NO_EPILOGUE
@@ -572,12 +571,7 @@ constexpr int BR = SCAN_BR, BQ = SCAN_BQ;
 #ifndef LHIP_ABL_PR_NOMERGE
 #define LHIP_ABL_PR_NOMERGE 0  // pool_refine: no top-k merge after a round (timing only)
 #endif
-#ifndef LHIP_ABL_PR_NOLOAD
-#define LHIP_ABL_PR_NOLOAD 0  // pool_refine (one-column-step path): rows not loaded (timing only)
-#endif
-#ifndef LHIP_ABL_PR_F32MATH
-#define LHIP_ABL_PR_F32MATH 0  // pool_refine (one-column-step path): f32 partial sums (timing only)
-#endif
+
 #ifndef LHIP_ABL_NO_MFMA
 #define LHIP_ABL_NO_MFMA 0  // fragments read, no MFMA
 #endif
@@ -2376,25 +2370,13 @@ __device__ __forceinline__ void exact_distance_multi(const T *__restrict__ X, in
 			float4 xv[NC];
 #pragma unroll
 			for (int r = 0; r < NC; ++r)
-				xv[r] = (r < nvalid && !LHIP_ABL_PR_NOLOAD) ? xval4(X + (int64_t)slots[r] * ld, 4 * i4)
-				                                          : make_float4(0.f, (float)r, 0.f, (float)i4);
-			if (LHIP_ABL_PR_F32MATH) {
-				float fa[NC];
+				xv[r] = r < nvalid ? xval4(X + (int64_t)slots[r] * ld, 4 * i4) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-				for (int r = 0; r < NC; ++r) {
-					const float dx = xv[r].x - qv.x, dy = xv[r].y - qv.y, dz = xv[r].z - qv.z, dw = xv[r].w - qv.w;
-					fa[r] = fmaf(dx, dx, fmaf(dy, dy, fmaf(dz, dz, dw * dw)));
-				}
-#pragma unroll
-				for (int r = 0; r < NC; ++r) a[r] += (double)fa[r];
-			} else {
-#pragma unroll
-				for (int r = 0; r < NC; ++r) {
-					exact_acc<METRIC>(xv[r].x, qv.x, a[r], b[r], c[r]);
-					exact_acc<METRIC>(xv[r].y, qv.y, a[r], b[r], c[r]);
-					exact_acc<METRIC>(xv[r].z, qv.z, a[r], b[r], c[r]);
-					exact_acc<METRIC>(xv[r].w, qv.w, a[r], b[r], c[r]);
-				}
+			for (int r = 0; r < NC; ++r) {
+				exact_acc<METRIC>(xv[r].x, qv.x, a[r], b[r], c[r]);
+				exact_acc<METRIC>(xv[r].y, qv.y, a[r], b[r], c[r]);
+				exact_acc<METRIC>(xv[r].z, qv.z, a[r], b[r], c[r]);
+				exact_acc<METRIC>(xv[r].w, qv.w, a[r], b[r], c[r]);
 			}
 		}
 	}

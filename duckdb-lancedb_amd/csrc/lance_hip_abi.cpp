@@ -178,8 +178,9 @@ bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *d
 		//    of smallest bound -> top-(k+8) of those by bound -> exact
 		//    distances -> tau[q] = the k-th smallest (an upper bound on the
 		//    k-th nearest distance: k real rows lie within it)
+		const int sdiv = sample_div_eff(n_tiles);
 		const int64_t n_sample = std::min<int64_t>(
-		    n_tiles, std::max<int64_t>({(n_tiles + sample_div - 1) / sample_div, 32, (k + 9) / 2}));
+		    n_tiles, std::max<int64_t>({(n_tiles + sdiv - 1) / sdiv, 32, (k + 9) / 2}));
 		const int64_t stride = std::max<int64_t>(1, n_tiles / n_sample);
 		const int Ms = k + 8;
 		// (int8 copy: scan8_kernel's tilemin mode, one entry per 32-row unit; else
@@ -1299,7 +1300,7 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 		}
 		if (k == "sample_div") {
 			const int d = std::stoi(v);
-			if (d < 1) throw Error("sample_div must be >= 1");
+			if (d < 0) throw Error("sample_div must be >= 1, or 0 (auto)");
 			ix->sample_div = d;
 			return 0;
 		}

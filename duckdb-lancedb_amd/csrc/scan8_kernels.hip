@@ -290,9 +290,6 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 
 #ifdef LHIP_S8_PROF
 		pf_t = __builtin_amdgcn_s_memtime();
-		const uint64_t rt_loop = __builtin_amdgcn_s_memrealtime();
-		if (w == 0 && lane == 0 && TM == 0 && tile0 == 0)
-			printf("S8T wg=%d phase=loop t=%llu tiles=%d\n", b_id, (unsigned long long)rt_loop, my_tiles);
 #endif
 		for (;;) {
 			const int unn_raw = claim();        // the unit after next (read at this block's end)
@@ -488,12 +485,11 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 #ifdef LHIP_S8_PROF
 	uint64_t pf_fl = 0;
 	S8_T(pf_fl);
-	if (lane == 0 && TM == 0 && tile0 == 0)
-		printf("S8T wg=%d w=%d phase=end t=%llu start=%llu\n", b_id, w, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
-		       (unsigned long long)rt_start);
+	const uint64_t rt_end = __builtin_amdgcn_s_memrealtime();
 	if (b_id < 3 && lane == 0)
-		printf("S8 wg=%d w=%d blocks=%d pro=%d k=%d scr=%d app=%d flush=%d list_end=%d hitblocks=%d\n", b_id, w,
-		       my_tiles, (int)pf_pro, (int)pf_k, (int)pf_scr, (int)pf_app, (int)pf_fl, nl_end, pf_hitb);
+		printf("S8 wg=%d w=%d blocks=%d pro=%d k=%d scr=%d app=%d flush=%d list_end=%d hitblocks=%d rt=%d\n", b_id, w,
+		       my_tiles, (int)pf_pro, (int)pf_k, (int)pf_scr, (int)pf_app, (int)pf_fl, nl_end, pf_hitb,
+		       (int)(rt_end - rt_start));
 #endif
 	__syncthreads();  // every wave's counter updates
 	// segment b_id of every query of the tile: this workgroup's counts for its

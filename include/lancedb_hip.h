@@ -194,7 +194,8 @@ int32_t lance_hip_device_count(void);
  *                  on the first search that needs it; refine and get_vector read
  *                  the f32 rows, results are unchanged
  *   "sample_div"   the threshold sample pass covers ~1/sample_div of the row
- *                  tiles (at least 32 tiles); default "32"
+ *                  tiles (at least 32 tiles); default "0" = auto (16 up to 8192
+ *                  tiles of 256 rows, 32 past that)
  *   "split_div"    int8 append pass over >= 128 * split_div tiles: the first
  *                  1/split_div of the tiles with the sample's threshold, the rest
  *                  with the tighter one their candidates give (e.g. "8"); "0"

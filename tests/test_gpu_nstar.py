@@ -1,0 +1,52 @@
+"""The north_star size on the GPU: flat squared L2 over 10M x 768 f32 rows,
+256 queries, k = 10 (BASELINE.json north_star; bench.py --config nstar).
+Every query's search runs the default large-store path (sample pass, int8
+scan8 append pass, pool_refine) and must come out certified (no rerun, no
+exact fallback); the ids of a 64-query subset are checked against the f64 C
+oracle (labels bit-exact, distances within 1e-4 relative), and recall@10 is
+1.0 on them.  Reference semantics: rust_lib/src/lance_manager.rs:393-451."""
+import numpy as np
+import pytest
+
+from oracle import c_oracle, flat_knn
+from tests.test_gpu_parity import assert_same
+
+pytestmark = pytest.mark.gpu
+
+N, D, K, B, NCHECK = 10_000_000, 768, 10, 256, 64
+
+
+def test_north_star_10m_exact(hip):
+    import torch
+
+    L = hip.lib()
+    h = hip.LanceCreateDetached("", D, "l2", "nstar")
+    Xh = np.empty((N, D), np.float32)
+    try:
+        hip.LanceHipSetOption(h, "reserve_rows", str(N))
+        g = torch.Generator(device="cuda")
+        g.manual_seed(10_000_019)
+        e = hip._err()
+        for lo in range(0, N, 1 << 20):
+            hi = min(N, lo + (1 << 20))
+            X = torch.randn((hi - lo, D), generator=g, device="cuda", dtype=torch.float32)
+            torch.cuda.synchronize()
+            assert L.lance_hip_add_batch_device(h, X.data_ptr(), hi - lo, D, e, len(e)) >= 0, e.value
+            Xh[lo:hi] = X.cpu().numpy()
+            del X
+        Q = torch.randn((B, D), generator=g, device="cuda", dtype=torch.float32)
+        hip.LanceHipSetOption(h, "time_kernels", "1")
+        gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q.cpu().numpy(), K)
+        st = hip.LanceHipLastSearchStats(h)
+        kt = hip.LanceHipKernelTimes(h)
+        assert kt["scan_kernel"] == "scan8_kernel" and kt["scan_elem_bytes"] == 1, kt
+        assert not st["dense_path"] and st["fallback_queries"] == 0 and st["retried_queries"] == 0, st
+        assert (gc == K).all()
+        el, ed, ec = c_oracle.flat_search_batch(Xh, Q[:NCHECK].cpu().numpy(), K, "l2", acc64=True, nthreads=16)
+        assert_same(gl[:NCHECK], gd[:NCHECK], gc[:NCHECK], el, ed, ec)
+        assert flat_knn.recall_at_k(gl[:NCHECK], el, K) == 1.0
+        # every distance row ascending, every label in range
+        assert (np.diff(gd, axis=1) >= 0).all() and gl.min() >= 0 and gl.max() < N
+    finally:
+        hip.LanceFreeDetached(h)
+        del Xh

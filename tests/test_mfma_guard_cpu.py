@@ -43,3 +43,44 @@ def test_no_valu_write_into_a_live_mfma_operand():
     assert s8, r.stdout[-2000:]
     assert all(abl == "0" for (_, _, _, abl) in s8), sorted(s8)
     assert {(d, rb) for (ks, d, rb, _) in s8 if ks == "12"} == {("4", "2")}, sorted(s8)
+
+
+def _kernel_metadata(obj):
+    """{kernel symbol: (private_segment_fixed_size, vgpr_count)} of an object's gfx950 code object."""
+    import tempfile
+
+    out = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        fb, co = os.path.join(tmp, "fb.bin"), os.path.join(tmp, "co.elf")
+        subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fb}", obj], check=True, capture_output=True)
+        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fb}", f"--output={co}"],
+                       check=True, capture_output=True)
+        notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True, capture_output=True,
+                               text=True).stdout
+    name = None
+    for ln in notes.splitlines():
+        ln = ln.strip()
+        if ln.startswith(".name:"):
+            name = ln.split(":", 1)[1].strip()
+        elif ln.startswith(".private_segment_fixed_size:") and name:
+            out.setdefault(name, [0, 0])[0] = int(ln.split(":", 1)[1])
+        elif ln.startswith(".vgpr_count:") and name:
+            out.setdefault(name, [0, 0])[1] = int(ln.split(":", 1)[1])
+    return out
+
+
+@pytest.mark.skipif(not OBJS or not os.path.exists(os.path.join(LLVM, "llvm-readelf")),
+                    reason="needs the built objects (make) and the ROCm LLVM tools")
+def test_hot_kernels_do_not_spill():
+    """The C2 / north_star hot kernels keep every value in registers: a scratch
+    spill in pool_refine's final mode cost 69 -> 104 us per C2 batch (round 4),
+    so a register-allocation change that spills fails here, before the GPU."""
+    meta = {}
+    for obj in OBJS:
+        if os.path.basename(obj) in ("knn_kernels.o", "scan8_kernels.o"):
+            meta.update(_kernel_metadata(obj))
+    hot = [k for k in meta if ("pool_refine_kernel" in k and "Ef" in k) or "scan8_kernel" in k]
+    assert len(hot) >= 10, sorted(meta)[:20]
+    spills = {k: v for k, v in meta.items() if k in hot and v[0] != 0}
+    assert not spills, spills

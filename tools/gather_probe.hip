@@ -68,6 +68,10 @@ __global__ __launch_bounds__(NT) void gather(const float *__restrict__ X, const 
 	if (lane == 0) out[blockIdx.x * NW + w] = (float)acc + facc;
 }
 
+constexpr int NSETS = 20;
+static void *g_flush = nullptr;
+static size_t g_flush_bytes = 0;
+
 template <int NT, int R, int F64>
 static void run(const float *X, const uint32_t *idx, const float *q, float *out, int wgs, int rows_per_wg,
                 const char *tag) {
@@ -79,8 +83,12 @@ static void run(const float *X, const uint32_t *idx, const float *q, float *out,
 	const int iters = 20;
 	float best = 1e30f, tot = 0.f;
 	for (int i = 0; i < iters; ++i) {
+		// cold rows: a fresh index set each launch (sets are disjoint slices of a
+		// larger random table, and a 1 GB flush write runs in between)
+		const uint32_t *ix = idx + (size_t)(i % NSETS) * wgs * rows_per_wg * (rows_per_wg <= 128 ? 1 : 0);
+		if (g_flush) CHK(hipMemsetAsync(g_flush, i, g_flush_bytes));
 		CHK(hipEventRecord(a));
-		gather<NT, R, F64><<<wgs, NT>>>(X, idx, q, rows_per_wg, out);
+		gather<NT, R, F64><<<wgs, NT>>>(X, ix, q, rows_per_wg, out);
 		CHK(hipEventRecord(b));
 		CHK(hipEventSynchronize(b));
 		float ms;
@@ -115,14 +123,19 @@ int main(int argc, char **argv) {
 	CHK(hipMemset(q, 0, LD * sizeof(float)));
 	CHK(hipMalloc(&out, 65536 * sizeof(float)));
 	const int maxr = 2048;
-	std::vector<uint32_t> h((size_t)wgs * maxr);
+	std::vector<uint32_t> h((size_t)wgs * std::max(maxr, 128 * NSETS));
 	std::mt19937 rng(7);
 	for (auto &v : h) v = (uint32_t)(rng() % N);
 	CHK(hipMalloc(&idx, h.size() * sizeof(uint32_t)));
 	CHK(hipMemcpy(idx, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-	printf("table %zu rows x %d f32 (%.2f GB, %s), %d workgroups\n", N, LD, N * LD * 4 / 1e9,
+	if (argc > 3 && atoi(argv[3]) == 1) {  // evict caches between launches
+		g_flush_bytes = (size_t)1 << 30;
+		CHK(hipMalloc(&g_flush, g_flush_bytes));
+	}
+	printf("table %zu rows x %d f32 (%.2f GB, %s%s), %d workgroups\n", N, LD, N * LD * 4 / 1e9,
+	       g_flush ? "cold: 1 GB flush between launches, " : "",
 	       argc > 2 && atoi(argv[2]) == 1 ? "random" : "zeros", wgs);
-	for (int rpw : {128, 2048}) {
+	for (int rpw : {128}) {
 		run<512, 4, 1>(X, idx, q, out, wgs, rpw, "gather");
 		run<512, 8, 1>(X, idx, q, out, wgs, rpw, "gather");
 		run<512, 16, 1>(X, idx, q, out, wgs, rpw, "gather");
@@ -133,6 +146,8 @@ int main(int argc, char **argv) {
 		run<1024, 8, 0>(X, idx, q, out, wgs, rpw, "gather");
 		run<256, 8, 1>(X, idx, q, out, wgs * 4, rpw / 4, "gather4x");
 		run<256, 4, 1>(X, idx, q, out, wgs * 4, rpw / 4, "gather4x");
+		run<1024, 2, 1>(X, idx, q, out, wgs, rpw, "gather");
+		run<512, 2, 1>(X, idx, q, out, wgs, rpw, "gather");
 	}
 	return 0;
 }
