@@ -696,7 +696,7 @@ def main():
     Q = torch.randn((BG, D), generator=g, device=dev, dtype=torch.float32)
     if a.normalize:
         Q /= torch.linalg.vector_norm(Q, dim=1, keepdim=True)
-    from lance_hip.sharded import AsyncPipeline, ShardedSearch, hip_device_merge, hip_device_search
+    from lance_hip.sharded import AsyncPipeline, ShardedPipeline, ShardedSearch, hip_device_merge, hip_device_search
 
     searcher = ShardedSearch(hip_device_search(L, h, D), hip_device_merge(L), label_offset=s0, dist=dist,
                              world=world)
@@ -707,11 +707,16 @@ def main():
     Qh_api = Q.cpu().numpy() if (a.api != "device" or (world == 1 and not a.no_host_batch)) else None
     call_i = [0]
 
-    # one GPU, device API: two batches in flight (lance_hip_search_batch_device_async;
+    # device API: two batches in flight per rank (lance_hip_search_batch_device_async;
     # every batch completes — certified, reruns / fallbacks done — at its wait
-    # inside the timed region); --sync: one synchronous call per batch
-    pipelined = world == 1 and a.api == "device" and not a.sync
-    pipe = AsyncPipeline(L, h, D) if pipelined else None
+    # inside the timed region; N > 1: batch i-1's all-gather + merge run while
+    # batch i scans); --sync: one synchronous call (+ exchange) per batch
+    pipelined = a.api == "device" and not a.sync
+    pipe = None
+    if pipelined:
+        pipe = AsyncPipeline(L, h, D)
+        if world > 1:
+            pipe = ShardedPipeline(pipe, searcher)
     last_out = [None]
 
     def step():
@@ -770,7 +775,7 @@ def main():
         del Qo
     syncleg = None
     if pipelined:
-        ts, rs, _ = timed_steps(lambda: searcher.search(Q, K, reuse_outputs=True), a.steps, a.warmup, None, dev,
+        ts, rs, _ = timed_steps(lambda: searcher.search(Q, K, reuse_outputs=True), a.steps, a.warmup, dist, dev,
                                 torch.cuda.synchronize)
         syncleg = {"value": round(BG * a.steps / ts, 1), "unit": "queries/s", "ms_per_step": round(1000.0 * ts / a.steps, 4),
                    "api": "lance_hip_search_batch_device, one synchronous call per batch",
@@ -931,7 +936,8 @@ def main():
             line[f"{other['scaling']}_scaling"] = other
         if pipelined:
             line["config"]["pipeline"] = ("async: 2 batches in flight on the handle's stream "
-                                          "(lance_hip_search_batch_device_async / lance_hip_search_wait)")
+                                          "(lance_hip_search_batch_device_async / lance_hip_search_wait)"
+                                          + ("; batch i-1's all-gather + merge overlap batch i's scan" if world > 1 else ""))
             line["sync"] = syncleg
         if hostb:
             line["host_batch"] = hostb

@@ -2973,10 +2973,13 @@ static void pool_refine_dispatch(const StoreView &s, const QueryView &q, const u
 	// mode's rounds are larger and keep 16 rows per wave one column step at a time
 	// (66 vs 75 us at C2: twice the rows per round, half the rounds and merges;
 	// r04d kernel traces)
+#ifndef LHIP_PR_FINAL_NI  // (development builds: 1 = the final mode on the all-in-flight path too)
+#define LHIP_PR_FINAL_NI 0
+#endif
 #ifdef LHIP_PR_FORCE_NI0  // (development builds: the one-column-step path everywhere)
 	const int ni = 0;
 #else
-	const int ni = mode == 1 ? 0 : s.dim <= 256 ? 1 : s.dim <= 512 ? 2 : s.dim <= 768 ? 3 : s.dim <= 1024 ? 4 : 0;
+	const int ni = (mode == 1 && !LHIP_PR_FINAL_NI) ? 0 : s.dim <= 256 ? 1 : s.dim <= 512 ? 2 : s.dim <= 768 ? 3 : s.dim <= 1024 ? 4 : 0;
 #endif
 	switch (s.metric) {
 	case METRIC_L2: LHIP_PR_NI(METRIC_L2); break;

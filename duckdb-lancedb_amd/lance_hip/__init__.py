@@ -101,6 +101,16 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} not built; run `make -C duckdb-lancedb_amd` (or __graft_entry__.build())")
+        # ONE HIP runtime per process: torch's wheel bundles its own libamdhip64 /
+        # libhsa-runtime64 (soname libamdhip64.so.7, but torch NEEDs it as
+        # "libamdhip64.so"), so loading this library first maps /opt/rocm's copy
+        # and a later `import torch` maps a second one; two HSA runtimes in one
+        # process leave the second to initialise without a device.  With torch
+        # loaded first, this library's libamdhip64.so.7 resolves to torch's copy.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, res, args in _SIGNATURES:
             fn = getattr(L, name)

@@ -39,7 +39,10 @@ class ShardedSearch:
         self._bufs = None
 
     def search(self, Q, k: int, **kw):
-        lab, dis, cnt = self.local_search(Q, k, **kw)
+        return self.exchange(*self.local_search(Q, k, **kw))
+
+    def exchange(self, lab, dis, cnt):
+        """This shard's top-k lists (local labels) -> the merged global lists."""
         if self.world == 1:
             return lab, dis, cnt
         # local -> global labels (unused slots stay -1)
@@ -182,3 +185,37 @@ class AsyncPipeline:
 
     def drain(self):
         return self.wait(0)
+
+
+class ShardedPipeline:
+    """Row-sharded search with two batches in flight per rank: ``step(Q, k)``
+    enqueues batch i on this rank's shard (``pipe.submit``, the handle's
+    stream), then completes batch i-1 (``pipe.wait``) and runs its exchange —
+    the one all-gather and the device merge — while batch i's scan is still on
+    the device.  Every rank calls ``step`` in the same order, so the collectives
+    of all ranks pair up batch for batch.  Returns the merged lists of the batch
+    completed by the call (None on the first); ``drain()`` completes the last.
+
+    ``pipe`` has ``submit(Q, k) -> ticket`` and ``wait(ticket) -> (labels,
+    dists, counts)`` (``AsyncPipeline`` on the GPU; a CPU stand-in in tests);
+    ``sharded`` is this rank's ``ShardedSearch`` (its exchange is used)."""
+
+    def __init__(self, pipe, sharded: ShardedSearch):
+        self.pipe = pipe
+        self.sharded = sharded
+        self.prev = None
+
+    def step(self, Q, k: int):
+        t = self.pipe.submit(Q, k)
+        out = None
+        if self.prev is not None:
+            out = self.sharded.exchange(*self.pipe.wait(self.prev))
+        self.prev = t
+        return out
+
+    def drain(self):
+        if self.prev is None:
+            return None
+        out = self.sharded.exchange(*self.pipe.wait(self.prev))
+        self.prev = None
+        return out

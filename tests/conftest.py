@@ -20,8 +20,8 @@ def hip():
     """The product library; GPU tests fail loudly (no fallback) if it is missing."""
     import lance_hip
 
-    # torch's bundled HIP runtime first (tests move queries and outputs through
-    # torch tensors): initialised after the library's runtime it finds no device
+    # one HIP runtime in the process: lance_hip.lib() imports torch before it
+    # maps the library (see there); torch's CUDA state is initialised here once
     try:
         import torch
 

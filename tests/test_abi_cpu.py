@@ -120,3 +120,20 @@ def test_cpp_caller_links_against_library(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip().endswith("OK")
+
+
+def test_one_hip_runtime_per_process():
+    """lance_hip.lib() maps torch's bundled HIP runtime, never a second copy:
+    two libamdhip64 / libhsa-runtime64 in one process leave the one initialised
+    second without a device (GPU suite: 'No HIP GPUs are available')."""
+    import subprocess
+    import sys
+
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import lance_hip; lance_hip.lib()\n"
+            "import torch\n"
+            "m = open('/proc/self/maps').read().splitlines()\n"
+            "print(len({l.split()[-1] for l in m if 'libamdhip64' in l}))\n") % (os.path.join(ROOT, "duckdb-lancedb_amd"),)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == "1", out.stdout

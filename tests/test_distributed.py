@@ -87,6 +87,75 @@ def test_sharded_merge_equals_unsharded_cpu(world, n):
         np.testing.assert_allclose(dd, ed, rtol=1e-6)
 
 
+class _CpuPipe:
+    """CPU stand-in for AsyncPipeline: submit computes, wait returns by ticket."""
+
+    def __init__(self, search):
+        self.search, self.done, self.t = search, {}, 0
+
+    def submit(self, Q, k):
+        self.t += 1
+        self.done[self.t] = self.search(Q, k)
+        return self.t
+
+    def wait(self, t):
+        return self.done.pop(t)
+
+
+def _cpu_pipeline_worker(rank, world, port, n, d, k, q, nb, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from lance_hip.sharded import ShardedPipeline
+    from oracle import flat_knn
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(9)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Qs = [rng.standard_normal((q, d)).astype(np.float32) for _ in range(nb)]
+    s0, s1 = shard_range(n, world, rank)
+    Xs = X[s0:s1]
+
+    def local_search(Qt, kk):
+        l, dd, c = flat_knn.flat_search_batch(Xs, np.arange(s1 - s0), np.ones(s1 - s0, bool), Qt.numpy(), kk)
+        return torch.from_numpy(l), torch.from_numpy(dd), torch.from_numpy(c)
+
+    sh = ShardedSearch(local_search, ref_merge, label_offset=s0, dist=dist, world=world)
+    pipe = ShardedPipeline(_CpuPipe(local_search), sh)
+    res = []
+    for Q in Qs:  # batch i's result arrives one step later
+        r = pipe.step(torch.from_numpy(Q), k)
+        if r is not None:
+            res.append(tuple(x.numpy() for x in r))
+    res.append(tuple(x.numpy() for x in pipe.drain()))
+    assert pipe.drain() is None
+    out[rank] = res
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_pipeline_two_batches_in_flight_cpu(world):
+    """bench.py's N > 1 loop: batch i-1's exchange runs after batch i is
+    submitted; every batch's merged lists equal the unsharded search, in order."""
+    from oracle import flat_knn
+
+    n, d, k, q, nb = 997, 8, 5, 4, 4
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_cpu_pipeline_worker, args=(world, _free_port(), n, d, k, q, nb, out), nprocs=world, join=True)
+    rng = np.random.default_rng(9)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Qs = [rng.standard_normal((q, d)).astype(np.float32) for _ in range(nb)]
+    for r in range(world):
+        assert len(out[r]) == nb
+        for Q, (l, dd, c) in zip(Qs, out[r]):
+            el, ed, ec = flat_knn.flat_search_batch(X, np.arange(n), np.ones(n, bool), Q, k)
+            np.testing.assert_array_equal(l, el)
+            np.testing.assert_array_equal(c, ec)
+            np.testing.assert_allclose(dd, ed, rtol=1e-6)
+
+
 def test_shard_range_partitions_exactly():
     for n in (0, 1, 7, 1000, 1_000_000):
         for world in (1, 2, 3, 8):
@@ -151,7 +220,7 @@ def test_sharded_hip_search_two_ranks_one_gpu():
         np.testing.assert_allclose(dd, ed, rtol=1e-4, atol=1e-5)
 
 
-def _gpu_scan8_worker(rank, world, port, n, d, k, q, out):
+def _gpu_scan8_worker(rank, world, port, n, d, k, q, out, pipelined=False):
     # the bench's flat multi-GPU flow on the DEFAULT large-store path: each shard
     # > 65536 rows at d = 768 takes the threshold pipeline (sample pass, int8
     # scan8_kernel append pass, pool_refine), per-shard lists gathered and merged
@@ -186,10 +255,32 @@ def _gpu_scan8_worker(rank, world, port, n, d, k, q, out):
         return l.cpu(), dd.cpu(), c.cpu()
 
     s = ShardedSearch(local_search, merge, label_offset=s0, dist=dist, world=world)
-    l, dd, c = s.search(torch.from_numpy(Q), k)
-    st = lance_hip.LanceHipLastSearchStats(h)
-    kt = lance_hip.LanceHipKernelTimes(h)
-    out[rank] = (l.numpy(), dd.numpy(), c.numpy(), st, kt["scan_kernel"], kt["scan_launches"])
+    if pipelined:
+        # bench.py's N > 1 loop: two batches in flight on the handle (the async
+        # C-ABI), batch i-1 exchanged while batch i is on the device
+        from lance_hip.sharded import AsyncPipeline, ShardedPipeline
+
+        lance_hip.LanceHipSetOption(h, "time_kernels", "0")  # (timing forces the synchronous path)
+        ap = AsyncPipeline(L, h, d)
+
+        class _Pipe:
+            def submit(self, Qt, kk):
+                return ap.submit(Qt.cuda(), kk)
+
+            def wait(self, t):
+                return tuple(x.cpu() for x in ap.wait(t))
+
+        pipe = ShardedPipeline(_Pipe(), s)
+        Qs = [torch.from_numpy(Q), torch.from_numpy(Q[::-1].copy()), torch.from_numpy(Q)]
+        res = [pipe.step(Qt, k) for Qt in Qs] + [pipe.drain()]
+        assert res[0] is None
+        st = lance_hip.LanceHipLastSearchStats(h)
+        out[rank] = [tuple(x.numpy() for x in r) for r in res[1:]] + [st]
+    else:
+        l, dd, c = s.search(torch.from_numpy(Q), k)
+        st = lance_hip.LanceHipLastSearchStats(h)
+        kt = lance_hip.LanceHipKernelTimes(h)
+        out[rank] = (l.numpy(), dd.numpy(), c.numpy(), st, kt["scan_kernel"], kt["scan_launches"])
     lance_hip.LanceFreeDetached(h)
     dist.barrier()
     dist.destroy_process_group()
@@ -217,6 +308,31 @@ def test_sharded_scan8_two_ranks_one_gpu():
         assert (c == k).all()
         np.testing.assert_array_equal(l, el)
         np.testing.assert_allclose(dd, ed, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_sharded_scan8_pipelined_two_ranks_one_gpu():
+    """The same shards through bench.py's pipelined N > 1 loop (async C-ABI,
+    two batches in flight, exchange one batch behind): three batches, each
+    merged result equal to the unsharded exact search, in submission order."""
+    from oracle import c_oracle
+
+    world, n, d, k, q = 2, 160_000, 768, 10, 256
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_gpu_scan8_worker, args=(world, _free_port(), n, d, k, q, out, True), nprocs=world, join=True)
+    rng = np.random.default_rng(21)
+    X = rng.standard_normal((n, d), dtype=np.float32)
+    Q = rng.standard_normal((q, d), dtype=np.float32)
+    el, ed, _ = c_oracle.flat_search_batch(X, Q, k, "l2", acc64=True, nthreads=16)
+    for r in range(world):
+        *res, st = out[r]
+        assert len(res) == 3 and st["fallback_queries"] == 0, st
+        for i, (l, dd, c) in enumerate(res):
+            el_i, ed_i = (el[::-1], ed[::-1]) if i == 1 else (el, ed)
+            assert (c == k).all()
+            np.testing.assert_array_equal(l, el_i)
+            np.testing.assert_allclose(dd, ed_i, rtol=1e-4, atol=1e-5)
 
 
 def _gpu_ivf_worker(rank, world, port, n, d, k, q, nlist, nprobe, out):
