@@ -260,6 +260,7 @@ struct Index {
 	int kmeans_iters = 50;  // lance k-means max_iters default
 	uint64_t ivf_seed = 0x5eedULL;
 	bool pq_fast = true;    // IVF_PQ list-major 8-bit-LUT scan (option "pq_scan" = "fast"; "exact_lut": f32 LUT, query-major)
+	bool pq_seed = true;    // fast scan: per-query bound seeded from the nearest probed list (option "pq_seed")
 	bool pq_fp8 = false;
 	bool ivf_flat_bound = true;  // IVF_FLAT list scan by MFMA bf16 lower bounds + certified exact re-rank (option "ivf_flat_scan" = "bound" | "exact")
 	int64_t ivf_flat_fallbacks = 0;  // batches the bound scan could not certify (rerun exactly)    // IVF_PQ ADC tables from e4m3 (fp8) queries (option "pq_query" = "fp8" | "f32")

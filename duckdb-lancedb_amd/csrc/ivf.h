@@ -188,6 +188,10 @@ void launch_pq_query_fp8(const float *Q, int qld, int nq, int dim, float *Qo, hi
 void launch_pq_lut_u8(const float *P, int nq, int m, float sP, uint8_t *lut8, float2 *qpar, hipStream_t st);
 // item_off [nlist+1]: work items of the fast scan per list (query groups x row chunks)
 void launch_pq_fast_items(const int *pstart, const int64_t *loff, int nlist, int *item_off, hipStream_t st);
+// per query: the kk-th smallest fast-scan key of its nearest probed list -> thrq (atomicMin)
+void launch_pq_seed(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
+                    const float *rowaux_f, int nq, int nprobe, const int64_t *probe_l, const float *probe_d,
+                    const float *ltau, const uint8_t *lut8, const float2 *qpar, int kk, uint64_t *thrq, hipStream_t st);
 int pq_fast_lds_bytes(int m);
 // list-major 8-bit-LUT scan: per query its candidate run out [nq][ocap] (count ocnt[q]);
 // work (1 int), thrq [nq] (~0) and ocnt [nq] (0) must be initialised

@@ -595,6 +595,10 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			HIPCHK(hipMemsetAsync(s->ocnt.p, 0, (size_t)n * sizeof(int), st));
 			HIPCHK(hipMemsetAsync(s->thrq.p, 0xFF, (size_t)n * sizeof(uint64_t), st));
 			HIPCHK(hipMemsetAsync(s->work.p, 0, sizeof(int), st));
+			if (ix->pq_seed)
+				launch_pq_seed(s->lcodes.p, s->m, s->mp, s->loff.p, s->lslot.p, reinterpret_cast<const float *>(sv.rowaux),
+				               n, nprobe, s->probe_l.p, s->probe_d.p, s->metric == METRIC_DOT ? nullptr : s->ltau.p,
+				               s->lut8.p, reinterpret_cast<const float2 *>(s->qpar.p), kp, s->thrq.p, st);
 			ix->tic(0);
 			launch_pq_fast_scan(s->lcodes.p, s->m, s->mp, s->loff.p, s->lslot.p,
 			                    reinterpret_cast<const float *>(sv.rowaux), s->nlist, nprobe, s->pstart.p, s->pairs.p,

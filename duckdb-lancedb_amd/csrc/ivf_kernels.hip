@@ -32,6 +32,22 @@ namespace lhip {
 
 static constexpr uint64_t KEY64_NONE = ~0ull;
 
+#ifdef LHIP_PQ_PROF
+// diagnostic build: per workgroup of pq_fast_scan_kernel, cycles in each phase
+// (LUT build, row rounds, candidate sorts, flush), items and sorted items;
+// thread 0 accumulates, the host prints after the launch (launch_pq_fast_scan)
+constexpr int PQ_PROF_WG = 4096, PQ_PROF_N = 8;
+__device__ uint64_t g_pq_prof[PQ_PROF_WG * PQ_PROF_N];
+#define PQ_T(i)                                                   \
+	{                                                             \
+		const uint64_t now_ = __builtin_amdgcn_s_memtime();        \
+		pq_acc[i] += now_ - pq_t;                                 \
+		pq_t = now_;                                              \
+	}
+#else
+#define PQ_T(i)
+#endif
+
 __device__ __forceinline__ uint64_t key64(float d, uint32_t slot) { return ((uint64_t)fkey(d) << 32) | slot; }
 __device__ __forceinline__ float key64_dist(uint64_t k) { return fkey_inv((uint32_t)(k >> 32)); }
 // tombstones and padding rows carry alpha = +inf in the row aux
@@ -1742,11 +1758,19 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 	const int t = threadIdx.x;
 	const int nch = mp >> 4;
 	const int total = item_off[nlist];
+#ifdef LHIP_PQ_PROF
+	uint64_t pq_acc[PQ_PROF_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+	uint64_t pq_t = __builtin_amdgcn_s_memtime();
+#endif
 	for (;;) {
+		PQ_T(0);  // (item claim + loop overhead)
 		if (t == 0) item = atomicAdd(work, 1);
 		__syncthreads();
 		const int it = item;
 		if (it >= total) break;
+#ifdef LHIP_PQ_PROF
+		pq_acc[5] += 1;
+#endif
 		// list of the item: last l with item_off[l] <= it (binary search)
 		int lo = 0, hi = nlist - 1;
 		while (lo < hi) {
@@ -1834,6 +1858,7 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 		}
 #endif
 		__syncthreads();
+		PQ_T(1);  // item setup + LUT build
 		const int64_t c0 = (int64_t)ch * FQ_CHUNK, c1 = len < c0 + FQ_CHUNK ? len : c0 + FQ_CHUNK;
 		// codes of the next round are loaded while the current round is summed
 		constexpr int NCH = FQ_MAX_M / 16;
@@ -1940,8 +1965,12 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 			cslot = nslot;
 			ctau = ntau;
 			__syncthreads();
+			PQ_T(2);  // row round
 			for (int i = 0; i < FQ_G; ++i) {
 				if (cnt[i] > FQ_CAP - FQ_THREADS) {  // the next round could overflow: sort, keep kk
+#ifdef LHIP_PQ_PROF
+					pq_acc[6] += 1;
+#endif
 					uint64_t *b = buf + i * FQ_CAP;
 					const int c = cnt[i];
 					const int n2 = pow2_ceil(c);
@@ -1957,9 +1986,13 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 			}
 			if (t < FQ_G && gthr < thr[t]) thr[t] = gthr;
 			__syncthreads();
+			PQ_T(3);  // candidate sorts
 		}
 		// flush: the item's keys within its final bound (entries appended before
 		// the bound tightened may lie above it)
+#ifdef LHIP_PQ_PROF
+		for (int i = 0; i < FQ_G; ++i) pq_acc[7] += qid[i] >= 0 ? (uint64_t)cnt[i] : 0;
+#endif
 		for (int i = 0; i < FQ_G; ++i) {
 			const int q = qid[i];
 			if (q < 0) continue;
@@ -1974,7 +2007,91 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 			}
 		}
 		__syncthreads();
+		PQ_T(4);  // flush
 	}
+#ifdef LHIP_PQ_PROF
+	if (t == 0 && blockIdx.x < PQ_PROF_WG)
+		for (int i = 0; i < PQ_PROF_N; ++i) g_pq_prof[blockIdx.x * PQ_PROF_N + i] = pq_acc[i];
+#endif
+}
+
+// Seed of the fast scan's per-query bound (thrq): one workgroup per query
+// scores the first PQ_SEED_ROWS positions of its NEAREST probed list with its
+// own 8-bit LUT, exactly as pq_fast_scan_kernel keys them (same ADC terms,
+// same rounding, live rows only), and stores the kk-th smallest key: kk real
+// keys of a probed list lie at or below it, so no key above it can be among
+// the query's kk smallest (the bound is inclusive, as the scan's).  Without
+// it every query's first items pass every row until a buffer sort sets one.
+constexpr int PQ_SEED_ROWS = 4096;
+template <int MT>
+__global__ __launch_bounds__(256) void pq_seed_kernel(const uint8_t *__restrict__ lcodes, int m, int mp,
+                                                      const int64_t *__restrict__ loff,
+                                                      const uint32_t *__restrict__ lslot,
+                                                      const float *__restrict__ rowaux_f, int nprobe,
+                                                      const int64_t *__restrict__ probe_l,
+                                                      const float *__restrict__ probe_d,
+                                                      const float *__restrict__ ltau, const uint8_t *__restrict__ lut8,
+                                                      const float2 *__restrict__ qpar, int kk,
+                                                      unsigned long long *__restrict__ thrq) {
+	__shared__ __attribute__((aligned(16))) uint8_t L[FQ_MAX_M * PQ_K];
+	__shared__ uint64_t keys[PQ_SEED_ROWS];
+	const int q = blockIdx.x, t = threadIdx.x;
+	const int mm = MT > 0 ? MT : m;
+	const int64_t l = probe_l[(int64_t)q * nprobe];
+	const float d0 = probe_d[(int64_t)q * nprobe];
+	const float2 qp = qpar[q];
+	const uint8_t *lq = lut8 + (int64_t)q * mm * PQ_K;
+	for (int i = t; i < mm * PQ_K / 16; i += 256) reinterpret_cast<uint4 *>(L)[i] = reinterpret_cast<const uint4 *>(lq)[i];
+	const int64_t p0 = loff[l], len = loff[l + 1] - p0;
+	const int n = (int)(len < PQ_SEED_ROWS ? len : PQ_SEED_ROWS);
+	int P = 64;
+	while (P < n) P <<= 1;
+	const int nch = mp >> 4;
+	__syncthreads();
+	for (int r = t; r < P; r += 256) {
+		uint64_t key = KEY64_NONE;
+		if (r < n) {
+			const int64_t ps = p0 + r;
+			const uint32_t slot = lslot[ps];
+			if (slot != SLOT_NONE && slot_alive(rowaux_f, slot)) {
+				const uint8_t *cp = lcodes + ((ps >> 6) * nch * 64 + (ps & 63)) * 16;
+				uint32_t S = 0;
+				for (int c = 0; c < nch; ++c) {
+					const uint4 w = *reinterpret_cast<const uint4 *>(cp + (int64_t)c * 64 * 16);
+					const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+					for (int u = 0; u < 16; ++u) {
+						const int j = c * 16 + u;
+						if (j < mm) S += L[j * PQ_K + ((wd[u >> 2] >> (8 * (u & 3))) & 255u)];
+					}
+				}
+				// the scan's key: ((d0 + tau) + L0) + D * S, each step rounded
+				float a = ltau ? __fadd_rn(d0, ltau[ps]) : d0;
+				a = __fadd_rn(a, qp.y);
+				a = __fadd_rn(a, __fmul_rn(qp.x, (float)S));
+				key = key64(a, slot);
+			}
+		}
+		keys[r] = key;
+	}
+	wg_bitonic_sort(keys, P);
+	if (t == 0 && kk <= n) {
+		const uint64_t b = keys[kk - 1];
+		if (b != KEY64_NONE) atomicMin(thrq + q, (unsigned long long)b);
+	}
+}
+
+void launch_pq_seed(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
+                    const float *rowaux_f, int nq, int nprobe, const int64_t *probe_l, const float *probe_d,
+                    const float *ltau, const uint8_t *lut8, const float2 *qpar, int kk, uint64_t *thrq, hipStream_t st) {
+	if (nq <= 0 || kk > PQ_SEED_ROWS || m > FQ_MAX_M) return;
+	auto thr = reinterpret_cast<unsigned long long *>(thrq);
+	if (m == 96)
+		pq_seed_kernel<96><<<dim3((unsigned)nq), 256, 0, st>>>(lcodes, m, mp, loff, lslot, rowaux_f, nprobe, probe_l,
+		                                                        probe_d, ltau, lut8, qpar, kk, thr);
+	else
+		pq_seed_kernel<0><<<dim3((unsigned)nq), 256, 0, st>>>(lcodes, m, mp, loff, lslot, rowaux_f, nprobe, probe_l,
+		                                                       probe_d, ltau, lut8, qpar, kk, thr);
 }
 
 int pq_fast_lds_bytes(int m) { return m * PQ_K * 4 + FQ_G * FQ_CAP * 8; }
@@ -1996,6 +2113,35 @@ void launch_pq_fast_scan(const uint8_t *lcodes, int m, int mp, const int64_t *lo
 		    lcodes, m, mp, loff, lslot, rowaux_f, nlist, nprobe, pstart, pairs, item_off, probe_d, ltau, lut8, qpar,
 		    kk, work, reinterpret_cast<unsigned long long *>(thrq), ocnt, out, ocap);
 	};
+#ifdef LHIP_PQ_PROF
+	{
+		std::vector<uint64_t> z((size_t)PQ_PROF_WG * PQ_PROF_N, 0);
+		HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_pq_prof), z.data(), z.size() * 8, 0, hipMemcpyHostToDevice, st));
+		HIPCHK(hipStreamSynchronize(st));
+	}
+	struct Dump {
+		hipStream_t st;
+		int grid;
+		~Dump() {
+			static int calls = 0;
+			if (++calls != 3 || hipStreamSynchronize(st) != hipSuccess) return;  // (the 3rd launch of the process)
+			std::vector<uint64_t> h((size_t)PQ_PROF_WG * PQ_PROF_N);
+			if (hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_pq_prof), h.size() * 8) != hipSuccess) return;
+			double sum[PQ_PROF_N] = {0};
+			uint64_t mx = 0;
+			const int g = std::min(grid, PQ_PROF_WG);
+			for (int b = 0; b < g; ++b) {
+				uint64_t tot = 0;
+				for (int i = 0; i < PQ_PROF_N; ++i) sum[i] += (double)h[(size_t)b * PQ_PROF_N + i];
+				for (int i = 0; i < 5; ++i) tot += h[(size_t)b * PQ_PROF_N + i];
+				mx = std::max(mx, tot);
+			}
+			fprintf(stderr, "PQPROF wgs=%d avg cycles: claim %.0f lut %.0f rows %.0f sort %.0f flush %.0f | items %.1f sorts %.1f cand %.0f | max wg total %llu\n",
+			        g, sum[0] / g, sum[1] / g, sum[2] / g, sum[3] / g, sum[4] / g, sum[5] / g, sum[6] / g, sum[7] / g,
+			        (unsigned long long)mx);
+		}
+	} dump_{st, grid};
+#endif
 	switch (m) {
 	case 96: go(pq_fast_scan_kernel<96>); break;
 	case 64: go(pq_fast_scan_kernel<64>); break;

@@ -1730,7 +1730,8 @@ struct SelSrc {
 };
 
 // exclusive scan of one value per thread across the block
-__device__ __forceinline__ unsigned block_excl_scan(unsigned v, unsigned *sh /*[SEL_THREADS/64]*/, unsigned &total) {
+template <int NT = SEL_THREADS>
+__device__ __forceinline__ unsigned block_excl_scan(unsigned v, unsigned *sh /*[NT/64]*/, unsigned &total) {
 	const int t = threadIdx.x, lane = t & 63, w = t >> 6;
 	unsigned x = v;
 #pragma unroll
@@ -1742,7 +1743,7 @@ __device__ __forceinline__ unsigned block_excl_scan(unsigned v, unsigned *sh /*[
 	__syncthreads();
 	unsigned base = 0, tot = 0;
 #pragma unroll
-	for (int i = 0; i < SEL_THREADS / 64; ++i) {
+	for (int i = 0; i < NT / 64; ++i) {
 		base += (i < w) ? sh[i] : 0u;
 		tot += sh[i];
 	}
@@ -2322,7 +2323,15 @@ void launch_finalize(const StoreView &s, const uint32_t *cand_slot, const int *c
 // certificate (cut = -inf), as select_kernel's does; the rows refined still
 // give the rerun a tau.  Returns the refined count and the pool size.
 // ---------------------------------------------------------------------------
-constexpr int PR_THREADS = 512;
+#ifndef LHIP_PR_THREADS
+#define LHIP_PR_THREADS 512
+#endif
+constexpr int PR_THREADS = LHIP_PR_THREADS;  // 512 or 1024 (one workgroup per query)
+static_assert(PR_THREADS == 512 || PR_THREADS == 1024, "pool_refine geometry");
+#ifdef LHIP_PR_PROF
+constexpr int PR_NSTAMP = 32, PR_PROF_Q = 4096;
+__device__ uint64_t g_pr_stamps[PR_PROF_Q * (PR_NSTAMP + 3)];
+#endif
 constexpr int PR_WAVES = PR_THREADS / 64;
 constexpr int PR_CAP = 16384;       // pool entries held in LDS
 constexpr int PR_PER_WAVE = 16;     // candidates per wave and round
@@ -2402,18 +2411,280 @@ __device__ __forceinline__ void exact_distance_multi(const T *__restrict__ X, in
 	}
 }
 
-// rows per wave and refine round of pool_refine: every load of a round in
-// flight at once (NI x NC 16-B loads per lane) within the register budget of
+// Exact distances of NC rows (NC a power of two <= 16) to one query by one
+// wave, NS = ceil(dim / 256) 16-B column steps per row, each the value
+// exact_distance returns (f64 accumulation, one rounding to f32):
+//   * loads: the rows' bases are wave-uniform (SGPR slots, recomputed per
+//     use); the rows in two halves, one half's loads in flight while the other
+//     half is summed (per-lane accumulation order unchanged: steps ascending,
+//     x y z w);
+//   * the per-row wave sums as a transpose-reduce: at each xor level a lane
+//     keeps half of its rows' partial sums and adds the partner's copy of them
+//     (NC-1 f64 shuffles for the halving levels + log2(64/NC) for the rest,
+//     instead of 6 NC); row r ends up in lanes r * (64 / NC) .. (r + 1) * (64 / NC) - 1.
+// Returns this lane's value (row lane / (64 / NC)); rows >= nvalid read nothing.
+// The query comes from LDS (qs: NS * 256 floats, zero past dim).
+template <int METRIC, typename T, int NC, int NS>
+__device__ __forceinline__ float exact_rows_ring(const T *__restrict__ X, int ld, const uint32_t *slots, int nvalid,
+                                                 const float *qs, int dim, int lane) {
+	static_assert(NC == 1 || NC == 2 || NC == 4 || NC == 8 || NC == 16, "NC: a power of two <= 16");
+	static_assert(NS >= 1 && NS <= 4, "NS: 256-element steps of a row");
+	constexpr int NSUM = METRIC == METRIC_COSINE ? 3 : 1;
+	const int d4 = dim >> 2;
+	uint32_t svr[NC];  // the rows' slots (wave-uniform: SGPRs)
+#pragma unroll
+	for (int r = 0; r < NC; ++r) svr[r] = __builtin_amdgcn_readfirstlane(slots[r]);
+	// a row's base, recomputed at each use (opaque to CSE: NC live 64-bit
+	// pointers would not fit the SGPR budget and spill into VGPRs)
+	auto xr = [&](int r) -> const T * {
+		uint32_t sv = svr[r];
+		asm volatile("" : "+s"(sv));
+		return X + (int64_t)sv * ld;
+	};
+	double acc[NSUM][NC];
+#pragma unroll
+	for (int r = 0; r < NC; ++r)
+#pragma unroll
+		for (int u = 0; u < NSUM; ++u) acc[u][r] = 0.0;
+	// loads: a rolled loop over the column steps in two halves of the rows: a
+	// half's loads are issued before the other half is summed, so the memory
+	// stays busy while the wave sums (a fully unrolled ring let the compiler
+	// hoist every step's loads and the 256 VGPRs of two waves per SIMD spilled)
+	constexpr int HR = NC > 1 ? NC / 2 : 1, NH = NC / HR;
+	auto issue = [&](int s, int h, float4 (&b)[HR]) {
+		const int i4 = lane + 64 * s;
+#pragma unroll
+		for (int r = 0; r < HR; ++r)
+			b[r] = (h * HR + r < nvalid && i4 < d4) ? xval4(xr(h * HR + r), 4 * i4) : make_float4(0.f, 0.f, 0.f, 0.f);
+	};
+	auto consume = [&](int s, int h, const float4 (&b)[HR]) {
+		const float4 qv = *reinterpret_cast<const float4 *>(qs + 4 * (lane + 64 * s));  // zero past dim
+#pragma unroll
+		for (int r = 0; r < HR; ++r) {
+			const int rr = h * HR + r;
+			double a = acc[0][rr], bb = NSUM > 1 ? acc[1][rr] : 0.0, cc = NSUM > 1 ? acc[2][rr] : 0.0;
+			exact_acc<METRIC>(b[r].x, qv.x, a, bb, cc);
+			exact_acc<METRIC>(b[r].y, qv.y, a, bb, cc);
+			exact_acc<METRIC>(b[r].z, qv.z, a, bb, cc);
+			exact_acc<METRIC>(b[r].w, qv.w, a, bb, cc);
+			acc[0][rr] = a;
+			if (NSUM > 1) {
+				acc[1][rr] = bb;
+				acc[2][rr] = cc;
+			}
+		}
+	};
+	float4 b0[HR], b1[HR];
+	issue(0, 0, b0);
+#pragma unroll 1
+	for (int s = 0; s < NS; ++s) {
+		if (NH > 1) issue(s, 1, b1);
+		consume(s, 0, b0);
+		if (s + 1 < NS) issue(s + 1, 0, b0);
+		if (NH > 1) consume(s, 1, b1);
+	}
+	// dim % 4 tail elements (rows of any dim the path admits)
+	for (int i = 4 * d4 + lane; i < dim; i += 64)
+#pragma unroll
+		for (int r = 0; r < NC; ++r)
+			if (r < nvalid) {
+				double a = acc[0][r], bb = NSUM > 1 ? acc[1][r] : 0.0, cc = NSUM > 1 ? acc[2][r] : 0.0;
+				exact_acc<METRIC>(xval(xr(r), i), qs[i], a, bb, cc);
+				acc[0][r] = a;
+				if (NSUM > 1) {
+					acc[1][r] = bb;
+					acc[2][r] = cc;
+				}
+			}
+	// transpose-reduce: level o (32, 16, ..) halves the rows a lane holds
+	double v[NSUM];
+	{
+		double cur[NSUM][NC];
+#pragma unroll
+		for (int u = 0; u < NSUM; ++u)
+#pragma unroll
+			for (int r = 0; r < NC; ++r) cur[u][r] = acc[u][r];
+		int o = 32;
+#pragma unroll
+		for (int h = NC / 2; h >= 1; h >>= 1, o >>= 1) {
+			const bool hi = (lane & o) != 0;
+#pragma unroll
+			for (int u = 0; u < NSUM; ++u)
+#pragma unroll
+				for (int r = 0; r < h; ++r) {
+					const double send = hi ? cur[u][r] : cur[u][r + h];
+					const double keep = hi ? cur[u][r + h] : cur[u][r];
+					cur[u][r] = keep + __shfl_xor(send, o, 64);
+				}
+		}
+#pragma unroll
+		for (int u = 0; u < NSUM; ++u) {
+			double x = cur[u][0];
+			for (int oo = o; oo > 0; oo >>= 1) x += __shfl_xor(x, oo, 64);
+			v[u] = x;
+		}
+	}
+	double res;
+	if (METRIC == METRIC_L2) {
+		res = v[0];
+	} else if (METRIC == METRIC_DOT) {
+		res = 1.0 - v[0];
+	} else {
+		res = 1.0 - v[0] / (sqrt(v[1]) * sqrt(v[NSUM - 1]));
+	}
+	float f = (float)res + 0.0f;  // canonical +0
+	if (__builtin_isnan(f)) f = __builtin_nanf("");
+	return f;
+}
+
+// rows per wave and refine round of pool_refine within the register budget of
 // two waves per SIMD; cosine keeps three f64 sums per row (half the rows)
+// NI: the refine path and row length of a pool_refine instantiation.
+//   NI = 1..4: rows of <= 256 NI elements, every load of a wave's round in
+//     flight at once (exact_distance_multi): small rounds (tau mode: k + 8
+//     rows) pay one memory latency;
+//   NI = 8 + (1..4): exact_rows_ring (SGPR row bases, half the rows' loads in
+//     flight while the other half is summed, transpose-reduced sums): twice
+//     the rows per wave, the final mode's large rounds;
+//   NI = 0: rows past 1024 elements, one column step at a time.
 template <int METRIC, int NI>
 struct PrGeom {
-#ifdef LHIP_PR_PW3  // (development builds: rows per wave of the ld <= 768 path)
-	static constexpr int base = NI == 0 ? 16 : NI == 1 ? 16 : NI == 2 ? 12 : NI == 3 ? LHIP_PR_PW3 : 8;
-#else
-	static constexpr int base = NI == 0 ? 16 : NI == 1 ? 16 : NI == 2 ? 12 : 8;
-#endif
-	static constexpr int PW = METRIC == METRIC_COSINE ? base / 2 : base;
+	static constexpr int NS = NI & 7;  // 256-element steps (0: any length)
+	static constexpr bool RING = NI >= 8;
+	// rows per wave: the all-in-flight loads within the 256 VGPRs of two waves
+	// per SIMD; cosine keeps three f64 sums per row (half the rows); 1024 threads
+	// (four waves per SIMD, 128 VGPRs): half as many
+	static constexpr int base = RING ? 16 : NS == 0 ? 16 : NS == 1 ? 16 : NS == 2 ? 12 : 8;
+	static constexpr int PW0 = METRIC == METRIC_COSINE ? base / 2 : base;
+	static constexpr int PW = PR_THREADS == 1024 ? PW0 / 2 : PW0;
 };
+
+// one refine round's exact distances of a wave's rows: lane r < nv gets row r's
+// (PrGeom: the ring path, the all-in-flight path or the column-step path)
+template <int METRIC, typename T, int PW, int NI>
+__device__ __forceinline__ float pr_distances(const T *__restrict__ X, int ld, const uint32_t *sl, int nv,
+                                              const float *__restrict__ qrow, const float *qs, int dim, int lane) {
+	if (nv <= 0) return 0.f;
+	constexpr int NS = PrGeom<METRIC, NI>::NS;
+	if constexpr (PrGeom<METRIC, NI>::RING) {
+		const float rv = exact_rows_ring<METRIC, T, PW, NS>(X, ld, sl, nv, qs, dim, lane);
+		return __shfl(rv, (lane & (PW - 1)) * (64 / PW), 64);
+	} else {
+		float d[PW];
+		exact_distance_multi<METRIC, T, PW, NS>(X, ld, sl, nv, qrow, qs, dim, lane, d);
+		float dv = d[0];
+#pragma unroll
+		for (int r = 1; r < PW; ++r)
+			if (lane == r) dv = d[r];
+		return dv;
+	}
+}
+
+// The k smallest of m entries (d[i], l[i]) by (distance, label) -> od/ol
+// [0, min(m, k)), ascending (hit_less order; distances are canonical: +0, one
+// NaN, so (fkey(d), label) is that order).  k <= PR_WMK, 48 < m <= 192: wave 0
+// alone, entries in registers (3 per lane): a 32-step radix select of the
+// min(m, k)-th smallest key by ballot counts, the entries at or below it
+// compacted into od/ol, then each ranked against the others (a handful).
+// Otherwise every thread ranks one entry against all m (O(m^2) LDS reads).
+// The caller synchronises the block afterwards.
+constexpr int PR_WMK = 32;
+constexpr int PR_WMK_MIN_M = 48;  // (smaller merges, e.g. the tau mode's k + 8 rows: the rank form is cheaper)
+__device__ __forceinline__ void pr_merge(const float *d, const int64_t *l, float *od, int64_t *ol, int m, int k) {
+	const int t = threadIdx.x, lane = t & 63;
+	if (k <= PR_WMK && m > PR_WMK_MIN_M && m <= 192) {
+		if (t >= 64) return;
+		constexpr int E = 3;
+		uint32_t kk[E];
+		bool vm[E];
+#pragma unroll
+		for (int e = 0; e < E; ++e) {
+			const int i = lane + 64 * e;
+			vm[e] = i < m;
+			kk[e] = vm[e] ? fkey(d[i]) : 0xFFFFFFFFu;
+		}
+		const int want = min(m, k);
+		// T = the want-th smallest key: bits from the top, below = keys < prefix
+		uint32_t T = 0u;
+		int below = 0;
+		for (int b = 31; b >= 0; --b) {
+			int c0 = 0;
+#pragma unroll
+			for (int e = 0; e < E; ++e)
+				c0 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(vm[e] && ((kk[e] ^ T) >> b) == 0u));
+			if (below + c0 < want) {
+				below += c0;
+				T |= 1u << b;
+			}
+		}
+		// every entry with key <= T (want of them, more on ties at T) -> od/ol [0, ns)
+		float dv[E];
+		int64_t lv[E];
+		int base = 0;
+#pragma unroll
+		for (int e = 0; e < E; ++e) {
+			const bool sel = vm[e] && kk[e] <= T;
+			const uint64_t bm = __builtin_amdgcn_ballot_w64(sel);
+			if (sel) {
+				const int i = lane + 64 * e;
+				dv[e] = d[i];
+				lv[e] = l[i];
+			}
+			const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+			base += __builtin_popcountll(bm);
+			kk[e] = sel ? (uint32_t)pos : 0xFFFFFFFFu;  // (now: the compacted position)
+		}
+		const int ns = base;
+		// (d and od may alias nothing: the caller's buffers are the two halves)
+#pragma unroll
+		for (int e = 0; e < E; ++e)
+			if (kk[e] != 0xFFFFFFFFu) {
+				od[kk[e]] = dv[e];
+				ol[kk[e]] = lv[e];
+			}
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+		__builtin_amdgcn_wave_barrier();
+		// rank each compacted entry (lane j < ns) among the ns: the smallest want go out
+		float dj[E];
+		int64_t lj[E];
+		int rk[E];
+#pragma unroll
+		for (int e = 0; e < E; ++e) {
+			const int j = lane + 64 * e;
+			rk[e] = 0;
+			if (j < ns) {
+				dj[e] = od[j];
+				lj[e] = ol[j];
+			}
+		}
+		for (int i = 0; i < ns; ++i) {
+			const float di = od[i];
+			const int64_t li = ol[i];
+#pragma unroll
+			for (int e = 0; e < E; ++e)
+				if (lane + 64 * e < ns) rk[e] += hit_less(di, li, dj[e], lj[e]) ? 1 : 0;
+		}
+		__builtin_amdgcn_wave_barrier();
+#pragma unroll
+		for (int e = 0; e < E; ++e)
+			if (lane + 64 * e < ns && rk[e] < want) {
+				od[rk[e]] = dj[e];
+				ol[rk[e]] = lj[e];
+			}
+		return;
+	}
+	for (int i = t; i < m; i += PR_THREADS) {
+		const float di = d[i];
+		const int64_t li = l[i];
+		int rank = 0;
+#pragma unroll 8
+		for (int j = 0; j < m; ++j) rank += hit_less(d[j], l[j], di, li) ? 1 : 0;
+		if (rank < k) {
+			od[rank] = di;
+			ol[rank] = li;
+		}
+	}
+}
 
 // ascending bitonic sort of a[0, P) (P a power of two >= 64) by the block
 __device__ __forceinline__ void pr_bitonic(uint64_t *a, int P) {
@@ -2436,6 +2707,8 @@ __device__ __forceinline__ void pr_bitonic(uint64_t *a, int P) {
 
 constexpr int PR_SEL = 1024;  // chunk capacity
 constexpr int PR_HB = 1024;   // histogram bins of a chunk selection
+constexpr int PR_BPT = PR_HB / PR_THREADS;  // bins per thread (2 or 1)
+static_assert(PR_BPT * PR_THREADS == PR_HB && (PR_BPT == 1 || PR_BPT == 2), "bins per thread");
 constexpr int PR_R = 96;      // first chunk of the final pass (C2: ~80 rows lie below d_k; refined rows
                               // are the kernel's HBM traffic: 96 refined 18 % fewer than 128 at equal
                               // step time or better, r03s2)
@@ -2456,15 +2729,18 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 	__shared__ int s_over, s_nnan, s_dnan;
 	__shared__ unsigned s_nfin, s_knf, s_kmin, s_kmax, s_bstar, s_cum, s_below, s_ns, s_hi, s_pmin, s_pmax;
 	__shared__ unsigned segc[PR_THREADS];  // (big pools) segment counts
-	__shared__ __attribute__((aligned(16))) float qs[NI > 0 ? 256 * NI : 4];  // the query row (NI > 0)
+	constexpr int NS_ = PrGeom<METRIC, NI>::NS;
+	__shared__ __attribute__((aligned(16))) float qs[NS_ > 0 ? 256 * NS_ : 4];  // the query row (NS_ > 0)
 	const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
 #ifdef LHIP_PR_PROF
-	// phase stamps (diagnostic build, one designated launch): thread 0 prints
-	// the cycles of each phase for the first queries and any slow workgroup
-	uint64_t stamp[24];
+	// phase stamps (diagnostic build, one designated launch): thread 0 keeps the
+	// cycle counter at each phase boundary and stores them to g_pr_stamps at the
+	// end (the host prints them after the launch: no printf inside the kernel,
+	// whose host calls slowed the workgroups still running)
+	uint64_t stamp[PR_NSTAMP];
 	int nst = 0;
 	auto mark = [&]() {
-		if (nst < 24) stamp[nst++] = __builtin_amdgcn_s_memtime();
+		if (nst < PR_NSTAMP) stamp[nst++] = __builtin_amdgcn_s_memtime();
 	};
 	mark();
 #else
@@ -2499,14 +2775,21 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 	};
 	// ---- gather the pool (thread s < n_seg: segment s) ----------------------
 	unsigned c = 0;
+	// the segment's first PR_SPEC entries (within its capacity) are loaded with
+	// its count: one memory latency for the typical segment, not two (entries
+	// past the count are never used)
+	constexpr int PR_SPEC = 8;
+	uint2 e0[PR_SPEC];
 	if (t < n_seg) {
+		const uint2 *seg = seg_pool + ((int64_t)t * nq + q) * seg_cap;
+#pragma unroll
+		for (int u = 0; u < PR_SPEC; ++u) e0[u] = u < seg_cap ? seg[u] : make_uint2(0u, 0u);
 		const int cs = seg_cnt[(int64_t)t * nq + q];
 		if (cs > seg_cap) s_over = 1;
 		c = (unsigned)min(cs, seg_cap);
 	}
 	unsigned total;
-	static_assert(PR_THREADS == SEL_THREADS, "block_excl_scan's geometry");
-	const unsigned off = block_excl_scan(c, sh, total);
+	const unsigned off = block_excl_scan<PR_THREADS>(c, sh, total);
 	// a pool past PR_CAP: keep its smallest bounds (whole histogram bins, at most
 	// PR_CAP) and treat the rest like rows outside the pool: cut <= the smallest
 	// bound left out (excl_min), an exact certificate without a rerun.  Only when
@@ -2571,15 +2854,14 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 		}
 		__syncthreads();
 		{
-			static_assert(PR_HB == 2 * PR_THREADS, "two bins per thread");
-			const unsigned h0 = hist[2 * t], h1 = hist[2 * t + 1];
+			const unsigned h0 = hist[PR_BPT * t], h1 = PR_BPT == 2 ? hist[PR_BPT * t + 1] : 0u;
 			unsigned tot;
-			const unsigned ex = block_excl_scan(h0 + h1, sh, tot);
+			const unsigned ex = block_excl_scan<PR_THREADS>(h0 + h1, sh, tot);
 			int cand = -1;  // the last bin whose inclusive count fits
-			if (ex + h0 + h1 <= (unsigned)PR_CAP)
-				cand = 2 * t + 1;
+			if (PR_BPT == 2 && ex + h0 + h1 <= (unsigned)PR_CAP)
+				cand = PR_BPT * t + 1;
 			else if (ex + h0 <= (unsigned)PR_CAP)
-				cand = 2 * t;
+				cand = PR_BPT * t;
 			if (cand >= 0) atomicMax(reinterpret_cast<int *>(&s_bstar) + 0, cand);  // (s_bstar starts at -1)
 		}
 		__syncthreads();
@@ -2606,7 +2888,13 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 	if (!big && t < n_seg && c && off < (unsigned)PR_CAP) {
 		const uint2 *seg = seg_pool + ((int64_t)t * nq + q) * seg_cap;
 		const unsigned cm = min(c, (unsigned)PR_CAP - off);
-		for (unsigned i = 0; i < cm; i += 8) {  // 8 loads in flight per thread
+#pragma unroll
+		for (int u = 0; u < PR_SPEC; ++u)
+			if ((unsigned)u < cm) {
+				keys[off + u] = ((uint64_t)e0[u].x << 32) | e0[u].y;
+				gstat(e0[u].x);
+			}
+		for (unsigned i = PR_SPEC; i < cm; i += 8) {  // 8 loads in flight per thread
 			uint2 e[8];
 #pragma unroll
 			for (int u = 0; u < 8; ++u)
@@ -2646,8 +2934,8 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 	const float ftau = tau ? tau[q] : F_INF;
 	const float *qrow = Qf + (int64_t)q * ld;
 	// the query row in LDS (NI > 0: every refine round reads it there, zero past dim)
-	if (NI > 0)
-		for (int i = t; i < 64 * 4 * (NI > 0 ? NI : 1); i += PR_THREADS) qs[i] = i < dim ? qrow[i] : 0.f;
+	if (NS_ > 0)
+		for (int i = t; i < 64 * 4 * (NS_ > 0 ? NS_ : 1); i += PR_THREADS) qs[i] = i < dim ? qrow[i] : 0.f;
 
 	// next chunk: the finite keys in [lo, hi_goal] up to a histogram bin holding
 	// the R-th smallest of them (all of them when fewer), at most PR_SEL, slots
@@ -2703,13 +2991,12 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 				if (kk >= kmin && kk <= kmax) atomicAdd(&hist[(kk - kmin) >> shift], 1u);
 			}
 			__syncthreads();
-			const unsigned h0 = hist[2 * t], h1 = hist[2 * t + 1];
-			static_assert(PR_HB == 2 * PR_THREADS, "two bins per thread");
+			const unsigned h0 = hist[PR_BPT * t], h1 = PR_BPT == 2 ? hist[PR_BPT * t + 1] : 0u;
 			unsigned tot;
-			const unsigned ex = block_excl_scan(h0 + h1, sh, tot);
+			const unsigned ex = block_excl_scan<PR_THREADS>(h0 + h1, sh, tot);
 			if (ex < (unsigned)R && ex + h0 + h1 >= (unsigned)R) {
 				const bool first = ex + h0 >= (unsigned)R;
-				s_bstar = first ? 2 * t : 2 * t + 1;
+				s_bstar = first ? PR_BPT * t : PR_BPT * t + 1;
 				s_cum = first ? ex + h0 : ex + h0 + h1;
 				s_below = first ? ex : ex + h0;
 			}
@@ -2781,32 +3068,19 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 				for (int r = 0; r < PW; ++r) sl[r] = r < nv ? slots[sp + b0 + r] : 0u;
 				// this lane's label load in flight with the row loads
 				const int64_t lab = lane < nv ? labels[slots[sp + b0 + lane]] : 0;
-				float d[PW];
-				if (nv > 0) exact_distance_multi<METRIC, T, PW, NI>(X, ld, sl, nv, qrow, qs, dim, lane, d);
+				const float dv = pr_distances<METRIC, T, PW, NI>(X, ld, sl, nv, qrow, qs, dim, lane);
 				if (lane < nv) {
-					float dv = d[0];
-#pragma unroll
-					for (int r = 1; r < PW; ++r)
-						if (lane == r) dv = d[r];
 					cd[cur][cnt + b0 + lane] = dv;
 					cl[cur][cnt + b0 + lane] = lab;
 					if (__builtin_isnan(dv)) s_dnan = 1;
 				}
 			}
+			mark();  // (thread 0 = wave 0: its own rows' distances done)
 			__syncthreads();
-			// merge: rank of every entry (top so far + this round) by (distance, label)
+			mark();
+			// merge the top so far and this round by (distance, label)
 			const int m = cnt + nr;
-			for (int i = t; i < (LHIP_ABL_PR_NOMERGE ? 0 : m); i += PR_THREADS) {
-				const float di = cd[cur][i];
-				const int64_t li = cl[cur][i];
-				int rank = 0;
-#pragma unroll 8
-				for (int j = 0; j < m; ++j) rank += hit_less(cd[cur][j], cl[cur][j], di, li) ? 1 : 0;
-				if (rank < k) {
-					cd[cur ^ 1][rank] = di;
-					cl[cur ^ 1][rank] = li;
-				}
-			}
+			if (!LHIP_ABL_PR_NOMERGE) pr_merge(cd[cur], cl[cur], cd[cur ^ 1], cl[cur ^ 1], m, k);
 			__syncthreads();
 			cur ^= 1;
 			cnt = min(m, k);
@@ -2834,14 +3108,12 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 				const int b0 = w * PW, nv = max(0, min(PW, nr - b0));
 #pragma unroll
 				for (int r = 0; r < PW; ++r) sl[r] = r < nv ? (uint32_t)order[sp + b0 + r] : 0u;
-				float d[PW];
-				if (nv > 0) exact_distance_multi<METRIC, T, PW, NI>(X, ld, sl, nv, qrow, qs, dim, lane, d);
+				const float dv = pr_distances<METRIC, T, PW, NI>(X, ld, sl, nv, qrow, qs, dim, lane);
 				if (lane < nv) {
-					float dv = d[0];
 					uint32_t sv = sl[0];
 #pragma unroll
 					for (int r = 1; r < PW; ++r)
-						if (lane == r) dv = d[r], sv = sl[r];
+						if (lane == r) sv = sl[r];
 					cd[cur][cnt + b0 + lane] = dv;
 					cl[cur][cnt + b0 + lane] = labels[sv];
 					if (__builtin_isnan(dv)) s_dnan = 1;
@@ -2849,17 +3121,7 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 			}
 			__syncthreads();
 			const int m = cnt + nr;
-			for (int i = t; i < m; i += PR_THREADS) {
-				const float di = cd[cur][i];
-				const int64_t li = cl[cur][i];
-				int rank = 0;
-#pragma unroll 8
-				for (int j = 0; j < m; ++j) rank += hit_less(cd[cur][j], cl[cur][j], di, li) ? 1 : 0;
-				if (rank < k) {
-					cd[cur ^ 1][rank] = di;
-					cl[cur ^ 1][rank] = li;
-				}
-			}
+			pr_merge(cd[cur], cl[cur], cd[cur ^ 1], cl[cur ^ 1], m, k);
 			__syncthreads();
 			cur ^= 1;
 			cnt = min(m, k);
@@ -2926,12 +3188,12 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 		cert[q] = ok ? 1 : 0;
 #ifdef LHIP_PR_PROF
 		mark();
-		if (prof_on && (q < 6 || stamp[nst - 1] - stamp[0] > 60000)) {
-			int d[12];
-			for (int i = 0; i < 12; ++i) d[i] = i + 1 < nst ? (int)(stamp[i + 1] - stamp[i]) : -1;
-			printf("PR q=%d pool=%d refined=%d nst=%d total=%d | %d %d %d %d %d %d %d %d %d %d %d %d\n", q, n, pos, nst,
-			       (int)(stamp[nst - 1] - stamp[0]), d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9], d[10],
-			       d[11]);
+		if (prof_on && q < PR_PROF_Q) {
+			uint64_t *o = g_pr_stamps + (size_t)q * (PR_NSTAMP + 3);
+			o[0] = (uint64_t)nst;
+			o[1] = (uint64_t)n;
+			o[2] = (uint64_t)pos;
+			for (int i = 0; i < nst; ++i) o[3 + i] = stamp[i];
 		}
 #endif
 		if (refined) refined[q] = pos;
@@ -2940,6 +3202,25 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 }
 
 int pool_refine_max_first() { return PR_SEL; }
+
+#ifdef LHIP_PR_PROF
+// host side of the phase stamps: the designated launch's per-query stamps,
+// printed as cycle deltas (PR q=.. pool=.. refined=.. | d0 d1 ...)
+static void pr_prof_dump(hipStream_t st) {
+	static uint64_t h[PR_PROF_Q * (PR_NSTAMP + 3)];
+	if (hipStreamSynchronize(st) != hipSuccess) return;
+	if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pr_stamps), sizeof(h)) != hipSuccess) return;
+	for (int q = 0; q < PR_PROF_Q; ++q) {
+		const uint64_t *o = h + (size_t)q * (PR_NSTAMP + 3);
+		const int nst = (int)o[0];
+		if (nst < 2) continue;
+		fprintf(stderr, "PR q=%d pool=%d refined=%d nst=%d total=%lld |", q, (int)o[1], (int)o[2], nst,
+		        (long long)(o[3 + nst - 1] - o[3]));
+		for (int i = 1; i < nst; ++i) fprintf(stderr, " %lld", (long long)(o[3 + i] - o[3 + i - 1]));
+		fprintf(stderr, "\n");
+	}
+}
+#endif
 
 template <typename T>
 static void pool_refine_dispatch(const StoreView &s, const QueryView &q, const uint2 *seg_pool, const int *seg_cnt,
@@ -2951,6 +3232,13 @@ static void pool_refine_dispatch(const StoreView &s, const QueryView &q, const u
 #ifdef LHIP_PR_PROF
 	static std::atomic<int> calls{0};  // (diagnostic build: the 12th final-mode launch of the process prints its phases)
 	const int prof_on = mode == 1 && ++calls == 12;
+	struct Dump {  // prints after the designated launch (any return path)
+		int on;
+		hipStream_t st;
+		~Dump() {
+			if (on) pr_prof_dump(st);
+		}
+	} dump_{prof_on, st};
 #else
 	const int prof_on = 0;
 #endif
@@ -2965,21 +3253,21 @@ static void pool_refine_dispatch(const StoreView &s, const QueryView &q, const u
 	case 2: LHIP_PR(MET, 2); break;                                                                                    \
 	case 3: LHIP_PR(MET, 3); break;                                                                                    \
 	case 4: LHIP_PR(MET, 4); break;                                                                                    \
+	case 9: LHIP_PR(MET, 9); break;                                                                                    \
+	case 10: LHIP_PR(MET, 10); break;                                                                                  \
+	case 11: LHIP_PR(MET, 11); break;                                                                                  \
+	case 12: LHIP_PR(MET, 12); break;                                                                                  \
 	default: LHIP_PR(MET, 0); break;                                                                                   \
 	}
-	// row length in 256-element steps (one 16-B load per lane each): <= 4 -> all in flight per round
-	// tau mode (at most m_tau <= MAX_CAND rows, typically k + 8: one round) takes every
-	// load of the round at once (NI path, measured 15.4 vs 17.0 us at C2); the final
-	// mode's rounds are larger and keep 16 rows per wave one column step at a time
-	// (66 vs 75 us at C2: twice the rows per round, half the rounds and merges;
-	// r04d kernel traces)
-#ifndef LHIP_PR_FINAL_NI  // (development builds: 1 = the final mode on the all-in-flight path too)
-#define LHIP_PR_FINAL_NI 0
-#endif
+	// row length in 256-element steps (one 16-B load per lane each, PrGeom): <= 4
+	// -> tau mode all loads of a round in flight, final mode exact_rows_ring;
+	// longer rows one column step at a time
 #ifdef LHIP_PR_FORCE_NI0  // (development builds: the one-column-step path everywhere)
 	const int ni = 0;
 #else
-	const int ni = (mode == 1 && !LHIP_PR_FINAL_NI) ? 0 : s.dim <= 256 ? 1 : s.dim <= 512 ? 2 : s.dim <= 768 ? 3 : s.dim <= 1024 ? 4 : 0;
+	const int ns = s.dim <= 256 ? 1 : s.dim <= 512 ? 2 : s.dim <= 768 ? 3 : s.dim <= 1024 ? 4 : 0;
+	// tau mode (k + 8 rows: one small round) every load in flight; final mode the ring
+	const int ni = ns == 0 ? 0 : mode == 1 ? 8 + ns : ns;
 #endif
 	switch (s.metric) {
 	case METRIC_L2: LHIP_PR_NI(METRIC_L2); break;

@@ -1330,6 +1330,12 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			ix->ivf_flat_bound = b;
 			return 0;
 		}
+		if (k == "pq_seed") {
+			if (v == "1") ix->pq_seed = true;
+			else if (v == "0") ix->pq_seed = false;
+			else throw Error("pq_seed: 1 or 0");
+			return 0;
+		}
 		if (k == "pq_scan") {
 			if (v == "fast") ix->pq_fast = true;
 			else if (v == "exact_lut") ix->pq_fast = false;

@@ -144,20 +144,35 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 	const int lr = lane & 15, lg = lane >> 4;
 
 	// ---- prologue: the 128 queries into LDS (chunk c of query n at c ^ (n & 15)) --
+	// every load of the prologue in flight together (a load-wait-store loop paid
+	// one L2 round trip per 16 B chunk step: 12 of them at ld = 768, ~10 us)
 	{
-		constexpr int NCH = KS * 4;  // 16 B chunks per query row
-		for (int i = tid; i < QH * NCH; i += T8) {
-			const int n = i / NCH, c = i - n * NCH;
-			const i32x4 v = *reinterpret_cast<const i32x4 *>(Qi + (int64_t)(qb + n) * 2 * ld + 16 * c);
-			*reinterpret_cast<i32x4 *>(QL + n * P + ((c ^ (n & 15)) << 4)) = v;
+		constexpr int NCH = KS * 4;          // 16 B chunks per query row
+		constexpr int PER = QH * NCH / T8;   // chunks per thread
+		static_assert(QH * NCH % T8 == 0, "whole chunk steps per thread");
+		float4 qa = make_float4(0.f, 0.f, 0.f, 0.f);
+		float tq = -F_INF;
+		if (tid < QH) {
+			const int q = qb + tid;
+			qa = qaux[q];
+			if (TM == 0 && q < nq) tq = tau[q];
 		}
-	}
-	if (tid < QH) {
-		const int q = qb + tid;
-		const float4 qa = qaux[q];
-		QA[tid] = qa;
-		QP[tid] = s8_query_terms(qa, (TM == 0 && q < nq) ? tau[q] : -F_INF);
-		CNT[tid] = 0u;
+		i32x4 v[PER];
+#pragma unroll
+		for (int j = 0; j < PER; ++j) {
+			const int i = tid + j * T8, n = i / NCH, c = i - n * NCH;
+			v[j] = *reinterpret_cast<const i32x4 *>(Qi + (int64_t)(qb + n) * 2 * ld + 16 * c);
+		}
+#pragma unroll
+		for (int j = 0; j < PER; ++j) {
+			const int i = tid + j * T8, n = i / NCH, c = i - n * NCH;
+			*reinterpret_cast<i32x4 *>(QL + n * P + ((c ^ (n & 15)) << 4)) = v[j];
+		}
+		if (tid < QH) {
+			QA[tid] = qa;
+			QP[tid] = s8_query_terms(qa, tq);
+			CNT[tid] = 0u;
+		}
 	}
 	if (tid == 0) *UCNT = (unsigned)NW;  // units 0 .. NW-1: one per wave, the rest claimed
 	__syncthreads();

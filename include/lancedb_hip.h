@@ -217,6 +217,9 @@ int32_t lance_hip_device_count(void);
  *                  lower bounds + certified exact re-rank, or exact f64 distances
  *   "pq_scan"      "fast" (default) | "exact_lut": IVF_PQ list-major 8-bit-LUT
  *                  scan, or the query-major f32-LUT scan
+ *   "pq_seed"      "1" (default) | "0": the fast scan's per-query bound starts
+ *                  at the kk-th smallest key of the query's nearest probed list
+ *                  (kk = k * refine_factor; results unchanged, less work)
  *   "pq_query"     "f32" (default) | "fp8": IVF_PQ distance tables from e4m3
  *                  (fp8) queries (BASELINE.json configs[4]); coarse search and
  *                  re-rank keep the f32 query

@@ -140,6 +140,14 @@ def test_c5_ivf_pq_m96_refine_sweep(hip, data, exact):
         # f32-LUT scan measured on MI355X: 0.294 / 0.818 / 0.996 (profiles/r02_c_ivf_params.log)
         assert recalls[10] >= 0.75
         assert recalls[50] >= 0.98
+        # the per-query bound seeded from the nearest probed list (option pq_seed,
+        # default on) only skips work: the same lists without it
+        g_seed = hip.LanceDetachedSearchBatch(h, Q, K, nprobes=NPROBE, refine_factor=10)
+        hip.LanceHipSetOption(h, "pq_seed", "0")
+        g_noseed = hip.LanceDetachedSearchBatch(h, Q, K, nprobes=NPROBE, refine_factor=10)
+        hip.LanceHipSetOption(h, "pq_seed", "1")
+        for a, b in zip(g_seed, g_noseed):
+            np.testing.assert_array_equal(a, b)
         hip.LanceHipSetOption(h, "pq_query", "fp8")
         gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, K, nprobes=NPROBE, refine_factor=10)
         check(gl, gd, gc, *port_search(hip, h, X, Q, NPROBE, 10, query_fp8=True))

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Development-only library variants (diagnostic / A-B builds), never the product:
 #   tools/devlib.sh NAME SOURCE DEFINES...   ->  duckdb-lancedb_amd/lib_dev/lib_NAME.so
-# SOURCE (knn | scan8 | ivf) is rebuilt with DEFINES; the other objects are the
+# SOURCE (knn | scan8 | ivf: the <name>_kernels.hip file) is rebuilt with DEFINES; the other objects are the
 # release ones (make first).  Run with LANCE_HIP_LIB=duckdb-lancedb_amd/lib_dev/lib_NAME.so.
 set -e
 cd "$(dirname "$0")/.."
@@ -13,7 +13,7 @@ make -s -C $D
 mkdir -p $D/lib_dev
 objs=""
 for o in knn_kernels scan8_kernels ivf_kernels lance_hip_abi ivf_index meta; do
-	if [ "${o%%_*}" = "$src" ]; then
+	if [ "$o" = "${src}_kernels" ]; then
 		/opt/rocm/bin/hipcc $F "$@" -c $D/csrc/$o.hip -o $D/lib_dev/${o}_$n.o
 		objs="$objs $D/lib_dev/${o}_$n.o"
 	else
