@@ -21,10 +21,13 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 
+#include <atomic>
+#include <vector>
+
 // Development-only timing ablations of pq_fast_scan_kernel (results are wrong
 // when set): only an ablation build (tools/pq_ablate.sh) may turn them on.
 #if !defined(LHIP_ABLATION_BUILD) && (defined(LHIP_PQ_ABL_NO_LUT) || defined(LHIP_PQ_ABL_NO_LOOKUP) || \
-                                      defined(LHIP_PQ_ABL_NO_CAND))
+                                      defined(LHIP_PQ_ABL_NO_CAND) || defined(LHIP_PQ_ABL_NO_ALIVE))
 #error "PQ ablation switches are for ablation builds only"
 #endif
 
@@ -1878,16 +1881,18 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 					if (c < nch) w[c] = *reinterpret_cast<const uint4 *>(cp + (int64_t)c * 64 * 16);
 			}
 		};
-		load_row(c0 + t, cw, cslot, ctau);
-		for (int64_t r0 = c0; r0 < c1; r0 += FQ_THREADS) {
-			uint4 nw[NCH];
-			uint32_t nslot;
-			float ntau;
-			load_row(r0 + FQ_THREADS + t, nw, nslot, ntau);
+		// two code buffers, the loop unrolled twice: round i sums one buffer while
+		// round i + 1's codes land in the other (a copy of the prefetched registers
+		// at the round's end made every round wait for its own prefetch)
+		auto round = [&](const uint4 (&cw)[NCH], uint32_t cslot, float ctau, uint4 (&nw)[NCH], uint32_t &nslot,
+		                 float &ntau, int64_t rpre) __attribute__((always_inline)) {
 			// the query's bound from its other items, consumed at the round's end
 			// (a stale read is only a looser bound)
+			// (issued before the prefetch: its wait at the round's end then leaves
+			// the prefetch in flight — vmcnt counts in issue order)
 			uint64_t gthr = KEY64_NONE;
 			if (t < FQ_G && qid[t] >= 0) gthr = __builtin_nontemporal_load(thrq + qid[t]);
+			load_row(rpre, nw, nslot, ntau);
 			uint32_t s02 = 0u, s13 = 0u;
 #ifdef LHIP_PQ_ABL_NO_LOOKUP
 			s02 = cw[0].x ^ cw[1].y ^ cw[2].z ^ cw[3].w ^ cw[4].x ^ cw[5].y;
@@ -1900,22 +1905,35 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 				if constexpr (MT > 0) {
 					// m known at compile time: 16 independent LDS reads per code
 					// piece, then the sums (no per-j branch, batched lgkm waits)
+					// PQ_LB code pieces (16 lookups each) per LDS wait
+#ifndef LHIP_PQ_LB
+#define LHIP_PQ_LB 1
+#endif
+					constexpr int NCP = (MT + 15) / 16, LB = LHIP_PQ_LB;
 #pragma unroll
-					for (int c = 0; c < (MT + 15) / 16; ++c) {
-						const uint32_t wd[4] = {cw[c].x, cw[c].y, cw[c].z, cw[c].w};
-						uint32_t v[16];
+					for (int c0 = 0; c0 < NCP; c0 += LB) {
+						uint32_t v[LB][16];
 #pragma unroll
-						for (int u = 0; u < 16; ++u) {
-							const int j = c * 16 + u;
-							if (j < MT) v[u] = L[j * PQ_K + ((wd[u >> 2] >> (8 * (u & 3))) & 255u)];
-						}
+						for (int cc = 0; cc < LB; ++cc) {
+							const int c = c0 + cc;
+							if (c < NCP) {
+								const uint32_t wd[4] = {cw[c].x, cw[c].y, cw[c].z, cw[c].w};
 #pragma unroll
-						for (int u = 0; u < 16; ++u) {
-							if (c * 16 + u < MT) {
-								s02 += v[u] & 0x00FF00FFu;
-								s13 += __builtin_amdgcn_perm(0u, v[u], 0x0c030c01u);  // bytes 1, 3 -> 0, 2
+								for (int u = 0; u < 16; ++u) {
+									const int j = c * 16 + u;
+									if (j < MT) v[cc][u] = L[j * PQ_K + ((wd[u >> 2] >> (8 * (u & 3))) & 255u)];
+								}
 							}
 						}
+#pragma unroll
+						for (int cc = 0; cc < LB; ++cc)
+#pragma unroll
+							for (int u = 0; u < 16; ++u) {
+								if (c0 + cc < NCP && (c0 + cc) * 16 + u < MT) {
+									s02 += v[cc][u] & 0x00FF00FFu;
+									s13 += __builtin_amdgcn_perm(0u, v[cc][u], 0x0c030c01u);  // bytes 1, 3 -> 0, 2
+								}
+							}
 					}
 				} else {
 #pragma unroll
@@ -1952,7 +1970,11 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 				any |= pass[i];
 			}
 			// row liveness (a random 4-B read) only for rows under some bound
+#ifdef LHIP_PQ_ABL_NO_ALIVE  // (timing ablation: no liveness read)
+			if (any) {
+#else
 			if (any && slot_alive(rowaux_f, cslot)) {
+#endif
 #pragma unroll
 				for (int i = 0; i < FQ_G; ++i)
 					if (pass[i]) {
@@ -1960,10 +1982,6 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 						buf[i * FQ_CAP + p] = key[i];
 					}
 			}
-#pragma unroll
-			for (int c = 0; c < NCH; ++c) cw[c] = nw[c];
-			cslot = nslot;
-			ctau = ntau;
 			__syncthreads();
 			PQ_T(2);  // row round
 			for (int i = 0; i < FQ_G; ++i) {
@@ -1987,6 +2005,15 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 			if (t < FQ_G && gthr < thr[t]) thr[t] = gthr;
 			__syncthreads();
 			PQ_T(3);  // candidate sorts
+		};
+		uint4 cwB[NCH];
+		uint32_t cslotB = SLOT_NONE;
+		float ctauB = 0.0f;
+		load_row(c0 + t, cw, cslot, ctau);
+		for (int64_t r0 = c0; r0 < c1; r0 += 2 * FQ_THREADS) {
+			round(cw, cslot, ctau, cwB, cslotB, ctauB, r0 + FQ_THREADS + t);
+			if (r0 + FQ_THREADS >= c1) break;
+			round(cwB, cslotB, ctauB, cw, cslot, ctau, r0 + 2 * FQ_THREADS + t);
 		}
 		// flush: the item's keys within its final bound (entries appended before
 		// the bound tightened may lie above it)
@@ -2123,7 +2150,7 @@ void launch_pq_fast_scan(const uint8_t *lcodes, int m, int mp, const int64_t *lo
 		hipStream_t st;
 		int grid;
 		~Dump() {
-			static int calls = 0;
+			static std::atomic<int> calls{0};
 			if (++calls != 3 || hipStreamSynchronize(st) != hipSuccess) return;  // (the 3rd launch of the process)
 			std::vector<uint64_t> h((size_t)PQ_PROF_WG * PQ_PROF_N);
 			if (hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_pq_prof), h.size() * 8) != hipSuccess) return;

@@ -3060,15 +3060,30 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 		lo = s_hi + 1u;  // (finite keys < KEY_INF: no wrap)
 		for (int sp = 0; sp < ns; sp += CH) {
 			const int nr = min(CH, ns - sp);
-			// wave w refines candidates sp + w*PW .. (all its loads in flight together)
+			// wave w refines candidates sp + w*PW .. (all its loads in flight together);
+			// a small round of the ring instantiation (a later chunk: typically a
+			// few dozen rows) spreads PR_SMALL rows per wave over every wave with all
+			// its loads in flight (one memory latency, not one per column step)
+			constexpr int PR_SMALL = 8;
+			constexpr bool HAS_SMALL = PrGeom<METRIC, NI>::RING && PW > PR_SMALL && PrGeom<METRIC, NI>::NS <= 3;
+			const bool small = HAS_SMALL && nr <= PR_WAVES * PR_SMALL;
 			{
+				const int pw = small ? PR_SMALL : PW;
 				uint32_t sl[PW];
-				const int b0 = w * PW, nv = max(0, min(PW, nr - b0));
+				const int b0 = w * pw, nv = max(0, min(pw, nr - b0));
 #pragma unroll
 				for (int r = 0; r < PW; ++r) sl[r] = r < nv ? slots[sp + b0 + r] : 0u;
 				// this lane's label load in flight with the row loads
 				const int64_t lab = lane < nv ? labels[slots[sp + b0 + lane]] : 0;
-				const float dv = pr_distances<METRIC, T, PW, NI>(X, ld, sl, nv, qrow, qs, dim, lane);
+				float dv;
+				if constexpr (HAS_SMALL) {
+					if (small)
+						dv = pr_distances<METRIC, T, PR_SMALL, PrGeom<METRIC, NI>::NS>(X, ld, sl, nv, qrow, qs, dim, lane);
+					else
+						dv = pr_distances<METRIC, T, PW, NI>(X, ld, sl, nv, qrow, qs, dim, lane);
+				} else {
+					dv = pr_distances<METRIC, T, PW, NI>(X, ld, sl, nv, qrow, qs, dim, lane);
+				}
 				if (lane < nv) {
 					cd[cur][cnt + b0 + lane] = dv;
 					cl[cur][cnt + b0 + lane] = lab;
