@@ -84,3 +84,23 @@ def test_hot_kernels_do_not_spill():
     assert len(hot) >= 10, sorted(meta)[:20]
     spills = {k: v for k, v in meta.items() if k in hot and v[0] != 0}
     assert not spills, spills
+
+
+@pytest.mark.skipif(not OBJS or not os.path.exists(os.path.join(LLVM, "llvm-readelf")),
+                    reason="needs the built objects (make) and the ROCm LLVM tools")
+def test_release_objects_carry_no_scan8_ablations():
+    """The timing ablations of scan8_kernel (ABL != 0: no screen / no appends,
+    wrong results by design) are not instantiated in a release build: every
+    scan8_kernel<KS, D, RB, ABL, TM> of the built object has ABL == 0."""
+    import re
+
+    meta = {}
+    for obj in OBJS:
+        if os.path.basename(obj) == "scan8_kernels.o":
+            meta.update(_kernel_metadata(obj))
+    names = [k for k in meta if "scan8_kernel" in k]
+    assert names, sorted(meta)[:10]
+    for k in names:
+        m = re.search(r"scan8_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", k)
+        assert m, k
+        assert int(m.group(4)) == 0, k
