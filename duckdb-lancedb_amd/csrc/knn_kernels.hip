@@ -2952,6 +2952,28 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 			s_hi = 0;
 		}
 		__syncthreads();
+		if (!whole_range && R >= PR_SEL) {
+			// a later chunk that takes every key in range (R = the capacity): one
+			// appending pass, no histogram, unless the range holds more than a chunk
+			for (int i = t; i < n; i += PR_THREADS) {
+				const uint64_t e = keys[i];
+				const uint32_t kk = (uint32_t)(e >> 32);
+				if (kk >= lo && kk <= hi_goal && kk < KEY_INF) {
+					const unsigned p = atomicAdd(&s_ns, 1u);
+					if (p < (unsigned)PR_SEL) sel[p] = (uint32_t)e;
+					atomicMax(&s_hi, kk);
+				}
+			}
+			__syncthreads();
+			const unsigned cnt_in = s_ns;
+			if (cnt_in <= (unsigned)PR_SEL) return (int)cnt_in;
+			__syncthreads();
+			if (t == 0) {
+				s_ns = 0;
+				s_hi = 0;
+			}
+			__syncthreads();
+		}
 		if (!whole_range) {
 			unsigned kmn = 0xFFFFFFFFu, kmx = 0;
 			for (int i = t; i < n; i += PR_THREADS) {

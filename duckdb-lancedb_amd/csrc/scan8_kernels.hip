@@ -46,7 +46,6 @@
 namespace lhip {
 
 namespace {
-constexpr int QH = 128;               // queries per workgroup (half a SCAN_BQ tile)
 constexpr int LDS8 = 160 * 1024;      // one workgroup per CU
 constexpr int BIG = 1 << 30;          // row part of a dead row / query part that passes nothing
 constexpr int LIVE_MAX = 1 << 29;     // largest row part of a live row
@@ -93,10 +92,17 @@ __device__ __forceinline__ int s8_query_part(float4 qp, float4 ts, float W) {
 //
 // TM = 1: the SAMPLE pass instead (tilemin: row tile t of the launch is tile
 // tile0 + t * tstride): no threshold, the accumulators hold s; per work unit
-// (32 rows) and query the row of smallest bound, (orderedkey(LB), slot), goes
-// to the workgroup's segment (+inf / NaN bounds skipped): 8 entries per tile
-// and query for pool_refine's tau mode.
-template <int KS, int D, int RB, int ABL = 0, int TM = 0>
+// (32 rows) and query the row of smallest score alpha - s_T |S| s (the bound's
+// row-dependent terms), (orderedkey(score), slot), goes to the workgroup's
+// segment (dead rows skipped): 8 entries per tile and query from which
+// pool_refine's tau mode refines the k + 8 smallest exactly.
+//
+// QB: query blocks of 16 per workgroup.  8 (QH = 128 queries, pairs of
+// workgroups on a 256-query tile) for batches; 1 for a batch of at most 16
+// queries (the one-query-per-call pattern): 16 queries resident, 1/8 of the
+// MFMAs (a QB = 8 launch on one query multiplied 127 padding queries), and the
+// registers that frees hold a deeper row ring.
+template <int KS, int D, int RB, int ABL = 0, int TM = 0, int QB = 8>
 __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *__restrict__ Xq, const float4 *__restrict__ aux8,
                                                       const float4 *__restrict__ tstat, int ld,
                                                       const int8_t *__restrict__ Qi, const float4 *__restrict__ qaux,
@@ -105,6 +111,8 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
                                                       uint2 *__restrict__ seg_pool, int *__restrict__ seg_cnt,
                                                       int seg_cap, int list_cap, int tstride) {
 	static_assert(KS % D == 0 && KS % 2 == 0, "ring slot and fragment buffer of a k-step must be static");
+	static_assert(QB == 8 || QB == 1, "a 256-query tile is two QB = 8 halves; QB = 1 only for nq <= 16");
+	constexpr int QH = 16 * QB;                // queries per workgroup
 	constexpr int NW = 16 / RB, T8 = 64 * NW;  // waves: each owns 16 RB rows of every tile
 	constexpr int WR = 16 * RB;                // rows per wave and tile
 	constexpr int P = (KS * 64 + 255) / 256 * 256;  // LDS bytes per query row (XOR groups of 16 chunks)
@@ -123,7 +131,7 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 	// (a small batch, a rerun) every workgroup its own row group, all queries.
 	const int nb = (int)gridDim.x, b_id = (int)blockIdx.x;
 	const int q_tile = (int)blockIdx.y * SCAN_BQ;
-	const bool halves = nq - q_tile > QH;
+	const bool halves = QB == 8 && nq - q_tile > QH;
 	int h = 0, pr = b_id, NP = nb;
 	if (halves) {
 		NP = nb >> 1;
@@ -148,8 +156,8 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 	// one L2 round trip per 16 B chunk step: 12 of them at ld = 768, ~10 us)
 	{
 		constexpr int NCH = KS * 4;          // 16 B chunks per query row
-		constexpr int PER = QH * NCH / T8;   // chunks per thread
-		static_assert(QH * NCH % T8 == 0, "whole chunk steps per thread");
+		constexpr int PER = (QH * NCH + T8 - 1) / T8;  // chunks per thread
+		constexpr bool EVEN = QH * NCH % T8 == 0;
 		float4 qa = make_float4(0.f, 0.f, 0.f, 0.f);
 		float tq = -F_INF;
 		if (tid < QH) {
@@ -161,12 +169,12 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 #pragma unroll
 		for (int j = 0; j < PER; ++j) {
 			const int i = tid + j * T8, n = i / NCH, c = i - n * NCH;
-			v[j] = *reinterpret_cast<const i32x4 *>(Qi + (int64_t)(qb + n) * 2 * ld + 16 * c);
+			if (EVEN || i < QH * NCH) v[j] = *reinterpret_cast<const i32x4 *>(Qi + (int64_t)(qb + n) * 2 * ld + 16 * c);
 		}
 #pragma unroll
 		for (int j = 0; j < PER; ++j) {
 			const int i = tid + j * T8, n = i / NCH, c = i - n * NCH;
-			*reinterpret_cast<i32x4 *>(QL + n * P + ((c ^ (n & 15)) << 4)) = v[j];
+			if (EVEN || i < QH * NCH) *reinterpret_cast<i32x4 *>(QL + n * P + ((c ^ (n & 15)) << 4)) = v[j];
 		}
 		if (tid < QH) {
 			QA[tid] = qa;
@@ -177,7 +185,7 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 	if (tid == 0) *UCNT = (unsigned)NW;  // units 0 .. NW-1: one per wave, the rest claimed
 	__syncthreads();
 	// -S: the same for every query with a usable bound (0 for padding / zero cosine queries)
-	float Sabs = fmaxf(-QA[lane].x, -QA[lane + 64].x);
+	float Sabs = QH > 64 ? fmaxf(-QA[lane].x, -QA[lane + 64].x) : -QA[lane % QH].x;
 #pragma unroll
 	for (int o = 32; o > 0; o >>= 1) Sabs = fmaxf(Sabs, __shfl_xor(Sabs, o, 64));
 
@@ -275,7 +283,7 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 
 		// the query terms of queries lane and lane + 64 (this lane's query parts,
 		// handed to the accumulator lanes of column 16 u + lr by ds_bpermute)
-		const float4 qp0 = QP[lane], qp1 = QP[lane + 64];
+		const float4 qp0 = QP[lane % QH], qp1 = QH > 64 ? QP[lane + 64] : qp0;
 		int unit = w;                                        // this block's unit
 		int unext = __builtin_amdgcn_readfirstlane(claim()); // the next one (>= NU: none)
 		float an;
@@ -299,9 +307,9 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 			}
 		}
 		// query fragments, double-buffered: k-step j + 1's are read while k-step j multiplies
-		i32x4 bq[2][8];
+		i32x4 bq[2][QB];
 #pragma unroll
-		for (int q8 = 0; q8 < 8; ++q8) bq[0][q8] = bload(0, q8);
+		for (int q8 = 0; q8 < QB; ++q8) bq[0][q8] = bload(0, q8);
 
 #ifdef LHIP_S8_PROF
 		pf_t = __builtin_amdgcn_s_memtime();
@@ -314,17 +322,17 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 			aload(ux, an, tn);
 			const float W = (Sabs > 0.f && ts.x > 0.f) ? 1.0f / (Sabs * ts.x) : 0.f;
 			i32x4 bias[RB];
-			int gi[8];
+			int gi[QB];
 			if (TM) {  // the sample pass: plain s in the accumulators
 #pragma unroll
 				for (int rb = 0; rb < RB; ++rb) bias[rb] = i32x4{0, 0, 0, 0};
 #pragma unroll
-				for (int u = 0; u < 8; ++u) gi[u] = BIG;
+				for (int u = 0; u < QB; ++u) gi[u] = BIG;
 			} else if (ABL & 2) {
 #pragma unroll
 				for (int rb = 0; rb < RB; ++rb) bias[rb] = i32x4{rb, 1, 2, 3};
 #pragma unroll
-				for (int u = 0; u < 8; ++u) gi[u] = BIG - u;
+				for (int u = 0; u < QB; ++u) gi[u] = BIG - u;
 			} else {
 				const int bl = -s8_row_part(al, W);  // row lane % WR
 #pragma unroll
@@ -333,16 +341,16 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 					for (int i = 0; i < 4; ++i) bias[rb][i] = __builtin_amdgcn_ds_bpermute(4 * (16 * rb + 4 * lg + i), bl);
 				const int g0 = s8_query_part(qp0, ts, W), g1 = s8_query_part(qp1, ts, W);
 #pragma unroll
-				for (int u = 0; u < 8; ++u) gi[u] = __builtin_amdgcn_ds_bpermute(4 * ((16 * u + lr) & 63), u < 4 ? g0 : g1);
+				for (int u = 0; u < QB; ++u) gi[u] = __builtin_amdgcn_ds_bpermute(4 * ((16 * u + lr) & 63), u < 4 ? g0 : g1);
 			}
 
 			// accumulators start at -Bi (copies, then every MFMA accumulates in place:
 			// a bias operand shared by 8 MFMAs made the compiler rename them per k-step)
-			i32x4 acc[RB][8];
+			i32x4 acc[RB][QB];
 #pragma unroll
 			for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-				for (int u = 0; u < 8; ++u) acc[rb][u] = bias[rb];
+				for (int u = 0; u < QB; ++u) acc[rb][u] = bias[rb];
 			const int8_t *tb_cur = xunit(unit), *tb_next = xunit(ux);
 			S8_T(pf_pro);
 			if (ABL & 8) __builtin_amdgcn_s_setprio(2);  // the k-loop: MFMA issue first on the SIMD
@@ -351,9 +359,9 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 			for (int j = 0; j < KS; ++j) {
 				const int sl = j % D, cur = j & 1;  // (KS even: k-step 0 of the next block reads buffer 0)
 #pragma unroll
-				for (int u = 0; u < 8; ++u) bq[cur ^ 1][u] = bload((j + 1) % KS, u);
+				for (int u = 0; u < QB; ++u) bq[cur ^ 1][u] = bload((j + 1) % KS, u);
 #pragma unroll
-				for (int u = 0; u < 8; ++u) {
+				for (int u = 0; u < QB; ++u) {
 #pragma unroll
 					for (int rb = 0; rb < RB; ++rb)
 						acc[rb][u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xa[sl][rb], bq[cur][u], acc[rb][u], 0, 0, 0);
@@ -369,36 +377,35 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 			if (ABL & 8) __builtin_amdgcn_s_setprio(0);  // screen, appends, next terms: behind the partner's MFMAs
 
 			if (TM) {
-				// per query: the smallest bound of this unit's WR rows (this lane: rows
-				// 16 rb + 4 lg + i, query 16 u + lr; then across the four lane groups)
+				// per query: the row of smallest SCORE among this unit's WR rows (this
+				// lane: rows 16 rb + 4 lg + i, query 16 u + lr; then across the four
+				// lane groups).  The sample only picks which rows the tau-mode refine
+				// computes exactly (tau = the k-th exact distance among real rows is an
+				// upper bound whichever rows they are), so the score keeps the two terms
+				// that separate rows of one tile for one query: alpha - (s_T |S|) s
+				// (|S| is common to the batch, s_T to the tile; the error terms and C
+				// barely move within a tile): two instructions per bound, not six
 				const float *ra = reinterpret_cast<const float *>(aux8);
 				const int64_t rbase = utile(unit) * SCAN_BR + (int64_t)(WR * (unit % NW));
-				float4 t4[RB][4];
+				float4 al4[RB];
 #pragma unroll
-				for (int rb = 0; rb < RB; ++rb)
+				for (int rb = 0; rb < RB; ++rb) al4[rb] = *reinterpret_cast<const float4 *>(ra + raix(rbase + 16 * rb + 4 * lg, 0));
+				const float cs = -ts.x * Sabs;  // -(s_T |S|) (ts: this unit's tile terms)
 #pragma unroll
-					for (int c = 0; c < 4; ++c)
-						t4[rb][c] = *reinterpret_cast<const float4 *>(ra + raix(rbase + 16 * rb + 4 * lg, c));
-#pragma unroll
-				for (int u = 0; u < 8; ++u) {
-					const float4 qa = QA[16 * u + lr];
-					uint64_t best = ~0ull;
+				for (int u = 0; u < QB; ++u) {
+					float bv = F_INF;
+					int bi = 0;
 #pragma unroll
 					for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
 						for (int i = 0; i < 4; ++i) {
-							const float al = i == 0 ? t4[rb][0].x : i == 1 ? t4[rb][0].y : i == 2 ? t4[rb][0].z : t4[rb][0].w;
-							const float xn = i == 0 ? t4[rb][1].x : i == 1 ? t4[rb][1].y : i == 2 ? t4[rb][1].z : t4[rb][1].w;
-							const float uxv = i == 0 ? t4[rb][2].x : i == 1 ? t4[rb][2].y : i == 2 ? t4[rb][2].z : t4[rb][2].w;
-							const float sc = i == 0 ? t4[rb][3].x : i == 1 ? t4[rb][3].y : i == 2 ? t4[rb][3].z : t4[rb][3].w;
-							// LB as the append pass's flush evaluates it
-							float v = fmaf(xn, qa.z, al);
-							v = fmaf(uxv, qa.y, v);
-							v = fmaf((float)acc[rb][u][i] * sc, qa.x, v);
-							v = v + qa.w;
-							const uint64_t key = ((uint64_t)fkey(v) << 32) | (uint32_t)(rbase + 16 * rb + 4 * lg + i);
-							best = key < best ? key : best;
+							const float a_ = i == 0 ? al4[rb].x : i == 1 ? al4[rb].y : i == 2 ? al4[rb].z : al4[rb].w;
+							const float v = fmaf(cs, (float)acc[rb][u][i], a_);
+							const bool lt = v < bv;  // (+inf alpha: a dead row, never picked; NaN never less)
+							bv = lt ? v : bv;
+							bi = lt ? 16 * rb + i : bi;
 						}
+					uint64_t best = ((uint64_t)fkey(bv) << 32) | (uint32_t)(rbase + 4 * lg + bi);
 #pragma unroll
 					for (int o = 16; o < 64; o <<= 1) {
 						const uint64_t ob = ((uint64_t)(uint32_t)__shfl_xor((int)(best >> 32), o, 64) << 32) |
@@ -422,11 +429,11 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 			if (ABL & 1) {
 				int m = 0;
 #pragma unroll
-				for (int u = 0; u < 8; ++u) m ^= acc[0][u][0];
+				for (int u = 0; u < QB; ++u) m ^= acc[0][u][0];
 				hitm = m == 0x7fffffff ? 1 : 0;  // (keeps the MFMAs alive)
 			} else
 #pragma unroll
-			for (int u = 0; u < 8; ++u) {
+			for (int u = 0; u < QB; ++u) {
 				int m = max(max(acc[0][u][0], acc[0][u][1]), max(acc[0][u][2], acc[0][u][3]));
 #pragma unroll
 				for (int rb = 1; rb < RB; ++rb)
@@ -448,7 +455,7 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 				// rare: append every passing (s, slot, query) to the wave's list
 				const uint32_t row0 = (uint32_t)(utile(unit) * SCAN_BR) + (uint32_t)(WR * (unit % NW)) + 4u * lg;
 #pragma unroll
-				for (int u = 0; u < 8; ++u) {
+				for (int u = 0; u < QB; ++u) {
 					if (!__builtin_amdgcn_ballot_w64((hitm >> u) & 1)) continue;
 					// this query block's passing bounds (one ballot per accumulator
 					// register), then ONE list-room check: a flush site per u, not per
@@ -537,13 +544,13 @@ bool scan8_fits(const StoreView &s) {
 
 int scan8_segments(int64_t n_tiles) { return s8_groups(n_tiles); }
 
-static int s8_list_cap(int ld, int nw) {
+static int s8_list_cap(int ld, int nw, int qh) {
 	const int P = (ld + 255) / 256 * 256;
-	const int room = LDS8 - QH * P - QH * 36 - 16;  // QA, QP, CNT, the unit counter
+	const int room = LDS8 - qh * P - qh * 36 - 16;  // QA, QP, CNT, the unit counter
 	return std::min(1024, room / (nw * 9) / 64 * 64);
 }
 
-template <int KS, int D, int RB, int ABL = 0, int TM = 0>
+template <int KS, int D, int RB, int ABL = 0, int TM = 0, int QB = 8>
 static void s8_launch(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
                       int seg_cap, int64_t t0, int64_t n_tiles, int seg_base, hipStream_t st, int tstride = 1) {
 #ifndef LHIP_ABLATION_BUILD
@@ -551,9 +558,10 @@ static void s8_launch(const StoreView &s, const QueryView &q, const float *tau, 
 #endif
 	const dim3 grid((unsigned)s8_groups(n_tiles), (unsigned)(q.nq_pad / SCAN_BQ));
 	constexpr int NW = 16 / RB;
-	scan8_kernel<KS, D, RB, ABL, TM><<<grid, dim3(64 * NW), 0, st>>>(
+	if (QB < 8 && q.nq > 16 * QB) throw std::runtime_error("scan8: small-batch geometry on a larger batch");
+	scan8_kernel<KS, D, RB, ABL, TM, QB><<<grid, dim3(64 * NW), 0, st>>>(
 	    static_cast<const int8_t *>(s.Xscan), s.scan_aux, s.tstat, s.ld, reinterpret_cast<const int8_t *>(q.Qb), q.qaux,
-	    q.nq, (int)n_tiles, (int)t0, seg_base, tau, seg_pool, seg_cnt, seg_cap, s8_list_cap(s.ld, NW), tstride);
+	    q.nq, (int)n_tiles, (int)t0, seg_base, tau, seg_pool, seg_cnt, seg_cap, s8_list_cap(s.ld, NW, 16 * QB), tstride);
 }
 
 int scan8_tilemin_cap(int64_t n_tiles) {
@@ -572,6 +580,16 @@ void launch_scan8_tilemin(const StoreView &s, const QueryView &q, int64_t n_tile
 	if (q.nq_pad % SCAN_BQ) throw std::runtime_error("scan8: query tile padding");
 	if (seg_cap < scan8_tilemin_cap(n_tiles)) throw std::runtime_error("scan8 tilemin: segment capacity");
 	const int ts = (int)tile_stride;
+	if (q.nq <= 16) {  // QB = 1, the row ring a whole unit deep (KS <= 12)
+		switch (s.ld / 64) {
+		case 8: s8_launch<8, 8, 2, 0, 1, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
+		case 10: s8_launch<10, 10, 2, 0, 1, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
+		case 12: s8_launch<12, 12, 2, 0, 1, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
+		case 14: s8_launch<14, 7, 2, 0, 1, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
+		default: s8_launch<16, 8, 2, 0, 1, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
+		}
+		return;
+	}
 	switch (s.ld / 64) {
 	case 8: s8_launch<8, 4, 2, 0, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
 	case 10: s8_launch<10, 5, 2, 0, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
@@ -600,6 +618,16 @@ void launch_scan8_append(const StoreView &s, const QueryView &q, const float *ta
 	if (all_tiles * (int64_t)SCAN_BR > ((int64_t)1 << 32)) throw std::runtime_error("scan8: slots past 2^32");
 	if (q.nq_pad % SCAN_BQ) throw std::runtime_error("scan8: query tile padding");
 	if (!scan8_variant_ok(s.s8_variant)) throw std::runtime_error("scan8: geometry variant of a development build");
+	if (q.nq <= 16) {  // QB = 1 (the one-query-per-call pattern)
+		switch (s.ld / 64) {
+		case 8: s8_launch<8, 8, 2, 0, 0, 1>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		case 10: s8_launch<10, 10, 2, 0, 0, 1>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		case 12: s8_launch<12, 12, 2, 0, 0, 1>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		case 14: s8_launch<14, 7, 2, 0, 0, 1>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		default: s8_launch<16, 8, 2, 0, 0, 1>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
+		}
+		return;
+	}
 	switch (s.ld / 64) {
 	case 8: s8_launch<8, 4, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
 	case 10: s8_launch<10, 5, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;

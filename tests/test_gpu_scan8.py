@@ -55,6 +55,32 @@ def test_scan8_every_ld(hip, tmp_path, d, metric):
         hip.LanceFreeDetached(h)
 
 
+@pytest.mark.parametrize("metric", ["l2", "dot", "cosine"])
+@pytest.mark.parametrize("d", [512, 600, 768, 896, 1000])
+def test_scan8_small_batch_every_ld(hip, tmp_path, d, metric):
+    # at most 16 queries: the QB = 1 geometry (16 queries resident per workgroup,
+    # a whole-unit row ring) for the sample and the append pass; deletes, k = 1,
+    # 10 and 100 (a deeper pool per query), one query (lance_search's pattern)
+    rng = np.random.default_rng(1000 + d)
+    n = 75_000
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Q = rng.standard_normal((16, d)).astype(np.float32)
+    h = _mk(hip, tmp_path, d, metric)
+    try:
+        hip.LanceDetachedAddBatch(h, X, n, d)
+        dead = rng.choice(n, 3_000, replace=False)
+        hip.LanceDetachedDeleteBatch(h, dead)
+        live = np.ones(n, bool)
+        live[dead] = False
+        for nq, k in ((16, 10), (16, 100), (1, 10), (5, 1)):
+            gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q[:nq], k)
+            assert _ran_scan8(hip, h)
+            el, ed, ec = c_oracle.flat_search_batch(X, Q[:nq], k, metric, live=live, acc64=True, nthreads=16)
+            assert_same(gl, gd, gc, el, ed, ec)
+    finally:
+        hip.LanceFreeDetached(h)
+
+
 def _datasets(rng, n, d):
     yield "heavy", rng.standard_cauchy((n, d)).clip(-1e4, 1e4).astype(np.float32)
     spike = rng.standard_normal((n, d)).astype(np.float32) * 1e-3
