@@ -580,6 +580,7 @@ void launch_scan8_tilemin(const StoreView &s, const QueryView &q, int64_t n_tile
 	if (q.nq_pad % SCAN_BQ) throw std::runtime_error("scan8: query tile padding");
 	if (seg_cap < scan8_tilemin_cap(n_tiles)) throw std::runtime_error("scan8 tilemin: segment capacity");
 	const int ts = (int)tile_stride;
+#ifndef LHIP_S8_QB8_ONLY  // (A/B development builds: the 128-query geometry for every batch)
 	if (q.nq <= 16) {  // QB = 1, the row ring a whole unit deep (KS <= 12)
 		switch (s.ld / 64) {
 		case 8: s8_launch<8, 8, 2, 0, 1, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
@@ -590,6 +591,7 @@ void launch_scan8_tilemin(const StoreView &s, const QueryView &q, int64_t n_tile
 		}
 		return;
 	}
+#endif
 	switch (s.ld / 64) {
 	case 8: s8_launch<8, 4, 2, 0, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
 	case 10: s8_launch<10, 5, 2, 0, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
@@ -618,6 +620,7 @@ void launch_scan8_append(const StoreView &s, const QueryView &q, const float *ta
 	if (all_tiles * (int64_t)SCAN_BR > ((int64_t)1 << 32)) throw std::runtime_error("scan8: slots past 2^32");
 	if (q.nq_pad % SCAN_BQ) throw std::runtime_error("scan8: query tile padding");
 	if (!scan8_variant_ok(s.s8_variant)) throw std::runtime_error("scan8: geometry variant of a development build");
+#ifndef LHIP_S8_QB8_ONLY
 	if (q.nq <= 16) {  // QB = 1 (the one-query-per-call pattern)
 		switch (s.ld / 64) {
 		case 8: s8_launch<8, 8, 2, 0, 0, 1>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
@@ -628,6 +631,7 @@ void launch_scan8_append(const StoreView &s, const QueryView &q, const float *ta
 		}
 		return;
 	}
+#endif
 	switch (s.ld / 64) {
 	case 8: s8_launch<8, 4, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
 	case 10: s8_launch<10, 5, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;

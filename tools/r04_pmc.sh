@@ -18,7 +18,7 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
 	run c4 $ctr --config c4
 	run c5 $ctr --config c5
 done
-S8="scan8_kernel<12, 4, 2, 0, 0>"
+S8="scan8_kernel<12, 4, 2, 0, 0, 8>"
 python3 tools/pmc_traffic.py $O/pmc4_c2_FETCH_SIZE $O/pmc4_c2_WRITE_SIZE $O/r04_c2_scan_traffic.json --n 1000000 --dim 768 --batch 256 --elem-bytes 1 --kernel "$S8" --bench-kernel "scan8_kernel<L2,append,i8>"
 python3 tools/pmc_traffic.py $O/pmc4_nstar_FETCH_SIZE $O/pmc4_nstar_WRITE_SIZE $O/r04_nstar_scan_traffic.json --n 10000000 --dim 768 --batch 256 --elem-bytes 1 --kernel "$S8" --bench-kernel "scan8_kernel<L2,append,i8>"
 python3 tools/pmc_traffic.py $O/pmc4_c3_FETCH_SIZE $O/pmc4_c3_WRITE_SIZE $O/r04_c3_scan_traffic.json --n 10000000 --dim 768 --batch 256 --elem-bytes 1 --kernel "$S8" --bench-kernel "scan8_kernel<DOT,append,i8>"
