@@ -46,6 +46,7 @@
 namespace lhip {
 
 namespace {
+constexpr int QH = 128;               // queries per workgroup (half a SCAN_BQ tile)
 constexpr int LDS8 = 160 * 1024;      // one workgroup per CU
 constexpr int BIG = 1 << 30;          // row part of a dead row / query part that passes nothing
 constexpr int LIVE_MAX = 1 << 29;     // largest row part of a live row
@@ -96,13 +97,7 @@ __device__ __forceinline__ int s8_query_part(float4 qp, float4 ts, float W) {
 // row-dependent terms), (orderedkey(score), slot), goes to the workgroup's
 // segment (dead rows skipped): 8 entries per tile and query from which
 // pool_refine's tau mode refines the k + 8 smallest exactly.
-//
-// QB: query blocks of 16 per workgroup.  8 (QH = 128 queries, pairs of
-// workgroups on a 256-query tile) for batches; 1 for a batch of at most 16
-// queries (the one-query-per-call pattern): 16 queries resident, 1/8 of the
-// MFMAs (a QB = 8 launch on one query multiplied 127 padding queries), and the
-// registers that frees hold a deeper row ring.
-template <int KS, int D, int RB, int ABL = 0, int TM = 0, int QB = 8>
+template <int KS, int D, int RB, int ABL = 0, int TM = 0>
 __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *__restrict__ Xq, const float4 *__restrict__ aux8,
                                                       const float4 *__restrict__ tstat, int ld,
                                                       const int8_t *__restrict__ Qi, const float4 *__restrict__ qaux,
@@ -111,8 +106,6 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
                                                       uint2 *__restrict__ seg_pool, int *__restrict__ seg_cnt,
                                                       int seg_cap, int list_cap, int tstride) {
 	static_assert(KS % D == 0 && KS % 2 == 0, "ring slot and fragment buffer of a k-step must be static");
-	static_assert(QB == 8 || QB == 1, "a 256-query tile is two QB = 8 halves; QB = 1 only for nq <= 16");
-	constexpr int QH = 16 * QB;                // queries per workgroup
 	constexpr int NW = 16 / RB, T8 = 64 * NW;  // waves: each owns 16 RB rows of every tile
 	constexpr int WR = 16 * RB;                // rows per wave and tile
 	constexpr int P = (KS * 64 + 255) / 256 * 256;  // LDS bytes per query row (XOR groups of 16 chunks)
@@ -131,7 +124,7 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 	// (a small batch, a rerun) every workgroup its own row group, all queries.
 	const int nb = (int)gridDim.x, b_id = (int)blockIdx.x;
 	const int q_tile = (int)blockIdx.y * SCAN_BQ;
-	const bool halves = QB == 8 && nq - q_tile > QH;
+	const bool halves = nq - q_tile > QH;
 	int h = 0, pr = b_id, NP = nb;
 	if (halves) {
 		NP = nb >> 1;
@@ -156,8 +149,8 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 	// one L2 round trip per 16 B chunk step: 12 of them at ld = 768, ~10 us)
 	{
 		constexpr int NCH = KS * 4;          // 16 B chunks per query row
-		constexpr int PER = (QH * NCH + T8 - 1) / T8;  // chunks per thread
-		constexpr bool EVEN = QH * NCH % T8 == 0;
+		constexpr int PER = QH * NCH / T8;   // chunks per thread
+		static_assert(QH * NCH % T8 == 0, "whole chunk steps per thread");
 		float4 qa = make_float4(0.f, 0.f, 0.f, 0.f);
 		float tq = -F_INF;
 		if (tid < QH) {
@@ -169,12 +162,12 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 #pragma unroll
 		for (int j = 0; j < PER; ++j) {
 			const int i = tid + j * T8, n = i / NCH, c = i - n * NCH;
-			if (EVEN || i < QH * NCH) v[j] = *reinterpret_cast<const i32x4 *>(Qi + (int64_t)(qb + n) * 2 * ld + 16 * c);
+			v[j] = *reinterpret_cast<const i32x4 *>(Qi + (int64_t)(qb + n) * 2 * ld + 16 * c);
 		}
 #pragma unroll
 		for (int j = 0; j < PER; ++j) {
 			const int i = tid + j * T8, n = i / NCH, c = i - n * NCH;
-			if (EVEN || i < QH * NCH) *reinterpret_cast<i32x4 *>(QL + n * P + ((c ^ (n & 15)) << 4)) = v[j];
+			*reinterpret_cast<i32x4 *>(QL + n * P + ((c ^ (n & 15)) << 4)) = v[j];
 		}
 		if (tid < QH) {
 			QA[tid] = qa;
@@ -185,7 +178,7 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 	if (tid == 0) *UCNT = (unsigned)NW;  // units 0 .. NW-1: one per wave, the rest claimed
 	__syncthreads();
 	// -S: the same for every query with a usable bound (0 for padding / zero cosine queries)
-	float Sabs = QH > 64 ? fmaxf(-QA[lane].x, -QA[lane + 64].x) : -QA[lane % QH].x;
+	float Sabs = fmaxf(-QA[lane].x, -QA[lane + 64].x);
 #pragma unroll
 	for (int o = 32; o > 0; o >>= 1) Sabs = fmaxf(Sabs, __shfl_xor(Sabs, o, 64));
 
@@ -283,7 +276,7 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 
 		// the query terms of queries lane and lane + 64 (this lane's query parts,
 		// handed to the accumulator lanes of column 16 u + lr by ds_bpermute)
-		const float4 qp0 = QP[lane % QH], qp1 = QH > 64 ? QP[lane + 64] : qp0;
+		const float4 qp0 = QP[lane], qp1 = QP[lane + 64];
 		int unit = w;                                        // this block's unit
 		int unext = __builtin_amdgcn_readfirstlane(claim()); // the next one (>= NU: none)
 		float an;
@@ -307,9 +300,9 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 			}
 		}
 		// query fragments, double-buffered: k-step j + 1's are read while k-step j multiplies
-		i32x4 bq[2][QB];
+		i32x4 bq[2][8];
 #pragma unroll
-		for (int q8 = 0; q8 < QB; ++q8) bq[0][q8] = bload(0, q8);
+		for (int q8 = 0; q8 < 8; ++q8) bq[0][q8] = bload(0, q8);
 
 #ifdef LHIP_S8_PROF
 		pf_t = __builtin_amdgcn_s_memtime();
@@ -322,17 +315,17 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 			aload(ux, an, tn);
 			const float W = (Sabs > 0.f && ts.x > 0.f) ? 1.0f / (Sabs * ts.x) : 0.f;
 			i32x4 bias[RB];
-			int gi[QB];
+			int gi[8];
 			if (TM) {  // the sample pass: plain s in the accumulators
 #pragma unroll
 				for (int rb = 0; rb < RB; ++rb) bias[rb] = i32x4{0, 0, 0, 0};
 #pragma unroll
-				for (int u = 0; u < QB; ++u) gi[u] = BIG;
+				for (int u = 0; u < 8; ++u) gi[u] = BIG;
 			} else if (ABL & 2) {
 #pragma unroll
 				for (int rb = 0; rb < RB; ++rb) bias[rb] = i32x4{rb, 1, 2, 3};
 #pragma unroll
-				for (int u = 0; u < QB; ++u) gi[u] = BIG - u;
+				for (int u = 0; u < 8; ++u) gi[u] = BIG - u;
 			} else {
 				const int bl = -s8_row_part(al, W);  // row lane % WR
 #pragma unroll
@@ -341,16 +334,16 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 					for (int i = 0; i < 4; ++i) bias[rb][i] = __builtin_amdgcn_ds_bpermute(4 * (16 * rb + 4 * lg + i), bl);
 				const int g0 = s8_query_part(qp0, ts, W), g1 = s8_query_part(qp1, ts, W);
 #pragma unroll
-				for (int u = 0; u < QB; ++u) gi[u] = __builtin_amdgcn_ds_bpermute(4 * ((16 * u + lr) & 63), u < 4 ? g0 : g1);
+				for (int u = 0; u < 8; ++u) gi[u] = __builtin_amdgcn_ds_bpermute(4 * ((16 * u + lr) & 63), u < 4 ? g0 : g1);
 			}
 
 			// accumulators start at -Bi (copies, then every MFMA accumulates in place:
 			// a bias operand shared by 8 MFMAs made the compiler rename them per k-step)
-			i32x4 acc[RB][QB];
+			i32x4 acc[RB][8];
 #pragma unroll
 			for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-				for (int u = 0; u < QB; ++u) acc[rb][u] = bias[rb];
+				for (int u = 0; u < 8; ++u) acc[rb][u] = bias[rb];
 			const int8_t *tb_cur = xunit(unit), *tb_next = xunit(ux);
 			S8_T(pf_pro);
 			if (ABL & 8) __builtin_amdgcn_s_setprio(2);  // the k-loop: MFMA issue first on the SIMD
@@ -359,9 +352,9 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 			for (int j = 0; j < KS; ++j) {
 				const int sl = j % D, cur = j & 1;  // (KS even: k-step 0 of the next block reads buffer 0)
 #pragma unroll
-				for (int u = 0; u < QB; ++u) bq[cur ^ 1][u] = bload((j + 1) % KS, u);
+				for (int u = 0; u < 8; ++u) bq[cur ^ 1][u] = bload((j + 1) % KS, u);
 #pragma unroll
-				for (int u = 0; u < QB; ++u) {
+				for (int u = 0; u < 8; ++u) {
 #pragma unroll
 					for (int rb = 0; rb < RB; ++rb)
 						acc[rb][u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xa[sl][rb], bq[cur][u], acc[rb][u], 0, 0, 0);
@@ -392,7 +385,7 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 				for (int rb = 0; rb < RB; ++rb) al4[rb] = *reinterpret_cast<const float4 *>(ra + raix(rbase + 16 * rb + 4 * lg, 0));
 				const float cs = -ts.x * Sabs;  // -(s_T |S|) (ts: this unit's tile terms)
 #pragma unroll
-				for (int u = 0; u < QB; ++u) {
+				for (int u = 0; u < 8; ++u) {
 					float bv = F_INF;
 					int bi = 0;
 #pragma unroll
@@ -429,11 +422,11 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 			if (ABL & 1) {
 				int m = 0;
 #pragma unroll
-				for (int u = 0; u < QB; ++u) m ^= acc[0][u][0];
+				for (int u = 0; u < 8; ++u) m ^= acc[0][u][0];
 				hitm = m == 0x7fffffff ? 1 : 0;  // (keeps the MFMAs alive)
 			} else
 #pragma unroll
-			for (int u = 0; u < QB; ++u) {
+			for (int u = 0; u < 8; ++u) {
 				int m = max(max(acc[0][u][0], acc[0][u][1]), max(acc[0][u][2], acc[0][u][3]));
 #pragma unroll
 				for (int rb = 1; rb < RB; ++rb)
@@ -455,7 +448,7 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 				// rare: append every passing (s, slot, query) to the wave's list
 				const uint32_t row0 = (uint32_t)(utile(unit) * SCAN_BR) + (uint32_t)(WR * (unit % NW)) + 4u * lg;
 #pragma unroll
-				for (int u = 0; u < QB; ++u) {
+				for (int u = 0; u < 8; ++u) {
 					if (!__builtin_amdgcn_ballot_w64((hitm >> u) & 1)) continue;
 					// this query block's passing bounds (one ballot per accumulator
 					// register), then ONE list-room check: a flush site per u, not per
@@ -544,13 +537,13 @@ bool scan8_fits(const StoreView &s) {
 
 int scan8_segments(int64_t n_tiles) { return s8_groups(n_tiles); }
 
-static int s8_list_cap(int ld, int nw, int qh) {
+static int s8_list_cap(int ld, int nw) {
 	const int P = (ld + 255) / 256 * 256;
-	const int room = LDS8 - qh * P - qh * 36 - 16;  // QA, QP, CNT, the unit counter
+	const int room = LDS8 - QH * P - QH * 36 - 16;  // QA, QP, CNT, the unit counter
 	return std::min(1024, room / (nw * 9) / 64 * 64);
 }
 
-template <int KS, int D, int RB, int ABL = 0, int TM = 0, int QB = 8>
+template <int KS, int D, int RB, int ABL = 0, int TM = 0>
 static void s8_launch(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
                       int seg_cap, int64_t t0, int64_t n_tiles, int seg_base, hipStream_t st, int tstride = 1) {
 #ifndef LHIP_ABLATION_BUILD
@@ -558,10 +551,9 @@ static void s8_launch(const StoreView &s, const QueryView &q, const float *tau, 
 #endif
 	const dim3 grid((unsigned)s8_groups(n_tiles), (unsigned)(q.nq_pad / SCAN_BQ));
 	constexpr int NW = 16 / RB;
-	if (QB < 8 && q.nq > 16 * QB) throw std::runtime_error("scan8: small-batch geometry on a larger batch");
-	scan8_kernel<KS, D, RB, ABL, TM, QB><<<grid, dim3(64 * NW), 0, st>>>(
+	scan8_kernel<KS, D, RB, ABL, TM><<<grid, dim3(64 * NW), 0, st>>>(
 	    static_cast<const int8_t *>(s.Xscan), s.scan_aux, s.tstat, s.ld, reinterpret_cast<const int8_t *>(q.Qb), q.qaux,
-	    q.nq, (int)n_tiles, (int)t0, seg_base, tau, seg_pool, seg_cnt, seg_cap, s8_list_cap(s.ld, NW, 16 * QB), tstride);
+	    q.nq, (int)n_tiles, (int)t0, seg_base, tau, seg_pool, seg_cnt, seg_cap, s8_list_cap(s.ld, NW), tstride);
 }
 
 int scan8_tilemin_cap(int64_t n_tiles) {
@@ -580,18 +572,6 @@ void launch_scan8_tilemin(const StoreView &s, const QueryView &q, int64_t n_tile
 	if (q.nq_pad % SCAN_BQ) throw std::runtime_error("scan8: query tile padding");
 	if (seg_cap < scan8_tilemin_cap(n_tiles)) throw std::runtime_error("scan8 tilemin: segment capacity");
 	const int ts = (int)tile_stride;
-#ifndef LHIP_S8_QB8_ONLY  // (A/B development builds: the 128-query geometry for every batch)
-	if (q.nq <= 16) {  // QB = 1, the row ring a whole unit deep (KS <= 12)
-		switch (s.ld / 64) {
-		case 8: s8_launch<8, 8, 2, 0, 1, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
-		case 10: s8_launch<10, 10, 2, 0, 1, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
-		case 12: s8_launch<12, 12, 2, 0, 1, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
-		case 14: s8_launch<14, 7, 2, 0, 1, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
-		default: s8_launch<16, 8, 2, 0, 1, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
-		}
-		return;
-	}
-#endif
 	switch (s.ld / 64) {
 	case 8: s8_launch<8, 4, 2, 0, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
 	case 10: s8_launch<10, 5, 2, 0, 1>(s, q, nullptr, seg_pool, seg_cnt, seg_cap, 0, n_tiles, 0, st, ts); break;
@@ -620,18 +600,6 @@ void launch_scan8_append(const StoreView &s, const QueryView &q, const float *ta
 	if (all_tiles * (int64_t)SCAN_BR > ((int64_t)1 << 32)) throw std::runtime_error("scan8: slots past 2^32");
 	if (q.nq_pad % SCAN_BQ) throw std::runtime_error("scan8: query tile padding");
 	if (!scan8_variant_ok(s.s8_variant)) throw std::runtime_error("scan8: geometry variant of a development build");
-#ifndef LHIP_S8_QB8_ONLY
-	if (q.nq <= 16) {  // QB = 1 (the one-query-per-call pattern)
-		switch (s.ld / 64) {
-		case 8: s8_launch<8, 8, 2, 0, 0, 1>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
-		case 10: s8_launch<10, 10, 2, 0, 0, 1>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
-		case 12: s8_launch<12, 12, 2, 0, 0, 1>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
-		case 14: s8_launch<14, 7, 2, 0, 0, 1>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
-		default: s8_launch<16, 8, 2, 0, 0, 1>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
-		}
-		return;
-	}
-#endif
 	switch (s.ld / 64) {
 	case 8: s8_launch<8, 4, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;
 	case 10: s8_launch<10, 5, 2>(s, q, tau, seg_pool, seg_cnt, seg_cap, t0, n_tiles, seg_base, st); break;

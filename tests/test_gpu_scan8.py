@@ -58,9 +58,10 @@ def test_scan8_every_ld(hip, tmp_path, d, metric):
 @pytest.mark.parametrize("metric", ["l2", "dot", "cosine"])
 @pytest.mark.parametrize("d", [512, 600, 768, 896, 1000])
 def test_scan8_small_batch_every_ld(hip, tmp_path, d, metric):
-    # at most 16 queries: the QB = 1 geometry (16 queries resident per workgroup,
-    # a whole-unit row ring) for the sample and the append pass; deletes, k = 1,
-    # 10 and 100 (a deeper pool per query), one query (lance_search's pattern)
+    # at most 16 queries (no halves: every workgroup its own row group, the
+    # padding queries of its 128 pass nothing) for the sample and the append
+    # pass; deletes, k = 1, 10 and 100 (a deeper pool per query), one query
+    # (lance_search's pattern)
     rng = np.random.default_rng(1000 + d)
     n = 75_000
     X = rng.standard_normal((n, d)).astype(np.float32)

@@ -13,8 +13,7 @@ allocation that reintroduces the hazard fails this test.
 
 The release build carries no scan8 timing ablation: every scan8_kernel
 instantiation in the code object has ABL = 0 and the ld = 768 default geometry
-<12, 4, 2> for batches (QB = 8), <12, 12, 2> for at most 16 queries (QB = 1)
-(the wrong-result variants exist only in LHIP_ABLATION_BUILD builds)."""
+<12, 4, 2> (the wrong-result variants exist only in LHIP_ABLATION_BUILD builds)."""
 import re
 import glob
 import os
@@ -40,11 +39,10 @@ def test_no_valu_write_into_a_live_mfma_operand():
     assert any(ln.startswith("knn_kernels.o") for ln in kernels_with_mfma), r.stdout
     assert any(ln.startswith("ivf_kernels.o") for ln in kernels_with_mfma), r.stdout
     # release scan8 instantiations: ABL = 0 only, ld = 768 only the default geometry
-    s8 = set(re.findall(r"scan8_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", r.stdout))
+    s8 = set(re.findall(r"scan8_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", r.stdout))
     assert s8, r.stdout[-2000:]
-    assert all(abl == "0" for (_, _, _, abl, _, _) in s8), sorted(s8)
-    assert {(d, rb) for (ks, d, rb, _, _, qb) in s8 if ks == "12" and qb == "8"} == {("4", "2")}, sorted(s8)
-    assert {(d, rb) for (ks, d, rb, _, _, qb) in s8 if ks == "12" and qb == "1"} == {("12", "2")}, sorted(s8)
+    assert all(abl == "0" for (_, _, _, abl) in s8), sorted(s8)
+    assert {(d, rb) for (ks, d, rb, _) in s8 if ks == "12"} == {("4", "2")}, sorted(s8)
 
 
 def _kernel_metadata(obj):
@@ -93,7 +91,7 @@ def test_hot_kernels_do_not_spill():
 def test_release_objects_carry_no_scan8_ablations():
     """The timing ablations of scan8_kernel (ABL != 0: no screen / no appends,
     wrong results by design) are not instantiated in a release build: every
-    scan8_kernel<KS, D, RB, ABL, TM, QB> of the built object has ABL == 0."""
+    scan8_kernel<KS, D, RB, ABL, TM> of the built object has ABL == 0."""
     import re
 
     meta = {}
@@ -103,6 +101,6 @@ def test_release_objects_carry_no_scan8_ablations():
     names = [k for k in meta if "scan8_kernel" in k]
     assert names, sorted(meta)[:10]
     for k in names:
-        m = re.search(r"scan8_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", k)
+        m = re.search(r"scan8_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", k)
         assert m, k
         assert int(m.group(4)) == 0, k
