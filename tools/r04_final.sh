@@ -3,7 +3,7 @@
 # driver's bench command, its rocprofv3 kernel stats, north_star / C3 lines, per-rank shapes
 source tools/gpu_step.sh
 T=${1:-r04z}
-step ${T}_pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+step ${T}_pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 step ${T}_smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"
 step ${T}_bench_c2 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
 step ${T}_prof_c2 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof_c2 -o run -- python3 bench.py --steps 20 --no-cpu-baseline --no-recall --no-host-batch
