@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4: one query per call A/B (scan8 QB = 1 geometry vs the 128-query geometry, same box,
-# (lib_qb8.so was a development build of a 16-query scan8 geometry, measured slower and since removed)
 # interleaved), then the C3 and C4 lines of the validated tree
+# (lib_qb8.so was a development build of a 16-query scan8 geometry, measured slower and since removed)
 source tools/gpu_step.sh
 T=${1:-r04u}
 QB8=duckdb-lancedb_amd/lib_dev/lib_qb8.so
