@@ -2065,6 +2065,7 @@ __global__ __launch_bounds__(256) void pq_seed_kernel(const uint8_t *__restrict_
 	const int q = blockIdx.x, t = threadIdx.x;
 	const int mm = MT > 0 ? MT : m;
 	const int64_t l = probe_l[(int64_t)q * nprobe];
+	if (l < 0) return;  // no probed list (a NaN query): no seed; the whole block leaves before any barrier
 	const float d0 = probe_d[(int64_t)q * nprobe];
 	const float2 qp = qpar[q];
 	const uint8_t *lq = lut8 + (int64_t)q * mm * PQ_K;
