@@ -148,6 +148,20 @@ def test_c5_ivf_pq_m96_refine_sweep(hip, data, exact):
         hip.LanceHipSetOption(h, "pq_seed", "1")
         for a, b in zip(g_seed, g_noseed):
             np.testing.assert_array_equal(a, b)
+        # a NaN query (no probed list: the seed skips it) and a zero query in the
+        # batch: seeded == unseeded, and the other queries keep their lists
+        Qx = Q.copy()
+        Qx[3] = np.nan
+        Qx[5] = 0.0
+        gx = hip.LanceDetachedSearchBatch(h, Qx, K, nprobes=NPROBE, refine_factor=10)
+        hip.LanceHipSetOption(h, "pq_seed", "0")
+        gx0 = hip.LanceDetachedSearchBatch(h, Qx, K, nprobes=NPROBE, refine_factor=10)
+        hip.LanceHipSetOption(h, "pq_seed", "1")
+        for a, b in zip(gx, gx0):
+            np.testing.assert_array_equal(a, b)
+        keep = np.setdiff1d(np.arange(len(Q)), [3, 5])
+        for a, b in zip(gx, g_seed):
+            np.testing.assert_array_equal(a[keep], b[keep])
         hip.LanceHipSetOption(h, "pq_query", "fp8")
         gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, K, nprobes=NPROBE, refine_factor=10)
         check(gl, gd, gc, *port_search(hip, h, X, Q, NPROBE, 10, query_fp8=True))
