@@ -433,6 +433,13 @@ struct Index {
 		return scan_i8 && X && n_slots > 0 && ld % 128 == 0 && ld <= 1024 && !filter_on &&
 		       !(metric_quirk && metric != METRIC_L2);
 	}
+	// whether a flat search of nq queries for k streams the int8 copy: any k on
+	// the threshold path (pool_refine refines as far as its certificate needs),
+	// k <= 32 on the dense path of small stores (a fixed candidate count)
+	bool scan_uses_i8(int nq, int k) const {
+		(void)nq;
+		return i8_usable() && (k <= 32 || (n_slots > 65536 && k + 8 <= MAX_CAND));
+	}
 	// (re)build the int8 scan copy and its row terms from X when stale
 	void ensure_i8() {
 		if (Xq && q8_ver == mut_ver && q8_cap == cap) return;

@@ -79,7 +79,7 @@ bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *d
 	// needs); k <= 32 on the dense path of small stores (a fixed candidate count:
 	// past that the looser bounds leave more rows below the k-th distance than
 	// it holds); otherwise bf16 rows
-	const bool use8 = i8_usable() && (k <= 32 || (n_slots > 65536 && k + 8 <= MAX_CAND));
+	const bool use8 = scan_uses_i8(nq, k);
 	if (!use8) ensure_xs();
 	const float mu = (metric_quirk && metric != METRIC_L2) ? max_ux_l2 : max_ux;
 	StoreView sv{X, aux, dlabels, n_slots, ld, dim, eff_metric, xbf16 ? 1 : 0,
@@ -212,8 +212,10 @@ bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *d
 		const size_t pool_a = (size_t)n_seg * nq * seg_cap + (size_t)n_seg * (nq_pad / SCAN_BQ);  // + per-workgroup sink
 		const size_t cnt_n = (size_t)std::max(n_seg_s, n_seg) * nq;
 		// kernels of a pending pass read seg_pool / seg_cnt: grow them only once it is done
-		if (async && !pending.empty() && (ws.seg_pool.n < std::max(pool_s, pool_a) || ws.seg_cnt.n < cnt_n))
+		if (async && !pending.empty() && (ws.seg_pool.n < std::max(pool_s, pool_a) || ws.seg_cnt.n < cnt_n)) {
 			drain();
+			for (auto &v : last_stats) v = 0;  // (the drained passes' statistics are not this pass's)
+		}
 		ws.seg_pool.need(std::max(pool_s, pool_a));
 		ws.seg_cnt.need(cnt_n);
 		if (s8s)
@@ -468,10 +470,12 @@ int64_t Index::search_async(const float *dQ, int nq, int k, int nprobes, int ref
 		return ticket;
 	}
 	while (pending.size() >= 2) finish_oldest();
-	// a stale int8 copy / missing scan copy is rebuilt in place: not under pending passes
-	if (!pending.empty() && ((i8_usable() && !(Xq && q8_ver == mut_ver && q8_cap == cap)) ||
-	                         (has_scan_copy() && !Xs)))
-		drain();
+	// a stale int8 copy / missing scan copy is rebuilt in place: not under pending
+	// passes (only the copy this search will stream: enqueue_chunk's choice)
+	if (!pending.empty()) {
+		const bool use8 = scan_uses_i8(nq, k);
+		if ((use8 && !(Xq && q8_ver == mut_ver && q8_cap == cap)) || (!use8 && has_scan_copy() && !Xs)) drain();
+	}
 	for (auto &v : last_stats) v = 0;
 	PendingPass p;
 	const int slot = pb_free_slot();
@@ -1190,6 +1194,7 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 	try {
 		Index *ix = as_index(handle);
 		std::lock_guard<std::mutex> g(ix->mu);
+		ix->bind();  // every pending asynchronous search completes under the options it was enqueued with
 		std::string k = cstr(key), v = cstr(value);
 		if (k == "metric_quirk") {
 			bool on = (v == "1" || v == "true");

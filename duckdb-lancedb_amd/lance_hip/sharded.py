@@ -131,7 +131,14 @@ class AsyncPipeline:
     ``step(Q, k)`` enqueues a batch and completes the previous one (certificate
     check, reruns, fallbacks at its wait), so the host's per-batch work overlaps
     the device's; ``drain()`` completes the last.  Returns the outputs of the
-    batch completed by the call (None on the first)."""
+    batch completed by the call (None on the first).
+
+    The pipeline holds each submitted query tensor until its batch completes
+    (the library reads it on its own stream, behind the previous pass, so a
+    temporary must not go back to torch's allocator before the wait).  Output
+    tensors are double-buffered per shape: the tensors a wait returns stay valid
+    until the next-but-one ``submit`` of the same shape (clone them to keep
+    them longer)."""
 
     def __init__(self, lib, handle, dim: int, nprobes: int = 20, refine_factor: int = 1, err_len: int = 2048):
         import ctypes
@@ -141,7 +148,8 @@ class AsyncPipeline:
         self.e = ctypes.create_string_buffer(err_len)
         self.err_len = err_len
         self.outs = {}
-        self.pending = []  # (ticket, outputs)
+        self.completed = {}
+        self.pending = []  # (ticket, outputs, query tensor held until the wait)
         self.i = 0
 
     def _out(self, nq, k, dev, j):
@@ -168,15 +176,22 @@ class AsyncPipeline:
                                                          self.e, self.err_len)
         if t < 0:
             raise RuntimeError(self.e.value.decode())
-        self.pending.append((t, o))
+        self.pending.append((t, o, Q))
         return t
 
     def wait(self, ticket=0):
+        """Completes every batch up to ``ticket`` (<= 0: all) and returns the
+        outputs of batch ``ticket`` (of the last completed one for <= 0);
+        ``completed`` maps the ticket of every batch this call completed to its
+        outputs."""
         if self.lib.lance_hip_search_wait(self.h, ticket, self.e, self.err_len) != 0:
             raise RuntimeError(self.e.value.decode())
         done = [p for p in self.pending if ticket <= 0 or p[0] <= ticket]
         self.pending = [p for p in self.pending if not (ticket <= 0 or p[0] <= ticket)]
-        return done[-1][1] if done else None
+        self.completed = {p[0]: p[1] for p in done}
+        if not done:
+            return None
+        return self.completed.get(ticket, done[-1][1]) if ticket > 0 else done[-1][1]
 
     def step(self, Q, k):
         prev = self.pending[-1][0] if self.pending else None

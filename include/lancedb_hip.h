@@ -284,8 +284,10 @@ int32_t lance_hip_search_batch_device(void *handle, const float *d_queries, int3
  * returns for that ticket.  d_queries must be ready on entry (stream-ordered
  * before the call); it and the outputs must stay valid until the wait.  At
  * most two searches are in flight per handle (a third call first completes
- * the oldest); any other call on the handle (search, add, delete, options,
- * ...) first completes every pending one.  Searches that are not a single
+ * the oldest); every other call that touches the device or the handle's
+ * options (search, add, delete, compact, create_index, get_vector,
+ * lance_hip_set_option, ...) first completes every pending one; count,
+ * dimension and the statistics getters only read host state.  Searches that are not a single
  * threshold-path pass (IVF, predicate, small stores, > 2048 queries, option
  * time_kernels) run synchronously inside the call. */
 int64_t lance_hip_search_batch_device_async(void *handle, const float *d_queries, int32_t nq, int32_t dim, int32_t k,

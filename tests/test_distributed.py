@@ -264,8 +264,12 @@ def _gpu_scan8_worker(rank, world, port, n, d, k, q, out, pipelined=False):
         ap = AsyncPipeline(L, h, d)
 
         class _Pipe:
+            held = []  # the device queries stay alive until their batch completes (AsyncPipeline holds them too)
+
             def submit(self, Qt, kk):
-                return ap.submit(Qt.cuda(), kk)
+                Qd = Qt.cuda()
+                self.held = (self.held + [Qd])[-3:]
+                return ap.submit(Qd, kk)
 
             def wait(self, t):
                 return tuple(x.cpu() for x in ap.wait(t))

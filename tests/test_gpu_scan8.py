@@ -327,10 +327,12 @@ def test_async_pipeline_matches_sync(hip):
         t = [pipe.submit(Qd[i], k) for i in range(3)]  # the third submit completes the first
         assert t[0] < t[1] < t[2]
         outs = {}
-        for i in (1, 2):
-            o = pipe.wait(t[i])
-            outs[i] = tuple(x.cpu().numpy() for x in o)
-        for i in (1, 2):
+        o = pipe.wait(t[1])  # completes batches 0 (already finished inside the third submit) and 1
+        assert set(pipe.completed) == {t[0], t[1]} and o is pipe.completed[t[1]]
+        outs[0] = tuple(x.cpu().numpy() for x in pipe.completed[t[0]])
+        outs[1] = tuple(x.cpu().numpy() for x in o)
+        outs[2] = tuple(x.cpu().numpy() for x in pipe.wait(t[2]))
+        for i in (0, 1, 2):
             assert_same(*outs[i], *exp[i])
         # a pending search, then an append: the append first completes it
         t3 = pipe.submit(Qd[3], k)
@@ -338,14 +340,82 @@ def test_async_pipeline_matches_sync(hip):
         hip.LanceDetachedAddBatch(h, X[100_000:], n - 100_000, d)
         pipe.wait(t3)
         assert_same(*(x.cpu().numpy() for x in o3), *exp[3])
-        # after the append: pipelined steps over the whole store == synchronous search
+        # after the append: pipelined steps over the whole store, a different batch
+        # each step (outputs copied out before the next-but-one submit reuses them)
         e0 = c_oracle.flat_search_batch(X, Qs[0], k, "l2", acc64=True, nthreads=16)
-        res = [pipe.step(Qd[0], k) for _ in range(4)]
-        last = pipe.drain()
-        for r in [x for x in res if x is not None] + [last]:
-            assert_same(*(x.cpu().numpy() for x in r), *e0)
+        Qr = Qd[0].flip(0).contiguous()
+        er = tuple(a[::-1] for a in e0)
+        steps = [Qd[0], Qr, Qd[0], Qr, Qd[0]]
+        got = []
+        for Qi in steps:
+            r = pipe.step(Qi, k)
+            if r is not None:
+                got.append(tuple(x.cpu().numpy() for x in r))
+        got.append(tuple(x.cpu().numpy() for x in pipe.drain()))
+        assert len(got) == len(steps)
+        for i, r in enumerate(got):
+            assert_same(*r, *(e0 if i % 2 == 0 else er))
         assert_same(*(x.cpu().numpy() for x in sync(Qd[0], k)), *e0)
         st = hip.LanceHipLastSearchStats(h)
         assert st["fallback_queries"] == 0 and st["append_launches"] == 1, st
+    finally:
+        hip.LanceFreeDetached(h)
+
+
+def test_async_rerun_and_fallback_with_next_pass_in_flight(hip):
+    """pass A's completion (reruns of uncertified queries and the
+    exact fallback, lance_hip_abi.cpp finish_chunk) runs while pass B is still
+    queued behind it on the handle's stream and shares the workspace (segment
+    pools, rerun / fallback buffers).  Cosine store; A holds three queries whose
+    neighbours sit packed in a tile the sample pass skips (their first pass
+    overflows a segment: rerun), one query equal to 200 duplicate rows and one
+    zero query (NaN distances: the exact fallback); B and C are plain batches,
+    C enqueued into A's pass buffers while B is pending.  Every batch equals the
+    f64 oracle, A's statistics equal those of the same batch run synchronously
+    (reruns and a fallback), and pass B really was in flight during A's wait."""
+    import torch
+    from lance_hip.sharded import AsyncPipeline
+
+    rng = np.random.default_rng(505)
+    n, d, k = 120_000, 128, 10
+    X = rng.standard_normal((n, d), dtype=np.float32)
+    q0 = rng.standard_normal(d).astype(np.float32)
+    dirs = rng.standard_normal((256, d))
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    X[256:512] = q0 + np.sqrt(rng.uniform(0, 60, 256))[:, None] * dirs
+    q1 = rng.standard_normal(d).astype(np.float32)
+    X[1000:1200] = q1
+    ZERO = 4
+    QA = np.concatenate([q0 + 0.01 * rng.standard_normal((3, d)), q1[None, :], np.zeros((1, d)),
+                         rng.standard_normal((60, d))]).astype(np.float32)
+    QB = rng.standard_normal((256, d), dtype=np.float32)
+    QC = rng.standard_normal((40, d), dtype=np.float32)
+    keep = np.arange(len(QA)) != ZERO
+    h = hip.LanceCreateDetached("", d, "cosine", "t")
+    try:
+        hip.LanceDetachedAddBatch(h, X, n, d)
+        hip.LanceHipSetOption(h, "sample_div", "100000")  # the sample skips tile 1
+        exp = [c_oracle.flat_search_batch(X, q, k, "cosine", acc64=True, nthreads=16) for q in (QA[keep], QB, QC)]
+        sync = hip.LanceDetachedSearchBatch(h, QA, k)
+        stS = hip.LanceHipLastSearchStats(h)
+        assert stS["retried_queries"] >= 1 and stS["fallback_queries"] >= 1, stS
+        assert_same(*hip.LanceDetachedSearchBatch(h, QB, k), *exp[1])  # (workspace sized for B: no drain at its submit)
+        pipe = AsyncPipeline(hip.lib(), h, d)
+        tA = pipe.submit(torch.from_numpy(QA).cuda(), k)
+        tB = pipe.submit(torch.from_numpy(QB).cuda(), k)  # B queued behind A
+        oA = tuple(x.cpu().numpy() for x in pipe.wait(tA))  # A's reruns + fallback, B still in flight
+        stA = hip.LanceHipLastSearchStats(h)
+        tC = pipe.submit(torch.from_numpy(QC).cuda(), k)  # C takes A's pass buffers while B is pending
+        oB = tuple(x.cpu().numpy() for x in pipe.wait(tB))
+        oC = tuple(x.cpu().numpy() for x in pipe.wait(tC))
+        stC = hip.LanceHipLastSearchStats(h)
+        assert stA == stS, (stA, stS)
+        assert stC["fallback_queries"] == 0, stC
+        for got in (sync, oA):
+            assert_same(got[0][keep], got[1][keep], got[2][keep], *exp[0])
+            assert got[2][ZERO] == k
+            assert list(got[0][3]) == list(range(1000, 1010)) and (np.abs(got[1][3]) < 1e-6).all()
+        assert_same(*oB, *exp[1])
+        assert_same(*oC, *exp[2])
     finally:
         hip.LanceFreeDetached(h)
