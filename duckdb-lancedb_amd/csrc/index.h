@@ -98,6 +98,8 @@ struct PassBufs {
 	DevBuf<float4> qaux;
 	DevBuf<float2> qm;  // int8 queries: per-query maxima (the batch scale)
 	DevBuf<int> status;
+	DevBuf<uint2> seg_pool;       // threshold path: per-(workgroup, query) segments of this pass
+	DevBuf<int> seg_cnt;
 	int *h_status = nullptr;      // pinned
 	int *d_status_map = nullptr;  // its device-visible address
 	size_t h_status_n = 0;
@@ -136,8 +138,6 @@ struct PendingPass {
 
 struct Workspace {
 	DevBuf<float> Qin, cut, dense, cand_dist, out_d, fb_keys, fb_keys2, stage;
-	DevBuf<uint2> seg_pool;
-	DevBuf<int> seg_cnt;
 	DevBuf<int> out_c;
 	DevBuf<int> selbig;         // per query: pool too large for the small select
 	// small exact search (search_chunk): per-workgroup partial top-k lists and
@@ -224,6 +224,15 @@ struct Index {
 	DevBuf<unsigned> stats;  // [0]=max alpha bits, [1]=max ux bits, [2],[3] for rowaux_l2
 	float max_alpha = 0.f, max_ux = 0.f, max_alpha_l2 = 0.f, max_ux_l2 = 0.f;
 	hipStream_t stream = nullptr;
+	// asynchronous passes run on their pass-buffer set's own stream (ordered after
+	// the handle's stream by ev_order): pass i+1's first kernels overlap pass i's last
+	hipStream_t pstream[2] = {nullptr, nullptr};
+	hipEvent_t ev_order = nullptr;
+	hipStream_t pass_stream(int slot) {
+		if (!pstream[slot]) HIPCHK(hipStreamCreateWithFlags(&pstream[slot], hipStreamNonBlocking));
+		if (!ev_order) HIPCHK(hipEventCreateWithFlags(&ev_order, hipEventDisableTiming));
+		return pstream[slot];
+	}
 	Workspace ws;
 	PassBufs pb[2];
 	std::deque<PendingPass> pending;  // asynchronous passes not finished yet (<= 2)
@@ -296,6 +305,8 @@ struct Index {
 
 	~Index() {
 		if (stream) (void)hipStreamSynchronize(stream);  // (pending passes: their kernels end first)
+		for (auto &ps : pstream)
+			if (ps) (void)hipStreamSynchronize(ps);
 		if (log) fclose(log);
 		ivf_free(ivf);
 		(void)hipSetDevice(device);
@@ -310,6 +321,9 @@ struct Index {
 		for (auto &e : ev)
 			if (e) (void)hipEventDestroy(e);
 		if (stream) (void)hipStreamDestroy(stream);
+		for (auto &ps : pstream)
+			if (ps) (void)hipStreamDestroy(ps);
+		if (ev_order) (void)hipEventDestroy(ev_order);
 	}
 
 	void tic(int i) {

@@ -70,10 +70,20 @@ int Index::pb_free_slot() const {
 bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *dL, float *dD, int *dC, int slot,
                           bool async, PendingPass &p) {
 	PassBufs &P = pb[slot];
+	// an asynchronous pass runs on its pass-buffer set's own stream, after
+	// everything already on the handle's stream: pass i+1's prep, sample pass and
+	// tau refine overlap pass i's final refine (they share no buffer: queries,
+	// status and segment pools are per set)
+	hipStream_t st = stream;
+	if (async) {
+		st = pass_stream(slot);
+		HIPCHK(hipEventRecord(ev_order, stream));
+		HIPCHK(hipStreamWaitEvent(st, ev_order, 0));
+	}
 	const int eff_metric = metric_quirk ? METRIC_L2 : metric;
 	const float4 *aux = search_aux((metric_quirk && metric != METRIC_L2) ? rowaux_l2 : rowaux);
 	const float ma = (metric_quirk && metric != METRIC_L2) ? max_alpha_l2 : max_alpha;
-	// int8 scan copy (option scan_i8): the scans stream int8 rows with their own
+	// int8 scan copy (option scan_i8): the scans st int8 rows with their own
 	// row terms; refine, fallback and the outputs read X and rowaux as always.
 	// Any k on the threshold path (pool_refine refines as far as its certificate
 	// needs); k <= 32 on the dense path of small stores (a fixed candidate count:
@@ -102,17 +112,17 @@ bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *d
 		ws.spart.need(np);
 		if (ws.scnt.n < (size_t)SMALL_MAX_Q) {
 			ws.scnt.need(SMALL_MAX_Q);
-			HIPCHK(hipMemsetAsync(ws.scnt.p, 0, ws.scnt.n * sizeof(unsigned), stream));
+			HIPCHK(hipMemsetAsync(ws.scnt.p, 0, ws.scnt.n * sizeof(unsigned), st));
 		}
 		tic(0);
-		launch_small_exact(sv, dQ, nq, k, ws.spart.p, ws.scnt.p, dL, dD, dC, stream);
+		launch_small_exact(sv, dQ, nq, k, ws.spart.p, ws.scnt.p, dL, dD, dC, st);
 		tic(1);
 		HIPCHK(hipGetLastError());
 		if (time_kernels) {
 			kt_dense_ms += toc_ms(0, 1);  // reported with the dense-path launches
 			kt_dense_n += 1;
 		}
-		if (!defer_sync) HIPCHK(hipStreamSynchronize(stream));
+		if (!defer_sync) HIPCHK(hipStreamSynchronize(st));
 		return false;
 	}
 	const int nq_pad = (int)round_up(nq, SCAN_BQ);
@@ -126,7 +136,7 @@ bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *d
 	P.need_host_status((size_t)3 * nq);
 	// [cert | cand_cnt | pool_cnt]: on the threshold path the kernels write it
 	// straight into pinned host memory (only pool_refine / retry_scatter store
-	// into it, no kernel reads it back), so the step ends with one stream wait
+	// into it, no kernel reads it back), so the step ends with one st wait
 	// and no readback copy; the dense path keeps it in HBM (its refine and
 	// finalize read the candidate counts) and copies it back once
 	const bool hmap = n_slots > 65536;
@@ -141,11 +151,11 @@ bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *d
 	if (use8) {
 		P.qm.need(nq);
 		launch_prep_queries_i8(dQ, nq, dim, ld, nq_pad, eff_metric, max_alpha8, max_x8, P.qm.p, P.Qf.p, P.Qb.p,
-		                       P.qaux.p, dstat, stream);
+		                       P.qaux.p, dstat, st);
 	}
 	else
 		launch_prep_queries(dQ, nq, dim, ld, nq_pad, eff_metric, ma, mu, P.Qf.p, P.Qb.p, P.qaux.p, dstat,
-		                    stream);
+		                    st);
 	QueryView qv{P.Qf.p, P.Qb.p, P.qaux.p, nq, nq_pad};
 
 	// refined candidates: k + max(32, k) — past k the bound slack (bf16 query
@@ -162,12 +172,12 @@ bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *d
 		const int64_t cols = n_tiles * SCAN_BR;
 		ws.dense.need((size_t)nq * cols);
 		tic(0);
-		launch_scan_dense(sv, qv, n_tiles, 1, ws.dense.p, cols, stream);
+		launch_scan_dense(sv, qv, n_tiles, 1, ws.dense.p, cols, st);
 		tic(1);
-		launch_select_dense(ws.dense.p, cols, cols, 1, nq, Mfinal, ws.cand_slot.p, d_cand_cnt, ws.cut.p, stream);
-		launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Mfinal, ws.cand_dist.p, stream);
+		launch_select_dense(ws.dense.p, cols, cols, 1, nq, Mfinal, ws.cand_slot.p, d_cand_cnt, ws.cut.p, st);
+		launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Mfinal, ws.cand_dist.p, st);
 		launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Mfinal, k, 1, 0, nullptr, dL,
-		                dD, dC, d_cert, stream, live_rows());
+		                dD, dC, d_cert, st, live_rows());
 		if (time_kernels) {
 			kt_dense_ms += toc_ms(0, 1);
 			kt_dense_n += 1;
@@ -211,47 +221,43 @@ bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *d
 		const size_t pool_s = (size_t)n_seg_s * nq * cap_s + (size_t)n_seg_s * (nq_pad / SCAN_BQ);
 		const size_t pool_a = (size_t)n_seg * nq * seg_cap + (size_t)n_seg * (nq_pad / SCAN_BQ);  // + per-workgroup sink
 		const size_t cnt_n = (size_t)std::max(n_seg_s, n_seg) * nq;
-		// kernels of a pending pass read seg_pool / seg_cnt: grow them only once it is done
-		if (async && !pending.empty() && (ws.seg_pool.n < std::max(pool_s, pool_a) || ws.seg_cnt.n < cnt_n)) {
-			drain();
-			for (auto &v : last_stats) v = 0;  // (the drained passes' statistics are not this pass's)
-		}
-		ws.seg_pool.need(std::max(pool_s, pool_a));
-		ws.seg_cnt.need(cnt_n);
+		// (this pass's own segment pools: no pending pass reads them)
+		P.seg_pool.need(std::max(pool_s, pool_a));
+		P.seg_cnt.need(cnt_n);
 		if (s8s)
-			launch_scan8_tilemin(sv, qv, n_sample, stride, ws.seg_pool.p, ws.seg_cnt.p, cap_s, stream);
+			launch_scan8_tilemin(sv, qv, n_sample, stride, P.seg_pool.p, P.seg_cnt.p, cap_s, st);
 		else
-			launch_scan_tilemin(sv, qv, n_sample, stride, ws.seg_pool.p, ws.seg_cnt.p, cap_s, stream);
-		launch_pool_refine(sv, qv, ws.seg_pool.p, ws.seg_cnt.p, cap_s, n_seg_s, nullptr, k, 0, Ms, -1, P.tau.p,
-		                   nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
+			launch_scan_tilemin(sv, qv, n_sample, stride, P.seg_pool.p, P.seg_cnt.p, cap_s, st);
+		launch_pool_refine(sv, qv, P.seg_pool.p, P.seg_cnt.p, cap_s, n_seg_s, nullptr, k, 0, Ms, -1, P.tau.p,
+		                   nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, st);
 		tic(2);
 		last_stats[5] += tA ? 2 : 1;  // threshold append launches of the first pass
 		if (tA) {
-			launch_scan8_append(sv, qv, P.tau.p, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, stream, 0, tA, 0);
+			launch_scan8_append(sv, qv, P.tau.p, P.seg_pool.p, P.seg_cnt.p, seg_cap, st, 0, tA, 0);
 			tic(3);
-			launch_pool_refine(sv, qv, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, nA, P.tau.p, k, 0, Ms, -1, P.tau.p,
-			                   nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
+			launch_pool_refine(sv, qv, P.seg_pool.p, P.seg_cnt.p, seg_cap, nA, P.tau.p, k, 0, Ms, -1, P.tau.p,
+			                   nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, st);
 			tic(4);
-			launch_scan8_append(sv, qv, P.tau.p, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, stream, tA, n_tiles, nA);
+			launch_scan8_append(sv, qv, P.tau.p, P.seg_pool.p, P.seg_cnt.p, seg_cap, st, tA, n_tiles, nA);
 			tic(5);
 		} else {
-			launch_scan_append(sv, qv, P.tau.p, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, stream);
+			launch_scan_append(sv, qv, P.tau.p, P.seg_pool.p, P.seg_cnt.p, seg_cap, st);
 			tic(3);
 		}
 		// 3) the pool in bound order, exact refine until certified
 #ifdef LHIP_DEV_PR_IDLE  // (development build: the final refine starts on an idle GPU, DVFS probe)
-		HIPCHK(hipStreamSynchronize(stream));
+		HIPCHK(hipStreamSynchronize(st));
 		usleep(LHIP_DEV_PR_IDLE);
 #endif
-		launch_pool_refine(sv, qv, ws.seg_pool.p, ws.seg_cnt.p, seg_cap, n_seg, P.tau.p, k, 1, 0, live_rows(),
-		                   nullptr, dL, dD, dC, d_cert, d_cand_cnt, d_pool_cnt, stream);
+		launch_pool_refine(sv, qv, P.seg_pool.p, P.seg_cnt.p, seg_cap, n_seg, P.tau.p, k, 1, 0, live_rows(),
+		                   nullptr, dL, dD, dC, d_cert, d_cand_cnt, d_pool_cnt, st);
 		p.two_append = tA > 0;
 	}
 	HIPCHK(hipGetLastError());
 	// [cert | cand_cnt | pool_cnt] on the host: written in place (threshold
 	// path) or one pinned readback (dense path)
 	if (!hmap)
-		HIPCHK(hipMemcpyAsync(P.h_status, P.status.p, (size_t)3 * nq * sizeof(int), hipMemcpyDeviceToHost, stream));
+		HIPCHK(hipMemcpyAsync(P.h_status, P.status.p, (size_t)3 * nq * sizeof(int), hipMemcpyDeviceToHost, st));
 	p.slot = slot;
 	p.nq = nq;
 	p.k = k;
@@ -266,7 +272,7 @@ bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *d
 	p.n_tiles = n_tiles;
 	if (async) {
 		if (!P.done) HIPCHK(hipEventCreateWithFlags(&P.done, hipEventDisableTiming));
-		HIPCHK(hipEventRecord(P.done, stream));
+		HIPCHK(hipEventRecord(P.done, st));
 	}
 	return true;
 }
@@ -275,6 +281,9 @@ bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *d
 // reruns of uncertified queries and the exact fallback (synchronous).
 void Index::finish_chunk(PendingPass &p) {
 	PassBufs &P = pb[p.slot];
+	// reruns and the exact fallback run on the pass's own stream (an
+	// asynchronous pass's kernels and the later pass share no buffer)
+	const hipStream_t st = p.async ? pass_stream(p.slot) : stream;
 	const int nq = p.nq, k = p.k;
 	int64_t *dL = p.dL;
 	float *dD = p.dD;
@@ -287,7 +296,7 @@ void Index::finish_chunk(PendingPass &p) {
 	int *dstat = hmap ? P.d_status_map : P.status.p;
 	int *d_cert = dstat;
 	// a pass enqueued asynchronously completes at its event (later passes may be
-	// queued behind it); a synchronous one at the end of the stream
+	// queued behind it); a synchronous one at the end of the st
 	if (p.async) {
 		for (auto &v : last_stats) v = 0;  // this pass's statistics alone
 		last_stats[3] = p.st3;
@@ -297,7 +306,7 @@ void Index::finish_chunk(PendingPass &p) {
 		}
 		if (e != hipSuccess) throw Error(std::string("HIP error: ") + hipGetErrorString(e) + " at pass completion");
 	} else {
-		spin_sync(stream);
+		spin_sync(st);
 	}
 	if (time_kernels && !all_fallback && !p.dense) {
 		// the append scan's own time (both launches of a progressive pass)
@@ -312,13 +321,9 @@ void Index::finish_chunk(PendingPass &p) {
 		last_stats[1] += P.h_status[nq + q];
 		last_stats[2] = std::max<int64_t>(last_stats[2], P.h_status[2 * nq + q]);
 	}
-	// any rerun / fallback below: first let every later pass queued behind this
-	// one finish (their kernels read the shared workspace these launches reuse)
-	bool synced = !p.async;
-	auto sync_later = [&]() {
-		if (!synced) spin_sync(stream);
-		synced = true;
-	};
+	// (reruns / fallback below: a later pass still in flight on the other pass
+	// stream reads none of the workspace they use — its queries, status, tau and
+	// segment pools are its own set's)
 	// threshold path: rerun the uncertified queries as a batch of their own,
 	// tau = their previous pass's k-th exact distance, full-size segments (up
 	// to two reruns: a pool over the selection's capacity still yields real
@@ -334,7 +339,6 @@ void Index::finish_chunk(PendingPass &p) {
 			if (rerun[q] && !h_cert[q]) fq.push_back(q);
 		const int nf = (int)fq.size();
 		if (nf == 0) break;
-		sync_later();
 		enqueued = true;
 		{
 			if (attempt == 0) last_stats[4] += nf;
@@ -348,27 +352,27 @@ void Index::finish_chunk(PendingPass &p) {
 			ws.rL.need((size_t)nf * k);
 			ws.rD.need((size_t)nf * k);
 			ws.rC.need(nf);
-			HIPCHK(hipMemcpyAsync(ws.rfq.p, fq.data(), (size_t)nf * sizeof(int), hipMemcpyHostToDevice, stream));
+			HIPCHK(hipMemcpyAsync(ws.rfq.p, fq.data(), (size_t)nf * sizeof(int), hipMemcpyHostToDevice, st));
 			// tau tightened to just above the first pass's k-th distance (a pool
 			// that overflowed shrinks; pool_refine refines as far as it needs)
 			launch_retry_gather(ws.rfq.p, nf, nf_pad, ld, k, qv, P.tau.p, dD, ws.rQf.p, ws.rQb.p, ws.rqaux.p,
-			                    ws.rtau.p, ws.rstat.p, stream);
+			                    ws.rtau.p, ws.rstat.p, st);
 			const QueryView qv2{ws.rQf.p, ws.rQb.p, ws.rqaux.p, nf, nf_pad};
 			const int n_seg = scan_append_segments(sv, n_tiles);
 			int cap2 = 1024;  // the scan's maximum, bounded to a 1 GiB pool
 			while (cap2 > 64 && (size_t)n_seg * nf * cap2 * sizeof(uint2) > ((size_t)1 << 30)) cap2 /= 2;
-			ws.seg_pool.need((size_t)n_seg * nf * cap2 + (size_t)n_seg * (nf_pad / SCAN_BQ));
-			ws.seg_cnt.need((size_t)n_seg * nf);
+			P.seg_pool.need((size_t)n_seg * nf * cap2 + (size_t)n_seg * (nf_pad / SCAN_BQ));
+			P.seg_cnt.need((size_t)n_seg * nf);
 			int *cert2 = ws.rstat.p, *cnt2 = ws.rstat.p + nf, *pool2 = ws.rstat.p + 2 * nf;
-			launch_scan_append(sv, qv2, ws.rtau.p, ws.seg_pool.p, ws.seg_cnt.p, cap2, stream);
-			launch_pool_refine(sv, qv2, ws.seg_pool.p, ws.seg_cnt.p, cap2, n_seg, ws.rtau.p, k, 1, 0, live_rows(),
-			                   nullptr, ws.rL.p, ws.rD.p, ws.rC.p, cert2, cnt2, pool2, stream);
+			launch_scan_append(sv, qv2, ws.rtau.p, P.seg_pool.p, P.seg_cnt.p, cap2, st);
+			launch_pool_refine(sv, qv2, P.seg_pool.p, P.seg_cnt.p, cap2, n_seg, ws.rtau.p, k, 1, 0, live_rows(),
+			                   nullptr, ws.rL.p, ws.rD.p, ws.rC.p, cert2, cnt2, pool2, st);
 			launch_retry_scatter(ws.rfq.p, nf, k, ws.rL.p, ws.rD.p, ws.rC.p, cert2, ws.rtau.p, dL, dD, dC, d_cert, P.tau.p,
-			                     stream);
+			                     st);
 			HIPCHK(hipGetLastError());
 			if (!hmap)
-				HIPCHK(hipMemcpyAsync(P.h_status, d_cert, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, stream));
-			spin_sync(stream);
+				HIPCHK(hipMemcpyAsync(P.h_status, d_cert, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st));
+			spin_sync(st);
 		}
 	}
 	// exact fallback for every query whose certificate failed: one batched
@@ -386,7 +390,6 @@ void Index::finish_chunk(PendingPass &p) {
 		if (all_fallback || !h_cert[q] || (P.h_status[nq + q] == 0 && live_rows() > 0)) fbq.push_back(q);
 	last_stats[0] += (int64_t)fbq.size();
 	std::vector<int> slow;
-	if (!fbq.empty()) sync_later();
 	if (!fbq.empty() && fast_ok) {
 		enqueued = true;
 		const int nf = (int)fbq.size();
@@ -400,9 +403,9 @@ void Index::finish_chunk(PendingPass &p) {
 		ws.rL.need((size_t)nf * k);
 		ws.rD.need((size_t)nf * k);
 		ws.rC.need(nf);
-		HIPCHK(hipMemcpyAsync(ws.rfq.p, fbq.data(), (size_t)nf * sizeof(int), hipMemcpyHostToDevice, stream));
+		HIPCHK(hipMemcpyAsync(ws.rfq.p, fbq.data(), (size_t)nf * sizeof(int), hipMemcpyHostToDevice, st));
 		launch_retry_gather(ws.rfq.p, nf, nf_pad, ld, k, qv, P.tau.p, dD, ws.rQf.p, ws.rQb.p, ws.rqaux.p, ws.rtau.p,
-		                    ws.rstat.p, stream);
+		                    ws.rstat.p, st);
 		// keys of up to FB_GROUP queries at a time, within 1 GiB
 		constexpr int FB_GROUP = 16;
 		const int64_t cols = round_up(n_slots, 4);
@@ -414,21 +417,21 @@ void Index::finish_chunk(PendingPass &p) {
 			const int gq = std::min(G, nf - g0);
 			const QueryView qg{ws.rQf.p + (size_t)g0 * ld, ws.rQb.p + (size_t)g0 * ld, ws.rqaux.p + g0, gq,
 			                   (int)round_up(gq, SCAN_BQ)};
-			launch_exact_dense(sv, qg, ws.fb_keys.p, cols, stream);
-			launch_select_dense(ws.fb_keys.p, cols, n_slots, 1, gq, k, ws.cand_slot.p, cnt2 + g0, ws.cut.p, stream);
-			launch_refine(sv, qg, ws.cand_slot.p, cnt2 + g0, k, ws.cand_dist.p, stream);
+			launch_exact_dense(sv, qg, ws.fb_keys.p, cols, st);
+			launch_select_dense(ws.fb_keys.p, cols, n_slots, 1, gq, k, ws.cand_slot.p, cnt2 + g0, ws.cut.p, st);
+			launch_refine(sv, qg, ws.cand_slot.p, cnt2 + g0, k, ws.cand_dist.p, st);
 			launch_finalize(sv, ws.cand_slot.p, cnt2 + g0, ws.cand_dist.p, ws.cut.p, gq, k, k, 1, 0, nullptr,
-			                ws.rL.p + (size_t)g0 * k, ws.rD.p + (size_t)g0 * k, ws.rC.p + g0, cert2 + g0, stream);
+			                ws.rL.p + (size_t)g0 * k, ws.rD.p + (size_t)g0 * k, ws.rC.p + g0, cert2 + g0, st);
 		}
 		// exact keys: the selection is the answer whatever the certificate
 		// says about ties at the cut
-		HIPCHK(hipMemsetAsync(cert2, 0x01, (size_t)nf * sizeof(int), stream));
+		HIPCHK(hipMemsetAsync(cert2, 0x01, (size_t)nf * sizeof(int), st));
 		launch_retry_scatter(ws.rfq.p, nf, k, ws.rL.p, ws.rD.p, ws.rC.p, cert2, ws.rtau.p, dL, dD, dC, d_cert,
-		                     P.tau.p, stream);
+		                     P.tau.p, st);
 		HIPCHK(hipGetLastError());
 		std::vector<int> hc((size_t)nf);
-		HIPCHK(hipMemcpyAsync(hc.data(), ws.rC.p, (size_t)nf * sizeof(int), hipMemcpyDeviceToHost, stream));
-		HIPCHK(hipStreamSynchronize(stream));
+		HIPCHK(hipMemcpyAsync(hc.data(), ws.rC.p, (size_t)nf * sizeof(int), hipMemcpyDeviceToHost, st));
+		HIPCHK(hipStreamSynchronize(st));
 		const int64_t want = std::min<int64_t>(k, live_rows());
 		for (int i = 0; i < nf; ++i)
 			if (hc[(size_t)i] < want) slow.push_back(fbq[(size_t)i]);
@@ -441,17 +444,17 @@ void Index::finish_chunk(PendingPass &p) {
 		ws.fb_keys2.need((size_t)n_slots);
 		ws.fb_vals.need((size_t)n_slots);
 		ws.fb_vals2.need((size_t)n_slots);
-		launch_exact_all(sv, qv, q, ws.fb_keys.p, ws.fb_vals.p, stream);
+		launch_exact_all(sv, qv, q, ws.fb_keys.p, ws.fb_vals.p, st);
 		size_t tb = 0;
 		HIPCHK((hipError_t)sort_pairs(nullptr, tb, ws.fb_keys.p, ws.fb_keys2.p, ws.fb_vals.p, ws.fb_vals2.p, n_slots,
-		                              stream));
+		                              st));
 		ws.sort_tmp.need(tb);
 		HIPCHK((hipError_t)sort_pairs(ws.sort_tmp.p, tb, ws.fb_keys.p, ws.fb_keys2.p, ws.fb_vals.p, ws.fb_vals2.p,
-		                              n_slots, stream));
-		launch_copy_fallback(ws.fb_keys2.p, ws.fb_vals2.p, live_rows(), k, q, dL, dD, dC, stream);
+		                              n_slots, st));
+		launch_copy_fallback(ws.fb_keys2.p, ws.fb_vals2.p, live_rows(), k, q, dL, dD, dC, st);
 		HIPCHK(hipGetLastError());
 	}
-	if (enqueued) HIPCHK(hipStreamSynchronize(stream));
+	if (enqueued) HIPCHK(hipStreamSynchronize(st));
 }
 
 // ---- asynchronous searches (lance_hip_search_batch_device_async) ----------
