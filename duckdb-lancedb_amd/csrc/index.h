@@ -276,6 +276,17 @@ struct Index {
 
 	int64_t last_stats[6] = {0, 0, 0, 0, 0, 0};
 
+	// multi-device handle (env LANCE_HIP_DEVICES or option "devices", shards.cpp):
+	// the rows live in `shards`, one Index per device holding whole ingest batches
+	// under their global labels; this handle keeps next_label, the live count and
+	// the table log, and merges the shards' top-k lists on the first device
+	std::vector<std::unique_ptr<Index>> shards;
+	bool sharded() const { return !shards.empty(); }
+	DevBuf<int64_t> m_pl;
+	DevBuf<float> m_pd;
+	DevBuf<int> m_pc;
+	DevBuf<uint8_t> m_out;
+
 	// optional HIP-event timing of the scan kernels, on the stream they run on
 	bool time_kernels = false;
 	// sample pass covers ~1/sample_div of the tiles (>= 32 tiles); 0 = auto: 16 up to
@@ -738,10 +749,11 @@ struct Index {
 		fwrite(b.data(), 1, b.size(), log);
 		fflush(log);
 	}
-	void log_meta_rows(int64_t s0, int64_t num) {
-		if (!log || !meta) return;
+	void log_meta_rows(int64_t s0, int64_t num, const MetaStore *from = nullptr) {
+		if (!from) from = meta.get();
+		if (!log || !from) return;
 		std::vector<uint8_t> b;
-		meta->serialize_rows(s0, num, b);
+		from->serialize_rows(s0, num, b);
 		uint8_t tag = 7;
 		int64_t n = (int64_t)b.size();
 		fwrite(&tag, 1, 1, log);
@@ -778,8 +790,9 @@ struct Index {
 	}
 
 	// IVF model record (tag 4: type, nlist, m, centroids [nlist][dim], codebook)
-	// and optimize record (tag 5); bodies in ivf_index.cpp
-	void log_model();
+	// of `src`'s model (default: this handle's) and optimize record (tag 5);
+	// bodies in ivf_index.cpp
+	void log_model(Index *src = nullptr);
 	void log_optimize();
 
 	// ---- search ------------------------------------------------------------
@@ -798,6 +811,22 @@ struct Index {
 	void finish_oldest();
 	void drain();
 };
+
+// ---- multi-device handles (shards.cpp) ---------------------------------------
+std::vector<int> parse_devices(const std::string &spec);
+std::vector<int> env_devices();
+void shard_init(Index *ix, const std::vector<int> &devs);
+Index *shard_for_add(Index *ix);
+int64_t shard_live(const Index *ix);
+int64_t shard_add(Index *ix, const float *v, int64_t num, int vdev, Index **into, Index *force = nullptr);
+std::vector<int64_t> shard_remove(Index *ix, const int64_t *labels, int64_t n);
+void shard_search(Index *ix, const float *Q, int qdev, int nq, int k, int nprobes, int refine, const char *pred,
+                  int64_t *L, float *D, int *C, bool out_host);
+Index *shard_of_label(Index *ix, int64_t label, int64_t *slot);
+void shard_all_rows(Index *ix, std::vector<int64_t> &labels, std::vector<float> &vecs);
+void shard_compact(Index *ix);
+void shard_create_index(Index *ix, int type, int num_partitions, int num_sub_vectors);
+void shard_counts(Index *ix);
 
 // A search with a predicate: evaluates it over the slots (host, vectorised),
 // uploads the mask and turns filtering on for the scope of the search call.

@@ -699,12 +699,13 @@ void ivf_export_slots(Index *ix, int32_t *slot_list, uint8_t *slot_codes) {
 	}
 }
 
-void Index::log_model() {
-	if (!log || !ivf) return;
+void Index::log_model(Index *src) {
+	if (!src) src = this;
+	if (!log || !src->ivf) return;
 	std::vector<float> C, cb;
-	model_host(this, C, cb);
+	model_host(src, C, cb);
 	uint8_t tag = 4;
-	int32_t hdr[3] = {ivf->type, ivf->nlist, ivf->m};
+	int32_t hdr[3] = {src->ivf->type, src->ivf->nlist, src->ivf->m};
 	fwrite(&tag, 1, 1, log);
 	fwrite(hdr, 4, 3, log);
 	fwrite(C.data(), sizeof(float), C.size(), log);

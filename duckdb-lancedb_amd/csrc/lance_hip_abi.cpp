@@ -517,8 +517,21 @@ static void replay_log(Index *ix, const std::string &path) {
 		fclose(f);
 		throw Error("corrupt table log: " + path);
 	}
+	if (ix->sharded() && ix->dim != d) {
+		fclose(f);
+		throw Error("table log dimension " + std::to_string(d) + " != handle dimension");
+	}
 	ix->dim = d;
 	ix->ld = (int)round_up(d, DPAD);
+	// the stores the records apply to: this handle, or (multi-device handle) its
+	// shards, an ingest record going whole to the shard with the fewest slots as
+	// at ingest time
+	std::vector<Index *> all;
+	if (ix->sharded())
+		for (auto &sh : ix->shards) all.push_back(sh.get());
+	else
+		all.push_back(ix);
+	Index *last_add = ix;
 	std::vector<float> buf;
 	for (;;) {
 		uint8_t tag;
@@ -528,22 +541,30 @@ static void replay_log(Index *ix, const std::string &path) {
 			if (fread(&first, 8, 1, f) != 1 || fread(&num, 8, 1, f) != 1) break;
 			buf.resize((size_t)num * d);
 			if (fread(buf.data(), sizeof(float), buf.size(), f) != buf.size()) break;  // torn tail: ignore
+			Index *t = ix->sharded() ? shard_for_add(ix) : ix;
 			// a label at or below an existing slot label can only follow a reopen
 			// that reused labels of deleted rows: drop the tombstones first so the
 			// slot -> label order stays strictly ascending
-			if (ix->n_slots > 0 && first <= ix->slot_label.back()) ix->compact();
-			ix->next_label = first;
-			ix->add_host(buf.data(), num);
+			if (t->n_slots > 0 && first <= t->slot_label.back()) t->compact();
+			if (ix->sharded()) t->bind();
+			t->next_label = first;
+			t->add_host(buf.data(), num);
+			ix->next_label = first + num;
+			last_add = t;
 		} else if (tag == 3) {
 			uint8_t v;
 			if (fread(&v, 1, 1, f) != 1) break;
-			ix->set_storage(v == 1);
+			if (ix->sharded()) ix->xbf16 = v == 1;
+			for (Index *t : all) t->set_storage(v == 1);
 		} else if (tag == 2) {
 			int64_t n;
 			if (fread(&n, 8, 1, f) != 1) break;
 			std::vector<int64_t> labs((size_t)n);
 			if (fread(labs.data(), 8, (size_t)n, f) != (size_t)n) break;
-			ix->remove(labs.data(), n);
+			for (Index *t : all) {
+				if (ix->sharded()) t->bind();
+				t->remove(labs.data(), n);
+			}
 		} else if (tag == 4) {
 			// IVF model (lance_detached_create_index): re-index the rows present
 			// at that point of the log with the persisted centroids / codebook
@@ -557,10 +578,16 @@ static void replay_log(Index *ix, const std::string &path) {
 				cb.resize((size_t)m * PQ_K * (d / m));
 				if (fread(cb.data(), sizeof(float), cb.size(), f) != cb.size()) break;
 			}
-			ivf_set_model(ix, type, nl, m, C.data(), type == IVF_PQ ? cb.data() : nullptr);
+			for (Index *t : all) {
+				if (ix->sharded()) t->bind();
+				ivf_set_model(t, type, nl, m, C.data(), type == IVF_PQ ? cb.data() : nullptr);
+			}
 		} else if (tag == 5) {
-			ix->compact();
-			ivf_optimize(ix);
+			for (Index *t : all) {
+				if (ix->sharded()) t->bind();
+				t->compact();
+				ivf_optimize(t);
+			}
 		} else if (tag == 8) {
 			// scalar index record: column, type (rebuilt over the rows present here)
 			uint32_t a = 0, b = 0;
@@ -569,9 +596,10 @@ static void replay_log(Index *ix, const std::string &path) {
 			if (fread(&col[0], 1, a, f) != a || fread(&b, 4, 1, f) != 1 || b > 64) break;
 			std::string ty(b, '\0');
 			if (fread(&ty[0], 1, b, f) != b) break;
-			if (ix->meta)
-				for (auto &c : ix->meta->cols)
-					if (c.name == col) c.build_index(ty);
+			for (Index *t : all)
+				if (t->meta)
+					for (auto &c : t->meta->cols)
+						if (c.name == col) c.build_index(ty);
 		} else if (tag == 6 || tag == 7) {
 			// multi-column table: metadata schema / the rows of the batch just replayed
 			int64_t n;
@@ -580,25 +608,37 @@ static void replay_log(Index *ix, const std::string &path) {
 			if (fread(b.data(), 1, b.size(), f) != b.size()) break;
 			if (tag == 6) {
 				ix->meta = MetaStore::deserialize_schema(b.data(), b.size());
-			} else if (ix->meta) {
+				if (ix->sharded())
+					for (Index *t : all) t->meta = MetaStore::deserialize_schema(b.data(), b.size());
+			} else if (last_add->meta) {
 				// the tag-1 record before it filled these slots with NULLs
-				const int64_t have = ix->meta->cols.empty() ? 0 : (int64_t)ix->meta->cols[0].size();
+				MetaStore *mt = last_add->meta.get();
+				const int64_t have = mt->cols.empty() ? 0 : (int64_t)mt->cols[0].size();
 				int64_t nrec = 0;
 				memcpy(&nrec, b.data(), std::min<size_t>(8, b.size()));
-				ix->meta->truncate((size_t)std::max<int64_t>(0, have - nrec));
-				ix->meta->deserialize_rows(b.data(), b.size());
+				mt->truncate((size_t)std::max<int64_t>(0, have - nrec));
+				mt->deserialize_rows(b.data(), b.size());
 			}
 		} else {
 			break;
 		}
 	}
 	fclose(f);
-	ix->compact();  // rows added after the last create_index / optimize stay unindexed
+	// rows added after the last create_index / optimize stay unindexed
+	for (Index *t : all) {
+		if (ix->sharded()) t->bind();
+		t->compact();
+	}
 	// next_label = MAX(label)+1 over live rows, 0 when empty (lance_manager.rs:157-158, :662-696)
 	int64_t mx = -1;
-	for (int64_t s = 0; s < ix->n_slots; ++s)
-		if (ix->live[(size_t)s]) mx = std::max(mx, ix->slot_label[(size_t)s]);
+	for (Index *t : all)
+		for (int64_t s = 0; s < t->n_slots; ++s)
+			if (t->live[(size_t)s]) mx = std::max(mx, t->slot_label[(size_t)s]);
 	ix->next_label = mx + 1;
+	if (ix->sharded()) {
+		shard_counts(ix);
+		HIPCHK(hipSetDevice(ix->device));
+	}
 }
 
 }  // namespace lhip
@@ -607,6 +647,24 @@ using lhip::Error;
 using lhip::Index;
 
 static Index *as_index(void *h) { return reinterpret_cast<Index *>(h); }
+
+// the handle's device(s): LANCE_HIP_DEVICES lists two or more -> a multi-device
+// handle (shards.cpp); one -> that device; unset -> the current device
+static void init_devices(Index *ix) {
+	const auto devs = lhip::env_devices();
+	ix->init_device(devs.empty() ? -1 : devs[0]);
+	if (devs.size() >= 2) lhip::shard_init(ix, devs);
+}
+
+// the device a device pointer lives on (-1 for host memory)
+static int pointer_device(const void *p) {
+	hipPointerAttribute_t a;
+	if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+		(void)hipGetLastError();
+		return -1;
+	}
+	return a.type == hipMemoryTypeDevice ? a.device : -1;
+}
 static std::string cstr(const char *p) { return p ? std::string(p) : std::string(); }
 
 #define API_GUARD(errprefix, failval)                                                                                  \
@@ -642,7 +700,7 @@ void *lance_create_detached(const char *db_path, int32_t dimension, const char *
 			ix->metric = lhip::metric_id(ix->metric_name);
 			ix->dim = dimension;
 			ix->ld = (int)lhip::round_up(dimension, lhip::DPAD);
-			ix->init_device(-1);
+			init_devices(ix);
 			ix->log_open(true);  // drop any existing table of that name (lance_manager.rs:42)
 		} catch (...) {
 			delete ix;
@@ -673,7 +731,7 @@ void *lance_create_detached_from_arrow(const char *db_path, void *arrow_schema, 
 			ix->dim = meta->dim;
 			ix->ld = (int)lhip::round_up(ix->dim, lhip::DPAD);
 			ix->meta = std::move(meta);
-			ix->init_device(-1);
+			init_devices(ix);
 			ix->log_open(true);
 			ix->log_meta_schema();
 		} catch (...) {
@@ -700,9 +758,15 @@ void *lance_open_detached(const char *db_path, const char *table_name, const cha
 			{
 				FILE *f = fopen(ix->log_path().c_str(), "rb");
 				if (!f) throw Error("table '" + ix->table + "' not found under " + ix->db_path);
+				char magic[8];
+				int32_t d = 0;
+				const bool ok = fread(magic, 1, 8, f) == 8 && fread(&d, 4, 1, f) == 1 && d > 0;
 				fclose(f);
+				if (!ok) throw Error("corrupt table log: " + ix->log_path());
+				ix->dim = d;  // (a multi-device handle lays its shards out before the replay)
+				ix->ld = (int)lhip::round_up(d, lhip::DPAD);
 			}
-			ix->init_device(-1);
+			init_devices(ix);
 			lhip::replay_log(ix, ix->log_path());
 			ix->log_open(false);
 		} catch (...) {
@@ -741,7 +805,7 @@ int64_t lance_detached_add(void *handle, const float *vector, int32_t dimension,
 			throw Error("expected dimension " + std::to_string(ix->dim) + ", got " + std::to_string(dimension));
 		if (!vector) throw Error("null vector");
 		ix->bind();
-		int64_t first = ix->add_host(vector, 1);
+		int64_t first = ix->sharded() ? lhip::shard_add(ix, vector, 1, -1, nullptr) : ix->add_host(vector, 1);
 		ix->log_add(first, vector, 1);
 		return first;
 	}
@@ -762,7 +826,7 @@ int32_t lance_detached_add_batch(void *handle, const float *vectors, int32_t num
 		if (num == 0) return 0;
 		if (!vectors || !out_labels) throw Error("null buffer");
 		ix->bind();
-		int64_t first = ix->add_host(vectors, num);
+		int64_t first = ix->sharded() ? lhip::shard_add(ix, vectors, num, -1, nullptr) : ix->add_host(vectors, num);
 		ix->log_add(first, vectors, num);
 		for (int32_t i = 0; i < num; ++i) out_labels[i] = first + i;
 		return num;
@@ -795,7 +859,8 @@ int32_t lance_detached_add_batch_arrow(void *handle, void *arrow_schema, void *a
 		const ArrowSchema *sch = static_cast<const ArrowSchema *>(arrow_schema);
 		std::lock_guard<std::mutex> g(ix->mu);
 		std::unique_ptr<lhip::MetaStore> tmp;
-		lhip::MetaStore *m = ix->meta.get();
+		Index *tgt = ix->sharded() ? lhip::shard_for_add(ix) : ix;  // (the store that takes the batch)
+		lhip::MetaStore *m = tgt->meta.get();
 		if (!m) {  // a vector-only table: the batch may only carry the vector column
 			tmp = lhip::MetaStore::from_schema(sch);
 			if (!tmp->cols.empty()) throw Error("the table has no metadata columns");
@@ -804,7 +869,7 @@ int32_t lance_detached_add_batch_arrow(void *handle, void *arrow_schema, void *a
 		if (m->dim != ix->dim)
 			throw Error("expected dimension " + std::to_string(ix->dim) + ", got " + std::to_string(m->dim));
 		std::vector<float> vecs;
-		const int64_t n0 = ix->n_slots;
+		const int64_t n0 = tgt->n_slots;
 		int64_t n;
 		try {
 			n = m->import_batch(sch, &owned.a, vecs);
@@ -818,9 +883,10 @@ int32_t lance_detached_add_batch_arrow(void *handle, void *arrow_schema, void *a
 			throw Error("null buffer");
 		}
 		ix->bind();
-		const int64_t first = ix->add_host(vecs.data(), n);
+		const int64_t first =
+		    ix->sharded() ? lhip::shard_add(ix, vecs.data(), n, -1, nullptr, tgt) : ix->add_host(vecs.data(), n);
 		ix->log_add(first, vecs.data(), n);
-		ix->log_meta_rows(n0, n);
+		ix->log_meta_rows(n0, n, tgt->meta.get());
 		for (int64_t i = 0; i < n; ++i) out_labels[i] = first + i;
 		return (int32_t)n;
 	}
@@ -882,12 +948,19 @@ int32_t lance_detached_create_scalar_index(void *handle, const char *column, con
 		if (ty != "BTREE" && ty != "BITMAP") throw Error("unsupported scalar index type '" + cstr(index_type) + "'");
 		const std::string col = cstr(column);
 		if (col == "label") return 0;
-		lhip::MetaColumn *mc = nullptr;
-		if (ix->meta)
-			for (auto &c : ix->meta->cols)
-				if (c.name == col) mc = &c;
-		if (!mc) throw Error("no column named '" + col + "'");
-		mc->build_index(ty);
+		std::vector<Index *> tg;
+		if (ix->sharded())
+			for (auto &sh : ix->shards) tg.push_back(sh.get());
+		else
+			tg.push_back(ix);
+		for (Index *t : tg) {
+			lhip::MetaColumn *mc = nullptr;
+			if (t->meta)
+				for (auto &c : t->meta->cols)
+					if (c.name == col) mc = &c;
+			if (!mc) throw Error("no column named '" + col + "'");
+			mc->build_index(ty);
+		}
 		ix->log_scalar_index(col, ty);
 		return 0;
 	}
@@ -906,6 +979,8 @@ int32_t lance_detached_merge(void *target_handle, void *source_handle, const int
 		Index *src = as_index(source_handle);
 		if (live_count <= 0 || !live_source_labels) return 0;
 		if (tg->dim != src->dim) throw Error("dimension mismatch between merged indexes");
+		if ((tg->sharded() || src->sharded()) && ((tg->meta && !tg->meta->cols.empty()) || (src->meta && !src->meta->cols.empty())))
+			throw Error("merging multi-column tables of a multi-device handle is not supported");
 		// rows of source selected by `label IN (...)`, in source (label) order
 		std::vector<int64_t> want(live_source_labels, live_source_labels + live_count);
 		std::sort(want.begin(), want.end());
@@ -917,9 +992,17 @@ int32_t lance_detached_merge(void *target_handle, void *source_handle, const int
 			src->bind();
 			std::vector<float> row((size_t)src->dim);
 			for (int64_t l : want) {
-				int64_t s = src->slot_of(l);
-				if (s < 0 || !src->live[(size_t)s]) continue;
-				src->read_rows(s, 1, row.data());
+				int64_t s = -1;
+				Index *from = src;
+				if (src->sharded()) {
+					from = lhip::shard_of_label(src, l, &s);
+					if (!from) continue;
+					from->bind();
+				} else {
+					s = src->slot_of(l);
+					if (s < 0 || !src->live[(size_t)s]) continue;
+				}
+				from->read_rows(s, 1, row.data());
 				vecs.insert(vecs.end(), row.begin(), row.end());
 				olds.push_back(l);
 				oslots.push_back(s);
@@ -933,7 +1016,8 @@ int32_t lance_detached_merge(void *target_handle, void *source_handle, const int
 			if (!src->meta) throw Error("merged indexes have different metadata columns");
 			tg->meta->append_rows(*src->meta, oslots);
 		}
-		int64_t first = tg->add_host(vecs.data(), (int64_t)olds.size());
+		int64_t first = tg->sharded() ? lhip::shard_add(tg, vecs.data(), (int64_t)olds.size(), -1, nullptr)
+		                              : tg->add_host(vecs.data(), (int64_t)olds.size());
 		tg->log_add(first, vecs.data(), (int64_t)olds.size());
 		tg->log_meta_rows(n0, (int64_t)olds.size());
 		for (size_t i = 0; i < olds.size(); ++i) {
@@ -961,6 +1045,15 @@ int32_t lance_detached_search_batch(void *handle, const float *queries, int32_t 
 		if (nq == 0) return 0;
 		if (!queries || !out_labels || !out_distances || !out_counts) throw Error("null buffer");
 		std::lock_guard<std::mutex> g(ix->mu);
+		if (ix->sharded()) {
+			if (k <= 0) {
+				for (int32_t i = 0; i < nq; ++i) out_counts[i] = 0;
+				return nq;
+			}
+			lhip::shard_search(ix, queries, -1, nq, k, nprobes, refine_factor, predicate, out_labels, out_distances,
+			                   out_counts, true);
+			return nq;
+		}
 		// prefilter (lance_index.cpp:452-453 passes the optimizer's predicate,
 		// lance_optimizer.cpp:555-584): slots whose predicate is TRUE
 		lhip::FilterScope fs(ix, predicate);
@@ -1059,7 +1152,7 @@ int64_t lance_detached_count(void *handle, char *err_buf, int err_buf_len) {
 	}
 	Index *ix = as_index(handle);
 	std::lock_guard<std::mutex> g(ix->mu);
-	return ix->n_live;
+	return ix->sharded() ? lhip::shard_live(ix) : ix->n_live;
 }
 
 int32_t lance_detached_delete_batch(void *handle, const int64_t *labels, int32_t count, char *err_buf,
@@ -1074,7 +1167,7 @@ int32_t lance_detached_delete_batch(void *handle, const int64_t *labels, int32_t
 		Index *ix = as_index(handle);
 		std::lock_guard<std::mutex> g(ix->mu);
 		ix->bind();
-		auto done = ix->remove(labels, count);
+		auto done = ix->sharded() ? lhip::shard_remove(ix, labels, count) : ix->remove(labels, count);
 		ix->log_del(done);
 		return 0;
 	}
@@ -1105,6 +1198,10 @@ int32_t lance_detached_create_index(void *handle, int32_t num_partitions, int32_
 		Index *ix = as_index(handle);
 		std::lock_guard<std::mutex> g(ix->mu);
 		ix->bind();
+		if (ix->sharded()) {
+			lhip::shard_create_index(ix, ix->ivf_type_opt, num_partitions, num_sub_vectors);
+			return 0;
+		}
 		lhip::ivf_build(ix, ix->ivf_type_opt, num_partitions, num_sub_vectors);
 		ix->log_model();
 		return 0;
@@ -1130,6 +1227,11 @@ int32_t lance_detached_compact(void *handle, char *err_buf, int err_buf_len) {
 		Index *ix = as_index(handle);
 		std::lock_guard<std::mutex> g(ix->mu);
 		ix->bind();
+		if (ix->sharded()) {
+			lhip::shard_compact(ix);
+			if (ix->shards[0]->ivf) ix->log_optimize();
+			return 0;
+		}
 		ix->compact();
 		if (ix->ivf) {
 			lhip::ivf_optimize(ix);  // optimize(All): unindexed rows join the partitions
@@ -1149,14 +1251,22 @@ int32_t lance_detached_get_vector(void *handle, int64_t label, float *out_vec, i
 	try {
 		Index *ix = as_index(handle);
 		std::lock_guard<std::mutex> g(ix->mu);
-		int64_t s = ix->slot_of(label);
-		if (s < 0 || !ix->live[(size_t)s]) throw Error("label " + std::to_string(label) + " not found");
+		int64_t s = -1;
+		Index *from = ix;
+		if (ix->sharded()) {
+			ix->bind();
+			from = lhip::shard_of_label(ix, label, &s);
+			if (!from) throw Error("label " + std::to_string(label) + " not found");
+		} else {
+			s = ix->slot_of(label);
+			if (s < 0 || !ix->live[(size_t)s]) throw Error("label " + std::to_string(label) + " not found");
+		}
 		if (ix->dim > capacity) {
 			lhip::write_err(err_buf, err_buf_len, "output buffer too small");
 			return -1;
 		}
-		ix->bind();
-		ix->read_rows(s, 1, out_vec);
+		from->bind();
+		from->read_rows(s, 1, out_vec);
 		return ix->dim;
 	}
 	API_GUARD("get_vector failed: ", -1)
@@ -1171,6 +1281,18 @@ int32_t lance_detached_get_all_vectors(void *handle, int64_t *out_labels, float 
 	try {
 		Index *ix = as_index(handle);
 		std::lock_guard<std::mutex> g(ix->mu);
+		if (ix->sharded()) {
+			const int64_t nl = lhip::shard_live(ix);
+			if (out_count) *out_count = nl;
+			if (out_labels && out_vectors && nl > 0) {
+				std::vector<int64_t> labs;
+				std::vector<float> vecs;
+				lhip::shard_all_rows(ix, labs, vecs);
+				memcpy(out_labels, labs.data(), labs.size() * sizeof(int64_t));
+				memcpy(out_vectors, vecs.data(), vecs.size() * sizeof(float));
+			}
+			return (int32_t)nl;
+		}
 		if (out_count) *out_count = ix->n_live;
 		if (out_labels && out_vectors && ix->n_live > 0) {
 			ix->bind();
@@ -1199,6 +1321,26 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 		std::lock_guard<std::mutex> g(ix->mu);
 		ix->bind();  // every pending asynchronous search completes under the options it was enqueued with
 		std::string k = cstr(key), v = cstr(value);
+		if (k == "devices") {  // a multi-device handle over these devices (empty table only)
+			lhip::shard_init(ix, lhip::parse_devices(v));
+			return 0;
+		}
+		if (ix->sharded()) {
+			// every shard takes the option; the handle keeps what its own log / new
+			// shards need (storage), reserve_rows is split between the shards
+			std::string fv = v;
+			if (k == "reserve_rows")
+				fv = std::to_string((std::stoll(v) + (int64_t)ix->shards.size() - 1) / (int64_t)ix->shards.size());
+			for (auto &sh : ix->shards)
+				if (lance_hip_set_option(sh.get(), key, fv.c_str(), err_buf, err_buf_len) != 0) return -1;
+			if (k == "storage") {
+				const bool was = ix->xbf16;
+				ix->xbf16 = v == "bf16";
+				if (was != ix->xbf16) ix->log_storage();
+			}
+			if (k == "index_type") ix->ivf_type_opt = ix->shards[0]->ivf_type_opt;
+			return 0;
+		}
 		if (k == "metric_quirk") {
 			bool on = (v == "1" || v == "true");
 			if (on && ix->metric != lhip::METRIC_L2 && !ix->rowaux_l2) {
@@ -1390,6 +1532,17 @@ int32_t lance_hip_kernel_times(void *handle, double *out, int32_t n) {
 	if (!handle || !out) return -1;
 	Index *ix = as_index(handle);
 	std::lock_guard<std::mutex> g(ix->mu);
+	if (ix->sharded()) {  // times and counts summed over the shards, geometry of the first
+		std::vector<double> acc(13, 0.0), one(13);
+		for (size_t i = 0; i < ix->shards.size(); ++i) {
+			lance_hip_kernel_times(ix->shards[i].get(), one.data(), 13);
+			for (int j : {0, 1, 4, 5, 7, 8, 9, 10, 11}) acc[(size_t)j] += one[(size_t)j];
+			if (i == 0)
+				for (int j : {2, 3, 6, 12}) acc[(size_t)j] = one[(size_t)j];
+		}
+		for (int32_t i = 0; i < n && i < 13; ++i) out[i] = acc[(size_t)i];
+		return 0;
+	}
 	double v[13] = {ix->kt_append_ms, (double)ix->kt_append_n, (double)ix->kt_append_rows,
 		               (double)ix->kt_append_qpad, ix->kt_dense_ms, (double)ix->kt_dense_n,
 		               ix->last_scan_esz ? (double)ix->last_scan_esz : (ix->xbf16 || ix->Xs) ? 2.0 : 4.0, ix->kt_ivf_ms,
@@ -1414,10 +1567,11 @@ int64_t lance_hip_add_batch_device(void *handle, const float *d_vectors, int64_t
 		if (dim != ix->dim) throw Error("vector data size mismatch");
 		if (num <= 0) return ix->next_label;
 		ix->bind();
-		int64_t first = ix->add_device(d_vectors, num);
+		int64_t first = ix->sharded() ? lhip::shard_add(ix, d_vectors, num, pointer_device(d_vectors), nullptr)
+		                              : ix->add_device(d_vectors, num);
 		if (ix->log) {
 			std::vector<float> h((size_t)num * dim);
-			HIPCHK(hipMemcpy(h.data(), d_vectors, h.size() * sizeof(float), hipMemcpyDeviceToHost));
+			HIPCHK(hipMemcpy(h.data(), d_vectors, h.size() * sizeof(float), hipMemcpyDefault));
 			ix->log_add(first, h.data(), num);
 		}
 		return first;
@@ -1442,6 +1596,11 @@ int32_t lance_hip_search_batch_device(void *handle, const float *d_queries, int3
 		if (!d_queries || !d_out_labels || !d_out_distances || !d_out_counts) throw Error("null buffer");
 		std::lock_guard<std::mutex> g(ix->mu);
 		ix->bind();
+		if (ix->sharded()) {  // queries on any device, outputs on the first device of the handle
+			lhip::shard_search(ix, d_queries, pointer_device(d_queries), nq, k, nprobes, refine_factor, nullptr,
+			                   d_out_labels, d_out_distances, d_out_counts, false);
+			return nq;
+		}
 		if (ix->n_live == 0) {
 			HIPCHK(hipMemsetAsync(d_out_counts, 0, (size_t)nq * sizeof(int32_t), ix->stream));
 			HIPCHK(hipStreamSynchronize(ix->stream));
@@ -1471,6 +1630,11 @@ int64_t lance_hip_search_batch_device_async(void *handle, const float *d_queries
 		std::lock_guard<std::mutex> g(ix->mu);
 		ix->bind_nodrain();
 		if (nq == 0) return ix->next_ticket++;
+		if (ix->sharded()) {  // (every shard's pass runs concurrently inside the call; complete on return)
+			lhip::shard_search(ix, d_queries, pointer_device(d_queries), nq, k, nprobes, refine_factor, nullptr,
+			                   d_out_labels, d_out_distances, d_out_counts, false);
+			return ix->next_ticket++;
+		}
 		if (ix->n_live == 0) {
 			ix->drain();
 			HIPCHK(hipMemsetAsync(d_out_counts, 0, (size_t)nq * sizeof(int32_t), ix->stream));
@@ -1559,7 +1723,14 @@ int32_t lance_hip_ivf_info(void *handle, int64_t *out, int32_t n) {
 	Index *ix = as_index(handle);
 	std::lock_guard<std::mutex> g(ix->mu);
 	int64_t v[6] = {-1, 0, 0, 0, 0, ix->n_slots};
-	if (ix->ivf) {
+	if (ix->sharded()) {  // the shards share one model; rows indexed and slots summed
+		lance_hip_ivf_info(ix->shards[0].get(), v, 6);
+		v[4] = v[5] = 0;
+		for (auto &sh : ix->shards) {
+			v[4] += sh->ivf ? sh->ivf->n_indexed : 0;
+			v[5] += sh->n_slots;
+		}
+	} else if (ix->ivf) {
 		v[0] = ix->ivf->type;
 		v[1] = ix->ivf->nlist;
 		v[2] = ix->ivf->m;
@@ -1580,6 +1751,7 @@ int32_t lance_hip_ivf_export(void *handle, float *centroids, float *codebook, in
 	try {
 		Index *ix = as_index(handle);
 		std::lock_guard<std::mutex> g(ix->mu);
+		if (ix->sharded()) throw Error("ivf_export: export a multi-device handle's shards one by one");
 		if (!ix->ivf) throw Error("no IVF index");
 		ix->bind();
 		lhip::ivf_export_model(ix, centroids, codebook);
@@ -1605,6 +1777,14 @@ int32_t lance_hip_ivf_set_model(void *handle, int32_t index_type, int32_t num_pa
 		if (index_type != lhip::IVF_FLAT && index_type != lhip::IVF_PQ) throw Error("index_type must be 0 or 1");
 		if (!centroids) throw Error("null centroids");
 		ix->bind();
+		if (ix->sharded()) {
+			for (auto &sh : ix->shards) {
+				sh->bind();
+				lhip::ivf_set_model(sh.get(), index_type, num_partitions, num_sub_vectors, centroids, codebook);
+			}
+			ix->log_model(ix->shards[0].get());
+			return 0;
+		}
 		lhip::ivf_set_model(ix, index_type, num_partitions, num_sub_vectors, centroids, codebook);
 		ix->log_model();
 		return 0;

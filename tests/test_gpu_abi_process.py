@@ -41,10 +41,16 @@ def caller(tmp_path_factory, hip):
     return exe
 
 
-def run(exe, tmp_path, lines, timeout=240):
+def run(exe, tmp_path, lines, timeout=240, devices=None):
+    """devices: LANCE_HIP_DEVICES for the process (e.g. "0,0": every handle it
+    creates or opens is row-sharded over two stores on device 0, shards.cpp)."""
     script = tmp_path / "script.txt"
     script.write_text("\n".join(lines) + "\n")
-    r = subprocess.run([exe, "gpu", str(script)], capture_output=True, text=True, timeout=timeout)
+    env = dict(os.environ)
+    env.pop("LANCE_HIP_DEVICES", None)
+    if devices:
+        env["LANCE_HIP_DEVICES"] = devices
+    r = subprocess.run([exe, "gpu", str(script)], capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     out = r.stdout.splitlines()
     assert out and out[-1] == "done", r.stdout + r.stderr
@@ -83,8 +89,9 @@ def test_process_maps_opt_rocm_runtime_and_no_torch(caller, tmp_path):
 INDEX_CASES = [c for c in load_sql_goldens() if "steps" in c and not c["name"].startswith("rust_")]
 
 
+@pytest.mark.parametrize("devices", [None, "0,0"], ids=["one_store", "two_shards"])
 @pytest.mark.parametrize("case", INDEX_CASES, ids=[c["name"] for c in INDEX_CASES])
-def test_sql_goldens_in_torch_free_process(caller, tmp_path, case):
+def test_sql_goldens_in_torch_free_process(caller, tmp_path, case, devices):
     lines = [f"index {case['dim']} l2 {tmp_path / 'db.lance' / case['name']} vectors"]
     checks = []
     for st in case["steps"]:
@@ -107,7 +114,7 @@ def test_sql_goldens_in_torch_free_process(caller, tmp_path, case):
             checks.append(st)
         else:
             raise ValueError(op)
-    out, errs = run(caller, tmp_path, lines)
+    out, errs = run(caller, tmp_path, lines, devices=devices)
     assert not errs, errs
     res = [parse_res(l) for l in out if l.startswith("res")]
     assert len(res) == len(checks)
@@ -125,7 +132,8 @@ def test_sql_goldens_in_torch_free_process(caller, tmp_path, case):
             assert len(r) > st["expect_count_gt"], (where, r)
 
 
-def test_filter_goldens_through_arrow_in_torch_free_process(caller, tmp_path):
+@pytest.mark.parametrize("devices", [None, "0,0"], ids=["one_store", "two_shards"])
+def test_filter_goldens_through_arrow_in_torch_free_process(caller, tmp_path, devices):
     # lance_optimizer_filter.test:9-99: CREATE INDEX .. USING LANCE (embedding, lang, score), rows handed over
     # through the Arrow C Data Interface, each WHERE pushed down as a Lance predicate
     case = next(c for c in load_sql_goldens() if c["name"] == "filter_pushdown")
@@ -138,7 +146,7 @@ def test_filter_goldens_through_arrow_in_torch_free_process(caller, tmp_path):
     lines.append("restart")  # the metadata columns persist with the table log
     for query in case["queries"]:
         lines.append(f"search {query['k']} 3 1 0 0" + (f" | {query['where']}" if query["where"] else ""))
-    out, errs = run(caller, tmp_path, lines)
+    out, errs = run(caller, tmp_path, lines, devices=devices)
     assert not errs, errs
     res = [parse_res(l) for l in out if l.startswith("res")]
     assert len(res) == 2 * len(case["queries"])
@@ -236,8 +244,10 @@ def test_seeded_fixture_in_torch_free_process(caller, tmp_path, name):
         check(L, D, C, exp["labels"], exp["dists"], exp["counts"])
 
 
-def test_deletes_and_appends_in_torch_free_process(caller, tmp_path):
-    # 90k x 128 rows in DuckDB's 2048-row Sink chunks, a third deleted, then searched per call and batched
+@pytest.mark.parametrize("devices", [None, "0,0"], ids=["one_store", "two_shards"])
+def test_deletes_and_appends_in_torch_free_process(caller, tmp_path, devices):
+    # 90k x 128 rows in DuckDB's 2048-row Sink chunks, a third deleted, then searched per call and batched;
+    # two_shards: the process sets LANCE_HIP_DEVICES, the handle row-shards the chunks over two stores
     rng = np.random.default_rng(77)
     n, d, nq, k = 90_000, 128, 24, 10
     X = gen(31, n, d)
@@ -251,7 +261,7 @@ def test_deletes_and_appends_in_torch_free_process(caller, tmp_path):
     lines = [f"bulk {d} l2 {tmp_path / 'x.bin'} {n} 2048", f"bulk_delete {tmp_path / 'del.bin'} {len(dead)}",
              f"bulk_search {tmp_path / 'q.bin'} {nq} {k} {tmp_path / 'pc.bin'} percall",
              f"bulk_search {tmp_path / 'q.bin'} {nq} {k} {tmp_path / 'b.bin'} batch", "count"]
-    out, errs = run(caller, tmp_path, lines, timeout=600)
+    out, errs = run(caller, tmp_path, lines, timeout=600, devices=devices)
     assert not errs, errs
     assert f"count {int(live.sum())}" in out
     el, ed, ec = flat_knn.flat_search_batch(X, np.arange(n), live, Q, k)
