@@ -122,6 +122,12 @@ def parse():
                          "batch); host_batch = lance_detached_search_batch on host buffers (H2D queries + D2H results "
                          "inside the step); per_call = one lance_detached_search per query, the DuckDB call pattern "
                          "(lance_search.cpp:73-74; a step = one query)")
+    ap.add_argument("--inproc", action="store_true",
+                    help="flat configs: ONE process drives --gpus N devices through one multi-device handle "
+                         "(option devices / LANCE_HIP_DEVICES, shards.cpp) — the form a DuckDB process uses; "
+                         "default: one process per GPU")
+    ap.add_argument("--inproc-devices", default=None,
+                    help="with --inproc: the device list (default 0..N-1; e.g. 0,0 rehearses two shards on one GPU)")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="extra index option (lance_hip_set_option), repeatable, e.g. --opt scan_i8=off")
     a = ap.parse_args()
@@ -635,11 +641,13 @@ def main():
     if a.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
     env_world = os.environ.get("WORLD_SIZE")
-    if env_world is None and a.gpus > 1:
+    if env_world is None and a.gpus > 1 and not a.inproc:
         # one process per GPU, started here (the driver may also start them with
         # torch.distributed.run, which sets WORLD_SIZE)
         return launch_ranks(a)
-    if env_world is not None and int(env_world) != a.gpus:
+    if a.inproc and env_world is not None and int(env_world) > 1:
+        raise SystemExit("--inproc: one process for every device (do not launch ranks)")
+    if env_world is not None and int(env_world) != a.gpus and not a.inproc:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={env_world}: launch one rank per GPU")
     if a.dry_run:
         return main_dry_run(a)
@@ -669,6 +677,11 @@ def main():
     h = L.lance_create_detached(b"", D, a.metric.encode(), b"bench", e, 2048)
     if not h:
         raise RuntimeError(e.value.decode())
+    inproc_devs = None
+    if a.inproc:
+        inproc_devs = a.inproc_devices or ",".join(str(i) for i in range(a.gpus))
+        if len(inproc_devs.split(",")) > 1:
+            lance_hip.LanceHipSetOption(h, "devices", inproc_devs)
     lance_hip.LanceHipSetOption(h, "storage", a.storage)
     lance_hip.LanceHipSetOption(h, "scan_copy", a.scan_copy)
     lance_hip.LanceHipSetOption(h, "reserve_rows", str(n_local))
@@ -910,7 +923,7 @@ def main():
             "metric": metric_name,
             "value": round(value, 1),
             "unit": "queries/s",
-            "n_gpus": world,
+            "n_gpus": len(inproc_devs.split(",")) if inproc_devs else world,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms_step, 4),
@@ -924,7 +937,10 @@ def main():
                                    f"query-batch={1 if a.api == 'per_call' else BG}{api_note}",
                        "api": a.api,
                        "n": N, "dim": D, "k": K, "global_batch": BG, "batch_per_gpu": B, "metric": a.metric, "storage": a.storage,
-                       "parallelism": f"rowshard{world}", "scan_copy": a.scan_copy,
+                       "parallelism": (f"inproc-rowshard{len(inproc_devs.split(','))}" if inproc_devs
+                                       else f"rowshard{world}"),
+                       **({"devices": inproc_devs} if inproc_devs else {}),
+                       "scan_copy": a.scan_copy,
                        **({"options": a.opt} if a.opt else {})},
             "recall_at_10": recall,
             "recall_queries": None if recall is None else nr,
@@ -934,7 +950,11 @@ def main():
         }
         if other:
             line[f"{other['scaling']}_scaling"] = other
-        if pipelined:
+        if pipelined and inproc_devs:
+            line["config"]["pipeline"] = ("multi-device handle: every shard's pass enqueued before the first wait "
+                                          "(shards scan concurrently), partial lists merged on the first device")
+            line["sync"] = syncleg
+        elif pipelined:
             line["config"]["pipeline"] = ("async: 2 batches in flight on the handle's stream "
                                           "(lance_hip_search_batch_device_async / lance_hip_search_wait)"
                                           + ("; batch i-1's all-gather + merge overlap batch i's scan" if world > 1 else ""))
