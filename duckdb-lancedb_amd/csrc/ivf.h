@@ -65,6 +65,7 @@ struct IvfState {
 	// IVF_FLAT bound scan: the bf16 (RNE) rows in list position order, [npos + 256][ld]
 	// (zero rows for padding): an item's 256 rows are one contiguous 256 x ld block
 	DevBuf<uint16_t> lrows;
+	DevBuf<float4> lterms;  // [npos + FLAT_BLK] static row terms in list order (with lrows)
 	bool lrows_ok = false;
 	DevBuf<int64_t> blk_pos0;
 	int nblk = 0, maxb = 1;
@@ -79,7 +80,8 @@ struct IvfState {
 	DevBuf<float> Qq;                        // fp8-rounded queries (option pq_query = fp8)
 	DevBuf<uint8_t> lut8;                    // [nq][m][256]
 	DevBuf<float> qpar;                      // [nq] (D, L0) pairs
-	DevBuf<int> item_off, work, ocnt;
+	DevBuf<int> item_off, work, ocnt, xbeg;
+	DevBuf<int> boff, btot;  // IVF_FLAT bound scan: work items per block, their total
 	DevBuf<uint64_t> thrq, okeys;
 	// IVF_FLAT bound scan workspace
 	DevBuf<float> lbQf, cut;
@@ -158,7 +160,10 @@ void launch_flat_list_scan(const StoreView &s, const int *blk_list, const int64_
 void launch_flat_list_lb(const StoreView &s, const int *blk_list, const int64_t *blk_pos0, const int *lblk0,
                          const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart, const int *pairs,
                          int nprobe, int maxb, const uint16_t *Qb, const float4 *qaux, uint64_t *out, hipStream_t st,
-                         const uint16_t *lrows = nullptr);
+                         const uint16_t *lrows, const float4 *lterms, int *boff /* [nblk + 1] */,
+                         int *tot /* [1] */);
+// out [npos] = (xn, ux, sc, 0) of the row at each list position (the bound scan's list-order row terms)
+void launch_list_terms(const float4 *rowaux, const uint32_t *lslot, int64_t npos, float4 *out, hipStream_t st);
 // out [npos][ld] = bf16 (RNE) of the row at each list position (f32 or bf16 store X), zero for padding
 void launch_list_rows_bf16(const void *X, int xbf16, int ld, int dim, const uint32_t *lslot, int64_t npos,
                            uint16_t *out, hipStream_t st);
@@ -186,20 +191,22 @@ void launch_pq_query_scan(const uint8_t *lcodes, int m, int mp, const int64_t *l
 void launch_pq_query_fp8(const float *Q, int qld, int nq, int dim, float *Qo, hipStream_t st);
 // 8-bit LUTs lut8 [nq][m][256] and qpar [nq] = (D, L0) from P (see pq_lut_u8_kernel)
 void launch_pq_lut_u8(const float *P, int nq, int m, float sP, uint8_t *lut8, float2 *qpar, hipStream_t st);
-// item_off [nlist+1]: work items of the fast scan per list (query groups x row chunks)
-void launch_pq_fast_items(const int *pstart, const int64_t *loff, int nlist, int *item_off, hipStream_t st);
+// item_off [nlist+1]: work items of the fast scan per list (query groups x row chunks), lists in
+// XCD-major order; xbeg [9]: each XCD's item range
+void launch_pq_fast_items(const int *pstart, const int64_t *loff, int nlist, int *item_off, int *xbeg,
+                          hipStream_t st);
 // per query: the kk-th smallest fast-scan key of its nearest probed list -> thrq (atomicMin)
 void launch_pq_seed(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
                     const float *rowaux_f, int nq, int nprobe, const int64_t *probe_l, const float *probe_d,
                     const float *ltau, const uint8_t *lut8, const float2 *qpar, int kk, uint64_t *thrq, hipStream_t st);
 int pq_fast_lds_bytes(int m);
 // list-major 8-bit-LUT scan: per query its candidate run out [nq][ocap] (count ocnt[q]);
-// work (1 int), thrq [nq] (~0) and ocnt [nq] (0) must be initialised
+// work (8 ints: one claim counter per XCD), thrq [nq] (~0) and ocnt [nq] (0) must be initialised
 void launch_pq_fast_scan(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
                          const float *rowaux_f, int nlist, int nprobe, const int *pstart, const int *pairs,
-                         const int *item_off, const float *probe_d, const float *ltau, const uint8_t *lut8,
-                         const float2 *qpar, int kk, int *work, uint64_t *thrq, int *ocnt, uint64_t *out, int ocap,
-                         int grid, hipStream_t st);
+                         const int *item_off, const int *xbeg, const float *probe_d, const float *ltau,
+                         const uint8_t *lut8, const float2 *qpar, int kk, int *work, uint64_t *thrq, int *ocnt,
+                         uint64_t *out, int ocap, int grid, hipStream_t st);
 void launch_pq_run_merge(const uint64_t *keys, const int *ocnt, int nq, int ocap, int K, uint64_t *out,
                          hipStream_t st);
 // ltau [npos]: per list position sum_j T[l][j][c_j] (f32, j ascending), 0 for padding

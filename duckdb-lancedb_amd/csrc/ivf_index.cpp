@@ -418,10 +418,14 @@ static void layout(Index *ix) {
 			s->lrows.need(rows * ix->ld);
 			HIPCHK(hipMemsetAsync(s->lrows.p + (size_t)npos * ix->ld, 0, (size_t)FLAT_BLK * ix->ld * sizeof(uint16_t), st));
 			launch_list_rows_bf16(ix->X, ix->xbf16 ? 1 : 0, ix->ld, ix->dim, s->lslot.p, npos, s->lrows.p, st);
+			s->lterms.need(rows);
+			HIPCHK(hipMemsetAsync(s->lterms.p + npos, 0, (size_t)FLAT_BLK * sizeof(float4), st));
+			launch_list_terms(ix->rowaux, s->lslot.p, npos, s->lterms.p, st);
 			HIPCHK(hipGetLastError());
 			s->lrows_ok = true;
 		} else {
 			s->lrows.release();
+			s->lterms.release();
 		}
 	} else {
 		s->lcodes.need((size_t)std::max<int64_t>(npos, 64) * s->mp);
@@ -529,9 +533,12 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			                    s->lbQf.p, s->lbQb.p, s->lbqaux.p, nullptr, st);
 			s->keys.need((size_t)n * nprobe * s->maxb * FL_KEYS);
 			ix->tic(0);
+			s->boff.need((size_t)s->nblk + 1);
+			s->btot.need(1);
 			launch_flat_list_lb(sv, s->blk_list.p, s->blk_pos0.p, s->lblk0.p, s->loff.p, s->lslot.p, s->nblk,
 			                    s->pstart.p, s->pairs.p, nprobe, s->maxb, s->lbQb.p, s->lbqaux.p, s->keys.p, st,
-			                    s->lrows_ok ? s->lrows.p : nullptr);
+			                    s->lrows_ok ? s->lrows.p : nullptr, s->lrows_ok ? s->lterms.p : nullptr, s->boff.p,
+			                    s->btot.p);
 			ix->tic(1);
 			const int M = std::min(IVF_TOPK_CAP - 1, k + 32);
 			s->cand_a.need((size_t)n * M);
@@ -583,7 +590,8 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			launch_pq_lut_u8(s->P.p, n, s->m, s->metric == METRIC_DOT ? -1.0f : -2.0f, s->lut8.p,
 			                 reinterpret_cast<float2 *>(s->qpar.p), st);
 			s->item_off.need((size_t)s->nlist + 1);
-			launch_pq_fast_items(s->pstart.p, s->loff.p, s->nlist, s->item_off.p, st);
+			s->xbeg.need(9);
+			launch_pq_fast_items(s->pstart.p, s->loff.p, s->nlist, s->item_off.p, s->xbeg.p, st);
 			int64_t maxpos = 0;
 			for (int l = 0; l < s->nlist; ++l) maxpos = std::max(maxpos, s->h_loff[(size_t)l + 1] - s->h_loff[(size_t)l]);
 			const int ocap = (int)std::min<int64_t>((int64_t)1 << 30,
@@ -591,10 +599,10 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			s->okeys.need((size_t)n * ocap);
 			s->ocnt.need((size_t)n);
 			s->thrq.need((size_t)n);
-			s->work.need(1);
+			s->work.need(8);
 			HIPCHK(hipMemsetAsync(s->ocnt.p, 0, (size_t)n * sizeof(int), st));
 			HIPCHK(hipMemsetAsync(s->thrq.p, 0xFF, (size_t)n * sizeof(uint64_t), st));
-			HIPCHK(hipMemsetAsync(s->work.p, 0, sizeof(int), st));
+			HIPCHK(hipMemsetAsync(s->work.p, 0, 8 * sizeof(int), st));
 			if (ix->pq_seed)
 				launch_pq_seed(s->lcodes.p, s->m, s->mp, s->loff.p, s->lslot.p, reinterpret_cast<const float *>(sv.rowaux),
 				               n, nprobe, s->probe_l.p, s->probe_d.p, s->metric == METRIC_DOT ? nullptr : s->ltau.p,
@@ -602,7 +610,7 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			ix->tic(0);
 			launch_pq_fast_scan(s->lcodes.p, s->m, s->mp, s->loff.p, s->lslot.p,
 			                    reinterpret_cast<const float *>(sv.rowaux), s->nlist, nprobe, s->pstart.p, s->pairs.p,
-			                    s->item_off.p, s->probe_d.p, s->metric == METRIC_DOT ? nullptr : s->ltau.p, s->lut8.p,
+			                    s->item_off.p, s->xbeg.p, s->probe_d.p, s->metric == METRIC_DOT ? nullptr : s->ltau.p, s->lut8.p,
 			                    reinterpret_cast<const float2 *>(s->qpar.p), kp, s->work.p, s->thrq.p, s->ocnt.p,
 			                    s->okeys.p, ocap, scan_grid(1 << 20), st);
 			ix->tic(1);

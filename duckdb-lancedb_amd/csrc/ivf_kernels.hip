@@ -1078,9 +1078,10 @@ template <int METRIC>
 __global__ __launch_bounds__(256) void flat_list_lb_kernel(
     const uint16_t *__restrict__ Xb, int ld, const float *__restrict__ rowaux_f, const int *__restrict__ blk_list,
     const int64_t *__restrict__ blk_pos0, const int *__restrict__ lblk0, const int64_t *__restrict__ loff,
-    const uint32_t *__restrict__ lslot, const int *__restrict__ pstart, const int *__restrict__ pairs, int nprobe,
-    int maxb, const uint16_t *__restrict__ Qb, const float4 *__restrict__ qaux, uint64_t *__restrict__ out,
-    const uint16_t *__restrict__ Lrows) {
+    const uint32_t *__restrict__ lslot, int nblk, const int *__restrict__ pstart, const int *__restrict__ pairs,
+    int nprobe, int maxb, const uint16_t *__restrict__ Qb, const float4 *__restrict__ qaux,
+    uint64_t *__restrict__ out, const uint16_t *__restrict__ Lrows, const float4 *__restrict__ Lterms,
+    const int *__restrict__ boff, const int *__restrict__ tot) {
 	extern __shared__ __attribute__((aligned(16))) uint8_t fl_smem[];
 	const int qrow = ld * 2 + 16;  // padded query row (bytes): 16 lanes reading 16 rows hit distinct banks
 	uint8_t *qs = fl_smem;                                                          // [FL_G][qrow]
@@ -1093,25 +1094,55 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
 	constexpr bool FOLD = METRIC != METRIC_COSINE;
 	const int t = threadIdx.x, lane = t & 63, w = t >> 6;
 	const int gq = lane >> 4, rr = lane & 15;
-	const int b = blockIdx.x;
+	// work items = (block b, query group g) for every block of a probed list
+	// (boff: exclusive prefix of ceil(probing queries / FL_G) over the blocks, tot
+	// = their sum), cut into 8 contiguous ranges, one per XCD (workgroups are
+	// dispatched round-robin over the XCDs: XCD = blockIdx.x % 8).  The workgroups
+	// of an XCD take consecutive items, so the query groups of one block run side
+	// by side on ONE XCD and its rows come from that XCD's L2 after the first
+	// group instead of from HBM once per group.
+	const int T = *tot, Tx = (T + 7) >> 3, xc = blockIdx.x & 7, Wx = gridDim.x >> 3;
+	for (int j = blockIdx.x >> 3; j < Tx; j += Wx) {
+	const int it = xc * Tx + j;
+	if (it >= T) break;
+	int b;
+	{
+		int lo = 0, hi = nblk - 1;  // the last block whose items start at or before it
+		while (lo < hi) {
+			const int mid = (lo + hi + 1) >> 1;
+			if (boff[mid] <= it) lo = mid;
+			else hi = mid - 1;
+		}
+		b = lo;
+	}
 	const int l = blk_list[b];
 	const int64_t p0 = blk_pos0[b];
 	const int64_t p1 = min<int64_t>(loff[l + 1], p0 + FLAT_BLK);
 	const int pa = pstart[l], pb = pstart[l + 1];
 	const int bi = b - lblk0[l];
-	if (pa >= pb) return;
+	__syncthreads();  // (the previous item's LDS reads done)
 	{
 		uint32_t s = SLOT_NONE;
 		if (p0 + t < p1) s = lslot[p0 + t];
 		sslot[t] = s;
-		// row terms (alpha, xn, ux, sc); padding: alpha = +inf (LB = +inf)
+		// row terms (alpha, xn, ux, sc); padding: alpha = +inf (LB = +inf).  With
+		// list-order rows the static terms (xn, ux, sc) come in list order too (one
+		// coalesced 16-B read per position) and only alpha (+inf for a tombstone or a
+		// filtered-out row) is read by slot: one random line per row instead of four
 		float4 r = make_float4(F_INF, 0.f, 0.f, 0.f);
-		if (s != SLOT_NONE)
-			r = make_float4(rowaux_f[raix(s, 0)], rowaux_f[raix(s, 1)], rowaux_f[raix(s, 2)], rowaux_f[raix(s, 3)]);
+		if (s != SLOT_NONE) {
+			if (Lterms) {
+				const float4 lt = Lterms[p0 + t];
+				r = make_float4(rowaux_f[raix(s, 0)], lt.x, lt.y, lt.z);
+			} else {
+				r = make_float4(rowaux_f[raix(s, 0)], rowaux_f[raix(s, 1)], rowaux_f[raix(s, 2)], rowaux_f[raix(s, 3)]);
+			}
+		}
 		ras[t] = r;
 	}
 	const int nw = ld / 64;  // 64-deep k windows (ld is a multiple of 64)
-	for (int g0 = pa; g0 < pb; g0 += FL_G) {
+	{
+		const int g0 = pa + (it - boff[b]) * FL_G;
 		const int ng = min(FL_G, pb - g0);
 		__syncthreads();
 		if (t < FL_G) {
@@ -1237,6 +1268,41 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
 			if (lane < FL_T) out[((int64_t)spair[c] * maxb + bi) * FL_T + lane] = best;
 		}
 	}
+	}  // items
+}
+
+// boff [nblk + 1]: exclusive prefix over the blocks of ceil(probing queries of
+// the block's list / FL_G) (the bound scan's work items); tot[0] = the total
+__global__ __launch_bounds__(1024) void flat_lb_items_kernel(const int *__restrict__ blk_list,
+                                                             const int *__restrict__ pstart, int nblk,
+                                                             int *__restrict__ boff, int *__restrict__ tot) {
+	__shared__ int sh[1024];
+	const int t = threadIdx.x;
+	const int per = (nblk + 1023) / 1024;
+	const int a = t * per, e = min(nblk, a + per);
+	auto items = [&](int b) {
+		const int l = blk_list[b];
+		return (pstart[l + 1] - pstart[l] + FL_G - 1) / FL_G;
+	};
+	int s = 0;
+	for (int i = a; i < e; ++i) s += items(i);
+	sh[t] = s;
+	__syncthreads();
+	for (int o = 1; o < 1024; o <<= 1) {
+		const int v = t >= o ? sh[t - o] : 0;
+		__syncthreads();
+		sh[t] += v;
+		__syncthreads();
+	}
+	int run = sh[t] - s;
+	for (int i = a; i < e; ++i) {
+		boff[i] = run;
+		run += items(i);
+	}
+	if (t == 1023) {
+		boff[nblk] = sh[1023];
+		*tot = sh[1023];
+	}
 }
 
 // per query: merge the items' leaders of its probed lists (FL_T - 1 per item
@@ -1337,8 +1403,9 @@ size_t flat_lb_lds_bytes(int ld) { return (size_t)FL_G * (ld * 2 + 16) + (size_t
 void launch_flat_list_lb(const StoreView &s, const int *blk_list, const int64_t *blk_pos0, const int *lblk0,
                          const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart, const int *pairs,
                          int nprobe, int maxb, const uint16_t *Qb, const float4 *qaux, uint64_t *out, hipStream_t st,
-                         const uint16_t *lrows) {
+                         const uint16_t *lrows, const float4 *lterms, int *boff, int *tot) {
 	if (nblk <= 0) return;
+	flat_lb_items_kernel<<<1, 1024, 0, st>>>(blk_list, pstart, nblk, boff, tot);
 	if ((!lrows && !s.scan_bf16) || s.ld % 64) throw std::runtime_error("IVF_FLAT bound scan needs bf16 scan rows");
 	const uint16_t *Xb = static_cast<const uint16_t *>(s.Xscan);
 	const float *ra = reinterpret_cast<const float *>(s.rowaux);
@@ -1346,8 +1413,11 @@ void launch_flat_list_lb(const StoreView &s, const int *blk_list, const int64_t 
 	auto go = [&](auto kern) {
 		HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
 		                           (int)lds));
-		kern<<<dim3((unsigned)nblk), 256, lds, st>>>(Xb, s.ld, ra, blk_list, blk_pos0, lblk0, loff, lslot, pstart,
-		                                              pairs, nprobe, maxb, Qb, qaux, out, lrows);
+		// persistent: 2 workgroups per CU (57 KB of LDS each: all resident), a multiple of the 8 XCDs
+		const int grid = std::max(8, (2 * scan_grid(1 << 20) / 8) * 8);
+		kern<<<dim3((unsigned)grid), 256, lds, st>>>(Xb, s.ld, ra, blk_list, blk_pos0, lblk0, loff, lslot, nblk, pstart,
+		                                             pairs, nprobe, maxb, Qb, qaux, out, lrows, lrows ? lterms : nullptr, boff,
+		                                             tot);
 	};
 	switch (s.metric) {
 	case METRIC_L2: go(flat_list_lb_kernel<METRIC_L2>); break;
@@ -1379,6 +1449,23 @@ __global__ __launch_bounds__(256) void list_rows_bf16_kernel(const void *__restr
 		}
 		*reinterpret_cast<uint4 *>(out + p * ld + c) = o;
 	}
+}
+
+// out [npos] = the static row terms (xn, ux, sc, 0) of the row at each list position (zero for padding)
+__global__ __launch_bounds__(256) void list_terms_kernel(const float *__restrict__ rowaux_f,
+                                                         const uint32_t *__restrict__ lslot, int64_t npos,
+                                                         float4 *__restrict__ out) {
+	const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+	if (p >= npos) return;
+	const uint32_t s = lslot[p];
+	out[p] = s == SLOT_NONE ? make_float4(0.f, 0.f, 0.f, 0.f)
+	                        : make_float4(rowaux_f[raix(s, 1)], rowaux_f[raix(s, 2)], rowaux_f[raix(s, 3)], 0.f);
+}
+
+void launch_list_terms(const float4 *rowaux, const uint32_t *lslot, int64_t npos, float4 *out, hipStream_t st) {
+	if (npos > 0)
+		list_terms_kernel<<<dim3((unsigned)((npos + 255) / 256)), 256, 0, st>>>(reinterpret_cast<const float *>(rowaux),
+		                                                                        lslot, npos, out);
 }
 
 void launch_list_rows_bf16(const void *X, int xbf16, int ld, int dim, const uint32_t *lslot, int64_t npos,
@@ -1702,16 +1789,37 @@ void launch_pq_lut_u8(const float *P, int nq, int m, float sP, uint8_t *lut8, fl
 	pq_lut_u8_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(P, m, sP, lut8, qpar);
 }
 
+// Work items are laid out XCD-major: the lists l = x, x + 8, x + 16, ... first
+// for XCD x, and a workgroup claims from its own XCD's counter (workgroups are
+// dispatched round-robin over the 8 XCDs: XCD = blockIdx.x % 8) before it steals
+// from the others.  The query groups of one list then run on one XCD, close in
+// time, so a list's codes come from that XCD's L2 after its first group instead
+// of from HBM once per group.
+constexpr int NXCD = 8;
+__device__ __forceinline__ int xcd_lists(int nlist, int x) { return x < nlist ? (nlist - x + NXCD - 1) / NXCD : 0; }
+// the list at position p of the XCD-major order
+__device__ __forceinline__ int lperm(int nlist, int p) {
+	int x = 0;
+	while (x < NXCD - 1 && p >= xcd_lists(nlist, x)) {
+		p -= xcd_lists(nlist, x);
+		++x;
+	}
+	return x + NXCD * p;
+}
+
 // work items: list l with np_l probing queries -> ceil(np_l / FQ_G) query
-// groups x ceil(positions_l / FQ_CHUNK) row chunks; item_off = exclusive prefix
+// groups x ceil(positions_l / FQ_CHUNK) row chunks; item_off [nlist + 1] =
+// exclusive prefix over the XCD-major list order, xbeg [NXCD + 1] = item_off
+// at each XCD's first list
 __global__ __launch_bounds__(1024) void pq_fast_items_kernel(const int *__restrict__ pstart,
                                                              const int64_t *__restrict__ loff, int nlist,
-                                                             int *__restrict__ item_off) {
+                                                             int *__restrict__ item_off, int *__restrict__ xbeg) {
 	__shared__ int sh[1024];
 	const int t = threadIdx.x;
 	const int per = (nlist + 1023) / 1024;
 	const int a = t * per, b = min(nlist, a + per);
-	auto items = [&](int l) {
+	auto items = [&](int p) {
+		const int l = lperm(nlist, p);
 		const int np = pstart[l + 1] - pstart[l];
 		const int64_t len = loff[l + 1] - loff[l];
 		return np > 0 && len > 0 ? ((np + FQ_G - 1) / FQ_G) * (int)((len + FQ_CHUNK - 1) / FQ_CHUNK) : 0;
@@ -1732,9 +1840,15 @@ __global__ __launch_bounds__(1024) void pq_fast_items_kernel(const int *__restri
 		run += items(i);
 	}
 	if (t == 1023) item_off[nlist] = sh[1023];
+	__syncthreads();
+	if (t <= NXCD) {
+		int p0 = 0;
+		for (int x = 0; x < t; ++x) p0 += xcd_lists(nlist, x);
+		xbeg[t] = item_off[min(p0, nlist)];
+	}
 }
 
-// Persistent: each workgroup takes work items (one atomic per item).  An item
+// Persistent: each workgroup takes work items (one atomic per item, XCD-major).  An item
 // = one 8192-position chunk of list l x up to FQ_G queries probing l: their
 // 8-bit LUTs interleaved in LDS as u32 [j][c] = (u_0, u_1, u_2, u_3)[j][c], so
 // ONE ds_read_b32 per (row, j) serves all FQ_G queries; the four byte lanes
@@ -1749,9 +1863,9 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
     const uint8_t *__restrict__ lcodes, int m, int mp, const int64_t *__restrict__ loff,
     const uint32_t *__restrict__ lslot, const float *__restrict__ rowaux_f, int nlist, int nprobe,
     const int *__restrict__ pstart, const int *__restrict__ pairs, const int *__restrict__ item_off,
-    const float *__restrict__ probe_d, const float *__restrict__ ltau, const uint8_t *__restrict__ lut8,
-    const float2 *__restrict__ qpar, int kk, int *__restrict__ work, unsigned long long *__restrict__ thrq,
-    int *__restrict__ ocnt, uint64_t *__restrict__ out, int ocap) {
+    const int *__restrict__ xbeg, const float *__restrict__ probe_d, const float *__restrict__ ltau,
+    const uint8_t *__restrict__ lut8, const float2 *__restrict__ qpar, int kk, int *__restrict__ work,
+    unsigned long long *__restrict__ thrq, int *__restrict__ ocnt, uint64_t *__restrict__ out, int ocap) {
 	extern __shared__ __attribute__((aligned(16))) uint8_t fq_smem[];
 	uint32_t *L = reinterpret_cast<uint32_t *>(fq_smem);                  // [m][256]
 	uint64_t *buf = reinterpret_cast<uint64_t *>(fq_smem + (size_t)m * PQ_K * 4);  // [FQ_G][FQ_CAP]
@@ -1760,31 +1874,43 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 	__shared__ float d0s[FQ_G], dls[FQ_G], l0s[FQ_G];
 	const int t = threadIdx.x;
 	const int nch = mp >> 4;
-	const int total = item_off[nlist];
+	int xc = blockIdx.x & (NXCD - 1), tries = 0;  // (thread 0's claim state: XCD counter, counters exhausted)
 #ifdef LHIP_PQ_PROF
 	uint64_t pq_acc[PQ_PROF_N] = {0, 0, 0, 0, 0, 0, 0, 0};
 	uint64_t pq_t = __builtin_amdgcn_s_memtime();
 #endif
 	for (;;) {
 		PQ_T(0);  // (item claim + loop overhead)
-		if (t == 0) item = atomicAdd(work, 1);
+		if (t == 0) {
+			int itc = -1;
+			while (tries < NXCD) {  // every workgroup ends once all 8 counters ran out
+				const int c = atomicAdd(work + xc, 1);
+				if (c < xbeg[xc + 1] - xbeg[xc]) {
+					itc = xbeg[xc] + c;
+					break;
+				}
+				xc = (xc + 1) & (NXCD - 1);
+				++tries;
+			}
+			item = itc;
+		}
 		__syncthreads();
 		const int it = item;
-		if (it >= total) break;
+		if (it < 0) break;
 #ifdef LHIP_PQ_PROF
 		pq_acc[5] += 1;
 #endif
-		// list of the item: last l with item_off[l] <= it (binary search)
+		// list of the item: last position p with item_off[p] <= it (binary search)
 		int lo = 0, hi = nlist - 1;
 		while (lo < hi) {
 			const int mid = (lo + hi + 1) >> 1;
 			if (item_off[mid] <= it) lo = mid;
 			else hi = mid - 1;
 		}
-		const int l = lo;
+		const int l = lperm(nlist, lo);
 		const int64_t p0 = loff[l], len = loff[l + 1] - p0;
 		const int nc = (int)((len + FQ_CHUNK - 1) / FQ_CHUNK);
-		const int loc = it - item_off[l], g = loc / nc, ch = loc % nc;
+		const int loc = it - item_off[lo], g = loc / nc, ch = loc % nc;
 		const int np = pstart[l + 1] - pstart[l];
 		const int ng = min(FQ_G, np - g * FQ_G);
 		if (t < FQ_G) {
@@ -1885,11 +2011,13 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 		// round i + 1's codes land in the other (a copy of the prefetched registers
 		// at the round's end made every round wait for its own prefetch)
 		auto round = [&](const uint4 (&cw)[NCH], uint32_t cslot, float ctau, uint4 (&nw)[NCH], uint32_t &nslot,
-		                 float &ntau, int64_t rpre) __attribute__((always_inline)) {
-			// the query's bound from its other items, consumed at the round's end
-			// (a stale read is only a looser bound)
-			// (issued before the prefetch: its wait at the round's end then leaves
-			// the prefetch in flight — vmcnt counts in issue order)
+		                 float &ntau, int64_t rpre, uint64_t &gprev) __attribute__((always_inline)) {
+			// the query's bound from its other items, consumed at the NEXT round's end
+			// (gprev): a whole round hides its latency (a global round trip under
+			// load is about one round; waiting on it in the same round stalled every
+			// round's barrier); a stale read is only a looser bound.  Issued before
+			// the prefetch: its wait then leaves the prefetch in flight (vmcnt counts
+			// in issue order)
 			uint64_t gthr = KEY64_NONE;
 			if (t < FQ_G && qid[t] >= 0) gthr = __builtin_nontemporal_load(thrq + qid[t]);
 			load_row(rpre, nw, nslot, ntau);
@@ -2002,18 +2130,25 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 					__syncthreads();
 				}
 			}
-			if (t < FQ_G && gthr < thr[t]) thr[t] = gthr;
+			if (t < FQ_G && gprev < thr[t]) thr[t] = gprev;
+			gprev = gthr;
 			__syncthreads();
 			PQ_T(3);  // candidate sorts
 		};
-		uint4 cwB[NCH];
-		uint32_t cslotB = SLOT_NONE;
-		float ctauB = 0.0f;
+		// three code buffers: round i sums one while rounds i + 1 and i + 2 land in the
+		// others (two rounds of codes in flight per thread: ~96 KiB per CU)
+		uint4 cwB[NCH], cwC[NCH];
+		uint32_t cslotB = SLOT_NONE, cslotC = SLOT_NONE;
+		float ctauB = 0.0f, ctauC = 0.0f;
+		uint64_t gprev = KEY64_NONE;
 		load_row(c0 + t, cw, cslot, ctau);
-		for (int64_t r0 = c0; r0 < c1; r0 += 2 * FQ_THREADS) {
-			round(cw, cslot, ctau, cwB, cslotB, ctauB, r0 + FQ_THREADS + t);
+		load_row(c0 + FQ_THREADS + t, cwB, cslotB, ctauB);
+		for (int64_t r0 = c0; r0 < c1; r0 += 3 * FQ_THREADS) {
+			round(cw, cslot, ctau, cwC, cslotC, ctauC, r0 + 2 * FQ_THREADS + t, gprev);
 			if (r0 + FQ_THREADS >= c1) break;
-			round(cwB, cslotB, ctauB, cw, cslot, ctau, r0 + 2 * FQ_THREADS + t);
+			round(cwB, cslotB, ctauB, cw, cslot, ctau, r0 + 3 * FQ_THREADS + t, gprev);
+			if (r0 + 2 * FQ_THREADS >= c1) break;
+			round(cwC, cslotC, ctauC, cwB, cslotB, ctauB, r0 + 4 * FQ_THREADS + t, gprev);
 		}
 		// flush: the item's keys within its final bound (entries appended before
 		// the bound tightened may lie above it)
@@ -2124,22 +2259,23 @@ void launch_pq_seed(const uint8_t *lcodes, int m, int mp, const int64_t *loff, c
 
 int pq_fast_lds_bytes(int m) { return m * PQ_K * 4 + FQ_G * FQ_CAP * 8; }
 
-void launch_pq_fast_items(const int *pstart, const int64_t *loff, int nlist, int *item_off, hipStream_t st) {
-	pq_fast_items_kernel<<<1, 1024, 0, st>>>(pstart, loff, nlist, item_off);
+void launch_pq_fast_items(const int *pstart, const int64_t *loff, int nlist, int *item_off, int *xbeg,
+                          hipStream_t st) {
+	pq_fast_items_kernel<<<1, 1024, 0, st>>>(pstart, loff, nlist, item_off, xbeg);
 }
 
 void launch_pq_fast_scan(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
                          const float *rowaux_f, int nlist, int nprobe, const int *pstart, const int *pairs,
-                         const int *item_off, const float *probe_d, const float *ltau, const uint8_t *lut8,
-                         const float2 *qpar, int kk, int *work, uint64_t *thrq, int *ocnt, uint64_t *out, int ocap,
-                         int grid, hipStream_t st) {
+                         const int *item_off, const int *xbeg, const float *probe_d, const float *ltau,
+                         const uint8_t *lut8, const float2 *qpar, int kk, int *work, uint64_t *thrq, int *ocnt,
+                         uint64_t *out, int ocap, int grid, hipStream_t st) {
 	const int lds = pq_fast_lds_bytes(m);
 	auto go = [&](auto kern) {
 		HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
 		                           160 * 1024 - 256));
 		kern<<<dim3((unsigned)grid), FQ_THREADS, (size_t)lds, st>>>(
-		    lcodes, m, mp, loff, lslot, rowaux_f, nlist, nprobe, pstart, pairs, item_off, probe_d, ltau, lut8, qpar,
-		    kk, work, reinterpret_cast<unsigned long long *>(thrq), ocnt, out, ocap);
+		    lcodes, m, mp, loff, lslot, rowaux_f, nlist, nprobe, pstart, pairs, item_off, xbeg, probe_d, ltau, lut8,
+		    qpar, kk, work, reinterpret_cast<unsigned long long *>(thrq), ocnt, out, ocap);
 	};
 #ifdef LHIP_PQ_PROF
 	{
