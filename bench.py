@@ -961,6 +961,10 @@ def main():
             line["sync"] = syncleg
         if hostb:
             line["host_batch"] = hostb
+            # SURVEY.md §8(d)'s QPS: the C-ABI search_batch wall time WITH the H2D of the
+            # queries and the D2H of the results (base resident); `value` is device-resident
+            line["qps_8d"] = {"value": hostb["value"], "unit": "queries/s",
+                              "definition": "lance_detached_search_batch on host buffers, H2D + D2H timed (SURVEY §8d)"}
         if recall is not None:
             line[f"recall_at_{K}"] = recall_k
             line["exact_ids_on_recall_subset"] = exact_ids

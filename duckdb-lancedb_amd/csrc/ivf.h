@@ -65,7 +65,7 @@ struct IvfState {
 	// IVF_FLAT bound scan: the bf16 (RNE) rows in list position order, [npos + 256][ld]
 	// (zero rows for padding): an item's 256 rows are one contiguous 256 x ld block
 	DevBuf<uint16_t> lrows;
-	DevBuf<float4> lterms;  // [npos + FLAT_BLK] static row terms in list order (with lrows)
+	DevBuf<float4> lterms;  // [npos + FLAT_BLK] row terms in list order at layout time (with lrows)
 	bool lrows_ok = false;
 	DevBuf<int64_t> blk_pos0;
 	int nblk = 0, maxb = 1;
@@ -82,6 +82,7 @@ struct IvfState {
 	DevBuf<float> qpar;                      // [nq] (D, L0) pairs
 	DevBuf<int> item_off, work, ocnt, xbeg;
 	DevBuf<int> boff, btot;  // IVF_FLAT bound scan: work items per block, their total
+	DevBuf<uint32_t> live_bits;  // IVF_FLAT bound scan: live slots of the search (1 bit each)
 	DevBuf<uint64_t> thrq, okeys;
 	// IVF_FLAT bound scan workspace
 	DevBuf<float> lbQf, cut;
@@ -160,8 +161,8 @@ void launch_flat_list_scan(const StoreView &s, const int *blk_list, const int64_
 void launch_flat_list_lb(const StoreView &s, const int *blk_list, const int64_t *blk_pos0, const int *lblk0,
                          const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart, const int *pairs,
                          int nprobe, int maxb, const uint16_t *Qb, const float4 *qaux, uint64_t *out, hipStream_t st,
-                         const uint16_t *lrows, const float4 *lterms, int *boff /* [nblk + 1] */,
-                         int *tot /* [1] */);
+                         const uint16_t *lrows, const float4 *lterms, uint32_t *live_bits /* [n_slots / 32 + 1] */,
+                         int *boff /* [nblk + 1] */, int *tot /* [1] */);
 // out [npos] = (xn, ux, sc, 0) of the row at each list position (the bound scan's list-order row terms)
 void launch_list_terms(const float4 *rowaux, const uint32_t *lslot, int64_t npos, float4 *out, hipStream_t st);
 // out [npos][ld] = bf16 (RNE) of the row at each list position (f32 or bf16 store X), zero for padding

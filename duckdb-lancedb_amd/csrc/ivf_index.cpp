@@ -419,7 +419,12 @@ static void layout(Index *ix) {
 			HIPCHK(hipMemsetAsync(s->lrows.p + (size_t)npos * ix->ld, 0, (size_t)FLAT_BLK * ix->ld * sizeof(uint16_t), st));
 			launch_list_rows_bf16(ix->X, ix->xbf16 ? 1 : 0, ix->ld, ix->dim, s->lslot.p, npos, s->lrows.p, st);
 			s->lterms.need(rows);
-			HIPCHK(hipMemsetAsync(s->lterms.p + npos, 0, (size_t)FLAT_BLK * sizeof(float4), st));
+			{  // padding positions past the last list: alpha = +inf
+				const std::vector<float4> pad((size_t)FLAT_BLK, make_float4(INFINITY, 0.f, 0.f, 0.f));
+				HIPCHK(hipMemcpyAsync(s->lterms.p + npos, pad.data(), pad.size() * sizeof(float4), hipMemcpyHostToDevice,
+				                      st));
+				HIPCHK(hipStreamSynchronize(st));  // (pad is a host temporary)
+			}
 			launch_list_terms(ix->rowaux, s->lslot.p, npos, s->lterms.p, st);
 			HIPCHK(hipGetLastError());
 			s->lrows_ok = true;
@@ -535,10 +540,11 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			ix->tic(0);
 			s->boff.need((size_t)s->nblk + 1);
 			s->btot.need(1);
+			s->live_bits.need((size_t)(ix->n_slots / 32 + 2));
 			launch_flat_list_lb(sv, s->blk_list.p, s->blk_pos0.p, s->lblk0.p, s->loff.p, s->lslot.p, s->nblk,
 			                    s->pstart.p, s->pairs.p, nprobe, s->maxb, s->lbQb.p, s->lbqaux.p, s->keys.p, st,
-			                    s->lrows_ok ? s->lrows.p : nullptr, s->lrows_ok ? s->lterms.p : nullptr, s->boff.p,
-			                    s->btot.p);
+			                    s->lrows_ok ? s->lrows.p : nullptr, s->lrows_ok ? s->lterms.p : nullptr, s->live_bits.p,
+			                    s->boff.p, s->btot.p);
 			ix->tic(1);
 			const int M = std::min(IVF_TOPK_CAP - 1, k + 32);
 			s->cand_a.need((size_t)n * M);

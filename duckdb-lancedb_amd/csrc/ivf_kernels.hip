@@ -1081,7 +1081,7 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
     const uint32_t *__restrict__ lslot, int nblk, const int *__restrict__ pstart, const int *__restrict__ pairs,
     int nprobe, int maxb, const uint16_t *__restrict__ Qb, const float4 *__restrict__ qaux,
     uint64_t *__restrict__ out, const uint16_t *__restrict__ Lrows, const float4 *__restrict__ Lterms,
-    const int *__restrict__ boff, const int *__restrict__ tot) {
+    const uint32_t *__restrict__ live_bits, const int *__restrict__ boff, const int *__restrict__ tot) {
 	extern __shared__ __attribute__((aligned(16))) uint8_t fl_smem[];
 	const int qrow = ld * 2 + 16;  // padded query row (bytes): 16 lanes reading 16 rows hit distinct banks
 	uint8_t *qs = fl_smem;                                                          // [FL_G][qrow]
@@ -1126,14 +1126,15 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
 		if (p0 + t < p1) s = lslot[p0 + t];
 		sslot[t] = s;
 		// row terms (alpha, xn, ux, sc); padding: alpha = +inf (LB = +inf).  With
-		// list-order rows the static terms (xn, ux, sc) come in list order too (one
-		// coalesced 16-B read per position) and only alpha (+inf for a tombstone or a
-		// filtered-out row) is read by slot: one random line per row instead of four
+		// list-order rows the terms come in list order too (one coalesced 16-B read
+		// per position, fixed since the layout was built) and whether the row is live
+		// (not deleted, selected by the predicate) from a bitmap of the slots built
+		// per search (live_bits: 1 bit per slot, L2-resident) instead of four random
+		// row-aux lines per row
 		float4 r = make_float4(F_INF, 0.f, 0.f, 0.f);
 		if (s != SLOT_NONE) {
 			if (Lterms) {
-				const float4 lt = Lterms[p0 + t];
-				r = make_float4(rowaux_f[raix(s, 0)], lt.x, lt.y, lt.z);
+				if ((live_bits[s >> 5] >> (s & 31)) & 1u) r = Lterms[p0 + t];
 			} else {
 				r = make_float4(rowaux_f[raix(s, 0)], rowaux_f[raix(s, 1)], rowaux_f[raix(s, 2)], rowaux_f[raix(s, 3)]);
 			}
@@ -1400,11 +1401,20 @@ __global__ __launch_bounds__(256) void flat_lb_refine_kernel(const T *__restrict
 
 size_t flat_lb_lds_bytes(int ld) { return (size_t)FL_G * (ld * 2 + 16) + (size_t)FL_G * FLAT_BLK * 8; }
 
+__global__ __launch_bounds__(256) void live_bits_kernel(const float *__restrict__ rowaux_f, int64_t n,
+                                                        uint32_t *__restrict__ bits);
+
 void launch_flat_list_lb(const StoreView &s, const int *blk_list, const int64_t *blk_pos0, const int *lblk0,
                          const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart, const int *pairs,
                          int nprobe, int maxb, const uint16_t *Qb, const float4 *qaux, uint64_t *out, hipStream_t st,
-                         const uint16_t *lrows, const float4 *lterms, int *boff, int *tot) {
+                         const uint16_t *lrows, const float4 *lterms, uint32_t *live_bits, int *boff, int *tot) {
 	if (nblk <= 0) return;
+	if (lrows) {  // the live bitmap of the slots (deletes / the predicate of this search: alpha = +inf)
+		const int64_t n = s.n_slots;
+		if (n > 0)
+			live_bits_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, st>>>(reinterpret_cast<const float *>(s.rowaux), n,
+			                                                                    live_bits);
+	}
 	flat_lb_items_kernel<<<1, 1024, 0, st>>>(blk_list, pstart, nblk, boff, tot);
 	if ((!lrows && !s.scan_bf16) || s.ld % 64) throw std::runtime_error("IVF_FLAT bound scan needs bf16 scan rows");
 	const uint16_t *Xb = static_cast<const uint16_t *>(s.Xscan);
@@ -1416,8 +1426,8 @@ void launch_flat_list_lb(const StoreView &s, const int *blk_list, const int64_t 
 		// persistent: 2 workgroups per CU (57 KB of LDS each: all resident), a multiple of the 8 XCDs
 		const int grid = std::max(8, (2 * scan_grid(1 << 20) / 8) * 8);
 		kern<<<dim3((unsigned)grid), 256, lds, st>>>(Xb, s.ld, ra, blk_list, blk_pos0, lblk0, loff, lslot, nblk, pstart,
-		                                             pairs, nprobe, maxb, Qb, qaux, out, lrows, lrows ? lterms : nullptr, boff,
-		                                             tot);
+		                                             pairs, nprobe, maxb, Qb, qaux, out, lrows, lrows ? lterms : nullptr,
+		                                             live_bits, boff, tot);
 	};
 	switch (s.metric) {
 	case METRIC_L2: go(flat_list_lb_kernel<METRIC_L2>); break;
@@ -1451,15 +1461,28 @@ __global__ __launch_bounds__(256) void list_rows_bf16_kernel(const void *__restr
 	}
 }
 
-// out [npos] = the static row terms (xn, ux, sc, 0) of the row at each list position (zero for padding)
+// out [npos] = the row terms (alpha, xn, ux, sc) of the row at each list position (+inf alpha for padding);
+// fixed for the rows of a layout (a deleted row is masked by live_bits, not here)
 __global__ __launch_bounds__(256) void list_terms_kernel(const float *__restrict__ rowaux_f,
                                                          const uint32_t *__restrict__ lslot, int64_t npos,
                                                          float4 *__restrict__ out) {
 	const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
 	if (p >= npos) return;
 	const uint32_t s = lslot[p];
-	out[p] = s == SLOT_NONE ? make_float4(0.f, 0.f, 0.f, 0.f)
-	                        : make_float4(rowaux_f[raix(s, 1)], rowaux_f[raix(s, 2)], rowaux_f[raix(s, 3)], 0.f);
+	out[p] = s == SLOT_NONE ? make_float4(F_INF, 0.f, 0.f, 0.f)
+	                        : make_float4(rowaux_f[raix(s, 0)], rowaux_f[raix(s, 1)], rowaux_f[raix(s, 2)],
+	                                      rowaux_f[raix(s, 3)]);
+}
+
+// bits [ceil(n / 32)]: bit s = slot s is live for this search (its row aux alpha < +inf)
+__global__ __launch_bounds__(256) void live_bits_kernel(const float *__restrict__ rowaux_f, int64_t n,
+                                                        uint32_t *__restrict__ bits) {
+	const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+	const bool live = s < n && rowaux_f[raix(s, 0)] != F_INF;
+	const uint64_t m = __builtin_amdgcn_ballot_w64(live);
+	const int lane = threadIdx.x & 63;
+	if (lane == 0 && s < n) bits[s >> 5] = (uint32_t)m;
+	if (lane == 32 && s < n) bits[s >> 5] = (uint32_t)(m >> 32);
 }
 
 void launch_list_terms(const float4 *rowaux, const uint32_t *lslot, int64_t npos, float4 *out, hipStream_t st) {

@@ -232,7 +232,14 @@ int32_t lance_hip_device_count(void);
  *   "pr_first"     bounds refined in the first chunk of the final
  *                  threshold-path refine, this handle only: "0" = the default
  *                  (96), else 8..1024; results are exact for every value
- * The handle is bound to the HIP device current when it was created.
+ *   "devices"      "0,1,..." (two or more ids, repeats allowed): this empty
+ *                  handle row-shards its table over one store per listed
+ *                  device; searches run on every store and the per-store top-k
+ *                  lists merge on the first device (results as one store)
+ * The handle is bound to the HIP device current when it was created, or, with
+ * LANCE_HIP_DEVICES=0,1,... in the process environment at create / open time,
+ * is a multi-device handle over those devices (one id: that device).  Every
+ * option of a multi-device handle applies to each of its stores.
  * Returns 0 or -1. */
 int32_t lance_hip_set_option(void *handle, const char *key, const char *value, char *err_buf, int err_buf_len);
 
