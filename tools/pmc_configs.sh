@@ -1,7 +1,7 @@
 #!/bin/bash
-# round-5 PMC traffic passes (MI355X_MICROARCH.md 'HBM': one counter per rocprofv3 run, no trace
+# PMC traffic passes (MI355X_MICROARCH.md 'HBM': one counter per rocprofv3 run, no trace
 # domains): FETCH_SIZE / WRITE_SIZE of the dominant kernel of each listed config.
-# usage: tools/r05_pmc.sh TAG CONFIG... (configs: c2 nstar c3 c4 c5); summaries -> gpurun_out/r05_<cfg>_*_traffic.json
+# usage: tools/pmc_configs.sh TAG CONFIG... (configs: c2 nstar c3 c4 c5); summaries -> gpurun_out/TAG_<cfg>_*_traffic.json
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out
