@@ -59,7 +59,7 @@ struct IvfState {
 	std::vector<int64_t> h_lcnt;             // [nlist] rows per list (unpadded)
 	DevBuf<int64_t> loff;
 	DevBuf<uint32_t> lslot;                  // [npos] slot, SLOT_NONE for padding
-	DevBuf<uint8_t> lcodes;                  // [npos/64][mp/16][64][16] blocked codes
+	DevBuf<uint8_t> lcodes;                  // [npos][mp] codes, row-major in list order
 	DevBuf<float> ltau;                      // [npos] row term of the L2 / cosine ADC (list order)
 	DevBuf<int> blk_list, lblk0;             // IVF_FLAT work items (256 positions each)
 	// IVF_FLAT bound scan: the bf16 (RNE) rows in list position order, [npos + 256][ld]
@@ -81,6 +81,7 @@ struct IvfState {
 	DevBuf<uint8_t> lut8;                    // [nq][m][256]
 	DevBuf<float> qpar;                      // [nq] (D, L0) pairs
 	DevBuf<int> item_off, work, ocnt, xbeg;
+	DevBuf<int4> itab;  // fast-scan item table (launch_pq_fast_items)
 	DevBuf<int> boff, btot;  // IVF_FLAT bound scan: work items per block, their total
 	DevBuf<uint32_t> live_bits;  // IVF_FLAT bound scan: live slots of the search (1 bit each)
 	DevBuf<uint64_t> thrq, okeys;
@@ -194,8 +195,9 @@ void launch_pq_query_fp8(const float *Q, int qld, int nq, int dim, float *Qo, hi
 void launch_pq_lut_u8(const float *P, int nq, int m, float sP, uint8_t *lut8, float2 *qpar, hipStream_t st);
 // item_off [nlist+1]: work items of the fast scan per list (query groups x row chunks), lists in
 // XCD-major order; xbeg [9]: each XCD's item range
-void launch_pq_fast_items(const int *pstart, const int64_t *loff, int nlist, int *item_off, int *xbeg,
-                          hipStream_t st);
+// itab [2 x items] (when non-null): per item (list, row chunk, -, -), (pair ids of its query group)
+void launch_pq_fast_items(const int *pstart, const int64_t *loff, const int *pairs, int nlist, int *item_off,
+                          int *xbeg, int4 *itab, int itab_cap, hipStream_t st);
 // per query: the kk-th smallest fast-scan key of its nearest probed list -> thrq (atomicMin)
 void launch_pq_seed(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
                     const float *rowaux_f, int nq, int nprobe, const int64_t *probe_l, const float *probe_d,
@@ -207,7 +209,7 @@ void launch_pq_fast_scan(const uint8_t *lcodes, int m, int mp, const int64_t *lo
                          const float *rowaux_f, int nlist, int nprobe, const int *pstart, const int *pairs,
                          const int *item_off, const int *xbeg, const float *probe_d, const float *ltau,
                          const uint8_t *lut8, const float2 *qpar, int kk, int *work, uint64_t *thrq, int *ocnt,
-                         uint64_t *out, int ocap, int grid, hipStream_t st);
+                         uint64_t *out, int ocap, const int4 *itab, int grid, hipStream_t st);
 void launch_pq_run_merge(const uint64_t *keys, const int *ocnt, int nq, int ocap, int K, uint64_t *out,
                          hipStream_t st);
 // ltau [npos]: per list position sum_j T[l][j][c_j] (f32, j ascending), 0 for padding

@@ -597,9 +597,15 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			                 reinterpret_cast<float2 *>(s->qpar.p), st);
 			s->item_off.need((size_t)s->nlist + 1);
 			s->xbeg.need(9);
-			launch_pq_fast_items(s->pstart.p, s->loff.p, s->nlist, s->item_off.p, s->xbeg.p, st);
 			int64_t maxpos = 0;
 			for (int l = 0; l < s->nlist; ++l) maxpos = std::max(maxpos, s->h_loff[(size_t)l + 1] - s->h_loff[(size_t)l]);
+			// items <= (query groups: n nprobe / FQ_G, + one partial group per list) x row chunks per list
+			const int64_t maxnc = (maxpos + FQ_CHUNK - 1) / FQ_CHUNK;
+			const int itab_cap = (int)std::min<int64_t>(((int64_t)n * nprobe / FQ_G + s->nlist) * std::max<int64_t>(maxnc, 1),
+			                                            (int64_t)1 << 28);
+			s->itab.need((size_t)2 * itab_cap);
+			launch_pq_fast_items(s->pstart.p, s->loff.p, s->pairs.p, s->nlist, s->item_off.p, s->xbeg.p, s->itab.p,
+			                     itab_cap, st);
 			const int ocap = (int)std::min<int64_t>((int64_t)1 << 30,
 			                                        (int64_t)nprobe * ((maxpos + FQ_CHUNK - 1) / FQ_CHUNK) * FQ_CAP);
 			s->okeys.need((size_t)n * ocap);
@@ -618,7 +624,7 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			                    reinterpret_cast<const float *>(sv.rowaux), s->nlist, nprobe, s->pstart.p, s->pairs.p,
 			                    s->item_off.p, s->xbeg.p, s->probe_d.p, s->metric == METRIC_DOT ? nullptr : s->ltau.p, s->lut8.p,
 			                    reinterpret_cast<const float2 *>(s->qpar.p), kp, s->work.p, s->thrq.p, s->ocnt.p,
-			                    s->okeys.p, ocap, scan_grid(1 << 20), st);
+			                    s->okeys.p, ocap, s->itab.p, scan_grid(1 << 20), st);
 			ix->tic(1);
 			s->cand_a.need((size_t)n * kp);
 			launch_pq_run_merge(s->okeys.p, s->ocnt.p, n, ocap, kp, s->cand_a.p, st);

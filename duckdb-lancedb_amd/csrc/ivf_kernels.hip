@@ -11,10 +11,10 @@
 //             IVF_FLAT  256-row work items, rows staged through LDS, f64
 //                       exact distances for every query of the list, bitonic
 //                       top-k per (query, item)
-//             IVF_PQ    one workgroup per list, the (query, list) ADC LUT
-//                       (m x 256 f32) resident in LDS, codes streamed in a
-//                       64-row blocked layout (1 KiB per wave load), LDS
-//                       threshold top-k per (query, list)
+//             IVF_PQ    work items of (list chunk, 4 probing queries): the
+//                       4 queries' 8-bit LUTs interleaved in LDS, codes
+//                       streamed row-major in list order, LDS threshold
+//                       candidates per (query, item); exact re-rank after
 //           -> per-query merge -> exact re-rank (PQ) -> (distance, label) top-k
 #include "ivf.h"
 #include "device_common.h"
@@ -27,7 +27,7 @@
 // Development-only timing ablations of pq_fast_scan_kernel (results are wrong
 // when set): only an ablation build (tools/pq_ablate.sh) may turn them on.
 #if !defined(LHIP_ABLATION_BUILD) && (defined(LHIP_PQ_ABL_NO_LUT) || defined(LHIP_PQ_ABL_NO_LOOKUP) || \
-                                      defined(LHIP_PQ_ABL_NO_CAND) || defined(LHIP_PQ_ABL_NO_ALIVE))
+                                      defined(LHIP_PQ_ABL_NO_CAND))
 #error "PQ ablation switches are for ablation builds only"
 #endif
 
@@ -50,6 +50,23 @@ __device__ uint64_t g_pq_prof[PQ_PROF_WG * PQ_PROF_N];
 #else
 #define PQ_T(i)
 #endif
+
+// f32 steps rounded one at a time, as the oracle's ISO C11 port does them: HIP
+// compiles with fp-contract=fast-honor-pragmas, and __fmul_rn / __fadd_rn
+// are plain operators in their headers, so a product feeding a sum became a
+// v_fmac; operators created under contract(off) carry no contract flag
+__device__ __forceinline__ float add_nc(float a, float b) {
+#pragma clang fp contract(off)
+	return a + b;
+}
+__device__ __forceinline__ float sub_nc(float a, float b) {
+#pragma clang fp contract(off)
+	return a - b;
+}
+__device__ __forceinline__ float mul_nc(float a, float b) {
+#pragma clang fp contract(off)
+	return a * b;
+}
 
 __device__ __forceinline__ uint64_t key64(float d, uint32_t slot) { return ((uint64_t)fkey(d) << 32) | slot; }
 __device__ __forceinline__ float key64_dist(uint64_t k) { return fkey_inv((uint32_t)(k >> 32)); }
@@ -100,6 +117,35 @@ __device__ __forceinline__ int pow2_ceil(int v) {
 	int p = 2;
 	while (p < v) p <<= 1;
 	return p;
+}
+
+// Sort one query's candidate buffer b[0..cnt_i) of a fast-scan item and cut it
+// to kk.  The scan loops offer rows without reading their liveness (a global
+// read in the loop makes the wave wait, vmcnt(0), for every load issued
+// before it: the rows prefetched two rounds ahead), so dead rows are dropped
+// here, before the kk-th key becomes the bound, and at the flush.  All
+// threads call it; cnt_i, thr_i and nlive are LDS.
+__device__ void fq_cut(uint64_t *b, int &cnt_i, uint64_t &thr_i, int q, int kk, const float *rowaux_f,
+                       unsigned long long *thrq, int &nlive) {
+	const int c = cnt_i, n2 = pow2_ceil(c);
+	if (threadIdx.x == 0) nlive = 0;
+	for (int e = threadIdx.x; e < n2; e += blockDim.x)
+		if (e >= c || !slot_alive(rowaux_f, (uint32_t)b[e])) b[e] = KEY64_NONE;
+	wg_bitonic_sort(b, n2);
+	for (int e = threadIdx.x; e < n2; e += blockDim.x)
+		if (b[e] != KEY64_NONE && (e + 1 == n2 || b[e + 1] == KEY64_NONE)) nlive = e + 1;
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		const int lv = nlive;
+		if (lv >= kk) {
+			thr_i = b[kk - 1];  // inclusive bound: the kk-th live key stays
+			cnt_i = kk;
+			atomicMin(thrq + q, (unsigned long long)b[kk - 1]);
+		} else {
+			cnt_i = lv;
+		}
+	}
+	__syncthreads();
 }
 
 // Streaming top-K of 64-bit keys in LDS: every round each thread offers at
@@ -722,7 +768,7 @@ __global__ __launch_bounds__(256) void pq_T_kernel(const float *__restrict__ C, 
 	const float *y = cb + ((int64_t)j * PQ_K + c) * dsub;
 	const float *cl = C + (int64_t)l * ld + j * dsub;
 	float acc = 0.0f;
-	for (int t = 0; t < dsub; ++t) acc = __fadd_rn(acc, __fmul_rn(y[t], __fadd_rn(y[t], 2.0f * cl[t])));
+	for (int t = 0; t < dsub; ++t) acc = add_nc(acc, mul_nc(y[t], add_nc(y[t], 2.0f * cl[t])));
 	T[((int64_t)l * m + j) * PQ_K + c] = acc;
 }
 
@@ -741,7 +787,7 @@ __global__ void pq_layout_kernel(const uint8_t *__restrict__ codes, const uint32
 	const uint32_t slot = lslot[pos];
 	uint4 v = make_uint4(0, 0, 0, 0);
 	if (slot != SLOT_NONE) v = *reinterpret_cast<const uint4 *>(codes + (int64_t)slot * mp + ch * 16);
-	*reinterpret_cast<uint4 *>(lcodes + (((pos >> 6) * nch + ch) * 64 + (pos & 63)) * 16) = v;
+	*reinterpret_cast<uint4 *>(lcodes + (pos * nch + ch) * 16) = v;
 }
 
 void launch_pq_layout(const uint8_t *codes, const uint32_t *lslot, int64_t npos, int mp, uint8_t *lcodes,
@@ -1563,7 +1609,7 @@ __global__ __launch_bounds__(256) void pq_P_kernel(const float *__restrict__ Q, 
 	const float *x = Q + (int64_t)q * qld + j * dsub;
 	const float *y = cb + ((int64_t)j * PQ_K + c) * dsub;
 	float acc = 0.0f;
-	for (int t = 0; t < dsub; ++t) acc = __fadd_rn(acc, __fmul_rn(x[t], y[t]));
+	for (int t = 0; t < dsub; ++t) acc = add_nc(acc, mul_nc(x[t], y[t]));
 	P[((int64_t)q * m + j) * PQ_K + c] = acc;
 }
 
@@ -1620,14 +1666,14 @@ __device__ __forceinline__ void pq_adc_r(const uint8_t *__restrict__ lcodes, int
 	const uint8_t *cp[PQ_R];
 #pragma unroll
 	for (int i = 0; i < PQ_R; ++i) {
-		cp[i] = lcodes + ((pos[i] >> 6) * nch * 64 + (pos[i] & 63)) * 16;
+		cp[i] = lcodes + pos[i] * nch * 16;
 		acc[i] = ltau ? d0 + ltau[pos[i]] : d0;
 	}
 	for (int ch = 0; ch < nch; ++ch) {
 		uint32_t wd[PQ_R][4];
 #pragma unroll
 		for (int i = 0; i < PQ_R; ++i) {
-			const uint4 w = *reinterpret_cast<const uint4 *>(cp[i] + (int64_t)ch * 64 * 16);
+			const uint4 w = *reinterpret_cast<const uint4 *>(cp[i] + ch * 16);
 			wd[i][0] = w.x;
 			wd[i][1] = w.y;
 			wd[i][2] = w.z;
@@ -1649,8 +1695,8 @@ __device__ __forceinline__ void pq_adc_r(const uint8_t *__restrict__ lcodes, int
 // builds the query's LUT -2 P[q] (L2 / cosine; -P[q] for dot) in LDS ONCE (the
 // list term T[l][j][c_j] is folded into the per-row tau at index time), and
 // keeps ONE streaming top-kk over its whole segment (the threshold tightens
-// across lists).  Rows stream as 16-B code pieces of the 64-row
-// blocked layout, PQ_R rows per thread per round.
+// across lists).  Rows stream as 16-B code pieces of the row-major list
+// layout, PQ_R rows per thread per round.
 __global__ __launch_bounds__(PQ_THREADS) void pq_query_scan_kernel(
     const uint8_t *__restrict__ lcodes, int m, int mp, const int64_t *__restrict__ loff,
     const uint32_t *__restrict__ lslot, const float *__restrict__ rowaux_f, int nprobe,
@@ -1741,7 +1787,7 @@ __device__ __forceinline__ float e4m3_round(float v) {
 	(void)frexpf(a, &e);  // a = f 2^e, f in [0.5, 1): exponent e - 1
 	const int E = e - 1 > -6 ? e - 1 : -6;
 	const float ulp = ldexpf(1.0f, E - 3);
-	const float r = fminf(__fmul_rn(rintf(__fdiv_rn(a, ulp)), ulp), 448.0f);
+	const float r = fminf(mul_nc(rintf(__fdiv_rn(a, ulp)), ulp), 448.0f);
 	return copysignf(r, v);
 }
 
@@ -1760,7 +1806,7 @@ __global__ __launch_bounds__(256) void pq_query_fp8_kernel(const float *__restri
 	const float sc = __fdiv_rn(mx, 448.0f);
 	float *y = Qo + (int64_t)q * qld;
 	for (int i = t; i < qld; i += 256)
-		y[i] = (i < dim && sc > 0.0f) ? __fmul_rn(e4m3_round(__fdiv_rn(x[i], sc)), sc) : 0.0f;
+		y[i] = (i < dim && sc > 0.0f) ? mul_nc(e4m3_round(__fdiv_rn(x[i], sc)), sc) : 0.0f;
 }
 
 void launch_pq_query_fp8(const float *Q, int qld, int nq, int dim, float *Qo, hipStream_t st) {
@@ -1771,7 +1817,16 @@ void launch_pq_query_fp8(const float *Q, int qld, int nq, int dim, float *Qo, hi
 // D = max_j (max_c L[j][c] - lo_j) / 255 (1 if 0), u[j][c] = min(255,
 // rint((L[j][c] - lo_j) * (1 / D))), L0 = sum_j lo_j (j ascending).
 // ADC(row) = ((d0 + tau) + L0) + D * sum_j u[j][c_j]  (oracle/ivf.py pq_lut_u8)
-__global__ __launch_bounds__(256) void pq_lut_u8_kernel(const float *__restrict__ P, int m, float sP,
+// Layout of lut8[q]: [j][c] (m x 256 bytes), or, for the bank-conflict-free
+// fast scan (wb = m / 32 > 0), its LUT-build order [x][c >> 4][b][c & 15]
+// with j = 4 wb (b >> 2) + 4 x + (b & 3): the 32 lanes that fill one LDS
+// store group read 512 contiguous bytes
+__host__ __device__ __forceinline__ int lut8_index(int wb, int j, int c) {
+	if (wb == 0) return j * PQ_K + c;
+	const int pp = j / (4 * wb), rem = j - pp * 4 * wb, x = rem >> 2, b = 4 * pp + (rem & 3);
+	return ((x * 16 + (c >> 4)) * 32 + b) * 16 + (c & 15);
+}
+__global__ __launch_bounds__(256) void pq_lut_u8_kernel(const float *__restrict__ P, int m, float sP, int wb,
                                                         uint8_t *__restrict__ lut8, float2 *__restrict__ qpar) {
 	__shared__ float lo[PQ_MAX_M], sp[PQ_MAX_M];
 	__shared__ float dsh;
@@ -1780,19 +1835,19 @@ __global__ __launch_bounds__(256) void pq_lut_u8_kernel(const float *__restrict_
 	if (t < m) {
 		float a = F_INF, b = -F_INF;
 		for (int c = 0; c < PQ_K; ++c) {
-			const float v = __fmul_rn(sP, Pq[t * PQ_K + c]);
+			const float v = mul_nc(sP, Pq[t * PQ_K + c]);
 			a = fminf(a, v);
 			b = fmaxf(b, v);
 		}
 		lo[t] = a;
-		sp[t] = __fsub_rn(b, a);
+		sp[t] = sub_nc(b, a);
 	}
 	__syncthreads();
 	if (t == 0) {
 		float mxs = 0.0f, l0 = 0.0f;
 		for (int j = 0; j < m; ++j) {
 			mxs = fmaxf(mxs, sp[j]);
-			l0 = __fadd_rn(l0, lo[j]);
+			l0 = add_nc(l0, lo[j]);
 		}
 		const float D = mxs > 0.0f ? __fdiv_rn(mxs, 255.0f) : 1.0f;
 		dsh = D;
@@ -1802,14 +1857,15 @@ __global__ __launch_bounds__(256) void pq_lut_u8_kernel(const float *__restrict_
 	const float inv = __fdiv_rn(1.0f, dsh);
 	uint8_t *o = lut8 + (int64_t)q * m * PQ_K;
 	for (int e = t; e < m * PQ_K; e += 256) {
-		const float v = __fmul_rn(sP, Pq[e]);
-		const float u = fminf(rintf(__fmul_rn(__fsub_rn(v, lo[e >> 8]), inv)), 255.0f);
-		o[e] = (uint8_t)u;
+		const float v = mul_nc(sP, Pq[e]);
+		const float u = fminf(rintf(mul_nc(sub_nc(v, lo[e >> 8]), inv)), 255.0f);
+		o[lut8_index(wb, e >> 8, e & 255)] = (uint8_t)u;
 	}
 }
 
+static int pq_bank_w(int m);
 void launch_pq_lut_u8(const float *P, int nq, int m, float sP, uint8_t *lut8, float2 *qpar, hipStream_t st) {
-	pq_lut_u8_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(P, m, sP, lut8, qpar);
+	pq_lut_u8_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(P, m, sP, pq_bank_w(m), lut8, qpar);
 }
 
 // Work items are laid out XCD-major: the lists l = x, x + 8, x + 16, ... first
@@ -1871,6 +1927,35 @@ __global__ __launch_bounds__(1024) void pq_fast_items_kernel(const int *__restri
 	}
 }
 
+// itab[2 it], itab[2 it + 1] = (list, row chunk, -, -), (the 4 pair ids of the
+// item's query group, -1 past the group): an item's whole description in one
+// 32-B read (pq_fast_scan_bank_kernel), instead of a binary search over
+// item_off and the pair ids behind it (a chain of dependent global reads at
+// every item).  One thread per list position.
+__global__ __launch_bounds__(256) void pq_fast_table_kernel(const int *__restrict__ pstart,
+                                                            const int64_t *__restrict__ loff,
+                                                            const int *__restrict__ pairs, int nlist,
+                                                            const int *__restrict__ item_off, int4 *__restrict__ itab,
+                                                            int cap) {
+	const int pos = blockIdx.x * blockDim.x + threadIdx.x;
+	if (pos >= nlist) return;
+	const int l = lperm(nlist, pos);
+	const int np = pstart[l + 1] - pstart[l];
+	const int64_t len = loff[l + 1] - loff[l];
+	if (np <= 0 || len <= 0) return;
+	const int nc = (int)((len + FQ_CHUNK - 1) / FQ_CHUNK), ngr = (np + FQ_G - 1) / FQ_G;
+	int it = item_off[pos];
+	for (int g = 0; g < ngr; ++g) {
+		int id[FQ_G];
+		for (int i = 0; i < FQ_G; ++i) id[i] = g * FQ_G + i < np ? pairs[pstart[l] + g * FQ_G + i] : -1;
+		for (int ch = 0; ch < nc; ++ch, ++it) {
+			if (it >= cap) return;
+			itab[2 * it] = make_int4(l, ch, 0, 0);
+			itab[2 * it + 1] = make_int4(id[0], id[1], id[2], id[3]);
+		}
+	}
+}
+
 // Persistent: each workgroup takes work items (one atomic per item, XCD-major).  An item
 // = one 8192-position chunk of list l x up to FQ_G queries probing l: their
 // 8-bit LUTs interleaved in LDS as u32 [j][c] = (u_0, u_1, u_2, u_3)[j][c], so
@@ -1892,7 +1977,7 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 	extern __shared__ __attribute__((aligned(16))) uint8_t fq_smem[];
 	uint32_t *L = reinterpret_cast<uint32_t *>(fq_smem);                  // [m][256]
 	uint64_t *buf = reinterpret_cast<uint64_t *>(fq_smem + (size_t)m * PQ_K * 4);  // [FQ_G][FQ_CAP]
-	__shared__ int cnt[FQ_G], qid[FQ_G], item;
+	__shared__ int cnt[FQ_G], qid[FQ_G], item, nlive;
 	__shared__ uint64_t thr[FQ_G];
 	__shared__ float d0s[FQ_G], dls[FQ_G], l0s[FQ_G];
 	const int t = threadIdx.x;
@@ -2024,10 +2109,10 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 				const int64_t ps = p0 + r;
 				sl = lslot[ps];
 				if (ltau) ta = ltau[ps];
-				const uint8_t *cp = lcodes + ((ps >> 6) * nch * 64 + (ps & 63)) * 16;
+				const uint8_t *cp = lcodes + ps * mp;
 #pragma unroll
 				for (int c = 0; c < NCH; ++c)
-					if (c < nch) w[c] = *reinterpret_cast<const uint4 *>(cp + (int64_t)c * 64 * 16);
+					if (c < nch) w[c] = *reinterpret_cast<const uint4 *>(cp + c * 16);
 			}
 		};
 		// two code buffers, the loop unrolled twice: round i sums one buffer while
@@ -2110,9 +2195,9 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 			bool pass[FQ_G], any = false;
 #pragma unroll
 			for (int i = 0; i < FQ_G; ++i) {
-				float a = ltau ? __fadd_rn(d0s[i], ctau) : d0s[i];
-				a = __fadd_rn(a, l0s[i]);
-				a = __fadd_rn(a, __fmul_rn(dls[i], (float)S[i]));
+				float a = ltau ? add_nc(d0s[i], ctau) : d0s[i];
+				a = add_nc(a, l0s[i]);
+				a = add_nc(a, mul_nc(dls[i], (float)S[i]));
 				key[i] = key64(a, cslot);
 				pass[i] = cslot != SLOT_NONE && qid[i] >= 0 && key[i] <= thr[i];
 #ifdef LHIP_PQ_ABL_NO_CAND
@@ -2120,12 +2205,8 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 #endif
 				any |= pass[i];
 			}
-			// row liveness (a random 4-B read) only for rows under some bound
-#ifdef LHIP_PQ_ABL_NO_ALIVE  // (timing ablation: no liveness read)
+			// (row liveness: checked at the cut and the flush, fq_cut)
 			if (any) {
-#else
-			if (any && slot_alive(rowaux_f, cslot)) {
-#endif
 #pragma unroll
 				for (int i = 0; i < FQ_G; ++i)
 					if (pass[i]) {
@@ -2140,17 +2221,7 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 #ifdef LHIP_PQ_PROF
 					pq_acc[6] += 1;
 #endif
-					uint64_t *b = buf + i * FQ_CAP;
-					const int c = cnt[i];
-					const int n2 = pow2_ceil(c);
-					for (int e = c + t; e < n2; e += FQ_THREADS) b[e] = KEY64_NONE;
-					wg_bitonic_sort(b, n2);
-					if (t == 0 && c >= kk) {
-						thr[i] = b[kk - 1];  // inclusive bound: the kk-th key stays
-						cnt[i] = kk;
-						atomicMin(thrq + qid[i], (unsigned long long)b[kk - 1]);
-					}
-					__syncthreads();
+					fq_cut(buf + i * FQ_CAP, cnt[i], thr[i], qid[i], kk, rowaux_f, thrq, nlive);
 				}
 			}
 			if (t < FQ_G && gprev < thr[t]) thr[t] = gprev;
@@ -2185,7 +2256,7 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 			const uint64_t *b = buf + i * FQ_CAP;
 			for (int e = t; e < cnt[i]; e += FQ_THREADS) {
 				const uint64_t key = b[e];
-				if (key <= th) {
+				if (key <= th && slot_alive(rowaux_f, (uint32_t)key)) {
 					const int p = atomicAdd(ocnt + q, 1);
 					if (p < ocap) out[(int64_t)q * ocap + p] = key;
 				}
@@ -2193,6 +2264,381 @@ __global__ __launch_bounds__(FQ_THREADS) void pq_fast_scan_kernel(
 		}
 		__syncthreads();
 		PQ_T(4);  // flush
+	}
+#ifdef LHIP_PQ_PROF
+	if (t == 0 && blockIdx.x < PQ_PROF_WG)
+		for (int i = 0; i < PQ_PROF_N; ++i) g_pq_prof[blockIdx.x * PQ_PROF_N + i] = pq_acc[i];
+#endif
+}
+
+// The fast scan for m = 32 W (W = 1..3; C5's m = 96 is W = 3), free of LDS
+// bank conflicts.  pq_fast_scan_kernel gives each lane one row: the 32 lanes
+// of a ds_read_b32 group look up 32 random codes of one table, and the bank
+// of a [j][c] entry is c mod 32, so a lookup costs ~3.5 LDS cycles per group
+// instead of 1.  Here 8 lanes share a row: lane p holds the 4W codes of
+// subspaces [4W p, 4W p + 4W) as W words, and the table of subspace
+// j = 4W p + 4x + y (word x, byte y) lives entirely in bank 4p + y.  At
+// sub-step s the lane of row r (r = 0..3 of its 32-lane group) looks up byte
+// y = (s + r) & 3 of word x, so the group's 32 lanes (4 rows x 8 parts) read
+// 32 distinct banks.  The lane builds the entry address from its code byte in
+// one v_perm (byte 1 = the code, byte 0 = its bank offset: 256-B code rows)
+// for x < 2; the third word's tables sit in a compact region with 128-B code
+// rows (bfe + shift-add).  A row's 8 partial sums meet by DPP (3 steps), and
+// lane p < 4 keys the row for query p of the item.  Items, LUT values, keys,
+// bounds and outputs are pq_fast_scan_kernel's (same integers summed: the
+// order of the sums is free), so the results are identical.
+// 1024 threads (16 waves: four per SIMD, for the VALU issue and the LDS / HBM
+// latencies; one workgroup per CU holds the 128 KiB of LUT and buffers), four
+// row steps per lane and round, the next round's rows in flight.  Codes, slots
+// and row terms come by buffer loads from per-item resources: the whole
+// per-lane part of an address is set once per item, the round and step parts
+// are scalar offsets, and rows past the chunk read 0 (out of range).
+constexpr int FB_THREADS = 1024;
+constexpr int FB_META_BYTES = 192;
+constexpr uint32_t FB_RSRC3 = 0x00020000u;  // gfx9 buffer descriptor word 3 (raw bytes, range checked)
+// cache policy of the row streams (read once): nt (aux 2) keeps the L2 for the
+// 4 x 24 KiB of LUT bytes every item re-reads
+#ifndef LHIP_FB_AUX
+#define LHIP_FB_AUX 2
+#endif
+constexpr int FB_AUX = LHIP_FB_AUX;
+// LUT entries by absolute LDS address (the kernel has no static LDS, so its
+// dynamic allocation starts at address 0): the constant part of an entry's
+// address then folds into the ds immediate instead of a per-lookup add
+__device__ __forceinline__ uint32_t lds_ld32(uint32_t a) {
+	return *(const __attribute__((address_space(3))) uint32_t *)(size_t)a;
+}
+__device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) {
+	*(__attribute__((address_space(3))) uint32_t *)(size_t)a = v;
+}
+constexpr int FB_RS = 4;                            // row steps per lane and round
+constexpr int FB_ROWS = FB_THREADS / 8 * FB_RS;     // rows per round (512)
+template <int W>
+__global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
+    const uint8_t *__restrict__ lcodes, const int64_t *__restrict__ loff, const uint32_t *__restrict__ lslot,
+    const float *__restrict__ rowaux_f, int nlist, int nprobe, const int *__restrict__ pstart,
+    const int *__restrict__ pairs, const int *__restrict__ item_off, const int *__restrict__ xbeg,
+    const float *__restrict__ probe_d, const float *__restrict__ ltau, const uint8_t *__restrict__ lut8,
+    const float2 *__restrict__ qpar, int kk, int *__restrict__ work, unsigned long long *__restrict__ thrq,
+    int *__restrict__ ocnt, uint64_t *__restrict__ out, int ocap, const int4 *__restrict__ itab) {
+	constexpr int MT = 32 * W;
+	constexpr int NPERM = W >= 2 ? 2 : 0, NCOMP = W - NPERM;
+	constexpr int PBASE = NCOMP * 32768;  // the v_perm region (words 0, 1) after the compact one
+	// no static LDS (see lds_ld32); FB_META_BYTES of per-item state follow the candidate buffers
+	extern __shared__ __attribute__((aligned(16))) uint8_t fq_smem[];
+	uint64_t *buf = reinterpret_cast<uint64_t *>(fq_smem + MT * PQ_K * 4);  // [FQ_G][FQ_CAP]
+	uint64_t *thr = buf + FQ_G * FQ_CAP;
+	int *cnt = reinterpret_cast<int *>(thr + FQ_G), *qid = cnt + FQ_G;
+	float *d0s = reinterpret_cast<float *>(qid + FQ_G), *dls = d0s + FQ_G, *l0s = dls + FQ_G;
+	int &item = *reinterpret_cast<int *>(l0s + FQ_G), &nlive = (&item)[1];
+	int4 *nent = reinterpret_cast<int4 *>(l0s + FQ_G + 4);  // the item's itab entry
+	const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+	const int p = lane & 7, rw = lane >> 3, r = rw & 3, pq = p & 3;
+	// per sub-step s (code byte y = (s + r) & 3, bank b = 4p + y): byte s of lb4 /
+	// lb8 is 4b / 8b, and ysel[s] makes v_perm(lb, word, ysel[s]) = (code << 8) | byte s
+	// of lb: the entry address 256 code + 4b in the v_perm region, and
+	// (256 code + 8b) >> 1 = 128 code + 4b in the compact one
+	uint32_t ysel[4], lb4 = 0u, lb8 = 0u;
+#pragma unroll
+	for (int s = 0; s < 4; ++s) {
+		const uint32_t y = (uint32_t)((s + r) & 3), bk = 4u * (uint32_t)p + y;
+		ysel[s] = 0x0c0c0000u | (y << 8) | (4u + (uint32_t)s);
+		lb4 |= (4u * bk) << (8 * s);
+		lb8 |= (8u * bk) << (8 * s);
+	}
+	// the lane's row within a round step, and its per-item buffer offsets
+	const uint32_t lrow = (uint32_t)((wv << 3) + rw);
+	const uint32_t vcode = lrow * MT + 4 * W * p, vrow = lrow * 4;
+	int xc = blockIdx.x & (NXCD - 1), tries = 0;  // (thread 0's claim state, as pq_fast_scan_kernel)
+#ifdef LHIP_PQ_PROF
+	uint64_t pq_acc[PQ_PROF_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+	uint64_t pq_t = __builtin_amdgcn_s_memtime();
+#endif
+	// thread 0 issues the claim of the NEXT item when an item starts and resolves
+	// it in the item's first round, where wave 0 also reads its itab entry (a
+	// scalar read): an item starts with one global round trip (its LUT) instead
+	// of three (claim, entry, LUT)
+	auto claim = [&]() -> int {
+		int itc = -1;
+		while (tries < NXCD) {
+			const int c = atomicAdd(work + xc, 1);
+			if (c < xbeg[xc + 1] - xbeg[xc]) {
+				itc = xbeg[xc] + c;
+				break;
+			}
+			xc = (xc + 1) & (NXCD - 1);
+			++tries;
+		}
+		return itc;
+	};
+	if (t == 0) {
+		const int c = claim();
+		item = c;
+		if (c >= 0) {
+			nent[0] = itab[2 * c];
+			nent[1] = itab[2 * c + 1];
+		}
+	}
+	__syncthreads();
+	for (;;) {
+		PQ_T(0);
+		const int it = item;
+		if (it < 0) break;
+#ifdef LHIP_PQ_PROF
+		pq_acc[5] += 1;
+#endif
+		const int4 e0 = nent[0], e1 = nent[1];
+		// (thread 0: the next claim's atomic, issued now, its result read in round 0)
+		int pend = 0;
+		if (t == 0 && tries < NXCD) pend = atomicAdd(work + xc, 1);
+		const int l = e0.x, ch = e0.y;
+		const int ids[FQ_G] = {e1.x, e1.y, e1.z, e1.w};
+		int qv[FQ_G];
+#pragma unroll
+		for (int i = 0; i < FQ_G; ++i) qv[i] = ids[i] >= 0 ? ids[i] / nprobe : -1;
+		const int64_t p0 = loff[l], len = loff[l + 1] - p0;
+		if (t < FQ_G) {
+			const int id = t == 0 ? e1.x : t == 1 ? e1.y : t == 2 ? e1.z : e1.w;
+			const int q = id >= 0 ? id / nprobe : -1;
+			if (q >= 0) {
+				d0s[t] = probe_d[id];
+				const float2 qp = qpar[q];
+				dls[t] = qp.x;
+				l0s[t] = qp.y;
+				thr[t] = thrq[q];
+			} else {
+				thr[t] = 0;
+			}
+			qid[t] = q;
+			cnt[t] = 0;
+		}
+		// LUT: thread (word set xs, piece cp of 16 codes, bank b = 4 pp + yy) writes
+		// the 16 entries of subspaces 4W pp + 4x + yy for x = xs, xs + 2: the 32 lanes
+		// of a store group write 32 distinct banks
+		{
+			constexpr int NX = (W + 1) / 2;
+			const int b = t & 31, cp = (t >> 5) & 15, xs = t >> 9;
+			uint4 w[NX][FQ_G];
+#pragma unroll
+			for (int xi = 0; xi < NX; ++xi) {
+				const int x = xs + 2 * xi;
+#pragma unroll
+				for (int i = 0; i < FQ_G; ++i)
+					w[xi][i] = x < W && qv[i] >= 0 ? reinterpret_cast<const uint4 *>(
+					                                      lut8 + (int64_t)qv[i] * MT * PQ_K)[(x * 16 + cp) * 32 + b]
+					                                : make_uint4(0u, 0u, 0u, 0u);
+			}
+#pragma unroll
+			for (int xi = 0; xi < NX; ++xi) {
+				const int x = xs + 2 * xi;
+				if (x >= W) continue;
+				const uint32_t dst = x < NPERM ? PBASE + 128 * x + 4 * b : (x - NPERM) * 32768 + 4 * b;
+				const uint32_t cstride = x < NPERM ? 256 : 128;
+#pragma unroll
+				for (int sub = 0; sub < 4; ++sub) {
+					const uint4 *wx = w[xi];
+					const uint32_t w0 = sub == 0 ? wx[0].x : sub == 1 ? wx[0].y : sub == 2 ? wx[0].z : wx[0].w;
+					const uint32_t w1 = sub == 0 ? wx[1].x : sub == 1 ? wx[1].y : sub == 2 ? wx[1].z : wx[1].w;
+					const uint32_t w2 = sub == 0 ? wx[2].x : sub == 1 ? wx[2].y : sub == 2 ? wx[2].z : wx[2].w;
+					const uint32_t w3 = sub == 0 ? wx[3].x : sub == 1 ? wx[3].y : sub == 2 ? wx[3].z : wx[3].w;
+					const uint32_t a01 = __builtin_amdgcn_perm(w1, w0, 0x05010400u);
+					const uint32_t a23 = __builtin_amdgcn_perm(w3, w2, 0x05010400u);
+					const uint32_t b01 = __builtin_amdgcn_perm(w1, w0, 0x07030602u);
+					const uint32_t b23 = __builtin_amdgcn_perm(w3, w2, 0x07030602u);
+					const uint32_t c = (uint32_t)(cp * 16 + sub * 4);
+					lds_st32(dst + (c + 0) * cstride, __builtin_amdgcn_perm(a23, a01, 0x05040100u));
+					lds_st32(dst + (c + 1) * cstride, __builtin_amdgcn_perm(a23, a01, 0x07060302u));
+					lds_st32(dst + (c + 2) * cstride, __builtin_amdgcn_perm(b23, b01, 0x05040100u));
+					lds_st32(dst + (c + 3) * cstride, __builtin_amdgcn_perm(b23, b01, 0x07060302u));
+				}
+			}
+		}
+		__syncthreads();
+		PQ_T(1);
+		const int64_t c0 = (int64_t)ch * FQ_CHUNK, c1 = len < c0 + FQ_CHUNK ? len : c0 + FQ_CHUNK;
+		const uint32_t nrow = (uint32_t)(c1 - c0);  // rows of the item
+		// the item's rows [c0, c1) as buffer resources: rows past the end read 0
+		const __amdgpu_buffer_rsrc_t rcode =
+		    __builtin_amdgcn_make_buffer_rsrc((void *)(lcodes + (p0 + c0) * MT), 0, (int)(nrow * MT), FB_RSRC3);
+		const __amdgpu_buffer_rsrc_t rslot =
+		    __builtin_amdgcn_make_buffer_rsrc((void *)(lslot + p0 + c0), 0, (int)(nrow * 4), FB_RSRC3);
+		const __amdgpu_buffer_rsrc_t rtau =
+		    __builtin_amdgcn_make_buffer_rsrc((void *)(ltau ? ltau + p0 + c0 : nullptr), 0, ltau ? (int)(nrow * 4) : 0,
+		                                      FB_RSRC3);
+		const int myq = qid[pq];
+		const float myd0 = d0s[pq], mydl = dls[pq], myl0 = l0s[pq];
+		uint64_t mythr = thr[pq];
+		struct Rows {
+			uint32_t cw[FB_RS][W];
+			uint32_t sl[FB_RS];
+			float ta[FB_RS];
+		};
+		// row step k of the round at item row rb: the wave's 8 consecutive rows
+		auto load = [&](uint32_t rb, Rows &R) __attribute__((always_inline)) {
+#pragma unroll
+			for (int k = 0; k < FB_RS; ++k) {
+				const uint32_t srow = rb + (uint32_t)(k * (FB_THREADS / 8));  // (scalar)
+				if constexpr (W == 3) {
+					const auto v = __builtin_amdgcn_raw_buffer_load_b96(rcode, vcode, (int)(srow * MT), FB_AUX);
+					R.cw[k][0] = v[0];
+					R.cw[k][1] = v[1];
+					R.cw[k][2] = v[2];
+				} else if constexpr (W == 2) {
+					const auto v = __builtin_amdgcn_raw_buffer_load_b64(rcode, vcode, (int)(srow * MT), FB_AUX);
+					R.cw[k][0] = v[0];
+					R.cw[k][1] = v[1];
+				} else {
+					R.cw[k][0] = __builtin_amdgcn_raw_buffer_load_b32(rcode, vcode, (int)(srow * MT), FB_AUX);
+				}
+				const uint32_t sl = __builtin_amdgcn_raw_buffer_load_b32(rslot, vrow, (int)(srow * 4), FB_AUX);
+				R.sl[k] = srow + lrow < nrow ? sl : SLOT_NONE;
+				R.ta[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rtau, vrow, (int)(srow * 4), FB_AUX));
+			}
+		};
+		auto round = [&](const Rows &R, Rows &N, uint32_t rpre, uint64_t &gprev, bool first) __attribute__((always_inline)) {
+			uint64_t gthr = KEY64_NONE;  // (the query's bound from its other items: as pq_fast_scan_kernel)
+			if (t < FQ_G && qid[t] >= 0) gthr = __builtin_nontemporal_load(thrq + qid[t]);
+			load(rpre, N);
+			// (the next item: resolved by thread 0 after the prefetch is issued, its
+			// entry read by wave 0 (uniform) and stored before the round's barrier)
+			int nxt = -1;
+			if (first && t == 0) {
+				if (tries < NXCD && pend < xbeg[xc + 1] - xbeg[xc]) {
+					nxt = xbeg[xc] + pend;
+				} else {
+					if (tries < NXCD) {
+						xc = (xc + 1) & (NXCD - 1);
+						++tries;
+					}
+					nxt = claim();
+				}
+			}
+			const int nx = __builtin_amdgcn_readfirstlane(nxt);
+			int4 ne0 = make_int4(0, 0, 0, 0), ne1 = ne0;
+			if (first && wv == 0 && nx >= 0) {
+				ne0 = itab[2 * nx];
+				ne1 = itab[2 * nx + 1];
+			}
+			// two steps' totals are keyed together: lanes p < 4 key step k, lanes
+			// p >= 4 step k + 1, for query p & 3
+			uint32_t va[4 * W];
+			auto lookups = [&](int k, uint32_t (&v)[4 * W]) __attribute__((always_inline)) {
+#pragma unroll
+				for (int x = 0; x < W; ++x)
+#pragma unroll
+					for (int s = 0; s < 4; ++s) {
+						uint32_t a;
+						if (x < NPERM)
+							a = PBASE + 128 * x + __builtin_amdgcn_perm(lb4, R.cw[k][x], ysel[s]);
+						else
+							a = (x - NPERM) * 32768 + (__builtin_amdgcn_perm(lb8, R.cw[k][x], ysel[s]) >> 1);
+						v[4 * x + s] = lds_ld32(a);
+					}
+			};
+			uint64_t key[FB_RS / 2];
+			uint32_t pass = 0u;
+			uint32_t s02[2], s13[2];
+#pragma unroll
+			for (int k = 0; k < FB_RS; ++k) {
+				lookups(k, va);
+				const uint32_t(&v)[4 * W] = va;
+				uint32_t e02 = 0u, e13 = 0u;
+#pragma unroll
+				for (int e = 0; e < 4 * W; ++e) {
+					e02 += v[e] & 0x00FF00FFu;
+					e13 += __builtin_amdgcn_perm(0u, v[e], 0x0c030c01u);  // bytes 1, 3 -> 0, 2
+				}
+				s02[k & 1] = e02;
+				s13[k & 1] = e13;
+				if (k & 1) {
+					// the rows' 8 parts: xor 1, xor 2 (quad_perm), then 7 - i (row_half_mirror);
+					// four chains interleaved
+#pragma unroll
+					for (int h = 0; h < 2; ++h) {
+						s02[h] += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s02[h], 0xB1, 0xF, 0xF, false);
+						s13[h] += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s13[h], 0xB1, 0xF, 0xF, false);
+					}
+#pragma unroll
+					for (int h = 0; h < 2; ++h) {
+						s02[h] += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s02[h], 0x4E, 0xF, 0xF, false);
+						s13[h] += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s13[h], 0x4E, 0xF, 0xF, false);
+					}
+#pragma unroll
+					for (int h = 0; h < 2; ++h) {
+						s02[h] += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s02[h], 0x141, 0xF, 0xF, false);
+						s13[h] += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s13[h], 0x141, 0xF, 0xF, false);
+					}
+					const int h = p >> 2;  // which of the two steps this lane keys
+					const int kh = k - 1 + h;
+					const uint32_t sv = (p & 1) ? (h ? s13[1] : s13[0]) : (h ? s02[1] : s02[0]);
+					const uint32_t S = (p & 2) ? (sv >> 16) : (sv & 0xFFFFu);
+					const uint32_t sl = h ? R.sl[k] : R.sl[k - 1];
+					const float ta = h ? R.ta[k] : R.ta[k - 1];
+					float a = ltau ? add_nc(myd0, ta) : myd0;
+					a = add_nc(a, myl0);
+					a = add_nc(a, mul_nc(mydl, (float)S));
+					key[k >> 1] = key64(a, sl);
+					(void)kh;
+					if (myq >= 0 && sl != SLOT_NONE && key[k >> 1] <= mythr) pass |= 1u << (k >> 1);  // (liveness: fq_cut, flush)
+				}
+			}
+			// the offers after all row steps: no branch inside the lookup block
+			if (pass) {
+#pragma unroll
+				for (int j = 0; j < FB_RS / 2; ++j)
+					if (pass & (1u << j)) {
+						const int e = atomicAdd(&cnt[pq], 1);
+						buf[pq * FQ_CAP + e] = key[j];
+					}
+			}
+			if (first && t == 0) {  // (every thread read item / nent before the LUT barrier)
+				item = nx;
+				nent[0] = ne0;
+				nent[1] = ne1;
+			}
+			__syncthreads();
+			PQ_T(2);
+			for (int i = 0; i < FQ_G; ++i) {
+				if (cnt[i] > FQ_CAP - FB_ROWS) {  // the next round could overflow: sort, keep kk
+#ifdef LHIP_PQ_PROF
+					pq_acc[6] += 1;
+#endif
+					fq_cut(buf + i * FQ_CAP, cnt[i], thr[i], qid[i], kk, rowaux_f, thrq, nlive);
+				}
+			}
+			if (t < FQ_G && gprev < thr[t]) thr[t] = gprev;
+			gprev = gthr;
+			__syncthreads();
+			mythr = thr[pq];
+			PQ_T(3);
+		};
+		// two row buffers: the next round's rows land while one is summed
+		Rows RA, RB;
+		uint64_t gprev = KEY64_NONE;
+		load(0, RA);
+		for (uint32_t r0 = 0; r0 < nrow; r0 += 2 * FB_ROWS) {
+			round(RA, RB, r0 + FB_ROWS, gprev, r0 == 0);
+			if (r0 + FB_ROWS >= nrow) break;
+			round(RB, RA, r0 + 2 * FB_ROWS, gprev, false);
+		}
+#ifdef LHIP_PQ_PROF
+		for (int i = 0; i < FQ_G; ++i) pq_acc[7] += qid[i] >= 0 ? (uint64_t)cnt[i] : 0;
+#endif
+		for (int i = 0; i < FQ_G; ++i) {
+			const int q = qid[i];
+			if (q < 0) continue;
+			const uint64_t th = thr[i];
+			const uint64_t *b = buf + i * FQ_CAP;
+			for (int e = t; e < cnt[i]; e += FB_THREADS) {
+				const uint64_t key = b[e];
+				if (key <= th && slot_alive(rowaux_f, (uint32_t)key)) {
+					const int o = atomicAdd(ocnt + q, 1);
+					if (o < ocap) out[(int64_t)q * ocap + o] = key;
+				}
+			}
+		}
+		__syncthreads();
+		PQ_T(4);
 	}
 #ifdef LHIP_PQ_PROF
 	if (t == 0 && blockIdx.x < PQ_PROF_WG)
@@ -2216,7 +2662,7 @@ __global__ __launch_bounds__(256) void pq_seed_kernel(const uint8_t *__restrict_
                                                       const int64_t *__restrict__ probe_l,
                                                       const float *__restrict__ probe_d,
                                                       const float *__restrict__ ltau, const uint8_t *__restrict__ lut8,
-                                                      const float2 *__restrict__ qpar, int kk,
+                                                      const float2 *__restrict__ qpar, int kk, int wb,
                                                       unsigned long long *__restrict__ thrq) {
 	__shared__ __attribute__((aligned(16))) uint8_t L[FQ_MAX_M * PQ_K];
 	__shared__ uint64_t keys[PQ_SEED_ROWS];
@@ -2240,21 +2686,21 @@ __global__ __launch_bounds__(256) void pq_seed_kernel(const uint8_t *__restrict_
 			const int64_t ps = p0 + r;
 			const uint32_t slot = lslot[ps];
 			if (slot != SLOT_NONE && slot_alive(rowaux_f, slot)) {
-				const uint8_t *cp = lcodes + ((ps >> 6) * nch * 64 + (ps & 63)) * 16;
+				const uint8_t *cp = lcodes + ps * mp;
 				uint32_t S = 0;
 				for (int c = 0; c < nch; ++c) {
-					const uint4 w = *reinterpret_cast<const uint4 *>(cp + (int64_t)c * 64 * 16);
+					const uint4 w = *reinterpret_cast<const uint4 *>(cp + c * 16);
 					const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
 					for (int u = 0; u < 16; ++u) {
 						const int j = c * 16 + u;
-						if (j < mm) S += L[j * PQ_K + ((wd[u >> 2] >> (8 * (u & 3))) & 255u)];
+						if (j < mm) S += L[lut8_index(wb, j, (int)((wd[u >> 2] >> (8 * (u & 3))) & 255u))];
 					}
 				}
 				// the scan's key: ((d0 + tau) + L0) + D * S, each step rounded
-				float a = ltau ? __fadd_rn(d0, ltau[ps]) : d0;
-				a = __fadd_rn(a, qp.y);
-				a = __fadd_rn(a, __fmul_rn(qp.x, (float)S));
+				float a = ltau ? add_nc(d0, ltau[ps]) : d0;
+				a = add_nc(a, qp.y);
+				a = add_nc(a, mul_nc(qp.x, (float)S));
 				key = key64(a, slot);
 			}
 		}
@@ -2272,26 +2718,42 @@ void launch_pq_seed(const uint8_t *lcodes, int m, int mp, const int64_t *loff, c
                     const float *ltau, const uint8_t *lut8, const float2 *qpar, int kk, uint64_t *thrq, hipStream_t st) {
 	if (nq <= 0 || kk > PQ_SEED_ROWS || m > FQ_MAX_M) return;
 	auto thr = reinterpret_cast<unsigned long long *>(thrq);
+	const int wb = pq_bank_w(m);
 	if (m == 96)
 		pq_seed_kernel<96><<<dim3((unsigned)nq), 256, 0, st>>>(lcodes, m, mp, loff, lslot, rowaux_f, nprobe, probe_l,
-		                                                        probe_d, ltau, lut8, qpar, kk, thr);
+		                                                        probe_d, ltau, lut8, qpar, kk, wb, thr);
 	else
 		pq_seed_kernel<0><<<dim3((unsigned)nq), 256, 0, st>>>(lcodes, m, mp, loff, lslot, rowaux_f, nprobe, probe_l,
-		                                                       probe_d, ltau, lut8, qpar, kk, thr);
+		                                                       probe_d, ltau, lut8, qpar, kk, wb, thr);
 }
+
+// LANCE_HIP_PQ_LANE_ROWS=1: the one-row-per-lane fast scan for every m (A/B of
+// the two forms; the same results)
+static bool pq_scan_lane_rows() {
+	static const bool v = [] {
+		const char *e = getenv("LANCE_HIP_PQ_LANE_ROWS");
+		return e && e[0] == '1';
+	}();
+	return v;
+}
+
+// m / 32 when the fast scan takes the bank-conflict-free form (m = 32, 64, 96), else 0
+static int pq_bank_w(int m) { return (m == 32 || m == 64 || m == 96) && !pq_scan_lane_rows() ? m / 32 : 0; }
 
 int pq_fast_lds_bytes(int m) { return m * PQ_K * 4 + FQ_G * FQ_CAP * 8; }
 
-void launch_pq_fast_items(const int *pstart, const int64_t *loff, int nlist, int *item_off, int *xbeg,
-                          hipStream_t st) {
+void launch_pq_fast_items(const int *pstart, const int64_t *loff, const int *pairs, int nlist, int *item_off,
+                          int *xbeg, int4 *itab, int itab_cap, hipStream_t st) {
 	pq_fast_items_kernel<<<1, 1024, 0, st>>>(pstart, loff, nlist, item_off, xbeg);
+	if (itab) pq_fast_table_kernel<<<dim3((unsigned)((nlist + 255) / 256)), 256, 0, st>>>(pstart, loff, pairs, nlist,
+	                                                                                       item_off, itab, itab_cap);
 }
 
 void launch_pq_fast_scan(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
                          const float *rowaux_f, int nlist, int nprobe, const int *pstart, const int *pairs,
                          const int *item_off, const int *xbeg, const float *probe_d, const float *ltau,
                          const uint8_t *lut8, const float2 *qpar, int kk, int *work, uint64_t *thrq, int *ocnt,
-                         uint64_t *out, int ocap, int grid, hipStream_t st) {
+                         uint64_t *out, int ocap, const int4 *itab, int grid, hipStream_t st) {
 	const int lds = pq_fast_lds_bytes(m);
 	auto go = [&](auto kern) {
 		HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2329,6 +2791,18 @@ void launch_pq_fast_scan(const uint8_t *lcodes, int m, int mp, const int64_t *lo
 		}
 	} dump_{st, grid};
 #endif
+	auto bank = [&](auto kern) {
+		HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+		                           160 * 1024 - 256));
+		kern<<<dim3((unsigned)grid), FB_THREADS, (size_t)(lds + FB_META_BYTES), st>>>(
+		    lcodes, loff, lslot, rowaux_f, nlist, nprobe, pstart, pairs, item_off, xbeg, probe_d, ltau, lut8, qpar,
+		    kk, work, reinterpret_cast<unsigned long long *>(thrq), ocnt, out, ocap, itab);
+	};
+	if (pq_bank_w(m)) {  // m = 32, 64, 96: the bank-conflict-free form (lut8 in its layout)
+		if (m == 96) return bank(pq_fast_scan_bank_kernel<3>);
+		if (m == 64) return bank(pq_fast_scan_bank_kernel<2>);
+		if (m == 32) return bank(pq_fast_scan_bank_kernel<1>);
+	}
 	switch (m) {
 	case 96: go(pq_fast_scan_kernel<96>); break;
 	case 64: go(pq_fast_scan_kernel<64>); break;
