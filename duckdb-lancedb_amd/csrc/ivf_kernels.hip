@@ -27,7 +27,7 @@
 // Development-only timing ablations of pq_fast_scan_kernel (results are wrong
 // when set): only an ablation build (tools/pq_ablate.sh) may turn them on.
 #if !defined(LHIP_ABLATION_BUILD) && (defined(LHIP_PQ_ABL_NO_LUT) || defined(LHIP_PQ_ABL_NO_LOOKUP) || \
-                                      defined(LHIP_PQ_ABL_NO_CAND))
+                                      defined(LHIP_PQ_ABL_NO_CAND) || defined(LHIP_FB_ABL_LUTLOAD))
 #error "PQ ablation switches are for ablation builds only"
 #endif
 
@@ -1927,7 +1927,8 @@ __global__ __launch_bounds__(1024) void pq_fast_items_kernel(const int *__restri
 	}
 }
 
-// itab[2 it], itab[2 it + 1] = (list, row chunk, -, -), (the 4 pair ids of the
+// itab[2 it], itab[2 it + 1] = (list position of the item's first row (lo, hi),
+// its rows, list), (the 4 pair ids of the
 // item's query group, -1 past the group): an item's whole description in one
 // 32-B read (pq_fast_scan_bank_kernel), instead of a binary search over
 // item_off and the pair ids behind it (a chain of dependent global reads at
@@ -1950,7 +1951,9 @@ __global__ __launch_bounds__(256) void pq_fast_table_kernel(const int *__restric
 		for (int i = 0; i < FQ_G; ++i) id[i] = g * FQ_G + i < np ? pairs[pstart[l] + g * FQ_G + i] : -1;
 		for (int ch = 0; ch < nc; ++ch, ++it) {
 			if (it >= cap) return;
-			itab[2 * it] = make_int4(l, ch, 0, 0);
+			const int64_t pos = loff[l] + (int64_t)ch * FQ_CHUNK;
+			const int nrow = (int)min<int64_t>(FQ_CHUNK, len - (int64_t)ch * FQ_CHUNK);
+			itab[2 * it] = make_int4((int)(uint32_t)pos, (int)(pos >> 32), nrow, l);
 			itab[2 * it + 1] = make_int4(id[0], id[1], id[2], id[3]);
 		}
 	}
@@ -2388,15 +2391,56 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 		pq_acc[5] += 1;
 #endif
 		const int4 e0 = nent[0], e1 = nent[1];
-		// (thread 0: the next claim's atomic, issued now, its result read in round 0)
+		// the next item: thread 0 issues its claim in round 0 after the row
+		// prefetch and resolves it at the round's end; wave 0 then reads its entry
+		// (scalar) and stores it at this item's flush.  No wait on a global
+		// atomic or entry sits between two items.
 		int pend = 0;
-		if (t == 0 && tries < NXCD) pend = atomicAdd(work + xc, 1);
-		const int l = e0.x, ch = e0.y;
+		int4 ne0 = make_int4(0, 0, 0, 0), ne1 = ne0;
+		const int64_t pos0 = (int64_t)(((uint64_t)(uint32_t)e0.y << 32) | (uint32_t)e0.x);
+		const uint32_t nrow = (uint32_t)e0.z;  // rows of the item, from list position pos0
 		const int ids[FQ_G] = {e1.x, e1.y, e1.z, e1.w};
 		int qv[FQ_G];
 #pragma unroll
 		for (int i = 0; i < FQ_G; ++i) qv[i] = ids[i] >= 0 ? ids[i] / nprobe : -1;
-		const int64_t p0 = loff[l], len = loff[l + 1] - p0;
+		// the item's rows as buffer resources (rows past the end read 0); round 0's
+		// rows are requested before the LUT build, in the same round trip as its reads
+		const __amdgpu_buffer_rsrc_t rcode =
+		    __builtin_amdgcn_make_buffer_rsrc((void *)(lcodes + pos0 * MT), 0, (int)(nrow * MT), FB_RSRC3);
+		const __amdgpu_buffer_rsrc_t rslot =
+		    __builtin_amdgcn_make_buffer_rsrc((void *)(lslot + pos0), 0, (int)(nrow * 4), FB_RSRC3);
+		const __amdgpu_buffer_rsrc_t rtau =
+		    __builtin_amdgcn_make_buffer_rsrc((void *)(ltau ? ltau + pos0 : nullptr), 0, ltau ? (int)(nrow * 4) : 0,
+		                                      FB_RSRC3);
+		struct Rows {
+			uint32_t cw[FB_RS][W];
+			uint32_t sl[FB_RS];
+			float ta[FB_RS];
+		};
+		// row step k of the round at item row rb: the wave's 8 consecutive rows
+		auto load = [&](uint32_t rb, Rows &R) __attribute__((always_inline)) {
+#pragma unroll
+			for (int k = 0; k < FB_RS; ++k) {
+				const uint32_t srow = rb + (uint32_t)(k * (FB_THREADS / 8));  // (scalar)
+				if constexpr (W == 3) {
+					const auto v = __builtin_amdgcn_raw_buffer_load_b96(rcode, vcode, (int)(srow * MT), FB_AUX);
+					R.cw[k][0] = v[0];
+					R.cw[k][1] = v[1];
+					R.cw[k][2] = v[2];
+				} else if constexpr (W == 2) {
+					const auto v = __builtin_amdgcn_raw_buffer_load_b64(rcode, vcode, (int)(srow * MT), FB_AUX);
+					R.cw[k][0] = v[0];
+					R.cw[k][1] = v[1];
+				} else {
+					R.cw[k][0] = __builtin_amdgcn_raw_buffer_load_b32(rcode, vcode, (int)(srow * MT), FB_AUX);
+				}
+				const uint32_t sl = __builtin_amdgcn_raw_buffer_load_b32(rslot, vrow, (int)(srow * 4), FB_AUX);
+				R.sl[k] = srow + lrow < nrow ? sl : SLOT_NONE;
+				R.ta[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rtau, vrow, (int)(srow * 4), FB_AUX));
+			}
+		};
+		Rows RA, RB;
+		load(0, RA);
 		if (t < FQ_G) {
 			const int id = t == 0 ? e1.x : t == 1 ? e1.y : t == 2 ? e1.z : e1.w;
 			const int q = id >= 0 ? id / nprobe : -1;
@@ -2424,9 +2468,13 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 				const int x = xs + 2 * xi;
 #pragma unroll
 				for (int i = 0; i < FQ_G; ++i)
+#ifdef LHIP_FB_ABL_LUTLOAD  // (timing ablation: no LUT reads)
+					w[xi][i] = make_uint4((uint32_t)qv[i], (uint32_t)b, (uint32_t)cp, (uint32_t)x);
+#else
 					w[xi][i] = x < W && qv[i] >= 0 ? reinterpret_cast<const uint4 *>(
 					                                      lut8 + (int64_t)qv[i] * MT * PQ_K)[(x * 16 + cp) * 32 + b]
 					                                : make_uint4(0u, 0u, 0u, 0u);
+#endif
 			}
 #pragma unroll
 			for (int xi = 0; xi < NX; ++xi) {
@@ -2455,70 +2503,14 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 		}
 		__syncthreads();
 		PQ_T(1);
-		const int64_t c0 = (int64_t)ch * FQ_CHUNK, c1 = len < c0 + FQ_CHUNK ? len : c0 + FQ_CHUNK;
-		const uint32_t nrow = (uint32_t)(c1 - c0);  // rows of the item
-		// the item's rows [c0, c1) as buffer resources: rows past the end read 0
-		const __amdgpu_buffer_rsrc_t rcode =
-		    __builtin_amdgcn_make_buffer_rsrc((void *)(lcodes + (p0 + c0) * MT), 0, (int)(nrow * MT), FB_RSRC3);
-		const __amdgpu_buffer_rsrc_t rslot =
-		    __builtin_amdgcn_make_buffer_rsrc((void *)(lslot + p0 + c0), 0, (int)(nrow * 4), FB_RSRC3);
-		const __amdgpu_buffer_rsrc_t rtau =
-		    __builtin_amdgcn_make_buffer_rsrc((void *)(ltau ? ltau + p0 + c0 : nullptr), 0, ltau ? (int)(nrow * 4) : 0,
-		                                      FB_RSRC3);
 		const int myq = qid[pq];
 		const float myd0 = d0s[pq], mydl = dls[pq], myl0 = l0s[pq];
 		uint64_t mythr = thr[pq];
-		struct Rows {
-			uint32_t cw[FB_RS][W];
-			uint32_t sl[FB_RS];
-			float ta[FB_RS];
-		};
-		// row step k of the round at item row rb: the wave's 8 consecutive rows
-		auto load = [&](uint32_t rb, Rows &R) __attribute__((always_inline)) {
-#pragma unroll
-			for (int k = 0; k < FB_RS; ++k) {
-				const uint32_t srow = rb + (uint32_t)(k * (FB_THREADS / 8));  // (scalar)
-				if constexpr (W == 3) {
-					const auto v = __builtin_amdgcn_raw_buffer_load_b96(rcode, vcode, (int)(srow * MT), FB_AUX);
-					R.cw[k][0] = v[0];
-					R.cw[k][1] = v[1];
-					R.cw[k][2] = v[2];
-				} else if constexpr (W == 2) {
-					const auto v = __builtin_amdgcn_raw_buffer_load_b64(rcode, vcode, (int)(srow * MT), FB_AUX);
-					R.cw[k][0] = v[0];
-					R.cw[k][1] = v[1];
-				} else {
-					R.cw[k][0] = __builtin_amdgcn_raw_buffer_load_b32(rcode, vcode, (int)(srow * MT), FB_AUX);
-				}
-				const uint32_t sl = __builtin_amdgcn_raw_buffer_load_b32(rslot, vrow, (int)(srow * 4), FB_AUX);
-				R.sl[k] = srow + lrow < nrow ? sl : SLOT_NONE;
-				R.ta[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rtau, vrow, (int)(srow * 4), FB_AUX));
-			}
-		};
 		auto round = [&](const Rows &R, Rows &N, uint32_t rpre, uint64_t &gprev, bool first) __attribute__((always_inline)) {
 			uint64_t gthr = KEY64_NONE;  // (the query's bound from its other items: as pq_fast_scan_kernel)
 			if (t < FQ_G && qid[t] >= 0) gthr = __builtin_nontemporal_load(thrq + qid[t]);
 			load(rpre, N);
-			// (the next item: resolved by thread 0 after the prefetch is issued, its
-			// entry read by wave 0 (uniform) and stored before the round's barrier)
-			int nxt = -1;
-			if (first && t == 0) {
-				if (tries < NXCD && pend < xbeg[xc + 1] - xbeg[xc]) {
-					nxt = xbeg[xc] + pend;
-				} else {
-					if (tries < NXCD) {
-						xc = (xc + 1) & (NXCD - 1);
-						++tries;
-					}
-					nxt = claim();
-				}
-			}
-			const int nx = __builtin_amdgcn_readfirstlane(nxt);
-			int4 ne0 = make_int4(0, 0, 0, 0), ne1 = ne0;
-			if (first && wv == 0 && nx >= 0) {
-				ne0 = itab[2 * nx];
-				ne1 = itab[2 * nx + 1];
-			}
+			if (first && t == 0 && tries < NXCD) pend = atomicAdd(work + xc, 1);
 			// two steps' totals are keyed together: lanes p < 4 key step k, lanes
 			// p >= 4 step k + 1, for query p & 3
 			uint32_t va[4 * W];
@@ -2591,10 +2583,25 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 						buf[pq * FQ_CAP + e] = key[j];
 					}
 			}
-			if (first && t == 0) {  // (every thread read item / nent before the LUT barrier)
-				item = nx;
-				nent[0] = ne0;
-				nent[1] = ne1;
+			if (first) {
+				int nxt = -1;
+				if (t == 0) {
+					if (tries < NXCD && pend < xbeg[xc + 1] - xbeg[xc]) {
+						nxt = xbeg[xc] + pend;
+					} else {
+						if (tries < NXCD) {
+							xc = (xc + 1) & (NXCD - 1);
+							++tries;
+						}
+						nxt = claim();
+					}
+					item = nxt;  // (every thread read item before the LUT barrier)
+				}
+				const int nx = __builtin_amdgcn_readfirstlane(nxt);
+				if (wv == 0 && nx >= 0) {
+					ne0 = itab[2 * nx];
+					ne1 = itab[2 * nx + 1];
+				}
 			}
 			__syncthreads();
 			PQ_T(2);
@@ -2613,9 +2620,7 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 			PQ_T(3);
 		};
 		// two row buffers: the next round's rows land while one is summed
-		Rows RA, RB;
 		uint64_t gprev = KEY64_NONE;
-		load(0, RA);
 		for (uint32_t r0 = 0; r0 < nrow; r0 += 2 * FB_ROWS) {
 			round(RA, RB, r0 + FB_ROWS, gprev, r0 == 0);
 			if (r0 + FB_ROWS >= nrow) break;
@@ -2624,6 +2629,10 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 #ifdef LHIP_PQ_PROF
 		for (int i = 0; i < FQ_G; ++i) pq_acc[7] += qid[i] >= 0 ? (uint64_t)cnt[i] : 0;
 #endif
+		if (t == 0) {  // the next item's entry (read in round 0; nent was read before the LUT barrier)
+			nent[0] = ne0;
+			nent[1] = ne1;
+		}
 		for (int i = 0; i < FQ_G; ++i) {
 			const int q = qid[i];
 			if (q < 0) continue;
