@@ -534,7 +534,8 @@ def main_ivf(a):
             bound_flat = a.index_type == "ivf_flat" and a.scan_copy == "on" and K <= 15 and \
                 "ivf_flat_scan=exact" not in a.opt
             kname = (("flat_list_lb_kernel" if bound_flat else "flat_list_scan_kernel") if a.index_type == "ivf_flat" else
-                     "pq_fast_scan_kernel" if fast_pq else "pq_query_scan_kernel")
+                     ("pq_fast_scan_bank_kernel" if a.m in (32, 64, 96) and os.environ.get("LANCE_HIP_PQ_LANE_ROWS") != "1"
+                      else "pq_fast_scan_kernel") if fast_pq else "pq_query_scan_kernel")
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": ivf_traffic(a.config, N, D, BG, kname), "kernel": kname,
                     "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(bytes_launch),

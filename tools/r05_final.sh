@@ -1,0 +1,32 @@
+#!/bin/bash
+# round-5 closing check on one MI355X, in three calls:
+#   A: the committed tree's GPU suite and smoke
+#   B: the driver's bench command, its rocprofv3 kernel stats, the other configs' lines, per-rank
+#      shapes, the in-process two-shard form, and the C5 step's kernel stats
+#   C: PMC traffic passes of each config's dominant kernel (tools/pmc_configs.sh)
+source tools/gpu_step.sh
+T=${2:-r05f}
+case $1 in
+A)
+	step ${T}_pytest 1100 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread
+	step ${T}_smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"
+	;;
+B)
+	step ${T}_bench_c2 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+	step ${T}_prof_c2 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof_c2 -o run -- python3 bench.py --steps 20 --no-cpu-baseline --no-recall --no-host-batch
+	python3 tools/trace_kernels.py gpurun_out/${T}_prof_c2/run_kernel_trace.csv 20 > gpurun_out/${T}_c2_step_kernels.txt 2>&1
+	step ${T}_bench_nstar 300 python -u bench.py --config nstar --steps 10 --recall-queries 64 --no-cpu-baseline --no-host-batch
+	step ${T}_bench_c3 400 python -u bench.py --config c3 --steps 10 --recall-queries 64 --no-cpu-baseline --no-host-batch
+	step ${T}_bench_c4 400 python -u bench.py --config c4 --steps 10 --no-cpu-baseline
+	step ${T}_bench_c5 400 python -u bench.py --config c5 --steps 10 --no-cpu-baseline
+	step ${T}_bench_c1 300 python -u bench.py --config c1 --steps 20 --no-cpu-baseline
+	step ${T}_rank_c2s8 200 python -u bench.py --n 125000 --steps 30 --no-cpu-baseline --no-host-batch
+	step ${T}_rank_nstar8 200 python -u bench.py --n 1250000 --steps 30 --no-cpu-baseline --no-host-batch
+	step ${T}_inproc 300 python -u bench.py --inproc --inproc-devices 0,0 --steps 20 --no-cpu-baseline --no-host-batch
+	step ${T}_prof_c5 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof_c5 -o run -- python3 bench.py --config c5 --steps 10 --no-cpu-baseline --no-recall --no-host-batch
+	rm -f gpurun_out/${T}_prof_c*/run_kernel_trace.csv.gz
+	;;
+C)
+	step ${T}_pmc 1100 bash tools/pmc_configs.sh $T c2 nstar c3 c4 c5
+	;;
+esac
