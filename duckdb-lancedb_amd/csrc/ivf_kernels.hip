@@ -1603,18 +1603,44 @@ void launch_flat_list_scan(const StoreView &s, const int *blk_list, const int64_
 // IVF_PQ
 // ---------------------------------------------------------------------------
 // P[q][j][c] = sum_t q_{j,t} y_{j,c,t}  (f32, t in order, no contraction)
+// (a workgroup per (PQ_PQB queries, sub-space): the codebook slice is read once
+// for the group; one query per workgroup was 24576 tiny workgroups for C5,
+// ~90 us of workgroup dispatch)
+constexpr int PQ_PQB = 8, PQ_PDS = 16;
 __global__ __launch_bounds__(256) void pq_P_kernel(const float *__restrict__ Q, int qld, const float *__restrict__ cb,
-                                                   int m, int dsub, float *__restrict__ P) {
-	const int q = blockIdx.x, j = blockIdx.y, c = threadIdx.x;
-	const float *x = Q + (int64_t)q * qld + j * dsub;
+                                                   int nq, int m, int dsub, float *__restrict__ P) {
+	const int q0 = blockIdx.x * PQ_PQB, j = blockIdx.y, c = threadIdx.x;
 	const float *y = cb + ((int64_t)j * PQ_K + c) * dsub;
-	float acc = 0.0f;
-	for (int t = 0; t < dsub; ++t) acc = add_nc(acc, mul_nc(x[t], y[t]));
-	P[((int64_t)q * m + j) * PQ_K + c] = acc;
+	if (dsub <= PQ_PDS) {
+		// every load in flight before the sums (a runtime-length loop waited on each)
+		float yv[PQ_PDS];
+#pragma unroll
+		for (int t = 0; t < PQ_PDS; ++t) yv[t] = t < dsub ? y[t] : 0.0f;
+		for (int qi = 0; qi < PQ_PQB && q0 + qi < nq; ++qi) {
+			const int q = q0 + qi;
+			const float *x = Q + (int64_t)q * qld + j * dsub;
+			float xv[PQ_PDS];
+#pragma unroll
+			for (int t = 0; t < PQ_PDS; ++t) xv[t] = t < dsub ? x[t] : 0.0f;
+			float acc = 0.0f;
+#pragma unroll
+			for (int t = 0; t < PQ_PDS; ++t)
+				if (t < dsub) acc = add_nc(acc, mul_nc(xv[t], yv[t]));
+			P[((int64_t)q * m + j) * PQ_K + c] = acc;
+		}
+		return;
+	}
+	for (int qi = 0; qi < PQ_PQB && q0 + qi < nq; ++qi) {
+		const int q = q0 + qi;
+		const float *x = Q + (int64_t)q * qld + j * dsub;
+		float acc = 0.0f;
+		for (int t = 0; t < dsub; ++t) acc = add_nc(acc, mul_nc(x[t], y[t]));
+		P[((int64_t)q * m + j) * PQ_K + c] = acc;
+	}
 }
 
 void launch_pq_P(const float *Q, int qld, int nq, const float *cb, int m, int dsub, float *P, hipStream_t st) {
-	pq_P_kernel<<<dim3((unsigned)nq, (unsigned)m), PQ_K, 0, st>>>(Q, qld, cb, m, dsub, P);
+	pq_P_kernel<<<dim3((unsigned)((nq + PQ_PQB - 1) / PQ_PQB), (unsigned)m), PQ_K, 0, st>>>(Q, qld, cb, nq, m, dsub, P);
 }
 
 constexpr int PQ_THREADS = 512;
@@ -1832,15 +1858,29 @@ __global__ __launch_bounds__(256) void pq_lut_u8_kernel(const float *__restrict_
 	__shared__ float dsh;
 	const int q = blockIdx.x, t = threadIdx.x;
 	const float *Pq = P + (int64_t)q * m * PQ_K;
-	if (t < m) {
-		float a = F_INF, b = -F_INF;
-		for (int c = 0; c < PQ_K; ++c) {
-			const float v = mul_nc(sP, Pq[t * PQ_K + c]);
-			a = fminf(a, v);
-			b = fmaxf(b, v);
+	// per sub-space j (wave w takes j = w, w + 4, ...): min / max over its 256
+	// entries, 4 per lane and a wave reduction (one serial 256-read loop per j was
+	// ~29 us for C5)
+	{
+		const int w = t >> 6, lane = t & 63;
+		for (int j = w; j < m; j += 4) {
+			float a = F_INF, b = -F_INF;
+#pragma unroll
+			for (int i = 0; i < 4; ++i) {
+				const float v = mul_nc(sP, Pq[j * PQ_K + lane + 64 * i]);
+				a = fminf(a, v);
+				b = fmaxf(b, v);
+			}
+#pragma unroll
+			for (int o = 32; o > 0; o >>= 1) {
+				a = fminf(a, __shfl_xor(a, o, 64));
+				b = fmaxf(b, __shfl_xor(b, o, 64));
+			}
+			if (lane == 0) {
+				lo[j] = a;
+				sp[j] = sub_nc(b, a);
+			}
 		}
-		lo[t] = a;
-		sp[t] = sub_nc(b, a);
 	}
 	__syncthreads();
 	if (t == 0) {
@@ -1856,10 +1896,35 @@ __global__ __launch_bounds__(256) void pq_lut_u8_kernel(const float *__restrict_
 	__syncthreads();
 	const float inv = __fdiv_rn(1.0f, dsh);
 	uint8_t *o = lut8 + (int64_t)q * m * PQ_K;
-	for (int e = t; e < m * PQ_K; e += 256) {
-		const float v = mul_nc(sP, Pq[e]);
-		const float u = fminf(rintf(mul_nc(sub_nc(v, lo[e >> 8]), inv)), 255.0f);
-		o[lut8_index(wb, e >> 8, e & 255)] = (uint8_t)u;
+	// 16-byte output chunks: chunk d holds codes c0 .. c0 + 15 of sub-space j
+	// (lut8_index(wb, j, c0 + i) = 16 d + i), from four float4 reads of P
+#pragma unroll 2
+	for (int d = t; d < m * 16; d += 256) {
+		int j, c0;
+		if (wb) {
+			const int b = d & 31, cp = (d >> 5) & 15, x = d >> 9;
+			j = 4 * wb * (b >> 2) + 4 * x + (b & 3);
+			c0 = cp * 16;
+		} else {
+			j = d >> 4;
+			c0 = (d & 15) * 16;
+		}
+		const float4 *src = reinterpret_cast<const float4 *>(Pq + j * PQ_K + c0);
+		const float l = lo[j];
+		uint32_t w[4];
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			const float4 f = src[i];
+			const float fv[4] = {f.x, f.y, f.z, f.w};
+			uint32_t word = 0u;
+#pragma unroll
+			for (int k2 = 0; k2 < 4; ++k2) {
+				const float u = fminf(rintf(mul_nc(sub_nc(mul_nc(sP, fv[k2]), l), inv)), 255.0f);
+				word |= (uint32_t)u << (8 * k2);
+			}
+			w[i] = word;
+		}
+		reinterpret_cast<uint4 *>(o)[d] = make_uint4(w[0], w[1], w[2], w[3]);
 	}
 }
 
@@ -2662,9 +2727,9 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 // keys of a probed list lie at or below it, so no key above it can be among
 // the query's kk smallest (the bound is inclusive, as the scan's).  Without
 // it every query's first items pass every row until a buffer sort sets one.
-constexpr int PQ_SEED_ROWS = 4096;
+constexpr int PQ_SEED_ROWS = 4096, PQ_SEED_THREADS = 1024;  // (4 rows per thread: short per-thread chains)
 template <int MT>
-__global__ __launch_bounds__(256) void pq_seed_kernel(const uint8_t *__restrict__ lcodes, int m, int mp,
+__global__ __launch_bounds__(PQ_SEED_THREADS) void pq_seed_kernel(const uint8_t *__restrict__ lcodes, int m, int mp,
                                                       const int64_t *__restrict__ loff,
                                                       const uint32_t *__restrict__ lslot,
                                                       const float *__restrict__ rowaux_f, int nprobe,
@@ -2682,14 +2747,20 @@ __global__ __launch_bounds__(256) void pq_seed_kernel(const uint8_t *__restrict_
 	const float d0 = probe_d[(int64_t)q * nprobe];
 	const float2 qp = qpar[q];
 	const uint8_t *lq = lut8 + (int64_t)q * mm * PQ_K;
-	for (int i = t; i < mm * PQ_K / 16; i += 256) reinterpret_cast<uint4 *>(L)[i] = reinterpret_cast<const uint4 *>(lq)[i];
+	// the LUT in [j][c] order (lut8 may be in the bank scan's layout: lut8_index)
+	const int wbc = MT > 0 ? (wb ? MT / 32 : 0) : wb;  // (a compile-time divisor for MT = 96)
+	if (wbc == 0) {
+		for (int i = t; i < mm * PQ_K / 16; i += PQ_SEED_THREADS) reinterpret_cast<uint4 *>(L)[i] = reinterpret_cast<const uint4 *>(lq)[i];
+	} else {
+		for (int e = t; e < mm * PQ_K; e += PQ_SEED_THREADS) L[e] = lq[lut8_index(wbc, e >> 8, e & 255)];
+	}
 	const int64_t p0 = loff[l], len = loff[l + 1] - p0;
 	const int n = (int)(len < PQ_SEED_ROWS ? len : PQ_SEED_ROWS);
 	int P = 64;
 	while (P < n) P <<= 1;
 	const int nch = mp >> 4;
 	__syncthreads();
-	for (int r = t; r < P; r += 256) {
+	for (int r = t; r < P; r += PQ_SEED_THREADS) {
 		uint64_t key = KEY64_NONE;
 		if (r < n) {
 			const int64_t ps = p0 + r;
@@ -2703,7 +2774,7 @@ __global__ __launch_bounds__(256) void pq_seed_kernel(const uint8_t *__restrict_
 #pragma unroll
 					for (int u = 0; u < 16; ++u) {
 						const int j = c * 16 + u;
-						if (j < mm) S += L[lut8_index(wb, j, (int)((wd[u >> 2] >> (8 * (u & 3))) & 255u))];
+						if (j < mm) S += L[j * PQ_K + ((wd[u >> 2] >> (8 * (u & 3))) & 255u)];
 					}
 				}
 				// the scan's key: ((d0 + tau) + L0) + D * S, each step rounded
@@ -2729,10 +2800,10 @@ void launch_pq_seed(const uint8_t *lcodes, int m, int mp, const int64_t *loff, c
 	auto thr = reinterpret_cast<unsigned long long *>(thrq);
 	const int wb = pq_bank_w(m);
 	if (m == 96)
-		pq_seed_kernel<96><<<dim3((unsigned)nq), 256, 0, st>>>(lcodes, m, mp, loff, lslot, rowaux_f, nprobe, probe_l,
+		pq_seed_kernel<96><<<dim3((unsigned)nq), PQ_SEED_THREADS, 0, st>>>(lcodes, m, mp, loff, lslot, rowaux_f, nprobe, probe_l,
 		                                                        probe_d, ltau, lut8, qpar, kk, wb, thr);
 	else
-		pq_seed_kernel<0><<<dim3((unsigned)nq), 256, 0, st>>>(lcodes, m, mp, loff, lslot, rowaux_f, nprobe, probe_l,
+		pq_seed_kernel<0><<<dim3((unsigned)nq), PQ_SEED_THREADS, 0, st>>>(lcodes, m, mp, loff, lslot, rowaux_f, nprobe, probe_l,
 		                                                       probe_d, ltau, lut8, qpar, kk, wb, thr);
 }
 
