@@ -498,9 +498,16 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 		s->Qf.need((size_t)n * ld);
 		if (cos) s->Qn.need((size_t)n * dim);
 		launch_ivf_prep(dQ + (int64_t)q0 * dim, n, dim, ld, cos ? 1 : 0, s->Qf.p, cos ? s->Qn.p : nullptr, st);
-		s->Qd.need((size_t)n * ld);
-		s->qn2.need((size_t)n);
-		launch_ivf_qd(s->Qf.p, n, ld, dim, s->Qd.p, s->qn2.p, st);
+		// f64 queries for the exact f64 scans (tail, IVF_FLAT exact / fallback): made
+		// only when one of them runs (the IVF_PQ fast path never reads them)
+		bool qd_ready = false;
+		auto need_qd = [&]() {
+			if (qd_ready) return;
+			s->Qd.need((size_t)n * ld);
+			s->qn2.need((size_t)n);
+			launch_ivf_qd(s->Qf.p, n, ld, dim, s->Qd.p, s->qn2.p, st);
+			qd_ready = true;
+		};
 		HIPCHK(hipGetLastError());
 		HIPCHK(hipStreamSynchronize(st));
 		// coarse: exact top-nprobe partitions (synchronous on the centroid store's stream)
@@ -522,6 +529,7 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 		float *oD = dD + (int64_t)q0 * k;
 		int *oC = dC + q0;
 		if (tail_n > 0) {
+			need_qd();
 			s->tkeys.need((size_t)n * tail_nb * kk);
 			launch_flat_list_scan(sv, nullptr, nullptr, nullptr, nullptr, nullptr, tail_nb, nullptr, nullptr, 1, 1,
 			                      s->n_indexed, tail_n, n, s->Qd.p, s->qn2.p, kk, s->tkeys.p, st);
@@ -568,6 +576,7 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			if (ix->time_kernels) account_list_scan(ix, 2, n, 0);
 		}
 		if (exact_flat) {
+			need_qd();
 			s->keys.need((size_t)n * nprobe * s->maxb * kk);
 			ix->tic(0);
 			launch_flat_list_scan(sv, s->blk_list.p, s->blk_pos0.p, s->lblk0.p, s->loff.p, s->lslot.p, s->nblk,

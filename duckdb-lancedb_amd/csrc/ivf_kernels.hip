@@ -2727,7 +2727,12 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 // keys of a probed list lie at or below it, so no key above it can be among
 // the query's kk smallest (the bound is inclusive, as the scan's).  Without
 // it every query's first items pass every row until a buffer sort sets one.
-constexpr int PQ_SEED_ROWS = 4096, PQ_SEED_THREADS = 1024;  // (4 rows per thread: short per-thread chains)
+// (2048 positions: half the seed's cost of 4096 for the same scan time at C5,
+// while 1024 loosened the bound enough to slow the scan; profiles/r05j_ab_*)
+#ifndef LHIP_SEED_ROWS
+#define LHIP_SEED_ROWS 2048
+#endif
+constexpr int PQ_SEED_ROWS = LHIP_SEED_ROWS, PQ_SEED_THREADS = 1024;  // (2 rows per thread: short per-thread chains)
 template <int MT>
 __global__ __launch_bounds__(PQ_SEED_THREADS) void pq_seed_kernel(const uint8_t *__restrict__ lcodes, int m, int mp,
                                                       const int64_t *__restrict__ loff,
