@@ -62,12 +62,23 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 	for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
 	return v;
 }
-// (distance, label) total order used everywhere: NaN after +inf, then label.
-__device__ __forceinline__ bool hit_less(float da, int64_t la, float db, int64_t lb) {
+// Tie rule of the final (exact-distance) order, per handle (option "tie",
+// LANCE_HIP_TIE): label ascending, or label descending — the order the
+// reference's own golden shows at a tie (lance_optimizer_filter.test:36-44:
+// ids 3 and 4 tie at d = 2.0 and LanceDB returns 4).  Applied as an XOR on the
+// label (int64, labels >= 0) or on the slot of a (key << 32 | slot) word
+// (slots < 2^31; slots ascend with labels): 0 keeps the order, the all-ones
+// pattern below the sign bit reverses it and never forms the all-ones
+// "no entry" word.
+__host__ __device__ __forceinline__ int64_t tie_x64(int desc) { return desc ? INT64_MAX : 0; }
+__host__ __device__ __forceinline__ uint32_t tie_x32(int desc) { return desc ? 0x7FFFFFFFu : 0u; }
+// (distance, label) total order used everywhere: NaN after +inf, then the
+// label under the tie rule tx = tie_x64(desc).
+__device__ __forceinline__ bool hit_less(float da, int64_t la, float db, int64_t lb, int64_t tx) {
 	bool an = __builtin_isnan(da), bn = __builtin_isnan(db);
 	if (an != bn) return bn;
 	if (!an && da != db) return da < db;
-	return la < lb;
+	return (la ^ tx) < (lb ^ tx);
 }
 // unit roundoff used by the bounds; 2^-23 (not 2^-24) leaves room for an
 // accumulation that truncates instead of rounding.

@@ -304,6 +304,7 @@ struct Index {
 	int split_div = 0;
 	int pr_first = 0;    // option "pr_first": pool_refine's first final-mode chunk (0 = the kernel's default)
 	int s8_variant = 0;  // option "scan8_variant": scan8 geometry (release builds: 0 only)
+	int tie_desc = 1;    // option "tie" / LANCE_HIP_TIE: 1 = (distance, label desc), 0 = (distance, label asc)
 	double kt_append_ms = 0.0, kt_dense_ms = 0.0;
 	int64_t kt_append_n = 0, kt_dense_n = 0;
 	int64_t kt_append_rows = 0, kt_append_qpad = 0;
@@ -815,6 +816,11 @@ struct Index {
 // ---- multi-device handles (shards.cpp) ---------------------------------------
 std::vector<int> parse_devices(const std::string &spec);
 std::vector<int> env_devices();
+// tie rule of the final order: "label_desc" (1, the default: the reference's
+// golden at lance_optimizer_filter.test:36-44) or "label_asc" (0); the handle's
+// default comes from LANCE_HIP_TIE, option "tie" sets it per handle
+int parse_tie(const std::string &v);
+int env_tie();
 void shard_init(Index *ix, const std::vector<int> &devs);
 Index *shard_for_add(Index *ix);
 int64_t shard_live(const Index *ix);

@@ -220,7 +220,7 @@ void launch_pq_tau(const uint8_t *codes, const uint32_t *lslot, const int64_t *l
 void launch_ivf_merge(int nq, int nprobe, const int64_t *probe_l, const int *lblk0, int maxb, int kk,
                       const uint64_t *keys, int tail_nb, const uint64_t *tkeys, int K, uint64_t *out, hipStream_t st);
 void launch_keys_to_output(const uint64_t *keys, int nq, int K, int k, const int64_t *labels, int64_t *outL,
-                           float *outD, int *outC, hipStream_t st);
+                           float *outD, int *outC, hipStream_t st, int tie_desc);
 void launch_ivf_refine_final(const StoreView &s, const float *Qf, const uint64_t *ca, int ka, const uint64_t *cb,
                              int kb, int nq, int k, int64_t *outL, float *outD, int *outC, hipStream_t st);
 

@@ -30,8 +30,10 @@ void ivf_free(IvfState *s) { delete s; }
 static StoreView store_view(Index *ix) {
 	// (the IVF_FLAT bound scan streams its own list-order bf16 rows, IvfState::lrows;
 	// the exact list scans, re-ranks and PQ read X)
-	return StoreView{ix->X,  ix->rowaux, ix->dlabels, ix->n_slots, ix->ld, ix->dim, ix->metric, ix->xbf16 ? 1 : 0,
-	                 ix->Xs ? static_cast<const void *>(ix->Xs) : ix->X, (ix->xbf16 || ix->Xs) ? 1 : 0};
+	StoreView sv{ix->X,  ix->rowaux, ix->dlabels, ix->n_slots, ix->ld, ix->dim, ix->metric, ix->xbf16 ? 1 : 0,
+	             ix->Xs ? static_cast<const void *>(ix->Xs) : ix->X, (ix->xbf16 || ix->Xs) ? 1 : 0};
+	sv.tie_desc = ix->tie_desc;
+	return sv;
 }
 
 static int bits_for(int64_t n) {
@@ -226,6 +228,7 @@ static void install_model(Index *ix, int type, int nlist, int m, const float *dC
 	// dot index, L2 otherwise; cosine probes with normalised queries)
 	auto co = std::make_unique<Index>();
 	co->table = "ivf_centroids";
+	co->tie_desc = 0;  // probes at a distance tie: the lower partition id (oracle/ivf.py, flat_knn.c)
 	co->metric = s->metric == METRIC_DOT ? METRIC_DOT : METRIC_L2;
 	co->dim = ix->dim;
 	co->ld = ix->ld;
@@ -585,7 +588,7 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			s->cand_a.need((size_t)n * k);
 			launch_ivf_merge(n, nprobe, s->probe_l.p, s->lblk0.p, s->maxb, kk, s->keys.p, tail_nb,
 			                 tail_n > 0 ? s->tkeys.p : nullptr, k, s->cand_a.p, st);
-			launch_keys_to_output(s->cand_a.p, n, k, k, ix->dlabels, oL, oD, oC, st);
+			launch_keys_to_output(s->cand_a.p, n, k, k, ix->dlabels, oL, oD, oC, st, ix->tie_desc);
 		} else if (s->type == IVF_FLAT) {
 			// bound scan certified every query of the pass
 		} else if (ix->pq_fast && s->m <= FQ_MAX_M && kp <= FQ_MAX_KK) {

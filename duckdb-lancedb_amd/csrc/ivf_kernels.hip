@@ -978,7 +978,7 @@ template <int METRIC, typename T, int G>
 __device__ __forceinline__ void fs_group(const T *__restrict__ X, int ld, int dim, const double *__restrict__ Qd,
                                          const double *__restrict__ qn2, int ng, const uint32_t *sslot,
                                          const int *sq, const int *spair, float4 (*xs)[FS_NP], uint64_t *sk,
-                                         uint64_t *o0, int64_t ostride, int kk) {
+                                         uint64_t *o0, int64_t ostride, int kk, uint32_t sx) {
 	const int t = threadIdx.x;
 	const double *qp[G];
 #pragma unroll
@@ -1019,7 +1019,9 @@ __device__ __forceinline__ void fs_group(const T *__restrict__ X, int ld, int di
 			r = 1.0 - acc[g] / (sqrt(xx) * sqrt(qq));
 		float f = (float)r + 0.0f;
 		if (__builtin_isnan(f)) f = __builtin_nanf("");
-		const uint64_t key = valid ? key64(f, sslot[t]) : KEY64_NONE;
+		// (exact keys: slot ^ sx, the tie rule of the final order; decoded by
+		// whoever reads them: keys_to_output, the re-rank kernels' tail lists)
+		const uint64_t key = valid ? key64(f, sslot[t] ^ sx) : KEY64_NONE;
 		uint64_t *o = o0 + (int64_t)spair[g] * ostride;
 		__syncthreads();  // sk reuse
 		if (kk <= 16) {
@@ -1048,7 +1050,7 @@ __global__ __launch_bounds__(256) void flat_list_scan_kernel(
     const int64_t *__restrict__ blk_pos0, const int *__restrict__ lblk0, const int64_t *__restrict__ loff,
     const uint32_t *__restrict__ lslot, const int *__restrict__ pstart, const int *__restrict__ pairs, int nprobe,
     int maxb, int64_t tail_s0, int64_t tail_n, int nq, const double *__restrict__ Qd, const double *__restrict__ qn2,
-    int kk, uint64_t *__restrict__ out) {
+    int kk, uint64_t *__restrict__ out, uint32_t sx) {
 	__shared__ float4 xs[FLAT_BLK][FS_NP];
 	__shared__ uint32_t sslot[FLAT_BLK];
 	__shared__ uint64_t sk[FLAT_BLK];
@@ -1094,7 +1096,7 @@ __global__ __launch_bounds__(256) void flat_list_scan_kernel(
 		}
 		__syncthreads();
 		// per-item query count decides the register block (f64 work scales with it)
-#define FS_CALL(GG) fs_group<METRIC, T, GG>(X, ld, dim, Qd, qn2, ng, sslot, sq, spair, xs, sk, o0, ostride, kk)
+#define FS_CALL(GG) fs_group<METRIC, T, GG>(X, ld, dim, Qd, qn2, ng, sslot, sq, spair, xs, sk, o0, ostride, kk, sx)
 		if (ng <= 2) FS_CALL(2);
 		else if (ng <= 4) FS_CALL(4);
 		else if (ng <= 8) FS_CALL(8);
@@ -1403,7 +1405,8 @@ __global__ __launch_bounds__(256) void flat_lb_refine_kernel(const T *__restrict
                                                              const float *__restrict__ cut, int k,
                                                              const int64_t *__restrict__ labels,
                                                              int64_t *__restrict__ outL, float *__restrict__ outD,
-                                                             int *__restrict__ outC, int *__restrict__ cert) {
+                                                             int *__restrict__ outC, int *__restrict__ cert,
+                                                             uint32_t sx) {
 	__shared__ uint64_t sk[IVF_TOPK_CAP];
 	__shared__ uint32_t ss[IVF_TOPK_CAP];
 	__shared__ int n;
@@ -1411,15 +1414,16 @@ __global__ __launch_bounds__(256) void flat_lb_refine_kernel(const T *__restrict
 	if (t == 0) n = 0;
 	__syncthreads();
 	for (int i = t; i < M + kb; i += 256) {
+		// (bound keys carry the slot; the tail's exact keys slot ^ sx)
 		const uint64_t key = i < M ? ca[(int64_t)q * M + i] : cbk[(int64_t)q * kb + (i - M)];
-		if (key != KEY64_NONE) ss[atomicAdd(&n, 1)] = (uint32_t)key;
+		if (key != KEY64_NONE) ss[atomicAdd(&n, 1)] = (uint32_t)key ^ (i < M ? 0u : sx);
 	}
 	__syncthreads();
 	const int nc = n;
 	for (int i = w; i < nc; i += 4) {
 		const uint32_t slot = ss[i];
 		const float d = exact_distance<METRIC, T>(X + (int64_t)slot * ld, Qf + (int64_t)q * ld, dim, lane);
-		if (lane == 0) sk[i] = key64(d, slot);
+		if (lane == 0) sk[i] = key64(d, slot ^ sx);
 	}
 	const int np = pow2_ceil(nc);
 	__syncthreads();
@@ -1428,7 +1432,7 @@ __global__ __launch_bounds__(256) void flat_lb_refine_kernel(const T *__restrict
 	const int nout = nc < k ? nc : k;
 	for (int i = t; i < k; i += 256) {
 		if (i < nout) {
-			outL[(int64_t)q * k + i] = labels[(uint32_t)sk[i]];
+			outL[(int64_t)q * k + i] = labels[(uint32_t)sk[i] ^ sx];
 			outD[(int64_t)q * k + i] = key64_dist(sk[i]);
 		} else {
 			outL[(int64_t)q * k + i] = -1;
@@ -1554,7 +1558,8 @@ void launch_flat_lb_refine(const StoreView &s, const float *Qf, const uint64_t *
                            hipStream_t st) {
 	dim3 grid((unsigned)nq);
 	auto go = [&](auto kern, auto X) {
-		kern<<<grid, 256, 0, st>>>(X, s.ld, s.dim, Qf, ca, M, cb, kb, cut, k, s.labels, outL, outD, outC, cert);
+		kern<<<grid, 256, 0, st>>>(X, s.ld, s.dim, Qf, ca, M, cb, kb, cut, k, s.labels, outL, outD, outC, cert,
+		                           tie_x32(s.tie_desc));
 	};
 	if (s.xbf16) {
 		const uint16_t *X = static_cast<const uint16_t *>(s.X);
@@ -1577,7 +1582,7 @@ static void flat_scan_dispatch(const StoreView &s, const int *blk_list, const in
 	const T *X = static_cast<const T *>(s.X);
 	const float *ra = reinterpret_cast<const float *>(s.rowaux);
 	dim3 grid((unsigned)nblk);
-#define FS_ARGS X, s.ld, s.dim, ra, blk_list, blk_pos0, lblk0, loff, lslot, pstart, pairs, nprobe, maxb, tail_s0, tail_n, nq, Qd, qn2, kk, out
+#define FS_ARGS X, s.ld, s.dim, ra, blk_list, blk_pos0, lblk0, loff, lslot, pstart, pairs, nprobe, maxb, tail_s0, tail_n, nq, Qd, qn2, kk, out, tie_x32(s.tie_desc)
 	switch (s.metric) {
 	case METRIC_L2: flat_list_scan_kernel<METRIC_L2, T><<<grid, 256, 0, st>>>(FS_ARGS); break;
 	case METRIC_DOT: flat_list_scan_kernel<METRIC_DOT, T><<<grid, 256, 0, st>>>(FS_ARGS); break;
@@ -2973,7 +2978,7 @@ void launch_ivf_merge(int nq, int nprobe, const int64_t *probe_l, const int *lbl
 
 __global__ void keys_to_output_kernel(const uint64_t *__restrict__ keys, int K, int k,
                                       const int64_t *__restrict__ labels, int64_t *__restrict__ outL,
-                                      float *__restrict__ outD, int *__restrict__ outC) {
+                                      float *__restrict__ outD, int *__restrict__ outC, uint32_t sx) {
 	const int q = blockIdx.x;
 	__shared__ int n;
 	if (threadIdx.x == 0) n = 0;
@@ -2981,7 +2986,7 @@ __global__ void keys_to_output_kernel(const uint64_t *__restrict__ keys, int K, 
 	for (int i = threadIdx.x; i < k; i += blockDim.x) {
 		const uint64_t key = i < K ? keys[(int64_t)q * K + i] : KEY64_NONE;
 		if (key != KEY64_NONE) {
-			outL[(int64_t)q * k + i] = labels[(uint32_t)key];
+			outL[(int64_t)q * k + i] = labels[(uint32_t)key ^ sx];
 			outD[(int64_t)q * k + i] = key64_dist(key);
 			atomicAdd(&n, 1);
 		} else {
@@ -2994,8 +2999,9 @@ __global__ void keys_to_output_kernel(const uint64_t *__restrict__ keys, int K, 
 }
 
 void launch_keys_to_output(const uint64_t *keys, int nq, int K, int k, const int64_t *labels, int64_t *outL,
-                           float *outD, int *outC, hipStream_t st) {
-	keys_to_output_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(keys, K, k, labels, outL, outD, outC);
+                           float *outD, int *outC, hipStream_t st, int tie_desc) {
+	keys_to_output_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(keys, K, k, labels, outL, outD, outC,
+	                                                           tie_x32(tie_desc));
 }
 
 // exact re-rank of the ADC candidates (+ the tail's exact candidates): one
@@ -3007,7 +3013,7 @@ __global__ __launch_bounds__(256) void ivf_refine_final_kernel(const T *__restri
                                                                const uint64_t *__restrict__ cbk, int kb, int k,
                                                                const int64_t *__restrict__ labels,
                                                                int64_t *__restrict__ outL, float *__restrict__ outD,
-                                                               int *__restrict__ outC) {
+                                                               int *__restrict__ outC, uint32_t sx) {
 	__shared__ uint64_t sk[IVF_TOPK_CAP];
 	__shared__ uint32_t ss[IVF_TOPK_CAP];
 	__shared__ int n;
@@ -3015,15 +3021,16 @@ __global__ __launch_bounds__(256) void ivf_refine_final_kernel(const T *__restri
 	if (t == 0) n = 0;
 	__syncthreads();
 	for (int i = t; i < ka + kb; i += 256) {
+		// (ADC keys carry the slot; the tail's exact keys slot ^ sx)
 		const uint64_t key = i < ka ? ca[(int64_t)q * ka + i] : cbk[(int64_t)q * kb + (i - ka)];
-		if (key != KEY64_NONE) ss[atomicAdd(&n, 1)] = (uint32_t)key;
+		if (key != KEY64_NONE) ss[atomicAdd(&n, 1)] = (uint32_t)key ^ (i < ka ? 0u : sx);
 	}
 	__syncthreads();
 	const int nc = n;
 	for (int i = w; i < nc; i += 4) {
 		const uint32_t slot = ss[i];
 		const float d = exact_distance<METRIC, T>(X + (int64_t)slot * ld, Qf + (int64_t)q * ld, dim, lane);
-		if (lane == 0) sk[i] = key64(d, slot);
+		if (lane == 0) sk[i] = key64(d, slot ^ sx);
 	}
 	const int np = pow2_ceil(nc);
 	__syncthreads();
@@ -3032,7 +3039,7 @@ __global__ __launch_bounds__(256) void ivf_refine_final_kernel(const T *__restri
 	const int nout = nc < k ? nc : k;
 	for (int i = t; i < k; i += 256) {
 		if (i < nout) {
-			outL[(int64_t)q * k + i] = labels[(uint32_t)sk[i]];
+			outL[(int64_t)q * k + i] = labels[(uint32_t)sk[i] ^ sx];
 			outD[(int64_t)q * k + i] = key64_dist(sk[i]);
 		} else {
 			outL[(int64_t)q * k + i] = -1;
@@ -3047,7 +3054,7 @@ static void refine_final_dispatch(const StoreView &s, const float *Qf, const uin
                                   int kb, int nq, int k, int64_t *outL, float *outD, int *outC, hipStream_t st) {
 	const T *X = static_cast<const T *>(s.X);
 	dim3 grid((unsigned)nq);
-#define RF_ARGS X, s.ld, s.dim, Qf, ca, ka, cb, kb, k, s.labels, outL, outD, outC
+#define RF_ARGS X, s.ld, s.dim, Qf, ca, ka, cb, kb, k, s.labels, outL, outD, outC, tie_x32(s.tie_desc)
 	switch (s.metric) {
 	case METRIC_L2: ivf_refine_final_kernel<METRIC_L2, T><<<grid, 256, 0, st>>>(RF_ARGS); break;
 	case METRIC_DOT: ivf_refine_final_kernel<METRIC_DOT, T><<<grid, 256, 0, st>>>(RF_ARGS); break;

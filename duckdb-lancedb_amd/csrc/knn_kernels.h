@@ -50,6 +50,9 @@ struct StoreView {
 	// default; other values only in LHIP_ABLATION_BUILD builds)
 	int pr_first = 0;
 	int s8_variant = 0;
+	// tie rule of the final order (option "tie"): 0 = (distance, label asc),
+	// 1 = (distance, label desc) (device_common.h tie_x64)
+	int tie_desc = 0;
 };
 
 // Per-query constants for the lower-bound epilogue:
@@ -155,8 +158,10 @@ int scan_append_segments(const StoreView &s, int64_t n_tiles);
 // certificate fails).  Dense source: n_entries per query, entry i -> slot
 // (i/BR)*stride*BR + i%BR.  Segment source: the append scan's output;
 // pool_total[q] = entries seen (-1 on overflow); tau may be null (= +inf).
+// tie_desc: equal keys straddling the M-th place are taken by slot descending
+// (the exact fallback under the label-descending tie rule), else ascending.
 void launch_select_dense(const float *dense, int64_t ld_dense, int64_t n_entries, int64_t tile_stride, int nq, int M,
-                         uint32_t *cand_slot, int *cand_cnt, float *cut, hipStream_t st);
+                         uint32_t *cand_slot, int *cand_cnt, float *cut, hipStream_t st, int tie_desc);
 void launch_select_segments(const uint2 *seg_pool, const int *seg_cnt, int seg_cap, int n_seg, const float *tau,
                             int nq, int M, uint32_t *cand_slot, int *cand_cnt, float *cut, int *pool_total,
                             int *big, hipStream_t st);
@@ -196,7 +201,9 @@ void launch_finalize(const StoreView &s, const uint32_t *cand_slot, const int *c
                     int64_t live = -1);
 
 // Exact fallback for one query: exact distance of every slot into keys[n_slots]
-// (dead slots -> NaN with all-ones payload so they sort last), labels into vals.
+// (dead slots -> NaN with all-ones payload so they sort last), labels into vals;
+// under the label-descending tie rule in reverse slot order (entry n-1-slot),
+// so that a stable ascending sort puts equal distances in label-descending order.
 void launch_exact_all(const StoreView &s, const QueryView &q, int qi, float *keys, int64_t *vals, hipStream_t st);
 
 // Batched exact fallback: keys[i][r] (row stride ld_keys >= n_slots) = exact
@@ -238,10 +245,11 @@ void launch_retry_scatter(const int *fq, int nf, int k, const int64_t *L2, const
                           const int *cert2, const float *tau2, int64_t *L, float *D, int *C, int *cert, float *tau,
                           hipStream_t st);
 
-// Merge nshard partial top-k lists (device pointers) into the global top-k.
+// Merge nshard partial top-k lists (device pointers) into the global top-k,
+// (distance, label) order under the tie rule tie_desc.
 void launch_merge_topk(int nshard, int nq, int k, const int64_t *part_labels, const float *part_dists,
                        const int *part_counts, int64_t *out_labels, float *out_dists, int *out_counts,
-                       hipStream_t st);
+                       hipStream_t st, int tie_desc);
 
 // Copies the first n_live entries of a sorted fallback result into the outputs.
 void launch_copy_fallback(const float *keys, const int64_t *vals, int64_t n_live, int k, int qi,

@@ -1727,6 +1727,7 @@ struct SelSrc {
 	const uint2 *seg_pool;
 	const int *seg_cnt;
 	int seg_cap, n_seg;
+	int tie_desc;  // dense ties at the M-th place: by slot descending
 };
 
 // exclusive scan of one value per thread across the block
@@ -1935,13 +1936,14 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const f
 		unsigned my_min = 0xFFFFFFFFu;            // smallest key left out
 		if (dense && s_heq > rem) {
 			// Dense source with ties straddling the M-th place: take the equal
-			// keys in entry order = slot order (one block scan per chunk), so
-			// the selection is the M smallest by (key, slot) — the order the
-			// batched exact fallback relies on (slots ascend with labels).
+			// keys in entry order = slot order (one block scan per chunk; the
+			// label-descending tie rule walks the entries backwards), so the
+			// selection is the M smallest by (key, slot) under the tie rule — the
+			// order the batched exact fallback relies on (slots ascend with labels).
 			unsigned base = 0;
 			for (int64_t i0 = 0; i0 < n; i0 += SEL_THREADS) {
-				const int64_t i = i0 + t;
-				const uint32_t k = i < n ? (in_lds ? s_keys[i] : fkey(row[i])) : KEY_NAN;
+				const int64_t ii = i0 + t, i = src.tie_desc ? n - 1 - ii : ii;
+				const uint32_t k = ii < n ? (in_lds ? s_keys[i] : fkey(row[i])) : KEY_NAN;
 				if (k < T) {
 					unsigned p = atomicAdd(&s_nlt, 1u);
 					cand_slot[(int64_t)q * M + p] = slot_at(i);
@@ -1990,8 +1992,8 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelSrc src, const f
 }
 
 void launch_select_dense(const float *dense, int64_t ld_dense, int64_t n_entries, int64_t tile_stride, int nq, int M,
-                         uint32_t *cand_slot, int *cand_cnt, float *cut, hipStream_t st) {
-	SelSrc s{dense, ld_dense, n_entries, tile_stride, nullptr, nullptr, 0, 0};
+                         uint32_t *cand_slot, int *cand_cnt, float *cut, hipStream_t st, int tie_desc) {
+	SelSrc s{dense, ld_dense, n_entries, tile_stride, nullptr, nullptr, 0, 0, tie_desc};
 	select_kernel<<<dim3(nq), dim3(SEL_THREADS), 0, st>>>(s, nullptr, nq, M, cand_slot, cand_cnt, cut, nullptr,
 	                                                        nullptr);
 }
@@ -2222,7 +2224,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(const int64_t *__restrict
                                                        int need_for_tau, float *__restrict__ tau,
                                                        int64_t *__restrict__ out_labels,
                                                        float *__restrict__ out_dists, int *__restrict__ out_counts,
-                                                       int *__restrict__ cert_ok, int64_t live) {
+                                                       int *__restrict__ cert_ok, int64_t live, int64_t tx) {
 	__shared__ float sd[MAX_CAND];
 	__shared__ int64_t sl[MAX_CAND];
 	__shared__ float s_dk;
@@ -2260,7 +2262,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(const int64_t *__restrict
 		int rank = 0;
 		const float d = sd[i];
 		const int64_t l = sl[i];
-		for (int j = 0; j < m; ++j) rank += hit_less(sd[j], sl[j], d, l) ? 1 : 0;
+		for (int j = 0; j < m; ++j) rank += hit_less(sd[j], sl[j], d, l, tx) ? 1 : 0;
 		if (rank < k) {
 			out_labels[(int64_t)q * k + rank] = l;
 			out_dists[(int64_t)q * k + rank] = d;
@@ -2295,7 +2297,7 @@ void launch_finalize(const StoreView &s, const uint32_t *cand_slot, const int *c
                      int64_t live) {
 	finalize_kernel<<<dim3(nq), dim3(256), 0, st>>>(s.labels, cand_slot, cand_cnt, cand_dist, cut, M, k, mode,
 	                                                 need_for_tau, tau, out_labels, out_dists, out_counts, cert_ok,
-	                                                 live);
+	                                                 live, tie_x64(s.tie_desc));
 }
 
 // ---------------------------------------------------------------------------
@@ -2590,7 +2592,8 @@ __device__ __forceinline__ float pr_distances(const T *__restrict__ X, int ld, c
 // The caller synchronises the block afterwards.
 constexpr int PR_WMK = 32;
 constexpr int PR_WMK_MIN_M = 48;  // (smaller merges, e.g. the tau mode's k + 8 rows: the rank form is cheaper)
-__device__ __forceinline__ void pr_merge(const float *d, const int64_t *l, float *od, int64_t *ol, int m, int k) {
+__device__ __forceinline__ void pr_merge(const float *d, const int64_t *l, float *od, int64_t *ol, int m, int k,
+                                         int64_t tx) {
 	const int t = threadIdx.x, lane = t & 63;
 	if (k <= PR_WMK && m > PR_WMK_MIN_M && m <= 192) {
 		if (t >= 64) return;
@@ -2662,7 +2665,7 @@ __device__ __forceinline__ void pr_merge(const float *d, const int64_t *l, float
 			const int64_t li = ol[i];
 #pragma unroll
 			for (int e = 0; e < E; ++e)
-				if (lane + 64 * e < ns) rk[e] += hit_less(di, li, dj[e], lj[e]) ? 1 : 0;
+				if (lane + 64 * e < ns) rk[e] += hit_less(di, li, dj[e], lj[e], tx) ? 1 : 0;
 		}
 		__builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -2678,7 +2681,7 @@ __device__ __forceinline__ void pr_merge(const float *d, const int64_t *l, float
 		const int64_t li = l[i];
 		int rank = 0;
 #pragma unroll 8
-		for (int j = 0; j < m; ++j) rank += hit_less(d[j], l[j], di, li) ? 1 : 0;
+		for (int j = 0; j < m; ++j) rank += hit_less(d[j], l[j], di, li, tx) ? 1 : 0;
 		if (rank < k) {
 			od[rank] = di;
 			ol[rank] = li;
@@ -2719,7 +2722,7 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
     const float *__restrict__ tau, const T *__restrict__ X, int ld, int dim, const float *__restrict__ Qf,
     const int64_t *__restrict__ labels, int k, int mode, int m_tau, int64_t live, float *__restrict__ tau_out,
     int64_t *__restrict__ outL, float *__restrict__ outD, int *__restrict__ outC, int *__restrict__ cert,
-    int *__restrict__ refined, int *__restrict__ pool_total, int prof_on, int r_first) {
+    int *__restrict__ refined, int *__restrict__ pool_total, int prof_on, int r_first, int64_t tx) {
 	__shared__ uint64_t keys[PR_CAP];
 	__shared__ uint32_t sel[PR_SEL];  // slots of the chunk being refined
 	__shared__ unsigned hist[PR_HB];
@@ -3117,7 +3120,7 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 			mark();
 			// merge the top so far and this round by (distance, label)
 			const int m = cnt + nr;
-			if (!LHIP_ABL_PR_NOMERGE) pr_merge(cd[cur], cl[cur], cd[cur ^ 1], cl[cur ^ 1], m, k);
+			if (!LHIP_ABL_PR_NOMERGE) pr_merge(cd[cur], cl[cur], cd[cur ^ 1], cl[cur ^ 1], m, k, tx);
 			__syncthreads();
 			cur ^= 1;
 			cnt = min(m, k);
@@ -3158,7 +3161,7 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 			}
 			__syncthreads();
 			const int m = cnt + nr;
-			pr_merge(cd[cur], cl[cur], cd[cur ^ 1], cl[cur ^ 1], m, k);
+			pr_merge(cd[cur], cl[cur], cd[cur ^ 1], cl[cur ^ 1], m, k, tx);
 			__syncthreads();
 			cur ^= 1;
 			cnt = min(m, k);
@@ -3283,7 +3286,8 @@ static void pool_refine_dispatch(const StoreView &s, const QueryView &q, const u
 #define LHIP_PR(MET, NI)                                                                                              \
 	pool_refine_kernel<MET, T, NI><<<grid, PR_THREADS, 0, st>>>(seg_pool, seg_cnt, seg_cap, n_seg, q.nq, tau, X, s.ld,\
 	                                                            s.dim, q.Qf, s.labels, k, mode, m_tau, live, tau_out,  \
-	                                                            L, D, C, cert, refined, pool_total, prof_on, r_first)
+	                                                            L, D, C, cert, refined, pool_total, prof_on, r_first,  \
+	                                                            tie_x64(s.tie_desc))
 #define LHIP_PR_NI(MET)                                                                                               \
 	switch (ni) {                                                                                                      \
 	case 1: LHIP_PR(MET, 1); break;                                                                                    \
@@ -3338,7 +3342,8 @@ template <int METRIC, typename T>
 __global__ __launch_bounds__(256) void exact_all_kernel(const T *__restrict__ X, const float4 *__restrict__ rowaux,
                                                         const int64_t *__restrict__ labels, int64_t n, int ld,
                                                         int dim, const float *__restrict__ q,
-                                                        float *__restrict__ keys, int64_t *__restrict__ vals) {
+                                                        float *__restrict__ keys, int64_t *__restrict__ vals,
+                                                        int tie_desc) {
 	const int lane = threadIdx.x & 63;
 	const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
 	if (r >= n) return;
@@ -3346,8 +3351,11 @@ __global__ __launch_bounds__(256) void exact_all_kernel(const T *__restrict__ X,
 	if (lane == 0) {
 		const float a = reinterpret_cast<const float *>(rowaux)[raix(r, 0)];
 		const bool dead = (a == F_INF);
-		keys[r] = dead ? __uint_as_float(0x7FFFFFFFu) : d;
-		vals[r] = labels[r];
+		// (label-descending ties: entry n-1-r, the stable sort then keeps equal
+		// distances in reverse slot = label order)
+		const int64_t e = tie_desc ? n - 1 - r : r;
+		keys[e] = dead ? __uint_as_float(0x7FFFFFFFu) : d;
+		vals[e] = labels[r];
 	}
 }
 
@@ -3360,15 +3368,15 @@ static void exact_all_dispatch(const StoreView &s, const QueryView &q, int qi, f
 	switch (s.metric) {
 	case METRIC_L2:
 		exact_all_kernel<METRIC_L2, T><<<grid, 256, 0, st>>>(X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim, qq, keys,
-		                                                      vals);
+		                                                      vals, s.tie_desc);
 		break;
 	case METRIC_DOT:
 		exact_all_kernel<METRIC_DOT, T><<<grid, 256, 0, st>>>(X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim, qq, keys,
-		                                                       vals);
+		                                                       vals, s.tie_desc);
 		break;
 	default:
 		exact_all_kernel<METRIC_COSINE, T><<<grid, 256, 0, st>>>(X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim, qq,
-		                                                          keys, vals);
+		                                                          keys, vals, s.tie_desc);
 		break;
 	}
 }
@@ -3481,13 +3489,13 @@ struct SHit {
 	int64_t l;
 };
 
-__device__ __forceinline__ bool shit_less(const SHit &a, const SHit &b) {
+__device__ __forceinline__ bool shit_less(const SHit &a, const SHit &b, int64_t tx) {
 	if (a.v != b.v) return a.v > b.v;
-	return hit_less(a.d, a.l, b.d, b.l);
+	return hit_less(a.d, a.l, b.d, b.l, tx);
 }
 
 // ascending bitonic sort of s[0..n) (n a power of two) by the whole block
-__device__ __forceinline__ void shit_sort(SHit *s, int n) {
+__device__ __forceinline__ void shit_sort(SHit *s, int n, int64_t tx) {
 	const int t = threadIdx.x;
 	for (int size = 2; size <= n; size <<= 1) {
 		for (int j = size >> 1, lj = __builtin_ctz(size >> 1); j > 0; j >>= 1, --lj) {
@@ -3495,7 +3503,7 @@ __device__ __forceinline__ void shit_sort(SHit *s, int n) {
 				const int lo = ((i >> lj) << (lj + 1)) | (i & (j - 1)), hi = lo + j;
 				const bool up = (lo & size) == 0;
 				const SHit a = s[lo], b = s[hi];
-				if (up ? shit_less(b, a) : shit_less(a, b)) {
+				if (up ? shit_less(b, a, tx) : shit_less(a, b, tx)) {
 					s[lo] = b;
 					s[hi] = a;
 				}
@@ -3540,7 +3548,9 @@ __global__ __launch_bounds__(SMALL_THREADS) void small_exact_kernel(const T *__r
                                                                     unsigned *__restrict__ counter,
                                                                     int64_t *__restrict__ out_l,
                                                                     float *__restrict__ out_d, int *__restrict__ out_c,
-                                                                    int se_prof) {
+                                                                    int se_prof, int tie_desc) {
+	const int64_t tx = tie_x64(tie_desc);
+	const uint32_t sx = tie_x32(tie_desc);  // (k <= 32 keys: slot ^ sx)
 	__shared__ __attribute__((aligned(16))) float sq[SMALL_MAX_DIM];
 	__shared__ SHit s_rows[SMALL_MAX_PART], s2[SMALL_MAX_PART], red[SMALL_THREADS];
 	__shared__ unsigned s_ns;
@@ -3636,8 +3646,9 @@ __global__ __launch_bounds__(SMALL_THREADS) void small_exact_kernel(const T *__r
 				s[w * 64 + g * 8 + (lane >> 3)] = h;
 			}
 			// (every lane of the 8 holds the sums: lane sub keeps group sub's row,
-			// one row per lane; key = (ordered distance, slot): slots ascend with
-			// labels, so key order is (distance, label) order, NaN last, none last)
+			// one row per lane; key = (ordered distance, slot ^ sx): slots ascend
+			// with labels, so key order is (distance, label) order under the tie
+			// rule, NaN last, none last)
 			if (sub == g && ok[g]) {
 				double v;
 				if (METRIC == METRIC_L2)
@@ -3648,7 +3659,7 @@ __global__ __launch_bounds__(SMALL_THREADS) void small_exact_kernel(const T *__r
 					v = 1.0 - a[g] / (sqrt(b[g]) * sqrt(c[g]));
 				float f = (float)v + 0.0f;
 				if (__builtin_isnan(f)) f = __builtin_nanf("");
-				mykey = ((uint64_t)fkey(f) << 32) | (uint32_t)r[g];
+				mykey = ((uint64_t)fkey(f) << 32) | ((uint32_t)r[g] ^ sx);
 			}
 		}
 	}
@@ -3719,7 +3730,7 @@ __global__ __launch_bounds__(SMALL_THREADS) void small_exact_kernel(const T *__r
 			}
 			if (lane < k) {
 				const bool valid = acc != ~0ull;
-				out_l[(int64_t)q * k + lane] = valid ? labels[(uint32_t)acc] : -1;
+				out_l[(int64_t)q * k + lane] = valid ? labels[(uint32_t)acc ^ sx] : -1;
 				out_d[(int64_t)q * k + lane] = valid ? fkey_inv((uint32_t)(acc >> 32)) : __builtin_nanf("");
 			}
 			const uint64_t vm = __builtin_amdgcn_ballot_w64(lane < k && acc != ~0ull);
@@ -3732,7 +3743,7 @@ __global__ __launch_bounds__(SMALL_THREADS) void small_exact_kernel(const T *__r
 	}
 	// ---- k > 32: bitonic sorts of the workgroup's rows ------------------------
 	// this workgroup's top-k: sorted by (distance, label)
-	if (!LHIP_ABL_SMALL_NOWGSORT) shit_sort(s, SMALL_THREADS);
+	if (!LHIP_ABL_SMALL_NOWGSORT) shit_sort(s, SMALL_THREADS, tx);
 	SE_T();
 	SHit *mine = part + ((int64_t)q * G + blockIdx.x) * k;
 	for (int i = t; i < k; i += SMALL_THREADS) mine[i] = s[i];
@@ -3759,13 +3770,13 @@ __global__ __launch_bounds__(SMALL_THREADS) void small_exact_kernel(const T *__r
 	if (t < G) red[t] = s[t * k + k - 1];
 	__syncthreads();
 	for (int w = 1; w < G; w <<= 1) {
-		if ((t & (2 * w - 1)) == 0 && t + w < G && shit_less(red[t + w], red[t])) red[t] = red[t + w];
+		if ((t & (2 * w - 1)) == 0 && t + w < G && shit_less(red[t + w], red[t], tx)) red[t] = red[t + w];
 		__syncthreads();
 	}
 	const SHit thr = red[0];
 	SE_T();
 	for (int i = t; i < P; i += SMALL_THREADS)
-		if (!shit_less(thr, s[i])) s2[atomicAdd(&s_ns, 1u)] = s[i];
+		if (!shit_less(thr, s[i], tx)) s2[atomicAdd(&s_ns, 1u)] = s[i];
 	__syncthreads();
 	const int ns = (int)s_ns;
 	int n2 = 2;
@@ -3773,7 +3784,7 @@ __global__ __launch_bounds__(SMALL_THREADS) void small_exact_kernel(const T *__r
 	for (int i = ns + t; i < n2; i += SMALL_THREADS) s2[i] = SHit{F_INF, 0, INT64_MAX};
 	__syncthreads();
 	SE_T();
-	if (!LHIP_ABL_SMALL_NOMERGE) shit_sort(s2, n2);
+	if (!LHIP_ABL_SMALL_NOMERGE) shit_sort(s2, n2, tx);
 	SE_T();
 	s = s2;
 	for (int i = t; i < k; i += SMALL_THREADS) {
@@ -3818,15 +3829,18 @@ static void small_exact_dispatch(const StoreView &s, const float *Q, int nq, int
 	switch (s.metric) {
 	case METRIC_L2:
 		small_exact_kernel<METRIC_L2, T><<<grid, SMALL_THREADS, 0, st>>>(X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim, Q,
-		                                                                 k, p, counter, L, D, C, se_prof);
+		                                                                 k, p, counter, L, D, C, se_prof,
+		                                                                 s.tie_desc);
 		break;
 	case METRIC_DOT:
 		small_exact_kernel<METRIC_DOT, T><<<grid, SMALL_THREADS, 0, st>>>(X, s.rowaux, s.labels, s.n_slots, s.ld, s.dim,
-		                                                                  Q, k, p, counter, L, D, C, se_prof);
+		                                                                  Q, k, p, counter, L, D, C, se_prof,
+		                                                                 s.tie_desc);
 		break;
 	default:
 		small_exact_kernel<METRIC_COSINE, T><<<grid, SMALL_THREADS, 0, st>>>(X, s.rowaux, s.labels, s.n_slots, s.ld,
-		                                                                     s.dim, Q, k, p, counter, L, D, C, se_prof);
+		                                                                     s.dim, Q, k, p, counter, L, D, C, se_prof,
+		                                                                 s.tie_desc);
 		break;
 	}
 }
@@ -3924,7 +3938,8 @@ __global__ __launch_bounds__(256) void merge_topk_kernel(int nshard, int nq, int
                                                          const float *__restrict__ part_dists,
                                                          const int *__restrict__ part_counts,
                                                          int64_t *__restrict__ out_labels,
-                                                         float *__restrict__ out_dists, int *__restrict__ out_counts) {
+                                                         float *__restrict__ out_dists, int *__restrict__ out_counts,
+                                                         int64_t tx) {
 	const int q = blockIdx.x;
 	const int t = threadIdx.x;
 	const int total = nshard * k;
@@ -3945,7 +3960,7 @@ __global__ __launch_bounds__(256) void merge_topk_kernel(int nshard, int nq, int
 			int c2 = part_counts[(int64_t)s2 * nq + q];
 			c2 = c2 < k ? c2 : k;
 			const int64_t b2 = ((int64_t)s2 * nq + q) * k;
-			for (int j = 0; j < c2; ++j) rank += hit_less(part_dists[b2 + j], part_labels[b2 + j], d, l) ? 1 : 0;
+			for (int j = 0; j < c2; ++j) rank += hit_less(part_dists[b2 + j], part_labels[b2 + j], d, l, tx) ? 1 : 0;
 			if (rank >= k) break;
 		}
 		if (rank < k) {
@@ -3963,9 +3978,9 @@ __global__ __launch_bounds__(256) void merge_topk_kernel(int nshard, int nq, int
 
 void launch_merge_topk(int nshard, int nq, int k, const int64_t *part_labels, const float *part_dists,
                        const int *part_counts, int64_t *out_labels, float *out_dists, int *out_counts,
-                       hipStream_t st) {
+                       hipStream_t st, int tie_desc) {
 	merge_topk_kernel<<<dim3(nq), dim3(256), 0, st>>>(nshard, nq, k, part_labels, part_dists, part_counts,
-	                                                   out_labels, out_dists, out_counts);
+	                                                   out_labels, out_dists, out_counts, tie_x64(tie_desc));
 }
 
 // ---------------------------------------------------------------------------

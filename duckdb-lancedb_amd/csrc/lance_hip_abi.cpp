@@ -96,6 +96,7 @@ bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *d
 	             Xs ? static_cast<const void *>(Xs) : X, (xbf16 || Xs) ? 1 : 0};
 	sv.pr_first = pr_first;
 	sv.s8_variant = s8_variant;
+	sv.tie_desc = tie_desc;
 	last_scan_esz = use8 ? 1 : (xbf16 || Xs) ? 2 : 4;
 	if (use8) {
 		ensure_i8();
@@ -174,7 +175,8 @@ bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *d
 		tic(0);
 		launch_scan_dense(sv, qv, n_tiles, 1, ws.dense.p, cols, st);
 		tic(1);
-		launch_select_dense(ws.dense.p, cols, cols, 1, nq, Mfinal, ws.cand_slot.p, d_cand_cnt, ws.cut.p, st);
+		launch_select_dense(ws.dense.p, cols, cols, 1, nq, Mfinal, ws.cand_slot.p, d_cand_cnt, ws.cut.p, st,
+		                    tie_desc);
 		launch_refine(sv, qv, ws.cand_slot.p, d_cand_cnt, Mfinal, ws.cand_dist.p, st);
 		launch_finalize(sv, ws.cand_slot.p, d_cand_cnt, ws.cand_dist.p, ws.cut.p, nq, Mfinal, k, 1, 0, nullptr, dL,
 		                dD, dC, d_cert, st, live_rows());
@@ -418,7 +420,8 @@ void Index::finish_chunk(PendingPass &p) {
 			const QueryView qg{ws.rQf.p + (size_t)g0 * ld, ws.rQb.p + (size_t)g0 * ld, ws.rqaux.p + g0, gq,
 			                   (int)round_up(gq, SCAN_BQ)};
 			launch_exact_dense(sv, qg, ws.fb_keys.p, cols, st);
-			launch_select_dense(ws.fb_keys.p, cols, n_slots, 1, gq, k, ws.cand_slot.p, cnt2 + g0, ws.cut.p, st);
+			launch_select_dense(ws.fb_keys.p, cols, n_slots, 1, gq, k, ws.cand_slot.p, cnt2 + g0, ws.cut.p, st,
+			                    tie_desc);
 			launch_refine(sv, qg, ws.cand_slot.p, cnt2 + g0, k, ws.cand_dist.p, st);
 			launch_finalize(sv, ws.cand_slot.p, cnt2 + g0, ws.cand_dist.p, ws.cut.p, gq, k, k, 1, 0, nullptr,
 			                ws.rL.p + (size_t)g0 * k, ws.rD.p + (size_t)g0 * k, ws.rC.p + g0, cert2 + g0, st);
@@ -651,6 +654,7 @@ static Index *as_index(void *h) { return reinterpret_cast<Index *>(h); }
 // the handle's device(s): LANCE_HIP_DEVICES lists two or more -> a multi-device
 // handle (shards.cpp); one -> that device; unset -> the current device
 static void init_devices(Index *ix) {
+	ix->tie_desc = lhip::env_tie();
 	const auto devs = lhip::env_devices();
 	ix->init_device(devs.empty() ? -1 : devs[0]);
 	if (devs.size() >= 2) lhip::shard_init(ix, devs);
@@ -1341,6 +1345,10 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			if (k == "index_type") ix->ivf_type_opt = ix->shards[0]->ivf_type_opt;
 			return 0;
 		}
+		if (k == "tie") {  // the final order's tie rule (label_desc reproduces the reference's tie golden)
+			ix->tie_desc = lhip::parse_tie(v);
+			return 0;
+		}
 		if (k == "metric_quirk") {
 			bool on = (v == "1" || v == "true");
 			if (on && ix->metric != lhip::METRIC_L2 && !ix->rowaux_l2) {
@@ -1683,7 +1691,7 @@ int32_t lance_hip_merge_topk(int32_t nshard, int32_t nq, int32_t k, const int64_
 		HIPCHK(hipMemcpyAsync(pl, part_labels, P * sizeof(int64_t), hipMemcpyHostToDevice, st));
 		HIPCHK(hipMemcpyAsync(pd, part_dists, P * sizeof(float), hipMemcpyHostToDevice, st));
 		HIPCHK(hipMemcpyAsync(pc, part_counts, (size_t)nshard * nq * sizeof(int), hipMemcpyHostToDevice, st));
-		lhip::launch_merge_topk(nshard, nq, k, pl, pd, pc, ol, od, oc, st);
+		lhip::launch_merge_topk(nshard, nq, k, pl, pd, pc, ol, od, oc, st, lhip::env_tie());
 		HIPCHK(hipGetLastError());
 		HIPCHK(hipMemcpyAsync(out_labels, ol, (size_t)nq * k * sizeof(int64_t), hipMemcpyDeviceToHost, st));
 		HIPCHK(hipMemcpyAsync(out_dists, od, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, st));
@@ -1708,7 +1716,7 @@ int32_t lance_hip_merge_topk_device(int32_t nshard, int32_t nq, int32_t k, const
 	try {
 		if (nshard <= 0 || nq <= 0 || k <= 0) return 0;
 		lhip::launch_merge_topk(nshard, nq, k, d_part_labels, d_part_dists, d_part_counts, d_out_labels, d_out_dists,
-		                        d_out_counts, nullptr);
+		                        d_out_counts, nullptr, lhip::env_tie());
 		HIPCHK(hipGetLastError());
 		HIPCHK(hipStreamSynchronize(nullptr));
 		return nq;

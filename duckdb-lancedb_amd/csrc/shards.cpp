@@ -50,6 +50,20 @@ std::vector<int> env_devices() {
 	return parse_devices(e);
 }
 
+int parse_tie(const std::string &v) {
+	if (v == "label_desc" || v == "desc") return 1;
+	if (v == "label_asc" || v == "asc") return 0;
+	throw Error("tie must be 'label_desc' or 'label_asc', got '" + v + "'");
+}
+
+// LANCE_HIP_TIE=label_asc|label_desc (unset: label_desc), read when a handle
+// is created (the same channel as LANCE_HIP_DEVICES)
+int env_tie() {
+	const char *e = std::getenv("LANCE_HIP_TIE");
+	if (!e || !*e) return 1;
+	return parse_tie(e);
+}
+
 void shard_init(Index *ix, const std::vector<int> &devs) {
 	if (ix->sharded()) throw Error("the handle is already sharded");
 	if (ix->n_slots > 0) throw Error("devices can only be set on an empty table");
@@ -68,6 +82,7 @@ void shard_init(Index *ix, const std::vector<int> &devs) {
 		sh->dim = ix->dim;
 		sh->ld = ix->ld;
 		sh->xbf16 = ix->xbf16;
+		sh->tie_desc = ix->tie_desc;
 		if (ix->meta) sh->meta = MetaStore::deserialize_schema(schema.data(), schema.size());
 		sh->init_device(d);
 		ix->shards.push_back(std::move(sh));
@@ -206,7 +221,7 @@ void shard_search(Index *ix, const float *Q, int qdev, int nq, int k, int nprobe
 		oD = reinterpret_cast<float *>(ix->m_out.p + lb);
 		oC = reinterpret_cast<int *>(ix->m_out.p + lb + db);
 	}
-	launch_merge_topk(S, nq, k, ix->m_pl.p, ix->m_pd.p, ix->m_pc.p, oL, oD, oC, p0->stream);
+	launch_merge_topk(S, nq, k, ix->m_pl.p, ix->m_pd.p, ix->m_pc.p, oL, oD, oC, p0->stream, ix->tie_desc);
 	HIPCHK(hipGetLastError());
 	if (out_host) {
 		uint8_t *io = p0->ws.need_host_io(lb + db + cb);

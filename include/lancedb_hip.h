@@ -80,7 +80,8 @@ int32_t lance_detached_merge(void *target_handle, void *source_handle, const int
 /* ---- search --------------------------------------------------------------- */
 
 /* ffi.rs:295-329 (rust_ffi.cpp:130-139).  Exact top-k of one query over all
- * live rows, ascending distance (ties: label ascending); writes n <= k
+ * live rows, ascending distance (ties: the handle's tie rule, label
+ * descending by default — option "tie" below); writes n <= k
  * (label, distance) pairs, returns n or -1.  dim != index dim is an error here
  * (lance_manager.rs:401-407); the C++ caller returns {} before calling
  * (lance_index.cpp:444-446).  nprobes / refine_factor only matter once an
@@ -171,6 +172,13 @@ const char *lance_hip_version(void);
 int32_t lance_hip_device_count(void);
 
 /* Per-handle options, key/value strings (unknown keys: error, -1):
+ *   "tie"          "label_desc" (default) | "label_asc": which of several rows
+ *                  at an equal exact distance come first (and so which make the
+ *                  k-th place).  label_desc is what the reference's golden
+ *                  shows (test/sql/lance_optimizer_filter.test:36-44: ids 3 and
+ *                  4 tie at d = 2.0 and LanceDB returns 4); the default of a new
+ *                  handle comes from LANCE_HIP_TIE in the process environment
+ *                  (a DuckDB process has no option channel)
  *   "metric_quirk" "1" = rank every search by squared L2 whatever the index
  *                  metric, exactly as the reference does (lance_manager.rs:
  *                  411-418 never sets distance_type); default "0"
@@ -314,7 +322,8 @@ int32_t lance_hip_merge_topk_device(int32_t nshard, int32_t nq, int32_t k, const
 /* Merge per-shard partial top-k lists into a global top-k, on the device of
  * the handle (multi-GPU path: shards all-gathered over RCCL).
  * part_labels / part_dists: nshard x nq x k (host pointers), part_counts:
- * nshard x nq.  Order (distance asc, label asc).  Returns nq or -1. */
+ * nshard x nq.  Order (distance asc, label under LANCE_HIP_TIE: descending
+ * unless it says label_asc).  Returns nq or -1. */
 int32_t lance_hip_merge_topk(int32_t nshard, int32_t nq, int32_t k, const int64_t *part_labels,
                              const float *part_dists, const int32_t *part_counts, int64_t *out_labels,
                              float *out_dists, int32_t *out_counts, char *err_buf, int err_buf_len);

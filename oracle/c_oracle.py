@@ -42,15 +42,26 @@ def lib():
         L.oracle_ivf_search_batch.argtypes = [P, I32, P, P, P, I32, P, I64, P, P, I32, P, P, P, I32, I32, I32, I32,
                                               I32, I32, I32, I32, P, P, P]
         L.oracle_ivf_search_batch.restype = ctypes.c_int
+        L.oracle_set_tie.argtypes = [ctypes.c_int32]
+        L.oracle_set_tie.restype = None
         _lib = L
     return _lib
+
+
+def _set_tie(tie):
+    """The final order's tie rule for the next call (flat_knn.tie_desc:
+    label_desc by default, LANCE_HIP_TIE / tie="label_asc" otherwise)."""
+    t = tie or os.environ.get("LANCE_HIP_TIE") or "label_desc"
+    if t not in ("label_desc", "desc", "label_asc", "asc"):
+        raise ValueError(f"tie must be 'label_desc' or 'label_asc', got {t!r}")
+    lib().oracle_set_tie(1 if t in ("label_desc", "desc") else 0)
 
 
 def _ptr(a):
     return None if a is None else a.ctypes.data
 
 
-def flat_search_batch(base, Q, k, metric="l2", live=None, labels=None, acc64=True, nthreads=0):
+def flat_search_batch(base, Q, k, metric="l2", live=None, labels=None, acc64=True, nthreads=0, tie=None):
     base = np.ascontiguousarray(base, dtype=np.float32)
     Q = np.ascontiguousarray(Q, dtype=np.float32)
     n, d = base.shape
@@ -60,6 +71,7 @@ def flat_search_batch(base, Q, k, metric="l2", live=None, labels=None, acc64=Tru
     out_l = np.empty((nq, k), np.int64)
     out_d = np.empty((nq, k), np.float32)
     cnt = np.empty(nq, np.int32)
+    _set_tie(tie)
     rc = lib().oracle_flat_search_batch(_ptr(base), n, d, _ptr(live_a), _ptr(lab_a), _ptr(Q), nq, k,
                                         METRIC_IDS[metric], 1 if acc64 else 0, int(nthreads),
                                         _ptr(out_l), _ptr(out_d), _ptr(cnt))
@@ -94,7 +106,7 @@ class IvfLayout:
 
 
 def ivf_search_batch(base, labels, layout, centroids, Q, k, nprobe, metric="l2", codes=None, codebook=None, T=None,
-                     refine_factor=1, acc64=True, nthreads=0, lut="f32", query_fp8=False):
+                     refine_factor=1, acc64=True, nthreads=0, lut="f32", query_fp8=False, tie=None):
     """IVF_FLAT (codes None) / IVF_PQ search of oracle/flat_knn.c over a given
     model and layout.  base / labels / codes are per slot.  l2 and dot only.
     lut "u8": the fast scan's 8-bit LUT; query_fp8: ADC tables from e4m3 queries
@@ -113,6 +125,7 @@ def ivf_search_batch(base, labels, layout, centroids, Q, k, nprobe, metric="l2",
     out_l = np.empty((nq, k), np.int64)
     out_d = np.empty((nq, k), np.float32)
     cnt = np.empty(nq, np.int32)
+    _set_tie(tie)
     rc = lib().oracle_ivf_search_batch(_ptr(base), d, _ptr(labels), _ptr(layout.loff), _ptr(layout.lrows),
                                        layout.nlist, _ptr(layout.tail), len(layout.tail), _ptr(C), _ptr(codes), m,
                                        _ptr(codebook), _ptr(T), _ptr(Q), nq, k, nprobe, refine_factor,

@@ -19,7 +19,11 @@
  *               identical to oracle/flat_knn.py and to the HIP refine stage)
  *   acc64 = 0 : float32 accumulation in a SIMD-friendly loop (what
  *               lance-linalg does; used for the timed cpu_baseline)
- * Ties: (distance asc, label asc).
+ * Ties: (distance asc, label under the tie rule): label descending by default
+ * (the reference's golden at test/sql/lance_optimizer_filter.test:36-44 keeps
+ * the higher of two tied labels), ascending after oracle_set_tie(0) — the
+ * library's option "tie" / LANCE_HIP_TIE.  Coarse probes and PQ (ADC)
+ * candidates keep (value, id ascending), as the library does.
  */
 #include <math.h>
 #include <stdint.h>
@@ -32,22 +36,27 @@ typedef struct {
 	int64_t l;
 } hit_t;
 
-static inline int hit_less(hit_t a, hit_t b) {
+static int g_tie_desc = 1; /* the final order's tie rule (oracle_set_tie) */
+
+void oracle_set_tie(int32_t desc) { g_tie_desc = desc ? 1 : 0; }
+int32_t oracle_get_tie(void) { return g_tie_desc; }
+
+static inline int hit_less(hit_t a, hit_t b, int desc) {
 	/* NaN sorts after everything */
 	int an = isnan(a.d), bn = isnan(b.d);
 	if (an != bn) return bn;
 	if (a.d != b.d) return a.d < b.d;
-	return a.l < b.l;
+	return desc ? a.l > b.l : a.l < b.l;
 }
 
 /* max-heap on hit_less (root = worst kept hit) */
-static void heap_push(hit_t *h, int *n, int cap, hit_t x) {
+static void heap_push(hit_t *h, int *n, int cap, hit_t x, int desc) {
 	if (*n < cap) {
 		int i = (*n)++;
 		h[i] = x;
 		while (i > 0) {
 			int p = (i - 1) >> 1;
-			if (hit_less(h[p], h[i])) {
+			if (hit_less(h[p], h[i], desc)) {
 				hit_t t = h[p];
 				h[p] = h[i];
 				h[i] = t;
@@ -58,13 +67,13 @@ static void heap_push(hit_t *h, int *n, int cap, hit_t x) {
 		}
 		return;
 	}
-	if (!hit_less(x, h[0])) return;
+	if (!hit_less(x, h[0], desc)) return;
 	h[0] = x;
 	int i = 0;
 	for (;;) {
 		int l = 2 * i + 1, r = l + 1, m = i;
-		if (l < cap && hit_less(h[m], h[l])) m = l;
-		if (r < cap && hit_less(h[m], h[r])) m = r;
+		if (l < cap && hit_less(h[m], h[l], desc)) m = l;
+		if (r < cap && hit_less(h[m], h[r], desc)) m = r;
 		if (m == i) break;
 		hit_t t = h[m];
 		h[m] = h[i];
@@ -73,12 +82,19 @@ static void heap_push(hit_t *h, int *n, int cap, hit_t x) {
 	}
 }
 
-static int cmp_hit(const void *a, const void *b) {
+static int cmp_hit_asc(const void *a, const void *b) {
 	hit_t x = *(const hit_t *)a, y = *(const hit_t *)b;
-	if (hit_less(x, y)) return -1;
-	if (hit_less(y, x)) return 1;
+	if (hit_less(x, y, 0)) return -1;
+	if (hit_less(y, x, 0)) return 1;
 	return 0;
 }
+static int cmp_hit_desc(const void *a, const void *b) {
+	hit_t x = *(const hit_t *)a, y = *(const hit_t *)b;
+	if (hit_less(x, y, 1)) return -1;
+	if (hit_less(y, x, 1)) return 1;
+	return 0;
+}
+#define CMP_HIT(desc) ((desc) ? cmp_hit_desc : cmp_hit_asc)
 
 static inline float dist64(const float *x, const float *q, int32_t d, int metric, double qn2) {
 	if (metric == 0) {
@@ -148,6 +164,7 @@ int oracle_flat_search_batch(const float *base, int64_t n, int32_t d, const uint
                              int64_t *out_labels, float *out_dist, int32_t *out_counts) {
 	if (k <= 0 || nq <= 0) return 0;
 	if (nthreads <= 0) nthreads = omp_get_max_threads();
+	const int tie = g_tie_desc;
 	double *qn2 = (double *)calloc((size_t)nq, sizeof(double));
 	hit_t *heaps = (hit_t *)malloc((size_t)nthreads * nq * k * sizeof(hit_t));
 	int *hn = (int *)calloc((size_t)nthreads * nq, sizeof(int));
@@ -178,7 +195,7 @@ int oracle_flat_search_batch(const float *base, int64_t n, int32_t d, const uint
 					const float *x = base + (size_t)r * d;
 					float dd = acc64 ? dist64(x, q, d, metric, qn2[j]) : dist32(x, q, d, metric, (float)qn2[j]);
 					hit_t h = {dd, labels ? labels[r] : r};
-					heap_push(my + (size_t)j * k, &myn[j], k, h);
+					heap_push(my + (size_t)j * k, &myn[j], k, h, tie);
 				}
 			}
 		}
@@ -191,7 +208,7 @@ int oracle_flat_search_batch(const float *base, int64_t n, int32_t d, const uint
 			memcpy(tmp + m, heaps + ((size_t)t * nq + j) * k, (size_t)hn[(size_t)t * nq + j] * sizeof(hit_t));
 			m += hn[(size_t)t * nq + j];
 		}
-		qsort(tmp, (size_t)m, sizeof(hit_t), cmp_hit);
+		qsort(tmp, (size_t)m, sizeof(hit_t), CMP_HIT(tie));
 		int c = m < k ? m : k;
 		out_counts[j] = c;
 		for (int i = 0; i < k; i++) {
@@ -253,9 +270,9 @@ static void topk_sel(const float *dv, int64_t n, int32_t np, int32_t *ids, float
 	int hn = 0;
 	for (int64_t i = 0; i < n; i++) {
 		hit_t x = {dv[i], i};
-		heap_push(h, &hn, np, x);
+		heap_push(h, &hn, np, x, 0); /* probes: (distance, partition id ascending) */
 	}
-	qsort(h, (size_t)hn, sizeof(hit_t), cmp_hit);
+	qsort(h, (size_t)hn, sizeof(hit_t), cmp_hit_asc);
 	for (int i = 0; i < hn; i++) {
 		ids[i] = (int32_t)h[i].l;
 		ds[i] = h[i].d;
@@ -274,6 +291,9 @@ int oracle_ivf_search_batch(const float *base, int32_t d, const int64_t *labels,
 	if (nthreads <= 0) nthreads = omp_get_max_threads();
 	if (nprobe > nlist) nprobe = nlist;
 	const int pq = codes != NULL;
+	/* list candidates: PQ by (ADC, slot ascending); IVF_FLAT exact distances by
+	   slot under the tie rule (slots ascend with labels); the final order too */
+	const int tie = g_tie_desc, ltie = pq ? 0 : tie;
 	const int dsub = pq ? d / m : 0;
 	const int kp = pq ? k * (refine > 1 ? refine : 1) : k;
 	float *cd = (float *)malloc((size_t)nlist * sizeof(float));
@@ -371,7 +391,7 @@ int oracle_ivf_search_batch(const float *base, int32_t d, const int64_t *labels,
 						           : dist32(base + (size_t)s * d, q, d, metric, (float)qn2);
 					}
 					hit_t h = {dd, s}; /* by slot: slots ascend with labels, so ties go by label */
-					heap_push(my, &hn[t], kp, h);
+					heap_push(my, &hn[t], kp, h, ltie);
 				}
 			}
 			free(lut);
@@ -381,7 +401,7 @@ int oracle_ivf_search_batch(const float *base, int32_t d, const int64_t *labels,
 			memcpy(all + na, heaps + (size_t)t * kp, (size_t)hn[t] * sizeof(hit_t));
 			na += hn[t];
 		}
-		qsort(all, (size_t)na, sizeof(hit_t), cmp_hit);
+		qsort(all, (size_t)na, sizeof(hit_t), CMP_HIT(ltie));
 		if (na > kp) na = kp;
 		/* re-rank (PQ) + the unindexed tail, exact */
 		int nc = 0;
@@ -398,7 +418,7 @@ int oracle_ivf_search_batch(const float *base, int32_t d, const int64_t *labels,
 			hit_t h = {acc64 ? dist64(base + (size_t)s * d, q, d, metric, qn2) : dist32(base + (size_t)s * d, q, d, metric, (float)qn2), labels[s]};
 			cand[nc++] = h;
 		}
-		qsort(cand, (size_t)nc, sizeof(hit_t), cmp_hit);
+		qsort(cand, (size_t)nc, sizeof(hit_t), CMP_HIT(tie));
 		const int c = nc < k ? nc : k;
 		out_counts[qi] = c;
 		for (int i = 0; i < k; i++) {

@@ -26,16 +26,37 @@ What it restates (reference paths relative to ``/root/reference``):
 
 Canonical numerics of this build (documented in DESIGN.md): every distance is
 accumulated in float64 from the float32 inputs and rounded once to float32;
-hits are ordered by (float32 distance ascending, label ascending).  The
-reference's own f32 SIMD accumulation order is not reproducible bit-for-bit, so
-distances are compared at 1e-4 relative (BASELINE.json north_star) and ids
-bit-exactly under this order.
+hits are ordered by (float32 distance ascending, label under the tie rule).  The
+tie rule is label DESCENDING by default — the order the reference's own golden
+shows at a tie (``test/sql/lance_optimizer_filter.test:36-44``: ids 3 and 4 tie
+at d = 2.0 and LanceDB returns 4, the higher label) — or label ascending
+(``tie="label_asc"``; ``LANCE_HIP_TIE`` sets the default, as it does for the
+library's handles).  The reference's own f32 SIMD accumulation order is not
+reproducible bit-for-bit, so distances are compared at 1e-4 relative
+(BASELINE.json north_star) and ids bit-exactly under this order.
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 
 METRICS = ("l2", "dot", "cosine")
+TIES = ("label_desc", "label_asc")
+
+
+def default_tie() -> str:
+    """The tie rule a new handle gets: ``LANCE_HIP_TIE`` or label_desc."""
+    return os.environ.get("LANCE_HIP_TIE") or "label_desc"
+
+
+def tie_desc(tie: str | None) -> bool:
+    t = tie or default_tie()
+    if t in ("label_desc", "desc"):
+        return True
+    if t in ("label_asc", "asc"):
+        return False
+    raise ValueError(f"tie must be 'label_desc' or 'label_asc', got {t!r}")
 
 
 def normalize_metric(metric: str) -> str:
@@ -68,15 +89,16 @@ def exact_distances(base: np.ndarray, q: np.ndarray, metric: str = "l2") -> np.n
     return d.astype(np.float32)
 
 
-def _order(dist32: np.ndarray, labels: np.ndarray) -> np.ndarray:
-    """Indices sorting by (float32 distance asc, label asc); NaN sorts last."""
+def _order(dist32: np.ndarray, labels: np.ndarray, tie: str | None = None) -> np.ndarray:
+    """Indices sorting by (float32 distance asc, label under the tie rule); NaN sorts last."""
     key = np.where(np.isnan(dist32), np.float32(np.inf), dist32)
     nan_last = np.isnan(dist32).astype(np.int8)
-    return np.lexsort((labels, key, nan_last))
+    lab = np.asarray(labels, dtype=np.int64)
+    return np.lexsort((-lab if tie_desc(tie) else lab, key, nan_last))
 
 
 def flat_search(base: np.ndarray, labels: np.ndarray, live: np.ndarray, q: np.ndarray, k: int,
-                metric: str = "l2"):
+                metric: str = "l2", tie: str | None = None):
     """Exact flat top-k (restates ``lance_manager.rs:393-451``).
 
     Returns ``(labels int64[n_hit], distances float32[n_hit])`` with
@@ -91,11 +113,11 @@ def flat_search(base: np.ndarray, labels: np.ndarray, live: np.ndarray, q: np.nd
     if idx.size == 0:
         return np.zeros(0, np.int64), np.zeros(0, np.float32)
     d = exact_distances(base[idx], q, metric)
-    order = _order(d, labels[idx])[:k]
+    order = _order(d, labels[idx], tie)[:k]
     return labels[idx][order], d[order]
 
 
-def flat_search_batch(base, labels, live, Q, k, metric="l2", prefilter_k=None):
+def flat_search_batch(base, labels, live, Q, k, metric="l2", prefilter_k=None, tie=None):
     """Batched exact top-k.  For large ``n`` the candidate set per query is first
     narrowed with a float64 expanded-form ranking (error ~1e-12 relative) and the
     survivors are re-scored with :func:`exact_distances`; the margin of
@@ -120,7 +142,7 @@ def flat_search_batch(base, labels, live, Q, k, metric="l2", prefilter_k=None):
     if n <= 4 * prefilter_k:
         for i in range(nq):
             d = exact_distances(X, Q[i], metric)
-            o = _order(d, L)[:k]
+            o = _order(d, L, tie)[:k]
             counts[i] = o.size
             out_l[i, :o.size] = L[o]
             out_d[i, :o.size] = d[o]
@@ -143,7 +165,7 @@ def flat_search_batch(base, labels, live, Q, k, metric="l2", prefilter_k=None):
         for j in range(Qb.shape[0]):
             cand = part[j]
             d = exact_distances(X[cand], Q[s + j], metric)
-            o = _order(d, L[cand])[:k]
+            o = _order(d, L[cand], tie)[:k]
             i = s + j
             counts[i] = o.size
             out_l[i, :o.size] = L[cand][o]
@@ -164,9 +186,10 @@ class DetachedIndexOracle:
     (``rust_lib/src/ffi.rs:37-541`` over ``lance_manager.rs``): dense labels,
     label deletes, live count, per-label vector lookup, reopen semantics."""
 
-    def __init__(self, dim: int, metric: str = "l2", next_label: int = 0):
+    def __init__(self, dim: int, metric: str = "l2", next_label: int = 0, tie: str | None = None):
         self.dim = int(dim)
         self.metric = metric
+        self.tie = tie
         self.next_label = int(next_label)
         self.vectors: dict[int, np.ndarray] = {}
 
@@ -191,7 +214,7 @@ class DetachedIndexOracle:
     # lance_manager.rs:136-169, :662-696
     def reopen(self) -> "DetachedIndexOracle":
         nxt = (max(self.vectors) + 1) if self.vectors else 0
-        o = DetachedIndexOracle(self.dim, self.metric, nxt)
+        o = DetachedIndexOracle(self.dim, self.metric, nxt, self.tie)
         o.vectors = {k: v.copy() for k, v in self.vectors.items()}
         return o
 
@@ -207,16 +230,16 @@ class DetachedIndexOracle:
         if q.shape[0] != self.dim:
             raise ValueError(f"expected query dimension {self.dim}, got {q.shape[0]}")
         X, L = self.arrays()
-        return flat_search(X, L, np.ones(L.shape[0], bool), q, k, metric or self.metric)
+        return flat_search(X, L, np.ones(L.shape[0], bool), q, k, metric or self.metric, self.tie)
 
 
 class LanceIndexOracle:
     """``src/lance_index.cpp`` semantics above the FFI: ``label_to_rowid_`` /
     ``rowid_to_label_`` maps, Search dim guard (``:442-465``), Delete (``:389-425``)."""
 
-    def __init__(self, dim: int, metric: str = "l2"):
+    def __init__(self, dim: int, metric: str = "l2", tie: str | None = None):
         self.dim = dim
-        self.detached = DetachedIndexOracle(dim, metric)
+        self.detached = DetachedIndexOracle(dim, metric, tie=tie)
         self.label_to_rowid: list[int] = []
         self.rowid_to_label: dict[int, int] = {}
 

@@ -30,7 +30,8 @@ What it restates (reference paths relative to ``/root/reference``):
             tau = 0.  P[j][c] = sum_t q_t y_t, T[l][j][c] = sum_t y_t (y_t +
             2 c_t), each an f32 sum in t order of f32 products (no fused
             multiply-add);
-            top-(k*r) by (ADC, label), exact re-rank, top-k by (dist, label)
+            top-(k*r) by (ADC, label ascending), exact re-rank, top-k by
+            (dist, label under the tie rule: flat_knn.tie_desc)
   cosine    q^ = q / f32(sqrt(sum q^2)) (an f32 division) for the coarse
             search and P; the final distances are exact cosine distances.
   u8 LUT    the fast scan (``pq_scan`` = "fast", the default): per query
@@ -79,20 +80,20 @@ def coarse_probes(C, Q, metric, nprobe):
     lab = np.arange(nl, dtype=np.int64)
     for i, q in enumerate(Qc):
         d = flat_knn.exact_distances(C, q, cm)
-        o = flat_knn._order(d, lab)[:nprobe]
+        o = flat_knn._order(d, lab, "label_asc")[:nprobe]  # probes: lower partition id at a tie
         ids[i], ds[i] = o, d[o]
     return ids, ds
 
 
-def _topk_exact(X, labels, slots, q, k, metric):
+def _topk_exact(X, labels, slots, q, k, metric, tie=None):
     if slots.size == 0:
         return np.zeros(0, np.int64), np.zeros(0, F32)
     d = flat_knn.exact_distances(X[slots], q, metric)
-    o = flat_knn._order(d, labels[slots])[:k]
+    o = flat_knn._order(d, labels[slots], tie)[:k]
     return slots[o], d[o]
 
 
-def ivf_flat_search(X, labels, live, lists, C, Q, k, nprobe, metric="l2"):
+def ivf_flat_search(X, labels, live, lists, C, Q, k, nprobe, metric="l2", tie=None):
     """IVF_FLAT: exact top-k over the live rows of the probed lists plus the
     live rows not indexed yet (``lists == -1``).  X / labels / live / lists
     are per slot (ascending labels).  Returns (labels [nq,k] -1 padded,
@@ -110,7 +111,7 @@ def ivf_flat_search(X, labels, live, lists, C, Q, k, nprobe, metric="l2"):
     for i, q in enumerate(np.asarray(Q, F32)):
         sel = live & np.isin(lists, probes[i])
         slots = np.nonzero(sel | tail)[0]
-        s, d = _topk_exact(X, labels, slots, q, k, metric)
+        s, d = _topk_exact(X, labels, slots, q, k, metric, tie)
         n = len(s)
         out_l[i, :n], out_d[i, :n], cnt[i] = labels[s], d, n
     return out_l, out_d, cnt
@@ -177,7 +178,7 @@ def pq_tables(C, codebook, Qp, metric):
 
 
 def ivf_pq_search(X, labels, live, lists, codes, C, codebook, Q, k, nprobe, refine_factor=1, metric="l2",
-                  lut="f32", query_fp8=False):
+                  lut="f32", query_fp8=False, tie=None):
     """IVF_PQ search (see the module docstring).  ``codes`` [slots, m] uint8.
     lut: "f32" (the query-major scan, pq_scan = exact_lut) or "u8" (the fast
     scan); query_fp8: ADC tables from fp8 queries (pq_query = fp8)."""
@@ -230,11 +231,11 @@ def ivf_pq_search(X, labels, live, lists, codes, C, codebook, Q, k, nprobe, refi
         if cand_adc:
             a = np.concatenate(cand_adc)
             s = np.concatenate(cand_slot)
-            o = flat_knn._order(a, labels[s])[:kp]
+            o = flat_knn._order(a, labels[s], "label_asc")[:kp]  # ADC candidates: (ADC, label ascending)
             sel = s[o]
-        ts, _ = _topk_exact(X, labels, tail, Q[i], k, metric)
+        ts, _ = _topk_exact(X, labels, tail, Q[i], k, metric, tie)
         allc = np.concatenate([sel, ts])
-        s, d = _topk_exact(X, labels, allc, Q[i], k, metric)
+        s, d = _topk_exact(X, labels, allc, Q[i], k, metric, tie)
         n = len(s)
         out_l[i, :n], out_d[i, :n], cnt[i] = labels[s], d, n
     return out_l, out_d, cnt

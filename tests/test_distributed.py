@@ -25,7 +25,11 @@ def _free_port():
 
 
 def ref_merge(gl, gd, gc):
-    """Reference merge under the (distance, label) order (test-side, numpy)."""
+    """Reference merge under the (distance, label) order, the default tie rule
+    (label_desc; LANCE_HIP_TIE) (test-side)."""
+    from oracle import flat_knn
+
+    sgn = -1 if flat_knn.tie_desc(None) else 1
     world, nq, k = gl.shape
     ol = torch.full((nq, k), -1, dtype=torch.int64)
     od = torch.full((nq, k), float("nan"), dtype=torch.float32)
@@ -34,9 +38,9 @@ def ref_merge(gl, gd, gc):
         items = []
         for s in range(world):
             for i in range(int(gc[s, q])):
-                items.append((float(gd[s, q, i]), int(gl[s, q, i])))
+                items.append((float(gd[s, q, i]), sgn * int(gl[s, q, i])))
         items.sort()
-        items = items[:k]
+        items = [(dd, sgn * l) for dd, l in items[:k]]
         oc[q] = len(items)
         for i, (d, l) in enumerate(items):
             ol[q, i] = l

@@ -22,7 +22,7 @@ import numpy as np
 import pytest
 
 from oracle import flat_knn
-from tests.golden_runner import check_filter_result, gen, hnsw_rows, load_seeded, load_sql_goldens, seeded_inputs
+from tests.golden_runner import check_expect, check_filter_result, gen, hnsw_rows, load_seeded, load_sql_goldens, seeded_inputs
 
 pytestmark = pytest.mark.gpu
 
@@ -41,15 +41,19 @@ def caller(tmp_path_factory, hip):
     return exe
 
 
-def run(exe, tmp_path, lines, timeout=240, devices=None):
+def run(exe, tmp_path, lines, timeout=240, devices=None, tie=None):
     """devices: LANCE_HIP_DEVICES for the process (e.g. "0,0": every handle it
-    creates or opens is row-sharded over two stores on device 0, shards.cpp)."""
+    creates or opens is row-sharded over two stores on device 0, shards.cpp);
+    tie: LANCE_HIP_TIE (the final order's tie rule; unset = label_desc)."""
     script = tmp_path / "script.txt"
     script.write_text("\n".join(lines) + "\n")
     env = dict(os.environ)
     env.pop("LANCE_HIP_DEVICES", None)
+    env.pop("LANCE_HIP_TIE", None)
     if devices:
         env["LANCE_HIP_DEVICES"] = devices
+    if tie:
+        env["LANCE_HIP_TIE"] = tie
     r = subprocess.run([exe, "gpu", str(script)], capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     out = r.stdout.splitlines()
@@ -121,9 +125,7 @@ def test_sql_goldens_in_torch_free_process(caller, tmp_path, case, devices):
     for st, r in zip(checks, res):
         where = st.get("ref", case["ref"])
         if "expect" in st:
-            assert len(r) == len(st["expect"]), (where, r)
-            for (rid, d), (erid, ed) in zip(r, st["expect"]):
-                assert rid == erid and math.isclose(d, ed, rel_tol=1e-4, abs_tol=1e-6), (where, r, st["expect"])
+            check_expect(r, st["expect"], where)
         if "expect_ids" in st:
             assert [x for x, _ in r] == st["expect_ids"], (where, r)
         if "expect_count" in st:
@@ -132,10 +134,12 @@ def test_sql_goldens_in_torch_free_process(caller, tmp_path, case, devices):
             assert len(r) > st["expect_count_gt"], (where, r)
 
 
+@pytest.mark.parametrize("tie", [None, "label_asc"], ids=["tie_default", "tie_asc"])
 @pytest.mark.parametrize("devices", [None, "0,0"], ids=["one_store", "two_shards"])
-def test_filter_goldens_through_arrow_in_torch_free_process(caller, tmp_path, devices):
+def test_filter_goldens_through_arrow_in_torch_free_process(caller, tmp_path, devices, tie):
     # lance_optimizer_filter.test:9-99: CREATE INDEX .. USING LANCE (embedding, lang, score), rows handed over
-    # through the Arrow C Data Interface, each WHERE pushed down as a Lance predicate
+    # through the Arrow C Data Interface, each WHERE pushed down as a Lance predicate.  Default tie rule
+    # (label_desc): every answer verbatim, including :36-44's tie (ids 3 and 4 at d = 2.0 -> 4)
     case = next(c for c in load_sql_goldens() if c["name"] == "filter_pushdown")
     rows = np.array(case["rows"], np.float32)
     lines = [f"index 3 l2 {tmp_path / 'docs'} docs_idx cols",
@@ -146,12 +150,16 @@ def test_filter_goldens_through_arrow_in_torch_free_process(caller, tmp_path, de
     lines.append("restart")  # the metadata columns persist with the table log
     for query in case["queries"]:
         lines.append(f"search {query['k']} 3 1 0 0" + (f" | {query['where']}" if query["where"] else ""))
-    out, errs = run(caller, tmp_path, lines, devices=devices)
+    out, errs = run(caller, tmp_path, lines, devices=devices, tie=tie)
     assert not errs, errs
     res = [parse_res(l) for l in out if l.startswith("res")]
     assert len(res) == 2 * len(case["queries"])
     for i, r in enumerate(res):
-        check_filter_result(case["queries"][i % len(case["queries"])], [case["ids"][rid] for rid, _ in r])
+        check_filter_result(case["queries"][i % len(case["queries"])], [case["ids"][rid] for rid, _ in r],
+                            tie or "label_desc")
+    if tie is None:  # the reference's tie golden, verbatim
+        q = next(i for i, x in enumerate(case["queries"]) if x["where"] == "score > 20")
+        assert [case["ids"][rid] for rid, _ in res[q]] == [5, 4]
 
 
 def test_rust_label_goldens_in_torch_free_process(caller, tmp_path):

@@ -27,8 +27,11 @@ def assert_same(gl, gd, gc, el, ed, ec):
         np.testing.assert_allclose(gd[i, :n], ed[i, :n], rtol=RTOL, atol=ATOL, err_msg=f"query {i}")
 
 
-def test_filter_goldens_through_index_mirror(hip, tmp_path):
-    # lance_optimizer_filter.test:9-99 — CREATE INDEX docs_idx ON docs USING LANCE (embedding, lang, score)
+@pytest.mark.parametrize("tie", ["label_desc", "label_asc"])
+def test_filter_goldens_through_index_mirror(hip, tmp_path, monkeypatch, tie):
+    # lance_optimizer_filter.test:9-99 — CREATE INDEX docs_idx ON docs USING LANCE (embedding, lang, score);
+    # the tie rule through LANCE_HIP_TIE, read when the handle is created (label_desc: :36-44 verbatim)
+    monkeypatch.setenv("LANCE_HIP_TIE", tie)
     case = next(c for c in load_sql_goldens() if c["name"] == "filter_pushdown")
     ix = hip.LanceIndex("docs_idx", 3, {}, lance_path=str(tmp_path),
                         extra_columns=[("lang", pa.string()), ("score", pa.int32())])
@@ -37,7 +40,7 @@ def test_filter_goldens_through_index_mirror(hip, tmp_path):
     q = np.array([1, 0, 0], np.float32)
     for query in case["queries"]:
         res = ix.Search(q, 3, query["k"], predicate=query["where"] or "")
-        check_filter_result(query, [case["ids"][r] for r, _ in res])
+        check_filter_result(query, [case["ids"][r] for r, _ in res], tie)
 
 
 def _meta(rng, n):

@@ -44,15 +44,17 @@ def clustered(rng, n, d, centers=48, spread=0.35):
     return (C[lab] + spread * rng.standard_normal((n, d))).astype(np.float32)
 
 
-def oracle_search(hip, h, X_by_label, Q, k, nprobe, rf, metric, lut="u8", query_fp8=False):
+def oracle_search(hip, h, X_by_label, Q, k, nprobe, rf, metric, lut="u8", query_fp8=False, tie=None):
     """lut: "u8" for the default fast scan (pq_scan = fast), "f32" for
-    pq_scan = exact_lut; query_fp8 mirrors pq_query = fp8."""
+    pq_scan = exact_lut; query_fp8 mirrors pq_query = fp8; tie: the handle's
+    tie rule (None: the default, label_desc)."""
     ex = hip.LanceHipIvfExport(h)
     X = X_by_label[ex["labels"]]
     if ex["type"] == "ivf_flat":
-        return ivf.ivf_flat_search(X, ex["labels"], ex["live"], ex["lists"], ex["centroids"], Q, k, nprobe, metric)
+        return ivf.ivf_flat_search(X, ex["labels"], ex["live"], ex["lists"], ex["centroids"], Q, k, nprobe, metric,
+                                   tie=tie)
     return ivf.ivf_pq_search(X, ex["labels"], ex["live"], ex["lists"], ex["codes"], ex["centroids"], ex["codebook"],
-                             Q, k, nprobe, rf, metric, lut=lut, query_fp8=query_fp8)
+                             Q, k, nprobe, rf, metric, lut=lut, query_fp8=query_fp8, tie=tie)
 
 
 @pytest.mark.parametrize("index_type", ["ivf_flat", "ivf_pq"])
@@ -234,6 +236,31 @@ def test_ivf_flat_bound_scan_matches_exact_scan(hip, mk, storage, metric):
         hip.LanceHipSetOption(h, "ivf_flat_scan", "exact")
         xl, xd, xc = hip.LanceDetachedSearchBatch(h, Q, k, nprobes=nprobe)
         assert_same(xl, xd, xc, el, ed, ec)
+
+
+@pytest.mark.parametrize("tie", ["label_desc", "label_asc"])
+@pytest.mark.parametrize("index_type,scan", [("ivf_flat", "bound"), ("ivf_flat", "exact"), ("ivf_pq", "fast")])
+def test_ivf_tie_rule(hip, mk, index_type, scan, tie):
+    """Exact-distance ties at the k-th place through the IVF paths (IVF_FLAT
+    bound scan + certified re-rank / its exact list scan, IVF_PQ's exact
+    re-rank) and the exact scan of the unindexed tail, under both tie rules:
+    the rule picks which tied rows come out, as the oracle's does."""
+    rng = np.random.default_rng(66)
+    n, d, nlist = 6_000, 64, 12
+    X = clustered(rng, n, d, centers=12)
+    for j, src in enumerate((100, 2000, 4000)):
+        X[rng.choice(n, 6 + 4 * j, replace=False)] = X[src]
+    Q = np.stack([X[100], X[2000], X[4000], X[100] + 0.01, X[7]]).astype(np.float32)
+    h = mk(d, "l2", index_type)
+    hip.LanceHipSetOption(h, "tie", tie)
+    hip.LanceHipSetOption(h, "ivf_flat_scan", scan) if index_type == "ivf_flat" else None
+    hip.LanceDetachedAddBatch(h, X[:5000], 5000, d)
+    hip.LanceDetachedCreateIndex(h, nlist, 8 if index_type == "ivf_pq" else 0)
+    hip.LanceDetachedAddBatch(h, X[5000:], n - 5000, d)  # the unindexed tail holds some copies too
+    rf = 20 if index_type == "ivf_pq" else 1
+    gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 8, nprobes=4, refine_factor=rf)
+    el, ed, ec = oracle_search(hip, h, X, Q, 8, 4, rf, "l2", tie=tie)
+    assert_same(gl, gd, gc, el, ed, ec)
 
 
 def test_ivf_flat_bound_scan_ties_fall_back_exactly(hip, mk):

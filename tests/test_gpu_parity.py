@@ -1,6 +1,7 @@
 """GPU parity: the HIP path through the C-ABI vs the oracle and the reference's
 goldens.  Bar (BASELINE.json north_star): returned labels bit-exact, distances
-within 1e-4 relative (f32); the canonical order is (distance, label)."""
+within 1e-4 relative (f32); the canonical order is (distance, label under the
+tie rule: label descending by default, option / LANCE_HIP_TIE label_asc)."""
 import os
 
 import numpy as np
@@ -213,12 +214,58 @@ def test_small_fixture(hip, mk, metric):
         np.testing.assert_array_equal(l, gl[i])
 
 
-def test_ties_by_label(hip, mk):
+@pytest.mark.parametrize("tie", [None, "label_desc", "label_asc"])
+def test_ties_by_label(hip, mk, tie):
     z = np.load("tests/golden/knn_ties.npz")
     h = mk(4)
+    if tie:
+        hip.LanceHipSetOption(h, "tie", tie)
     hip.LanceDetachedAddBatch(h, z["X"], 40, 4)
     gl, gd, gc = hip.LanceDetachedSearchBatch(h, z["Q"], 12)
-    assert_same(gl, gd, gc, z["labels"], z["dists"], z["counts"])
+    sfx = "_asc" if tie == "label_asc" else ""
+    assert_same(gl, gd, gc, z["labels" + sfx], z["dists" + sfx], z["counts" + sfx])
+    for i in range(len(z["Q"])):  # the one-query entry point (small exact kernel) agrees
+        l, d = hip.LanceDetachedSearch(h, z["Q"][i], 4, 12)
+        np.testing.assert_array_equal(l, gl[i])
+
+
+def test_tie_option_rejects_unknown(hip, mk):
+    h = mk(4)
+    with pytest.raises(hip.IOException, match="tie must be"):
+        hip.LanceHipSetOption(h, "tie", "random")
+
+
+@pytest.mark.parametrize("tie", ["label_desc", "label_asc"])
+@pytest.mark.parametrize("path", ["small_exact", "dense", "threshold"])
+def test_tie_rule_on_every_path(hip, mk, tie, path):
+    """Tie groups straddling the k-th place on each search path (one-launch small
+    exact search, the dense path of small stores, the threshold path with its
+    reruns / batched and per-query exact fallbacks), under both tie rules, vs
+    the oracle: the rule decides WHICH tied rows come out, not only their order."""
+    rng = np.random.default_rng(606)
+    d, k = 128, 10
+    n = {"small_exact": 3000, "dense": 40_000, "threshold": 120_000}[path]
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    base = rng.standard_normal((6, d)).astype(np.float32)
+    for j in range(6):  # group j: 4 + 3 j copies scattered over the store
+        X[rng.choice(n, 4 + 3 * j, replace=False)] = base[j]
+    Q = np.concatenate([base, base + np.float32(0.001), rng.standard_normal((4, d))]).astype(np.float32)
+    live = np.ones(n, bool)
+    live[rng.choice(n, n // 50, replace=False)] = False
+    h = mk(d)
+    hip.LanceHipSetOption(h, "tie", tie)
+    hip.LanceDetachedAddBatch(h, X, n, d)
+    hip.LanceDetachedDeleteBatch(h, np.nonzero(~live)[0])
+    el, ed, ec = c_oracle.flat_search_batch(X, Q, k, "l2", live=live, acc64=True, nthreads=16, tie=tie)
+    if path == "small_exact":
+        for i in range(len(Q)):
+            l, dd = hip.LanceDetachedSearch(h, Q[i], d, k)
+            np.testing.assert_array_equal(l, el[i, :ec[i]], err_msg=f"query {i}")
+        return
+    gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, k)
+    assert_same(gl, gd, gc, el, ed, ec)
+    st = hip.LanceHipLastSearchStats(h)
+    assert st["dense_path"] == (path == "dense")
 
 
 @pytest.mark.parametrize("spec", load_seeded(), ids=lambda s: s["name"])
@@ -264,23 +311,29 @@ def test_sampled_path_with_deletes_and_many_queries(hip, mk):
     assert_same(gl, gd, gc, el, ed, ec)
 
 
-def test_duplicates_force_exact_fallback(hip, mk):
+@pytest.mark.parametrize("tie", ["label_desc", "label_asc"])
+def test_duplicates_force_exact_fallback(hip, mk, tie):
     # 100k identical rows: every lower bound ties, the certificate cannot hold,
-    # the exact fallback must return the k smallest labels
+    # the exact fallback must return the k largest (label_desc) / smallest labels
     n, d = 100_000, 32
     X = np.ones((n, d), np.float32)
     h = mk(d)
+    hip.LanceHipSetOption(h, "tie", tie)
     hip.LanceDetachedAddBatch(h, X, n, d)
-    hip.LanceDetachedDeleteBatch(h, [0, 5])
+    hip.LanceDetachedDeleteBatch(h, [0, 5, n - 2])
     gl, gd, gc = hip.LanceDetachedSearchBatch(h, np.ones((2, d), np.float32), 10)
-    assert list(gl[0]) == [1, 2, 3, 4, 6, 7, 8, 9, 10, 11]
+    if tie == "label_asc":
+        assert list(gl[0]) == [1, 2, 3, 4, 6, 7, 8, 9, 10, 11]
+    else:
+        assert list(gl[0]) == [n - 1] + list(range(n - 3, n - 12, -1))
     assert np.all(gd == 0)
     st = hip.LanceHipLastSearchStats(h)
     assert st["fallback_queries"] == 2 and st["retried_queries"] == 2
 
 
+@pytest.mark.parametrize("tie", ["label_desc", "label_asc"])
 @pytest.mark.parametrize("metric", ["l2", "cosine"])
-def test_batched_exact_fallback_many_queries(hip, mk, metric):
+def test_batched_exact_fallback_many_queries(hip, mk, metric, tie):
     # 50 vectors each repeated ~1600 times among 100k rows: a query equal to
     # one of them ties at its nearest distance with ~1600 rows, so no
     # certificate can hold; the 50 queries (4 groups of the batched fallback)
@@ -296,12 +349,13 @@ def test_batched_exact_fallback_many_queries(hip, mk, metric):
     live = np.ones(n, bool)
     live[rng.choice(n, 3000, replace=False)] = False
     h = mk(d, metric)
+    hip.LanceHipSetOption(h, "tie", tie)
     hip.LanceDetachedAddBatch(h, X, n, d)
     hip.LanceDetachedDeleteBatch(h, np.nonzero(~live)[0])
     gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, k)
     st = hip.LanceHipLastSearchStats(h)
     assert st["fallback_queries"] >= 50, st
-    el, ed, ec = c_oracle.flat_search_batch(X, Q[:50], k, metric, live=live, acc64=True, nthreads=16)
+    el, ed, ec = c_oracle.flat_search_batch(X, Q[:50], k, metric, live=live, acc64=True, nthreads=16, tie=tie)
     assert_same(gl[:50], gd[:50], gc[:50], el, ed, ec)
     assert gc[50] == k
 
@@ -364,9 +418,11 @@ def test_merge_topk_kernel(hip):
             pd[s, q, :c] = d
             pl[s, q, :c] = s * 1000 + np.arange(c)
     ol, od, oc = hip.LanceHipMergeTopk(pl, pd, pc)
+    desc = flat_knn.tie_desc(None)  # the public merge: the process's LANCE_HIP_TIE (default label_desc)
     for q in range(nq):
-        items = [(pd[s, q, i], pl[s, q, i]) for s in range(nshard) for i in range(pc[s, q])]
+        items = [(pd[s, q, i], -pl[s, q, i] if desc else pl[s, q, i]) for s in range(nshard) for i in range(pc[s, q])]
         items.sort()
+        items = [(dd, -l if desc else l) for dd, l in items]
         items = items[:k]
         assert oc[q] == len(items)
         assert list(ol[q, :oc[q]]) == [l for _, l in items]

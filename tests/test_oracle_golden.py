@@ -42,14 +42,22 @@ def test_oracle_sql_goldens(case):
     run_index_case(case, _OracleIx, _restart)
 
 
-def test_oracle_filter_goldens():
+@pytest.mark.parametrize("tie", ["label_desc", "label_asc"])
+def test_oracle_filter_goldens(tie):
+    # label_desc (the default): every answer of lance_optimizer_filter.test verbatim, :36-44's tie included
     case = next(c for c in load_sql_goldens() if c["name"] == "filter_pushdown")
     X = np.array(case["rows"], np.float32)
     for q in case["queries"]:
         keep = np.array([eval_predicate(q["where"], l, s) for l, s in zip(case["lang"], case["score"])])
-        labs, d = flat_knn.flat_search(X, np.arange(len(X)), keep, np.array([1, 0, 0], np.float32), q["k"])
+        labs, d = flat_knn.flat_search(X, np.arange(len(X)), keep, np.array([1, 0, 0], np.float32), q["k"], tie=tie)
         ids = [case["ids"][i] for i in labs]
-        check_filter_result(q, ids)
+        check_filter_result(q, ids, tie)
+        if tie == "label_desc":
+            assert ids == q["expect_ids"]
+        keep8 = keep.astype(np.uint8)
+        lc, _, _ = c_oracle.flat_search_batch(X, np.array([[1, 0, 0]], np.float32), q["k"], "l2", live=keep8,
+                                              acc64=True, nthreads=1, tie=tie)
+        assert list(lc[0, :len(labs)]) == list(labs)
 
 
 def test_oracle_rust_label_semantics():
@@ -109,10 +117,17 @@ def test_ties_break_by_label():
     z = np.load("tests/golden/knn_ties.npz")
     l, d, c = flat_knn.flat_search_batch(z["X"], np.arange(40), np.ones(40, bool), z["Q"], 12)
     np.testing.assert_array_equal(l, z["labels"])
-    # 10 identical rows at distance 0: labels ascending
-    assert list(l[0, :10]) == list(range(10))
+    # 10 identical rows at distance 0: the default tie rule, labels descending
+    assert list(l[0, :10]) == list(range(9, -1, -1))
     lc, dc, _ = c_oracle.flat_search_batch(z["X"], z["Q"], 12, "l2", acc64=True, nthreads=3)
     np.testing.assert_array_equal(lc, l)
+    # 20 rows tie at the second query's k-th distance: the tie rule picks which come out
+    assert list(l[1]) == list(range(19, 7, -1))
+    la, _, _ = flat_knn.flat_search_batch(z["X"], np.arange(40), np.ones(40, bool), z["Q"], 12, tie="label_asc")
+    np.testing.assert_array_equal(la, z["labels_asc"])
+    assert list(la[0, :10]) == list(range(10)) and list(la[1]) == list(range(12))
+    lca, _, _ = c_oracle.flat_search_batch(z["X"], z["Q"], 12, "l2", acc64=True, nthreads=3, tie="label_asc")
+    np.testing.assert_array_equal(lca, la)
 
 
 @pytest.mark.parametrize("spec", [s for s in load_seeded() if s["n"] <= 10000], ids=lambda s: s["name"])

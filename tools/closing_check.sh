@@ -1,11 +1,12 @@
 #!/bin/bash
-# round-5 closing check on one MI355X, in three calls:
+# closing check on one MI355X (usage: tools/closing_check.sh A|B|C|S TAG), in separate calls:
 #   A: the committed tree's GPU suite and smoke
 #   B: the driver's bench command, its rocprofv3 kernel stats, the other configs' lines, per-rank
 #      shapes, the in-process two-shard form, and the C5 step's kernel stats
 #   C: PMC traffic passes of each config's dominant kernel (tools/pmc_configs.sh)
+#   S: one config's step: bench line + rocprofv3 kernel trace (CFG=c2|nstar|c4|c5, STEPS)
 source tools/gpu_step.sh
-T=${2:-r05f}
+T=${2:-r06f}
 case $1 in
 A)
 	step ${T}_pytest 1100 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread
@@ -24,9 +25,19 @@ B)
 	step ${T}_rank_nstar8 200 python -u bench.py --n 1250000 --steps 30 --no-cpu-baseline --no-host-batch
 	step ${T}_inproc 300 python -u bench.py --inproc --inproc-devices 0,0 --steps 20 --no-cpu-baseline --no-host-batch
 	step ${T}_prof_c5 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof_c5 -o run -- python3 bench.py --config c5 --steps 10 --no-cpu-baseline --no-recall --no-host-batch
+	python3 tools/trace_kernels.py gpurun_out/${T}_prof_c5/run_kernel_trace.csv 10 > gpurun_out/${T}_c5_step_kernels.txt 2>&1
 	rm -f gpurun_out/${T}_prof_c*/run_kernel_trace.csv.gz
 	;;
 C)
 	step ${T}_pmc 1100 bash tools/pmc_configs.sh $T c2 nstar c3 c4 c5
+	;;
+S)
+	C=${CFG:-c2}
+	N=${STEPS:-10}
+	step ${T}_${C} 400 python -u bench.py --config $C --steps $N --no-cpu-baseline
+	step ${T}_prof_${C} 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof_${C} -o run -- python3 bench.py --config $C --steps $N --no-cpu-baseline --no-recall --no-host-batch
+	python3 tools/trace_kernels.py gpurun_out/${T}_prof_${C}/run_kernel_trace.csv $N > gpurun_out/${T}_${C}_step_kernels.txt 2>&1
+	rm -f gpurun_out/${T}_prof_${C}/run_kernel_trace.csv
+	cat gpurun_out/${T}_${C}_step_kernels.txt
 	;;
 esac
