@@ -2384,6 +2384,21 @@ __device__ __forceinline__ uint32_t lds_ld32(uint32_t a) {
 __device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) {
 	*(__attribute__((address_space(3))) uint32_t *)(size_t)a = v;
 }
+// store at base + a compile-time byte offset (the offset folds into the
+// ds_write immediate: one address register for a thread's 16 LUT stores)
+template <uint32_t OFF>
+__device__ __forceinline__ void lds_st32o(uint32_t base, uint32_t v) {
+	*(__attribute__((address_space(3))) uint32_t *)((__attribute__((address_space(3))) uint8_t *)(size_t)base + OFF) = v;
+}
+// threadIdx.x through an opaque copy: lane quantities derived from it inside
+// the item loop are recomputed per item (a few VALU ops) instead of hoisted
+// out of it, where their long live ranges spilled at m = 96 (21 VGPRs, 88 B of
+// scratch reloaded at every item start, round 5)
+__device__ __forceinline__ int opaque_tid() {
+	int v = (int)threadIdx.x;
+	asm volatile("" : "+v"(v));
+	return v;
+}
 constexpr int FB_RS = 4;                            // row steps per lane and round
 constexpr int FB_ROWS = FB_THREADS / 8 * FB_RS;     // rows per round (512)
 template <int W>
@@ -2511,27 +2526,28 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 		};
 		Rows RA, RB;
 		load(0, RA);
-		if (t < FQ_G) {
-			const int id = t == 0 ? e1.x : t == 1 ? e1.y : t == 2 ? e1.z : e1.w;
+		const int tl = opaque_tid();  // (the item-start block's lane quantities: short live ranges)
+		if (tl < FQ_G) {
+			const int id = tl == 0 ? e1.x : tl == 1 ? e1.y : tl == 2 ? e1.z : e1.w;
 			const int q = id >= 0 ? id / nprobe : -1;
 			if (q >= 0) {
-				d0s[t] = probe_d[id];
+				d0s[tl] = probe_d[id];
 				const float2 qp = qpar[q];
-				dls[t] = qp.x;
-				l0s[t] = qp.y;
-				thr[t] = thrq[q];
+				dls[tl] = qp.x;
+				l0s[tl] = qp.y;
+				thr[tl] = thrq[q];
 			} else {
-				thr[t] = 0;
+				thr[tl] = 0;
 			}
-			qid[t] = q;
-			cnt[t] = 0;
+			qid[tl] = q;
+			cnt[tl] = 0;
 		}
 		// LUT: thread (word set xs, piece cp of 16 codes, bank b = 4 pp + yy) writes
 		// the 16 entries of subspaces 4W pp + 4x + yy for x = xs, xs + 2: the 32 lanes
 		// of a store group write 32 distinct banks
 		{
 			constexpr int NX = (W + 1) / 2;
-			const int b = t & 31, cp = (t >> 5) & 15, xs = t >> 9;
+			const int b = tl & 31, cp = (tl >> 5) & 15, xs = tl >> 9;  // (xs: 0 or 1)
 			uint4 w[NX][FQ_G];
 #pragma unroll
 			for (int xi = 0; xi < NX; ++xi) {
@@ -2546,15 +2562,20 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 					                                : make_uint4(0u, 0u, 0u, 0u);
 #endif
 			}
-#pragma unroll
-			for (int xi = 0; xi < NX; ++xi) {
+			// x = xs + 2 xi with xs in {0, 1}: xi = 0 is word 0 / 1 (the v_perm region
+			// when W >= 2, 256-B code rows), xi = 1 word 2 / 3 (the compact region,
+			// 128-B rows): the row stride is a compile-time constant per xi, so a
+			// thread's 16 stores of one xi are one base register + ds immediates
+			auto store_x = [&](auto xic) __attribute__((always_inline)) {
+				constexpr int xi = decltype(xic)::value;
+				constexpr uint32_t CS = (xi == 0 && NPERM == 2) ? 256u : 128u;
 				const int x = xs + 2 * xi;
-				if (x >= W) continue;
+				if (x >= W) return;
 				const uint32_t dst = x < NPERM ? PBASE + 128 * x + 4 * b : (x - NPERM) * 32768 + 4 * b;
-				const uint32_t cstride = x < NPERM ? 256 : 128;
-#pragma unroll
-				for (int sub = 0; sub < 4; ++sub) {
-					const uint4 *wx = w[xi];
+				const uint32_t base = dst + (uint32_t)cp * 16u * CS;
+				const uint4 *wx = w[xi];
+				auto sub4 = [&](auto subc) __attribute__((always_inline)) {
+					constexpr int sub = decltype(subc)::value;
 					const uint32_t w0 = sub == 0 ? wx[0].x : sub == 1 ? wx[0].y : sub == 2 ? wx[0].z : wx[0].w;
 					const uint32_t w1 = sub == 0 ? wx[1].x : sub == 1 ? wx[1].y : sub == 2 ? wx[1].z : wx[1].w;
 					const uint32_t w2 = sub == 0 ? wx[2].x : sub == 1 ? wx[2].y : sub == 2 ? wx[2].z : wx[2].w;
@@ -2563,19 +2584,25 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 					const uint32_t a23 = __builtin_amdgcn_perm(w3, w2, 0x05010400u);
 					const uint32_t b01 = __builtin_amdgcn_perm(w1, w0, 0x07030602u);
 					const uint32_t b23 = __builtin_amdgcn_perm(w3, w2, 0x07030602u);
-					const uint32_t c = (uint32_t)(cp * 16 + sub * 4);
-					lds_st32(dst + (c + 0) * cstride, __builtin_amdgcn_perm(a23, a01, 0x05040100u));
-					lds_st32(dst + (c + 1) * cstride, __builtin_amdgcn_perm(a23, a01, 0x07060302u));
-					lds_st32(dst + (c + 2) * cstride, __builtin_amdgcn_perm(b23, b01, 0x05040100u));
-					lds_st32(dst + (c + 3) * cstride, __builtin_amdgcn_perm(b23, b01, 0x07060302u));
-				}
-			}
+					lds_st32o<(sub * 4 + 0) * CS>(base, __builtin_amdgcn_perm(a23, a01, 0x05040100u));
+					lds_st32o<(sub * 4 + 1) * CS>(base, __builtin_amdgcn_perm(a23, a01, 0x07060302u));
+					lds_st32o<(sub * 4 + 2) * CS>(base, __builtin_amdgcn_perm(b23, b01, 0x05040100u));
+					lds_st32o<(sub * 4 + 3) * CS>(base, __builtin_amdgcn_perm(b23, b01, 0x07060302u));
+				};
+				sub4(std::integral_constant<int, 0>{});
+				sub4(std::integral_constant<int, 1>{});
+				sub4(std::integral_constant<int, 2>{});
+				sub4(std::integral_constant<int, 3>{});
+			};
+			store_x(std::integral_constant<int, 0>{});
+			if constexpr (NX > 1) store_x(std::integral_constant<int, 1>{});
 		}
 		__syncthreads();
 		PQ_T(1);
-		const int myq = qid[pq];
-		const float myd0 = d0s[pq], mydl = dls[pq], myl0 = l0s[pq];
-		uint64_t mythr = thr[pq];
+		const int pql = tl & 3;  // (= pq)
+		const int myq = qid[pql];
+		const float myd0 = d0s[pql], mydl = dls[pql], myl0 = l0s[pql];
+		uint64_t mythr = thr[pql];
 		auto round = [&](const Rows &R, Rows &N, uint32_t rpre, uint64_t &gprev, bool first) __attribute__((always_inline)) {
 			uint64_t gthr = KEY64_NONE;  // (the query's bound from its other items: as pq_fast_scan_kernel)
 			if (t < FQ_G && qid[t] >= 0) gthr = __builtin_nontemporal_load(thrq + qid[t]);

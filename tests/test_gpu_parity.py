@@ -144,7 +144,7 @@ def test_k_and_empty_edge_cases(hip, mk):
     l, d = hip.LanceDetachedSearch(h, np.zeros(4, np.float32), 4, 0)
     assert l.size == 0
     l, d = hip.LanceDetachedSearch(h, np.array([1, 0, 0, 0], np.float32), 4, 10)  # k > n
-    assert list(l) == [0, 1, 2, 3]
+    assert list(l) == [0, 3, 2, 1]  # labels 1..3 tie at d = 2: the default tie rule, label descending
     np.testing.assert_allclose(d, [0, 2, 2, 2])
     hip.LanceDetachedDeleteBatch(h, [0, 1, 2, 3])
     assert hip.LanceDetachedCount(h) == 0

@@ -73,15 +73,21 @@ def _kernel_metadata(obj):
 @pytest.mark.skipif(not OBJS or not os.path.exists(os.path.join(LLVM, "llvm-readelf")),
                     reason="needs the built objects (make) and the ROCm LLVM tools")
 def test_hot_kernels_do_not_spill():
-    """The C2 / north_star hot kernels keep every value in registers: a scratch
-    spill in pool_refine's final mode cost 69 -> 104 us per C2 batch (round 4),
-    so a register-allocation change that spills fails here, before the GPU."""
+    """The hot kernels keep every value in registers: a scratch spill in
+    pool_refine's final mode cost 69 -> 104 us per C2 batch (round 4), and the
+    m = 96 PQ fast scan reloaded 88 B of spilled lane state at every item start
+    (round 5), so a register-allocation change that spills fails here, before
+    the GPU.  Covered: scan8 (C2 / north_star / C3), pool_refine (f32), the
+    PQ fast scans (C5) and the IVF_FLAT bound scan (C4)."""
     meta = {}
     for obj in OBJS:
-        if os.path.basename(obj) in ("knn_kernels.o", "scan8_kernels.o"):
+        if os.path.basename(obj) in ("knn_kernels.o", "scan8_kernels.o", "ivf_kernels.o"):
             meta.update(_kernel_metadata(obj))
-    hot = [k for k in meta if ("pool_refine_kernel" in k and "Ef" in k) or "scan8_kernel" in k]
+    hot = [k for k in meta if ("pool_refine_kernel" in k and "Ef" in k) or "scan8_kernel" in k
+           or "pq_fast_scan_bank_kernel" in k or "flat_list_lb_kernel" in k]
     assert len(hot) >= 10, sorted(meta)[:20]
+    assert sum("pq_fast_scan_bank_kernel" in k for k in hot) == 3, hot  # m = 32, 64, 96
+    assert sum("flat_list_lb_kernel" in k for k in hot) == 3, hot       # l2, dot, cosine
     spills = {k: v for k, v in meta.items() if k in hot and v[0] != 0}
     assert not spills, spills
 
