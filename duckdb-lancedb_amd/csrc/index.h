@@ -100,6 +100,7 @@ struct PassBufs {
 	DevBuf<int> status;
 	DevBuf<uint2> seg_pool;       // threshold path: per-(workgroup, query) segments of this pass
 	DevBuf<int> seg_cnt;
+	DevBuf<unsigned long long> s8prog;  // scan8 pair-coupling progress words (epoch-tagged: zeroed once)
 	int *h_status = nullptr;      // pinned
 	int *d_status_map = nullptr;  // its device-visible address
 	size_t h_status_n = 0;
@@ -121,6 +122,19 @@ struct PassBufs {
 		HIPCHK(hipHostGetDevicePointer(&dv, h_status, 0));
 		d_status_map = static_cast<int *>(dv);
 	}
+};
+
+// A sharded search enqueued on every shard (shards.cpp shard_submit): the
+// shards' tickets, merged at shard_finish_oldest into the caller's outputs.
+struct ShardPending {
+	int64_t ticket = 0;
+	int slot = 0, nq = 0, k = 0, odev = -1;  // odev: device of the outputs (-1: host / unknown)
+	bool out_host = false;
+	std::vector<int64_t> st;
+	std::vector<char> empty;
+	int64_t *L = nullptr;
+	float *D = nullptr;
+	int *C = nullptr;
 };
 
 // An enqueued pass whose completion check (certificates, reruns, fallback)
@@ -282,10 +296,22 @@ struct Index {
 	// the table log, and merges the shards' top-k lists on the first device
 	std::vector<std::unique_ptr<Index>> shards;
 	bool sharded() const { return !shards.empty(); }
-	DevBuf<int64_t> m_pl;
-	DevBuf<float> m_pd;
-	DevBuf<int> m_pc;
-	DevBuf<uint8_t> m_out;
+	// per in-flight search slot (two sharded searches may be in flight): the
+	// shards' partial lists on the first device, the merged lists when the
+	// caller's outputs live elsewhere (host, another device)
+	DevBuf<int64_t> m_pl[2];
+	DevBuf<float> m_pd[2];
+	DevBuf<int> m_pc[2];
+	DevBuf<uint8_t> m_out[2];
+	std::deque<ShardPending> spending;  // sharded searches enqueued, not merged yet (<= 2)
+	// as a shard: its queries / partial lists per parent slot, and the event its
+	// peer copies of a slot's lists end at (the merge stream waits on it)
+	DevBuf<float> sh_q[2];
+	DevBuf<uint8_t> sh_out[2];
+	hipEvent_t sh_ev[2] = {nullptr, nullptr};
+	// option calls made before the handle became multi-device, replayed on each
+	// shard by shard_init (so `devices` may come after other options)
+	std::vector<std::pair<std::string, std::string>> opt_log;
 
 	// optional HIP-event timing of the scan kernels, on the stream they run on
 	bool time_kernels = false;
@@ -305,6 +331,7 @@ struct Index {
 	int pr_first = 0;    // option "pr_first": pool_refine's first final-mode chunk (0 = the kernel's default)
 	int s8_variant = 0;  // option "scan8_variant": scan8 geometry (release builds: 0 only)
 	int tie_desc = 1;    // option "tie" / LANCE_HIP_TIE: 1 = (distance, label desc), 0 = (distance, label asc)
+	int s8_couple = 0;   // option "s8_couple": scan8 pair coupling lag in 32-row units (0 = off; speed only)
 	double kt_append_ms = 0.0, kt_dense_ms = 0.0;
 	int64_t kt_append_n = 0, kt_dense_n = 0;
 	int64_t kt_append_rows = 0, kt_append_qpad = 0;
@@ -331,6 +358,8 @@ struct Index {
 		if (rowaux_l2) (void)hipFree(rowaux_l2);
 		if (dlabels) (void)hipFree(dlabels);
 		for (auto &e : ev)
+			if (e) (void)hipEventDestroy(e);
+		for (auto &e : sh_ev)
 			if (e) (void)hipEventDestroy(e);
 		if (stream) (void)hipStreamDestroy(stream);
 		for (auto &ps : pstream)
@@ -828,6 +857,13 @@ int64_t shard_add(Index *ix, const float *v, int64_t num, int vdev, Index **into
 std::vector<int64_t> shard_remove(Index *ix, const int64_t *labels, int64_t n);
 void shard_search(Index *ix, const float *Q, int qdev, int nq, int k, int nprobes, int refine, const char *pred,
                   int64_t *L, float *D, int *C, bool out_host);
+// asynchronous sharded search (no predicate): every shard's pass enqueued, a
+// ticket back; shard_finish_oldest completes the oldest (certificates on every
+// shard, peer copies, the merge on the first device into the outputs on device
+// odev, -1 = host)
+int64_t shard_submit(Index *ix, const float *Q, int qdev, int nq, int k, int nprobes, int refine, int64_t *L,
+                     float *D, int *C, bool out_host, int odev);
+void shard_finish_oldest(Index *ix);
 Index *shard_of_label(Index *ix, int64_t label, int64_t *slot);
 void shard_all_rows(Index *ix, std::vector<int64_t> &labels, std::vector<float> &vecs);
 void shard_compact(Index *ix);

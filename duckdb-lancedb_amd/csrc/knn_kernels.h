@@ -53,6 +53,12 @@ struct StoreView {
 	// tie rule of the final order (option "tie"): 0 = (distance, label asc),
 	// 1 = (distance, label desc) (device_common.h tie_x64)
 	int tie_desc = 0;
+	// scan8 pair coupling (option "s8_couple", speed only): a workgroup of a pair
+	// does not start a 32-row unit more than s8_couple units ahead of its
+	// partner's progress (s8_prog: one word per workgroup, epoch-tagged, owned by
+	// the pass's stream); 0 = off
+	unsigned long long *s8_prog = nullptr;
+	int s8_couple = 0;
 };
 
 // Per-query constants for the lower-bound epilogue:
@@ -138,6 +144,7 @@ int scan_grid(int64_t n_tiles);
 // launches over disjoint ranges fill disjoint segment sets of one pool.
 bool scan8_fits(const StoreView &s);
 int scan8_segments(int64_t n_tiles);
+int scan8_prog_words();  // StoreView::s8_prog words (pair coupling)
 bool scan8_variant_ok(int v);  // a geometry this build carries (release: 0 only)
 void launch_scan8_append(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
                          int seg_cap, hipStream_t st, int64_t t0 = 0, int64_t t1 = -1, int seg_base = 0);

@@ -97,6 +97,14 @@ bool Index::enqueue_chunk(const float *dQ, int nq, int k, int refine, int64_t *d
 	sv.pr_first = pr_first;
 	sv.s8_variant = s8_variant;
 	sv.tie_desc = tie_desc;
+	if (s8_couple > 0) {
+		if (!P.s8prog.p) {
+			P.s8prog.need((size_t)scan8_prog_words());
+			HIPCHK(hipMemsetAsync(P.s8prog.p, 0, (size_t)scan8_prog_words() * sizeof(unsigned long long), st));
+		}
+		sv.s8_prog = P.s8prog.p;
+		sv.s8_couple = s8_couple;
+	}
 	last_scan_esz = use8 ? 1 : (xbf16 || Xs) ? 2 : 4;
 	if (use8) {
 		ensure_i8();
@@ -501,10 +509,12 @@ void Index::finish_oldest() {
 }
 
 void Index::wait_ticket(int64_t ticket) {
+	while (!spending.empty() && (ticket <= 0 || spending.front().ticket <= ticket)) shard_finish_oldest(this);
 	while (!pending.empty() && (ticket <= 0 || pending.front().ticket <= ticket)) finish_oldest();
 }
 
 void Index::drain() {
+	while (!spending.empty()) shard_finish_oldest(this);
 	while (!pending.empty()) finish_oldest();
 }
 
@@ -1315,6 +1325,192 @@ int32_t lance_detached_get_all_vectors(void *handle, int64_t *out_labels, float 
 	API_GUARD("get_all_vectors failed: ", -1)
 }
 
+}  // extern "C"
+
+// the options of one store (a single-device handle, or each shard of a
+// multi-device one); throws on a bad key / value
+static void set_option_store(Index *ix, const std::string &k, const std::string &v) {
+	if (k == "s8_couple") {  // scan8 pair coupling lag in 32-row units (0 = off; results exact for any value)
+		const int c = std::stoi(v);
+		if (c < 0 || c > 4096) throw Error("s8_couple must be in [0, 4096]");
+		ix->s8_couple = c;
+		return;
+	}
+	if (k == "tie") {  // the final order's tie rule (label_desc reproduces the reference's tie golden)
+		ix->tie_desc = lhip::parse_tie(v);
+		return;
+	}
+	if (k == "metric_quirk") {
+		bool on = (v == "1" || v == "true");
+		if (on && ix->metric != lhip::METRIC_L2 && !ix->rowaux_l2) {
+			// build L2 aux for the rows already stored
+			ix->bind();
+			HIPCHK(hipMalloc(&ix->rowaux_l2, (size_t)std::max<int64_t>(ix->cap, 1) * sizeof(float4)));
+			if (ix->n_slots > 0) {
+				lhip::launch_rowaux(ix->X, ix->xbf16, ix->ld, ix->dim, lhip::METRIC_L2, 0, ix->n_slots, ix->rowaux_l2,
+				                    ix->stats.p + 2, ix->stream);
+				// re-apply tombstones
+				std::vector<int64_t> dead;
+				for (int64_t s = 0; s < ix->n_slots; ++s)
+					if (!ix->live[(size_t)s]) dead.push_back(s);
+				if (!dead.empty()) {
+					ix->ws.idx.need(dead.size());
+					HIPCHK(hipMemcpyAsync(ix->ws.idx.p, dead.data(), dead.size() * sizeof(int64_t),
+					                      hipMemcpyHostToDevice, ix->stream));
+					lhip::launch_tombstone(ix->rowaux_l2, ix->ws.idx.p, (int)dead.size(), ix->stream);
+				}
+				HIPCHK(hipStreamSynchronize(ix->stream));
+				ix->refresh_stats();
+			}
+		}
+		ix->metric_quirk = on;
+		return;
+	}
+	if (k == "time_kernels") {
+		ix->bind();
+		ix->time_kernels = (v == "1" || v == "true");
+		for (auto &e : ix->ev)
+			if (!e) HIPCHK(hipEventCreate(&e));
+		ix->kt_append_ms = ix->kt_dense_ms = 0.0;
+		ix->kt_append_n = ix->kt_dense_n = 0;
+		ix->kt_ivf_ms = ix->kt_ivf_bytes = ix->kt_ivf_pair_rows = ix->kt_ivf_coarse_ms = 0.0;
+		ix->kt_ivf_n = 0;
+		return;
+	}
+	if (k == "storage") {
+		if (v != "f32" && v != "bf16") throw Error("storage must be 'f32' or 'bf16'");
+		ix->bind();
+		const bool was = ix->xbf16;
+		ix->set_storage(v == "bf16");
+		if (was != ix->xbf16) ix->log_storage();
+		return;
+	}
+	if (k == "scan_copy") {
+		if (v != "on" && v != "off") throw Error("scan_copy must be 'on' or 'off'");
+		ix->bind();
+		ix->set_scan_copy(v == "on");
+		return;
+	}
+	if (k == "scan_i8") {
+		if (v != "on" && v != "off") throw Error("scan_i8 must be 'on' or 'off'");
+		ix->bind();
+		ix->scan_i8 = v == "on";
+		if (!ix->scan_i8) ix->drop_i8();
+		return;
+	}
+
+	if (k == "prepare") {
+		// build the derived scan structures now (the int8 scan copy) instead
+		// of on the first search after a change
+		ix->bind();
+		if (ix->i8_usable()) ix->ensure_i8();
+		return;
+	}
+	if (k == "pr_first") {  // this handle's first final-mode pool_refine chunk (results exact for any value)
+		const int r = std::stoi(v);
+		if (r != 0 && (r < 8 || r > lhip::pool_refine_max_first()))
+			throw Error("pr_first must be 0 (default) or in [8, " + std::to_string(lhip::pool_refine_max_first()) + "]");
+		ix->pr_first = r;
+		return;
+	}
+	if (k == "scan8_variant") {  // this handle's ld = 768 scan8 geometry; release builds: 0 only
+		const int r = std::stoi(v);
+		if (!lhip::scan8_variant_ok(r))
+			throw Error("scan8_variant " + v + " exists only in development (LHIP_ABLATION_BUILD) builds");
+		ix->s8_variant = r;
+		return;
+	}
+	if (k == "cand_extra_i8") {
+		const int d = std::stoi(v);
+		if (d != 0 && (d < 8 || d > 256)) throw Error("cand_extra_i8 must be 0 (auto) or in [8, 256]");
+		ix->cand_extra_i8 = d;
+		return;
+	}
+	if (k == "cand_extra") {
+		const int d = std::stoi(v);
+		if (d < 8 || d > 256) throw Error("cand_extra must be in [8, 256]");
+		ix->cand_extra = d;
+		return;
+	}
+	if (k == "small_exact") {
+		ix->small_exact = (v == "1" || v == "on" || v == "true");
+		return;
+	}
+
+	if (k == "retry_pass") {
+		ix->retry_pass = (v == "1" || v == "on" || v == "true");
+		return;
+	}
+	if (k == "split_div") {  // progressive threshold of the int8 append pass (0 or 1: one pass)
+		const int d = std::stoi(v);
+		if (d < 0 || d > 64) throw Error("split_div must be in [0, 64]");
+		ix->split_div = d;
+		return;
+	}
+	if (k == "sample_div") {
+		const int d = std::stoi(v);
+		if (d < 0) throw Error("sample_div must be >= 1, or 0 (auto)");
+		ix->sample_div = d;
+		return;
+	}
+	if (k == "index_type") {
+		if (v == "ivf_pq" || v == "IVF_PQ")
+			ix->ivf_type_opt = lhip::IVF_PQ;
+		else if (v == "ivf_flat" || v == "IVF_FLAT")
+			ix->ivf_type_opt = lhip::IVF_FLAT;
+		else
+			throw Error("index_type must be 'ivf_pq' or 'ivf_flat'");
+		return;
+	}
+	if (k == "kmeans_iters") {
+		const int it = std::stoi(v);
+		if (it < 0) throw Error("kmeans_iters must be >= 0");
+		ix->kmeans_iters = it;
+		return;
+	}
+	if (k == "ivf_flat_scan") {
+		bool b;
+		if (v == "bound") b = true;
+		else if (v == "exact") b = false;
+		else throw Error("ivf_flat_scan must be 'bound' or 'exact'");
+		ix->bind();
+		// the bound scan's list-order rows are built with the layout
+		if (b && !ix->ivf_flat_bound && ix->ivf) ix->ivf->dirty = true;
+		ix->ivf_flat_bound = b;
+		return;
+	}
+	if (k == "pq_seed") {
+		if (v == "1") ix->pq_seed = true;
+		else if (v == "0") ix->pq_seed = false;
+		else throw Error("pq_seed: 1 or 0");
+		return;
+	}
+	if (k == "pq_scan") {
+		if (v == "fast") ix->pq_fast = true;
+		else if (v == "exact_lut") ix->pq_fast = false;
+		else throw Error("pq_scan must be 'fast' or 'exact_lut'");
+		return;
+	}
+	if (k == "pq_query") {
+		if (v == "fp8") ix->pq_fp8 = true;
+		else if (v == "f32") ix->pq_fp8 = false;
+		else throw Error("pq_query must be 'fp8' or 'f32'");
+		return;
+	}
+	if (k == "ivf_seed") {
+		ix->ivf_seed = std::stoull(v);
+		return;
+	}
+	if (k == "reserve_rows") {
+		ix->bind();
+		ix->reserve(std::stoll(v));
+		return;
+	}
+	throw Error("unknown option '" + k + "'");
+}
+
+extern "C" {
+
 int32_t lance_hip_set_option(void *handle, const char *key, const char *value, char *err_buf, int err_buf_len) {
 	if (!handle) {
 		lhip::write_err(err_buf, err_buf_len, "null handle");
@@ -1345,177 +1541,10 @@ int32_t lance_hip_set_option(void *handle, const char *key, const char *value, c
 			if (k == "index_type") ix->ivf_type_opt = ix->shards[0]->ivf_type_opt;
 			return 0;
 		}
-		if (k == "tie") {  // the final order's tie rule (label_desc reproduces the reference's tie golden)
-			ix->tie_desc = lhip::parse_tie(v);
-			return 0;
-		}
-		if (k == "metric_quirk") {
-			bool on = (v == "1" || v == "true");
-			if (on && ix->metric != lhip::METRIC_L2 && !ix->rowaux_l2) {
-				// build L2 aux for the rows already stored
-				ix->bind();
-				HIPCHK(hipMalloc(&ix->rowaux_l2, (size_t)std::max<int64_t>(ix->cap, 1) * sizeof(float4)));
-				if (ix->n_slots > 0) {
-					lhip::launch_rowaux(ix->X, ix->xbf16, ix->ld, ix->dim, lhip::METRIC_L2, 0, ix->n_slots, ix->rowaux_l2,
-					                    ix->stats.p + 2, ix->stream);
-					// re-apply tombstones
-					std::vector<int64_t> dead;
-					for (int64_t s = 0; s < ix->n_slots; ++s)
-						if (!ix->live[(size_t)s]) dead.push_back(s);
-					if (!dead.empty()) {
-						ix->ws.idx.need(dead.size());
-						HIPCHK(hipMemcpyAsync(ix->ws.idx.p, dead.data(), dead.size() * sizeof(int64_t),
-						                      hipMemcpyHostToDevice, ix->stream));
-						lhip::launch_tombstone(ix->rowaux_l2, ix->ws.idx.p, (int)dead.size(), ix->stream);
-					}
-					HIPCHK(hipStreamSynchronize(ix->stream));
-					ix->refresh_stats();
-				}
-			}
-			ix->metric_quirk = on;
-			return 0;
-		}
-		if (k == "time_kernels") {
-			ix->bind();
-			ix->time_kernels = (v == "1" || v == "true");
-			for (auto &e : ix->ev)
-				if (!e) HIPCHK(hipEventCreate(&e));
-			ix->kt_append_ms = ix->kt_dense_ms = 0.0;
-			ix->kt_append_n = ix->kt_dense_n = 0;
-			ix->kt_ivf_ms = ix->kt_ivf_bytes = ix->kt_ivf_pair_rows = ix->kt_ivf_coarse_ms = 0.0;
-			ix->kt_ivf_n = 0;
-			return 0;
-		}
-		if (k == "storage") {
-			if (v != "f32" && v != "bf16") throw Error("storage must be 'f32' or 'bf16'");
-			ix->bind();
-			const bool was = ix->xbf16;
-			ix->set_storage(v == "bf16");
-			if (was != ix->xbf16) ix->log_storage();
-			return 0;
-		}
-		if (k == "scan_copy") {
-			if (v != "on" && v != "off") throw Error("scan_copy must be 'on' or 'off'");
-			ix->bind();
-			ix->set_scan_copy(v == "on");
-			return 0;
-		}
-		if (k == "scan_i8") {
-			if (v != "on" && v != "off") throw Error("scan_i8 must be 'on' or 'off'");
-			ix->bind();
-			ix->scan_i8 = v == "on";
-			if (!ix->scan_i8) ix->drop_i8();
-			return 0;
-		}
-
-		if (k == "prepare") {
-			// build the derived scan structures now (the int8 scan copy) instead
-			// of on the first search after a change
-			ix->bind();
-			if (ix->i8_usable()) ix->ensure_i8();
-			return 0;
-		}
-		if (k == "pr_first") {  // this handle's first final-mode pool_refine chunk (results exact for any value)
-			const int r = std::stoi(v);
-			if (r != 0 && (r < 8 || r > lhip::pool_refine_max_first()))
-				throw Error("pr_first must be 0 (default) or in [8, " + std::to_string(lhip::pool_refine_max_first()) + "]");
-			ix->pr_first = r;
-			return 0;
-		}
-		if (k == "scan8_variant") {  // this handle's ld = 768 scan8 geometry; release builds: 0 only
-			const int r = std::stoi(v);
-			if (!lhip::scan8_variant_ok(r))
-				throw Error("scan8_variant " + v + " exists only in development (LHIP_ABLATION_BUILD) builds");
-			ix->s8_variant = r;
-			return 0;
-		}
-		if (k == "cand_extra_i8") {
-			const int d = std::stoi(v);
-			if (d != 0 && (d < 8 || d > 256)) throw Error("cand_extra_i8 must be 0 (auto) or in [8, 256]");
-			ix->cand_extra_i8 = d;
-			return 0;
-		}
-		if (k == "cand_extra") {
-			const int d = std::stoi(v);
-			if (d < 8 || d > 256) throw Error("cand_extra must be in [8, 256]");
-			ix->cand_extra = d;
-			return 0;
-		}
-		if (k == "small_exact") {
-			ix->small_exact = (v == "1" || v == "on" || v == "true");
-			return 0;
-		}
-
-		if (k == "retry_pass") {
-			ix->retry_pass = (v == "1" || v == "on" || v == "true");
-			return 0;
-		}
-		if (k == "split_div") {  // progressive threshold of the int8 append pass (0 or 1: one pass)
-			const int d = std::stoi(v);
-			if (d < 0 || d > 64) throw Error("split_div must be in [0, 64]");
-			ix->split_div = d;
-			return 0;
-		}
-		if (k == "sample_div") {
-			const int d = std::stoi(v);
-			if (d < 0) throw Error("sample_div must be >= 1, or 0 (auto)");
-			ix->sample_div = d;
-			return 0;
-		}
-		if (k == "index_type") {
-			if (v == "ivf_pq" || v == "IVF_PQ")
-				ix->ivf_type_opt = lhip::IVF_PQ;
-			else if (v == "ivf_flat" || v == "IVF_FLAT")
-				ix->ivf_type_opt = lhip::IVF_FLAT;
-			else
-				throw Error("index_type must be 'ivf_pq' or 'ivf_flat'");
-			return 0;
-		}
-		if (k == "kmeans_iters") {
-			const int it = std::stoi(v);
-			if (it < 0) throw Error("kmeans_iters must be >= 0");
-			ix->kmeans_iters = it;
-			return 0;
-		}
-		if (k == "ivf_flat_scan") {
-			bool b;
-			if (v == "bound") b = true;
-			else if (v == "exact") b = false;
-			else throw Error("ivf_flat_scan must be 'bound' or 'exact'");
-			ix->bind();
-			// the bound scan's list-order rows are built with the layout
-			if (b && !ix->ivf_flat_bound && ix->ivf) ix->ivf->dirty = true;
-			ix->ivf_flat_bound = b;
-			return 0;
-		}
-		if (k == "pq_seed") {
-			if (v == "1") ix->pq_seed = true;
-			else if (v == "0") ix->pq_seed = false;
-			else throw Error("pq_seed: 1 or 0");
-			return 0;
-		}
-		if (k == "pq_scan") {
-			if (v == "fast") ix->pq_fast = true;
-			else if (v == "exact_lut") ix->pq_fast = false;
-			else throw Error("pq_scan must be 'fast' or 'exact_lut'");
-			return 0;
-		}
-		if (k == "pq_query") {
-			if (v == "fp8") ix->pq_fp8 = true;
-			else if (v == "f32") ix->pq_fp8 = false;
-			else throw Error("pq_query must be 'fp8' or 'f32'");
-			return 0;
-		}
-		if (k == "ivf_seed") {
-			ix->ivf_seed = std::stoull(v);
-			return 0;
-		}
-		if (k == "reserve_rows") {
-			ix->bind();
-			ix->reserve(std::stoll(v));
-			return 0;
-		}
-		throw Error("unknown option '" + k + "'");
+		set_option_store(ix, k, v);
+		// (replayed on each shard if the handle becomes multi-device later: shard_init)
+		if (k != "prepare" && k != "time_kernels") ix->opt_log.emplace_back(k, v);
+		return 0;
 	}
 	API_GUARD("set_option failed: ", -1)
 }
@@ -1604,9 +1633,11 @@ int32_t lance_hip_search_batch_device(void *handle, const float *d_queries, int3
 		if (!d_queries || !d_out_labels || !d_out_distances || !d_out_counts) throw Error("null buffer");
 		std::lock_guard<std::mutex> g(ix->mu);
 		ix->bind();
-		if (ix->sharded()) {  // queries on any device, outputs on the first device of the handle
-			lhip::shard_search(ix, d_queries, pointer_device(d_queries), nq, k, nprobes, refine_factor, nullptr,
-			                   d_out_labels, d_out_distances, d_out_counts, false);
+		if (ix->sharded()) {  // queries and outputs on any device (the merge runs on the handle's first device)
+			const int64_t t = lhip::shard_submit(ix, d_queries, pointer_device(d_queries), nq, k, nprobes,
+			                                     refine_factor, d_out_labels, d_out_distances, d_out_counts, false,
+			                                     pointer_device(d_out_labels));
+			ix->wait_ticket(t);
 			return nq;
 		}
 		if (ix->n_live == 0) {
@@ -1638,10 +1669,15 @@ int64_t lance_hip_search_batch_device_async(void *handle, const float *d_queries
 		std::lock_guard<std::mutex> g(ix->mu);
 		ix->bind_nodrain();
 		if (nq == 0) return ix->next_ticket++;
-		if (ix->sharded()) {  // (every shard's pass runs concurrently inside the call; complete on return)
-			lhip::shard_search(ix, d_queries, pointer_device(d_queries), nq, k, nprobes, refine_factor, nullptr,
-			                   d_out_labels, d_out_distances, d_out_counts, false);
-			return ix->next_ticket++;
+		if (ix->sharded()) {
+			// every shard's pass enqueued; certificates, peer copies and the merge at
+			// the wait (two searches in flight: the shards scan the next batch
+			// meanwhile).  Host queries complete here (their staging is reused).
+			const int qdev = pointer_device(d_queries);
+			const int64_t t = lhip::shard_submit(ix, d_queries, qdev, nq, k, nprobes, refine_factor, d_out_labels,
+			                                     d_out_distances, d_out_counts, false, pointer_device(d_out_labels));
+			if (qdev < 0) ix->wait_ticket(t);
+			return t;
 		}
 		if (ix->n_live == 0) {
 			ix->drain();

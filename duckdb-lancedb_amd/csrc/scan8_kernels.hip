@@ -39,6 +39,7 @@
 #include "knn_kernels.h"
 
 #include <algorithm>
+#include <atomic>
 #include <stdexcept>
 
 #include "device_common.h"
@@ -97,6 +98,16 @@ __device__ __forceinline__ int s8_query_part(float4 qp, float4 ts, float W) {
 // row-dependent terms), (orderedkey(score), slot), goes to the workgroup's
 // segment (dead rows skipped): 8 entries per tile and query from which
 // pool_refine's tau mode refines the k + 8 smallest exactly.
+// Pair coupling (couple > 0, speed only — results never depend on it): the two
+// workgroups of a pair read the same rows, the second from L2 only while the
+// first's copy is still there; left alone they drift apart (at 10M rows the
+// partner's reads miss L2: FETCH 1.22x the algorithmic bytes).  Each workgroup
+// publishes the highest unit it has claimed (prog[b], tagged with the launch's
+// epoch in the high word, atomicMax at agent scope) and a wave does not start a
+// unit more than `couple` units ahead of its partner's; the wait is bounded
+// (S8_COUPLE_SPINS sleeps, then the wave stops waiting), so a partner that is
+// not resident (another kernel on its CU) costs time, never progress.
+constexpr int S8_COUPLE_SPINS = 2048;
 template <int KS, int D, int RB, int ABL = 0, int TM = 0>
 __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *__restrict__ Xq, const float4 *__restrict__ aux8,
                                                       const float4 *__restrict__ tstat, int ld,
@@ -104,7 +115,9 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
                                                       int nq, int n_tiles, int tile0, int seg_base,
                                                       const float *__restrict__ tau,
                                                       uint2 *__restrict__ seg_pool, int *__restrict__ seg_cnt,
-                                                      int seg_cap, int list_cap, int tstride) {
+                                                      int seg_cap, int list_cap, int tstride,
+                                                      unsigned long long *__restrict__ prog, unsigned epoch,
+                                                      int couple) {
 	static_assert(KS % D == 0 && KS % 2 == 0, "ring slot and fragment buffer of a k-step must be static");
 	constexpr int NW = 16 / RB, T8 = 64 * NW;  // waves: each owns 16 RB rows of every tile
 	constexpr int WR = 16 * RB;                // rows per wave and tile
@@ -277,8 +290,31 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 		// the query terms of queries lane and lane + 64 (this lane's query parts,
 		// handed to the accumulator lanes of column 16 u + lr by ds_bpermute)
 		const float4 qp0 = QP[lane], qp1 = QP[lane + 64];
+		// pair coupling: only for pairs on one XCD (b, b ^ 8: the (nb & 15) == 0 layout),
+		// and in the ld <= 768 geometries (KS <= 12): the deeper register rings of
+		// ld 896 / 1024 have no room for its state (a 12-B spill)
+		const bool cpl = KS <= 12 && couple > 0 && prog && halves && (nb & 15) == 0;
+		const uint64_t etag = (uint64_t)epoch << 32;
+		int pseen = -1, spins = cpl ? S8_COUPLE_SPINS : 0;  // partner's unit last seen; sleeps left
+		auto publish = [&](int u) {
+			if (cpl && lane == 0) __hip_atomic_fetch_max(prog + b_id, etag | (uint32_t)u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		};
+		auto await_partner = [&](int u) {  // before this wave's loads of unit u
+			while (spins > 0 && u - couple > pseen) {
+				uint64_t v = 0;
+				if (lane == 0) v = __hip_atomic_load(prog + (b_id ^ 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				const int pv = (v >> 32) == (uint64_t)epoch ? (int)(uint32_t)v : -1;
+				pseen = __builtin_amdgcn_readfirstlane(pv);
+				if (u - couple <= pseen) break;
+				__builtin_amdgcn_s_sleep(8);
+				--spins;
+			}
+		};
 		int unit = w;                                        // this block's unit
+		publish(unit);
+		await_partner(unit);
 		int unext = __builtin_amdgcn_readfirstlane(claim()); // the next one (>= NU: none)
+		publish(unext);
 		float an;
 		float4 tn;
 		aload(unit, an, tn);
@@ -310,6 +346,10 @@ __global__ __launch_bounds__(64 * (16 / RB), 1) void scan8_kernel(const int8_t *
 		for (;;) {
 			const int unn_raw = claim();        // the unit after next (read at this block's end)
 			const int ux = unext < NU ? unext : unit;  // past the end: this unit's rows again (unused)
+			if (cpl) {
+				publish(__builtin_amdgcn_readfirstlane(unn_raw));
+				if (unext < NU) await_partner(unext);  // (its rows stream during this block)
+			}
 			const float al = an;
 			const float4 ts = tn;
 			aload(ux, an, tn);
@@ -543,6 +583,9 @@ static int s8_list_cap(int ld, int nw) {
 	return std::min(1024, room / (nw * 9) / 64 * 64);
 }
 
+// progress words a launch's pair coupling needs (StoreView::s8_prog)
+int scan8_prog_words() { return 2048; }
+
 template <int KS, int D, int RB, int ABL = 0, int TM = 0>
 static void s8_launch(const StoreView &s, const QueryView &q, const float *tau, uint2 *seg_pool, int *seg_cnt,
                       int seg_cap, int64_t t0, int64_t n_tiles, int seg_base, hipStream_t st, int tstride = 1) {
@@ -551,9 +594,15 @@ static void s8_launch(const StoreView &s, const QueryView &q, const float *tau, 
 #endif
 	const dim3 grid((unsigned)s8_groups(n_tiles), (unsigned)(q.nq_pad / SCAN_BQ));
 	constexpr int NW = 16 / RB;
+	// a launch's coupling words are tagged with a process-unique epoch (launches
+	// sharing the buffer run in order on one stream; a stale word never matches)
+	static std::atomic<unsigned> epochs{1u};
+	const bool cpl = s.s8_couple > 0 && s.s8_prog && grid.y == 1 && (int)grid.x <= scan8_prog_words();
+	const unsigned ep = cpl ? epochs.fetch_add(1u) : 0u;
 	scan8_kernel<KS, D, RB, ABL, TM><<<grid, dim3(64 * NW), 0, st>>>(
 	    static_cast<const int8_t *>(s.Xscan), s.scan_aux, s.tstat, s.ld, reinterpret_cast<const int8_t *>(q.Qb), q.qaux,
-	    q.nq, (int)n_tiles, (int)t0, seg_base, tau, seg_pool, seg_cnt, seg_cap, s8_list_cap(s.ld, NW), tstride);
+	    q.nq, (int)n_tiles, (int)t0, seg_base, tau, seg_pool, seg_cnt, seg_cap, s8_list_cap(s.ld, NW), tstride,
+	    cpl ? s.s8_prog : nullptr, ep, cpl ? s.s8_couple : 0);
 }
 
 int scan8_tilemin_cap(int64_t n_tiles) {

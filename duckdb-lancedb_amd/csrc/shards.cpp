@@ -18,7 +18,9 @@
 // same lists a single-device search returns.
 #include "index.h"
 #include "ivf.h"
+#include "../../include/lancedb_hip.h"
 
+#include <cmath>
 #include <cstdlib>
 
 namespace lhip {
@@ -100,8 +102,29 @@ void shard_init(Index *ix, const std::vector<int> &devs) {
 					(void)hipGetLastError();
 				}
 			}
-	ix->device = devs[0];
+	// the handle's own stream (the merge stream) and stats on the first device
+	if (ix->device != devs[0]) {
+		HIPCHK(hipSetDevice(ix->device));
+		if (ix->stream) {
+			HIPCHK(hipStreamSynchronize(ix->stream));
+			HIPCHK(hipStreamDestroy(ix->stream));
+			ix->stream = nullptr;
+		}
+		ix->stats.release();
+		ix->init_device(devs[0]);
+	}
 	HIPCHK(hipSetDevice(ix->device));
+	// options set before `devices`: every shard takes them (reserve_rows split)
+	for (const auto &kv : ix->opt_log) {
+		std::string v = kv.second;
+		if (kv.first == "reserve_rows")
+			v = std::to_string((std::stoll(v) + (int64_t)devs.size() - 1) / (int64_t)devs.size());
+		char err[512];
+		for (auto &sh : ix->shards)
+			if (lance_hip_set_option(sh.get(), kv.first.c_str(), v.c_str(), err, (int)sizeof(err)) != 0)
+				throw Error(std::string("devices: replaying option ") + kv.first + ": " + err);
+		if (kv.first == "index_type") ix->ivf_type_opt = ix->shards[0]->ivf_type_opt;
+	}
 }
 
 Index *shard_for_add(Index *ix) {
@@ -153,93 +176,141 @@ std::vector<int64_t> shard_remove(Index *ix, const int64_t *labels, int64_t n) {
 	return done;
 }
 
-// Sharded search.  Q: nq x dim f32 on the host (qdev < 0) or on device qdev;
-// outputs on the host (out_host) or on the first shard's device.
-void shard_search(Index *ix, const float *Q, int qdev, int nq, int k, int nprobes, int refine, const char *pred,
-                  int64_t *L, float *D, int *C, bool out_host) {
+// Sharded search, asynchronous: shard_submit enqueues every shard's pass (its
+// own pass streams; nothing waits), shard_finish_oldest completes the oldest
+// submitted search — per shard the certificate check / reruns / fallback
+// (host, Index::wait_ticket), the B*k partial lists copied to the first device
+// on the shard's stream and an event the merge stream waits on (no host wait
+// per shard), then ONE merge on the first device.  Two searches may be in
+// flight (per-slot query / list buffers on every shard): the shards scan batch
+// i+1 while batch i's lists are checked, copied and merged.
+// Q: nq x dim f32 on the host (qdev < 0) or on device qdev; outputs on the
+// host (out_host), on device odev, or (odev < 0, not out_host) anywhere the
+// first device can write through hipMemcpy.
+int64_t shard_submit(Index *ix, const float *Q, int qdev, int nq, int k, int nprobes, int refine, int64_t *L,
+                     float *D, int *C, bool out_host, int odev) {
+	while (ix->spending.size() >= 2) shard_finish_oldest(ix);
 	const int S = (int)ix->shards.size();
 	const int dim = ix->dim;
-	std::vector<std::unique_ptr<FilterScope>> fs;
-	for (auto &sh : ix->shards) fs.emplace_back(new FilterScope(sh.get(), pred));
-	Index *p0 = ix->shards[0].get();
+	int slot = 0;
+	for (const auto &p : ix->spending)
+		if (p.slot == slot) slot = 1;
+	ShardPending p;
+	p.ticket = ix->next_ticket++;
+	p.slot = slot;
+	p.nq = nq;
+	p.k = k;
+	p.odev = odev;
+	p.out_host = out_host;
+	p.L = L;
+	p.D = D;
+	p.C = C;
+	p.st.assign((size_t)S, 0);
+	p.empty.assign((size_t)S, 0);
 	const size_t qb = (size_t)nq * dim * sizeof(float), lb = (size_t)nq * k * sizeof(int64_t);
 	const size_t db = (size_t)nq * k * sizeof(float), cb = (size_t)nq * sizeof(int);
-	HIPCHK(hipSetDevice(p0->device));
-	ix->m_pl.need((size_t)S * nq * k);
-	ix->m_pd.need((size_t)S * nq * k);
-	ix->m_pc.need((size_t)S * nq);
-	std::vector<int64_t> ticket((size_t)S, 0);
-	std::vector<char> empty((size_t)S, 0);
-	// 1) every shard's search enqueued (asynchronous passes) before any wait
 	for (int s = 0; s < S; ++s) {
 		Index *t = ix->shards[(size_t)s].get();
-		t->bind();
+		t->bind_nodrain();
 		if (t->live_rows() == 0) {
-			empty[(size_t)s] = 1;
+			p.empty[(size_t)s] = 1;
 			continue;
 		}
-		t->ws.Qin.need((size_t)nq * dim);
-		t->ws.out_blk.need(lb + db + cb);
+		t->sh_q[slot].need((size_t)nq * dim);
+		t->sh_out[slot].need(lb + db + cb);
 		if (qdev < 0) {
+			// (host queries come from the synchronous wrappers only: the staging
+			// buffer is not reused before this search completes)
 			uint8_t *io = t->ws.need_host_io(qb);
 			memcpy(io, Q, qb);
-			HIPCHK(hipMemcpyAsync(t->ws.Qin.p, io, qb, hipMemcpyHostToDevice, t->stream));
+			HIPCHK(hipMemcpyAsync(t->sh_q[slot].p, io, qb, hipMemcpyHostToDevice, t->stream));
 		} else {
-			HIPCHK(hipMemcpyPeerAsync(t->ws.Qin.p, t->device, Q, qdev, qb, t->stream));
+			HIPCHK(hipMemcpyPeerAsync(t->sh_q[slot].p, t->device, Q, qdev, qb, t->stream));
 		}
-		int64_t *dL = reinterpret_cast<int64_t *>(t->ws.out_blk.p);
-		float *dD = reinterpret_cast<float *>(t->ws.out_blk.p + lb);
-		int *dC = reinterpret_cast<int *>(t->ws.out_blk.p + lb + db);
-		ticket[(size_t)s] = t->search_async(t->ws.Qin.p, nq, k, nprobes, refine, dL, dD, dC);
+		uint8_t *o = t->sh_out[slot].p;
+		p.st[(size_t)s] = t->search_async(t->sh_q[slot].p, nq, k, nprobes, refine, reinterpret_cast<int64_t *>(o),
+		                                  reinterpret_cast<float *>(o + lb), reinterpret_cast<int *>(o + lb + db));
 	}
-	// 2) completions (certificates, reruns, fallbacks) and the partial lists to
-	//    the first device
+	ix->spending.push_back(std::move(p));
+	return ix->spending.back().ticket;
+}
+
+void shard_finish_oldest(Index *ix) {
+	ShardPending p = std::move(ix->spending.front());
+	ix->spending.pop_front();
+	const int S = (int)ix->shards.size(), nq = p.nq, k = p.k, sl = p.slot;
+	const size_t lb = (size_t)nq * k * sizeof(int64_t), db = (size_t)nq * k * sizeof(float), cb = (size_t)nq * sizeof(int);
+	HIPCHK(hipSetDevice(ix->device));
+	ix->m_pl[sl].need((size_t)S * nq * k);
+	ix->m_pd[sl].need((size_t)S * nq * k);
+	ix->m_pc[sl].need((size_t)S * nq);
+	const hipStream_t ms = ix->stream;  // the merge stream (first device)
+	for (auto &v : ix->last_stats) v = 0;
 	for (int s = 0; s < S; ++s) {
 		Index *t = ix->shards[(size_t)s].get();
 		const size_t o = (size_t)s * nq * k;
-		if (empty[(size_t)s]) {
-			HIPCHK(hipSetDevice(p0->device));
-			HIPCHK(hipMemsetAsync(ix->m_pc.p + (size_t)s * nq, 0, cb, p0->stream));
+		if (p.empty[(size_t)s]) {
+			HIPCHK(hipSetDevice(ix->device));
+			HIPCHK(hipMemsetAsync(ix->m_pc[sl].p + (size_t)s * nq, 0, cb, ms));
 			continue;
 		}
 		t->bind_nodrain();
-		t->wait_ticket(ticket[(size_t)s]);
-		HIPCHK(hipMemcpyPeerAsync(ix->m_pl.p + o, p0->device, t->ws.out_blk.p, t->device, lb, t->stream));
-		HIPCHK(hipMemcpyPeerAsync(ix->m_pd.p + o, p0->device, t->ws.out_blk.p + lb, t->device, db, t->stream));
-		HIPCHK(hipMemcpyPeerAsync(ix->m_pc.p + (size_t)s * nq, p0->device, t->ws.out_blk.p + lb + db, t->device, cb,
+		t->wait_ticket(p.st[(size_t)s]);  // certificates, reruns, exact fallback of this shard's pass
+		// statistics of the search: summed over the shards that searched (max pool: the largest)
+		for (int i : {0, 1, 4, 5}) ix->last_stats[i] += t->last_stats[i];
+		ix->last_stats[2] = std::max(ix->last_stats[2], t->last_stats[2]);
+		ix->last_stats[3] = std::max(ix->last_stats[3], t->last_stats[3]);
+		const uint8_t *src = t->sh_out[sl].p;
+		HIPCHK(hipMemcpyPeerAsync(ix->m_pl[sl].p + o, ix->device, src, t->device, lb, t->stream));
+		HIPCHK(hipMemcpyPeerAsync(ix->m_pd[sl].p + o, ix->device, src + lb, t->device, db, t->stream));
+		HIPCHK(hipMemcpyPeerAsync(ix->m_pc[sl].p + (size_t)s * nq, ix->device, src + lb + db, t->device, cb,
 		                          t->stream));
-		HIPCHK(hipStreamSynchronize(t->stream));
+		if (!t->sh_ev[sl]) HIPCHK(hipEventCreateWithFlags(&t->sh_ev[sl], hipEventDisableTiming));
+		HIPCHK(hipEventRecord(t->sh_ev[sl], t->stream));
+		HIPCHK(hipSetDevice(ix->device));
+		HIPCHK(hipStreamWaitEvent(ms, t->sh_ev[sl], 0));
 	}
-	// 3) merge on the first device
-	HIPCHK(hipSetDevice(p0->device));
-	int64_t *oL = L;
-	float *oD = D;
-	int *oC = C;
-	if (out_host) {
-		ix->m_out.need(lb + db + cb);
-		oL = reinterpret_cast<int64_t *>(ix->m_out.p);
-		oD = reinterpret_cast<float *>(ix->m_out.p + lb);
-		oC = reinterpret_cast<int *>(ix->m_out.p + lb + db);
+	// merge on the first device: straight into the outputs when they live there,
+	// else into m_out and one copy to wherever they are (host, another device)
+	HIPCHK(hipSetDevice(ix->device));
+	const bool direct = !p.out_host && p.odev == ix->device;
+	int64_t *oL = p.L;
+	float *oD = p.D;
+	int *oC = p.C;
+	if (!direct) {
+		ix->m_out[sl].need(lb + db + cb);
+		oL = reinterpret_cast<int64_t *>(ix->m_out[sl].p);
+		oD = reinterpret_cast<float *>(ix->m_out[sl].p + lb);
+		oC = reinterpret_cast<int *>(ix->m_out[sl].p + lb + db);
 	}
-	launch_merge_topk(S, nq, k, ix->m_pl.p, ix->m_pd.p, ix->m_pc.p, oL, oD, oC, p0->stream, ix->tie_desc);
+	launch_merge_topk(S, nq, k, ix->m_pl[sl].p, ix->m_pd[sl].p, ix->m_pc[sl].p, oL, oD, oC, ms, ix->tie_desc);
 	HIPCHK(hipGetLastError());
-	if (out_host) {
-		uint8_t *io = p0->ws.need_host_io(lb + db + cb);
-		HIPCHK(hipMemcpyAsync(io, ix->m_out.p, lb + db + cb, hipMemcpyDeviceToHost, p0->stream));
-		spin_sync(p0->stream);
-		memcpy(L, io, lb);
-		memcpy(D, io + lb, db);
-		memcpy(C, io + lb + db, cb);
+	if (p.out_host) {
+		uint8_t *io = ix->shards[0]->ws.need_host_io(lb + db + cb);
+		HIPCHK(hipMemcpyAsync(io, ix->m_out[sl].p, lb + db + cb, hipMemcpyDeviceToHost, ms));
+		spin_sync(ms);
+		memcpy(p.L, io, lb);
+		memcpy(p.D, io + lb, db);
+		memcpy(p.C, io + lb + db, cb);
 	} else {
-		spin_sync(p0->stream);
+		if (!direct) {
+			HIPCHK(hipMemcpyAsync(p.L, oL, lb, hipMemcpyDefault, ms));
+			HIPCHK(hipMemcpyAsync(p.D, oD, db, hipMemcpyDefault, ms));
+			HIPCHK(hipMemcpyAsync(p.C, oC, cb, hipMemcpyDefault, ms));
+		}
+		spin_sync(ms);
 	}
-	// statistics of the search: summed over the shards (max pool: the largest)
-	for (auto &v : ix->last_stats) v = 0;
-	for (auto &sh : ix->shards) {
-		for (int i : {0, 1, 4, 5}) ix->last_stats[i] += sh->last_stats[i];
-		ix->last_stats[2] = std::max(ix->last_stats[2], sh->last_stats[2]);
-		ix->last_stats[3] = std::max(ix->last_stats[3], sh->last_stats[3]);
-	}
+}
+
+// Synchronous sharded search (the host-buffer entry points, predicates): the
+// predicate's mask per shard (FilterScope) for the duration of the search.
+void shard_search(Index *ix, const float *Q, int qdev, int nq, int k, int nprobes, int refine, const char *pred,
+                  int64_t *L, float *D, int *C, bool out_host) {
+	ix->drain();
+	std::vector<std::unique_ptr<FilterScope>> fs;
+	for (auto &sh : ix->shards) fs.emplace_back(new FilterScope(sh.get(), pred));
+	const int64_t t = shard_submit(ix, Q, qdev, nq, k, nprobes, refine, L, D, C, out_host, out_host ? -1 : ix->device);
+	ix->wait_ticket(t);
 }
 
 // this handle's live / slot counts from its shards (after compaction, replay)
@@ -298,25 +369,79 @@ void shard_compact(Index *ix) {
 	shard_counts(ix);
 }
 
-// IVF: trained on the shard with the most live rows (the shards hold whole
-// ingest batches, so that is a sample of the table), installed on every other
-// shard, each indexing its own rows with the same centroids / codebook (as the
-// multi-process path does, lance_hip_ivf_set_model)
+// IVF: one model for the whole table, installed on every shard (each indexes
+// its own rows with the same centroids / codebook, as the multi-process path
+// does, lance_hip_ivf_set_model).  nlist / m defaults and the size checks come
+// from the TABLE's live count, so a handle gets the model a single store of the
+// same rows would (ivf_build's rules: sqrt(live) lists, dim / 16 sub-vectors).
+// Training runs on the shard with the most live rows when it holds the sample
+// ivf_build would draw (min(live, 256 nlist) rows: the shards hold whole
+// ingest batches, so that is a sample of the table); otherwise on a temporary
+// store on the first device holding that many live rows drawn evenly from
+// every shard.
 void shard_create_index(Index *ix, int type, int num_partitions, int num_sub_vectors) {
+	const int64_t total = shard_live(ix);
+	if (total <= 0) throw Error("cannot build an index on an empty table");
+	const int dim = ix->dim;
+	const int nlist = num_partitions > 0 ? num_partitions : std::max(1, (int)std::sqrt((double)total));
+	const int m = num_sub_vectors > 0 ? num_sub_vectors : (dim % 16 == 0 ? dim / 16 : dim % 8 == 0 ? dim / 8 : 1);
+	if (nlist > total)
+		throw Error("KMeans: cannot train " + std::to_string(nlist) + " centroids with " + std::to_string(total) +
+		            " vectors");
+	if (type == IVF_PQ && total < PQ_K)
+		throw Error("PQ training needs at least 256 rows, the table has " + std::to_string(total));
 	Index *tr = nullptr;
 	for (auto &s : ix->shards)
 		if (!tr || s->n_live > tr->n_live) tr = s.get();
+	const int64_t want = std::min<int64_t>(total, (int64_t)nlist * 256);
+	std::unique_ptr<Index> tmp;
+	if (tr->n_live < want) {
+		tmp = std::make_unique<Index>();
+		tmp->table = "ivf_train";
+		tmp->metric_name = ix->metric_name;
+		tmp->metric = ix->metric;
+		tmp->dim = dim;
+		tmp->ld = ix->ld;
+		tmp->init_device(ix->device);
+		tmp->reserve(want + (int64_t)ix->shards.size());
+		for (auto &sp : ix->shards) {
+			Index *s = sp.get();
+			if (s->n_live == 0) continue;
+			// this shard's share, every (n_live / quota)-th live slot
+			const int64_t quota = std::min<int64_t>(s->n_live, (want * s->n_live + total - 1) / total);
+			std::vector<float> rows((size_t)quota * dim), chunk;
+			int64_t got = 0, c = 0;
+			constexpr int64_t CH = 65536;
+			s->bind();
+			for (int64_t s0 = 0; s0 < s->n_slots && got < quota; s0 += CH) {
+				const int64_t n = std::min<int64_t>(CH, s->n_slots - s0);
+				chunk.resize((size_t)n * dim);
+				s->read_rows(s0, n, chunk.data());
+				for (int64_t i = 0; i < n && got < quota; ++i) {
+					if (!s->live[(size_t)(s0 + i)]) continue;
+					if ((c * quota) / s->n_live != ((c + 1) * quota) / s->n_live)
+						memcpy(rows.data() + (size_t)got++ * dim, chunk.data() + (size_t)i * dim, (size_t)dim * sizeof(float));
+					++c;
+				}
+			}
+			tmp->bind();
+			if (got > 0) tmp->add_host(rows.data(), got);
+		}
+		tr = tmp.get();
+	}
 	tr->bind();
 	tr->ivf_type_opt = type;
-	ivf_build(tr, type, num_partitions, num_sub_vectors);
-	const int nl = tr->ivf->nlist, m = tr->ivf->m;
-	std::vector<float> C((size_t)nl * ix->dim), cb;
-	if (type == IVF_PQ) cb.resize((size_t)m * PQ_K * (ix->dim / m));
+	tr->kmeans_iters = ix->shards[0]->kmeans_iters;
+	tr->ivf_seed = ix->shards[0]->ivf_seed;
+	ivf_build(tr, type, nlist, m);
+	const int nl = tr->ivf->nlist, mm = tr->ivf->m;
+	std::vector<float> C((size_t)nl * dim), cb;
+	if (type == IVF_PQ) cb.resize((size_t)mm * PQ_K * (dim / mm));
 	ivf_export_model(tr, C.data(), cb.empty() ? nullptr : cb.data());
 	for (auto &s : ix->shards) {
 		if (s.get() == tr) continue;
 		s->bind();
-		ivf_set_model(s.get(), type, nl, m, C.data(), cb.empty() ? nullptr : cb.data());
+		ivf_set_model(s.get(), type, nl, mm, C.data(), cb.empty() ? nullptr : cb.data());
 	}
 	ix->log_model(tr);
 }

@@ -27,15 +27,29 @@ def _sharded(hip, d, metric="l2", path="", devices="0,0", table="t"):
     return h
 
 
+# "0,0": both shards on device 0 (every box); "0,1": two distinct devices — the
+# peer copies really cross xGMI and the merge reads lists of another GPU (runs
+# wherever two devices are visible; skipped on a one-GPU box)
+DEVLISTS = ["0,0", "0,1"]
+
+
+def _need(hip, devices):
+    want = max(int(x) for x in devices.split(",")) + 1
+    if hip.device_count() < want:
+        pytest.skip(f"needs {want} HIP devices (box has {hip.device_count()})")
+
+
+@pytest.mark.parametrize("devices", DEVLISTS)
 @pytest.mark.parametrize("metric", ["l2", "cosine"])
-def test_two_shards_d768_match_oracle(hip, metric):
+def test_two_shards_d768_match_oracle(hip, metric, devices):
     # 2 x ~75k rows x 768 in DuckDB's 2048-row chunks (every shard on the
     # threshold path: sample pass, int8 scan8 append pass, pool_refine)
+    _need(hip, devices)
     rng = np.random.default_rng(71)
     n, d, k = 150_000, 768, 10
     X = rng.standard_normal((n, d), dtype=np.float32)
     Q = rng.standard_normal((256, d), dtype=np.float32)
-    h = _sharded(hip, d, metric)
+    h = _sharded(hip, d, metric, devices=devices)
     try:
         for lo in range(0, n, 2048):
             hi = min(n, lo + 2048)
@@ -94,7 +108,7 @@ def test_device_api_and_compaction_on_two_shards(hip):
         Qd = torch.from_numpy(Q).cuda()
         got = hip_device_search(L, h, d)(Qd, k)
         assert_same(*(x.cpu().numpy() for x in got), el, ed, ec)
-        pipe = AsyncPipeline(L, h, d)  # (a multi-device handle completes inside the submit)
+        pipe = AsyncPipeline(L, h, d)  # (two sharded searches in flight; merged at the wait)
         t = pipe.submit(Qd, k)
         assert_same(*(x.cpu().numpy() for x in pipe.wait(t)), el, ed, ec)
         hip.LanceDetachedCompact(h)
@@ -199,3 +213,93 @@ def test_devices_option_errors(hip):
             hip.LanceHipSetOption(h, "devices", "0,0")
     finally:
         hip.LanceFreeDetached(h)
+
+
+@pytest.mark.parametrize("devices", DEVLISTS)
+def test_async_sharded_searches_in_flight(hip, devices):
+    """lance_hip_search_batch_device_async on a multi-device handle keeps two
+    searches in flight (every shard's pass enqueued at the submit; certificates,
+    peer copies and the merge at the wait): three batches submitted back to back
+    (the third completes the first), each equal to the oracle and to the
+    synchronous call; statistics count only the shards that searched."""
+    import torch
+    from lance_hip.sharded import AsyncPipeline
+
+    _need(hip, devices)
+    L = hip.lib()
+    rng = np.random.default_rng(76)
+    n, d, k = 160_000, 256, 10
+    X = rng.standard_normal((n, d), dtype=np.float32)
+    Qs = [rng.standard_normal((nq, d), dtype=np.float32) for nq in (256, 100, 256)]
+    h = _sharded(hip, d, devices=devices)
+    try:
+        for lo in range(0, n, 40_000):
+            hip.LanceDetachedAddBatch(h, X[lo:lo + 40_000], 40_000, d)
+        exp = [c_oracle.flat_search_batch(X, q, k, "l2", acc64=True, nthreads=16) for q in Qs]
+        pipe = AsyncPipeline(L, h, d)
+        Qd = [torch.from_numpy(q).cuda() for q in Qs]
+        t = [pipe.submit(q, k) for q in Qd[:2]]
+        t.append(pipe.submit(Qd[2], k))  # (a third submit completes the oldest first)
+        out = {}
+        for ti in t:
+            r = pipe.wait(ti)
+            out[ti] = tuple(x.cpu().numpy().copy() for x in r)
+        for ti, e in zip(t, exp):
+            assert_same(*out[ti], *e)
+        st = hip.LanceHipLastSearchStats(h)
+        assert st["fallback_queries"] == 0 and st["append_launches"] == 2, st
+        sync = hip.LanceDetachedSearchBatch(h, Qs[0], k)
+        np.testing.assert_array_equal(sync[0], out[t[0]][0])
+    finally:
+        hip.LanceFreeDetached(h)
+
+
+def test_options_before_devices_reach_every_shard(hip):
+    """Options set on a handle before `devices` are replayed on each shard (the
+    round-5 shard_init copied only the table's own settings): here the tie rule
+    and the int8 scan switch."""
+    rng = np.random.default_rng(77)
+    n, d, k = 100_000, 32, 10
+    X = np.ones((n, d), np.float32)  # every row ties: the tie rule alone orders them
+    h = hip.LanceCreateDetached("", d, "l2", "t")
+    try:
+        hip.LanceHipSetOption(h, "tie", "label_asc")
+        hip.LanceHipSetOption(h, "scan_i8", "off")
+        hip.LanceHipSetOption(h, "devices", "0,0")
+        for lo in range(0, n, 25_000):
+            hip.LanceDetachedAddBatch(h, X[lo:lo + 25_000], 25_000, d)
+        gl, gd, gc = hip.LanceDetachedSearchBatch(h, np.ones((2, d), np.float32), k)
+        assert list(gl[0]) == list(range(k))
+        kt = hip.LanceHipKernelTimes(h)
+        assert kt["scan_elem_bytes"] != 1  # scan_i8 off on the shards: no int8 scan
+    finally:
+        hip.LanceFreeDetached(h)
+
+
+@pytest.mark.parametrize("index_type", ["ivf_flat", "ivf_pq"])
+def test_ivf_defaults_from_the_whole_table(hip, index_type):
+    """create_index on a multi-device handle resolves nlist / m from the table's
+    live count (the model a single store of the same rows gets), and a table one
+    store can index is indexable on two shards even when no single shard could
+    train it alone (IVF_PQ needs 256 rows: 2 x 150 here)."""
+    rng = np.random.default_rng(78)
+    d = 64
+    for n, parts in ((40_000, 0), (300, 4)):
+        X = rng.standard_normal((n, d)).astype(np.float32)
+        h1 = hip.LanceCreateDetached("", d, "l2", "one")
+        h2 = _sharded(hip, d)
+        try:
+            for h in (h1, h2):
+                hip.LanceHipSetOption(h, "index_type", index_type)
+                for lo in range(0, n, 2048 if n > 2048 else 150):
+                    hi = min(n, lo + (2048 if n > 2048 else 150))
+                    hip.LanceDetachedAddBatch(h, X[lo:hi], hi - lo, d)
+                hip.LanceDetachedCreateIndex(h, parts, 0)
+            i1, i2 = hip.LanceHipIvfInfo(h1), hip.LanceHipIvfInfo(h2)
+            assert i2["type"] == index_type and i2["n_indexed"] == n, i2
+            assert (i1["nlist"], i1["m"]) == (i2["nlist"], i2["m"]), (i1, i2)
+            gl, gd, gc = hip.LanceDetachedSearchBatch(h2, X[:8], 5, nprobes=i2["nlist"], refine_factor=50)
+            assert list(gl[:, 0]) == list(range(8))  # each row finds itself
+        finally:
+            hip.LanceFreeDetached(h1)
+            hip.LanceFreeDetached(h2)

@@ -419,3 +419,29 @@ def test_async_rerun_and_fallback_with_next_pass_in_flight(hip):
         assert_same(*oC, *exp[2])
     finally:
         hip.LanceFreeDetached(h)
+
+
+@pytest.mark.parametrize("couple", ["1", "8", "64"])
+def test_scan8_pair_coupling_is_exact(hip, tmp_path, couple):
+    # option s8_couple (speed only): the workgroups of a pair wait for each
+    # other's progress; results must not change.  300k rows x 256 queries: 256
+    # workgroups in pairs (b, b ^ 8), two append launches (split_div) and the
+    # tilemin sample pass, each with its own coupling epoch
+    rng = np.random.default_rng(7070)
+    n, d = 300_000, 768
+    X = rng.standard_normal((n, d), dtype=np.float32)
+    Q = rng.standard_normal((256, d), dtype=np.float32)
+    h = _mk(hip, tmp_path, d, "l2")
+    try:
+        hip.LanceDetachedAddBatch(h, X, n, d)
+        hip.LanceHipSetOption(h, "s8_couple", couple)
+        hip.LanceHipSetOption(h, "split_div", "4")
+        gl, gd, gc = hip.LanceDetachedSearchBatch(h, Q, 10)
+        assert _ran_scan8(hip, h)
+        el, ed, ec = c_oracle.flat_search_batch(X, Q, 10, "l2", acc64=True, nthreads=16)
+        assert_same(gl, gd, gc, el, ed, ec)
+        for _ in range(3):  # repeated launches: fresh epochs over the same progress words
+            gl2, _, _ = hip.LanceDetachedSearchBatch(h, Q, 10)
+            np.testing.assert_array_equal(gl2, gl)
+    finally:
+        hip.LanceFreeDetached(h)
