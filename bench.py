@@ -892,7 +892,9 @@ def main():
             mfma_peak = MFMA_BF16_PEAK_TFS * (2 if esz == 1 else 1)
             ach = bytes_launch / (avg_ms * 1e-3) / 1e9
             kstr = f"{kt['scan_kernel']}<{ {'l2': 'L2', 'dot': 'DOT', 'cosine': 'COSINE'}[a.metric]},append,{xname}>"
-            traffic = measured_traffic(N // world, D, BG, esz, kstr)
+            # (per store: a rank's shard, or with --inproc one of the handle's device stores)
+            n_stores = world * (len(inproc_devs.split(",")) if inproc_devs else 1)
+            traffic = measured_traffic(N // n_stores, D, BG, esz, kstr)
             mfma_tfs = 2.0 * kt["scan_rows"] * D * BG / (avg_ms * 1e-3) / 1e12
             kname = {"l2": "L2", "dot": "DOT", "cosine": "COSINE"}[a.metric]
             # the bounding roof: HBM time of the bytes vs dense-bf16 MFMA time of the flops

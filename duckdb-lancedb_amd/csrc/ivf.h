@@ -91,8 +91,22 @@ struct IvfState {
 	DevBuf<float4> lbqaux;
 	DevBuf<int> cert;
 	std::vector<int> h_cert;
+	// fused coarse search (coarse_kernels.hip): per (query, partition) bounds, per-query fallback flags
+	DevBuf<float2> cbnd;
+	DevBuf<int> cflag;
+	std::vector<int> h_cflag;
 	~IvfState();
 };
+
+// ---- fused coarse search (coarse_kernels.hip) ----------------------------------
+// top-nprobe partitions of nq queries Q [nq][dim] (device, unpadded) over the
+// centroid rows C [nc][ld] f32, exact (the flat path's order and distances):
+// probe_l / probe_d [nq][nprobe], probe_c [nq]; flag[q] = 1 when query q must
+// take the flat path instead (non-finite bounds, candidate overflow).
+// bnd: nq * nc float2 scratch.
+bool coarse_fused_fits(int dim, int nc, int nprobe);
+void launch_coarse_search(const float *Q, int nq, int dim, const float *C, int ld, int nc, int metric, int nprobe,
+                          float2 *bnd, int64_t *probe_l, float *probe_d, int *probe_c, int *flag, hipStream_t st);
 
 // ---- host API (ivf_index.cpp) -----------------------------------------------
 // lance_detached_create_index: train (k-means on a seeded sample, PQ on the
@@ -211,7 +225,8 @@ void launch_pq_fast_scan(const uint8_t *lcodes, int m, int mp, const int64_t *lo
                          const uint8_t *lut8, const float2 *qpar, int kk, int *work, uint64_t *thrq, int *ocnt,
                          uint64_t *out, int ocap, const int4 *itab, int grid, hipStream_t st);
 void launch_pq_run_merge(const uint64_t *keys, const int *ocnt, int nq, int ocap, int K, uint64_t *out,
-                         hipStream_t st);
+                         hipStream_t st,
+                         const uint64_t *thrq = nullptr);
 // ltau [npos]: per list position sum_j T[l][j][c_j] (f32, j ascending), 0 for padding
 void launch_pq_tau(const uint8_t *codes, const uint32_t *lslot, const int64_t *loff, int nlist, int64_t npos, int m,
                    int mp, const float *T, float *ltau, hipStream_t st);

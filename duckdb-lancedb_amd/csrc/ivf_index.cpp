@@ -518,8 +518,28 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 		s->probe_d.need((size_t)n * nprobe);
 		s->probe_c.need((size_t)n);
 		const auto tc0 = std::chrono::steady_clock::now();
-		s->coarse->search_device(cos ? s->Qn.p : dQ + (int64_t)q0 * dim, n, nprobe, 1, s->probe_l.p, s->probe_d.p,
-		                         s->probe_c.p);
+		const float *Qc = cos ? s->Qn.p : dQ + (int64_t)q0 * dim;
+		bool coarse_done = false;
+		if (ix->ivf_coarse_fused && coarse_fused_fits(dim, s->nlist, nprobe) && s->coarse->n_slots == s->nlist &&
+		    !s->coarse->xbf16) {
+			// two launches (f32 MFMA bounds, per-query select + exact refine); a query
+			// it cannot certify sends the batch to the flat path below
+			s->cbnd.need((size_t)n * s->nlist);
+			s->cflag.need((size_t)n);
+			launch_coarse_search(Qc, n, dim, static_cast<const float *>(s->coarse->X), s->coarse->ld, s->nlist,
+			                     s->coarse->metric, nprobe, s->cbnd.p, s->probe_l.p, s->probe_d.p, s->probe_c.p,
+			                     s->cflag.p, st);
+			HIPCHK(hipGetLastError());
+			s->h_cflag.resize((size_t)n);
+			HIPCHK(hipMemcpyAsync(s->h_cflag.data(), s->cflag.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, st));
+			spin_sync(st);
+			coarse_done = true;
+			for (int i = 0; i < n; ++i)
+				if (s->h_cflag[(size_t)i]) coarse_done = false;
+			if (!coarse_done) ix->ivf_coarse_fallbacks += 1;
+		}
+		if (!coarse_done)
+			s->coarse->search_device(Qc, n, nprobe, 1, s->probe_l.p, s->probe_d.p, s->probe_c.p);
 		if (ix->time_kernels)
 			ix->kt_ivf_coarse_ms +=
 			    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count();
@@ -639,7 +659,8 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			                    s->okeys.p, ocap, s->itab.p, scan_grid(1 << 20), st);
 			ix->tic(1);
 			s->cand_a.need((size_t)n * kp);
-			launch_pq_run_merge(s->okeys.p, s->ocnt.p, n, ocap, kp, s->cand_a.p, st);
+			launch_pq_run_merge(s->okeys.p, s->ocnt.p, n, ocap, kp, s->cand_a.p, st,
+			                    ix->pq_merge_bound ? s->thrq.p : nullptr);
 			if (tail_n > 0) {
 				s->cand_b.need((size_t)n * k);
 				launch_ivf_merge(n, 0, nullptr, nullptr, 1, kk, nullptr, tail_nb, s->tkeys.p, k, s->cand_b.p, st);

@@ -2931,15 +2931,25 @@ void launch_pq_fast_scan(const uint8_t *lcodes, int m, int mp, const int64_t *lo
 	}
 }
 
-// per query: top-K of its output run (count ocnt[q], capped at ocap)
+// per query: top-K of its output run (count ocnt[q], capped at ocap).  thrq
+// (the scan's final per-query bound, nullable): an inclusive upper bound on the
+// run's K-th key — the cut that set it held K keys at or below it, and those
+// went out at their item's flush — so keys above it are never offered (no
+// buffer sorts for them)
 __global__ __launch_bounds__(256) void pq_run_merge_kernel(const uint64_t *__restrict__ keys, const int *__restrict__ ocnt,
-                                                           int ocap, int K, uint64_t *__restrict__ out) {
+                                                           int ocap, int K, uint64_t *__restrict__ out,
+                                                           const uint64_t *__restrict__ thrq) {
 	__shared__ uint64_t buf[IVF_TOPK_CAP];
 	__shared__ int cnt;
 	__shared__ uint64_t thr;
 	const int q = blockIdx.x, t = threadIdx.x;
 	TopK tk{buf, &cnt, &thr, K};
 	tk.reset();
+	if (thrq && t == 0) {
+		const uint64_t b = thrq[q];
+		thr = b == KEY64_NONE ? KEY64_NONE : b + 1;  // (offer keeps key < thr)
+	}
+	__syncthreads();
 	const int n = min(ocnt[q], ocap);
 	const uint64_t *src = keys + (int64_t)q * ocap;
 	for (int e0 = 0; e0 < n; e0 += 256) {
@@ -2952,8 +2962,8 @@ __global__ __launch_bounds__(256) void pq_run_merge_kernel(const uint64_t *__res
 }
 
 void launch_pq_run_merge(const uint64_t *keys, const int *ocnt, int nq, int ocap, int K, uint64_t *out,
-                         hipStream_t st) {
-	pq_run_merge_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(keys, ocnt, ocap, K, out);
+                         hipStream_t st, const uint64_t *thrq) {
+	pq_run_merge_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(keys, ocnt, ocap, K, out, thrq);
 }
 
 // ---------------------------------------------------------------------------

@@ -1479,6 +1479,18 @@ static void set_option_store(Index *ix, const std::string &k, const std::string 
 		ix->ivf_flat_bound = b;
 		return;
 	}
+	if (k == "ivf_coarse") {  // (results identical either way)
+		if (v == "fused") ix->ivf_coarse_fused = true;
+		else if (v == "flat") ix->ivf_coarse_fused = false;
+		else throw Error("ivf_coarse must be 'fused' or 'flat'");
+		return;
+	}
+	if (k == "pq_merge_bound") {  // (results identical either way; an A/B switch)
+		if (v == "1") ix->pq_merge_bound = true;
+		else if (v == "0") ix->pq_merge_bound = false;
+		else throw Error("pq_merge_bound: 1 or 0");
+		return;
+	}
 	if (k == "pq_seed") {
 		if (v == "1") ix->pq_seed = true;
 		else if (v == "0") ix->pq_seed = false;

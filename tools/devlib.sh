@@ -12,7 +12,7 @@ F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-inline-asm -Wno-unused-result
 make -s -C $D
 mkdir -p $D/lib_dev
 objs=""
-for o in knn_kernels scan8_kernels ivf_kernels lance_hip_abi ivf_index meta shards; do
+for o in knn_kernels scan8_kernels ivf_kernels coarse_kernels lance_hip_abi ivf_index meta shards; do
 	if [ "$o" = "${src}_kernels" ]; then
 		/opt/rocm/bin/hipcc $F "$@" -c $D/csrc/$o.hip -o $D/lib_dev/${o}_$n.o
 		objs="$objs $D/lib_dev/${o}_$n.o"

@@ -20,7 +20,8 @@ for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
     if r["Counter_Name"] != "FETCH_SIZE":
         continue
     n = r["Kernel_Name"]
-    key = "k16" if "k16" in n else ("k12c" if "k12ILi0E" in n else "k12" if "k12ILi2E" in n else None)
+    key = "k16" if "k16" in n else ("k12c" if ("k12<0>" in n or "k12ILi0E" in n) else
+                                     "k12" if ("k12<2>" in n or "k12ILi2E" in n) else None)
     if key:
         vals.setdefault(key, []).append(float(r["Counter_Value"]))
 res = {}
