@@ -1397,8 +1397,9 @@ __global__ __launch_bounds__(256) void flat_lb_merge_kernel(int nprobe, const in
 // exact f64 re-rank of the M bound candidates (+ the tail's exact keys), top k,
 // certificate: cut > the k-th exact distance of the result (or fewer than k
 // rows exist and nothing was cut)
+constexpr int RR_THREADS = 1024;  // re-rank workgroup: 16 waves, ~k r / 16 candidate rows each
 template <int METRIC, typename T>
-__global__ __launch_bounds__(256) void flat_lb_refine_kernel(const T *__restrict__ X, int ld, int dim,
+__global__ __launch_bounds__(RR_THREADS) void flat_lb_refine_kernel(const T *__restrict__ X, int ld, int dim,
                                                              const float *__restrict__ Qf,
                                                              const uint64_t *__restrict__ ca, int M,
                                                              const uint64_t *__restrict__ cbk, int kb,
@@ -1413,24 +1414,24 @@ __global__ __launch_bounds__(256) void flat_lb_refine_kernel(const T *__restrict
 	const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
 	if (t == 0) n = 0;
 	__syncthreads();
-	for (int i = t; i < M + kb; i += 256) {
+	for (int i = t; i < M + kb; i += RR_THREADS) {
 		// (bound keys carry the slot; the tail's exact keys slot ^ sx)
 		const uint64_t key = i < M ? ca[(int64_t)q * M + i] : cbk[(int64_t)q * kb + (i - M)];
 		if (key != KEY64_NONE) ss[atomicAdd(&n, 1)] = (uint32_t)key ^ (i < M ? 0u : sx);
 	}
 	__syncthreads();
 	const int nc = n;
-	for (int i = w; i < nc; i += 4) {
+	for (int i = w; i < nc; i += RR_THREADS / 64) {
 		const uint32_t slot = ss[i];
 		const float d = exact_distance<METRIC, T>(X + (int64_t)slot * ld, Qf + (int64_t)q * ld, dim, lane);
 		if (lane == 0) sk[i] = key64(d, slot ^ sx);
 	}
 	const int np = pow2_ceil(nc);
 	__syncthreads();
-	for (int i = nc + t; i < np; i += 256) sk[i] = KEY64_NONE;
+	for (int i = nc + t; i < np; i += RR_THREADS) sk[i] = KEY64_NONE;
 	wg_bitonic_sort(sk, np);
 	const int nout = nc < k ? nc : k;
-	for (int i = t; i < k; i += 256) {
+	for (int i = t; i < k; i += RR_THREADS) {
 		if (i < nout) {
 			outL[(int64_t)q * k + i] = labels[(uint32_t)sk[i] ^ sx];
 			outD[(int64_t)q * k + i] = key64_dist(sk[i]);
@@ -1558,7 +1559,7 @@ void launch_flat_lb_refine(const StoreView &s, const float *Qf, const uint64_t *
                            hipStream_t st) {
 	dim3 grid((unsigned)nq);
 	auto go = [&](auto kern, auto X) {
-		kern<<<grid, 256, 0, st>>>(X, s.ld, s.dim, Qf, ca, M, cb, kb, cut, k, s.labels, outL, outD, outC, cert,
+		kern<<<grid, RR_THREADS, 0, st>>>(X, s.ld, s.dim, Qf, ca, M, cb, kb, cut, k, s.labels, outL, outD, outC, cert,
 		                           tie_x32(s.tie_desc));
 	};
 	if (s.xbf16) {
@@ -2776,7 +2777,8 @@ __global__ __launch_bounds__(PQ_SEED_THREADS) void pq_seed_kernel(const uint8_t 
                                                       const float2 *__restrict__ qpar, int kk, int wb,
                                                       unsigned long long *__restrict__ thrq) {
 	__shared__ __attribute__((aligned(16))) uint8_t L[FQ_MAX_M * PQ_K];
-	__shared__ uint64_t keys[PQ_SEED_ROWS];
+	__shared__ unsigned hist[256];
+	__shared__ unsigned s_pre, s_rem;
 	const int q = blockIdx.x, t = threadIdx.x;
 	const int mm = MT > 0 ? MT : m;
 	const int64_t l = probe_l[(int64_t)q * nprobe];
@@ -2793,11 +2795,18 @@ __global__ __launch_bounds__(PQ_SEED_THREADS) void pq_seed_kernel(const uint8_t 
 	}
 	const int64_t p0 = loff[l], len = loff[l + 1] - p0;
 	const int n = (int)(len < PQ_SEED_ROWS ? len : PQ_SEED_ROWS);
-	int P = 64;
-	while (P < n) P <<= 1;
 	const int nch = mp >> 4;
+	if (t == 0) {
+		s_pre = 0;
+		s_rem = (unsigned)kk;
+	}
 	__syncthreads();
-	for (int r = t; r < P; r += PQ_SEED_THREADS) {
+	// this thread's rows' ordered distance keys (the high word of the scan's key)
+	constexpr int RPT = (PQ_SEED_ROWS + PQ_SEED_THREADS - 1) / PQ_SEED_THREADS;
+	uint32_t hk[RPT];
+#pragma unroll
+	for (int i = 0; i < RPT; ++i) {
+		const int r = t + i * PQ_SEED_THREADS;
 		uint64_t key = KEY64_NONE;
 		if (r < n) {
 			const int64_t ps = p0 + r;
@@ -2821,13 +2830,52 @@ __global__ __launch_bounds__(PQ_SEED_THREADS) void pq_seed_kernel(const uint8_t 
 				key = key64(a, slot);
 			}
 		}
-		keys[r] = key;
+		hk[i] = (uint32_t)(key >> 32);
 	}
-	wg_bitonic_sort(keys, P);
-	if (t == 0 && kk <= n) {
-		const uint64_t b = keys[kk - 1];
-		if (b != KEY64_NONE) atomicMin(thrq + q, (unsigned long long)b);
+	// the kk-th smallest high word T by a radix select (4 passes of 8 bits, no
+	// sort); (T << 32) | 0xFFFFFFFF is then an inclusive bound with kk live keys
+	// at or below it (as the kk-th full key was: looser only among equal high words)
+	if (kk > n) return;  // (uniform: fewer rows than kk, no seed)
+	uint32_t mask = 0;
+	for (int sh = 24; sh >= 0; sh -= 8) {
+		for (int i = t; i < 256; i += PQ_SEED_THREADS) hist[i] = 0;
+		__syncthreads();
+		const uint32_t pre = s_pre;
+#pragma unroll
+		for (int i = 0; i < RPT; ++i)
+			if (t + i * PQ_SEED_THREADS < n && (hk[i] & mask) == pre) atomicAdd(&hist[(hk[i] >> sh) & 255u], 1u);
+		__syncthreads();
+		if (t < 64) {  // wave 0: prefix sums over the 256 bins (4 per lane), find the bin holding the rem-th
+			const unsigned rem = s_rem;
+			unsigned h4[4], c = 0;
+#pragma unroll
+			for (int u = 0; u < 4; ++u) {
+				h4[u] = hist[4 * t + u];
+				c += h4[u];
+			}
+			unsigned x = c;
+#pragma unroll
+			for (int o = 1; o < 64; o <<= 1) {
+				const unsigned y = __shfl_up(x, o, 64);
+				if (t >= o) x += y;
+			}
+			unsigned ex = x - c;  // keys in bins before this lane's four
+			if (ex < rem && rem <= x) {
+#pragma unroll
+				for (int u = 0; u < 4; ++u) {
+					if (rem <= ex + h4[u]) {
+						s_pre = pre | ((uint32_t)(4 * t + u) << sh);
+						s_rem = rem - ex;
+						break;
+					}
+					ex += h4[u];
+				}
+			}
+		}
+		mask |= 255u << sh;
+		__syncthreads();
 	}
+	if (t == 0 && s_pre != KEY_NAN) atomicMin(thrq + q, ((unsigned long long)s_pre << 32) | 0xFFFFFFFFull);
 }
 
 void launch_pq_seed(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
@@ -3044,7 +3092,7 @@ void launch_keys_to_output(const uint64_t *keys, int nq, int K, int k, const int
 // exact re-rank of the ADC candidates (+ the tail's exact candidates): one
 // wave per candidate (f64, the flat path's refine arithmetic), bitonic sort
 template <int METRIC, typename T>
-__global__ __launch_bounds__(256) void ivf_refine_final_kernel(const T *__restrict__ X, int ld, int dim,
+__global__ __launch_bounds__(RR_THREADS) void ivf_refine_final_kernel(const T *__restrict__ X, int ld, int dim,
                                                                const float *__restrict__ Qf,
                                                                const uint64_t *__restrict__ ca, int ka,
                                                                const uint64_t *__restrict__ cbk, int kb, int k,
@@ -3057,24 +3105,24 @@ __global__ __launch_bounds__(256) void ivf_refine_final_kernel(const T *__restri
 	const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
 	if (t == 0) n = 0;
 	__syncthreads();
-	for (int i = t; i < ka + kb; i += 256) {
+	for (int i = t; i < ka + kb; i += RR_THREADS) {
 		// (ADC keys carry the slot; the tail's exact keys slot ^ sx)
 		const uint64_t key = i < ka ? ca[(int64_t)q * ka + i] : cbk[(int64_t)q * kb + (i - ka)];
 		if (key != KEY64_NONE) ss[atomicAdd(&n, 1)] = (uint32_t)key ^ (i < ka ? 0u : sx);
 	}
 	__syncthreads();
 	const int nc = n;
-	for (int i = w; i < nc; i += 4) {
+	for (int i = w; i < nc; i += RR_THREADS / 64) {
 		const uint32_t slot = ss[i];
 		const float d = exact_distance<METRIC, T>(X + (int64_t)slot * ld, Qf + (int64_t)q * ld, dim, lane);
 		if (lane == 0) sk[i] = key64(d, slot ^ sx);
 	}
 	const int np = pow2_ceil(nc);
 	__syncthreads();
-	for (int i = nc + t; i < np; i += 256) sk[i] = KEY64_NONE;
+	for (int i = nc + t; i < np; i += RR_THREADS) sk[i] = KEY64_NONE;
 	wg_bitonic_sort(sk, np);
 	const int nout = nc < k ? nc : k;
-	for (int i = t; i < k; i += 256) {
+	for (int i = t; i < k; i += RR_THREADS) {
 		if (i < nout) {
 			outL[(int64_t)q * k + i] = labels[(uint32_t)sk[i] ^ sx];
 			outD[(int64_t)q * k + i] = key64_dist(sk[i]);
@@ -3093,9 +3141,9 @@ static void refine_final_dispatch(const StoreView &s, const float *Qf, const uin
 	dim3 grid((unsigned)nq);
 #define RF_ARGS X, s.ld, s.dim, Qf, ca, ka, cb, kb, k, s.labels, outL, outD, outC, tie_x32(s.tie_desc)
 	switch (s.metric) {
-	case METRIC_L2: ivf_refine_final_kernel<METRIC_L2, T><<<grid, 256, 0, st>>>(RF_ARGS); break;
-	case METRIC_DOT: ivf_refine_final_kernel<METRIC_DOT, T><<<grid, 256, 0, st>>>(RF_ARGS); break;
-	default: ivf_refine_final_kernel<METRIC_COSINE, T><<<grid, 256, 0, st>>>(RF_ARGS); break;
+	case METRIC_L2: ivf_refine_final_kernel<METRIC_L2, T><<<grid, RR_THREADS, 0, st>>>(RF_ARGS); break;
+	case METRIC_DOT: ivf_refine_final_kernel<METRIC_DOT, T><<<grid, RR_THREADS, 0, st>>>(RF_ARGS); break;
+	default: ivf_refine_final_kernel<METRIC_COSINE, T><<<grid, RR_THREADS, 0, st>>>(RF_ARGS); break;
 	}
 #undef RF_ARGS
 }

@@ -302,3 +302,34 @@ def test_ivf_flat_bound_scan_zero_cosine_rows_and_query(hip, mk):
         np.testing.assert_array_equal(bc, xc)
         np.testing.assert_array_equal(bl, xl)
         np.testing.assert_allclose(bd, xd, rtol=1e-6, equal_nan=True)
+
+
+@pytest.mark.parametrize("metric", ["l2", "dot", "cosine"])
+def test_fused_coarse_search_equals_flat(hip, mk, metric):
+    """The fused coarse search (coarse_kernels.hip: f32 MFMA bounds, per-query
+    select + exact refine) returns exactly the probes of the flat path over the
+    centroid store (ivf_coarse = flat), so every search result is identical; a
+    NaN query sends its batch to the flat path (the fallback counter moves)."""
+    rng = np.random.default_rng(91)
+    n, d, nlist = 20_000, 96, 300
+    X = clustered(rng, n, d, centers=64)
+    Q = (X[rng.choice(n, 120, replace=False)] + 0.3 * rng.standard_normal((120, d))).astype(np.float32)
+    h = mk(d, metric, "ivf_flat")
+    hip.LanceDetachedAddBatch(h, X, n, d)
+    hip.LanceDetachedCreateIndex(h, nlist, 0)
+    for nprobe in (1, 37, 300):
+        hip.LanceHipSetOption(h, "ivf_coarse", "fused")
+        a = hip.LanceDetachedSearchBatch(h, Q, 10, nprobes=nprobe)
+        hip.LanceHipSetOption(h, "ivf_coarse", "flat")
+        b = hip.LanceDetachedSearchBatch(h, Q, 10, nprobes=nprobe)
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])
+        el, ed, ec = oracle_search(hip, h, X, Q, 10, nprobe, 1, metric)
+        assert_same(*a, el, ed, ec)
+    hip.LanceHipSetOption(h, "ivf_coarse", "fused")
+    Qn = Q.copy()
+    Qn[3] = np.nan
+    a = hip.LanceDetachedSearchBatch(h, Qn, 10, nprobes=16)
+    hip.LanceHipSetOption(h, "ivf_coarse", "flat")
+    b = hip.LanceDetachedSearchBatch(h, Qn, 10, nprobes=16)
+    np.testing.assert_array_equal(a[0], b[0])

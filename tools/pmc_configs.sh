@@ -23,7 +23,7 @@ for cfg in "$@"; do
 	nstar) python3 tools/pmc_traffic.py $F $W $O/${T}_nstar_scan_traffic.json --n 10000000 --dim 768 --batch 256 --elem-bytes 1 --kernel "$S8" --bench-kernel "scan8_kernel<L2,append,i8>" ;;
 	c3) python3 tools/pmc_traffic.py $F $W $O/${T}_c3_scan_traffic.json --n 10000000 --dim 768 --batch 256 --elem-bytes 1 --kernel "$S8" --bench-kernel "scan8_kernel<DOT,append,i8>" ;;
 	c4) python3 tools/pmc_traffic.py $F $W $O/${T}_c4_ivf_traffic.json --n 12500000 --dim 768 --batch 256 --kernel "flat_list_lb_kernel" --bench-kernel "flat_list_lb_kernel" ;;
-	c5) python3 tools/pmc_traffic.py $F $W $O/${T}_c5_ivf_traffic.json --n 12500000 --dim 768 --batch 256 --kernel "pq_fast_scan_bank_kernel" --bench-kernel "pq_fast_scan_bank_kernel" ;;
+	c5) python3 tools/pmc_traffic.py $F $W $O/${T}_c5_ivf_traffic.json --n 12500000 --dim 768 --batch 256 --kernel "pq_fast_scan_bank_kernel" --bench-kernel "pq_fast_scan_bank_kernel" --fetch-factor 1.918 ;;
 	esac
 	rm -rf $F $W  # (the raw CSVs: gpurun returns at most 64 MiB)
 done

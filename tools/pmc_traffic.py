@@ -36,16 +36,20 @@ def main():
     ap.add_argument("--elem-bytes", type=int, default=4, help="bytes per element the scan streams")
     ap.add_argument("--kernel", default="scan_kernel<0, 1>")
     ap.add_argument("--bench-kernel", default=None, help="bench.py's roofline.kernel name the passes belong to")
+    ap.add_argument("--fetch-factor", type=float, default=2.0,
+                    help="bytes per FETCH_SIZE byte of this kernel's access pattern (2.0: 16-B/lane streams, "
+                         "MI355X_MICROARCH.md 'HBM'; the PQ scan's 12-B/lane row stream: profiles/r06b_fetch_calib.json)")
     a = ap.parse_args()
     fk, nf = per_launch(a.fetch_dir, "FETCH_SIZE", a.kernel)
     wk, nw = per_launch(a.write_dir, "WRITE_SIZE", a.kernel)
-    read_b = 2.0 * fk * 1024.0
+    read_b = a.fetch_factor * fk * 1024.0
     write_b = wk * 1024.0
     out = {"kernel": a.kernel, "n": a.n, "dim": a.dim, "batch": a.batch, "scan_elem_bytes": a.elem_bytes, "launches": [nf, nw],
            "fetch_size_kib_per_launch": fk, "write_size_kib_per_launch": wk,
            "hbm_read_bytes_corrected": read_b, "hbm_write_bytes": write_b,
            "traffic_bytes_per_launch": read_b + write_b,
-           "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE as is; KiB -> bytes"}
+           "correction": f"FETCH_SIZE x{a.fetch_factor:g} (gfx950 wide-read undercount, calibrated for this access pattern), "
+                         "WRITE_SIZE as is; KiB -> bytes"}
     if a.bench_kernel:
         out["bench_kernel"] = a.bench_kernel
     with open(a.out, "w") as f:
