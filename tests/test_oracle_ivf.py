@@ -3,6 +3,7 @@ tests compare against: with every list probed IVF_FLAT is the exact flat
 search, and IVF_PQ with a re-rank window covering every row is too; the ADC
 tables follow their f32 definitions."""
 import numpy as np
+import pytest
 
 from oracle import flat_knn, ivf
 
@@ -128,3 +129,39 @@ def test_u8_lut_bounds_the_f32_lut():
     rec = lo[:, None] + D * u.astype(np.float32)
     assert np.all(np.abs(rec - L) <= D * 0.5 * (1 + 1e-5) + 1e-5)
     assert u.max() <= 255 and abs(L0 - lo.astype(np.float64).sum()) < 1e-3
+
+
+@pytest.mark.parametrize("tie", ["label_desc", "label_asc"])
+def test_c_ivf_port_matches_numpy_oracle_with_ties(tie):
+    """Duplicate rows (exact-distance ties at the k-th place, in the probed lists
+    and in the unindexed tail): the C port and oracle/ivf.py pick the same tied
+    rows under either tie rule (final order: distance, then label by the rule;
+    probes and ADC candidates: lower id first)."""
+    from oracle import c_oracle
+
+    rng = np.random.default_rng(33)
+    n, d, nlist, m = 900, 32, 10, 8
+    X, C, lists, cb, codes = _model(rng, n, d, nlist, m)
+    X = X.copy()
+    for src in (3, 100, 500):
+        X[rng.choice(n, 12, replace=False)] = X[src]
+    Q = np.stack([X[3], X[100], X[500], X[3] + 0.01]).astype(np.float32)
+    lab = np.arange(n, dtype=np.int64)
+    live = np.ones(n, bool)
+    lists = lists.copy()
+    lists[850:] = -1
+    lay = c_oracle.IvfLayout(lists, live, nlist)
+    for nprobe, k in [(nlist, 8), (3, 6)]:
+        el, ed, ec = ivf.ivf_flat_search(X, lab, live, lists, C, Q, k, nprobe, "l2", tie=tie)
+        gl, gd, gc = c_oracle.ivf_search_batch(X, lab, lay, C, Q, k, nprobe, "l2", tie=tie)
+        np.testing.assert_array_equal(gl, el)
+        np.testing.assert_array_equal(gd, ed)
+        _, T = ivf.pq_tables(C, cb, Q[:1], "l2")
+        el, ed, ec = ivf.ivf_pq_search(X, lab, live, lists, codes, C, cb, Q, k, nprobe, 50, "l2", lut="u8", tie=tie)
+        gl, gd, gc = c_oracle.ivf_search_batch(X, lab, lay, C, Q, k, nprobe, "l2", codes=codes, codebook=cb, T=T,
+                                               refine_factor=50, lut="u8", tie=tie)
+        np.testing.assert_array_equal(gl, el)
+    # with every list probed the flat IVF result is the exact flat result under the same rule
+    fl, fd, fc = flat_knn.flat_search_batch(X, lab, live, Q, 8, "l2", tie=tie)
+    el, ed, ec = ivf.ivf_flat_search(X, lab, live, lists, C, Q, 8, nlist, "l2", tie=tie)
+    np.testing.assert_array_equal(el, fl)
