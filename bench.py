@@ -80,6 +80,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--settle-s", type=float, default=0.3,
+                    help="untimed steps for about this long BEFORE the W warmup steps: the GPU clocks up over its "
+                         "first ~40-60 steps under load (C2 0.34 -> 0.27 ms per step, tools/ramp_probe.py, "
+                         "profiles/r06e_ramp.jsonl); 0 = none")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--dim", type=int, default=None)
@@ -178,6 +182,28 @@ def launch_ranks(a):
                     o.terminate()
         time.sleep(0.05)
     return rc
+
+
+def settle(step, sync, seconds, dist, device):
+    """Untimed steps for about `seconds` before the warmup and timed steps (the
+    GPU's clock / power state ramps over the first tens of ms of a load:
+    profiles/r06e_ramp.jsonl).  Every rank runs the same number of steps (a
+    multi-GPU step holds a collective): each times 3 steps, the max over ranks
+    sets the count.  Returns the steps run."""
+    if seconds <= 0:
+        return 0
+    t0 = time.perf_counter()
+    for _ in range(3):
+        step()
+    sync()
+    est = torch.tensor([(time.perf_counter() - t0) / 3.0], dtype=torch.float64, device=device)
+    if dist:
+        dist.all_reduce(est, op=dist.ReduceOp.MAX)
+    n = int(min(200_000, max(0.0, seconds / max(float(est.item()), 1e-6) - 3)))
+    for _ in range(n):
+        step()
+    sync()
+    return n + 3
 
 
 def timed_steps(step, steps, warmup, dist, device, sync):
@@ -445,6 +471,7 @@ def main_ivf(a):
             return lance_hip.LanceDetachedSearch(h, Qh_api[i], D, K)
         return searcher.search(Q, K, reuse_outputs=True)
 
+    settled = settle(step, torch.cuda.synchronize, a.settle_s, dist, dev)
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -545,6 +572,7 @@ def main_ivf(a):
         line = {
             "metric": f"kNN queries/sec + recall@10, {what} nlist={a.nlist} nprobe={a.nprobe}, {N}x{D} f32 per GPU",
             "value": round(value, 1), "unit": "queries/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "settle": {"steps": settled, "seconds": a.settle_s},
             "ms_per_step": round(1000.0 * t / a.steps, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": a.storage,
             "data": f"synthetic clustered rows: {NCENT} Gaussian clusters (centers N(0,1), sigma {SIGMA}), queries "
@@ -586,6 +614,13 @@ def main_c1(a):
     Q = np.random.default_rng(5678).standard_normal((max(a.steps, 64), D), dtype=np.float32)
     h = lance_hip.LanceCreateDetached("", D, a.metric, "c1")
     lance_hip.LanceDetachedAddBatch(h, X, N, D)
+    ci = [0]
+
+    def one():
+        lance_hip.LanceDetachedSearch(h, Q[ci[0] % len(Q)], D, K)
+        ci[0] += 1
+
+    settled = settle(one, lambda: None, a.settle_s, None, "cpu")
     for i in range(a.warmup):
         lance_hip.LanceDetachedSearch(h, Q[i % len(Q)], D, K)
     got = []
@@ -625,6 +660,7 @@ def main_c1(a):
                 "note": "a 10k-row store is one short launch: latency, not bandwidth, sets the call time"}
     line = {"metric": "lance_search() queries/sec, 10kx128 f32 flat L2 k=10, one query per call (C1)",
             "value": round(a.steps / t, 1), "unit": "queries/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+            "settle": {"steps": settled, "seconds": a.settle_s},
             "ms_per_step": round(1000.0 * t / a.steps, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic N(0,1) rows and queries (numpy default_rng)",
             "config": {"workload": "C1 flat l2 10000x128 f32 k=10, lance_detached_search per query (host buffers)",
@@ -752,7 +788,9 @@ def main():
             last_out[0] = r if r is not None else last_out[0]
         torch.cuda.synchronize()
 
-    # warmup for per_call: the timed calls then start at query 0 (the recall subset below)
+    # settle (clocks), then warmup; for per_call the timed calls then start at
+    # query 0 (the recall subset below)
+    settled = settle(step, sync, a.settle_s, dist, dev)
     for _ in range(a.warmup):
         step()
     sync()
@@ -929,6 +967,8 @@ def main():
             "n_gpus": len(inproc_devs.split(",")) if inproc_devs else world,
             "steps": a.steps,
             "warmup": a.warmup,
+            "settle": {"steps": settled, "seconds": a.settle_s,
+                       "why": "untimed steps before the warmup: the GPU clocks up over its first ~50 steps"},
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
             "scaling": a.scaling,

@@ -55,20 +55,46 @@ __global__ __launch_bounds__(256) void coarse_bounds_kernel(const float *__restr
 	f32x16 acc;
 #pragma unroll
 	for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-	double n2 = 0.0;  // threads 0..63: query q0 + t; 64..127: centroid c0 + t - 64
-	for (int k0 = 0; k0 < dim; k0 += CB_KC) {
-		__syncthreads();
-		// stage: 64 rows x 64 floats of each operand, 16 floats per thread and operand
-		for (int e = t; e < CB_T * CB_KC; e += 256) {
-			const int r = e / CB_KC, c = e % CB_KC, k = k0 + c;
+	// staging: a 64 x 64 f32 tile of each operand = 1024 float4, 4 per thread and
+	// operand, loaded for the NEXT chunk while this one multiplies (every load in
+	// flight together: dim % 4 == 0, coarse_fused_fits)
+	float4 rq[4], rc[4];
+	auto fetch = [&](int k0) {
+#pragma unroll
+		for (int j = 0; j < 4; ++j) {
+			const int e = t + 256 * j, r = e >> 4, c4 = (e & 15) * 4, k = k0 + c4;
 			const int q = q0 + r, cc = c0 + r;
-			Qs[r][c] = (q < nq && k < dim) ? Q[(int64_t)q * dim + k] : 0.f;
-			Cs[r][c] = (cc < nc && k < dim) ? C[(int64_t)cc * ld + k] : 0.f;
+			rq[j] = (q < nq && k < dim) ? *reinterpret_cast<const float4 *>(Q + (int64_t)q * dim + k)
+			                            : make_float4(0.f, 0.f, 0.f, 0.f);
+			rc[j] = (cc < nc && k < dim) ? *reinterpret_cast<const float4 *>(C + (int64_t)cc * ld + k)
+			                             : make_float4(0.f, 0.f, 0.f, 0.f);
+		}
+	};
+	// norms: thread t sums row t >> 1 of the 128 staged rows (query rows, then
+	// centroid rows), columns 32 (t & 1) .. + 32 of each chunk, in f64
+	const int nr = t >> 1, nh = (t & 1) * 32;
+	double n2 = 0.0;
+	fetch(0);
+	for (int k0 = 0; k0 < dim; k0 += CB_KC) {
+		__syncthreads();  // the previous chunk consumed
+#pragma unroll
+		for (int j = 0; j < 4; ++j) {
+			const int e = t + 256 * j, r = e >> 4, c4 = (e & 15) * 4;
+			Qs[r][c4] = rq[j].x;
+			Qs[r][c4 + 1] = rq[j].y;
+			Qs[r][c4 + 2] = rq[j].z;
+			Qs[r][c4 + 3] = rq[j].w;
+			Cs[r][c4] = rc[j].x;
+			Cs[r][c4 + 1] = rc[j].y;
+			Cs[r][c4 + 2] = rc[j].z;
+			Cs[r][c4 + 3] = rc[j].w;
 		}
 		__syncthreads();
-		if (t < 2 * CB_T) {
-			const float *row = t < CB_T ? Qs[t] : Cs[t - CB_T];
-			for (int c = 0; c < CB_KC; ++c) n2 = fma((double)row[c], (double)row[c], n2);
+		if (k0 + CB_KC < dim) fetch(k0 + CB_KC);  // in flight during the MFMAs
+		{
+			const float *row = nr < CB_T ? Qs[nr] : Cs[nr - CB_T];
+#pragma unroll 8
+			for (int c = 0; c < 32; ++c) n2 = fma((double)row[nh + c], (double)row[nh + c], n2);
 		}
 #pragma unroll 8
 		for (int kk = 0; kk < CB_KC; kk += 2) {
@@ -78,7 +104,8 @@ __global__ __launch_bounds__(256) void coarse_bounds_kernel(const float *__restr
 		}
 	}
 	mfma_operand_guard();
-	if (t < 2 * CB_T) nrm[t < CB_T ? 0 : 1][t & (CB_T - 1)] = n2;
+	n2 += __shfl_xor(n2, 1, 64);
+	if ((t & 1) == 0) nrm[nr < CB_T ? 0 : 1][nr & (CB_T - 1)] = n2;
 	__syncthreads();
 	// |S~ - S| <= g |q||c|: an f32 sum of ld exact products, every addition rounded
 	const double g = (double)ld * 0x1p-23;
@@ -128,28 +155,56 @@ __global__ __launch_bounds__(CS_THREADS) void coarse_select_kernel(const float2 
 	}
 	for (int i = t; i < ((dim + 3) & ~3); i += CS_THREADS) qs[i] = i < dim ? Q[(int64_t)q * dim + i] : 0.f;
 	__syncthreads();
-	// radix select of the rem-th smallest UB key, 8 bits at a time
+	// this thread's bounds in registers (read once), then a radix select of the
+	// rem-th smallest UB key, 8 bits at a time (wave 0 scans the 256 bins)
+	constexpr int BPT = 8;  // (nc <= CS_THREADS * BPT, coarse_fused_fits)
+	float lbv[BPT];
+	uint32_t ubk[BPT];
+	bool bad = false;
+#pragma unroll
+	for (int j = 0; j < BPT; ++j) {
+		const int i = t + j * CS_THREADS;
+		const float2 v = i < nc ? b[i] : make_float2(F_INF, F_INF);
+		if (i < nc && !(__builtin_isfinite(v.x) && __builtin_isfinite(v.y))) bad = true;
+		lbv[j] = v.x;
+		ubk[j] = i < nc ? fkey(v.y) : 0xFFFFFFFFu;
+	}
+	if (bad) s_bad = 1;
 	unsigned mask = 0;
 	for (int sh = 24; sh >= 0; sh -= 8) {
 		for (int i = t; i < 256; i += CS_THREADS) hist[i] = 0;
 		__syncthreads();
 		const unsigned pre = s_prefix;
-		for (int i = t; i < nc; i += CS_THREADS) {
-			const float2 v = b[i];
-			if (!(__builtin_isfinite(v.x) && __builtin_isfinite(v.y))) s_bad = 1;
-			const uint32_t k = fkey(v.y);
-			if ((k & mask) == pre) atomicAdd(&hist[(k >> sh) & 255], 1u);
-		}
+#pragma unroll
+		for (int j = 0; j < BPT; ++j)
+			if (t + j * CS_THREADS < nc && (ubk[j] & mask) == pre) atomicAdd(&hist[(ubk[j] >> sh) & 255], 1u);
 		__syncthreads();
-		if (t == 0) {
-			unsigned rem = s_rem, c = 0;
-			int d = 0;
-			for (; d < 256; ++d) {
-				if (c + hist[d] >= rem) break;
-				c += hist[d];
+		if (t < 64) {
+			const unsigned rem = s_rem;
+			unsigned h4[4], c = 0;
+#pragma unroll
+			for (int u = 0; u < 4; ++u) {
+				h4[u] = hist[4 * t + u];
+				c += h4[u];
 			}
-			s_prefix = pre | ((unsigned)d << sh);
-			s_rem = rem - c;
+			unsigned x = c;
+#pragma unroll
+			for (int o = 1; o < 64; o <<= 1) {
+				const unsigned y = __shfl_up(x, o, 64);
+				if (t >= o) x += y;
+			}
+			unsigned ex = x - c;
+			if (ex < rem && rem <= x) {
+#pragma unroll
+				for (int u = 0; u < 4; ++u) {
+					if (rem <= ex + h4[u]) {
+						s_prefix = pre | ((unsigned)(4 * t + u) << sh);
+						s_rem = rem - ex;
+						break;
+					}
+					ex += h4[u];
+				}
+			}
 		}
 		mask |= 255u << sh;
 		__syncthreads();
@@ -160,8 +215,10 @@ __global__ __launch_bounds__(CS_THREADS) void coarse_select_kernel(const float2 
 	}
 	const float T = fkey_inv(s_prefix);
 	// candidates: every partition whose LB <= T
-	for (int i = t; i < nc; i += CS_THREADS) {
-		if (b[i].x <= T) {
+#pragma unroll
+	for (int j = 0; j < BPT; ++j) {
+		const int i = t + j * CS_THREADS;
+		if (i < nc && lbv[j] <= T) {
 			const unsigned p = atomicAdd(&s_n, 1u);
 			if (p < (unsigned)CS_CAP) keys[p] = (uint64_t)i;
 		}
@@ -209,7 +266,9 @@ __global__ __launch_bounds__(CS_THREADS) void coarse_select_kernel(const float2 
 	}
 }
 
-bool coarse_fused_fits(int dim, int nc, int nprobe) { return dim <= 4096 && nprobe <= nc && nc > 0 && nprobe > 0; }
+bool coarse_fused_fits(int dim, int nc, int nprobe) {
+	return dim <= 4096 && dim % 4 == 0 && nprobe <= nc && nc > 0 && nc <= CS_THREADS * 8 && nprobe > 0;
+}
 
 void launch_coarse_search(const float *Q, int nq, int dim, const float *C, int ld, int nc, int metric, int nprobe,
                           float2 *bnd, int64_t *probe_l, float *probe_d, int *probe_c, int *flag, hipStream_t st) {

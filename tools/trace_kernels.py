@@ -18,8 +18,11 @@ for r in rows:
     short = n.split("(")[0].replace("void ", "").replace("lhip::", "")
     dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
     seq.append((short, dur, int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
-# steps start at query_absmax (int8 path) or prep_queries
-starts = [i for i, s in enumerate(seq) if s[0].startswith("query_absmax") or s[0].startswith("prep_queries_kernel")]
+# steps start at ivf_prep (IVF configs) or else query_absmax (int8 path) / prep_queries
+if any(s[0].startswith("ivf_prep_kernel") for s in seq):
+    starts = [i for i, s in enumerate(seq) if s[0].startswith("ivf_prep_kernel")]
+else:
+    starts = [i for i, s in enumerate(seq) if s[0].startswith("query_absmax") or s[0].startswith("prep_queries_kernel")]
 steps = [seq[a:b] for a, b in zip(starts, starts[1:] + [len(seq)])][-last:]
 for st in steps:
     npr = 0
