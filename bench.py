@@ -188,22 +188,26 @@ def settle(step, sync, seconds, dist, device):
     """Untimed steps for about `seconds` before the warmup and timed steps (the
     GPU's clock / power state ramps over the first tens of ms of a load:
     profiles/r06e_ramp.jsonl).  Every rank runs the same number of steps (a
-    multi-GPU step holds a collective): each times 3 steps, the max over ranks
-    sets the count.  Returns the steps run."""
+    multi-GPU step holds a collective): each times steps 4..8 (past the first
+    calls' lazy allocations), the max over ranks sets the count.  Returns the
+    steps run."""
     if seconds <= 0:
         return 0
-    t0 = time.perf_counter()
     for _ in range(3):
         step()
     sync()
-    est = torch.tensor([(time.perf_counter() - t0) / 3.0], dtype=torch.float64, device=device)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        step()
+    sync()
+    est = torch.tensor([(time.perf_counter() - t0) / 5.0], dtype=torch.float64, device=device)
     if dist:
         dist.all_reduce(est, op=dist.ReduceOp.MAX)
-    n = int(min(200_000, max(0.0, seconds / max(float(est.item()), 1e-6) - 3)))
+    n = int(min(200_000, max(0.0, seconds / max(float(est.item()), 1e-6) - 8)))
     for _ in range(n):
         step()
     sync()
-    return n + 3
+    return n + 8
 
 
 def timed_steps(step, steps, warmup, dist, device, sync):

@@ -2993,13 +2993,41 @@ __global__ __launch_bounds__(256) void pq_run_merge_kernel(const uint64_t *__res
 	const int q = blockIdx.x, t = threadIdx.x;
 	TopK tk{buf, &cnt, &thr, K};
 	tk.reset();
-	if (thrq && t == 0) {
-		const uint64_t b = thrq[q];
-		thr = b == KEY64_NONE ? KEY64_NONE : b + 1;  // (offer keeps key < thr)
-	}
-	__syncthreads();
 	const int n = min(ocnt[q], ocap);
 	const uint64_t *src = keys + (int64_t)q * ocap;
+	if (thrq) {
+		// one pass: only keys at or below the bound (typically ~K .. 2K of the
+		// run) go to the buffer, 8 loads in flight per thread; then one sort
+		const uint64_t bq = thrq[q];
+		for (int e0 = t; e0 < n; e0 += 256 * 8) {
+			uint64_t kv[8];
+#pragma unroll
+			for (int u = 0; u < 8; ++u) kv[u] = e0 + 256 * u < n ? src[e0 + 256 * u] : KEY64_NONE;
+#pragma unroll
+			for (int u = 0; u < 8; ++u)
+				if (kv[u] != KEY64_NONE && kv[u] <= bq) {
+					const int p = atomicAdd(&cnt, 1);
+					if (p < IVF_TOPK_CAP) buf[p] = kv[u];
+				}
+		}
+		__syncthreads();
+		const int c = cnt;
+		if (c <= IVF_TOPK_CAP) {
+			const int np = pow2_ceil(c);
+			for (int i = c + t; i < np; i += 256) buf[i] = KEY64_NONE;
+			wg_bitonic_sort(buf, np);
+			const int nout = c < K ? c : K;
+			for (int i = t; i < K; i += 256) out[(int64_t)q * K + i] = i < nout ? buf[i] : KEY64_NONE;
+			return;
+		}
+		// (more than the buffer at or below the bound: the streaming top-K below, from the bound)
+		__syncthreads();
+		if (t == 0) {
+			cnt = 0;
+			thr = bq == KEY64_NONE ? KEY64_NONE : bq + 1;  // (offer keeps key < thr)
+		}
+		__syncthreads();
+	}
 	for (int e0 = 0; e0 < n; e0 += 256) {
 		const int e = e0 + t;
 		const uint64_t k = e < n ? src[e] : KEY64_NONE;
