@@ -455,7 +455,7 @@ def main_ivf(a):
     BG = B * world
     qids = torch.randint(0, NCENT, (BG,), generator=g, device=dev)
     Q = (centers[qids] + SIGMA * torch.randn((BG, D), generator=g, device=dev, dtype=torch.float32)).contiguous()
-    from lance_hip.sharded import ShardedSearch, hip_device_merge, hip_device_search
+    from lance_hip.sharded import AsyncPipeline, ShardedPipeline, ShardedSearch, hip_device_merge, hip_device_search
 
     searcher = ShardedSearch(hip_device_search(L, h, D, nprobes=a.nprobe, refine_factor=a.refine),
                              hip_device_merge(L), label_offset=s0, dist=dist, world=world)
@@ -465,6 +465,17 @@ def main_ivf(a):
         raise SystemExit("--api host_batch / per_call: one GPU (the host C-ABI is unsharded)")
     Qh_api = Q.cpu().numpy() if a.api != "device" else None
     call_i = [0]
+    # device API: two searches in flight on the handle (lance_hip_search_batch_device_async:
+    # the IVF search is enqueued whole, its completion — the fused coarse search's flags,
+    # a rerun if one is set — at its wait inside the timed region); --sync: one
+    # synchronous call per batch
+    pipelined = a.api == "device" and not a.sync
+    pipe = None
+    if pipelined:
+        pipe = AsyncPipeline(L, h, D, nprobes=a.nprobe, refine_factor=a.refine)
+        if world > 1:
+            pipe = ShardedPipeline(pipe, searcher)
+    last_out = [None]
 
     def step():
         if a.api == "host_batch":
@@ -473,18 +484,28 @@ def main_ivf(a):
             i = call_i[0] % BG
             call_i[0] += 1
             return lance_hip.LanceDetachedSearch(h, Qh_api[i], D, K)
+        if pipelined:
+            r = pipe.step(Q, K)
+            last_out[0] = r if r is not None else last_out[0]
+            return r
         return searcher.search(Q, K, reuse_outputs=True)
 
-    settled = settle(step, torch.cuda.synchronize, a.settle_s, dist, dev)
+    def sync():
+        if pipelined:
+            r = pipe.drain()
+            last_out[0] = r if r is not None else last_out[0]
+        torch.cuda.synchronize()
+
+    settled = settle(step, sync, a.settle_s, dist, dev)
     for _ in range(a.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         res = step()
-    torch.cuda.synchronize()
+    sync()
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
@@ -492,6 +513,17 @@ def main_ivf(a):
     if dist:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     t = float(elapsed.item())
+    if pipelined:
+        res = tuple(x.clone() for x in last_out[0])
+    sync_leg = None
+    if pipelined and world == 1:
+        # the synchronous call beside it (one lance_hip_search_batch_device per batch)
+        ts, rs, _ = timed_steps(lambda: searcher.search(Q, K, reuse_outputs=True), a.steps, a.warmup, None, dev,
+                                torch.cuda.synchronize)
+        sync_leg = {"value": round(BG * a.steps / ts, 1), "unit": "queries/s",
+                    "ms_per_step": round(1000.0 * ts / a.steps, 4),
+                    "api": "lance_hip_search_batch_device, one synchronous call per batch",
+                    "ids_equal_pipelined": bool(np.array_equal(rs[0].cpu().numpy(), res[0].cpu().numpy()))}
     lance_hip.LanceHipSetOption(h, "time_kernels", "1")
     for _ in range(max(3, min(a.steps, 10))):
         step()
@@ -593,6 +625,7 @@ def main_ivf(a):
             **({"recall_at_10_by_refine": recall_sweep} if recall_sweep else {}),
             "roofline": roof,
             "cpu_baseline": cpu,
+            **({"sync": sync_leg} if sync_leg else {}),
             "build_s": round(build_s, 2), "gen_s": round(gen_s, 2),
         }
         print(json.dumps(line), flush=True)

@@ -209,8 +209,20 @@ __global__ __launch_bounds__(CS_THREADS) void coarse_select_kernel(const float2 
 		mask |= 255u << sh;
 		__syncthreads();
 	}
+	// a flagged query leaves no probes (every later kernel skips probe -1; the
+	// host reruns the batch on the flat path once the pass has completed)
+	auto flagged = [&]() {
+		for (int i = t; i < nprobe; i += CS_THREADS) {
+			probe_l[(int64_t)q * nprobe + i] = -1;
+			probe_d[(int64_t)q * nprobe + i] = __builtin_nanf("");
+		}
+		if (t == 0) {
+			probe_c[q] = 0;
+			flag[q] = 1;
+		}
+	};
 	if (s_bad) {
-		if (t == 0) flag[q] = 1;
+		flagged();
 		return;
 	}
 	const float T = fkey_inv(s_prefix);
@@ -226,7 +238,7 @@ __global__ __launch_bounds__(CS_THREADS) void coarse_select_kernel(const float2 
 	__syncthreads();
 	const int n = (int)s_n;
 	if (n > CS_CAP) {
-		if (t == 0) flag[q] = 1;
+		flagged();
 		return;
 	}
 	// exact distances, one wave per candidate (the row from L2: the centroids are

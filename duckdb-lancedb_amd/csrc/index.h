@@ -148,6 +148,12 @@ struct PendingPass {
 	QueryView qv{};
 	bool hmap = false, fast_ok = false, dense = false, two_append = false, async = false;
 	int64_t n_tiles = 0, ticket = 0, st3 = 0, st5 = 0;
+	// an asynchronous IVF search (ivf_search enqueued without its end wait): the
+	// pinned slot of its fused coarse flags, and what a rerun on the flat coarse
+	// path needs (ivf_finish)
+	bool ivf = false, ivf_fused = false;
+	int ivf_flag_slot = 0, nprobes = 0, refine = 0;
+	const float *dQ = nullptr;
 };
 
 struct Workspace {
@@ -284,12 +290,12 @@ struct Index {
 	uint64_t ivf_seed = 0x5eedULL;
 	bool pq_fast = true;    // IVF_PQ list-major 8-bit-LUT scan (option "pq_scan" = "fast"; "exact_lut": f32 LUT, query-major)
 	bool pq_seed = true;    // fast scan: per-query bound seeded from the nearest probed list (option "pq_seed")
-	bool pq_merge_bound = true;
-	bool ivf_coarse_fused = true;     // IVF coarse search by coarse_kernels.hip (option "ivf_coarse" = fused | flat)
-	int64_t ivf_coarse_fallbacks = 0;  // batches the fused coarse search sent to the flat path  // fast scan: the run merge skips keys above the scan's final bound (option "pq_merge_bound")
-	bool pq_fp8 = false;
+	bool pq_merge_bound = true;  // fast scan: the run merge skips keys above the scan's final bound (option "pq_merge_bound")
+	bool ivf_coarse_fused = true;      // IVF coarse search by coarse_kernels.hip (option "ivf_coarse" = fused | flat)
+	int64_t ivf_coarse_fallbacks = 0;  // passes the fused coarse search sent to the flat path
+	bool pq_fp8 = false;         // IVF_PQ ADC tables from e4m3 (fp8) queries (option "pq_query" = "fp8" | "f32")
 	bool ivf_flat_bound = true;  // IVF_FLAT list scan by MFMA bf16 lower bounds + certified exact re-rank (option "ivf_flat_scan" = "bound" | "exact")
-	int64_t ivf_flat_fallbacks = 0;  // batches the bound scan could not certify (rerun exactly)    // IVF_PQ ADC tables from e4m3 (fp8) queries (option "pq_query" = "fp8" | "f32")
+	int64_t ivf_flat_fallbacks = 0;  // batches the bound scan could not certify (rerun exactly)
 
 	int64_t last_stats[6] = {0, 0, 0, 0, 0, 0};
 

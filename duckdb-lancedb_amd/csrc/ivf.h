@@ -94,7 +94,10 @@ struct IvfState {
 	// fused coarse search (coarse_kernels.hip): per (query, partition) bounds, per-query fallback flags
 	DevBuf<float2> cbnd;
 	DevBuf<int> cflag;
-	std::vector<int> h_cflag;
+	// pinned, 2 x MAX_PASS_Q: the flags' copy is enqueued with the pass and read
+	// after its completion (two slots: two asynchronous searches in flight)
+	int *h_cflag = nullptr;
+	int cflag_slot = 0;
 	~IvfState();
 };
 
@@ -102,7 +105,9 @@ struct IvfState {
 // top-nprobe partitions of nq queries Q [nq][dim] (device, unpadded) over the
 // centroid rows C [nc][ld] f32, exact (the flat path's order and distances):
 // probe_l / probe_d [nq][nprobe], probe_c [nq]; flag[q] = 1 when query q must
-// take the flat path instead (non-finite bounds, candidate overflow).
+// take the flat path instead (non-finite bounds, candidate overflow); such a
+// query's probes are written as -1 / NaN / count 0, so the rest of the pass can
+// run before the host reads the flags.
 // bnd: nq * nc float2 scratch.
 bool coarse_fused_fits(int dim, int nc, int nprobe);
 void launch_coarse_search(const float *Q, int nq, int dim, const float *C, int ld, int nc, int metric, int nprobe,
@@ -118,8 +123,13 @@ void ivf_build(Index *ix, int type, int num_partitions, int num_sub_vectors);
 void ivf_set_model(Index *ix, int type, int nlist, int m, const float *centroids, const float *codebook);
 // lance_detached_compact (= optimize(All)): index the rows added since the build.
 void ivf_optimize(Index *ix);
-// Batched IVF search; device pointers, synchronous.
-void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refine, int64_t *dL, float *dD, int *dC);
+// Batched IVF search; device pointers.  Synchronous, unless `defer` is given
+// and the search is one pass: then everything is enqueued on the handle's
+// stream, defer->ivf is set, and ivf_finish completes it once the stream has
+// passed it (the fused coarse flags' check, a rerun on the flat coarse path).
+void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refine, int64_t *dL, float *dD, int *dC,
+                PendingPass *defer = nullptr);
+void ivf_finish(Index *ix, PendingPass &p);
 
 // Host copies of the model (centroids [nlist][dim], codebook [m][256][dsub]) and
 // of the per-slot list / codes (slots >= n_indexed: list -1, codes 0).

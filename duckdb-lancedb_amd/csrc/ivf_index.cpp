@@ -24,7 +24,10 @@
 
 namespace lhip {
 
-IvfState::~IvfState() { delete coarse; }
+IvfState::~IvfState() {
+	delete coarse;
+	if (h_cflag) (void)hipHostFree(h_cflag);
+}
 void ivf_free(IvfState *s) { delete s; }
 
 static StoreView store_view(Index *ix) {
@@ -473,7 +476,8 @@ static void account_list_scan(Index *ix, int esz, int nq, int lut_bytes) {
 	ix->kt_ivf_pair_rows += pair_rows;
 }
 
-void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refine, int64_t *dL, float *dD, int *dC) {
+void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refine, int64_t *dL, float *dD, int *dC,
+                PendingPass *defer) {
 	IvfState *s = ix->ivf;
 	hipStream_t st = ix->stream;
 	if (s->dirty) layout(ix);
@@ -498,214 +502,270 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 	                     k <= FL_KEYS - 1;
 	for (int q0 = 0; q0 < nq; q0 += pass) {
 		const int n = std::min(pass, nq - q0);
-		s->Qf.need((size_t)n * ld);
-		if (cos) s->Qn.need((size_t)n * dim);
-		launch_ivf_prep(dQ + (int64_t)q0 * dim, n, dim, ld, cos ? 1 : 0, s->Qf.p, cos ? s->Qn.p : nullptr, st);
-		// f64 queries for the exact f64 scans (tail, IVF_FLAT exact / fallback): made
-		// only when one of them runs (the IVF_PQ fast path never reads them)
-		bool qd_ready = false;
-		auto need_qd = [&]() {
-			if (qd_ready) return;
-			s->Qd.need((size_t)n * ld);
-			s->qn2.need((size_t)n);
-			launch_ivf_qd(s->Qf.p, n, ld, dim, s->Qd.p, s->qn2.p, st);
-			qd_ready = true;
-		};
-		HIPCHK(hipGetLastError());
-		HIPCHK(hipStreamSynchronize(st));
-		// coarse: exact top-nprobe partitions (synchronous on the centroid store's stream)
-		s->probe_l.need((size_t)n * nprobe);
-		s->probe_d.need((size_t)n * nprobe);
-		s->probe_c.need((size_t)n);
-		const auto tc0 = std::chrono::steady_clock::now();
-		const float *Qc = cos ? s->Qn.p : dQ + (int64_t)q0 * dim;
-		bool coarse_done = false;
-		if (ix->ivf_coarse_fused && coarse_fused_fits(dim, s->nlist, nprobe) && s->coarse->n_slots == s->nlist &&
-		    !s->coarse->xbf16) {
-			// two launches (f32 MFMA bounds, per-query select + exact refine); a query
-			// it cannot certify sends the batch to the flat path below
-			s->cbnd.need((size_t)n * s->nlist);
-			s->cflag.need((size_t)n);
-			launch_coarse_search(Qc, n, dim, static_cast<const float *>(s->coarse->X), s->coarse->ld, s->nlist,
-			                     s->coarse->metric, nprobe, s->cbnd.p, s->probe_l.p, s->probe_d.p, s->probe_c.p,
-			                     s->cflag.p, st);
+		bool fused = ix->ivf_coarse_fused && coarse_fused_fits(dim, s->nlist, nprobe) && s->coarse->n_slots == s->nlist &&
+		             !s->coarse->xbf16;
+		// one pass, asynchronous: the end wait and the flag check move to ivf_finish
+		const bool deferred = defer && n == nq;
+		for (;;) {  // (twice when the fused coarse search flagged a query: the second time on the flat path)
+			s->Qf.need((size_t)n * ld);
+			if (cos) s->Qn.need((size_t)n * dim);
+			launch_ivf_prep(dQ + (int64_t)q0 * dim, n, dim, ld, cos ? 1 : 0, s->Qf.p, cos ? s->Qn.p : nullptr, st);
+			// f64 queries for the exact f64 scans (tail, IVF_FLAT exact / fallback): made
+			// only when one of them runs (the IVF_PQ fast path never reads them)
+			bool qd_ready = false;
+			auto need_qd = [&]() {
+				if (qd_ready) return;
+				s->Qd.need((size_t)n * ld);
+				s->qn2.need((size_t)n);
+				launch_ivf_qd(s->Qf.p, n, ld, dim, s->Qd.p, s->qn2.p, st);
+				qd_ready = true;
+			};
 			HIPCHK(hipGetLastError());
-			s->h_cflag.resize((size_t)n);
-			HIPCHK(hipMemcpyAsync(s->h_cflag.data(), s->cflag.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, st));
-			spin_sync(st);
-			coarse_done = true;
-			for (int i = 0; i < n; ++i)
-				if (s->h_cflag[(size_t)i]) coarse_done = false;
-			if (!coarse_done) ix->ivf_coarse_fallbacks += 1;
-		}
-		if (!coarse_done)
-			s->coarse->search_device(Qc, n, nprobe, 1, s->probe_l.p, s->probe_d.p, s->probe_c.p);
-		if (ix->time_kernels)
-			ix->kt_ivf_coarse_ms +=
-			    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count();
-		ix->bind();
-		s->lcnt.need((size_t)s->nlist);
-		s->pstart.need((size_t)s->nlist + 1);
-		s->pairs.need((size_t)n * nprobe);
-		launch_invert(s->probe_l.p, n, nprobe, s->nlist, s->lcnt.p, s->pstart.p, s->pairs.p, st);
-		int64_t *oL = dL + (int64_t)q0 * k;
-		float *oD = dD + (int64_t)q0 * k;
-		int *oC = dC + q0;
-		if (tail_n > 0) {
-			need_qd();
-			s->tkeys.need((size_t)n * tail_nb * kk);
-			launch_flat_list_scan(sv, nullptr, nullptr, nullptr, nullptr, nullptr, tail_nb, nullptr, nullptr, 1, 1,
-			                      s->n_indexed, tail_n, n, s->Qd.p, s->qn2.p, kk, s->tkeys.p, st);
-		}
-		bool exact_flat = s->type == IVF_FLAT;
-		if (s->type == IVF_FLAT && lb_flat) {
-			// MFMA lower bounds per (query, item) -> top-M by bound -> exact
-			// re-rank with a certificate; an uncertified pass reruns exactly
-			const int nq_pad = (int)round_up(n, SCAN_BQ);
-			s->lbQf.need((size_t)nq_pad * ld);
-			s->lbQb.need((size_t)nq_pad * ld);
-			s->lbqaux.need((size_t)nq_pad);
-			launch_prep_queries(dQ + (int64_t)q0 * dim, n, dim, ld, nq_pad, s->metric, ix->max_alpha, ix->max_ux,
-			                    s->lbQf.p, s->lbQb.p, s->lbqaux.p, nullptr, st);
-			s->keys.need((size_t)n * nprobe * s->maxb * FL_KEYS);
-			ix->tic(0);
-			s->boff.need((size_t)s->nblk + 1);
-			s->btot.need(1);
-			s->live_bits.need((size_t)(ix->n_slots / 32 + 2));
-			launch_flat_list_lb(sv, s->blk_list.p, s->blk_pos0.p, s->lblk0.p, s->loff.p, s->lslot.p, s->nblk,
-			                    s->pstart.p, s->pairs.p, nprobe, s->maxb, s->lbQb.p, s->lbqaux.p, s->keys.p, st,
-			                    s->lrows_ok ? s->lrows.p : nullptr, s->lrows_ok ? s->lterms.p : nullptr, s->live_bits.p,
-			                    s->boff.p, s->btot.p);
-			ix->tic(1);
-			const int M = std::min(IVF_TOPK_CAP - 1, k + 32);
-			s->cand_a.need((size_t)n * M);
-			s->cut.need((size_t)n);
-			launch_flat_lb_merge(n, nprobe, s->probe_l.p, s->lblk0.p, s->maxb, s->keys.p, M, s->cand_a.p, s->cut.p, st);
-			if (tail_n > 0) {
-				s->cand_b.need((size_t)n * k);
-				launch_ivf_merge(n, 0, nullptr, nullptr, 1, kk, nullptr, tail_nb, s->tkeys.p, k, s->cand_b.p, st);
+			if (!fused) HIPCHK(hipStreamSynchronize(st));
+			// coarse: exact top-nprobe partitions (fused: on this stream; else synchronous on the
+			// centroid store's stream)
+			s->probe_l.need((size_t)n * nprobe);
+			s->probe_d.need((size_t)n * nprobe);
+			s->probe_c.need((size_t)n);
+			const auto tc0 = std::chrono::steady_clock::now();
+			const float *Qc = cos ? s->Qn.p : dQ + (int64_t)q0 * dim;
+			if (fused) {
+				// two launches (f32 MFMA bounds, per-query select + exact refine); the flags'
+				// copy is enqueued behind them and read once the pass has completed (no host
+				// wait here): a flagged query has no probes, and the pass reruns on the flat
+				// path below
+				s->cbnd.need((size_t)n * s->nlist);
+				s->cflag.need((size_t)n);
+				launch_coarse_search(Qc, n, dim, static_cast<const float *>(s->coarse->X), s->coarse->ld, s->nlist,
+				                     s->coarse->metric, nprobe, s->cbnd.p, s->probe_l.p, s->probe_d.p, s->probe_c.p,
+				                     s->cflag.p, st);
+				HIPCHK(hipGetLastError());
+				if (!s->h_cflag) HIPCHK(hipHostMalloc(&s->h_cflag, (size_t)2 * MAX_PASS_Q * sizeof(int)));
+				s->cflag_slot ^= 1;  // (the other slot may belong to a search still in flight)
+				HIPCHK(hipMemcpyAsync(s->h_cflag + (size_t)s->cflag_slot * MAX_PASS_Q, s->cflag.p, (size_t)n * sizeof(int),
+				                      hipMemcpyDeviceToHost, st));
+				if (ix->time_kernels) spin_sync(st);  // (the coarse time below is host-measured)
+			} else {
+				s->coarse->search_device(Qc, n, nprobe, 1, s->probe_l.p, s->probe_d.p, s->probe_c.p);
 			}
-			s->cert.need((size_t)n);
-			launch_flat_lb_refine(sv, s->Qf.p, s->cand_a.p, M, tail_n > 0 ? s->cand_b.p : nullptr, tail_n > 0 ? k : 0,
-			                      s->cut.p, n, k, oL, oD, oC, s->cert.p, st);
+			if (ix->time_kernels)
+				ix->kt_ivf_coarse_ms +=
+				    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count();
+			ix->bind_nodrain();  // (the coarse store's search may have switched the device; nothing to drain here)
+			s->lcnt.need((size_t)s->nlist);
+			s->pstart.need((size_t)s->nlist + 1);
+			s->pairs.need((size_t)n * nprobe);
+			launch_invert(s->probe_l.p, n, nprobe, s->nlist, s->lcnt.p, s->pstart.p, s->pairs.p, st);
+			int64_t *oL = dL + (int64_t)q0 * k;
+			float *oD = dD + (int64_t)q0 * k;
+			int *oC = dC + q0;
+			if (tail_n > 0) {
+				need_qd();
+				s->tkeys.need((size_t)n * tail_nb * kk);
+				launch_flat_list_scan(sv, nullptr, nullptr, nullptr, nullptr, nullptr, tail_nb, nullptr, nullptr, 1, 1,
+				                      s->n_indexed, tail_n, n, s->Qd.p, s->qn2.p, kk, s->tkeys.p, st);
+			}
+			bool exact_flat = s->type == IVF_FLAT;
+			if (s->type == IVF_FLAT && lb_flat) {
+				// MFMA lower bounds per (query, item) -> top-M by bound -> exact
+				// re-rank with a certificate; an uncertified pass reruns exactly
+				const int nq_pad = (int)round_up(n, SCAN_BQ);
+				s->lbQf.need((size_t)nq_pad * ld);
+				s->lbQb.need((size_t)nq_pad * ld);
+				s->lbqaux.need((size_t)nq_pad);
+				launch_prep_queries(dQ + (int64_t)q0 * dim, n, dim, ld, nq_pad, s->metric, ix->max_alpha, ix->max_ux,
+				                    s->lbQf.p, s->lbQb.p, s->lbqaux.p, nullptr, st);
+				s->keys.need((size_t)n * nprobe * s->maxb * FL_KEYS);
+				ix->tic(0);
+				s->boff.need((size_t)s->nblk + 1);
+				s->btot.need(1);
+				s->live_bits.need((size_t)(ix->n_slots / 32 + 2));
+				launch_flat_list_lb(sv, s->blk_list.p, s->blk_pos0.p, s->lblk0.p, s->loff.p, s->lslot.p, s->nblk,
+				                    s->pstart.p, s->pairs.p, nprobe, s->maxb, s->lbQb.p, s->lbqaux.p, s->keys.p, st,
+				                    s->lrows_ok ? s->lrows.p : nullptr, s->lrows_ok ? s->lterms.p : nullptr, s->live_bits.p,
+				                    s->boff.p, s->btot.p);
+				ix->tic(1);
+				const int M = std::min(IVF_TOPK_CAP - 1, k + 32);
+				s->cand_a.need((size_t)n * M);
+				s->cut.need((size_t)n);
+				launch_flat_lb_merge(n, nprobe, s->probe_l.p, s->lblk0.p, s->maxb, s->keys.p, M, s->cand_a.p, s->cut.p, st);
+				if (tail_n > 0) {
+					s->cand_b.need((size_t)n * k);
+					launch_ivf_merge(n, 0, nullptr, nullptr, 1, kk, nullptr, tail_nb, s->tkeys.p, k, s->cand_b.p, st);
+				}
+				s->cert.need((size_t)n);
+				launch_flat_lb_refine(sv, s->Qf.p, s->cand_a.p, M, tail_n > 0 ? s->cand_b.p : nullptr, tail_n > 0 ? k : 0,
+				                      s->cut.p, n, k, oL, oD, oC, s->cert.p, st);
+				HIPCHK(hipGetLastError());
+				s->h_cert.resize((size_t)n);
+				HIPCHK(hipMemcpyAsync(s->h_cert.data(), s->cert.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, st));
+				spin_sync(st);
+				exact_flat = false;
+				for (int i = 0; i < n; ++i)
+					if (!s->h_cert[(size_t)i]) exact_flat = true;
+				if (exact_flat) ix->ivf_flat_fallbacks += 1;
+				if (ix->time_kernels) account_list_scan(ix, 2, n, 0);
+			}
+			if (exact_flat) {
+				need_qd();
+				s->keys.need((size_t)n * nprobe * s->maxb * kk);
+				ix->tic(0);
+				launch_flat_list_scan(sv, s->blk_list.p, s->blk_pos0.p, s->lblk0.p, s->loff.p, s->lslot.p, s->nblk,
+				                      s->pstart.p, s->pairs.p, nprobe, s->maxb, 0, 0, n, s->Qd.p, s->qn2.p, kk, s->keys.p, st);
+				ix->tic(1);
+				s->cand_a.need((size_t)n * k);
+				launch_ivf_merge(n, nprobe, s->probe_l.p, s->lblk0.p, s->maxb, kk, s->keys.p, tail_nb,
+				                 tail_n > 0 ? s->tkeys.p : nullptr, k, s->cand_a.p, st);
+				launch_keys_to_output(s->cand_a.p, n, k, k, ix->dlabels, oL, oD, oC, st, ix->tie_desc);
+			} else if (s->type == IVF_FLAT) {
+				// bound scan certified every query of the pass
+			} else if (ix->pq_fast && s->m <= FQ_MAX_M && kp <= FQ_MAX_KK) {
+				// list-major 8-bit-LUT scan: FQ_G queries per LUT lookup, each probed
+				// list's codes streamed once per query group
+				const float *Qp = cos ? s->Qn.p : s->Qf.p;
+				const int qld = cos ? dim : ld;
+				if (ix->pq_fp8) {
+					s->Qq.need((size_t)n * qld);
+					launch_pq_query_fp8(Qp, qld, n, dim, s->Qq.p, st);
+					Qp = s->Qq.p;
+				}
+				s->P.need((size_t)n * s->m * PQ_K);
+				launch_pq_P(Qp, qld, n, s->codebook.p, s->m, s->dsub, s->P.p, st);
+				s->lut8.need((size_t)n * s->m * PQ_K);
+				s->qpar.need((size_t)2 * n);
+				launch_pq_lut_u8(s->P.p, n, s->m, s->metric == METRIC_DOT ? -1.0f : -2.0f, s->lut8.p,
+				                 reinterpret_cast<float2 *>(s->qpar.p), st);
+				s->item_off.need((size_t)s->nlist + 1);
+				s->xbeg.need(9);
+				int64_t maxpos = 0;
+				for (int l = 0; l < s->nlist; ++l) maxpos = std::max(maxpos, s->h_loff[(size_t)l + 1] - s->h_loff[(size_t)l]);
+				// items <= (query groups: n nprobe / FQ_G, + one partial group per list) x row chunks per list
+				const int64_t maxnc = (maxpos + FQ_CHUNK - 1) / FQ_CHUNK;
+				const int itab_cap = (int)std::min<int64_t>(((int64_t)n * nprobe / FQ_G + s->nlist) * std::max<int64_t>(maxnc, 1),
+				                                            (int64_t)1 << 28);
+				s->itab.need((size_t)2 * itab_cap);
+				launch_pq_fast_items(s->pstart.p, s->loff.p, s->pairs.p, s->nlist, s->item_off.p, s->xbeg.p, s->itab.p,
+				                     itab_cap, st);
+				const int ocap = (int)std::min<int64_t>((int64_t)1 << 30,
+				                                        (int64_t)nprobe * ((maxpos + FQ_CHUNK - 1) / FQ_CHUNK) * FQ_CAP);
+				s->okeys.need((size_t)n * ocap);
+				s->ocnt.need((size_t)n);
+				s->thrq.need((size_t)n);
+				s->work.need(8);
+				HIPCHK(hipMemsetAsync(s->ocnt.p, 0, (size_t)n * sizeof(int), st));
+				HIPCHK(hipMemsetAsync(s->thrq.p, 0xFF, (size_t)n * sizeof(uint64_t), st));
+				HIPCHK(hipMemsetAsync(s->work.p, 0, 8 * sizeof(int), st));
+				if (ix->pq_seed)
+					launch_pq_seed(s->lcodes.p, s->m, s->mp, s->loff.p, s->lslot.p, reinterpret_cast<const float *>(sv.rowaux),
+					               n, nprobe, s->probe_l.p, s->probe_d.p, s->metric == METRIC_DOT ? nullptr : s->ltau.p,
+					               s->lut8.p, reinterpret_cast<const float2 *>(s->qpar.p), kp, s->thrq.p, st);
+				ix->tic(0);
+				launch_pq_fast_scan(s->lcodes.p, s->m, s->mp, s->loff.p, s->lslot.p,
+				                    reinterpret_cast<const float *>(sv.rowaux), s->nlist, nprobe, s->pstart.p, s->pairs.p,
+				                    s->item_off.p, s->xbeg.p, s->probe_d.p, s->metric == METRIC_DOT ? nullptr : s->ltau.p, s->lut8.p,
+				                    reinterpret_cast<const float2 *>(s->qpar.p), kp, s->work.p, s->thrq.p, s->ocnt.p,
+				                    s->okeys.p, ocap, s->itab.p, scan_grid(1 << 20), st);
+				ix->tic(1);
+				s->cand_a.need((size_t)n * kp);
+				launch_pq_run_merge(s->okeys.p, s->ocnt.p, n, ocap, kp, s->cand_a.p, st,
+				                    ix->pq_merge_bound ? s->thrq.p : nullptr);
+				if (tail_n > 0) {
+					s->cand_b.need((size_t)n * k);
+					launch_ivf_merge(n, 0, nullptr, nullptr, 1, kk, nullptr, tail_nb, s->tkeys.p, k, s->cand_b.p, st);
+				}
+				launch_ivf_refine_final(sv, s->Qf.p, s->cand_a.p, kp, tail_n > 0 ? s->cand_b.p : nullptr,
+				                        tail_n > 0 ? k : 0, n, k, oL, oD, oC, st);
+			} else {
+				const float *Qp = cos ? s->Qn.p : s->Qf.p;
+				const int qld = cos ? dim : ld;
+				if (ix->pq_fp8) {
+					s->Qq.need((size_t)n * qld);
+					launch_pq_query_fp8(Qp, qld, n, dim, s->Qq.p, st);
+					Qp = s->Qq.p;
+				}
+				s->P.need((size_t)n * s->m * PQ_K);
+				launch_pq_P(Qp, qld, n, s->codebook.p, s->m, s->dsub, s->P.p, st);
+				const int S = pq_segments(n);
+				s->pref.need((size_t)n * (nprobe + 1));
+				launch_probe_prefix(s->probe_l.p, n, nprobe, s->loff.p, s->pref.p, st);
+				s->keys.need((size_t)n * S * kp);
+				ix->tic(0);
+				launch_pq_query_scan(s->lcodes.p, s->m, s->mp, s->loff.p, s->lslot.p,
+				                     reinterpret_cast<const float *>(sv.rowaux), n, nprobe, s->probe_l.p, s->probe_d.p,
+				                     s->metric == METRIC_DOT ? nullptr : s->ltau.p, s->P.p, s->pref.p, S, kp, s->keys.p, st);
+				ix->tic(1);
+				s->cand_a.need((size_t)n * kp);
+				// the S segment lists of each query: the merge kernel's tail mode ([q][S][kp])
+				launch_ivf_merge(n, 0, nullptr, nullptr, 1, kp, nullptr, S, s->keys.p, kp, s->cand_a.p, st);
+				if (tail_n > 0) {
+					s->cand_b.need((size_t)n * k);
+					launch_ivf_merge(n, 0, nullptr, nullptr, 1, kk, nullptr, tail_nb, s->tkeys.p, k, s->cand_b.p, st);
+				}
+				launch_ivf_refine_final(sv, s->Qf.p, s->cand_a.p, kp, tail_n > 0 ? s->cand_b.p : nullptr,
+				                        tail_n > 0 ? k : 0, n, k, oL, oD, oC, st);
+			}
 			HIPCHK(hipGetLastError());
-			s->h_cert.resize((size_t)n);
-			HIPCHK(hipMemcpyAsync(s->h_cert.data(), s->cert.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, st));
+			if (deferred) {
+				defer->ivf = true;
+				defer->ivf_fused = fused;
+				defer->ivf_flag_slot = s->cflag_slot;
+				defer->dQ = dQ;
+				defer->nq = nq;
+				defer->k = k;
+				defer->nprobes = nprobes;
+				defer->refine = refine;
+				defer->dL = dL;
+				defer->dD = dD;
+				defer->dC = dC;
+				return;
+			}
 			spin_sync(st);
-			exact_flat = false;
-			for (int i = 0; i < n; ++i)
-				if (!s->h_cert[(size_t)i]) exact_flat = true;
-			if (exact_flat) ix->ivf_flat_fallbacks += 1;
-			if (ix->time_kernels) account_list_scan(ix, 2, n, 0);
+			if (fused) {
+				bool flagged = false;
+				const int *fl = s->h_cflag + (size_t)s->cflag_slot * MAX_PASS_Q;
+				for (int i = 0; i < n; ++i) flagged = flagged || fl[i] != 0;
+				if (flagged) {
+					ix->ivf_coarse_fallbacks += 1;
+					fused = false;
+					continue;
+				}
+			}
+			if (ix->time_kernels && !(s->type == IVF_FLAT && lb_flat && !exact_flat))
+				account_list_scan(ix, s->type == IVF_FLAT ? (ix->xbf16 ? 2 : 4) : 0, n, fast_pq ? 1 : 4);
+			break;
 		}
-		if (exact_flat) {
-			need_qd();
-			s->keys.need((size_t)n * nprobe * s->maxb * kk);
-			ix->tic(0);
-			launch_flat_list_scan(sv, s->blk_list.p, s->blk_pos0.p, s->lblk0.p, s->loff.p, s->lslot.p, s->nblk,
-			                      s->pstart.p, s->pairs.p, nprobe, s->maxb, 0, 0, n, s->Qd.p, s->qn2.p, kk, s->keys.p, st);
-			ix->tic(1);
-			s->cand_a.need((size_t)n * k);
-			launch_ivf_merge(n, nprobe, s->probe_l.p, s->lblk0.p, s->maxb, kk, s->keys.p, tail_nb,
-			                 tail_n > 0 ? s->tkeys.p : nullptr, k, s->cand_a.p, st);
-			launch_keys_to_output(s->cand_a.p, n, k, k, ix->dlabels, oL, oD, oC, st, ix->tie_desc);
-		} else if (s->type == IVF_FLAT) {
-			// bound scan certified every query of the pass
-		} else if (ix->pq_fast && s->m <= FQ_MAX_M && kp <= FQ_MAX_KK) {
-			// list-major 8-bit-LUT scan: FQ_G queries per LUT lookup, each probed
-			// list's codes streamed once per query group
-			const float *Qp = cos ? s->Qn.p : s->Qf.p;
-			const int qld = cos ? dim : ld;
-			if (ix->pq_fp8) {
-				s->Qq.need((size_t)n * qld);
-				launch_pq_query_fp8(Qp, qld, n, dim, s->Qq.p, st);
-				Qp = s->Qq.p;
-			}
-			s->P.need((size_t)n * s->m * PQ_K);
-			launch_pq_P(Qp, qld, n, s->codebook.p, s->m, s->dsub, s->P.p, st);
-			s->lut8.need((size_t)n * s->m * PQ_K);
-			s->qpar.need((size_t)2 * n);
-			launch_pq_lut_u8(s->P.p, n, s->m, s->metric == METRIC_DOT ? -1.0f : -2.0f, s->lut8.p,
-			                 reinterpret_cast<float2 *>(s->qpar.p), st);
-			s->item_off.need((size_t)s->nlist + 1);
-			s->xbeg.need(9);
-			int64_t maxpos = 0;
-			for (int l = 0; l < s->nlist; ++l) maxpos = std::max(maxpos, s->h_loff[(size_t)l + 1] - s->h_loff[(size_t)l]);
-			// items <= (query groups: n nprobe / FQ_G, + one partial group per list) x row chunks per list
-			const int64_t maxnc = (maxpos + FQ_CHUNK - 1) / FQ_CHUNK;
-			const int itab_cap = (int)std::min<int64_t>(((int64_t)n * nprobe / FQ_G + s->nlist) * std::max<int64_t>(maxnc, 1),
-			                                            (int64_t)1 << 28);
-			s->itab.need((size_t)2 * itab_cap);
-			launch_pq_fast_items(s->pstart.p, s->loff.p, s->pairs.p, s->nlist, s->item_off.p, s->xbeg.p, s->itab.p,
-			                     itab_cap, st);
-			const int ocap = (int)std::min<int64_t>((int64_t)1 << 30,
-			                                        (int64_t)nprobe * ((maxpos + FQ_CHUNK - 1) / FQ_CHUNK) * FQ_CAP);
-			s->okeys.need((size_t)n * ocap);
-			s->ocnt.need((size_t)n);
-			s->thrq.need((size_t)n);
-			s->work.need(8);
-			HIPCHK(hipMemsetAsync(s->ocnt.p, 0, (size_t)n * sizeof(int), st));
-			HIPCHK(hipMemsetAsync(s->thrq.p, 0xFF, (size_t)n * sizeof(uint64_t), st));
-			HIPCHK(hipMemsetAsync(s->work.p, 0, 8 * sizeof(int), st));
-			if (ix->pq_seed)
-				launch_pq_seed(s->lcodes.p, s->m, s->mp, s->loff.p, s->lslot.p, reinterpret_cast<const float *>(sv.rowaux),
-				               n, nprobe, s->probe_l.p, s->probe_d.p, s->metric == METRIC_DOT ? nullptr : s->ltau.p,
-				               s->lut8.p, reinterpret_cast<const float2 *>(s->qpar.p), kp, s->thrq.p, st);
-			ix->tic(0);
-			launch_pq_fast_scan(s->lcodes.p, s->m, s->mp, s->loff.p, s->lslot.p,
-			                    reinterpret_cast<const float *>(sv.rowaux), s->nlist, nprobe, s->pstart.p, s->pairs.p,
-			                    s->item_off.p, s->xbeg.p, s->probe_d.p, s->metric == METRIC_DOT ? nullptr : s->ltau.p, s->lut8.p,
-			                    reinterpret_cast<const float2 *>(s->qpar.p), kp, s->work.p, s->thrq.p, s->ocnt.p,
-			                    s->okeys.p, ocap, s->itab.p, scan_grid(1 << 20), st);
-			ix->tic(1);
-			s->cand_a.need((size_t)n * kp);
-			launch_pq_run_merge(s->okeys.p, s->ocnt.p, n, ocap, kp, s->cand_a.p, st,
-			                    ix->pq_merge_bound ? s->thrq.p : nullptr);
-			if (tail_n > 0) {
-				s->cand_b.need((size_t)n * k);
-				launch_ivf_merge(n, 0, nullptr, nullptr, 1, kk, nullptr, tail_nb, s->tkeys.p, k, s->cand_b.p, st);
-			}
-			launch_ivf_refine_final(sv, s->Qf.p, s->cand_a.p, kp, tail_n > 0 ? s->cand_b.p : nullptr,
-			                        tail_n > 0 ? k : 0, n, k, oL, oD, oC, st);
-		} else {
-			const float *Qp = cos ? s->Qn.p : s->Qf.p;
-			const int qld = cos ? dim : ld;
-			if (ix->pq_fp8) {
-				s->Qq.need((size_t)n * qld);
-				launch_pq_query_fp8(Qp, qld, n, dim, s->Qq.p, st);
-				Qp = s->Qq.p;
-			}
-			s->P.need((size_t)n * s->m * PQ_K);
-			launch_pq_P(Qp, qld, n, s->codebook.p, s->m, s->dsub, s->P.p, st);
-			const int S = pq_segments(n);
-			s->pref.need((size_t)n * (nprobe + 1));
-			launch_probe_prefix(s->probe_l.p, n, nprobe, s->loff.p, s->pref.p, st);
-			s->keys.need((size_t)n * S * kp);
-			ix->tic(0);
-			launch_pq_query_scan(s->lcodes.p, s->m, s->mp, s->loff.p, s->lslot.p,
-			                     reinterpret_cast<const float *>(sv.rowaux), n, nprobe, s->probe_l.p, s->probe_d.p,
-			                     s->metric == METRIC_DOT ? nullptr : s->ltau.p, s->P.p, s->pref.p, S, kp, s->keys.p, st);
-			ix->tic(1);
-			s->cand_a.need((size_t)n * kp);
-			// the S segment lists of each query: the merge kernel's tail mode ([q][S][kp])
-			launch_ivf_merge(n, 0, nullptr, nullptr, 1, kp, nullptr, S, s->keys.p, kp, s->cand_a.p, st);
-			if (tail_n > 0) {
-				s->cand_b.need((size_t)n * k);
-				launch_ivf_merge(n, 0, nullptr, nullptr, 1, kk, nullptr, tail_nb, s->tkeys.p, k, s->cand_b.p, st);
-			}
-			launch_ivf_refine_final(sv, s->Qf.p, s->cand_a.p, kp, tail_n > 0 ? s->cand_b.p : nullptr,
-			                        tail_n > 0 ? k : 0, n, k, oL, oD, oC, st);
-		}
-		HIPCHK(hipGetLastError());
-		spin_sync(st);
-		if (ix->time_kernels && !(s->type == IVF_FLAT && lb_flat && !exact_flat))
-			account_list_scan(ix, s->type == IVF_FLAT ? (ix->xbf16 ? 2 : 4) : 0, n, fast_pq ? 1 : 4);
 	}
 }
 
 }  // namespace lhip
 
 namespace lhip {
+
+// completion of an asynchronous IVF search: the stream has passed it (its
+// event); a query the fused coarse search flagged reruns the whole search on
+// the flat coarse path (synchronously, behind anything enqueued since)
+void ivf_finish(Index *ix, PendingPass &p) {
+	IvfState *s = ix->ivf;
+	hipError_t e;
+	while ((e = hipEventQuery(ix->pb[p.slot].done)) == hipErrorNotReady) {
+	}
+	if (e != hipSuccess) throw Error(std::string("HIP error: ") + hipGetErrorString(e) + " at search completion");
+	if (!p.ivf_fused) return;
+	const int *fl = s->h_cflag + (size_t)p.ivf_flag_slot * MAX_PASS_Q;
+	bool flagged = false;
+	for (int i = 0; i < p.nq; ++i) flagged = flagged || fl[i] != 0;
+	if (!flagged) return;
+	ix->ivf_coarse_fallbacks += 1;
+	const bool f = ix->ivf_coarse_fused;
+	ix->ivf_coarse_fused = false;
+	try {
+		ivf_search(ix, p.dQ, p.nq, p.k, p.nprobes, p.refine, p.dL, p.dD, p.dC);
+	} catch (...) {
+		ix->ivf_coarse_fused = f;
+		throw;
+	}
+	ix->ivf_coarse_fused = f;
+}
 
 void Index::search_any(const float *dQ, int nq, int k, int nprobes, int refine, int64_t *dL, float *dD, int *dC) {
 	if (ivf)

@@ -3037,9 +3037,149 @@ __global__ __launch_bounds__(256) void pq_run_merge_kernel(const uint64_t *__res
 	for (int i = t; i < K; i += 256) out[(int64_t)q * K + i] = i < nout ? buf[i] : KEY64_NONE;
 }
 
+// The run merge with the scan's final bound (pq_merge_bound, the default), on
+// 1024 threads: the run's keys at or below thrq[q] are gathered into LDS; up
+// to RS_SORT of them are sorted directly, more (a bound that stayed loose: no
+// item of the query ever cut its buffer, so thrq is the seed's) go through a
+// radix select of the K-th smallest distance word (4 passes of 8 bits, wave 0
+// scans the 256 bins) and only the keys at or below that word are sorted.  A
+// gather past RS_CAP, or a tie group leaving more than RS_SORT keys at the
+// selected word, takes the streaming top-K over the whole run.  The output is
+// the same K keys as pq_run_merge_kernel's in every case.
+constexpr int RS_THREADS = 1024, RS_CAP = 8192, RS_SORT = 2048, RS_PT = RS_CAP / RS_THREADS;
+static_assert(IVF_TOPK_CAP <= RS_CAP && FQ_MAX_KK <= IVF_TOPK_CAP - RS_THREADS, "run select buffers");
+__global__ __launch_bounds__(RS_THREADS) void pq_run_select_kernel(const uint64_t *__restrict__ keys,
+                                                                   const int *__restrict__ ocnt, int ocap, int K,
+                                                                   uint64_t *__restrict__ out,
+                                                                   const uint64_t *__restrict__ thrq) {
+	__shared__ uint64_t buf[RS_CAP];
+	__shared__ unsigned hist[256];
+	__shared__ int s_cnt, s_n2;
+	__shared__ unsigned s_pre, s_rem;
+	__shared__ uint64_t s_thr;
+	const int q = blockIdx.x, t = threadIdx.x;
+	const int n = min(ocnt[q], ocap);
+	const uint64_t *src = keys + (int64_t)q * ocap;
+	const uint64_t bq = thrq[q];
+	if (t == 0) {
+		s_cnt = 0;
+		s_n2 = 0;
+		s_pre = 0;
+		s_rem = (unsigned)K;
+	}
+	__syncthreads();
+	for (int e0 = t; e0 < n; e0 += RS_THREADS * 4) {
+		uint64_t kv[4];
+#pragma unroll
+		for (int u = 0; u < 4; ++u) kv[u] = e0 + RS_THREADS * u < n ? src[e0 + RS_THREADS * u] : KEY64_NONE;
+#pragma unroll
+		for (int u = 0; u < 4; ++u)
+			if (kv[u] != KEY64_NONE && kv[u] <= bq) {
+				const int p = atomicAdd(&s_cnt, 1);
+				if (p < RS_CAP) buf[p] = kv[u];
+			}
+	}
+	__syncthreads();
+	const int c = s_cnt;
+	// buf[0, m) sorted, its first K out
+	auto emit_sorted = [&](int m) {
+		const int np = pow2_ceil(m);
+		for (int i = m + t; i < np; i += RS_THREADS) buf[i] = KEY64_NONE;
+		wg_bitonic_sort(buf, np);
+		const int nout = m < K ? m : K;
+		for (int i = t; i < K; i += RS_THREADS) out[(int64_t)q * K + i] = i < nout ? buf[i] : KEY64_NONE;
+	};
+	if (c <= RS_SORT) {
+		emit_sorted(c);
+		return;
+	}
+	if (c <= RS_CAP) {
+		uint32_t hw[RS_PT];
+		uint64_t kv[RS_PT];
+#pragma unroll
+		for (int j = 0; j < RS_PT; ++j) {
+			const int i = t + j * RS_THREADS;
+			kv[j] = i < c ? buf[i] : KEY64_NONE;
+			hw[j] = (uint32_t)(kv[j] >> 32);
+		}
+		unsigned mask = 0;
+		for (int sh = 24; sh >= 0; sh -= 8) {
+			if (t < 256) hist[t] = 0;
+			__syncthreads();
+			const unsigned pre = s_pre;
+#pragma unroll
+			for (int j = 0; j < RS_PT; ++j)
+				if (t + j * RS_THREADS < c && (hw[j] & mask) == pre) atomicAdd(&hist[(hw[j] >> sh) & 255], 1u);
+			__syncthreads();
+			if (t < 64) {
+				const unsigned rem = s_rem;
+				unsigned h4[4], cs = 0;
+#pragma unroll
+				for (int u = 0; u < 4; ++u) {
+					h4[u] = hist[4 * t + u];
+					cs += h4[u];
+				}
+				unsigned x = cs;
+#pragma unroll
+				for (int o = 1; o < 64; o <<= 1) {
+					const unsigned y = __shfl_up(x, o, 64);
+					if (t >= o) x += y;
+				}
+				unsigned ex = x - cs;
+				if (ex < rem && rem <= x) {
+#pragma unroll
+					for (int u = 0; u < 4; ++u) {
+						if (rem <= ex + h4[u]) {
+							s_pre = pre | ((unsigned)(4 * t + u) << sh);
+							s_rem = rem - ex;
+							break;
+						}
+						ex += h4[u];
+					}
+				}
+			}
+			mask |= 255u << sh;
+			__syncthreads();
+		}
+		// T: the K-th smallest distance word (K < c); at least K keys lie at or
+		// below it and every key above it has K smaller ones
+		const uint32_t T = s_pre;
+#pragma unroll
+		for (int j = 0; j < RS_PT; ++j)
+			if (t + j * RS_THREADS < c && hw[j] <= T) {
+				const int p = atomicAdd(&s_n2, 1);
+				if (p < RS_SORT) buf[p] = kv[j];
+			}
+		__syncthreads();
+		const int m2 = s_n2;
+		if (m2 <= RS_SORT) {
+			emit_sorted(m2);
+			return;
+		}
+	}
+	// streaming top-K over the whole run from the bound (buf as its buffer)
+	__syncthreads();
+	if (t == 0) {
+		s_cnt = 0;
+		s_thr = bq == KEY64_NONE ? KEY64_NONE : bq + 1;  // (offer keeps key < thr)
+	}
+	__syncthreads();
+	TopK tk{buf, &s_cnt, &s_thr, K};
+	for (int e0 = 0; e0 < n; e0 += RS_THREADS) {
+		const int e = e0 + t;
+		const uint64_t k = e < n ? src[e] : KEY64_NONE;
+		tk.offer(k, k != KEY64_NONE);
+	}
+	const int nout = tk.finish();
+	for (int i = t; i < K; i += RS_THREADS) out[(int64_t)q * K + i] = i < nout ? buf[i] : KEY64_NONE;
+}
+
 void launch_pq_run_merge(const uint64_t *keys, const int *ocnt, int nq, int ocap, int K, uint64_t *out,
                          hipStream_t st, const uint64_t *thrq) {
-	pq_run_merge_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(keys, ocnt, ocap, K, out, thrq);
+	if (thrq && K <= FQ_MAX_KK)
+		pq_run_select_kernel<<<dim3((unsigned)nq), RS_THREADS, 0, st>>>(keys, ocnt, ocap, K, out, thrq);
+	else
+		pq_run_merge_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(keys, ocnt, ocap, K, out, thrq);
 }
 
 // ---------------------------------------------------------------------------

@@ -416,11 +416,12 @@ void launch_prep_queries(const float *Q, int nq, int dim, int ld, int nq_pad, in
 // S is the same for every query of the batch (scan8_kernel relies on it).
 // slack: f32 evaluation of the five-term sum, every intermediate bounded by
 // max_alpha + |q|^2 + 4 max_x (|q| + |e_q|) (max_x = max over rows of xn, ux).
-__global__ __launch_bounds__(256) void query_absmax_kernel(const float *__restrict__ Q, int nq, int dim, int metric,
-                                                           float2 *__restrict__ qm) {
-	__shared__ float redm[4];
-	__shared__ double reds[4];
-	const int q = blockIdx.x, t = threadIdx.x;
+// (max|v_i|, |q|) of query q by the block (all threads call; every thread gets
+// the result): one code path for query_absmax_kernel and the fused prep, so
+// both give the same bits
+__device__ __forceinline__ float2 query_absmax_block(const float *__restrict__ Q, int q, int dim, int metric,
+                                                     float *redm, double *reds) {
+	const int t = threadIdx.x;
 	float m = 0.f;
 	double s2 = 0.0;
 	for (int i = t; i < dim; i += 256) {
@@ -436,11 +437,19 @@ __global__ __launch_bounds__(256) void query_absmax_kernel(const float *__restri
 		reds[t >> 6] = s2;
 	}
 	__syncthreads();
-	if (t != 0) return;
 	m = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
 	const double qn = sqrt(reds[0] + reds[1] + reds[2] + reds[3]);
+	__syncthreads();  // (redm / reds are reused by the next call)
 	const float mv = metric == METRIC_COSINE ? (qn > 0.0 ? (float)((double)m / qn) : 0.f) : m;
-	qm[q] = make_float2(mv, (float)qn);
+	return make_float2(mv, (float)qn);
+}
+
+__global__ __launch_bounds__(256) void query_absmax_kernel(const float *__restrict__ Q, int nq, int dim, int metric,
+                                                           float2 *__restrict__ qm) {
+	__shared__ float redm[4];
+	__shared__ double reds[4];
+	const float2 r = query_absmax_block(Q, blockIdx.x, dim, metric, redm, reds);
+	if (threadIdx.x == 0) qm[blockIdx.x] = r;
 }
 
 __global__ __launch_bounds__(256) void prep_queries_i8_kernel(const float *__restrict__ Q, int nq, int dim, int ld,
@@ -455,14 +464,26 @@ __global__ __launch_bounds__(256) void prep_queries_i8_kernel(const float *__res
 	if (zero3 && t < 3 && q < nq) zero3[t * nq + q] = 0;
 	// the batch scale: max over every query's max|v_i|
 	float m = 0.f;
-	for (int i = t; i < nq; i += 256) m = fmaxf(m, qm[i].x);
+	double qn0 = 0.0;  // (|q| rounded to f32: only scales v below)
+	if (qm) {
+		for (int i = t; i < nq; i += 256) m = fmaxf(m, qm[i].x);
 #pragma unroll
-	for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-	if ((t & 63) == 0) redm[t >> 6] = m;
-	__syncthreads();
-	m = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
+		for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+		if ((t & 63) == 0) redm[t >> 6] = m;
+		__syncthreads();
+		m = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
+		if (q < nq) qn0 = (double)qm[q].y;
+	} else {
+		// fused (a few queries: one launch instead of two): every block computes
+		// every query's (max|v_i|, |q|) itself, with query_absmax_kernel's code
+		__shared__ double reds[4];
+		for (int j = 0; j < nq; ++j) {
+			const float2 r = query_absmax_block(Q, j, dim, metric, redm, reds);
+			m = fmaxf(m, r.x);
+			if (j == q) qn0 = (double)r.y;
+		}
+	}
 	const bool cosine = metric == METRIC_COSINE;
-	const double qn0 = q < nq ? (double)qm[q].y : 0.0;  // (|q| rounded to f32: only scales v below)
 	const float sq = m / 127.0f;
 	const double inv = m > 0.f ? 127.0 / (double)m : 0.0;
 	double s2 = 0.0, e2 = 0.0;
@@ -515,8 +536,13 @@ __global__ __launch_bounds__(256) void prep_queries_i8_kernel(const float *__res
 void launch_prep_queries_i8(const float *Q, int nq, int dim, int ld, int nq_pad, int metric, float max_alpha,
                             float max_x, float2 *qm, float *Qf, uint16_t *Qb, float4 *qaux, int *zero3,
                             hipStream_t st) {
-	if (nq > 0) query_absmax_kernel<<<dim3(nq), dim3(256), 0, st>>>(Q, nq, dim, metric, qm);
-	prep_queries_i8_kernel<<<dim3(nq_pad), dim3(256), 0, st>>>(Q, nq, dim, ld, metric, max_alpha, max_x, qm, Qf,
+	// up to PREP_FUSE_Q queries (DuckDB's one query per call): one launch, each
+	// block reading the few query rows itself
+	constexpr int PREP_FUSE_Q = 8;
+	const bool fuse = nq <= PREP_FUSE_Q;
+	if (nq > 0 && !fuse) query_absmax_kernel<<<dim3(nq), dim3(256), 0, st>>>(Q, nq, dim, metric, qm);
+	prep_queries_i8_kernel<<<dim3(nq_pad), dim3(256), 0, st>>>(Q, nq, dim, ld, metric, max_alpha, max_x,
+	                                                              fuse ? nullptr : qm, Qf,
 	                                                              reinterpret_cast<int8_t *>(Qb), qaux, zero3);
 }
 

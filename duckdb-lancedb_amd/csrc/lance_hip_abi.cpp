@@ -476,6 +476,30 @@ void Index::finish_chunk(PendingPass &p) {
 int64_t Index::search_async(const float *dQ, int nq, int k, int nprobes, int refine, int64_t *dL, float *dD,
                             int *dC) {
 	const int64_t ticket = next_ticket++;
+	if (ivf && !filter_on && !time_kernels && nq <= MAX_PASS_Q) {
+		// IVF: the whole search enqueued on the handle's stream (its kernels run in
+		// stream order behind the previous search's, which shares the workspace),
+		// the end wait and the coarse flags' check at ivf_finish.  A search whose
+		// shape differs from the pending ones' drains them first (its workspace
+		// may grow: no buffer is reallocated under a search in flight).
+		while (pending.size() >= 2) finish_oldest();
+		if (!pending.empty()) {
+			const PendingPass &b = pending.back();
+			if (!b.ivf || b.nq != nq || b.k != k || b.nprobes != nprobes || b.refine != refine) drain();
+		}
+		for (auto &v : last_stats) v = 0;
+		PendingPass p;
+		p.slot = pb_free_slot();
+		ivf_search(this, dQ, nq, k, nprobes, refine, dL, dD, dC, &p);
+		if (!p.ivf) return ticket;  // (completed: more than one pass)
+		PassBufs &P = pb[p.slot];
+		if (!P.done) HIPCHK(hipEventCreateWithFlags(&P.done, hipEventDisableTiming));
+		HIPCHK(hipEventRecord(P.done, stream));
+		p.async = true;
+		p.ticket = ticket;
+		pending.push_back(p);
+		return ticket;
+	}
 	const bool asyncable = !ivf && !filter_on && !time_kernels && nq <= MAX_PASS_Q && n_slots > 65536 &&
 	                       !(small_exact && small_exact_fits(n_slots, dim, nq, k));
 	if (!asyncable) {
@@ -505,7 +529,10 @@ int64_t Index::search_async(const float *dQ, int nq, int k, int nprobes, int ref
 void Index::finish_oldest() {
 	PendingPass p = pending.front();
 	pending.pop_front();
-	finish_chunk(p);
+	if (p.ivf)
+		ivf_finish(this, p);
+	else
+		finish_chunk(p);
 }
 
 void Index::wait_ticket(int64_t ticket) {

@@ -17,7 +17,9 @@
 // as Serialize / LoadFromStorage :492-587).  Multi-column rows go through the
 // Arrow C Data Interface as DuckDB's ArrowConverter hands them over
 // (lance_index.cpp:322-360).
+#include <algorithm>
 #include <cerrno>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -609,6 +611,33 @@ static int run_script(const char *path) {
 				write_file(out, D.data(), D.size() * 4, true);
 				write_file(out, C.data(), C.size() * 4, true);
 				std::printf("bulk_search %d\n", nq);
+			} else if (op == "time_percall") {
+				// lance_search()'s one-Search-per-query pattern timed from C++ (no
+				// Python in the loop): `settle` untimed calls (the GPU clock ramp),
+				// then `reps` passes over the nq queries
+				std::string qf;
+				int nq, k, settle, reps;
+				is >> qf >> nq >> k >> settle >> reps;
+				const int d = ix->dim;
+				auto b = read_file(qf, (size_t)nq * d * sizeof(float));
+				const float *Q = reinterpret_cast<const float *>(b.data());
+				size_t got = 0;
+				for (int i = 0; i < settle; ++i) got += ix->Search(Q + (size_t)(i % nq) * d, d, k, pred).size();
+				std::vector<double> per;
+				per.reserve((size_t)nq * reps);
+				const auto t0 = std::chrono::steady_clock::now();
+				auto tp = t0;
+				for (int r = 0; r < reps; ++r)
+					for (int i = 0; i < nq; ++i) {
+						got += ix->Search(Q + (size_t)i * d, d, k, pred).size();
+						const auto tn = std::chrono::steady_clock::now();
+						per.push_back(std::chrono::duration<double, std::micro>(tn - tp).count());
+						tp = tn;
+					}
+				const double s = std::chrono::duration<double>(tp - t0).count();
+				std::sort(per.begin(), per.end());
+				std::printf("time_percall %zu %.6f %.3f %.3f %zu\n", per.size(), s, 1e6 * s / (double)per.size(),
+				            per[per.size() / 2], got);
 			} else {
 				throw std::runtime_error("unknown op " + op);
 			}

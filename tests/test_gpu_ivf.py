@@ -333,3 +333,106 @@ def test_fused_coarse_search_equals_flat(hip, mk, metric):
     hip.LanceHipSetOption(h, "ivf_coarse", "flat")
     b = hip.LanceDetachedSearchBatch(h, Qn, 10, nprobes=16)
     np.testing.assert_array_equal(a[0], b[0])
+
+
+@pytest.mark.parametrize("itype", ["ivf_pq", "ivf_flat"])
+def test_fused_coarse_flag_reruns_the_pass(hip, mk, itype):
+    """The fused coarse search's flags are read only after the whole pass has
+    run (round 6: no host wait between the coarse search and the list scans).
+    A flagged query (NaN) leaves no probes, so the pass runs harmlessly and is
+    then rerun on the flat coarse path: every query's result equals the flat
+    path's, the good queries' and the NaN query's alike, batch after batch."""
+    rng = np.random.default_rng(93)
+    n, d, nlist = 12_000, 64, 128
+    X = clustered(rng, n, d, centers=32)
+    Q = (X[rng.choice(n, 40, replace=False)] + 0.3 * rng.standard_normal((40, d))).astype(np.float32)
+    h = mk(d, "l2", itype)
+    hip.LanceDetachedAddBatch(h, X, n, d)
+    hip.LanceDetachedCreateIndex(h, nlist, 16 if itype == "ivf_pq" else 0)
+    for bad in (None, 5, None, 0):
+        Qb = Q.copy()
+        if bad is not None:
+            Qb[bad] = np.nan
+        for nprobe in (8, 128):
+            hip.LanceHipSetOption(h, "ivf_coarse", "fused")
+            a = hip.LanceDetachedSearchBatch(h, Qb, 10, nprobes=nprobe, refine_factor=2)
+            hip.LanceHipSetOption(h, "ivf_coarse", "flat")
+            b = hip.LanceDetachedSearchBatch(h, Qb, 10, nprobes=nprobe, refine_factor=2)
+            np.testing.assert_array_equal(a[2], b[2])
+            np.testing.assert_array_equal(a[0], b[0])
+            np.testing.assert_allclose(a[1], b[1], rtol=0, atol=0, equal_nan=True)
+
+
+@pytest.mark.parametrize("seed", ["1", "0"])
+def test_pq_run_merge_bound_paths_equal(hip, mk, seed):
+    """The run merge with the scan's final bound (pq_merge_bound = 1, the
+    default: direct sort of up to 2048 keys at or below the bound, a radix
+    select of the K-th distance word past that, the streaming top-K past 8192)
+    returns the same lists as the streaming merge over the whole run
+    (pq_merge_bound = 0), and the oracle's.  Without the seed (pq_seed = 0) a
+    query whose items never cut its buffer keeps an unbounded thrq, so every
+    probed row reaches the merge: nprobe 4 / 16 / 40 / 128 over ~310-row lists
+    span the three regimes."""
+    rng = np.random.default_rng(95)
+    n, d, nlist = 40_000, 64, 128
+    X = clustered(rng, n, d, centers=32)
+    Q = (X[rng.choice(n, 48, replace=False)] + 0.3 * rng.standard_normal((48, d))).astype(np.float32)
+    h = mk(d, "l2", "ivf_pq")
+    hip.LanceDetachedAddBatch(h, X, n, d)
+    hip.LanceDetachedCreateIndex(h, nlist, 16)
+    hip.LanceHipSetOption(h, "pq_seed", seed)
+    for nprobe, rf in [(4, 2), (16, 10), (40, 10), (128, 51)]:
+        res = {}
+        for mb in ("1", "0"):
+            hip.LanceHipSetOption(h, "pq_merge_bound", mb)
+            res[mb] = hip.LanceDetachedSearchBatch(h, Q, 10, nprobes=nprobe, refine_factor=rf)
+        for x, y in zip(res["1"], res["0"]):
+            np.testing.assert_array_equal(x, y, err_msg=f"nprobe {nprobe}")
+        el, ed, ec = oracle_search(hip, h, X, Q, 10, nprobe, rf, "l2")
+        assert_same(*res["1"], el, ed, ec)
+    hip.LanceHipSetOption(h, "pq_merge_bound", "1")
+
+
+@pytest.mark.parametrize("itype", ["ivf_pq", "ivf_flat"])
+def test_ivf_async_two_in_flight(hip, mk, itype):
+    """lance_hip_search_batch_device_async on an IVF handle (round 6): the whole
+    search is enqueued on the handle's stream, two searches in flight sharing
+    the IVF workspace in stream order, the fused coarse flags read at the wait.
+    Batches: plain, one with a NaN query (its flag reruns that search on the
+    flat coarse path while the next search is already queued behind it), a
+    different batch size (drains first: the workspace may grow), and a
+    different nprobes.  Every batch equals the synchronous search."""
+    import torch
+    from lance_hip.sharded import AsyncPipeline, hip_device_search
+
+    rng = np.random.default_rng(97)
+    n, d, nlist, k = 20_000, 64, 96, 10
+    X = clustered(rng, n, d, centers=32)
+    h = mk(d, "l2", itype)
+    hip.LanceDetachedAddBatch(h, X, n, d)
+    hip.LanceDetachedCreateIndex(h, nlist, 16 if itype == "ivf_pq" else 0)
+    L = hip.lib()
+
+    def batch(nq, nan_at=None):
+        Q = (X[rng.choice(n, nq, replace=False)] + 0.3 * rng.standard_normal((nq, d))).astype(np.float32)
+        if nan_at is not None:
+            Q[nan_at] = np.nan
+        return torch.from_numpy(Q).cuda()
+
+    for nprobe in (8, 20):
+        pipe = AsyncPipeline(L, h, d, nprobes=nprobe, refine_factor=3)
+        sync = hip_device_search(L, h, d, nprobes=nprobe, refine_factor=3)
+        Qs = [batch(64), batch(64, nan_at=7), batch(64), batch(40), batch(64, nan_at=0), batch(64)]
+        outs = []
+        for q in Qs:  # batch i enqueued, then batch i - 1 completed (its outputs copied out at once)
+            r = pipe.step(q, k)
+            if r is not None:
+                outs.append(tuple(x.cpu().numpy() for x in r))
+        outs.append(tuple(x.cpu().numpy() for x in pipe.drain()))
+        assert len(outs) == len(Qs)
+        for i, q in enumerate(Qs):
+            e = tuple(x.cpu().numpy() for x in sync(q, k))
+            g = outs[i]
+            np.testing.assert_array_equal(g[2], e[2], err_msg=f"batch {i}")
+            np.testing.assert_array_equal(g[0], e[0], err_msg=f"batch {i}")
+            np.testing.assert_allclose(g[1], e[1], rtol=0, atol=0, equal_nan=True, err_msg=f"batch {i}")

@@ -21,8 +21,10 @@ for r in rows:
 # steps start at ivf_prep (IVF configs) or else query_absmax (int8 path) / prep_queries
 if any(s[0].startswith("ivf_prep_kernel") for s in seq):
     starts = [i for i, s in enumerate(seq) if s[0].startswith("ivf_prep_kernel")]
-else:
+elif any(s[0].startswith("query_absmax") for s in seq):
     starts = [i for i, s in enumerate(seq) if s[0].startswith("query_absmax") or s[0].startswith("prep_queries_kernel")]
+else:  # (a few queries per call: the int8 prep is one fused launch)
+    starts = [i for i, s in enumerate(seq) if s[0].startswith("prep_queries")]
 steps = [seq[a:b] for a, b in zip(starts, starts[1:] + [len(seq)])][-last:]
 for st in steps:
     npr = 0
