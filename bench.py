@@ -102,6 +102,8 @@ def parse():
                          "flight (the synchronous figure is reported beside the pipelined one either way)")
     ap.add_argument("--no-host-batch", action="store_true",
                     help="N = 1 flat configs: skip the extra host-buffer leg (H2D + D2H timed, SURVEY.md §8d QPS)")
+    ap.add_argument("--no-sync-leg", action="store_true",
+                    help="IVF configs: skip the extra synchronous-call leg (kernel traces of the pipelined steps)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: ranks join a gloo group and time a CPU stand-in step "
                          "through the same barrier / max-over-ranks code (tests/test_bench_launcher_cpu.py)")
@@ -516,7 +518,7 @@ def main_ivf(a):
     if pipelined:
         res = tuple(x.clone() for x in last_out[0])
     sync_leg = None
-    if pipelined and world == 1:
+    if pipelined and world == 1 and not a.no_sync_leg:
         # the synchronous call beside it (one lance_hip_search_batch_device per batch)
         ts, rs, _ = timed_steps(lambda: searcher.search(Q, K, reuse_outputs=True), a.steps, a.warmup, None, dev,
                                 torch.cuda.synchronize)

@@ -290,6 +290,7 @@ struct Index {
 	uint64_t ivf_seed = 0x5eedULL;
 	bool pq_fast = true;    // IVF_PQ list-major 8-bit-LUT scan (option "pq_scan" = "fast"; "exact_lut": f32 LUT, query-major)
 	bool pq_seed = true;    // fast scan: per-query bound seeded from the nearest probed list (option "pq_seed")
+	bool pq_lut_fused = true;    // fast scan: fp8 + ADC table + 8-bit LUT in one launch (option "pq_lut" = fused | split)
 	bool pq_merge_bound = true;  // fast scan: the run merge skips keys above the scan's final bound (option "pq_merge_bound")
 	bool ivf_coarse_fused = true;      // IVF coarse search by coarse_kernels.hip (option "ivf_coarse" = fused | flat)
 	int64_t ivf_coarse_fallbacks = 0;  // passes the fused coarse search sent to the flat path

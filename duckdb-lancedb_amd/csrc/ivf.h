@@ -175,8 +175,12 @@ void launch_pq_layout(const uint8_t *codes, const uint32_t *lslot, int64_t npos,
                       hipStream_t st);
 // search side
 void launch_ivf_prep(const float *Q, int nq, int dim, int ld, int normalize, float *Qf, float *Qn, hipStream_t st);
+// probes -> per-list query sets (pstart [nlist + 1], pairs).  With loff (needs
+// invert_fused_fits): also the fast scan's item_off / xbeg, as launch_pq_fast_items
+// would lay them out (then call it with offsets_done)
+bool invert_fused_fits(int nlist);
 void launch_invert(const int64_t *probe_l, int nq, int nprobe, int nlist, int *lcnt, int *pstart, int *pairs,
-                   hipStream_t st);
+                   hipStream_t st, const int64_t *loff = nullptr, int *item_off = nullptr, int *xbeg = nullptr);
 void launch_flat_list_scan(const StoreView &s, const int *blk_list, const int64_t *blk_pos0, const int *lblk0,
                            const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart, const int *pairs,
                            int nprobe, int maxb, int64_t tail_s0, int64_t tail_n, int nq, const double *Qd,
@@ -217,11 +221,16 @@ void launch_pq_query_scan(const uint8_t *lcodes, int m, int mp, const int64_t *l
 void launch_pq_query_fp8(const float *Q, int qld, int nq, int dim, float *Qo, hipStream_t st);
 // 8-bit LUTs lut8 [nq][m][256] and qpar [nq] = (D, L0) from P (see pq_lut_u8_kernel)
 void launch_pq_lut_u8(const float *P, int nq, int m, float sP, uint8_t *lut8, float2 *qpar, hipStream_t st);
+// fp8 rounding (fp8 != 0) + ADC table + 8-bit LUT of each query in one launch
+// (pq_query_fp8 + pq_P + pq_lut_u8, bit-identical); Q [nq][qld], dim = m * dsub
+bool pq_lut_fused_fits(int m, int dim);
+void launch_pq_lut_fused(const float *Q, int qld, int nq, int dim, int fp8, const float *cb, int m, int dsub, float sP,
+                         uint8_t *lut8, float2 *qpar, hipStream_t st);
 // item_off [nlist+1]: work items of the fast scan per list (query groups x row chunks), lists in
 // XCD-major order; xbeg [9]: each XCD's item range
 // itab [2 x items] (when non-null): per item (list, row chunk, -, -), (pair ids of its query group)
 void launch_pq_fast_items(const int *pstart, const int64_t *loff, const int *pairs, int nlist, int *item_off,
-                          int *xbeg, int4 *itab, int itab_cap, hipStream_t st);
+                          int *xbeg, int4 *itab, int itab_cap, hipStream_t st, bool offsets_done = false);
 // per query: the kk-th smallest fast-scan key of its nearest probed list -> thrq (atomicMin)
 void launch_pq_seed(const uint8_t *lcodes, int m, int mp, const int64_t *loff, const uint32_t *lslot,
                     const float *rowaux_f, int nq, int nprobe, const int64_t *probe_l, const float *probe_d,

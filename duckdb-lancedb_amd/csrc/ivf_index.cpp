@@ -555,7 +555,15 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 			s->lcnt.need((size_t)s->nlist);
 			s->pstart.need((size_t)s->nlist + 1);
 			s->pairs.need((size_t)n * nprobe);
-			launch_invert(s->probe_l.p, n, nprobe, s->nlist, s->lcnt.p, s->pstart.p, s->pairs.p, st);
+			// (fast PQ scan: the invert also lays out the scan's work items)
+			const bool items_in_invert = fast_pq && invert_fused_fits(s->nlist);
+			if (items_in_invert) {
+				s->item_off.need((size_t)s->nlist + 1);
+				s->xbeg.need(9);
+			}
+			launch_invert(s->probe_l.p, n, nprobe, s->nlist, s->lcnt.p, s->pstart.p, s->pairs.p, st,
+			              items_in_invert ? s->loff.p : nullptr, items_in_invert ? s->item_off.p : nullptr,
+			              items_in_invert ? s->xbeg.p : nullptr);
 			int64_t *oL = dL + (int64_t)q0 * k;
 			float *oD = dD + (int64_t)q0 * k;
 			int *oC = dC + q0;
@@ -624,17 +632,22 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 				// list's codes streamed once per query group
 				const float *Qp = cos ? s->Qn.p : s->Qf.p;
 				const int qld = cos ? dim : ld;
-				if (ix->pq_fp8) {
-					s->Qq.need((size_t)n * qld);
-					launch_pq_query_fp8(Qp, qld, n, dim, s->Qq.p, st);
-					Qp = s->Qq.p;
-				}
-				s->P.need((size_t)n * s->m * PQ_K);
-				launch_pq_P(Qp, qld, n, s->codebook.p, s->m, s->dsub, s->P.p, st);
+				const float sP = s->metric == METRIC_DOT ? -1.0f : -2.0f;
 				s->lut8.need((size_t)n * s->m * PQ_K);
 				s->qpar.need((size_t)2 * n);
-				launch_pq_lut_u8(s->P.p, n, s->m, s->metric == METRIC_DOT ? -1.0f : -2.0f, s->lut8.p,
-				                 reinterpret_cast<float2 *>(s->qpar.p), st);
+				if (ix->pq_lut_fused && s->m * s->dsub == dim && pq_lut_fused_fits(s->m, dim)) {
+					launch_pq_lut_fused(Qp, qld, n, dim, ix->pq_fp8 ? 1 : 0, s->codebook.p, s->m, s->dsub, sP, s->lut8.p,
+					                    reinterpret_cast<float2 *>(s->qpar.p), st);
+				} else {
+					if (ix->pq_fp8) {
+						s->Qq.need((size_t)n * qld);
+						launch_pq_query_fp8(Qp, qld, n, dim, s->Qq.p, st);
+						Qp = s->Qq.p;
+					}
+					s->P.need((size_t)n * s->m * PQ_K);
+					launch_pq_P(Qp, qld, n, s->codebook.p, s->m, s->dsub, s->P.p, st);
+					launch_pq_lut_u8(s->P.p, n, s->m, sP, s->lut8.p, reinterpret_cast<float2 *>(s->qpar.p), st);
+				}
 				s->item_off.need((size_t)s->nlist + 1);
 				s->xbeg.need(9);
 				int64_t maxpos = 0;
@@ -645,7 +658,7 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 				                                            (int64_t)1 << 28);
 				s->itab.need((size_t)2 * itab_cap);
 				launch_pq_fast_items(s->pstart.p, s->loff.p, s->pairs.p, s->nlist, s->item_off.p, s->xbeg.p, s->itab.p,
-				                     itab_cap, st);
+				                     itab_cap, st, items_in_invert);
 				const int ocap = (int)std::min<int64_t>((int64_t)1 << 30,
 				                                        (int64_t)nprobe * ((maxpos + FQ_CHUNK - 1) / FQ_CHUNK) * FQ_CAP);
 				s->okeys.need((size_t)n * ocap);

@@ -920,9 +920,157 @@ __global__ void invert_fill_kernel(const int64_t *__restrict__ probe_l, int n, c
 	pairs[pstart[l] + p] = i;
 }
 
+// Work items are laid out XCD-major: the lists l = x, x + 8, x + 16, ... first
+// for XCD x, and a workgroup claims from its own XCD's counter (workgroups are
+// dispatched round-robin over the 8 XCDs: XCD = blockIdx.x % 8) before it steals
+// from the others.  The query groups of one list then run on one XCD, close in
+// time, so a list's codes come from that XCD's L2 after its first group instead
+// of from HBM once per group.
+constexpr int NXCD = 8;
+__device__ __forceinline__ int xcd_lists(int nlist, int x) { return x < nlist ? (nlist - x + NXCD - 1) / NXCD : 0; }
+// the list at position p of the XCD-major order
+__device__ __forceinline__ int lperm(int nlist, int p) {
+	int x = 0;
+	while (x < NXCD - 1 && p >= xcd_lists(nlist, x)) {
+		p -= xcd_lists(nlist, x);
+		++x;
+	}
+	return x + NXCD * p;
+}
+
+// the three launches above (and the cursor memset) as one workgroup when the
+// per-list counters fit in LDS (round 6: ~17 -> a few us at C5): count with
+// LDS atomics, exclusive scan (a thread per run of lists, wave scans), fill.
+// With loff (the IVF_PQ fast scan), the same workgroup then lays out the scan's
+// work items as pq_fast_items_kernel does (item_off over the XCD-major list
+// order, xbeg), from the counts it already holds: one launch less.
+constexpr int INV_THREADS = 1024, INV_MAX_LISTS = 16384;
+__device__ __forceinline__ int block_excl_scan_i(int s, int *wsum, int &total) {
+	const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+	int x = s;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const int y = __shfl_up(x, o, 64);
+		if (lane >= o) x += y;
+	}
+	if (lane == 63) wsum[w] = x;
+	__syncthreads();
+	int woff = 0, tot = 0;
+	for (int j = 0; j < INV_THREADS / 64; ++j) {
+		woff += j < w ? wsum[j] : 0;
+		tot += wsum[j];
+	}
+	__syncthreads();  // (wsum is reused by the next scan)
+	total = tot;
+	return woff + x - s;
+}
+constexpr int INV_PT = 32;  // probes per thread kept in registers between the count and the fill
+__global__ __launch_bounds__(INV_THREADS) void invert_fused_kernel(const int64_t *__restrict__ probe_l, int n,
+                                                                   int nlist, int *__restrict__ pstart,
+                                                                   int *__restrict__ pairs,
+                                                                   const int64_t *__restrict__ loff,
+                                                                   int *__restrict__ item_off,
+                                                                   int *__restrict__ xbeg) {
+	__shared__ int cnt[INV_MAX_LISTS];
+	__shared__ int wsum[INV_THREADS / 64];
+	const int t = threadIdx.x;
+	const int per = (nlist + INV_THREADS - 1) / INV_THREADS;
+	const int a = min(nlist, t * per), b = min(nlist, a + per);
+	// every global read first, all in flight together: this thread's probes
+	// (kept for the fill) and the row counts of its positions of the XCD-major
+	// list order (the item layout)
+	constexpr int IPT = 16;  // (per <= INV_MAX_LISTS / INV_THREADS)
+	int pl[INV_PT];
+#pragma unroll
+	for (int u = 0; u < INV_PT; ++u) {
+		const int i = t + u * INV_THREADS;
+		pl[u] = i < n ? (int)probe_l[i] : -1;
+	}
+	int len[IPT], lst[IPT];
+	if (loff) {
+#pragma unroll
+		for (int u = 0; u < IPT; ++u) {
+			const int p = a + u;
+			lst[u] = p < b ? lperm(nlist, p) : 0;
+			len[u] = p < b ? (int)(loff[lst[u] + 1] - loff[lst[u]]) : 0;
+		}
+	}
+	for (int i = t; i < nlist; i += INV_THREADS) cnt[i] = 0;
+	__syncthreads();
+#pragma unroll
+	for (int u = 0; u < INV_PT; ++u)
+		if (pl[u] >= 0) atomicAdd(&cnt[pl[u]], 1);
+	for (int i = t + INV_PT * INV_THREADS; i < n; i += INV_THREADS) {  // (past the registers' share)
+		const int64_t l = probe_l[i];
+		if (l >= 0) atomicAdd(&cnt[l], 1);
+	}
+	__syncthreads();
+	int is = 0, itm[IPT];
+	if (loff) {
+#pragma unroll
+		for (int u = 0; u < IPT; ++u) {
+			const int np = a + u < b ? cnt[lst[u]] : 0;
+			itm[u] = np > 0 && len[u] > 0 ? ((np + FQ_G - 1) / FQ_G) * ((len[u] + FQ_CHUNK - 1) / FQ_CHUNK) : 0;
+			is += itm[u];
+		}
+	}
+	int s = 0;
+	for (int i = a; i < b; ++i) s += cnt[i];
+	int total;
+	int run = block_excl_scan_i(s, wsum, total);
+	for (int i = a; i < b; ++i) {  // (this thread's lists only: cnt becomes their fill cursor)
+		const int c = cnt[i];
+		pstart[i] = run;
+		cnt[i] = run;
+		run += c;
+	}
+	if (t == 0) pstart[nlist] = total;
+	if (loff) {
+		int itot;
+		int ir = block_excl_scan_i(is, wsum, itot);
+		// item_off over the positions; xbeg[x] = item_off at XCD x's first position
+		// (written by the thread holding it; thread 0 writes those at nlist)
+#pragma unroll
+		for (int u = 0; u < IPT; ++u)
+			if (a + u < b) {
+				const int p = a + u;
+				item_off[p] = ir;
+				int p0 = 0;
+				for (int x = 0; x < NXCD; ++x) {
+					if (p == p0) xbeg[x] = ir;
+					p0 += xcd_lists(nlist, x);
+				}
+				ir += itm[u];
+			}
+		if (t == 0) {
+			item_off[nlist] = itot;
+			int p0 = 0;
+			for (int x = 0; x <= NXCD; ++x) {
+				if (p0 >= nlist) xbeg[x] = itot;
+				if (x < NXCD) p0 += xcd_lists(nlist, x);
+			}
+		}
+	}
+	__syncthreads();
+#pragma unroll
+	for (int u = 0; u < INV_PT; ++u)
+		if (pl[u] >= 0) pairs[atomicAdd(&cnt[pl[u]], 1)] = t + u * INV_THREADS;
+	for (int i = t + INV_PT * INV_THREADS; i < n; i += INV_THREADS) {
+		const int64_t l = probe_l[i];
+		if (l >= 0) pairs[atomicAdd(&cnt[l], 1)] = i;
+	}
+}
+
+bool invert_fused_fits(int nlist) { return nlist <= INV_MAX_LISTS; }
+
 void launch_invert(const int64_t *probe_l, int nq, int nprobe, int nlist, int *lcnt, int *pstart, int *pairs,
-                   hipStream_t st) {
+                   hipStream_t st, const int64_t *loff, int *item_off, int *xbeg) {
 	const int n = nq * nprobe;
+	if (invert_fused_fits(nlist)) {
+		invert_fused_kernel<<<1, INV_THREADS, 0, st>>>(probe_l, n, nlist, pstart, pairs, loff, item_off, xbeg);
+		return;
+	}
+	if (loff) throw std::runtime_error("launch_invert: the fused item layout needs nlist <= INV_MAX_LISTS");
 	(void)hipMemsetAsync(lcnt, 0, (size_t)nlist * sizeof(int), st);
 	invert_count_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, st>>>(probe_l, n, lcnt);
 	invert_scan_kernel<<<1, 1024, 0, st>>>(lcnt, nlist, pstart);
@@ -1939,22 +2087,146 @@ void launch_pq_lut_u8(const float *P, int nq, int m, float sP, uint8_t *lut8, fl
 	pq_lut_u8_kernel<<<dim3((unsigned)nq), 256, 0, st>>>(P, m, sP, pq_bank_w(m), lut8, qpar);
 }
 
-// Work items are laid out XCD-major: the lists l = x, x + 8, x + 16, ... first
-// for XCD x, and a workgroup claims from its own XCD's counter (workgroups are
-// dispatched round-robin over the 8 XCDs: XCD = blockIdx.x % 8) before it steals
-// from the others.  The query groups of one list then run on one XCD, close in
-// time, so a list's codes come from that XCD's L2 after its first group instead
-// of from HBM once per group.
-constexpr int NXCD = 8;
-__device__ __forceinline__ int xcd_lists(int nlist, int x) { return x < nlist ? (nlist - x + NXCD - 1) / NXCD : 0; }
-// the list at position p of the XCD-major order
-__device__ __forceinline__ int lperm(int nlist, int p) {
-	int x = 0;
-	while (x < NXCD - 1 && p >= xcd_lists(nlist, x)) {
-		p -= xcd_lists(nlist, x);
-		++x;
+// The fast scan's per-query tables in one launch (round 6; was pq_query_fp8 +
+// pq_P + pq_lut_u8, three launches and two 25-MB round trips of P through
+// HBM at C5): one workgroup per query keeps its query row (fp8-rounded when
+// asked, pq_query_fp8_kernel's arithmetic) and its m x 256 f32 table P in LDS,
+// then takes the per-sub-space ranges, D, L0 and the 8-bit entries from LDS
+// (pq_lut_u8_kernel's arithmetic).  The codebook comes from L2 (every query's
+// workgroup reads the same m x 256 x dsub floats).  Bit-identical to the three
+// launches.
+constexpr int PQL_THREADS = 1024, PQL_W = PQL_THREADS / 64;
+constexpr int PQL_PS = PQ_K + 1;  // P row stride in LDS: the quantize reads of 32 sub-spaces hit 32 banks
+__global__ __launch_bounds__(PQL_THREADS) void pq_lut_fused_kernel(const float *__restrict__ Q, int qld, int dim,
+                                                                   int fp8, const float *__restrict__ cb, int m,
+                                                                   int dsub, float sP, int wb,
+                                                                   uint8_t *__restrict__ lut8,
+                                                                   float2 *__restrict__ qpar) {
+	extern __shared__ __attribute__((aligned(16))) float pql_smem[];
+	float *Ps = pql_smem;                  // [m][PQL_PS]
+	float *xq = pql_smem + m * PQL_PS;     // [dim]
+	__shared__ float lo[PQ_MAX_M], sp[PQ_MAX_M], red[PQL_W];
+	__shared__ float dsh;
+	const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+	const float *x = Q + (int64_t)q * qld;
+	float sc = 0.0f;
+	if (fp8) {
+		float mx = 0.0f;
+		for (int i = t; i < dim; i += PQL_THREADS) mx = fmaxf(mx, fabsf(x[i]));
+#pragma unroll
+		for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+		if (lane == 0) red[w] = mx;
+		__syncthreads();
+		mx = red[0];
+#pragma unroll
+		for (int i = 1; i < PQL_W; ++i) mx = fmaxf(mx, red[i]);
+		sc = __fdiv_rn(mx, 448.0f);
 	}
-	return x + NXCD * p;
+	for (int i = t; i < dim; i += PQL_THREADS)
+		xq[i] = !fp8 ? x[i] : (sc > 0.0f ? mul_nc(e4m3_round(__fdiv_rn(x[i], sc)), sc) : 0.0f);
+	__syncthreads();
+	// P[j][c] = sum_t x_{j,t} y_{j,c,t} (t ascending, no contraction): thread
+	// (c = t & 255, j = t >> 8, +4, ...); a codebook row is dsub / 4 16-B loads,
+	// two sub-spaces' rows requested before their sums
+	{
+		const int c = t & (PQ_K - 1);
+		constexpr int JS = PQL_THREADS / PQ_K;
+		if (dsub == 8) {
+			for (int j0 = t >> 8; j0 < m; j0 += 2 * JS) {
+				const int j1 = j0 + JS;
+				const float4 *p0 = reinterpret_cast<const float4 *>(cb + ((int64_t)j0 * PQ_K + c) * 8);
+				const float4 *p1 = reinterpret_cast<const float4 *>(cb + ((int64_t)(j1 < m ? j1 : j0) * PQ_K + c) * 8);
+				const float4 a0 = p0[0], a1 = p0[1], b0 = p1[0], b1 = p1[1];
+				const float ya[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+				const float yb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+				float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+				for (int u = 0; u < 8; ++u) {
+					s0 = add_nc(s0, mul_nc(xq[j0 * 8 + u], ya[u]));
+					s1 = add_nc(s1, mul_nc(xq[(j1 < m ? j1 : j0) * 8 + u], yb[u]));
+				}
+				Ps[j0 * PQL_PS + c] = s0;
+				if (j1 < m) Ps[j1 * PQL_PS + c] = s1;
+			}
+		} else {
+			for (int j = t >> 8; j < m; j += JS) {
+				const float *y = cb + ((int64_t)j * PQ_K + c) * dsub;
+				float a = 0.0f;
+				for (int u = 0; u < dsub; ++u) a = add_nc(a, mul_nc(xq[j * dsub + u], y[u]));
+				Ps[j * PQL_PS + c] = a;
+			}
+		}
+	}
+	__syncthreads();
+	// per sub-space: min / max of sP P over its 256 entries (wave w: j = w, w + 16, ...)
+	for (int j = w; j < m; j += PQL_W) {
+		float a = F_INF, b = -F_INF;
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			const float v = mul_nc(sP, Ps[j * PQL_PS + lane + 64 * i]);
+			a = fminf(a, v);
+			b = fmaxf(b, v);
+		}
+#pragma unroll
+		for (int o = 32; o > 0; o >>= 1) {
+			a = fminf(a, __shfl_xor(a, o, 64));
+			b = fmaxf(b, __shfl_xor(b, o, 64));
+		}
+		if (lane == 0) {
+			lo[j] = a;
+			sp[j] = sub_nc(b, a);
+		}
+	}
+	__syncthreads();
+	if (t == 0) {
+		float mxs = 0.0f, l0 = 0.0f;
+		for (int j = 0; j < m; ++j) {
+			mxs = fmaxf(mxs, sp[j]);
+			l0 = add_nc(l0, lo[j]);
+		}
+		const float D = mxs > 0.0f ? __fdiv_rn(mxs, 255.0f) : 1.0f;
+		dsh = D;
+		qpar[q] = make_float2(D, l0);
+	}
+	__syncthreads();
+	const float inv = __fdiv_rn(1.0f, dsh);
+	uint8_t *o = lut8 + (int64_t)q * m * PQ_K;
+	for (int d = t; d < m * 16; d += PQL_THREADS) {
+		int j, c0;
+		if (wb) {
+			const int b = d & 31, cp = (d >> 5) & 15, xx = d >> 9;
+			j = 4 * wb * (b >> 2) + 4 * xx + (b & 3);
+			c0 = cp * 16;
+		} else {
+			j = d >> 4;
+			c0 = (d & 15) * 16;
+		}
+		const float *src = Ps + j * PQL_PS + c0;
+		const float l = lo[j];
+		uint32_t wd[4];
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			uint32_t word = 0u;
+#pragma unroll
+			for (int k2 = 0; k2 < 4; ++k2) {
+				const float u = fminf(rintf(mul_nc(sub_nc(mul_nc(sP, src[4 * i + k2]), l), inv)), 255.0f);
+				word |= (uint32_t)u << (8 * k2);
+			}
+			wd[i] = word;
+		}
+		reinterpret_cast<uint4 *>(o)[d] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+	}
+}
+
+bool pq_lut_fused_fits(int m, int dim) { return m <= PQ_MAX_M && (size_t)(m * PQL_PS + dim) * 4 <= 150 * 1024; }
+
+void launch_pq_lut_fused(const float *Q, int qld, int nq, int dim, int fp8, const float *cb, int m, int dsub, float sP,
+                         uint8_t *lut8, float2 *qpar, hipStream_t st) {
+	const size_t lds = (size_t)(m * PQL_PS + dim) * sizeof(float);
+	HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(pq_lut_fused_kernel),
+	                           hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
+	pq_lut_fused_kernel<<<dim3((unsigned)nq), PQL_THREADS, lds, st>>>(Q, qld, dim, fp8, cb, m, dsub, sP, pq_bank_w(m),
+	                                                                   lut8, qpar);
 }
 
 // work items: list l with np_l probing queries -> ceil(np_l / FQ_G) query
@@ -2400,6 +2672,9 @@ __device__ __forceinline__ int opaque_tid() {
 	asm volatile("" : "+v"(v));
 	return v;
 }
+#ifndef LHIP_FB_ROWS_FIRST
+#define LHIP_FB_ROWS_FIRST 0  // 1: round 0's rows requested before the LUT reads (round 5; 0 measured 1.6 % faster, r06o)
+#endif
 constexpr int FB_RS = 4;                            // row steps per lane and round
 constexpr int FB_ROWS = FB_THREADS / 8 * FB_RS;     // rows per round (512)
 template <int W>
@@ -2526,7 +2801,9 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 			}
 		};
 		Rows RA, RB;
+#if LHIP_FB_ROWS_FIRST
 		load(0, RA);
+#endif
 		const int tl = opaque_tid();  // (the item-start block's lane quantities: short live ranges)
 		if (tl < FQ_G) {
 			const int id = tl == 0 ? e1.x : tl == 1 ? e1.y : tl == 2 ? e1.z : e1.w;
@@ -2563,6 +2840,11 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 					                                : make_uint4(0u, 0u, 0u, 0u);
 #endif
 			}
+#if !LHIP_FB_ROWS_FIRST
+			// round 0's rows behind the LUT reads: the LUT stores wait for the LUT
+			// reads only (vmcnt counts in issue order), the rows land meanwhile
+			load(0, RA);
+#endif
 			// x = xs + 2 xi with xs in {0, 1}: xi = 0 is word 0 / 1 (the v_perm region
 			// when W >= 2, 256-B code rows), xi = 1 word 2 / 3 (the compact region,
 			// 128-B rows): the row stride is a compile-time constant per xi, so a
@@ -2908,8 +3190,8 @@ static int pq_bank_w(int m) { return (m == 32 || m == 64 || m == 96) && !pq_scan
 int pq_fast_lds_bytes(int m) { return m * PQ_K * 4 + FQ_G * FQ_CAP * 8; }
 
 void launch_pq_fast_items(const int *pstart, const int64_t *loff, const int *pairs, int nlist, int *item_off,
-                          int *xbeg, int4 *itab, int itab_cap, hipStream_t st) {
-	pq_fast_items_kernel<<<1, 1024, 0, st>>>(pstart, loff, nlist, item_off, xbeg);
+                          int *xbeg, int4 *itab, int itab_cap, hipStream_t st, bool offsets_done) {
+	if (!offsets_done) pq_fast_items_kernel<<<1, 1024, 0, st>>>(pstart, loff, nlist, item_off, xbeg);
 	if (itab) pq_fast_table_kernel<<<dim3((unsigned)((nlist + 255) / 256)), 256, 0, st>>>(pstart, loff, pairs, nlist,
 	                                                                                       item_off, itab, itab_cap);
 }

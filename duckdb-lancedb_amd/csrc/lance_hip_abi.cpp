@@ -1512,6 +1512,12 @@ static void set_option_store(Index *ix, const std::string &k, const std::string 
 		else throw Error("ivf_coarse must be 'fused' or 'flat'");
 		return;
 	}
+	if (k == "pq_lut") {  // (results identical either way; an A/B switch)
+		if (v == "fused") ix->pq_lut_fused = true;
+		else if (v == "split") ix->pq_lut_fused = false;
+		else throw Error("pq_lut must be 'fused' or 'split'");
+		return;
+	}
 	if (k == "pq_merge_bound") {  // (results identical either way; an A/B switch)
 		if (v == "1") ix->pq_merge_bound = true;
 		else if (v == "0") ix->pq_merge_bound = false;

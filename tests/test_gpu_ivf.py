@@ -436,3 +436,29 @@ def test_ivf_async_two_in_flight(hip, mk, itype):
             np.testing.assert_array_equal(g[2], e[2], err_msg=f"batch {i}")
             np.testing.assert_array_equal(g[0], e[0], err_msg=f"batch {i}")
             np.testing.assert_allclose(g[1], e[1], rtol=0, atol=0, equal_nan=True, err_msg=f"batch {i}")
+
+
+@pytest.mark.parametrize("metric", ["l2", "dot", "cosine"])
+def test_pq_lut_fused_equals_split(hip, mk, metric):
+    """The fast scan's per-query tables in one launch (pq_lut = fused, the
+    default: fp8 rounding + ADC table + 8-bit LUT with P in LDS) give the same
+    searches as the three launches (pq_lut = split), f32 and fp8 queries, and
+    the oracle's (whose LUT restates pq_lut_u8 bit for bit)."""
+    rng = np.random.default_rng(99)
+    n, d, nlist = 15_000, 96, 64
+    X = clustered(rng, n, d, centers=24)
+    Q = (X[rng.choice(n, 50, replace=False)] + 0.3 * rng.standard_normal((50, d))).astype(np.float32)
+    h = mk(d, metric, "ivf_pq")
+    hip.LanceDetachedAddBatch(h, X, n, d)
+    hip.LanceDetachedCreateIndex(h, nlist, 12)
+    for qm in ("f32", "fp8"):
+        hip.LanceHipSetOption(h, "pq_query", qm)
+        res = {}
+        for mode in ("fused", "split"):
+            hip.LanceHipSetOption(h, "pq_lut", mode)
+            res[mode] = hip.LanceDetachedSearchBatch(h, Q, 10, nprobes=12, refine_factor=4)
+        for x, y in zip(res["fused"], res["split"]):
+            np.testing.assert_array_equal(x, y)
+        el, ed, ec = oracle_search(hip, h, X, Q, 10, 12, 4, metric, "u8", qm == "fp8")
+        assert_same(*res["fused"], el, ed, ec)
+    hip.LanceHipSetOption(h, "pq_lut", "fused")

@@ -78,13 +78,18 @@ def test_hot_kernels_do_not_spill():
     m = 96 PQ fast scan reloaded 88 B of spilled lane state at every item start
     (round 5), so a register-allocation change that spills fails here, before
     the GPU.  Covered: scan8 (C2 / north_star / C3), pool_refine (f32), the
-    PQ fast scans (C5) and the IVF_FLAT bound scan (C4)."""
+    PQ fast scans (C5) and the IVF_FLAT bound scan (C4); round 6: the C5 step's
+    fused kernels (coarse bounds / select, per-query tables, invert + item
+    layout, run select)."""
     meta = {}
     for obj in OBJS:
-        if os.path.basename(obj) in ("knn_kernels.o", "scan8_kernels.o", "ivf_kernels.o"):
+        if os.path.basename(obj) in ("knn_kernels.o", "scan8_kernels.o", "ivf_kernels.o", "coarse_kernels.o"):
             meta.update(_kernel_metadata(obj))
+    step = ("coarse_bounds_kernel", "coarse_select_kernel", "pq_lut_fused_kernel", "invert_fused_kernel",
+            "pq_run_select_kernel")
     hot = [k for k in meta if ("pool_refine_kernel" in k and "Ef" in k) or "scan8_kernel" in k
-           or "pq_fast_scan_bank_kernel" in k or "flat_list_lb_kernel" in k]
+           or "pq_fast_scan_bank_kernel" in k or "flat_list_lb_kernel" in k or any(s in k for s in step)]
+    assert all(any(s in k for k in hot) for s in step), hot
     assert len(hot) >= 10, sorted(meta)[:20]
     assert sum("pq_fast_scan_bank_kernel" in k for k in hot) == 3, hot  # m = 32, 64, 96
     assert sum("flat_list_lb_kernel" in k for k in hot) == 3, hot       # l2, dot, cosine

@@ -26,8 +26,8 @@ B)
 	step ${T}_inproc 300 python -u bench.py --inproc --inproc-devices 0,0 --steps 20 --no-cpu-baseline --no-host-batch
 	step ${T}_percall_c2 300 python -u bench.py --api per_call --steps 256 --warmup 16 --no-cpu-baseline
 	step ${T}_percall_nstar 400 python -u bench.py --config nstar --api per_call --steps 64 --warmup 8 --no-cpu-baseline
-	step ${T}_prof_c5 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof_c5 -o run -- python3 bench.py --config c5 --steps 10 --no-cpu-baseline --no-recall --no-host-batch
-	python3 tools/trace_kernels.py gpurun_out/${T}_prof_c5/run_kernel_trace.csv 10 > gpurun_out/${T}_c5_step_kernels.txt 2>&1
+	step ${T}_prof_c5 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof_c5 -o run -- python3 bench.py --config c5 --steps 10 --no-cpu-baseline --no-recall --no-host-batch --no-sync-leg
+	python3 tools/trace_kernels.py gpurun_out/${T}_prof_c5/run_kernel_trace.csv 10 10 > gpurun_out/${T}_c5_step_kernels.txt 2>&1
 	rm -f gpurun_out/${T}_prof_c*/run_kernel_trace.csv.gz
 	;;
 C)

@@ -1,0 +1,11 @@
+#!/bin/bash
+# round 6: fused per-query PQ tables (pq_lut = fused): IVF GPU tests, the C5 line, and the
+# C5 trace of the pipelined steps (the time_kernels leg's 10 steps left out)
+source tools/gpu_step.sh
+T=$1
+step ${T}_ivf 700 python -u -m pytest tests/test_gpu_ivf.py tests/test_gpu_ivf_params.py -x -q --timeout 300 --timeout-method thread
+step ${T}_c5 400 python -u bench.py --config c5 --steps 20 --no-cpu-baseline
+step ${T}_prof_c5 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof_c5 -o run -- python3 bench.py --config c5 --steps 10 --no-cpu-baseline --no-recall --no-host-batch --no-sync-leg
+python3 tools/trace_kernels.py gpurun_out/${T}_prof_c5/run_kernel_trace.csv 10 10 > gpurun_out/${T}_c5_step_kernels.txt 2>&1
+rm -f gpurun_out/${T}_prof_*/run_kernel_trace.csv
+cat gpurun_out/${T}_c5_step_kernels.txt

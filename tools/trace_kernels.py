@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-kernel duration summary of a rocprofv3 --kernel-trace CSV, with the
 pool_refine launches split by their order in a step (tau mode first, then the
-final mode).  usage: tools/trace_kernels.py run_kernel_trace.csv [last_n_steps]"""
+final mode).  usage: tools/trace_kernels.py run_kernel_trace.csv [last_n_steps [skip_last]]
+(skip_last: steps at the end to leave out, e.g. bench.py's time_kernels leg)"""
 import csv
 import statistics
 import sys
@@ -9,6 +10,7 @@ from collections import defaultdict
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 last = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+skip = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 d = defaultdict(list)
 seq = []
 for r in rows:
@@ -25,7 +27,8 @@ elif any(s[0].startswith("query_absmax") for s in seq):
     starts = [i for i, s in enumerate(seq) if s[0].startswith("query_absmax") or s[0].startswith("prep_queries_kernel")]
 else:  # (a few queries per call: the int8 prep is one fused launch)
     starts = [i for i, s in enumerate(seq) if s[0].startswith("prep_queries")]
-steps = [seq[a:b] for a, b in zip(starts, starts[1:] + [len(seq)])][-last:]
+steps = [seq[a:b] for a, b in zip(starts, starts[1:] + [len(seq)])]
+steps = steps[:len(steps) - skip][-last:]
 for st in steps:
     npr = 0
     for (n, dur, _, _) in st:
