@@ -83,6 +83,7 @@ struct IvfState {
 	DevBuf<int> item_off, work, ocnt, xbeg;
 	DevBuf<int4> itab;  // fast-scan item table (launch_pq_fast_items)
 	DevBuf<int> boff, btot;  // IVF_FLAT bound scan: work items per block, their total
+	DevBuf<int> itb;         // IVF_FLAT bound scan: item -> block table (flat_lb_table_kernel)
 	DevBuf<uint32_t> live_bits;  // IVF_FLAT bound scan: live slots of the search (1 bit each)
 	DevBuf<uint64_t> thrq, okeys;
 	// IVF_FLAT bound scan workspace
@@ -191,7 +192,8 @@ void launch_flat_list_lb(const StoreView &s, const int *blk_list, const int64_t 
                          const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart, const int *pairs,
                          int nprobe, int maxb, const uint16_t *Qb, const float4 *qaux, uint64_t *out, hipStream_t st,
                          const uint16_t *lrows, const float4 *lterms, uint32_t *live_bits /* [n_slots / 32 + 1] */,
-                         int *boff /* [nblk + 1] */, int *tot /* [1] */);
+                         int *boff /* [nblk + 1] */, int *tot /* [1] */,
+                         int *itb = nullptr /* item -> block table, itb_cap entries */, int itb_cap = 0);
 // out [npos] = (xn, ux, sc, 0) of the row at each list position (the bound scan's list-order row terms)
 void launch_list_terms(const float4 *rowaux, const uint32_t *lslot, int64_t npos, float4 *out, hipStream_t st);
 // out [npos][ld] = bf16 (RNE) of the row at each list position (f32 or bf16 store X), zero for padding

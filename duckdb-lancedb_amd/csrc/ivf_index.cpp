@@ -586,12 +586,15 @@ void ivf_search(Index *ix, const float *dQ, int nq, int k, int nprobes, int refi
 				s->keys.need((size_t)n * nprobe * s->maxb * FL_KEYS);
 				ix->tic(0);
 				s->boff.need((size_t)s->nblk + 1);
+				// items <= blocks x query groups of the pass (a block's list is probed by at most n queries)
+				const int itb_cap = (int)std::min<int64_t>((int64_t)s->nblk * ((n + 15) / 16), (int64_t)1 << 28);
+				s->itb.need((size_t)itb_cap);
 				s->btot.need(1);
 				s->live_bits.need((size_t)(ix->n_slots / 32 + 2));
 				launch_flat_list_lb(sv, s->blk_list.p, s->blk_pos0.p, s->lblk0.p, s->loff.p, s->lslot.p, s->nblk,
 				                    s->pstart.p, s->pairs.p, nprobe, s->maxb, s->lbQb.p, s->lbqaux.p, s->keys.p, st,
 				                    s->lrows_ok ? s->lrows.p : nullptr, s->lrows_ok ? s->lterms.p : nullptr, s->live_bits.p,
-				                    s->boff.p, s->btot.p);
+				                    s->boff.p, s->btot.p, s->itb.p, itb_cap);
 				ix->tic(1);
 				const int M = std::min(IVF_TOPK_CAP - 1, k + 32);
 				s->cand_a.need((size_t)n * M);

@@ -1267,6 +1267,9 @@ __global__ __launch_bounds__(256) void flat_list_scan_kernel(
 // Block: 4 waves x 64 rows (4 blocks of 16), one 16-query MFMA column block.
 // ---------------------------------------------------------------------------
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+#ifndef LHIP_FL_V2
+#define LHIP_FL_V2 1  // round 6: bound words in the query rows' LDS, 3 workgroups per CU (0: round 5's layout, an A/B)
+#endif
 constexpr int FL_G = 16;   // queries per MFMA column block
 constexpr int FL_T = FL_KEYS;  // keys per (query, item)
 
@@ -1277,11 +1280,19 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
     const uint32_t *__restrict__ lslot, int nblk, const int *__restrict__ pstart, const int *__restrict__ pairs,
     int nprobe, int maxb, const uint16_t *__restrict__ Qb, const float4 *__restrict__ qaux,
     uint64_t *__restrict__ out, const uint16_t *__restrict__ Lrows, const float4 *__restrict__ Lterms,
-    const uint32_t *__restrict__ live_bits, const int *__restrict__ boff, const int *__restrict__ tot) {
+    const uint32_t *__restrict__ live_bits, const int *__restrict__ boff, const int *__restrict__ tot,
+    const int *__restrict__ itb, int itb_cap) {
 	extern __shared__ __attribute__((aligned(16))) uint8_t fl_smem[];
 	const int qrow = ld * 2 + 16;  // padded query row (bytes): 16 lanes reading 16 rows hit distinct banks
-	uint8_t *qs = fl_smem;                                                          // [FL_G][qrow]
+	uint8_t *qs = fl_smem;  // [FL_G][qrow]
+#if LHIP_FL_V2
+	// the bound words [FL_G][256] (u32: the row's slot is sslot[row]) share the
+	// query rows' LDS, which the K loop has finished reading when they are
+	// written: ~31 KB per workgroup, 3 resident per CU (was 57 KB, 2)
+	uint32_t *sk = reinterpret_cast<uint32_t *>(fl_smem);
+#else
 	uint64_t *sk = reinterpret_cast<uint64_t *>(fl_smem + FL_G * qrow);            // [FL_G][256] keys
+#endif
 	__shared__ uint32_t sslot[FLAT_BLK];
 	__shared__ float4 ras[FLAT_BLK];
 	__shared__ float4 qas[FL_G];
@@ -1302,7 +1313,9 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
 	const int it = xc * Tx + j;
 	if (it >= T) break;
 	int b;
-	{
+	if (itb && it < itb_cap) {
+		b = itb[it];  // (flat_lb_table_kernel: one read instead of a chain of dependent ones)
+	} else {
 		int lo = 0, hi = nblk - 1;  // the last block whose items start at or before it
 		while (lo < hi) {
 			const int mid = (lo + hi + 1) >> 1;
@@ -1421,6 +1434,9 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
 			}
 		}
 		mfma_operand_guard();
+#if LHIP_FL_V2
+		__syncthreads();  // (every wave's query-row reads done: the bound words overwrite them)
+#endif
 		// keys -> LDS [query][row]
 		{
 			const float4 qa = qas[rr];
@@ -1445,7 +1461,11 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
 					// a live row without a bound cannot be certified away: the
 					// item's boundary becomes -inf (the query reruns exactly)
 					if (live && __builtin_isnan(lb)) snan[rr] = 1;
+#if LHIP_FL_V2
+					sk[rr * FLAT_BLK + r] = ok ? fkey(lb) : 0xFFFFFFFFu;  // (fkey of a non-NaN float < 0xFFFFFFFF)
+#else
 					sk[rr * FLAT_BLK + r] = ok ? key64(lb, s) : KEY64_NONE;
+#endif
 				}
 		}
 		__syncthreads();
@@ -1455,7 +1475,13 @@ __global__ __launch_bounds__(256) void flat_list_lb_kernel(
 			uint64_t best = KEY64_NONE;
 #pragma unroll
 			for (int ww = 0; ww < 4; ++ww) {
+#if LHIP_FL_V2
+				const uint32_t hw = sk[c * FLAT_BLK + 64 * ww + lane];
+				const uint64_t ks = wave_sort64(hw == 0xFFFFFFFFu ? KEY64_NONE
+				                                                  : ((uint64_t)hw << 32) | sslot[64 * ww + lane]);
+#else
 				const uint64_t ks = wave_sort64(sk[c * FLAT_BLK + 64 * ww + lane]);
+#endif
 				// leader lanes 16 ww .. 16 ww + 15 of the final sort take ks[0..15]
 				const uint64_t moved = __shfl(ks, lane & 15, 64);
 				if ((lane >> 4) == ww) best = moved;
@@ -1500,6 +1526,17 @@ __global__ __launch_bounds__(1024) void flat_lb_items_kernel(const int *__restri
 		boff[nblk] = sh[1023];
 		*tot = sh[1023];
 	}
+}
+
+// itb[it] = the block of bound-scan item it (thread per block: its
+// ceil(probing queries / FL_G) items), so the scan finds an item's block with
+// one read
+__global__ __launch_bounds__(256) void flat_lb_table_kernel(const int *__restrict__ boff, int nblk,
+                                                            int *__restrict__ itb, int itb_cap) {
+	const int b = blockIdx.x * 256 + threadIdx.x;
+	if (b >= nblk) return;
+	const int e = min(boff[b + 1], itb_cap);
+	for (int it = boff[b]; it < e; ++it) itb[it] = b;
 }
 
 // per query: merge the items' leaders of its probed lists (FL_T - 1 per item
@@ -1598,7 +1635,13 @@ __global__ __launch_bounds__(RR_THREADS) void flat_lb_refine_kernel(const T *__r
 	}
 }
 
-size_t flat_lb_lds_bytes(int ld) { return (size_t)FL_G * (ld * 2 + 16) + (size_t)FL_G * FLAT_BLK * 8; }
+size_t flat_lb_lds_bytes(int ld) {
+#if LHIP_FL_V2
+	return std::max((size_t)FL_G * (ld * 2 + 16), (size_t)FL_G * FLAT_BLK * 4);
+#else
+	return (size_t)FL_G * (ld * 2 + 16) + (size_t)FL_G * FLAT_BLK * 8;
+#endif
+}
 
 __global__ __launch_bounds__(256) void live_bits_kernel(const float *__restrict__ rowaux_f, int64_t n,
                                                         uint32_t *__restrict__ bits);
@@ -1606,7 +1649,8 @@ __global__ __launch_bounds__(256) void live_bits_kernel(const float *__restrict_
 void launch_flat_list_lb(const StoreView &s, const int *blk_list, const int64_t *blk_pos0, const int *lblk0,
                          const int64_t *loff, const uint32_t *lslot, int nblk, const int *pstart, const int *pairs,
                          int nprobe, int maxb, const uint16_t *Qb, const float4 *qaux, uint64_t *out, hipStream_t st,
-                         const uint16_t *lrows, const float4 *lterms, uint32_t *live_bits, int *boff, int *tot) {
+                         const uint16_t *lrows, const float4 *lterms, uint32_t *live_bits, int *boff, int *tot,
+                         int *itb, int itb_cap) {
 	if (nblk <= 0) return;
 	if (lrows) {  // the live bitmap of the slots (deletes / the predicate of this search: alpha = +inf)
 		const int64_t n = s.n_slots;
@@ -1615,6 +1659,7 @@ void launch_flat_list_lb(const StoreView &s, const int *blk_list, const int64_t 
 			                                                                    live_bits);
 	}
 	flat_lb_items_kernel<<<1, 1024, 0, st>>>(blk_list, pstart, nblk, boff, tot);
+	if (itb) flat_lb_table_kernel<<<dim3((unsigned)((nblk + 255) / 256)), 256, 0, st>>>(boff, nblk, itb, itb_cap);
 	if ((!lrows && !s.scan_bf16) || s.ld % 64) throw std::runtime_error("IVF_FLAT bound scan needs bf16 scan rows");
 	const uint16_t *Xb = static_cast<const uint16_t *>(s.Xscan);
 	const float *ra = reinterpret_cast<const float *>(s.rowaux);
@@ -1622,11 +1667,12 @@ void launch_flat_list_lb(const StoreView &s, const int *blk_list, const int64_t 
 	auto go = [&](auto kern) {
 		HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
 		                           (int)lds));
-		// persistent: 2 workgroups per CU (57 KB of LDS each: all resident), a multiple of the 8 XCDs
-		const int grid = std::max(8, (2 * scan_grid(1 << 20) / 8) * 8);
+		// persistent, a multiple of the 8 XCDs: LHIP_FL_V2 3 workgroups per CU (31 KB
+		// of LDS, 148 VGPRs: 3 waves per SIMD), else 2 (57 KB)
+		const int grid = std::max(8, ((LHIP_FL_V2 ? 3 : 2) * scan_grid(1 << 20) / 8) * 8);
 		kern<<<dim3((unsigned)grid), 256, lds, st>>>(Xb, s.ld, ra, blk_list, blk_pos0, lblk0, loff, lslot, nblk, pstart,
 		                                             pairs, nprobe, maxb, Qb, qaux, out, lrows, lrows ? lterms : nullptr,
-		                                             live_bits, boff, tot);
+		                                             live_bits, boff, tot, itb, itb_cap);
 	};
 	switch (s.metric) {
 	case METRIC_L2: go(flat_list_lb_kernel<METRIC_L2>); break;
@@ -2765,7 +2811,7 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 #pragma unroll
 		for (int i = 0; i < FQ_G; ++i) qv[i] = ids[i] >= 0 ? ids[i] / nprobe : -1;
 		// the item's rows as buffer resources (rows past the end read 0); round 0's
-		// rows are requested before the LUT build, in the same round trip as its reads
+		// rows are requested with the LUT build's reads, in the same round trip
 		const __amdgpu_buffer_rsrc_t rcode =
 		    __builtin_amdgcn_make_buffer_rsrc((void *)(lcodes + pos0 * MT), 0, (int)(nrow * MT), FB_RSRC3);
 		const __amdgpu_buffer_rsrc_t rslot =

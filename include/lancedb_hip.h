@@ -231,6 +231,14 @@ int32_t lance_hip_device_count(void);
  *   "pq_query"     "f32" (default) | "fp8": IVF_PQ distance tables from e4m3
  *                  (fp8) queries (BASELINE.json configs[4]); coarse search and
  *                  re-rank keep the f32 query
+ *   "pq_lut"       "fused" (default) | "split": the fast scan's per-query
+ *                  tables in one launch or three (bit-identical)
+ *   "pq_merge_bound" "1" (default) | "0": the fast scan's run merge keeps only
+ *                  keys at or below the scan's final bound (same lists)
+ *   "ivf_coarse"   "fused" (default) | "flat": IVF coarse search by the fused
+ *                  MFMA-bound + exact-refine kernels or by the flat path over
+ *                  the centroid store (same probes)
+ *   "s8_couple"    "0" (default) | lag: int8 append scan pair coupling
  *   "time_kernels" "1" = record HIP events around scan launches
  *                  (lance_hip_kernel_times); default "0"
  *   "scan8_variant" geometry of the int8 append kernel at dim 768: "0" (the
@@ -302,9 +310,11 @@ int32_t lance_hip_search_batch_device(void *handle, const float *d_queries, int3
  * the oldest); every other call that touches the device or the handle's
  * options (search, add, delete, compact, create_index, get_vector,
  * lance_hip_set_option, ...) first completes every pending one; count,
- * dimension and the statistics getters only read host state.  Searches that are not a single
- * threshold-path pass (IVF, predicate, small stores, > 2048 queries, option
- * time_kernels) run synchronously inside the call. */
+ * dimension and the statistics getters only read host state.  An IVF search
+ * that fits one pass (<= 2048 queries) is enqueued whole (round 6; its
+ * coarse-search flags and any rerun at the wait); flat searches that are not a single
+ * threshold-path pass (small stores, > 2048 queries) and every search with a
+ * predicate or option time_kernels run synchronously inside the call. */
 int64_t lance_hip_search_batch_device_async(void *handle, const float *d_queries, int32_t nq, int32_t dim, int32_t k,
                                             int32_t nprobes, int32_t refine_factor, int64_t *d_out_labels,
                                             float *d_out_distances, int32_t *d_out_counts, char *err_buf,
