@@ -2,11 +2,12 @@
 # closing check on one MI355X (usage: tools/closing_check.sh A|B|C|S TAG), in separate calls:
 #   A: the committed tree's GPU suite and smoke
 #   B: the driver's bench command, its rocprofv3 kernel stats, the other configs' lines, per-rank
-#      shapes, the in-process two-shard form, and the C5 step's kernel stats
+#      shapes, the in-process two-shard form, the per-call legs (Python and torch-free C++), and
+#      the C5 step's kernel stats
 #   C: PMC traffic passes of each config's dominant kernel (tools/pmc_configs.sh)
 #   S: one config's step: bench line + rocprofv3 kernel trace (CFG=c2|nstar|c4|c5, STEPS)
 source tools/gpu_step.sh
-T=${2:-r06f}
+T=${2:-r06x}
 case $1 in
 A)
 	step ${T}_pytest 1100 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread
@@ -26,6 +27,7 @@ B)
 	step ${T}_inproc 300 python -u bench.py --inproc --inproc-devices 0,0 --steps 20 --no-cpu-baseline --no-host-batch
 	step ${T}_percall_c2 300 python -u bench.py --api per_call --steps 256 --warmup 16 --no-cpu-baseline
 	step ${T}_percall_nstar 400 python -u bench.py --config nstar --api per_call --steps 64 --warmup 8 --no-cpu-baseline
+	step ${T}_cpp_percall 600 python -u tools/cpp_percall.py
 	step ${T}_prof_c5 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof_c5 -o run -- python3 bench.py --config c5 --steps 10 --no-cpu-baseline --no-recall --no-host-batch --no-sync-leg
 	python3 tools/trace_kernels.py gpurun_out/${T}_prof_c5/run_kernel_trace.csv 10 10 > gpurun_out/${T}_c5_step_kernels.txt 2>&1
 	rm -f gpurun_out/${T}_prof_c*/run_kernel_trace.csv.gz
