@@ -2354,14 +2354,20 @@ void launch_finalize(const StoreView &s, const uint32_t *cand_slot, const int *c
 #ifndef LHIP_PR_THREADS
 #define LHIP_PR_THREADS 512
 #endif
-constexpr int PR_THREADS = LHIP_PR_THREADS;  // 512 or 1024 (one workgroup per query)
-static_assert(PR_THREADS == 512 || PR_THREADS == 1024, "pool_refine geometry");
+constexpr int PR_THREADS = LHIP_PR_THREADS;  // 256, 512 or 1024 (one workgroup per query)
+static_assert(PR_THREADS == 256 || PR_THREADS == 512 || PR_THREADS == 1024, "pool_refine geometry");
+#ifndef LHIP_PR_CAP
+#define LHIP_PR_CAP 16384
+#endif
+// (256 threads with a 4096-entry pool: ~54 KB of LDS and one wave per SIMD, two
+// workgroups per CU — a development geometry for A/B timing)
+constexpr int PR_MIN_WAVES = PR_THREADS == 256 ? 2 : 1;  // waves per SIMD the register allocation must allow
 #ifdef LHIP_PR_PROF
 constexpr int PR_NSTAMP = 32, PR_PROF_Q = 4096;
 __device__ uint64_t g_pr_stamps[PR_PROF_Q * (PR_NSTAMP + 3)];
 #endif
 constexpr int PR_WAVES = PR_THREADS / 64;
-constexpr int PR_CAP = 16384;       // pool entries held in LDS
+constexpr int PR_CAP = LHIP_PR_CAP;  // pool entries held in LDS
 constexpr int PR_PER_WAVE = 16;     // candidates per wave and round
 constexpr int PR_CHUNK = PR_WAVES * PR_PER_WAVE;
 constexpr int PR_MAXK = MAX_CAND;   // k of the fast path (k + 8 <= MAX_CAND)
@@ -2736,14 +2742,14 @@ __device__ __forceinline__ void pr_bitonic(uint64_t *a, int P) {
 
 constexpr int PR_SEL = 1024;  // chunk capacity
 constexpr int PR_HB = 1024;   // histogram bins of a chunk selection
-constexpr int PR_BPT = PR_HB / PR_THREADS;  // bins per thread (2 or 1)
-static_assert(PR_BPT * PR_THREADS == PR_HB && (PR_BPT == 1 || PR_BPT == 2), "bins per thread");
+constexpr int PR_BPT = PR_HB / PR_THREADS;  // bins per thread (4, 2 or 1)
+static_assert(PR_BPT * PR_THREADS == PR_HB && PR_BPT >= 1 && PR_BPT <= 4, "bins per thread");
 constexpr int PR_R = 96;      // first chunk of the final pass (C2: ~80 rows lie below d_k; refined rows
                               // are the kernel's HBM traffic: 96 refined 18 % fewer than 128 at equal
                               // step time or better, r03s2)
 
 template <int METRIC, typename T, int NI>
-__global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
+__global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
     const uint2 *__restrict__ seg_pool, const int *__restrict__ seg_cnt, int seg_cap, int n_seg, int nq,
     const float *__restrict__ tau, const T *__restrict__ X, int ld, int dim, const float *__restrict__ Qf,
     const int64_t *__restrict__ labels, int k, int mode, int m_tau, int64_t live, float *__restrict__ tau_out,
@@ -2883,14 +2889,21 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 		}
 		__syncthreads();
 		{
-			const unsigned h0 = hist[PR_BPT * t], h1 = PR_BPT == 2 ? hist[PR_BPT * t + 1] : 0u;
+			unsigned hb[PR_BPT], hs = 0;
+#pragma unroll
+			for (int b = 0; b < PR_BPT; ++b) {
+				hb[b] = hist[PR_BPT * t + b];
+				hs += hb[b];
+			}
 			unsigned tot;
-			const unsigned ex = block_excl_scan<PR_THREADS>(h0 + h1, sh, tot);
+			const unsigned ex = block_excl_scan<PR_THREADS>(hs, sh, tot);
 			int cand = -1;  // the last bin whose inclusive count fits
-			if (PR_BPT == 2 && ex + h0 + h1 <= (unsigned)PR_CAP)
-				cand = PR_BPT * t + 1;
-			else if (ex + h0 <= (unsigned)PR_CAP)
-				cand = PR_BPT * t;
+			unsigned run = ex;
+#pragma unroll
+			for (int b = 0; b < PR_BPT; ++b) {
+				run += hb[b];
+				if (run <= (unsigned)PR_CAP) cand = PR_BPT * t + b;
+			}
 			if (cand >= 0) atomicMax(reinterpret_cast<int *>(&s_bstar) + 0, cand);  // (s_bstar starts at -1)
 		}
 		__syncthreads();
@@ -3042,14 +3055,28 @@ __global__ __launch_bounds__(PR_THREADS) void pool_refine_kernel(
 				if (kk >= kmin && kk <= kmax) atomicAdd(&hist[(kk - kmin) >> shift], 1u);
 			}
 			__syncthreads();
-			const unsigned h0 = hist[PR_BPT * t], h1 = PR_BPT == 2 ? hist[PR_BPT * t + 1] : 0u;
+			unsigned hb[PR_BPT], hs = 0;
+#pragma unroll
+			for (int b = 0; b < PR_BPT; ++b) {
+				hb[b] = hist[PR_BPT * t + b];
+				hs += hb[b];
+			}
 			unsigned tot;
-			const unsigned ex = block_excl_scan<PR_THREADS>(h0 + h1, sh, tot);
-			if (ex < (unsigned)R && ex + h0 + h1 >= (unsigned)R) {
-				const bool first = ex + h0 >= (unsigned)R;
-				s_bstar = first ? PR_BPT * t : PR_BPT * t + 1;
-				s_cum = first ? ex + h0 : ex + h0 + h1;
-				s_below = first ? ex : ex + h0;
+			const unsigned ex = block_excl_scan<PR_THREADS>(hs, sh, tot);
+			if (ex < (unsigned)R && ex + hs >= (unsigned)R) {
+				// this thread's first bin where the count reaches R
+				unsigned run = ex;
+				bool found = false;
+#pragma unroll
+				for (int b = 0; b < PR_BPT; ++b) {
+					if (!found && run + hb[b] >= (unsigned)R) {
+						s_bstar = PR_BPT * t + b;
+						s_cum = run + hb[b];
+						s_below = run;
+						found = true;
+					}
+					run += hb[b];
+				}
 			}
 			__syncthreads();
 			bstar = s_bstar;
