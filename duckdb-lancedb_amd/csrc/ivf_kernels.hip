@@ -2721,9 +2721,6 @@ __device__ __forceinline__ int opaque_tid() {
 #ifndef LHIP_FB_ROWS_FIRST
 #define LHIP_FB_ROWS_FIRST 0  // 1: round 0's rows requested before the LUT reads (round 5; 0 measured 1.6 % faster, r06o)
 #endif
-#ifndef LHIP_FB_XPRE
-#define LHIP_FB_XPRE 1  // the next item's round-0 rows requested in this item's last round (0: at its start, an A/B)
-#endif
 constexpr int FB_RS = 4;                            // row steps per lane and round
 constexpr int FB_ROWS = FB_THREADS / 8 * FB_RS;     // rows per round (512)
 template <int W>
@@ -2745,8 +2742,6 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 	float *d0s = reinterpret_cast<float *>(qid + FQ_G), *dls = d0s + FQ_G, *l0s = dls + FQ_G;
 	int &item = *reinterpret_cast<int *>(l0s + FQ_G), &nlive = (&item)[1];
 	int4 *nent = reinterpret_cast<int4 *>(l0s + FQ_G + 4);  // the item's itab entry
-	int4 *nnext = nent + 2;  // the next item's first itab word (published in round 1, read from round 2 on)
-	static_assert(FB_META_BYTES >= 176, "per-item LDS state");
 	const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
 	const int p = lane & 7, rw = lane >> 3, r = rw & 3, pq = p & 3;
 	// per sub-step s (code byte y = (s + r) & 3, bank b = 4p + y): byte s of lb4 /
@@ -2795,50 +2790,6 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 		}
 	}
 	__syncthreads();
-	struct Rows {
-		uint32_t cw[FB_RS][W];
-		uint32_t sl[FB_RS];
-		float ta[FB_RS];
-	};
-	// row step k of a round at item row rb of the item whose rows the buffer
-	// resources describe (nr rows): the wave's 8 consecutive rows
-	auto load_codes = [&](const __amdgpu_buffer_rsrc_t &rc, uint32_t rb, Rows &R) __attribute__((always_inline)) {
-#pragma unroll
-		for (int k = 0; k < FB_RS; ++k) {
-			const uint32_t srow = rb + (uint32_t)(k * (FB_THREADS / 8));  // (scalar)
-			if constexpr (W == 3) {
-				const auto v = __builtin_amdgcn_raw_buffer_load_b96(rc, vcode, (int)(srow * MT), FB_AUX);
-				R.cw[k][0] = v[0];
-				R.cw[k][1] = v[1];
-				R.cw[k][2] = v[2];
-			} else if constexpr (W == 2) {
-				const auto v = __builtin_amdgcn_raw_buffer_load_b64(rc, vcode, (int)(srow * MT), FB_AUX);
-				R.cw[k][0] = v[0];
-				R.cw[k][1] = v[1];
-			} else {
-				R.cw[k][0] = __builtin_amdgcn_raw_buffer_load_b32(rc, vcode, (int)(srow * MT), FB_AUX);
-			}
-		}
-	};
-	auto load_terms = [&](const __amdgpu_buffer_rsrc_t &rs, const __amdgpu_buffer_rsrc_t &rt, uint32_t nr, uint32_t rb,
-	                      Rows &R) __attribute__((always_inline)) {
-#pragma unroll
-		for (int k = 0; k < FB_RS; ++k) {
-			const uint32_t srow = rb + (uint32_t)(k * (FB_THREADS / 8));  // (scalar)
-			const uint32_t sl = __builtin_amdgcn_raw_buffer_load_b32(rs, vrow, (int)(srow * 4), FB_AUX);
-			R.sl[k] = srow + lrow < nr ? sl : SLOT_NONE;
-			R.ta[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rt, vrow, (int)(srow * 4), FB_AUX));
-		}
-	};
-	auto codes_rsrc = [&](int64_t p0, uint32_t nr) __attribute__((always_inline)) {
-		return __builtin_amdgcn_make_buffer_rsrc((void *)(lcodes + p0 * MT), 0, (int)(nr * MT), FB_RSRC3);
-	};
-	// two row buffers: the next round's rows land while one is summed.  pre: the
-	// current item's round-0 codes are already in RA (requested in the previous
-	// item's last round, into whichever buffer was free: pre_swap); its slots and
-	// row terms are requested at its start (fewer registers live across items)
-	Rows RA, RB;
-	bool pre = false, pre_swap = false;
 	for (;;) {
 		PQ_T(0);
 		const int it = item;
@@ -2861,31 +2812,43 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 		for (int i = 0; i < FQ_G; ++i) qv[i] = ids[i] >= 0 ? ids[i] / nprobe : -1;
 		// the item's rows as buffer resources (rows past the end read 0); round 0's
 		// rows are requested with the LUT build's reads, in the same round trip
-		const __amdgpu_buffer_rsrc_t rcode = codes_rsrc(pos0, nrow);
+		const __amdgpu_buffer_rsrc_t rcode =
+		    __builtin_amdgcn_make_buffer_rsrc((void *)(lcodes + pos0 * MT), 0, (int)(nrow * MT), FB_RSRC3);
 		const __amdgpu_buffer_rsrc_t rslot =
 		    __builtin_amdgcn_make_buffer_rsrc((void *)(lslot + pos0), 0, (int)(nrow * 4), FB_RSRC3);
 		const __amdgpu_buffer_rsrc_t rtau =
 		    __builtin_amdgcn_make_buffer_rsrc((void *)(ltau ? ltau + pos0 : nullptr), 0, ltau ? (int)(nrow * 4) : 0,
 		                                      FB_RSRC3);
-		auto load = [&](uint32_t rb, Rows &R) __attribute__((always_inline)) {
-			load_codes(rcode, rb, R);
-			load_terms(rslot, rtau, nrow, rb, R);
+		struct Rows {
+			uint32_t cw[FB_RS][W];
+			uint32_t sl[FB_RS];
+			float ta[FB_RS];
 		};
-		if (pre && pre_swap) {  // (round 0's codes landed in RB: make them RA's)
+		// row step k of the round at item row rb: the wave's 8 consecutive rows
+		auto load = [&](uint32_t rb, Rows &R) __attribute__((always_inline)) {
 #pragma unroll
-			for (int k = 0; k < FB_RS; ++k)
-#pragma unroll
-				for (int x = 0; x < W; ++x) {
-					const uint32_t tmp = RA.cw[k][x];
-					RA.cw[k][x] = RB.cw[k][x];
-					RB.cw[k][x] = tmp;
+			for (int k = 0; k < FB_RS; ++k) {
+				const uint32_t srow = rb + (uint32_t)(k * (FB_THREADS / 8));  // (scalar)
+				if constexpr (W == 3) {
+					const auto v = __builtin_amdgcn_raw_buffer_load_b96(rcode, vcode, (int)(srow * MT), FB_AUX);
+					R.cw[k][0] = v[0];
+					R.cw[k][1] = v[1];
+					R.cw[k][2] = v[2];
+				} else if constexpr (W == 2) {
+					const auto v = __builtin_amdgcn_raw_buffer_load_b64(rcode, vcode, (int)(srow * MT), FB_AUX);
+					R.cw[k][0] = v[0];
+					R.cw[k][1] = v[1];
+				} else {
+					R.cw[k][0] = __builtin_amdgcn_raw_buffer_load_b32(rcode, vcode, (int)(srow * MT), FB_AUX);
 				}
-		}
+				const uint32_t sl = __builtin_amdgcn_raw_buffer_load_b32(rslot, vrow, (int)(srow * 4), FB_AUX);
+				R.sl[k] = srow + lrow < nrow ? sl : SLOT_NONE;
+				R.ta[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rtau, vrow, (int)(srow * 4), FB_AUX));
+			}
+		};
+		Rows RA, RB;
 #if LHIP_FB_ROWS_FIRST
-		if (pre)
-			load_terms(rslot, rtau, nrow, 0, RA);
-		else
-			load(0, RA);
+		load(0, RA);
 #endif
 		const int tl = opaque_tid();  // (the item-start block's lane quantities: short live ranges)
 		if (tl < FQ_G) {
@@ -2926,10 +2889,7 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 #if !LHIP_FB_ROWS_FIRST
 			// round 0's rows behind the LUT reads: the LUT stores wait for the LUT
 			// reads only (vmcnt counts in issue order), the rows land meanwhile
-			if (pre)
-				load_terms(rslot, rtau, nrow, 0, RA);
-			else
-				load(0, RA);
+			load(0, RA);
 #endif
 			// x = xs + 2 xi with xs in {0, 1}: xi = 0 is word 0 / 1 (the v_perm region
 			// when W >= 2, 256-B code rows), xi = 1 word 2 / 3 (the compact region,
@@ -2972,25 +2932,10 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 		const int myq = qid[pql];
 		const float myd0 = d0s[pql], mydl = dls[pql], myl0 = l0s[pql];
 		uint64_t mythr = thr[pql];
-		pre = false;
-		auto round = [&](const Rows &R, Rows &N, uint32_t rpre, uint64_t &gprev, uint32_t ri) __attribute__((always_inline)) {
-			const bool first = ri == 0;
+		auto round = [&](const Rows &R, Rows &N, uint32_t rpre, uint64_t &gprev, bool first) __attribute__((always_inline)) {
 			uint64_t gthr = KEY64_NONE;  // (the query's bound from its other items: as pq_fast_scan_kernel)
 			if (t < FQ_G && qid[t] >= 0) gthr = __builtin_nontemporal_load(thrq + qid[t]);
-			if (rpre < nrow) {
-				load(rpre, N);
-			} else if (LHIP_FB_XPRE && ri >= 2) {
-				// this item's last round: the next item's round-0 rows into the free buffer
-				const int4 nx = *nnext;
-				const uint32_t nlo = (uint32_t)__builtin_amdgcn_readfirstlane(nx.x);  // (uniform: scalar registers)
-				const uint32_t nhi = (uint32_t)__builtin_amdgcn_readfirstlane(nx.y);
-				const uint32_t nnr = (uint32_t)__builtin_amdgcn_readfirstlane(nx.z);
-				if (nnr > 0) {
-					load_codes(codes_rsrc((int64_t)(((uint64_t)nhi << 32) | nlo), nnr), 0, N);
-					pre = true;
-				}
-			}
-			if (LHIP_FB_XPRE && ri == 1 && t == 0) *nnext = ne0;  // (wave 0 read it in round 0; z = 0: none)
+			load(rpre, N);
 			if (first && t == 0 && tries < NXCD) pend = atomicAdd(work + xc, 1);
 			// two steps' totals are keyed together: lanes p < 4 key step k, lanes
 			// p >= 4 step k + 1, for query p & 3
@@ -3100,17 +3045,13 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 			mythr = thr[pq];
 			PQ_T(3);
 		};
+		// two row buffers: the next round's rows land while one is summed
 		uint64_t gprev = KEY64_NONE;
-		uint32_t ri = 0;
-		bool last_b = false;  // the last round's free buffer was RB
 		for (uint32_t r0 = 0; r0 < nrow; r0 += 2 * FB_ROWS) {
-			round(RA, RB, r0 + FB_ROWS, gprev, ri++);
-			last_b = true;
+			round(RA, RB, r0 + FB_ROWS, gprev, r0 == 0);
 			if (r0 + FB_ROWS >= nrow) break;
-			round(RB, RA, r0 + 2 * FB_ROWS, gprev, ri++);
-			last_b = false;
+			round(RB, RA, r0 + 2 * FB_ROWS, gprev, false);
 		}
-		pre_swap = last_b;
 #ifdef LHIP_PQ_PROF
 		for (int i = 0; i < FQ_G; ++i) pq_acc[7] += qid[i] >= 0 ? (uint64_t)cnt[i] : 0;
 #endif
