@@ -2721,6 +2721,9 @@ __device__ __forceinline__ int opaque_tid() {
 #ifndef LHIP_FB_ROWS_FIRST
 #define LHIP_FB_ROWS_FIRST 0  // 1: round 0's rows requested before the LUT reads (round 5; 0 measured 1.6 % faster, r06o)
 #endif
+#ifndef LHIP_FB_L2PRE
+#define LHIP_FB_L2PRE 0  // 1: an item's last round pulls the next item's first codes and LUTs into L2 (measured 2.6 % slower, r06u)
+#endif
 constexpr int FB_RS = 4;                            // row steps per lane and round
 constexpr int FB_ROWS = FB_THREADS / 8 * FB_RS;     // rows per round (512)
 template <int W>
@@ -2742,6 +2745,10 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 	float *d0s = reinterpret_cast<float *>(qid + FQ_G), *dls = d0s + FQ_G, *l0s = dls + FQ_G;
 	int &item = *reinterpret_cast<int *>(l0s + FQ_G), &nlive = (&item)[1];
 	int4 *nent = reinterpret_cast<int4 *>(l0s + FQ_G + 4);  // the item's itab entry
+#if LHIP_FB_L2PRE
+	int4 *nnext = nent + 2;  // the next item's itab entry, published in round 1
+	static_assert(FB_META_BYTES >= 192, "per-item LDS state");
+#endif
 	const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
 	const int p = lane & 7, rw = lane >> 3, r = rw & 3, pq = p & 3;
 	// per sub-step s (code byte y = (s + r) & 3, bank b = 4p + y): byte s of lb4 /
@@ -2790,6 +2797,9 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 		}
 	}
 	__syncthreads();
+	// (LHIP_FB_L2PRE) the L2 prefetch's dword, consumed one item later so that no
+	// wait for it lands in the item that issued it
+	uint32_t pf_v = 0u;
 	for (;;) {
 		PQ_T(0);
 		const int it = item;
@@ -2935,7 +2945,38 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 		auto round = [&](const Rows &R, Rows &N, uint32_t rpre, uint64_t &gprev, bool first) __attribute__((always_inline)) {
 			uint64_t gthr = KEY64_NONE;  // (the query's bound from its other items: as pq_fast_scan_kernel)
 			if (t < FQ_G && qid[t] >= 0) gthr = __builtin_nontemporal_load(thrq + qid[t]);
-			load(rpre, N);
+			load(rpre, N);  // (past the item's rows: reads 0, no memory traffic; N stays a fresh value)
+#if LHIP_FB_L2PRE
+			if (rpre >= nrow && rpre >= 3 * FB_ROWS) {
+				// this item's last round (round 2 on; round 1 published the next entry):
+				// the next item's first round of codes and its queries' LUTs pulled into
+				// L2, one dword per 128-B line with the default cache policy, so that its
+				// start reads them from L2 rather than from HBM / the fabric
+				const int4 nx = nnext[0], np4 = nnext[1];
+				const uint32_t nnr = (uint32_t)__builtin_amdgcn_readfirstlane(nx.z);
+				if (nnr > 0) {
+					constexpr int CL = FB_ROWS * MT / 128;  // code lines of a round (threads [0, CL))
+					if (t < CL) {
+						const uint32_t nlo = (uint32_t)__builtin_amdgcn_readfirstlane(nx.x);
+						const uint32_t nhi = (uint32_t)__builtin_amdgcn_readfirstlane(nx.y);
+						const int64_t p0 = (int64_t)(((uint64_t)nhi << 32) | nlo);
+						if ((uint32_t)t * 128u < min(nnr, (uint32_t)FB_ROWS) * (uint32_t)MT)
+							pf_v = *reinterpret_cast<const uint32_t *>(lcodes + p0 * MT + (int64_t)t * 128);
+					} else {
+						constexpr int QL = MT * PQ_K / 128;  // LUT lines of a query
+						const int li = t - CL, qi = li / QL;
+						const int pid = qi == 0 ? np4.x : qi == 1 ? np4.y : qi == 2 ? np4.z : qi == 3 ? np4.w : -1;
+						if (pid >= 0)
+							pf_v = *reinterpret_cast<const uint32_t *>(lut8 + (int64_t)(pid / nprobe) * MT * PQ_K +
+							                                           (int64_t)(li - qi * QL) * 128);
+					}
+				}
+			}
+			if (rpre == 2 * FB_ROWS && t == 0) {  // round 1: wave 0 read the next entry in round 0
+				nnext[0] = ne0;
+				nnext[1] = ne1;
+			}
+#endif
 			if (first && t == 0 && tries < NXCD) pend = atomicAdd(work + xc, 1);
 			// two steps' totals are keyed together: lanes p < 4 key step k, lanes
 			// p >= 4 step k + 1, for query p & 3
@@ -3031,6 +3072,7 @@ __global__ __launch_bounds__(FB_THREADS) void pq_fast_scan_bank_kernel(
 			}
 			__syncthreads();
 			PQ_T(2);
+			if (LHIP_FB_L2PRE && first) asm volatile("" ::"v"(pf_v));  // (the previous item's prefetch: long complete)
 			for (int i = 0; i < FQ_G; ++i) {
 				if (cnt[i] > FQ_CAP - FB_ROWS) {  // the next round could overflow: sort, keep kk
 #ifdef LHIP_PQ_PROF
