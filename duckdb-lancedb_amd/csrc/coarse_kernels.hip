@@ -28,7 +28,6 @@
 #include "device_common.h"
 
 #include <stdexcept>
-#include <type_traits>
 
 namespace lhip {
 
@@ -57,45 +56,41 @@ __global__ __launch_bounds__(256) void coarse_bounds_kernel(const float *__restr
 #pragma unroll
 	for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 	// staging: a 64 x 64 f32 tile of each operand = 1024 float4, 4 per thread and
-	// operand, in two register sets: chunk c + 2 is requested once chunk c is in
-	// LDS, so every load has two chunks of MFMAs to land in (one chunk of f32
-	// MFMAs, ~1 us, is shorter than a load under load; dim % 4 == 0,
-	// coarse_fused_fits)
-	float4 rq[2][4], rc[2][4];
-	auto fetch = [&](int k0, auto setc) __attribute__((always_inline)) {
-		constexpr int S = decltype(setc)::value;
+	// operand, loaded for the NEXT chunk while this one multiplies (every load in
+	// flight together: dim % 4 == 0, coarse_fused_fits)
+	float4 rq[4], rc[4];
+	auto fetch = [&](int k0) {
 #pragma unroll
 		for (int j = 0; j < 4; ++j) {
 			const int e = t + 256 * j, r = e >> 4, c4 = (e & 15) * 4, k = k0 + c4;
 			const int q = q0 + r, cc = c0 + r;
-			rq[S][j] = (q < nq && k < dim) ? *reinterpret_cast<const float4 *>(Q + (int64_t)q * dim + k)
-			                               : make_float4(0.f, 0.f, 0.f, 0.f);
-			rc[S][j] = (cc < nc && k < dim) ? *reinterpret_cast<const float4 *>(C + (int64_t)cc * ld + k)
-			                                : make_float4(0.f, 0.f, 0.f, 0.f);
+			rq[j] = (q < nq && k < dim) ? *reinterpret_cast<const float4 *>(Q + (int64_t)q * dim + k)
+			                            : make_float4(0.f, 0.f, 0.f, 0.f);
+			rc[j] = (cc < nc && k < dim) ? *reinterpret_cast<const float4 *>(C + (int64_t)cc * ld + k)
+			                             : make_float4(0.f, 0.f, 0.f, 0.f);
 		}
 	};
 	// norms: thread t sums row t >> 1 of the 128 staged rows (query rows, then
 	// centroid rows), columns 32 (t & 1) .. + 32 of each chunk, in f64
 	const int nr = t >> 1, nh = (t & 1) * 32;
 	double n2 = 0.0;
-	const int nch = (dim + CB_KC - 1) / CB_KC;
-	auto chunk = [&](int ci, auto setc) __attribute__((always_inline)) {
-		constexpr int S = decltype(setc)::value;
+	fetch(0);
+	for (int k0 = 0; k0 < dim; k0 += CB_KC) {
 		__syncthreads();  // the previous chunk consumed
 #pragma unroll
 		for (int j = 0; j < 4; ++j) {
 			const int e = t + 256 * j, r = e >> 4, c4 = (e & 15) * 4;
-			Qs[r][c4] = rq[S][j].x;
-			Qs[r][c4 + 1] = rq[S][j].y;
-			Qs[r][c4 + 2] = rq[S][j].z;
-			Qs[r][c4 + 3] = rq[S][j].w;
-			Cs[r][c4] = rc[S][j].x;
-			Cs[r][c4 + 1] = rc[S][j].y;
-			Cs[r][c4 + 2] = rc[S][j].z;
-			Cs[r][c4 + 3] = rc[S][j].w;
+			Qs[r][c4] = rq[j].x;
+			Qs[r][c4 + 1] = rq[j].y;
+			Qs[r][c4 + 2] = rq[j].z;
+			Qs[r][c4 + 3] = rq[j].w;
+			Cs[r][c4] = rc[j].x;
+			Cs[r][c4 + 1] = rc[j].y;
+			Cs[r][c4 + 2] = rc[j].z;
+			Cs[r][c4 + 3] = rc[j].w;
 		}
 		__syncthreads();
-		if (ci + 2 < nch) fetch((ci + 2) * CB_KC, setc);  // (this set is free again)
+		if (k0 + CB_KC < dim) fetch(k0 + CB_KC);  // in flight during the MFMAs
 		{
 			const float *row = nr < CB_T ? Qs[nr] : Cs[nr - CB_T];
 #pragma unroll 8
@@ -107,12 +102,6 @@ __global__ __launch_bounds__(256) void coarse_bounds_kernel(const float *__restr
 			const float b = Cs[ca + (lane & 31)][kk + (lane >> 5)];
 			acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
 		}
-	};
-	fetch(0, std::integral_constant<int, 0>{});
-	if (nch > 1) fetch(CB_KC, std::integral_constant<int, 1>{});
-	for (int ci = 0; ci < nch; ci += 2) {
-		chunk(ci, std::integral_constant<int, 0>{});
-		if (ci + 1 < nch) chunk(ci + 1, std::integral_constant<int, 1>{});
 	}
 	mfma_operand_guard();
 	n2 += __shfl_xor(n2, 1, 64);
