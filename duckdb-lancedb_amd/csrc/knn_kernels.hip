@@ -2371,6 +2371,9 @@ constexpr int PR_CAP = LHIP_PR_CAP;  // pool entries held in LDS
 constexpr int PR_PER_WAVE = 16;     // candidates per wave and round
 constexpr int PR_CHUNK = PR_WAVES * PR_PER_WAVE;
 constexpr int PR_MAXK = MAX_CAND;   // k of the fast path (k + 8 <= MAX_CAND)
+#ifndef LHIP_PR_SPREAD
+#define LHIP_PR_SPREAD 0  // 1: the pool gather spread over every thread (an A/B: within noise, r06w)
+#endif
 
 // exact distances of NC rows to one query by one wave (each the value
 // exact_distance returns), every row's loads issued before any accumulates.
@@ -2927,6 +2930,55 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 		excl_min = s_hi;
 	}
 	const int n = big ? (int)s_ns : (int)min(total, (unsigned)PR_CAP);
+#if LHIP_PR_SPREAD
+	if (!big) {
+		// each segment's first PR_SPEC entries came with its count (its owner thread
+		// stores them); the rest are spread over every thread, 8 loads in flight,
+		// each entry's segment found by a binary search of the segment offsets in
+		// LDS: one or two memory latencies whatever the longest segment (the tau
+		// mode's ~120 sample segments hold ~64 entries each: 7 rounds of 8 loads
+		// for their owners before, round 6)
+		if (t < n_seg && c && off < (unsigned)PR_CAP) {
+			const unsigned cm = min(min(c, (unsigned)PR_CAP - off), (unsigned)PR_SPEC);
+#pragma unroll
+			for (int u = 0; u < PR_SPEC; ++u)
+				if ((unsigned)u < cm) {
+					keys[off + u] = ((uint64_t)e0[u].x << 32) | e0[u].y;
+					gstat(e0[u].x);
+				}
+		}
+		if (t < n_seg) segc[t] = off;  // segment start offsets (ascending; an empty one shares the next's)
+		__syncthreads();
+		for (int i0 = t; i0 < n; i0 += PR_THREADS * 8) {
+			uint2 e[8];
+			int dst[8];
+#pragma unroll
+			for (int u = 0; u < 8; ++u) {
+				const int i = i0 + u * PR_THREADS;
+				dst[u] = -1;
+				if (i < n) {
+					int lo = 0, hi = n_seg - 1;  // the last segment starting at or before i
+					while (lo < hi) {
+						const int mid = (lo + hi + 1) >> 1;
+						if (segc[mid] <= (unsigned)i) lo = mid;
+						else hi = mid - 1;
+					}
+					const unsigned j = (unsigned)i - segc[lo];
+					if (j >= (unsigned)PR_SPEC) {
+						e[u] = seg_pool[((int64_t)lo * nq + q) * seg_cap + j];
+						dst[u] = i;
+					}
+				}
+			}
+#pragma unroll
+			for (int u = 0; u < 8; ++u)
+				if (dst[u] >= 0) {
+					keys[dst[u]] = ((uint64_t)e[u].x << 32) | e[u].y;
+					gstat(e[u].x);
+				}
+		}
+	}
+#else
 	if (!big && t < n_seg && c && off < (unsigned)PR_CAP) {
 		const uint2 *seg = seg_pool + ((int64_t)t * nq + q) * seg_cap;
 		const unsigned cm = min(c, (unsigned)PR_CAP - off);
@@ -2949,6 +3001,7 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 				}
 		}
 	}
+#endif
 	// finite bounds (key < KEY_INF), NaN bounds, the smallest non-finite key and
 	// the finite range, from the gather (big: NaN bounds were counted over the
 	// whole pool above)
