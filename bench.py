@@ -102,6 +102,10 @@ def parse():
                          "flight (the synchronous figure is reported beside the pipelined one either way)")
     ap.add_argument("--no-host-batch", action="store_true",
                     help="N = 1 flat configs: skip the extra host-buffer leg (H2D + D2H timed, SURVEY.md §8d QPS)")
+    ap.add_argument("--exchange-rehearsal", action="store_true",
+                    help="flat configs, one GPU: a one-rank RCCL process group and the multi-rank exchange "
+                         "(packed all-gather + device merge) on every batch, to exercise that path without a "
+                         "multi-GPU node")
     ap.add_argument("--no-sync-leg", action="store_true",
                     help="IVF configs: skip the extra synchronous-call leg (kernel traces of the pipelined steps)")
     ap.add_argument("--dry-run", action="store_true",
@@ -742,6 +746,17 @@ def main():
         import torch.distributed as dist
 
         dist.init_process_group("nccl", device_id=dev)
+    elif a.exchange_rehearsal:
+        import socket
+
+        import torch.distributed as dist
+
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(port))
+        dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
     L = lance_hip.lib()
 
     N, D, K, B = a.n, a.dim, a.k, a.batch
@@ -788,7 +803,7 @@ def main():
     from lance_hip.sharded import AsyncPipeline, ShardedPipeline, ShardedSearch, hip_device_merge, hip_device_search
 
     searcher = ShardedSearch(hip_device_search(L, h, D), hip_device_merge(L), label_offset=s0, dist=dist,
-                             world=world)
+                             world=world, force_exchange=a.exchange_rehearsal)
     torch.cuda.synchronize()
 
     if a.api != "device" and world > 1:
@@ -804,7 +819,7 @@ def main():
     pipe = None
     if pipelined:
         pipe = AsyncPipeline(L, h, D)
-        if world > 1:
+        if world > 1 or a.exchange_rehearsal:
             pipe = ShardedPipeline(pipe, searcher)
     last_out = [None]
 
@@ -1022,6 +1037,8 @@ def main():
                        "parallelism": (f"inproc-rowshard{len(inproc_devs.split(','))}" if inproc_devs
                                        else f"rowshard{world}"),
                        **({"devices": inproc_devs} if inproc_devs else {}),
+                       **({"exchange": "rehearsal: one-rank RCCL group, packed all-gather + device merge per batch"}
+                          if a.exchange_rehearsal and world == 1 else {}),
                        "scan_copy": a.scan_copy,
                        **({"options": a.opt} if a.opt else {})},
             "recall_at_10": recall,

@@ -30,12 +30,15 @@ class ShardedSearch:
     """
 
     def __init__(self, local_search: Callable, merge: Callable, label_offset: int, dist=None,
-                 world: int = 1):
+                 world: int = 1, force_exchange: bool = False):
         self.local_search = local_search
         self.merge = merge
         self.label_offset = int(label_offset)
         self.dist = dist
         self.world = int(world)
+        # (force_exchange: a one-rank rehearsal of the multi-rank path — the packed
+        # all-gather and the device merge run even for world == 1)
+        self.force_exchange = bool(force_exchange)
         self._bufs = None
 
     def search(self, Q, k: int, **kw):
@@ -43,7 +46,7 @@ class ShardedSearch:
 
     def exchange(self, lab, dis, cnt):
         """This shard's top-k lists (local labels) -> the merged global lists."""
-        if self.world == 1:
+        if self.world == 1 and not self.force_exchange:
             return lab, dis, cnt
         # local -> global labels (unused slots stay -1)
         import torch

@@ -324,7 +324,11 @@ int64_t lance_hip_search_batch_device_async(void *handle, const float *d_queries
  * (<= 0: all of them).  0 or -1. */
 int32_t lance_hip_search_wait(void *handle, int64_t ticket, char *err_buf, int err_buf_len);
 
-/* Device-pointer variant of lance_hip_merge_topk (current device, null stream). */
+/* Device-pointer variant of lance_hip_merge_topk (current device): enqueued on
+ * the null stream behind whatever the caller put there (e.g. the all-gather of
+ * the partial lists) and returns without waiting; the outputs are ready in that
+ * stream's order (a host read through the null stream, or a synchronize, sees
+ * them).  Returns nq or -1 (launch errors only). */
 int32_t lance_hip_merge_topk_device(int32_t nshard, int32_t nq, int32_t k, const int64_t *d_part_labels,
                                     const float *d_part_dists, const int32_t *d_part_counts, int64_t *d_out_labels,
                                     float *d_out_dists, int32_t *d_out_counts, char *err_buf, int err_buf_len);
