@@ -103,9 +103,13 @@ def parse():
     ap.add_argument("--no-host-batch", action="store_true",
                     help="N = 1 flat configs: skip the extra host-buffer leg (H2D + D2H timed, SURVEY.md §8d QPS)")
     ap.add_argument("--exchange-rehearsal", action="store_true",
-                    help="flat configs, one GPU: a one-rank RCCL process group and the multi-rank exchange "
+                    help="one GPU: a one-rank RCCL process group and the multi-rank exchange "
                          "(packed all-gather + device merge) on every batch, to exercise that path without a "
                          "multi-GPU node")
+    ap.add_argument("--exchange", choices=["packed", "generic"], default="packed",
+                    help="N > 1 / rehearsal exchange: packed (the search writes into the rank's packed row, one "
+                         "all-gather + lance_hip_merge_topk_packed) or generic (label shift, pack, all-gather, "
+                         "unpack copies, lance_hip_merge_topk_device)")
     ap.add_argument("--no-sync-leg", action="store_true",
                     help="IVF configs: skip the extra synchronous-call leg (kernel traces of the pipelined steps)")
     ap.add_argument("--dry-run", action="store_true",
@@ -390,6 +394,38 @@ def cpu_threads(a):
     return a.cpu_threads or host_cpus()["usable"]
 
 
+def init_dist(a, world, dev):
+    """torch.distributed for N > 1 (nccl = RCCL), or the one-rank nccl group of
+    --exchange-rehearsal; None otherwise."""
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+        return dist
+    if a.exchange_rehearsal:
+        import socket
+
+        import torch.distributed as dist
+
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(port))
+        dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
+        return dist
+    return None
+
+
+def exchange_note(a, world, pipelined):
+    if not (a.exchange_rehearsal or world > 1):
+        return {}
+    return {"exchange": ("rehearsal: one-rank RCCL group, " if world == 1 else "")
+            + ("packed: one all-gather of the rank's packed row + lance_hip_merge_topk_packed"
+               if a.exchange == "packed" and pipelined else
+               "generic: label shift + pack + all-gather + unpack + lance_hip_merge_topk_device") + " per batch"}
+
+
 def main_ivf(a):
     """IVF configs (C4 IVF-Flat / C5 IVF-PQ of BASELINE.json): every rank holds
     a shard of a.n rows (the 8-GPU configs' 100M rows = 8 x 12.5M), rank 0
@@ -402,11 +438,7 @@ def main_ivf(a):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group("nccl", device_id=dev)
+    dist = init_dist(a, world, dev)
     L = lance_hip.lib()
     N, D, K, B = a.n, a.dim, a.k, a.batch
     s0 = rank * N  # global label offset of this shard
@@ -461,10 +493,12 @@ def main_ivf(a):
     BG = B * world
     qids = torch.randint(0, NCENT, (BG,), generator=g, device=dev)
     Q = (centers[qids] + SIGMA * torch.randn((BG, D), generator=g, device=dev, dtype=torch.float32)).contiguous()
-    from lance_hip.sharded import AsyncPipeline, ShardedPipeline, ShardedSearch, hip_device_merge, hip_device_search
+    from lance_hip.sharded import (AsyncPipeline, ShardedPipeline, ShardedSearch, hip_device_merge, hip_device_search,
+                                   hip_packed_merge)
 
     searcher = ShardedSearch(hip_device_search(L, h, D, nprobes=a.nprobe, refine_factor=a.refine),
-                             hip_device_merge(L), label_offset=s0, dist=dist, world=world)
+                             hip_device_merge(L), label_offset=s0, dist=dist, world=world,
+                             force_exchange=a.exchange_rehearsal, merge_packed=hip_packed_merge(L))
     torch.cuda.synchronize()
 
     if a.api != "device" and world > 1:
@@ -478,8 +512,10 @@ def main_ivf(a):
     pipelined = a.api == "device" and not a.sync
     pipe = None
     if pipelined:
-        pipe = AsyncPipeline(L, h, D, nprobes=a.nprobe, refine_factor=a.refine)
-        if world > 1:
+        pipe = AsyncPipeline(L, h, D, nprobes=a.nprobe, refine_factor=a.refine,
+                             packed=(world > 1 or a.exchange_rehearsal) and a.exchange == "packed",
+                             label_offset=s0)
+        if world > 1 or a.exchange_rehearsal:
             pipe = ShardedPipeline(pipe, searcher)
     last_out = [None]
 
@@ -624,6 +660,7 @@ def main_ivf(a):
                        "n_per_gpu": N, "n_total": N * world, "dim": D, "k": K, "global_batch": BG,
                        "metric": a.metric, "index_type": a.index_type, "nlist": a.nlist, "nprobe": a.nprobe,
                        "m": a.m, "refine_factor": a.refine, "parallelism": f"rowshard{world}",
+                       **exchange_note(a, world, pipelined),
                        **({"pq_query": a.pq_query or "f32", "pq_scan": a.pq_scan or "fast"}
                           if a.index_type == "ivf_pq" else {}),
                        **({"options": a.opt} if a.opt else {})},
@@ -741,22 +778,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group("nccl", device_id=dev)
-    elif a.exchange_rehearsal:
-        import socket
-
-        import torch.distributed as dist
-
-        with socket.socket() as sk:
-            sk.bind(("127.0.0.1", 0))
-            port = sk.getsockname()[1]
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", str(port))
-        dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
+    dist = init_dist(a, world, dev)
     L = lance_hip.lib()
 
     N, D, K, B = a.n, a.dim, a.k, a.batch
@@ -800,10 +822,11 @@ def main():
     Q = torch.randn((BG, D), generator=g, device=dev, dtype=torch.float32)
     if a.normalize:
         Q /= torch.linalg.vector_norm(Q, dim=1, keepdim=True)
-    from lance_hip.sharded import AsyncPipeline, ShardedPipeline, ShardedSearch, hip_device_merge, hip_device_search
+    from lance_hip.sharded import (AsyncPipeline, ShardedPipeline, ShardedSearch, hip_device_merge, hip_device_search,
+                                   hip_packed_merge)
 
     searcher = ShardedSearch(hip_device_search(L, h, D), hip_device_merge(L), label_offset=s0, dist=dist,
-                             world=world, force_exchange=a.exchange_rehearsal)
+                             world=world, force_exchange=a.exchange_rehearsal, merge_packed=hip_packed_merge(L))
     torch.cuda.synchronize()
 
     if a.api != "device" and world > 1:
@@ -818,7 +841,8 @@ def main():
     pipelined = a.api == "device" and not a.sync
     pipe = None
     if pipelined:
-        pipe = AsyncPipeline(L, h, D)
+        pipe = AsyncPipeline(L, h, D, packed=(world > 1 or a.exchange_rehearsal) and a.exchange == "packed",
+                             label_offset=s0)
         if world > 1 or a.exchange_rehearsal:
             pipe = ShardedPipeline(pipe, searcher)
     last_out = [None]
@@ -1037,8 +1061,7 @@ def main():
                        "parallelism": (f"inproc-rowshard{len(inproc_devs.split(','))}" if inproc_devs
                                        else f"rowshard{world}"),
                        **({"devices": inproc_devs} if inproc_devs else {}),
-                       **({"exchange": "rehearsal: one-rank RCCL group, packed all-gather + device merge per batch"}
-                          if a.exchange_rehearsal and world == 1 else {}),
+                       **exchange_note(a, world, pipelined),
                        "scan_copy": a.scan_copy,
                        **({"options": a.opt} if a.opt else {})},
             "recall_at_10": recall,

@@ -258,6 +258,13 @@ void launch_merge_topk(int nshard, int nq, int k, const int64_t *part_labels, co
                        const int *part_counts, int64_t *out_labels, float *out_dists, int *out_counts,
                        hipStream_t st, int tie_desc);
 
+// The same merge over nshard packed rows of one all-gather (row s at
+// gathered + s * stride int32 words: labels int64[nq*k], dists f32[nq*k],
+// counts i32[nq], the shard's label offset int64 in the last two words);
+// local labels >= 0 are shifted by their shard's offset.  stride is even.
+void launch_merge_packed(int nshard, int nq, int k, const int32_t *gathered, int64_t stride, int64_t *out_labels,
+                         float *out_dists, int *out_counts, hipStream_t st, int tie_desc);
+
 // Copies the first n_live entries of a sorted fallback result into the outputs.
 void launch_copy_fallback(const float *keys, const int64_t *vals, int64_t n_live, int k, int qi,
                           int64_t *out_labels, float *out_dists, int *out_counts, hipStream_t st);

@@ -4089,6 +4089,104 @@ void launch_merge_topk(int nshard, int nq, int k, const int64_t *part_labels, co
 	                                                   out_labels, out_dists, out_counts, tie_x64(tie_desc));
 }
 
+// Merge of packed shard rows as one all-gather delivers them (row s at
+// g + s * stride, int32 units: labels int64[nq*k], dists f32[nq*k], counts
+// i32[nq], and the shard's label offset int64 in the row's last two words).
+// The local -> global label shift happens here, so the exchange is the
+// all-gather and this one launch.  LDS: the query's live entries of every
+// shard are staged compacted (nshard * k <= MP_LDS_CAP), then each entry's rank
+// is its count of (distance, label)-smaller entries, as in merge_topk_kernel.
+#define MP_LDS_CAP 4096
+
+template <bool LDS>
+__global__ __launch_bounds__(256) void merge_packed_kernel(int nshard, int nq, int k, const int32_t *__restrict__ g,
+                                                           int64_t stride, int64_t *__restrict__ out_labels,
+                                                           float *__restrict__ out_dists,
+                                                           int *__restrict__ out_counts, int64_t tx) {
+	extern __shared__ __align__(16) unsigned char mp_smem[];
+	const int q = blockIdx.x;
+	const int t = threadIdx.x;
+	const int64_t nqk = (int64_t)nq * k;
+	auto lab = [&](int s, int i) { return reinterpret_cast<const int64_t *>(g + s * stride)[(int64_t)q * k + i]; };
+	auto dis = [&](int s, int i) { return reinterpret_cast<const float *>(g + s * stride + 2 * nqk)[(int64_t)q * k + i]; };
+	auto cnt = [&](int s) {
+		const int c = g[s * stride + 3 * nqk + q];
+		return c < 0 ? 0 : (c < k ? c : k);
+	};
+	auto off = [&](int s) { return *reinterpret_cast<const int64_t *>(g + s * stride + stride - 2); };
+	auto glob = [&](int64_t l, int s) { return l >= 0 ? l + off(s) : l; };
+	int m = 0;
+	if (LDS) {
+		const int cap = nshard * k;
+		int64_t *sl = reinterpret_cast<int64_t *>(mp_smem);
+		float *sd = reinterpret_cast<float *>(sl + cap);
+		int *sbase = reinterpret_cast<int *>(sd + cap);
+		if (t == 0) {
+			for (int s = 0; s < nshard; ++s) {
+				sbase[s] = m;
+				m += cnt(s);
+			}
+			sbase[nshard] = m;
+		}
+		__syncthreads();
+		m = sbase[nshard];
+		for (int e = t; e < cap; e += 256) {
+			const int s = e / k, i = e - s * k;
+			const int b = sbase[s];
+			if (i < sbase[s + 1] - b) {
+				sl[b + i] = glob(lab(s, i), s);
+				sd[b + i] = dis(s, i);
+			}
+		}
+		__syncthreads();
+		for (int e = t; e < m; e += 256) {
+			const float d = sd[e];
+			const int64_t l = sl[e];
+			int rank = 0;
+			for (int j = 0; j < m && rank < k; ++j) rank += hit_less(sd[j], sl[j], d, l, tx) ? 1 : 0;
+			if (rank < k) {
+				out_labels[(int64_t)q * k + rank] = l;
+				out_dists[(int64_t)q * k + rank] = d;
+			}
+		}
+	} else {
+		for (int s = 0; s < nshard; ++s) m += cnt(s);
+		for (int64_t e = t; e < (int64_t)nshard * k; e += 256) {
+			const int s = (int)(e / k), i = (int)(e - (int64_t)s * k);
+			if (i >= cnt(s)) continue;
+			const float d = dis(s, i);
+			const int64_t l = glob(lab(s, i), s);
+			int rank = 0;
+			for (int s2 = 0; s2 < nshard && rank < k; ++s2) {
+				const int c2 = cnt(s2);
+				for (int j = 0; j < c2; ++j) rank += hit_less(dis(s2, j), glob(lab(s2, j), s2), d, l, tx) ? 1 : 0;
+			}
+			if (rank < k) {
+				out_labels[(int64_t)q * k + rank] = l;
+				out_dists[(int64_t)q * k + rank] = d;
+			}
+		}
+	}
+	const int nout = m < k ? m : k;
+	for (int i = nout + t; i < k; i += 256) {
+		out_labels[(int64_t)q * k + i] = -1;
+		out_dists[(int64_t)q * k + i] = __builtin_nanf("");
+	}
+	if (t == 0) out_counts[q] = nout;
+}
+
+void launch_merge_packed(int nshard, int nq, int k, const int32_t *gathered, int64_t stride, int64_t *out_labels,
+                         float *out_dists, int *out_counts, hipStream_t st, int tie_desc) {
+	if ((int64_t)nshard * k <= MP_LDS_CAP) {
+		const size_t lds = (size_t)nshard * k * (sizeof(int64_t) + sizeof(float)) + (size_t)(nshard + 1) * sizeof(int);
+		merge_packed_kernel<true><<<dim3(nq), dim3(256), lds, st>>>(nshard, nq, k, gathered, stride, out_labels,
+		                                                           out_dists, out_counts, tie_x64(tie_desc));
+	} else {
+		merge_packed_kernel<false><<<dim3(nq), dim3(256), 0, st>>>(nshard, nq, k, gathered, stride, out_labels,
+		                                                          out_dists, out_counts, tie_x64(tie_desc));
+	}
+}
+
 // ---------------------------------------------------------------------------
 // compaction gather
 // ---------------------------------------------------------------------------

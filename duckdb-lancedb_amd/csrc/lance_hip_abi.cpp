@@ -1808,6 +1808,30 @@ int32_t lance_hip_merge_topk_device(int32_t nshard, int32_t nq, int32_t k, const
 	API_GUARD("merge_topk failed: ", -1)
 }
 
+int64_t lance_hip_merge_packed_stride(int32_t nq, int32_t k) {
+	if (nq <= 0 || k <= 0) return -1;
+	const int64_t body = 3 * (int64_t)nq * k + nq;  // labels (2 words each), dists, counts
+	return (body + 1) / 2 * 2 + 2;                  // even, then the label offset
+}
+
+int32_t lance_hip_merge_topk_packed(int32_t nshard, int32_t nq, int32_t k, const int32_t *d_gathered,
+                                    int64_t row_stride, int64_t *d_out_labels, float *d_out_dists,
+                                    int32_t *d_out_counts, char *err_buf, int err_buf_len) {
+	try {
+		if (nshard <= 0 || nq <= 0 || k <= 0) return 0;
+		if (row_stride < lance_hip_merge_packed_stride(nq, k) || (row_stride & 1) ||
+		    (reinterpret_cast<uintptr_t>(d_gathered) & 7))
+			throw std::invalid_argument("row_stride must be even and >= lance_hip_merge_packed_stride(nq, k), "
+			                            "the gathered buffer 8-byte aligned");
+		// stream-ordered on the null stream like lance_hip_merge_topk_device
+		lhip::launch_merge_packed(nshard, nq, k, d_gathered, row_stride, d_out_labels, d_out_dists, d_out_counts,
+		                          nullptr, lhip::env_tie());
+		HIPCHK(hipGetLastError());
+		return nq;
+	}
+	API_GUARD("merge_topk failed: ", -1)
+}
+
 // ---- IVF model / layout (multi-GPU model broadcast, parity tests) ----------
 
 int32_t lance_hip_ivf_info(void *handle, int64_t *out, int32_t n) {

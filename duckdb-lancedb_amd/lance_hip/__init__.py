@@ -79,6 +79,9 @@ _SIGNATURES = [
     ("lance_hip_search_wait", i32, [c_void_p, i64, c_char_p, c_int]),
     ("lance_hip_merge_topk_device", i32,
      [i32, i32, i32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_char_p, c_int]),
+    ("lance_hip_merge_packed_stride", i64, [i32, i32]),
+    ("lance_hip_merge_topk_packed", i32,
+     [i32, i32, i32, c_void_p, i64, c_void_p, c_void_p, c_void_p, c_char_p, c_int]),
     ("lance_hip_ivf_info", i32, [c_void_p, c_void_p, i32]),
     ("lance_hip_ivf_export", i32,
      [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_char_p, c_int]),

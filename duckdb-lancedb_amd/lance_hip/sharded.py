@@ -9,6 +9,14 @@ its shard for the same query batch; the per-shard top-k lists are exchanged by
 ONE all-gather (RCCL over xGMI on GPUs, gloo in CPU tests; labels, distances
 and counts packed into one int32 buffer) and merged on the
 device by ``lance_hip_merge_topk_device`` under the (distance, label) order.
+
+Packed exchange (``AsyncPipeline(packed=True)`` + ``hip_packed_merge``): the
+search writes its outputs straight into the rank's packed row, whose last two
+words hold the rank's label offset, and the merge kernel reads the gathered
+rows in place and shifts the labels itself — the exchange is then two
+launches (the all-gather and ``lance_hip_merge_topk_packed``) where the
+generic path needs eight (label shift, pack, three unpack copies, ...), and
+every launch waits for a CU the next batch's scan is holding.
 """
 from __future__ import annotations
 
@@ -20,6 +28,49 @@ def shard_range(n_total: int, world: int, rank: int) -> Tuple[int, int]:
     return rank * n_total // world, (rank + 1) * n_total // world
 
 
+class Outputs(tuple):
+    """``(labels, dists, counts)``; ``pack`` is the packed int32 row the three
+    are views of (``None`` when they are separate tensors)."""
+    pack = None
+
+
+def packed_stride(nq: int, k: int) -> int:
+    """int32 words per packed row (= ``lance_hip_merge_packed_stride``): the
+    lists (3 * nq * k + nq words) rounded up to even, then the label offset."""
+    body = 3 * nq * k + nq
+    return (body + 1) // 2 * 2 + 2
+
+
+def unpack_rows(g, nq: int, k: int):
+    """Gathered packed rows ``g[world, stride]`` -> ``(labels[world,nq,k] with
+    each row's label offset applied, dists, counts)``: the layout the packed
+    merge kernel reads, restated with torch views (CPU tests' stand-in)."""
+    import torch
+
+    nqk = nq * k
+    off = g[:, -2:].contiguous().view(torch.int64)  # [world, 1]
+    gl = g[:, :2 * nqk].contiguous().view(torch.int64).view(-1, nq, k)
+    gl = torch.where(gl >= 0, gl + off.view(-1, 1, 1), gl)
+    gd = g[:, 2 * nqk:3 * nqk].contiguous().view(torch.float32).view(-1, nq, k)
+    gc = g[:, 3 * nqk:3 * nqk + nq].contiguous()
+    return gl, gd, gc
+
+
+def packed_outputs(nq: int, k: int, device, label_offset: int, stride: int):
+    """Output tensors as views of one packed row of ``stride`` int32 words
+    (``lance_hip_merge_packed_stride``): labels int64[nq,k], dists f32[nq,k],
+    counts i32[nq], the label offset (int64) in the last two words."""
+    import torch
+
+    buf = torch.empty((stride,), dtype=torch.int32, device=device)
+    nqk = nq * k
+    o = Outputs((buf[:2 * nqk].view(torch.int64).view(nq, k), buf[2 * nqk:3 * nqk].view(torch.float32).view(nq, k),
+                 buf[3 * nqk:3 * nqk + nq]))
+    buf[stride - 2:].view(torch.int64).fill_(int(label_offset))
+    o.pack = buf
+    return o
+
+
 class ShardedSearch:
     """One rank's view of a sharded index.
 
@@ -27,10 +78,12 @@ class ShardedSearch:
     searches this rank's shard (local labels).  ``merge(gl, gd, gc) -> same``
     merges ``world`` gathered lists; ``dist`` is ``torch.distributed`` (or None
     for a single shard).  Tensors may live on the GPU (RCCL) or the CPU (gloo).
+    ``merge_packed(g[world, stride], nq, k) -> same`` (optional) merges gathered
+    packed rows; it is used when the outputs carry their ``pack``.
     """
 
     def __init__(self, local_search: Callable, merge: Callable, label_offset: int, dist=None,
-                 world: int = 1, force_exchange: bool = False):
+                 world: int = 1, force_exchange: bool = False, merge_packed: Optional[Callable] = None):
         self.local_search = local_search
         self.merge = merge
         self.label_offset = int(label_offset)
@@ -39,15 +92,31 @@ class ShardedSearch:
         # (force_exchange: a one-rank rehearsal of the multi-rank path — the packed
         # all-gather and the device merge run even for world == 1)
         self.force_exchange = bool(force_exchange)
+        self.merge_packed = merge_packed
         self._bufs = None
 
     def search(self, Q, k: int, **kw):
         return self.exchange(*self.local_search(Q, k, **kw))
 
-    def exchange(self, lab, dis, cnt):
-        """This shard's top-k lists (local labels) -> the merged global lists."""
+    def _gather(self, pack):
+        import torch
+
+        key = (pack.numel(), pack.device)
+        if self._bufs is None or self._bufs[0] != key:
+            self._bufs = (key, torch.empty((self.world * pack.numel(),), dtype=torch.int32, device=pack.device))
+        g = self._bufs[1]
+        self.dist.all_gather_into_tensor(g, pack)
+        return g.view(self.world, -1)
+
+    def exchange(self, lab, dis, cnt, pack=None):
+        """This shard's top-k lists (local labels) -> the merged global lists.
+        ``pack``: the packed row the lists are views of (``packed_outputs``,
+        label offset already in its tail) — gathered and merged as it is."""
         if self.world == 1 and not self.force_exchange:
             return lab, dis, cnt
+        if pack is not None and self.merge_packed is not None:
+            nq, kk = lab.shape
+            return self.merge_packed(self._gather(pack), nq, kk)
         # local -> global labels (unused slots stay -1)
         import torch
 
@@ -58,12 +127,7 @@ class ShardedSearch:
         # not bytes, is the cost at these sizes: 3 all-gathers would pay it 3x)
         pack = torch.cat([lab.contiguous().view(torch.int32).reshape(-1),
                           dis.contiguous().view(torch.int32).reshape(-1), cnt.to(torch.int32).reshape(-1)])
-        key = (pack.numel(), pack.device)
-        if self._bufs is None or self._bufs[0] != key:
-            self._bufs = (key, torch.empty((self.world * pack.numel(),), dtype=torch.int32, device=pack.device))
-        g = self._bufs[1]
-        self.dist.all_gather_into_tensor(g, pack)
-        g = g.view(self.world, -1)
+        g = self._gather(pack)
         nl, nd = 2 * nq * kk, nq * kk
         gl = g[:, :nl].contiguous().view(torch.int64).view(self.world, nq, kk)
         gd = g[:, nl:nl + nd].contiguous().view(torch.float32).view(self.world, nq, kk)
@@ -85,6 +149,29 @@ def hip_device_merge(lib, err_len: int = 2048):
         e = ctypes.create_string_buffer(err_len)
         r = lib.lance_hip_merge_topk_device(world, nq, k, gl.data_ptr(), gd.data_ptr(), gc.data_ptr(),
                                             ol.data_ptr(), od.data_ptr(), oc.data_ptr(), e, err_len)
+        if r < 0:
+            raise RuntimeError(e.value.decode())
+        return ol, od, oc
+
+    return merge
+
+
+def hip_packed_merge(lib, err_len: int = 2048):
+    """The packed-exchange merge: ``lance_hip_merge_topk_packed`` over the
+    gathered rows ``g[world, stride]`` on the current device."""
+    import ctypes
+
+    import torch
+
+    e = ctypes.create_string_buffer(err_len)
+
+    def merge(g, nq, k):
+        world, stride = g.shape
+        ol = torch.empty((nq, k), dtype=torch.int64, device=g.device)
+        od = torch.empty((nq, k), dtype=torch.float32, device=g.device)
+        oc = torch.empty((nq,), dtype=torch.int32, device=g.device)
+        r = lib.lance_hip_merge_topk_packed(world, nq, k, g.data_ptr(), stride, ol.data_ptr(), od.data_ptr(),
+                                            oc.data_ptr(), e, err_len)
         if r < 0:
             raise RuntimeError(e.value.decode())
         return ol, od, oc
@@ -141,9 +228,14 @@ class AsyncPipeline:
     temporary must not go back to torch's allocator before the wait).  Output
     tensors are double-buffered per shape: the tensors a wait returns stay valid
     until the next-but-one ``submit`` of the same shape (clone them to keep
-    them longer)."""
+    them longer).
 
-    def __init__(self, lib, handle, dim: int, nprobes: int = 20, refine_factor: int = 1, err_len: int = 2048):
+    ``packed=True``: the outputs are views of one packed row per buffer
+    (``packed_outputs``, carrying ``label_offset``), for ``ShardedSearch``'s
+    packed exchange."""
+
+    def __init__(self, lib, handle, dim: int, nprobes: int = 20, refine_factor: int = 1, err_len: int = 2048,
+                 packed: bool = False, label_offset: int = 0):
         import ctypes
 
         self.lib, self.h, self.dim = lib, handle, dim
@@ -151,6 +243,7 @@ class AsyncPipeline:
         self.e = ctypes.create_string_buffer(err_len)
         self.err_len = err_len
         self.outs = {}
+        self.packed, self.label_offset = bool(packed), int(label_offset)
         self.completed = {}
         self.pending = []  # (ticket, outputs, query tensor held until the wait)
         self.i = 0
@@ -159,6 +252,9 @@ class AsyncPipeline:
         import torch
 
         key = (nq, k, dev, j)
+        if key not in self.outs and self.packed:
+            self.outs[key] = packed_outputs(nq, k, dev, self.label_offset,
+                                            int(self.lib.lance_hip_merge_packed_stride(nq, k)))
         if key not in self.outs:
             self.outs[key] = (torch.empty((nq, k), dtype=torch.int64, device=dev),
                               torch.empty((nq, k), dtype=torch.float32, device=dev),
@@ -227,13 +323,15 @@ class ShardedPipeline:
         t = self.pipe.submit(Q, k)
         out = None
         if self.prev is not None:
-            out = self.sharded.exchange(*self.pipe.wait(self.prev))
+            o = self.pipe.wait(self.prev)
+            out = self.sharded.exchange(*o, pack=getattr(o, "pack", None))
         self.prev = t
         return out
 
     def drain(self):
         if self.prev is None:
             return None
-        out = self.sharded.exchange(*self.pipe.wait(self.prev))
+        o = self.pipe.wait(self.prev)
+        out = self.sharded.exchange(*o, pack=getattr(o, "pack", None))
         self.prev = None
         return out

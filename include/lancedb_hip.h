@@ -333,6 +333,18 @@ int32_t lance_hip_merge_topk_device(int32_t nshard, int32_t nq, int32_t k, const
                                     const float *d_part_dists, const int32_t *d_part_counts, int64_t *d_out_labels,
                                     float *d_out_dists, int32_t *d_out_counts, char *err_buf, int err_buf_len);
 
+/* NEW — the exchange's merge in one launch: nshard packed rows exactly as one
+ * all-gather of every rank's row delivers them.  Row s starts at
+ * d_gathered + s * row_stride (int32 words, 8-byte aligned, row_stride even and
+ * >= lance_hip_merge_packed_stride(nq, k)): labels int64[nq*k] (shard-local),
+ * dists f32[nq*k], counts i32[nq], and in the row's last two words the shard's
+ * label offset (int64); labels >= 0 are shifted by it before the merge.  Same
+ * order, stream and return as lance_hip_merge_topk_device. */
+int64_t lance_hip_merge_packed_stride(int32_t nq, int32_t k);
+int32_t lance_hip_merge_topk_packed(int32_t nshard, int32_t nq, int32_t k, const int32_t *d_gathered,
+                                    int64_t row_stride, int64_t *d_out_labels, float *d_out_dists,
+                                    int32_t *d_out_counts, char *err_buf, int err_buf_len);
+
 /* Merge per-shard partial top-k lists into a global top-k, on the device of
  * the handle (multi-GPU path: shards all-gathered over RCCL).
  * part_labels / part_dists: nshard x nq x k (host pointers), part_counts:

@@ -160,6 +160,95 @@ def test_sharded_pipeline_two_batches_in_flight_cpu(world):
             np.testing.assert_allclose(dd, ed, rtol=1e-6)
 
 
+class _CpuPackedPipe(_CpuPipe):
+    """CPU stand-in for ``AsyncPipeline(packed=True)``: the results land in a
+    packed row (``packed_outputs``) carrying the rank's label offset."""
+
+    def __init__(self, search, label_offset):
+        super().__init__(search)
+        self.off = label_offset
+
+    def submit(self, Q, k):
+        from lance_hip.sharded import packed_outputs, packed_stride
+
+        l, dd, c = self.search(Q, k)
+        o = packed_outputs(l.shape[0], k, "cpu", self.off, packed_stride(l.shape[0], k))
+        for dst, src in zip(o, (l, dd, c)):
+            dst.copy_(src)
+        self.t += 1
+        self.done[self.t] = o
+        return self.t
+
+
+def _cpu_packed_worker(rank, world, port, n, d, k, q, nb, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from lance_hip.sharded import ShardedPipeline, unpack_rows
+    from oracle import flat_knn
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(13)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Qs = [rng.standard_normal((q, d)).astype(np.float32) for _ in range(nb)]
+    s0, s1 = shard_range(n, world, rank)
+    Xs = X[s0:s1]
+
+    def local_search(Qt, kk):
+        l, dd, c = flat_knn.flat_search_batch(Xs, np.arange(s1 - s0), np.ones(s1 - s0, bool), Qt.numpy(), kk)
+        return torch.from_numpy(l), torch.from_numpy(dd), torch.from_numpy(c)
+
+    def no_generic(*_):
+        raise AssertionError("the packed outputs must take the packed exchange")
+
+    sh = ShardedSearch(local_search, no_generic, label_offset=s0, dist=dist, world=world,
+                       merge_packed=lambda g, nq, kk: ref_merge(*unpack_rows(g, nq, kk)))
+    pipe = ShardedPipeline(_CpuPackedPipe(local_search, s0), sh)
+    res = []
+    for Q in Qs:
+        r = pipe.step(torch.from_numpy(Q), k)
+        if r is not None:
+            res.append(tuple(x.numpy() for x in r))
+    res.append(tuple(x.numpy() for x in pipe.drain()))
+    out[rank] = res
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,q", [(2, 4), (3, 5)])
+def test_sharded_pipeline_packed_exchange_cpu(world, q):
+    """The packed exchange (one gathered row per rank, label offsets carried in
+    the rows' tails, odd nq padded): merged lists equal the unsharded search."""
+    from oracle import flat_knn
+
+    n, d, k, nb = 1003, 8, 6, 3
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_cpu_packed_worker, args=(world, _free_port(), n, d, k, q, nb, out), nprocs=world, join=True)
+    rng = np.random.default_rng(13)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Qs = [rng.standard_normal((q, d)).astype(np.float32) for _ in range(nb)]
+    for r in range(world):
+        assert len(out[r]) == nb
+        for Q, (l, dd, c) in zip(Qs, out[r]):
+            el, ed, ec = flat_knn.flat_search_batch(X, np.arange(n), np.ones(n, bool), Q, k)
+            np.testing.assert_array_equal(l, el)
+            np.testing.assert_array_equal(c, ec)
+            np.testing.assert_allclose(dd, ed, rtol=1e-6)
+
+
+def test_packed_stride_matches_the_library():
+    import lance_hip
+    from lance_hip.sharded import packed_stride
+
+    L = lance_hip.lib()
+    for nq, k in ((1, 1), (5, 6), (256, 10), (255, 100), (4096, 1000)):
+        s = packed_stride(nq, k)
+        assert s % 2 == 0 and s >= 3 * nq * k + nq + 2
+        assert L.lance_hip_merge_packed_stride(nq, k) == s
+    assert L.lance_hip_merge_packed_stride(0, 10) == -1
+
+
 def test_shard_range_partitions_exactly():
     for n in (0, 1, 7, 1000, 1_000_000):
         for world in (1, 2, 3, 8):
@@ -258,14 +347,23 @@ def _gpu_scan8_worker(rank, world, port, n, d, k, q, out, pipelined=False):
         l, dd, c = dev_merge(gl.cuda(), gd.cuda(), gc.cuda())
         return l.cpu(), dd.cpu(), c.cpu()
 
-    s = ShardedSearch(local_search, merge, label_offset=s0, dist=dist, world=world)
+    packed = pipelined == "packed"
+    from lance_hip.sharded import hip_packed_merge
+
+    dev_pmerge = hip_packed_merge(L)
+
+    def merge_packed(g, nq, kk):  # the packed exchange's one-launch merge on the device
+        return tuple(x.cpu() for x in dev_pmerge(g.cuda(), nq, kk))
+
+    s = ShardedSearch(local_search, merge, label_offset=s0, dist=dist, world=world,
+                      merge_packed=merge_packed if packed else None)
     if pipelined:
         # bench.py's N > 1 loop: two batches in flight on the handle (the async
         # C-ABI), batch i-1 exchanged while batch i is on the device
         from lance_hip.sharded import AsyncPipeline, ShardedPipeline
 
         lance_hip.LanceHipSetOption(h, "time_kernels", "0")  # (timing forces the synchronous path)
-        ap = AsyncPipeline(L, h, d)
+        ap = AsyncPipeline(L, h, d, packed=packed, label_offset=s0)
 
         class _Pipe:
             held = []  # the device queries stay alive until their batch completes (AsyncPipeline holds them too)
@@ -276,7 +374,14 @@ def _gpu_scan8_worker(rank, world, port, n, d, k, q, out, pipelined=False):
                 return ap.submit(Qd, kk)
 
             def wait(self, t):
-                return tuple(x.cpu() for x in ap.wait(t))
+                from lance_hip.sharded import Outputs
+
+                o = ap.wait(t)
+                r = Outputs(x.cpu() for x in o)
+                if packed:  # (gloo gathers host tensors: the packed row moves as one)
+                    assert o.pack is not None
+                    r.pack = o.pack.cpu()
+                return r
 
         pipe = ShardedPipeline(_Pipe(), s)
         Qs = [torch.from_numpy(Q), torch.from_numpy(Q[::-1].copy()), torch.from_numpy(Q)]
@@ -319,16 +424,19 @@ def test_sharded_scan8_two_ranks_one_gpu():
 
 
 @pytest.mark.gpu
-def test_sharded_scan8_pipelined_two_ranks_one_gpu():
+@pytest.mark.parametrize("exchange", ["generic", "packed"])
+def test_sharded_scan8_pipelined_two_ranks_one_gpu(exchange):
     """The same shards through bench.py's pipelined N > 1 loop (async C-ABI,
     two batches in flight, exchange one batch behind): three batches, each
-    merged result equal to the unsharded exact search, in submission order."""
+    merged result equal to the unsharded exact search, in submission order.
+    packed: the search writes into the rank's packed row (label offset in its
+    tail), gathered as one and merged by lance_hip_merge_topk_packed."""
     from oracle import c_oracle
 
     world, n, d, k, q = 2, 160_000, 768, 10, 256
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_gpu_scan8_worker, args=(world, _free_port(), n, d, k, q, out, True), nprocs=world, join=True)
+    mp.spawn(_gpu_scan8_worker, args=(world, _free_port(), n, d, k, q, out, exchange), nprocs=world, join=True)
     rng = np.random.default_rng(21)
     X = rng.standard_normal((n, d), dtype=np.float32)
     Q = rng.standard_normal((q, d), dtype=np.float32)

@@ -428,6 +428,58 @@ def test_merge_topk_kernel(hip):
         assert list(ol[q, :oc[q]]) == [l for _, l in items]
 
 
+@pytest.mark.parametrize("nshard,nq,k", [(4, 5, 7), (8, 256, 10), (3, 33, 100), (3, 7, 1500)])
+def test_merge_topk_packed_kernel(hip, nshard, nq, k):
+    """lance_hip_merge_topk_packed over gathered packed rows (the exchange's
+    one-launch merge): per-shard label offsets from the rows' tails, ragged
+    counts (0..k, a few out of range), distance ties across shards, -1 slots;
+    (3, 7, 1500) takes the global-memory variant (nshard * k > the LDS cap)."""
+    import torch
+
+    from lance_hip.sharded import hip_packed_merge, packed_outputs, packed_stride
+
+    rng = np.random.default_rng(40 + k)
+    stride = packed_stride(nq, k)
+    offs = [int(s * 10**9 + rng.integers(0, 1000)) for s in range(nshard)]
+    pl = np.full((nshard, nq, k), -1, np.int64)
+    pd = np.full((nshard, nq, k), np.nan, np.float32)
+    pc = rng.integers(0, k + 1, (nshard, nq)).astype(np.int32)
+    pc[0, 0] = k + 5  # counts above k are read as k
+    for s in range(nshard):
+        for q in range(nq):
+            c = min(pc[s, q], k)
+            pd[s, q, :c] = np.sort(rng.integers(0, 3 * k, c).astype(np.float32))
+            pl[s, q, :c] = rng.permutation(5 * k)[:c]
+    rows = []
+    for s in range(nshard):
+        o = packed_outputs(nq, k, "cuda", offs[s], stride)
+        o[0].copy_(torch.from_numpy(pl[s]))
+        o[1].copy_(torch.from_numpy(pd[s]))
+        o[2].copy_(torch.from_numpy(pc[s]))
+        rows.append(o.pack)
+    g = torch.stack(rows)
+    ol, od, oc = (x.cpu().numpy() for x in hip_packed_merge(hip.lib())(g, nq, k))
+    desc = flat_knn.tie_desc(None)
+    for q in range(nq):
+        items = [(pd[s, q, i], pl[s, q, i] + offs[s]) for s in range(nshard) for i in range(min(pc[s, q], k))]
+        items.sort(key=lambda t: (t[0], -t[1] if desc else t[1]))
+        items = items[:k]
+        assert oc[q] == len(items)
+        assert list(ol[q, :oc[q]]) == [l for _, l in items]
+        assert list(od[q, :oc[q]]) == [d for d, _ in items]
+        assert (ol[q, oc[q]:] == -1).all() and np.isnan(od[q, oc[q]:]).all()
+
+
+def test_merge_topk_packed_rejects_bad_strides(hip):
+    import torch
+
+    from lance_hip.sharded import hip_packed_merge, packed_stride
+
+    g = torch.zeros((2, packed_stride(4, 3) - 2), dtype=torch.int32, device="cuda")
+    with pytest.raises(RuntimeError, match="row_stride"):
+        hip_packed_merge(hip.lib())(g, 4, 3)
+
+
 def test_cosine_repeated_searches_are_stable(hip, mk):
     # regression: the cosine epilogue once read accumulators before the last
     # MFMAs had landed (~1% of queries, timing dependent); 40 repeats x 40 queries
