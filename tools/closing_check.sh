@@ -6,6 +6,8 @@
 #      the C5 step's kernel stats
 #   C: PMC traffic passes of each config's dominant kernel (tools/pmc_configs.sh)
 #   S: one config's step: bench line + rocprofv3 kernel trace (CFG=c2|nstar|c4|c5, STEPS)
+#   E: the multi-rank exchange rehearsed on one GPU (one-rank RCCL group): the rehearsal test, then
+#      C2 / per-rank shapes / C5 with the packed and the generic exchange beside no exchange
 source tools/gpu_step.sh
 T=${2:-r06x}
 case $1 in
@@ -43,5 +45,17 @@ S)
 	python3 tools/trace_kernels.py gpurun_out/${T}_prof_${C}/run_kernel_trace.csv $N > gpurun_out/${T}_${C}_step_kernels.txt 2>&1
 	rm -f gpurun_out/${T}_prof_${C}/run_kernel_trace.csv
 	cat gpurun_out/${T}_${C}_step_kernels.txt
+	;;
+E)
+	step ${T}_xtests 700 python -u -m pytest tests/test_distributed.py tests/test_gpu_exchange_rehearsal.py -m gpu -x -q --timeout 300 --timeout-method thread
+	R="--no-cpu-baseline --no-host-batch --exchange-rehearsal"
+	step ${T}_x_c2_packed 400 python -u bench.py --steps 20 $R
+	step ${T}_x_c2_generic 400 python -u bench.py --steps 20 $R --exchange generic
+	step ${T}_x_c2 400 python -u bench.py --steps 20 --no-cpu-baseline --no-host-batch
+	step ${T}_x_rank_packed 400 python -u bench.py --n 125000 --steps 30 $R
+	step ${T}_x_rank_generic 400 python -u bench.py --n 125000 --steps 30 $R --exchange generic
+	step ${T}_x_rank 400 python -u bench.py --n 125000 --steps 30 --no-cpu-baseline --no-host-batch
+	step ${T}_x_nstar_rank_packed 400 python -u bench.py --n 1250000 --steps 30 $R
+	step ${T}_x_c5_packed 400 python -u bench.py --config c5 --steps 10 --no-cpu-baseline --exchange-rehearsal --no-sync-leg
 	;;
 esac
