@@ -2366,10 +2366,8 @@ constexpr int PR_MIN_WAVES = PR_THREADS == 256 ? 2 : 1;  // waves per SIMD the r
 constexpr int PR_NSTAMP = 32, PR_PROF_Q = 4096;
 __device__ uint64_t g_pr_stamps[PR_PROF_Q * (PR_NSTAMP + 3)];
 #endif
-constexpr int PR_WAVES = PR_THREADS / 64;
 constexpr int PR_CAP = LHIP_PR_CAP;  // pool entries held in LDS
 constexpr int PR_PER_WAVE = 16;     // candidates per wave and round
-constexpr int PR_CHUNK = PR_WAVES * PR_PER_WAVE;
 constexpr int PR_MAXK = MAX_CAND;   // k of the fast path (k + 8 <= MAX_CAND)
 #ifndef LHIP_PR_SPREAD
 #define LHIP_PR_SPREAD 0  // 1: the pool gather spread over every thread (an A/B: within noise, r06w)
@@ -2627,6 +2625,7 @@ __device__ __forceinline__ float pr_distances(const T *__restrict__ X, int ld, c
 // The caller synchronises the block afterwards.
 constexpr int PR_WMK = 32;
 constexpr int PR_WMK_MIN_M = 48;  // (smaller merges, e.g. the tau mode's k + 8 rows: the rank form is cheaper)
+template <int TH>
 __device__ __forceinline__ void pr_merge(const float *d, const int64_t *l, float *od, int64_t *ol, int m, int k,
                                          int64_t tx) {
 	const int t = threadIdx.x, lane = t & 63;
@@ -2711,7 +2710,7 @@ __device__ __forceinline__ void pr_merge(const float *d, const int64_t *l, float
 			}
 		return;
 	}
-	for (int i = t; i < m; i += PR_THREADS) {
+	for (int i = t; i < m; i += TH) {
 		const float di = d[i];
 		const int64_t li = l[i];
 		int rank = 0;
@@ -2725,11 +2724,12 @@ __device__ __forceinline__ void pr_merge(const float *d, const int64_t *l, float
 }
 
 // ascending bitonic sort of a[0, P) (P a power of two >= 64) by the block
+template <int TH>
 __device__ __forceinline__ void pr_bitonic(uint64_t *a, int P) {
 	const int t = threadIdx.x;
 	for (int size = 2; size <= P; size <<= 1) {
 		for (int stride = size >> 1; stride > 0; stride >>= 1) {
-			for (int i = t; i < (P >> 1); i += PR_THREADS) {
+			for (int i = t; i < (P >> 1); i += TH) {
 				const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
 				const bool asc = (lo & size) == 0;
 				const uint64_t x = a[lo], y = a[hi];
@@ -2745,28 +2745,53 @@ __device__ __forceinline__ void pr_bitonic(uint64_t *a, int P) {
 
 constexpr int PR_SEL = 1024;  // chunk capacity
 constexpr int PR_HB = 1024;   // histogram bins of a chunk selection
-constexpr int PR_BPT = PR_HB / PR_THREADS;  // bins per thread (4, 2 or 1)
-static_assert(PR_BPT * PR_THREADS == PR_HB && PR_BPT >= 1 && PR_BPT <= 4, "bins per thread");
+// Geometry of one pool_refine instantiation.  The tau-mode instantiations (NI
+// = 1..4: the dispatch gives mode 0 the all-loads-in-flight path, mode 1 the
+// ring) may take a smaller workgroup and pool (LHIP_PR_TAU_THREADS /
+// LHIP_PR_TAU_CAP): they refine k + 8 rows, and a pool past the cap keeps its
+// smallest bounds (any >= k real rows give a valid tau), so several of them
+// can share a CU with the scans and the final refine.
+#ifndef LHIP_PR_TAU_THREADS
+#define LHIP_PR_TAU_THREADS LHIP_PR_THREADS
+#endif
+#ifndef LHIP_PR_TAU_CAP
+#define LHIP_PR_TAU_CAP LHIP_PR_CAP
+#endif
+#ifndef LHIP_PR_TAU_MINW
+#define LHIP_PR_TAU_MINW (LHIP_PR_TAU_THREADS == 256 ? 2 : 1)
+#endif
+template <int NI>
+struct PrCfg {
+	static constexpr bool TAU = NI >= 1 && NI <= 4;
+	static constexpr int TH = TAU ? LHIP_PR_TAU_THREADS : PR_THREADS;
+	static constexpr int CAP = TAU ? LHIP_PR_TAU_CAP : PR_CAP;
+	static constexpr int MINW = TAU ? LHIP_PR_TAU_MINW : PR_MIN_WAVES;
+	static constexpr int WAVES = TH / 64;
+	static constexpr int BPT = PR_HB / TH;  // histogram bins per thread (4, 2 or 1)
+	static_assert(TH == 256 || TH == 512 || TH == 1024, "pool_refine geometry");
+	static_assert(BPT * TH == PR_HB && BPT >= 1 && BPT <= 4, "bins per thread");
+};
 constexpr int PR_R = 96;      // first chunk of the final pass (C2: ~80 rows lie below d_k; refined rows
                               // are the kernel's HBM traffic: 96 refined 18 % fewer than 128 at equal
                               // step time or better, r03s2)
 
 template <int METRIC, typename T, int NI>
-__global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
+__global__ __launch_bounds__(PrCfg<NI>::TH, PrCfg<NI>::MINW) void pool_refine_kernel(
     const uint2 *__restrict__ seg_pool, const int *__restrict__ seg_cnt, int seg_cap, int n_seg, int nq,
     const float *__restrict__ tau, const T *__restrict__ X, int ld, int dim, const float *__restrict__ Qf,
     const int64_t *__restrict__ labels, int k, int mode, int m_tau, int64_t live, float *__restrict__ tau_out,
     int64_t *__restrict__ outL, float *__restrict__ outD, int *__restrict__ outC, int *__restrict__ cert,
     int *__restrict__ refined, int *__restrict__ pool_total, int prof_on, int r_first, int64_t tx) {
-	__shared__ uint64_t keys[PR_CAP];
+	constexpr int TH = PrCfg<NI>::TH, CAP = PrCfg<NI>::CAP, WAVES = PrCfg<NI>::WAVES, BPT = PrCfg<NI>::BPT;
+	__shared__ uint64_t keys[CAP];
 	__shared__ uint32_t sel[PR_SEL];  // slots of the chunk being refined
 	__shared__ unsigned hist[PR_HB];
-	__shared__ float cd[2][PR_MAXK + PR_CHUNK];  // running top-k (double-buffered) + the round's distances
-	__shared__ int64_t cl[2][PR_MAXK + PR_CHUNK];
-	__shared__ unsigned sh[PR_WAVES];
+	__shared__ float cd[2][PR_MAXK + WAVES * PR_PER_WAVE];  // running top-k (double-buffered) + the round's distances
+	__shared__ int64_t cl[2][PR_MAXK + WAVES * PR_PER_WAVE];
+	__shared__ unsigned sh[WAVES];
 	__shared__ int s_over, s_nnan, s_dnan;
 	__shared__ unsigned s_nfin, s_knf, s_kmin, s_kmax, s_bstar, s_cum, s_below, s_ns, s_hi, s_pmin, s_pmax;
-	__shared__ unsigned segc[PR_THREADS];  // (big pools) segment counts
+	__shared__ unsigned segc[TH];  // (big pools) segment counts
 	constexpr int NS_ = PrGeom<METRIC, NI>::NS;
 	__shared__ __attribute__((aligned(16))) float qs[NS_ > 0 ? 256 * NS_ : 4];  // the query row (NS_ > 0)
 	const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -2785,8 +2810,8 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 	auto mark = [&]() {};
 #endif
 	// candidates per wave and round (cosine: three f64 sums per row, half as many)
-	constexpr int PW = PrGeom<METRIC, NI>::PW, CH = PR_WAVES * PW;
-	static_assert(CH <= PR_CHUNK, "round buffer");
+	constexpr int PW = PrGeom<METRIC, NI>::PW, CH = WAVES * PW;
+	static_assert(CH <= WAVES * PR_PER_WAVE, "round buffer");
 	if (t == 0) {
 		s_over = 0;
 		s_nnan = 0;
@@ -2827,14 +2852,14 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 		c = (unsigned)min(cs, seg_cap);
 	}
 	unsigned total;
-	const unsigned off = block_excl_scan<PR_THREADS>(c, sh, total);
-	// a pool past PR_CAP: keep its smallest bounds (whole histogram bins, at most
-	// PR_CAP) and treat the rest like rows outside the pool: cut <= the smallest
+	const unsigned off = block_excl_scan<TH>(c, sh, total);
+	// a pool past CAP: keep its smallest bounds (whole histogram bins, at most
+	// CAP) and treat the rest like rows outside the pool: cut <= the smallest
 	// bound left out (excl_min), an exact certificate without a rerun.  Only when
-	// one bin alone overflows do the first PR_CAP entries stay (uncertified).
+	// one bin alone overflows do the first CAP entries stay (uncertified).
 	unsigned excl_min = 0xFFFFFFFFu;
 	bool big = false;
-	if (total > (unsigned)PR_CAP) {
+	if (total > (unsigned)CAP) {
 		if (t < n_seg) segc[t] = c;
 		if (t == 0) {
 			s_kmin = 0xFFFFFFFFu;
@@ -2843,9 +2868,9 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 			s_ns = 0;
 			s_hi = 0xFFFFFFFFu;
 		}
-		for (int i = t; i < PR_HB; i += PR_THREADS) hist[i] = 0;
+		for (int i = t; i < PR_HB; i += TH) hist[i] = 0;
 		__syncthreads();
-		const int m = max(1, PR_THREADS / max(n_seg, 1));  // threads per segment
+		const int m = max(1, TH / max(n_seg, 1));  // threads per segment
 		const int sg = t / m, sub = t - sg * m;
 		// every entry of this thread's segment share, 4 loads in flight
 		auto each = [&](auto &&f) {
@@ -2892,20 +2917,20 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 		}
 		__syncthreads();
 		{
-			unsigned hb[PR_BPT], hs = 0;
+			unsigned hb[BPT], hs = 0;
 #pragma unroll
-			for (int b = 0; b < PR_BPT; ++b) {
-				hb[b] = hist[PR_BPT * t + b];
+			for (int b = 0; b < BPT; ++b) {
+				hb[b] = hist[BPT * t + b];
 				hs += hb[b];
 			}
 			unsigned tot;
-			const unsigned ex = block_excl_scan<PR_THREADS>(hs, sh, tot);
+			const unsigned ex = block_excl_scan<TH>(hs, sh, tot);
 			int cand = -1;  // the last bin whose inclusive count fits
 			unsigned run = ex;
 #pragma unroll
-			for (int b = 0; b < PR_BPT; ++b) {
+			for (int b = 0; b < BPT; ++b) {
 				run += hb[b];
-				if (run <= (unsigned)PR_CAP) cand = PR_BPT * t + b;
+				if (run <= (unsigned)CAP) cand = BPT * t + b;
 			}
 			if (cand >= 0) atomicMax(reinterpret_cast<int *>(&s_bstar) + 0, cand);  // (s_bstar starts at -1)
 		}
@@ -2929,7 +2954,7 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 		__syncthreads();
 		excl_min = s_hi;
 	}
-	const int n = big ? (int)s_ns : (int)min(total, (unsigned)PR_CAP);
+	const int n = big ? (int)s_ns : (int)min(total, (unsigned)CAP);
 #if LHIP_PR_SPREAD
 	if (!big) {
 		// each segment's first PR_SPEC entries came with its count (its owner thread
@@ -2938,8 +2963,8 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 		// LDS: one or two memory latencies whatever the longest segment (the tau
 		// mode's ~120 sample segments hold ~64 entries each: 7 rounds of 8 loads
 		// for their owners before, round 6)
-		if (t < n_seg && c && off < (unsigned)PR_CAP) {
-			const unsigned cm = min(min(c, (unsigned)PR_CAP - off), (unsigned)PR_SPEC);
+		if (t < n_seg && c && off < (unsigned)CAP) {
+			const unsigned cm = min(min(c, (unsigned)CAP - off), (unsigned)PR_SPEC);
 #pragma unroll
 			for (int u = 0; u < PR_SPEC; ++u)
 				if ((unsigned)u < cm) {
@@ -2949,12 +2974,12 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 		}
 		if (t < n_seg) segc[t] = off;  // segment start offsets (ascending; an empty one shares the next's)
 		__syncthreads();
-		for (int i0 = t; i0 < n; i0 += PR_THREADS * 8) {
+		for (int i0 = t; i0 < n; i0 += TH * 8) {
 			uint2 e[8];
 			int dst[8];
 #pragma unroll
 			for (int u = 0; u < 8; ++u) {
-				const int i = i0 + u * PR_THREADS;
+				const int i = i0 + u * TH;
 				dst[u] = -1;
 				if (i < n) {
 					int lo = 0, hi = n_seg - 1;  // the last segment starting at or before i
@@ -2979,9 +3004,9 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 		}
 	}
 #else
-	if (!big && t < n_seg && c && off < (unsigned)PR_CAP) {
+	if (!big && t < n_seg && c && off < (unsigned)CAP) {
 		const uint2 *seg = seg_pool + ((int64_t)t * nq + q) * seg_cap;
-		const unsigned cm = min(c, (unsigned)PR_CAP - off);
+		const unsigned cm = min(c, (unsigned)CAP - off);
 #pragma unroll
 		for (int u = 0; u < PR_SPEC; ++u)
 			if ((unsigned)u < cm) {
@@ -3024,13 +3049,13 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 	}
 	__syncthreads();
 	mark();
-	if (t == 0 && total > (unsigned)PR_CAP && !big) s_over = 1;
+	if (t == 0 && total > (unsigned)CAP && !big) s_over = 1;
 	const int nfin = (int)s_nfin;
 	const float ftau = tau ? tau[q] : F_INF;
 	const float *qrow = Qf + (int64_t)q * ld;
 	// the query row in LDS (NI > 0: every refine round reads it there, zero past dim)
 	if (NS_ > 0)
-		for (int i = t; i < 64 * 4 * (NS_ > 0 ? NS_ : 1); i += PR_THREADS) qs[i] = i < dim ? qrow[i] : 0.f;
+		for (int i = t; i < 64 * 4 * (NS_ > 0 ? NS_ : 1); i += TH) qs[i] = i < dim ? qrow[i] : 0.f;
 
 	// next chunk: the finite keys in [lo, hi_goal] up to a histogram bin holding
 	// the R-th smallest of them (all of them when fewer), at most PR_SEL, slots
@@ -3050,7 +3075,7 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 		if (!whole_range && R >= PR_SEL) {
 			// a later chunk that takes every key in range (R = the capacity): one
 			// appending pass, no histogram, unless the range holds more than a chunk
-			for (int i = t; i < n; i += PR_THREADS) {
+			for (int i = t; i < n; i += TH) {
 				const uint64_t e = keys[i];
 				const uint32_t kk = (uint32_t)(e >> 32);
 				if (kk >= lo && kk <= hi_goal && kk < KEY_INF) {
@@ -3071,7 +3096,7 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 		}
 		if (!whole_range) {
 			unsigned kmn = 0xFFFFFFFFu, kmx = 0;
-			for (int i = t; i < n; i += PR_THREADS) {
+			for (int i = t; i < n; i += TH) {
 				const uint32_t kk = (uint32_t)(keys[i] >> 32);
 				if (kk >= lo && kk <= hi_goal && kk < KEY_INF) {
 					kmn = min(kmn, kk);
@@ -3096,34 +3121,34 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 		for (;;) {  // narrow until the chunk fits
 			const unsigned span = kmax - kmin;
 			shift = span >= (unsigned)PR_HB ? (32 - __builtin_clz(span)) - 10 : 0;  // (span >> shift) < PR_HB
-			for (int i = t; i < PR_HB; i += PR_THREADS) hist[i] = 0;
+			for (int i = t; i < PR_HB; i += TH) hist[i] = 0;
 			if (t == 0) {
 				s_bstar = PR_HB - 1;
 				s_cum = 0xFFFFFFFFu;
 				s_below = 0;
 			}
 			__syncthreads();
-			for (int i = t; i < n; i += PR_THREADS) {
+			for (int i = t; i < n; i += TH) {
 				const uint32_t kk = (uint32_t)(keys[i] >> 32);
 				if (kk >= kmin && kk <= kmax) atomicAdd(&hist[(kk - kmin) >> shift], 1u);
 			}
 			__syncthreads();
-			unsigned hb[PR_BPT], hs = 0;
+			unsigned hb[BPT], hs = 0;
 #pragma unroll
-			for (int b = 0; b < PR_BPT; ++b) {
-				hb[b] = hist[PR_BPT * t + b];
+			for (int b = 0; b < BPT; ++b) {
+				hb[b] = hist[BPT * t + b];
 				hs += hb[b];
 			}
 			unsigned tot;
-			const unsigned ex = block_excl_scan<PR_THREADS>(hs, sh, tot);
+			const unsigned ex = block_excl_scan<TH>(hs, sh, tot);
 			if (ex < (unsigned)R && ex + hs >= (unsigned)R) {
 				// this thread's first bin where the count reaches R
 				unsigned run = ex;
 				bool found = false;
 #pragma unroll
-				for (int b = 0; b < PR_BPT; ++b) {
+				for (int b = 0; b < BPT; ++b) {
 					if (!found && run + hb[b] >= (unsigned)R) {
-						s_bstar = PR_BPT * t + b;
+						s_bstar = BPT * t + b;
 						s_cum = run + hb[b];
 						s_below = run;
 						found = true;
@@ -3148,7 +3173,7 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 			kmax = min(kmax, nlo + ((1u << shift) - 1u));
 			__syncthreads();
 		}
-		for (int i = t; i < n; i += PR_THREADS) {
+		for (int i = t; i < n; i += TH) {
 			const uint64_t e = keys[i];
 			const uint32_t kk = (uint32_t)(e >> 32);
 			if (kk >= kmin && kk <= kmax && ((kk - kmin) >> shift) <= bstar) {
@@ -3197,7 +3222,7 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 			// its loads in flight (one memory latency, not one per column step)
 			constexpr int PR_SMALL = 8;
 			constexpr bool HAS_SMALL = PrGeom<METRIC, NI>::RING && PW > PR_SMALL && PrGeom<METRIC, NI>::NS <= 3;
-			const bool small = HAS_SMALL && nr <= PR_WAVES * PR_SMALL;
+			const bool small = HAS_SMALL && nr <= WAVES * PR_SMALL;
 			{
 				const int pw = small ? PR_SMALL : PW;
 				uint32_t sl[PW];
@@ -3226,7 +3251,7 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 			mark();
 			// merge the top so far and this round by (distance, label)
 			const int m = cnt + nr;
-			if (!LHIP_ABL_PR_NOMERGE) pr_merge(cd[cur], cl[cur], cd[cur ^ 1], cl[cur ^ 1], m, k, tx);
+			if (!LHIP_ABL_PR_NOMERGE) pr_merge<TH>(cd[cur], cl[cur], cd[cur ^ 1], cl[cur ^ 1], m, k, tx);
 			__syncthreads();
 			cur ^= 1;
 			cnt = min(m, k);
@@ -3240,9 +3265,9 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 		// from the sorted pool, as a bound-order refine takes them
 		int P = 64;
 		while (P < n) P <<= 1;
-		for (int i = n + t; i < P; i += PR_THREADS) keys[i] = ~0ull;
+		for (int i = n + t; i < P; i += TH) keys[i] = ~0ull;
 		__syncthreads();
-		pr_bitonic(keys, P);
+		pr_bitonic<TH>(keys, P);
 		order = keys;
 		int sp = pos;  // the first pos entries of the sorted pool are the keys < lo
 		const int limit = mode == 0 ? min(nfin, m_tau) : nfin;
@@ -3267,7 +3292,7 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 			}
 			__syncthreads();
 			const int m = cnt + nr;
-			pr_merge(cd[cur], cl[cur], cd[cur ^ 1], cl[cur ^ 1], m, k, tx);
+			pr_merge<TH>(cd[cur], cl[cur], cd[cur ^ 1], cl[cur ^ 1], m, k, tx);
 			__syncthreads();
 			cur ^= 1;
 			cnt = min(m, k);
@@ -3294,7 +3319,7 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 	__syncthreads();
 	if (!whole) {
 		unsigned kmn = 0xFFFFFFFFu;
-		for (int i = t; i < n; i += PR_THREADS) {
+		for (int i = t; i < n; i += TH) {
 			const uint32_t kk = (uint32_t)(keys[i] >> 32);
 			if (kk >= lo && kk < KEY_INF) kmn = min(kmn, kk);
 		}
@@ -3304,7 +3329,7 @@ __global__ __launch_bounds__(PR_THREADS, PR_MIN_WAVES) void pool_refine_kernel(
 	} else if (t == 0 && lo < KEY_INF) {
 		s_kmin = lo;
 	}
-	for (int i = t; i < k; i += PR_THREADS) {
+	for (int i = t; i < k; i += TH) {
 		outL[(int64_t)q * k + i] = i < cnt ? cl[cur][i] : -1;
 		outD[(int64_t)q * k + i] = i < cnt ? cd[cur][i] : __builtin_nanf("");
 	}
@@ -3390,7 +3415,7 @@ static void pool_refine_dispatch(const StoreView &s, const QueryView &q, const u
 #endif
 	const int r_first = s.pr_first > 0 ? std::max(8, std::min(PR_SEL, s.pr_first)) : PR_R;
 #define LHIP_PR(MET, NI)                                                                                              \
-	pool_refine_kernel<MET, T, NI><<<grid, PR_THREADS, 0, st>>>(seg_pool, seg_cnt, seg_cap, n_seg, q.nq, tau, X, s.ld,\
+	pool_refine_kernel<MET, T, NI><<<grid, PrCfg<NI>::TH, 0, st>>>(seg_pool, seg_cnt, seg_cap, n_seg, q.nq, tau, X, s.ld,\
 	                                                            s.dim, q.Qf, s.labels, k, mode, m_tau, live, tau_out,  \
 	                                                            L, D, C, cert, refined, pool_total, prof_on, r_first,  \
 	                                                            tie_x64(s.tie_desc))
@@ -3414,7 +3439,9 @@ static void pool_refine_dispatch(const StoreView &s, const QueryView &q, const u
 #else
 	const int ns = s.dim <= 256 ? 1 : s.dim <= 512 ? 2 : s.dim <= 768 ? 3 : s.dim <= 1024 ? 4 : 0;
 	// tau mode (k + 8 rows: one small round) every load in flight; final mode the ring
-	const int ni = ns == 0 ? 0 : mode == 1 ? 8 + ns : ns;
+	// (more segments than a tau-mode workgroup has threads: the column-step path,
+	// which keeps the default geometry)
+	const int ni = ns == 0 ? 0 : mode == 1 ? 8 + ns : n_seg > PrCfg<1>::TH ? 0 : ns;
 #endif
 	switch (s.metric) {
 	case METRIC_L2: LHIP_PR_NI(METRIC_L2); break;
