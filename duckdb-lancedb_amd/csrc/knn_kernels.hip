@@ -2624,7 +2624,10 @@ __device__ __forceinline__ float pr_distances(const T *__restrict__ X, int ld, c
 // Otherwise every thread ranks one entry against all m (O(m^2) LDS reads).
 // The caller synchronises the block afterwards.
 constexpr int PR_WMK = 32;
-constexpr int PR_WMK_MIN_M = 48;  // (smaller merges, e.g. the tau mode's k + 8 rows: the rank form is cheaper)
+#ifndef LHIP_PR_WMK_MIN_M
+#define LHIP_PR_WMK_MIN_M 48
+#endif
+constexpr int PR_WMK_MIN_M = LHIP_PR_WMK_MIN_M;  // (smaller merges, e.g. the tau mode's k + 8 rows: the rank form is cheaper)
 template <int TH>
 __device__ __forceinline__ void pr_merge(const float *d, const int64_t *l, float *od, int64_t *ol, int m, int k,
                                          int64_t tx) {
