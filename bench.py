@@ -110,6 +110,9 @@ def parse():
                     help="N > 1 / rehearsal exchange: packed (the search writes into the rank's packed row, one "
                          "all-gather + lance_hip_merge_topk_packed) or generic (label shift, pack, all-gather, "
                          "unpack copies, lance_hip_merge_topk_device)")
+    ap.add_argument("--submit-host-sync", action="store_true",
+                    help="pipelined submits wait on the host for torch's stream (an A/B of the default device-side "
+                         "ordering, lance_hip_stream_after)")
     ap.add_argument("--no-sync-leg", action="store_true",
                     help="IVF configs: skip the extra synchronous-call leg (kernel traces of the pipelined steps)")
     ap.add_argument("--dry-run", action="store_true",
@@ -514,7 +517,7 @@ def main_ivf(a):
     if pipelined:
         pipe = AsyncPipeline(L, h, D, nprobes=a.nprobe, refine_factor=a.refine,
                              packed=(world > 1 or a.exchange_rehearsal) and a.exchange == "packed",
-                             label_offset=s0)
+                             label_offset=s0, host_sync=a.submit_host_sync)
         if world > 1 or a.exchange_rehearsal:
             pipe = ShardedPipeline(pipe, searcher)
     last_out = [None]
@@ -842,7 +845,7 @@ def main():
     pipe = None
     if pipelined:
         pipe = AsyncPipeline(L, h, D, packed=(world > 1 or a.exchange_rehearsal) and a.exchange == "packed",
-                             label_offset=s0)
+                             label_offset=s0, host_sync=a.submit_host_sync)
         if world > 1 or a.exchange_rehearsal:
             pipe = ShardedPipeline(pipe, searcher)
     last_out = [None]

@@ -248,6 +248,7 @@ struct Index {
 	// the handle's stream by ev_order): pass i+1's first kernels overlap pass i's last
 	hipStream_t pstream[2] = {nullptr, nullptr};
 	hipEvent_t ev_order = nullptr;
+	hipEvent_t ev_caller = nullptr;  // (lance_hip_stream_after: the caller's stream, recorded)
 	hipStream_t pass_stream(int slot) {
 		if (!pstream[slot]) HIPCHK(hipStreamCreateWithFlags(&pstream[slot], hipStreamNonBlocking));
 		if (!ev_order) HIPCHK(hipEventCreateWithFlags(&ev_order, hipEventDisableTiming));
@@ -375,6 +376,7 @@ struct Index {
 		for (auto &ps : pstream)
 			if (ps) (void)hipStreamDestroy(ps);
 		if (ev_order) (void)hipEventDestroy(ev_order);
+		if (ev_caller) (void)hipEventDestroy(ev_caller);
 	}
 
 	void tic(int i) {

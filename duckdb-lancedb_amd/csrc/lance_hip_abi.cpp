@@ -1735,6 +1735,32 @@ int64_t lance_hip_search_batch_device_async(void *handle, const float *d_queries
 	API_GUARD("search failed: ", -1)
 }
 
+int32_t lance_hip_stream_after(void *handle, void *caller_stream, char *err_buf, int err_buf_len) {
+	if (!handle) {
+		lhip::write_err(err_buf, err_buf_len, "null handle");
+		return -1;
+	}
+	try {
+		Index *ix = as_index(handle);
+		std::lock_guard<std::mutex> g(ix->mu);
+		hipStream_t cs = static_cast<hipStream_t>(caller_stream);
+		if (ix->sharded()) {  // (stores on several devices: a host wait on the caller's stream)
+			HIPCHK(hipStreamSynchronize(cs));
+			return 0;
+		}
+		ix->bind_nodrain();
+		// an event on the caller's stream that the handle's stream waits on: every
+		// later search of the handle (flat passes are ordered after the handle's
+		// stream, IVF runs on it) starts after the caller's work so far, and the
+		// host does not wait
+		if (!ix->ev_caller) HIPCHK(hipEventCreateWithFlags(&ix->ev_caller, hipEventDisableTiming));
+		HIPCHK(hipEventRecord(ix->ev_caller, cs));
+		HIPCHK(hipStreamWaitEvent(ix->stream, ix->ev_caller, 0));
+		return 0;
+	}
+	API_GUARD("stream_after failed: ", -1)
+}
+
 int32_t lance_hip_search_wait(void *handle, int64_t ticket, char *err_buf, int err_buf_len) {
 	if (!handle) {
 		lhip::write_err(err_buf, err_buf_len, "null handle");

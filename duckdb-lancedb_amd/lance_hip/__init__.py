@@ -77,6 +77,7 @@ _SIGNATURES = [
     ("lance_hip_search_batch_device_async", i64,
      [c_void_p, c_void_p, i32, i32, i32, i32, i32, c_void_p, c_void_p, c_void_p, c_char_p, c_int]),
     ("lance_hip_search_wait", i32, [c_void_p, i64, c_char_p, c_int]),
+    ("lance_hip_stream_after", i32, [c_void_p, c_void_p, c_char_p, c_int]),
     ("lance_hip_merge_topk_device", i32,
      [i32, i32, i32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_char_p, c_int]),
     ("lance_hip_merge_packed_stride", i64, [i32, i32]),

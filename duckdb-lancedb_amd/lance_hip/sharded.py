@@ -235,7 +235,7 @@ class AsyncPipeline:
     packed exchange."""
 
     def __init__(self, lib, handle, dim: int, nprobes: int = 20, refine_factor: int = 1, err_len: int = 2048,
-                 packed: bool = False, label_offset: int = 0):
+                 packed: bool = False, label_offset: int = 0, host_sync: bool = False):
         import ctypes
 
         self.lib, self.h, self.dim = lib, handle, dim
@@ -244,6 +244,7 @@ class AsyncPipeline:
         self.err_len = err_len
         self.outs = {}
         self.packed, self.label_offset = bool(packed), int(label_offset)
+        self.host_sync = bool(host_sync)  # (an A/B: a host wait on torch's stream instead)
         self.completed = {}
         self.pending = []  # (ticket, outputs, query tensor held until the wait)
         self.i = 0
@@ -267,9 +268,15 @@ class AsyncPipeline:
         nq = Q.shape[0]
         ol, od, oc = o = self._out(nq, k, Q.device, self.i & 1)
         self.i += 1
+        # Q (and, with a packed exchange, the all-gather still reading the output
+        # row this batch overwrites) on torch's stream: the handle's stream waits
+        # for that stream's work so far on the device (no host wait)
         cs = torch.cuda.current_stream()
         if not cs.query():
-            cs.synchronize()
+            if self.host_sync:
+                cs.synchronize()
+            elif self.lib.lance_hip_stream_after(self.h, cs.cuda_stream, self.e, self.err_len) != 0:
+                raise RuntimeError(self.e.value.decode())
         t = self.lib.lance_hip_search_batch_device_async(self.h, Q.data_ptr(), nq, self.dim, k, self.nprobes,
                                                          self.refine, ol.data_ptr(), od.data_ptr(), oc.data_ptr(),
                                                          self.e, self.err_len)

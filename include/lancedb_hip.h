@@ -320,6 +320,14 @@ int64_t lance_hip_search_batch_device_async(void *handle, const float *d_queries
                                             float *d_out_distances, int32_t *d_out_counts, char *err_buf,
                                             int err_buf_len);
 
+/* NEW — orders the handle's later searches after everything enqueued so far on
+ * `caller_stream` (a hipStream_t of the handle's device, NULL = the null stream),
+ * without a host wait: an event recorded there that the handle's stream waits on.
+ * For a caller that writes the queries (or reads a previous batch's outputs, e.g.
+ * an all-gather of them) on its own stream before lance_hip_search_batch_device_async.
+ * Multi-device handles wait on the host instead.  0 or -1. */
+int32_t lance_hip_stream_after(void *handle, void *caller_stream, char *err_buf, int err_buf_len);
+
 /* NEW — completes every asynchronous search of the handle up to `ticket`
  * (<= 0: all of them).  0 or -1. */
 int32_t lance_hip_search_wait(void *handle, int64_t ticket, char *err_buf, int err_buf_len);

@@ -303,6 +303,44 @@ def test_release_build_rejects_development_knobs(hip):
         hip.LanceFreeDetached(h2)
 
 
+def test_async_submit_orders_after_torch_stream(hip):
+    """AsyncPipeline.submit with torch's stream still busy: the queries are
+    written there (behind a long chain of matmuls) right before the submit, and
+    lance_hip_stream_after orders the search after that work on the device (no
+    host wait): the results are those of the new queries, every time."""
+    import torch
+    from lance_hip.sharded import AsyncPipeline
+
+    rng = np.random.default_rng(43)
+    n, d, k = 100_000, 768, 10
+    X = rng.standard_normal((n, d), dtype=np.float32)
+    Qa = rng.standard_normal((256, d), dtype=np.float32)
+    Qb = rng.standard_normal((256, d), dtype=np.float32)
+    ea = c_oracle.flat_search_batch(X, Qa, k, "l2", acc64=True, nthreads=16)
+    eb = c_oracle.flat_search_batch(X, Qb, k, "l2", acc64=True, nthreads=16)
+    h = hip.LanceCreateDetached("", d, "l2", "t")
+    try:
+        hip.LanceDetachedAddBatch(h, X, n, d)
+        pipe = AsyncPipeline(hip.lib(), h, d)
+        Q = torch.from_numpy(Qa).cuda()
+        srcs = [torch.from_numpy(Qb).cuda(), torch.from_numpy(Qa).cuda()]
+        M = torch.randn((4096, 4096), device="cuda")
+        torch.cuda.synchronize()
+        outs = []
+        for i in range(4):
+            for _ in range(6):  # keep torch's stream busy for milliseconds
+                M = torch.tanh(M @ M * 1e-3)
+            Q.copy_(srcs[i % 2])  # the batch's queries, written on torch's stream
+            assert not torch.cuda.current_stream().query()
+            t = pipe.submit(Q, k)
+            o = pipe.wait(t)
+            outs.append(tuple(x.cpu().numpy() for x in o))
+        for i, r in enumerate(outs):
+            assert_same(*r, *(eb if i % 2 == 0 else ea))
+    finally:
+        hip.LanceFreeDetached(h)
+
+
 def test_async_pipeline_matches_sync(hip):
     """lance_hip_search_batch_device_async / lance_hip_search_wait: two batches
     in flight per handle (the second pass enqueued while the first is on the
