@@ -4207,7 +4207,7 @@ __global__ __launch_bounds__(256) void merge_packed_kernel(int nshard, int nq, i
 
 void launch_merge_packed(int nshard, int nq, int k, const int32_t *gathered, int64_t stride, int64_t *out_labels,
                          float *out_dists, int *out_counts, hipStream_t st, int tie_desc) {
-	if ((int64_t)nshard * k <= MP_LDS_CAP) {
+	if ((int64_t)nshard * k <= MP_LDS_CAP && nshard <= 1024) {  // (<= 53 KB of LDS)
 		const size_t lds = (size_t)nshard * k * (sizeof(int64_t) + sizeof(float)) + (size_t)(nshard + 1) * sizeof(int);
 		merge_packed_kernel<true><<<dim3(nq), dim3(256), lds, st>>>(nshard, nq, k, gathered, stride, out_labels,
 		                                                           out_dists, out_counts, tie_x64(tie_desc));

@@ -1824,8 +1824,7 @@ int32_t lance_hip_merge_topk_device(int32_t nshard, int32_t nq, int32_t k, const
 		if (nshard <= 0 || nq <= 0 || k <= 0) return 0;
 		// stream-ordered on the null stream, no host wait: a multi-rank pipeline's
 		// exchange of batch i-1 must not hold the host until the scan of batch i
-		// (which holds every CU) has finished (round 6: one-rank RCCL rehearsal,
-		// C2 748k -> see DESIGN section 7)
+		// (which holds every CU) has finished (round 6: DESIGN section 7)
 		lhip::launch_merge_topk(nshard, nq, k, d_part_labels, d_part_dists, d_part_counts, d_out_labels, d_out_dists,
 		                        d_out_counts, nullptr, lhip::env_tie());
 		HIPCHK(hipGetLastError());
@@ -1845,6 +1844,7 @@ int32_t lance_hip_merge_topk_packed(int32_t nshard, int32_t nq, int32_t k, const
                                     int32_t *d_out_counts, char *err_buf, int err_buf_len) {
 	try {
 		if (nshard <= 0 || nq <= 0 || k <= 0) return 0;
+		if (!d_gathered || !d_out_labels || !d_out_dists || !d_out_counts) throw std::invalid_argument("null buffer");
 		if (row_stride < lance_hip_merge_packed_stride(nq, k) || (row_stride & 1) ||
 		    (reinterpret_cast<uintptr_t>(d_gathered) & 7))
 			throw std::invalid_argument("row_stride must be even and >= lance_hip_merge_packed_stride(nq, k), "

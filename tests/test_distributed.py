@@ -247,6 +247,17 @@ def test_packed_stride_matches_the_library():
         assert s % 2 == 0 and s >= 3 * nq * k + nq + 2
         assert L.lance_hip_merge_packed_stride(nq, k) == s
     assert L.lance_hip_merge_packed_stride(0, 10) == -1
+    # argument checks come before any device call (no GPU needed)
+    import ctypes
+
+    e = ctypes.create_string_buffer(2048)
+    assert L.lance_hip_merge_topk_packed(2, 4, 3, None, packed_stride(4, 3), None, None, None, e, 2048) == -1
+    assert "null buffer" in e.value.decode()
+    buf = ctypes.create_string_buffer(1024)
+    addr = (ctypes.addressof(buf) + 7) // 8 * 8
+    assert L.lance_hip_merge_topk_packed(2, 4, 3, addr, packed_stride(4, 3) - 2, addr, addr, addr, e, 2048) == -1
+    assert "row_stride" in e.value.decode()
+    assert L.lance_hip_merge_topk_packed(0, 4, 3, None, 0, None, None, None, e, 2048) == 0
 
 
 def test_shard_range_partitions_exactly():
